@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""bench.py -- CRDT delta merges/s and HBM roofline (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): PNCOUNT,
+16M keys x 64 replicas x {P, N} per GPU shard.  One step = converge one full
+delta batch (64 flushed peer batches, one per replica column, each covering
+every key of the shard, both signs) = 2^31 cell merges, in ONE engine call
+(jy_pncount_converge_block) on HBM-resident input.  Keys are hash-sharded:
+every rank owns its own 16M keys (weak scaling, no data-path collective --
+the merge itself exchanges nothing; see DESIGN.md for the routed variant).
+
+Inputs: seeded splitmix64 streams generated in HBM (jylis_amd/synth.py);
+state starts from a synthetic full state; `--batches` distinct delta batches
+(a monotone chain, 75% advanced / 25% stale cells) are cycled through, so
+every step performs real state changes on fresh input.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import time
+
+import numpy as np
+
+METRIC = "CRDT delta merges/sec (keys×replicas) + achieved HBM GB/s vs peak, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BYTES_PER_CELL = 24    # 8 delta read + 8 state read + 8 state write
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--keys", type=int, default=16 * 1024 * 1024, help="keys per GPU shard")
+    ap.add_argument("--replicas", type=int, default=64)
+    ap.add_argument("--batches", type=int, default=4, help="distinct delta batches held in HBM")
+    ap.add_argument("--cpu-keys", type=int, default=65536, help="cpu_baseline sample: keys (x replicas x 2)")
+    ap.add_argument("--cpu-rounds", type=int, default=6, help="cpu_baseline sample: peer-batch rounds")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-file", default=None, help="per-launch HBM bytes from a PMC run (json)")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, seed):
+    """The oracle (a C++ restatement of the reference's per-key converge loop,
+    repo_manager.pony:92-93 over Map[String, PNCounter]) timed single-threaded
+    on a bounded sample of the same stream: cpu_keys keys x R replicas x 2
+    signs, `cpu_rounds` rounds of R peer batches."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "oracle"))
+    import oracle as O
+    from jylis_amd import synth as S
+    K, R = args.cpu_keys, args.replicas
+    kb, ko = S.counter_keys(K, prefix=b"c")
+    rids = S.replica_ids(R, seed)
+    st = S.counter_state_np(K, R, 2, seed)
+    repo = O.Repo(O.PNCOUNT, 1)
+    for t in S.counter_batch_tables(st, rids, (kb, ko)):
+        repo.converge(t)
+    dt = 0.0
+    cur = st
+    for r in range(args.cpu_rounds):
+        # decode (untimed) one round of R peer batches, then time the converge loop
+        cur = S.counter_delta_np(cur, r, seed)
+        batches = [O.Batch(O.PNCOUNT, t) for t in S.counter_batch_tables(cur, rids, (kb, ko))]
+        t0 = time.perf_counter()
+        for b in batches:
+            repo.converge(b)
+        dt += time.perf_counter() - t0
+        del batches
+    cells = K * R * 2 * args.cpu_rounds
+    return {"value": cells / dt, "unit": "merges/s", "cores": 1, "kind": "port",
+            "sample": f"PNCOUNT {K} keys x {R} replicas x 2 signs x {args.cpu_rounds} rounds of {R} peer batches "
+                      f"({cells} cell merges, {dt:.2f} s, oracle/jy_oracle.cpp unordered_map path, 1 thread)",
+            "host_cpus": os.cpu_count()}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from jylis_amd import synth as S
+    from jylis_amd.engine import Engine
+    K, R = args.keys, args.replicas
+    seed = S.BASE_SEED + 2  # config 2
+    dev = torch.device("cuda", local)
+    eng = Engine(device=local, counter_columns=R, key_capacity=[1024, K, 1024, 1024, 1024])
+    eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+
+    # key shard of this rank: interned on the host like any key (s<rank>:p########)
+    kb, ko = S.counter_keys(K, prefix=f"s{rank}:p".encode())
+    slots = eng.intern(1, (kb, ko))
+    assert slots[0] == 0 and slots[-1] == K - 1
+    del kb, ko, slots
+    cols = eng.replica_cols(S.replica_ids(R, seed).tolist())
+
+    # initial state and the delta chain, generated in HBM
+    shape = (2, R, K)
+    tmp = torch.empty(shape, dtype=torch.int64, device=dev)
+    S.counter_rows_torch(tmp, seed)
+    eng.pncount_converge_block(cols, 0, tmp[0], tmp[1])  # load: max(0, s) = s
+    nb = max(1, args.batches)
+    deltas = []
+    prev = tmp
+    for j in range(nb):
+        d = torch.empty(shape, dtype=torch.int64, device=dev)
+        S.counter_rows_torch(d, seed, rnd=j, prev=prev)
+        deltas.append(d)
+        prev = d
+    del tmp, prev
+    torch.cuda.synchronize(dev)
+
+    def step(i):
+        d = deltas[i % nb]
+        eng.pncount_converge_block(cols, 0, d[0], d[1])
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record()
+        step(args.warmup + i)
+        evs[i][1].record()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in evs]
+
+    # correctness spot-check on sampled cells: state == max(initial, applied batches)
+    applied = sorted({(args.warmup + i) % nb for i in range(args.steps)} | {i % nb for i in range(args.warmup)})
+    rng = np.random.default_rng(rank)
+    s0 = int(rng.integers(0, K - 64))
+    cells = (np.arange(2)[:, None, None] * R * K + np.arange(R)[None, :, None] * K
+             + (s0 + np.arange(64))[None, None, :]).astype(np.uint64)
+    exp = S.counter_state_np(K, R, 2, seed, cells=cells)
+    chain = exp.copy()
+    best = exp.copy()
+    for j in range(nb):
+        chain = S.counter_delta_np(chain, j, seed, cells=cells)
+        if j in applied:
+            best = np.maximum(best, chain)
+    got = eng.counter_export(1, R, s0, 64)
+    ok = bool((got == best).all())
+    sums = eng.pncount_get(np.arange(s0, s0 + 64, dtype=np.uint32))
+    exp_sum = (best[0].sum(axis=0, dtype=np.uint64) - best[1].sum(axis=0, dtype=np.uint64)).view(np.int64)
+    ok = ok and bool((sums == exp_sum).all())
+
+    t_max = elapsed
+    if dist:
+        tt = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max, bad = float(tt[0]), float(tt[1])
+        ok = bad == 0.0
+    cells_per_step = 2 * R * K
+    value = world * cells_per_step * args.steps / t_max
+    avg_kern_s = float(np.mean(kern_ms)) / 1e3
+    achieved = BYTES_PER_CELL * cells_per_step / avg_kern_s / 1e9
+
+    traffic = None
+    tf = args.traffic_file or os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
+    if os.path.exists(tf):
+        try:
+            with open(tf) as f:
+                tj = json.load(f)
+            if tj.get("workload_cells_per_launch") == cells_per_step:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, seed)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "merges/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": t_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (seeded splitmix64 in HBM; SURVEY.md 8d config 2)",
+            "config": {"workload": "PNCOUNT converge: 16M keys x 64 replicas x {P,N} per GPU shard, "
+                                   "one full delta batch (64 peer batches) per step",
+                       "keys_per_gpu": K, "replicas": R, "signs": 2, "cells_per_step_per_gpu": cells_per_step,
+                       "parallelism": f"key-sharded x{world}", "distinct_batches": nb},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_block_max_v2", "kernel_ms_avg": avg_kern_s * 1e3,
+                         "bytes_per_cell": BYTES_PER_CELL},
+            "cpu_baseline": cpu,
+            "verified": ok,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,163 @@
+/* jylis_gpu.h -- C ABI of the MI355X CRDT delta-convergence engine.
+ *
+ * Drop-in point: RepoManagerCore.converge_deltas (jylis/repo_manager.pony:92-93)
+ * loops `_repo.converge(k, d)` over one decoded MsgPushDeltas batch
+ * (jylis/msg.pony:20-24).  A GPU-backed Repo* marshals that whole
+ * Array[(String, Any box)] into structure-of-arrays once and makes ONE call
+ * here per batch (see INTEGRATION.md for the Pony FFI declarations).
+ *
+ * Conventions
+ *   - every entry returns int32 status: 0 ok, < 0 error (detail in
+ *     jy_last_error).  Pony FFI has no exceptions; the reference swallows
+ *     converge failures (`try ... end`, repo_gcount.pony:51), so malformed
+ *     entries are skipped and counted, never fatal (jy_skipped()).
+ *   - pointers are borrowed for the duration of the call only.  `mem` says
+ *     where they live: JY_HOST (copied through pinned staging) or JY_DEVICE
+ *     (HBM-resident; read asynchronously on the engine stream, keep them
+ *     alive until jy_sync).
+ *   - one engine = one GPU = one key shard.  An engine handle is not
+ *     thread-safe: the caller serialises calls (one RepoManager actor per
+ *     type, repo_manager.pony:18).  No thread-local HIP state is assumed.
+ *   - keys are interned to dense per-type slots (u32); replica identities
+ *     (u64 Address.hash64, jylis/address.pony:29-33) to dense columns (u16).
+ *   - within ONE converge call every slot appears at most once (a batch
+ *     comes from the sender's `_deltas` Map, repo_gcount.pony:14,19-23).
+ *     Host-pointer calls enforce this by splitting into rounds; device
+ *     batches must honour it (routed batches are converged per source).
+ */
+#ifndef JYLIS_GPU_H
+#define JYLIS_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define JY_OK 0
+#define JY_EINVAL (-1)
+#define JY_ENOMEM (-2)
+#define JY_EHIP (-3)
+#define JY_ERANGE (-4)
+#define JY_ETYPE (-5)
+
+#define JY_NO_SLOT 0xFFFFFFFFu
+
+/* CRDT types: the RepoManager names of database.pony:18-22 */
+enum { JY_GCOUNT = 0, JY_PNCOUNT = 1, JY_TREG = 2, JY_TLOG = 3, JY_UJSON = 4, JY_NTYPES = 5 };
+enum { JY_HOST = 0, JY_DEVICE = 1 };
+
+typedef struct jy_engine jy_engine;
+
+typedef struct jy_config {
+  int32_t device;            /* HIP device ordinal                                   */
+  uint32_t counter_columns;  /* initial replica-column capacity of GCOUNT/PNCOUNT    */
+  uint32_t ujson_columns;    /* version-vector width of UJSON contexts (fixed)       */
+  uint32_t reserved;
+  uint64_t key_capacity[JY_NTYPES];   /* initial slots per type (grows by doubling)  */
+  uint64_t entry_capacity[JY_NTYPES]; /* initial TLOG entries / UJSON dots            */
+  uint64_t arena_capacity[JY_NTYPES]; /* initial string arena bytes (TREG, TLOG)      */
+} jy_config;
+
+/* ---- engine lifecycle (replaces RepoXXX.create(identity), repo_manager.pony:6) ---- */
+void jy_config_default(jy_config* cfg);
+int32_t jy_engine_create(const jy_config* cfg, jy_engine** out);
+void jy_engine_destroy(jy_engine* eng);
+const char* jy_last_error(const jy_engine* eng);
+uint64_t jy_skipped(const jy_engine* eng);      /* malformed entries skipped so far  */
+int32_t jy_set_stream(jy_engine* eng, void* hip_stream); /* NULL: engine-owned stream */
+void* jy_get_stream(jy_engine* eng);
+int32_t jy_sync(jy_engine* eng);
+
+/* ---- replica dictionary: u64 identity <-> dense column ---- */
+int32_t jy_replica_col(jy_engine* eng, uint64_t replica_id, uint32_t* col_out);
+int32_t jy_replica_id(const jy_engine* eng, uint32_t col, uint64_t* id_out);
+uint32_t jy_replica_count(const jy_engine* eng);
+
+/* ---- key interning: `_data_for(key)` (repo_gcount.pony:36-41) creates on miss,
+ *      `_data(key)?` (repo_gcount.pony:53-55) only looks up (JY_NO_SLOT) ---- */
+int32_t jy_keys_intern(jy_engine* eng, int32_t type, uint64_t n, const uint8_t* key_bytes,
+                       const uint64_t* key_offs, uint32_t* slots_out);
+int32_t jy_keys_lookup(const jy_engine* eng, int32_t type, uint64_t n, const uint8_t* key_bytes,
+                       const uint64_t* key_offs, uint32_t* slots_out);
+uint64_t jy_keys_count(const jy_engine* eng, int32_t type);
+int32_t jy_keys_reserve(jy_engine* eng, int32_t type, uint64_t key_capacity);
+/* owner shard of a key when keys are hash-sharded over `nshards` engines */
+uint32_t jy_key_owner(const uint8_t* key, uint64_t len, uint32_t nshards);
+
+/* ---- string arena of TREG / TLOG values (value bytes beyond the 8-byte prefix) ----
+ * A value is held as (prefix u64 = first 8 bytes big-endian, zero padded;
+ * lr u64 = arena_offset << 24 | length).  Values of <= 8 bytes never touch
+ * the arena.  jy_values_pack appends long values and fills pre/lr. */
+int32_t jy_values_pack(jy_engine* eng, int32_t type, uint64_t n, const uint8_t* bytes,
+                       const uint64_t* offs, uint64_t* pre_out, uint64_t* lr_out);
+
+/* ---- GCOUNT: GCounter.converge (repo_gcount.pony:50-51) / value (:53-55) ----
+ * COO form: n cells (slot, col, value): s[slot][col] = max(s, value). */
+int32_t jy_gcount_converge(jy_engine* eng, uint64_t n, const uint32_t* slot, const uint16_t* col,
+                           const uint64_t* val, int32_t mem);
+/* Column-block form: ncols peer columns over the slot run [slot0, slot0+nslots);
+ * vals is [ncols][nslots] (one flushed peer batch per column, in slot order). */
+int32_t jy_gcount_converge_block(jy_engine* eng, uint32_t ncols, const uint16_t* cols_host,
+                                 uint32_t slot0, uint32_t nslots, const uint64_t* vals, int32_t mem);
+int32_t jy_gcount_get(jy_engine* eng, uint64_t n, const uint32_t* slots, uint64_t* out, int32_t mem);
+
+/* ---- PNCOUNT: two GCounters (repo_pncount.pony:52-57); GET = (sum P - sum N) as i64 ---- */
+int32_t jy_pncount_converge(jy_engine* eng, uint64_t np, const uint32_t* pslot, const uint16_t* pcol,
+                            const uint64_t* pval, uint64_t nn, const uint32_t* nslot,
+                            const uint16_t* ncol, const uint64_t* nval, int32_t mem);
+/* vals_p / vals_n are each [ncols][nslots] */
+int32_t jy_pncount_converge_block(jy_engine* eng, uint32_t ncols, const uint16_t* cols_host,
+                                  uint32_t slot0, uint32_t nslots, const uint64_t* vals_p,
+                                  const uint64_t* vals_n, int32_t mem);
+int32_t jy_pncount_get(jy_engine* eng, uint64_t n, const uint32_t* slots, int64_t* out, int32_t mem);
+
+/* counter state dump for parity checks: out is [nsigns][ncols][nslots] over
+ * columns [0, ncols) and slots [slot0, slot0+nslots) (host memory) */
+int32_t jy_counter_export(jy_engine* eng, int32_t type, uint32_t ncols, uint32_t slot0,
+                          uint32_t nslots, uint64_t* out);
+
+/* ---- TREG: TRegString.converge (repo_treg.pony:51-52), LWW by (ts, value) ---- */
+int32_t jy_treg_converge(jy_engine* eng, uint64_t n, const uint32_t* slot, const uint64_t* ts,
+                         const uint64_t* pre, const uint64_t* lr, int32_t mem);
+/* read (ts, pre, lr) for n slots (host out) and fetch arena bytes */
+int32_t jy_treg_read(jy_engine* eng, uint64_t n, const uint32_t* slots, uint64_t* ts_out,
+                     uint64_t* pre_out, uint64_t* lr_out);
+int32_t jy_arena_read(jy_engine* eng, int32_t type, uint64_t offset, uint64_t len, uint8_t* dst);
+
+/* ---- TLOG: TLog[String].converge (repo_tlog.pony:66-67) ----
+ * nkeys delta logs, CSR: entries of key i are [ent_offs[i], ent_offs[i+1]),
+ * canonical (later ts first, then greater value; unique; ts >= cutoff[i]).
+ * Non-canonical segments are skipped (counted in jy_skipped). */
+int32_t jy_tlog_converge(jy_engine* eng, uint64_t nkeys, const uint32_t* slot, const uint64_t* cutoff,
+                         const uint64_t* ent_offs, uint64_t nent, const uint64_t* ts,
+                         const uint64_t* pre, const uint64_t* lr, int32_t mem);
+/* two-phase read: sizes (n entries per slot + cutoffs), then entries */
+int32_t jy_tlog_read_sizes(jy_engine* eng, uint64_t n, const uint32_t* slots, uint64_t* len_out,
+                           uint64_t* cutoff_out);
+int32_t jy_tlog_read(jy_engine* eng, uint64_t n, const uint32_t* slots, const uint64_t* out_offs,
+                     uint64_t* ts_out, uint64_t* pre_out, uint64_t* lr_out);
+
+/* ---- UJSON: UJSON.converge (repo_ujson.pony:65-66), dot-kernel join ----
+ * dots are packed (col << 48 | seq), seq in [1, 2^48).  Per doc i:
+ *   elements [el_offs[i], el_offs[i+1]) of (dots, elems), dots ascending;
+ *   context  version vector [vv_offs[i], vv_offs[i+1]) of packed (col << 48 | n)
+ *            meaning "every seq <= n of col seen", plus
+ *            cloud [cloud_offs[i], cloud_offs[i+1]) of packed dots, ascending. */
+int32_t jy_ujson_converge(jy_engine* eng, uint64_t ndocs, const uint32_t* slot, const uint64_t* el_offs,
+                          uint64_t nel, const uint64_t* dots, const uint64_t* elems,
+                          const uint64_t* vv_offs, uint64_t nvv, const uint64_t* vv,
+                          const uint64_t* cloud_offs, uint64_t ncloud, const uint64_t* cloud,
+                          int32_t mem);
+/* two-phase read: per slot element / cloud counts, then contents; vv_out is
+ * [n][ujson_columns] dense */
+int32_t jy_ujson_read_sizes(jy_engine* eng, uint64_t n, const uint32_t* slots, uint64_t* nel_out,
+                            uint64_t* ncloud_out);
+int32_t jy_ujson_read(jy_engine* eng, uint64_t n, const uint32_t* slots, const uint64_t* el_offs,
+                      uint64_t* dots_out, uint64_t* elems_out, uint64_t* vv_out,
+                      const uint64_t* cloud_offs, uint64_t* cloud_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JYLIS_GPU_H */

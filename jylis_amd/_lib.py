@@ -1,0 +1,91 @@
+"""ctypes binding of libjylis_gpu.so (include/jylis_gpu.h).
+
+The product path has no CPU fallback: if the HIP library is missing or no
+GPU is present, loading fails loudly.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libjylis_gpu.so")
+
+JY_OK, JY_EINVAL, JY_ENOMEM, JY_EHIP, JY_ERANGE, JY_ETYPE = 0, -1, -2, -3, -4, -5
+JY_NO_SLOT = 0xFFFFFFFF
+GCOUNT, PNCOUNT, TREG, TLOG, UJSON = 0, 1, 2, 3, 4
+TYPE_NAMES = {"GCOUNT": GCOUNT, "PNCOUNT": PNCOUNT, "TREG": TREG, "TLOG": TLOG, "UJSON": UJSON}
+HOST, DEVICE = 0, 1
+
+
+class JyConfig(C.Structure):
+    _fields_ = [
+        ("device", C.c_int32),
+        ("counter_columns", C.c_uint32),
+        ("ujson_columns", C.c_uint32),
+        ("reserved", C.c_uint32),
+        ("key_capacity", C.c_uint64 * 5),
+        ("entry_capacity", C.c_uint64 * 5),
+        ("arena_capacity", C.c_uint64 * 5),
+    ]
+
+
+P = C.c_void_p
+U64 = C.c_uint64
+U32 = C.c_uint32
+I32 = C.c_int32
+
+# name -> (restype, argtypes); every symbol include/jylis_gpu.h declares
+SIGNATURES = {
+    "jy_config_default": (None, [P]),
+    "jy_engine_create": (I32, [P, P]),
+    "jy_engine_destroy": (None, [P]),
+    "jy_last_error": (C.c_char_p, [P]),
+    "jy_skipped": (U64, [P]),
+    "jy_set_stream": (I32, [P, P]),
+    "jy_get_stream": (P, [P]),
+    "jy_sync": (I32, [P]),
+    "jy_replica_col": (I32, [P, U64, P]),
+    "jy_replica_id": (I32, [P, U32, P]),
+    "jy_replica_count": (U32, [P]),
+    "jy_keys_intern": (I32, [P, I32, U64, P, P, P]),
+    "jy_keys_lookup": (I32, [P, I32, U64, P, P, P]),
+    "jy_keys_count": (U64, [P, I32]),
+    "jy_keys_reserve": (I32, [P, I32, U64]),
+    "jy_key_owner": (U32, [P, U64, U32]),
+    "jy_values_pack": (I32, [P, I32, U64, P, P, P, P]),
+    "jy_gcount_converge": (I32, [P, U64, P, P, P, I32]),
+    "jy_gcount_converge_block": (I32, [P, U32, P, U32, U32, P, I32]),
+    "jy_gcount_get": (I32, [P, U64, P, P, I32]),
+    "jy_pncount_converge": (I32, [P, U64, P, P, P, U64, P, P, P, I32]),
+    "jy_pncount_converge_block": (I32, [P, U32, P, U32, U32, P, P, I32]),
+    "jy_pncount_get": (I32, [P, U64, P, P, I32]),
+    "jy_counter_export": (I32, [P, I32, U32, U32, U32, P]),
+    "jy_treg_converge": (I32, [P, U64, P, P, P, P, I32]),
+    "jy_treg_read": (I32, [P, U64, P, P, P, P]),
+    "jy_arena_read": (I32, [P, I32, U64, U64, P]),
+    "jy_tlog_converge": (I32, [P, U64, P, P, P, U64, P, P, P, I32]),
+    "jy_tlog_read_sizes": (I32, [P, U64, P, P, P]),
+    "jy_tlog_read": (I32, [P, U64, P, P, P, P, P]),
+    "jy_ujson_converge": (I32, [P, U64, P, P, U64, P, P, P, U64, P, P, U64, P, I32]),
+    "jy_ujson_read_sizes": (I32, [P, U64, P, P, P]),
+    "jy_ujson_read": (I32, [P, U64, P, P, P, P, P, P, P]),
+}
+
+_lib = None
+
+
+def load(path=LIB_PATH):
+    """Load the engine library (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"{path} is missing: build it with `make -C jylis_amd` (hipcc, gfx950); "
+            "there is no CPU fallback for the converge path")
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib

@@ -1,0 +1,618 @@
+// engine.hip -- engine lifecycle, interning, staging and the C ABI wrappers.
+//
+// Boundary: RepoManagerCore.converge_deltas (jylis/repo_manager.pony:92-93)
+// and the per-type Repo*.converge / get entry points (repo_gcount.pony:50-55,
+// repo_pncount.pony:52-57, repo_treg.pony:51-63, repo_tlog.pony:66-96,
+// repo_ujson.pony:65-72).  See include/jylis_gpu.h for the contract.
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "jy_internal.hpp"
+
+namespace {
+
+u64 round_up(u64 x, u64 a) { return (x + a - 1) / a * a; }
+
+int32_t check_type(jy_engine* eng, int32_t type) {
+  if (type < 0 || type >= JY_NTYPES) return eng->fail(JY_ETYPE, "unknown CRDT type");
+  return JY_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// memory helpers
+
+int32_t jy_realloc(jy_engine* eng, void** p, u64 old_bytes, u64 new_bytes, bool zero_tail) {
+  if (new_bytes <= old_bytes && *p) return JY_OK;
+  void* np = nullptr;
+  hipError_t e = hipMalloc(&np, new_bytes ? new_bytes : 8);
+  if (e != hipSuccess)
+    return eng->fail(JY_ENOMEM, "hipMalloc(" + std::to_string(new_bytes) + "): " + hipGetErrorString(e));
+  if (*p && old_bytes) JY_HIP(eng, hipMemcpyAsync(np, *p, old_bytes, hipMemcpyDeviceToDevice, eng->stream));
+  if (zero_tail && new_bytes > old_bytes)
+    JY_HIP(eng, hipMemsetAsync(static_cast<uint8_t*>(np) + old_bytes, 0, new_bytes - old_bytes, eng->stream));
+  if (*p) {
+    // the old buffer may still be read by queued work: free in stream order
+    JY_HIP(eng, hipStreamSynchronize(eng->stream));
+    JY_HIP(eng, hipFree(*p));
+  }
+  *p = np;
+  return JY_OK;
+}
+
+int32_t jy_scratch(jy_engine* eng, int idx, u64 bytes, void** out) {
+  DevArray& a = eng->scratch[idx];
+  if (a.bytes < bytes) {
+    u64 nb = std::max<u64>(round_up(bytes + bytes / 4, 256), 4096);
+    if (a.p) {
+      JY_HIP(eng, hipStreamSynchronize(eng->stream));
+      JY_HIP(eng, hipFree(a.p));
+      a.p = nullptr;
+    }
+    hipError_t e = hipMalloc(&a.p, nb);
+    if (e != hipSuccess) return eng->fail(JY_ENOMEM, std::string("scratch hipMalloc: ") + hipGetErrorString(e));
+    a.bytes = nb;
+  }
+  *out = a.p;
+  return JY_OK;
+}
+
+static int32_t stage_begin(jy_engine* eng) {
+  eng->pin_used = false;
+  return JY_OK;
+}
+static int32_t stage_end(jy_engine* eng) {
+  if (eng->pin_used) JY_HIP(eng, hipEventRecord(eng->pin_ready, eng->stream));
+  return JY_OK;
+}
+
+int32_t jy_stage(jy_engine* eng, int idx, const void* src, u64 bytes, int32_t mem, const void** dev_out) {
+  if (mem == JY_DEVICE || bytes == 0) {
+    *dev_out = src;
+    if (bytes == 0 && mem != JY_DEVICE) {
+      void* d;
+      JY_TRY(jy_scratch(eng, idx, 8, &d));
+      *dev_out = d;
+    }
+    return JY_OK;
+  }
+  if (mem != JY_HOST) return eng->fail(JY_EINVAL, "mem must be JY_HOST or JY_DEVICE");
+  void* d;
+  JY_TRY(jy_scratch(eng, idx, bytes, &d));
+  if (!eng->pin_used) {
+    // the previous call's staging copies must have drained before reuse
+    JY_HIP(eng, hipEventSynchronize(eng->pin_ready));
+    eng->pin_cursor = 0;
+    eng->pin_used = true;
+  }
+  u64 need = round_up(eng->pin_cursor, 256) + bytes;
+  if (need > eng->pin_bytes) {
+    // grow: drain everything that may read the old pinned region
+    JY_HIP(eng, hipStreamSynchronize(eng->stream));
+    if (eng->pin) JY_HIP(eng, hipHostFree(eng->pin));
+    eng->pin = nullptr;
+    u64 nb = std::max<u64>(need * 2, 1ull << 20);
+    JY_HIP(eng, hipHostMalloc(&eng->pin, nb, hipHostMallocDefault));
+    eng->pin_bytes = nb;
+    eng->pin_cursor = 0;
+  }
+  u64 at = round_up(eng->pin_cursor, 256);
+  std::memcpy(static_cast<uint8_t*>(eng->pin) + at, src, bytes);
+  JY_HIP(eng, hipMemcpyAsync(d, static_cast<uint8_t*>(eng->pin) + at, bytes, hipMemcpyHostToDevice, eng->stream));
+  eng->pin_cursor = at + bytes;
+  *dev_out = d;
+  return JY_OK;
+}
+
+// Device copy of a block merge's column list; re-uploaded only when it changes.
+static int32_t cols_to_device(jy_engine* eng, u32 ncols, const u16* cols, const u16** out) {
+  if (eng->cols_cache.size() == ncols && eng->cols_dev &&
+      std::equal(eng->cols_cache.begin(), eng->cols_cache.end(), cols)) {
+    *out = eng->cols_dev;
+    return JY_OK;
+  }
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));  // queued merges may still read the old list
+  if (ncols > eng->cols_dev_cap) {
+    if (eng->cols_dev) JY_HIP(eng, hipFree(eng->cols_dev));
+    eng->cols_dev = nullptr;
+    JY_HIP(eng, hipMalloc(reinterpret_cast<void**>(&eng->cols_dev), std::max<u64>(ncols, 64) * 2));
+    eng->cols_dev_cap = std::max<u64>(ncols, 64);
+  }
+  JY_HIP(eng, hipMemcpy(eng->cols_dev, cols, (u64)ncols * 2, hipMemcpyHostToDevice));
+  eng->cols_cache.assign(cols, cols + ncols);
+  *out = eng->cols_dev;
+  return JY_OK;
+}
+
+int32_t jy_ensure_slots(jy_engine* eng, int32_t type, u64 n) {
+  switch (type) {
+    case JY_GCOUNT: return jy_counter_grow(eng, 0, 0, n);
+    case JY_PNCOUNT: return jy_counter_grow(eng, 1, 0, n);
+    case JY_TREG: return jy_treg_grow(eng, n);
+    case JY_TLOG: return jy_tlog_grow(eng, n);
+    case JY_UJSON: return jy_ujson_grow(eng, n);
+  }
+  return eng->fail(JY_ETYPE, "unknown CRDT type");
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+
+extern "C" {
+
+void jy_config_default(jy_config* cfg) {
+  std::memset(cfg, 0, sizeof(*cfg));
+  cfg->device = 0;
+  cfg->counter_columns = 16;
+  cfg->ujson_columns = 16;
+  for (int t = 0; t < JY_NTYPES; t++) {
+    cfg->key_capacity[t] = 1024;
+    cfg->entry_capacity[t] = 8192;
+    cfg->arena_capacity[t] = 1 << 16;
+  }
+}
+
+int32_t jy_engine_create(const jy_config* cfg, jy_engine** out) {
+  *out = nullptr;
+  jy_engine* eng = new jy_engine();
+  if (cfg) eng->cfg = *cfg;
+  else jy_config_default(&eng->cfg);
+  if (eng->cfg.counter_columns == 0) eng->cfg.counter_columns = 16;
+  if (eng->cfg.ujson_columns == 0) eng->cfg.ujson_columns = 16;
+  eng->device = eng->cfg.device;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    // the product path has no CPU fallback: fail loudly
+    delete eng;
+    return JY_EHIP;
+  }
+  if (hipSetDevice(eng->device) != hipSuccess ||
+      hipStreamCreateWithFlags(&eng->own_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&eng->pin_ready, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&eng->total_ready, hipEventDisableTiming) != hipSuccess ||
+      hipMalloc(&eng->skipped_dev, 8) != hipSuccess || hipMemset(eng->skipped_dev, 0, 8) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&eng->pin_total), 64, hipHostMallocDefault) != hipSuccess) {
+    delete eng;
+    return JY_EHIP;
+  }
+  eng->stream = eng->own_stream;
+  std::memset(eng->pin_total, 0, 64);
+  hipEventRecord(eng->pin_ready, eng->stream);
+  hipEventRecord(eng->total_ready, eng->stream);
+  int32_t rc = JY_OK;
+  for (int t = 0; t < JY_NTYPES && rc == JY_OK; t++) rc = jy_ensure_slots(eng, t, eng->cfg.key_capacity[t]);
+  if (rc == JY_OK) rc = jy_counter_grow(eng, 0, eng->cfg.counter_columns, 0);
+  if (rc == JY_OK) rc = jy_counter_grow(eng, 1, eng->cfg.counter_columns, 0);
+  if (rc != JY_OK) {
+    std::fprintf(stderr, "jy_engine_create: %s\n", eng->err.c_str());
+    jy_engine_destroy(eng);
+    return rc;
+  }
+  hipStreamSynchronize(eng->stream);
+  *out = eng;
+  return JY_OK;
+}
+
+void jy_engine_destroy(jy_engine* eng) {
+  if (!eng) return;
+  hipSetDevice(eng->device);
+  if (eng->stream) hipStreamSynchronize(eng->stream);
+  auto F = [](void* p) {
+    if (p) hipFree(p);
+  };
+  for (int w = 0; w < 2; w++) F(eng->cnt[w].slab);
+  F(eng->treg.ts);
+  F(eng->treg.pre);
+  F(eng->treg.lr);
+  for (int b = 0; b < 2; b++) {
+    F(eng->tlog.off[b]);
+    F(eng->tlog.ts[b]);
+    F(eng->tlog.pre[b]);
+    F(eng->tlog.lr[b]);
+    F(eng->ujson.eoff[b]);
+    F(eng->ujson.dots[b]);
+    F(eng->ujson.elems[b]);
+    F(eng->ujson.coff[b]);
+    F(eng->ujson.cloud[b]);
+  }
+  F(eng->tlog.cutoff);
+  F(eng->ujson.vv);
+  for (auto& a : eng->arena) F(a.p);
+  for (auto& s : eng->scratch) F(s.p);
+  F(eng->skipped_dev);
+  F(eng->cols_dev);
+  if (eng->pin) hipHostFree(eng->pin);
+  if (eng->pin_total) hipHostFree(eng->pin_total);
+  if (eng->pin_ready) hipEventDestroy(eng->pin_ready);
+  if (eng->total_ready) hipEventDestroy(eng->total_ready);
+  if (eng->own_stream) hipStreamDestroy(eng->own_stream);
+  delete eng;
+}
+
+const char* jy_last_error(const jy_engine* eng) { return eng ? eng->err.c_str() : "null engine"; }
+
+uint64_t jy_skipped(const jy_engine* eng) {
+  jy_engine* e = const_cast<jy_engine*>(eng);
+  u64 dev = 0;
+  hipSetDevice(e->device);
+  hipStreamSynchronize(e->stream);
+  hipMemcpy(&dev, e->skipped_dev, 8, hipMemcpyDeviceToHost);
+  return dev + e->skipped_host;
+}
+
+int32_t jy_set_stream(jy_engine* eng, void* s) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  eng->stream = s ? static_cast<hipStream_t>(s) : eng->own_stream;
+  // events recorded on the previous stream are complete (synchronised above)
+  JY_HIP(eng, hipEventRecord(eng->pin_ready, eng->stream));
+  JY_HIP(eng, hipEventRecord(eng->total_ready, eng->stream));
+  return JY_OK;
+}
+void* jy_get_stream(jy_engine* eng) { return eng->stream; }
+
+int32_t jy_sync(jy_engine* eng) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  return JY_OK;
+}
+
+// ---- replicas ----
+int32_t jy_replica_col(jy_engine* eng, uint64_t id, uint32_t* col) {
+  auto it = eng->rep_col.find(id);
+  if (it != eng->rep_col.end()) {
+    *col = it->second;
+    return JY_OK;
+  }
+  if (eng->rep_id.size() >= 0xFFFF) return eng->fail(JY_ERANGE, "more than 65535 replica identities");
+  u32 c = (u32)eng->rep_id.size();
+  eng->rep_id.push_back(id);
+  eng->rep_col.emplace(id, c);
+  *col = c;
+  return JY_OK;
+}
+int32_t jy_replica_id(const jy_engine* eng, uint32_t col, uint64_t* id) {
+  if (col >= eng->rep_id.size()) return JY_ERANGE;
+  *id = eng->rep_id[col];
+  return JY_OK;
+}
+uint32_t jy_replica_count(const jy_engine* eng) { return (uint32_t)eng->rep_id.size(); }
+
+// ---- keys ----
+int32_t jy_keys_intern(jy_engine* eng, int32_t type, uint64_t n, const uint8_t* kb, const uint64_t* ko,
+                       uint32_t* slots) {
+  JY_TRY(check_type(eng, type));
+  JY_HIP(eng, hipSetDevice(eng->device));
+  KeyIndex& ix = eng->keys[type];
+  u64 nk = eng->nkeys[type];
+  if (ix.map.empty()) ix.map.reserve(std::max<u64>(n, 1024));
+  for (u64 i = 0; i < n; i++) {
+    std::string k(reinterpret_cast<const char*>(kb) + ko[i], ko[i + 1] - ko[i]);
+    auto r = ix.map.emplace(std::move(k), (u32)nk);
+    if (r.second) {
+      if (nk >= 0xFFFFFFFEull) return eng->fail(JY_ERANGE, "slot space exhausted");
+      nk++;
+    }
+    slots[i] = r.first->second;
+  }
+  JY_TRY(jy_ensure_slots(eng, type, nk));
+  eng->nkeys[type] = nk;
+  return JY_OK;
+}
+
+int32_t jy_keys_lookup(const jy_engine* eng, int32_t type, uint64_t n, const uint8_t* kb, const uint64_t* ko,
+                       uint32_t* slots) {
+  if (type < 0 || type >= JY_NTYPES) return JY_ETYPE;
+  const KeyIndex& ix = eng->keys[type];
+  for (u64 i = 0; i < n; i++) {
+    auto it = ix.map.find(std::string(reinterpret_cast<const char*>(kb) + ko[i], ko[i + 1] - ko[i]));
+    slots[i] = it == ix.map.end() ? JY_NO_SLOT : it->second;
+  }
+  return JY_OK;
+}
+
+uint64_t jy_keys_count(const jy_engine* eng, int32_t type) {
+  return (type < 0 || type >= JY_NTYPES) ? 0 : eng->nkeys[type];
+}
+
+int32_t jy_keys_reserve(jy_engine* eng, int32_t type, uint64_t cap) {
+  JY_TRY(check_type(eng, type));
+  JY_HIP(eng, hipSetDevice(eng->device));
+  eng->keys[type].map.reserve(cap);
+  return jy_ensure_slots(eng, type, cap);
+}
+
+// Owner shard: FNV-1a 64 over the key bytes, splitmix64 finaliser, mod S.
+uint32_t jy_key_owner(const uint8_t* key, uint64_t len, uint32_t nshards) {
+  u64 h = 0xCBF29CE484222325ull;
+  for (u64 i = 0; i < len; i++) {
+    h ^= key[i];
+    h *= 0x100000001B3ull;
+  }
+  h ^= h >> 30;
+  h *= 0xBF58476D1CE4E5B9ull;
+  h ^= h >> 27;
+  h *= 0x94D049BB133111EBull;
+  h ^= h >> 31;
+  return nshards ? (uint32_t)(h % nshards) : 0;
+}
+
+// ---- string values ----
+int32_t jy_values_pack(jy_engine* eng, int32_t type, uint64_t n, const uint8_t* bytes, const uint64_t* offs,
+                       uint64_t* pre, uint64_t* lr) {
+  JY_TRY(check_type(eng, type));
+  JY_HIP(eng, hipSetDevice(eng->device));
+  Arena& a = eng->arena[type];
+  u64 add = 0;
+  for (u64 i = 0; i < n; i++) {
+    u64 len = offs[i + 1] - offs[i];
+    if (len > JY_MAX_VALUE_LEN) return eng->fail(JY_ERANGE, "value longer than 16 MiB");
+    if (len > 8) add += len;
+  }
+  if (a.len + add > a.cap) {
+    u64 nc = std::max<u64>(std::max<u64>(a.cap * 2, a.len + add), 1 << 16);
+    void* p = a.p;
+    JY_TRY(jy_realloc(eng, &p, a.len, nc, false));
+    a.p = static_cast<uint8_t*>(p);
+    a.cap = nc;
+  }
+  if ((a.len + add) >> (64 - JY_LR_LEN_BITS)) return eng->fail(JY_ERANGE, "arena offset overflow");
+  std::vector<uint8_t> tail;
+  tail.reserve(add);
+  u64 at = a.len;
+  for (u64 i = 0; i < n; i++) {
+    const uint8_t* v = bytes + offs[i];
+    u64 len = offs[i + 1] - offs[i];
+    u64 p = 0;
+    for (u64 j = 0; j < 8; j++) p = (p << 8) | (j < len ? v[j] : 0);
+    pre[i] = p;
+    if (len > 8) {
+      lr[i] = (at << JY_LR_LEN_BITS) | len;
+      tail.insert(tail.end(), v, v + len);
+      at += len;
+    } else {
+      lr[i] = len;
+    }
+  }
+  if (add) {
+    JY_TRY(stage_begin(eng));
+    const void* d;
+    // stage through pinned memory, then device-to-device into the arena
+    JY_TRY(jy_stage(eng, 7, tail.data(), add, JY_HOST, &d));
+    JY_HIP(eng, hipMemcpyAsync(a.p + a.len, d, add, hipMemcpyDeviceToDevice, eng->stream));
+    JY_TRY(stage_end(eng));
+  }
+  a.len += add;
+  return JY_OK;
+}
+
+int32_t jy_arena_read(jy_engine* eng, int32_t type, uint64_t off, uint64_t len, uint8_t* dst) {
+  JY_TRY(check_type(eng, type));
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (off + len > eng->arena[type].len) return eng->fail(JY_ERANGE, "arena read out of range");
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  JY_HIP(eng, hipMemcpy(dst, eng->arena[type].p + off, len, hipMemcpyDeviceToHost));
+  return JY_OK;
+}
+
+// ---- counters ----
+static int32_t counter_cols_check(jy_engine* eng, int which, u64 n, const u16* col, int32_t mem) {
+  // columns must name known replicas; grow the slab's column capacity
+  u32 nrep = (u32)eng->rep_id.size();
+  if (mem == JY_HOST) {
+    for (u64 i = 0; i < n; i++)
+      if (col[i] >= nrep) return eng->fail(JY_ERANGE, "column names no registered replica");
+  }
+  return jy_counter_grow(eng, which, nrep, 0);
+}
+
+static int32_t slots_check(jy_engine* eng, int32_t type, u64 n, const u32* slot, int32_t mem) {
+  if (mem != JY_HOST) return JY_OK;
+  u64 nk = eng->nkeys[type];
+  for (u64 i = 0; i < n; i++)
+    if (slot[i] >= nk) return eng->fail(JY_ERANGE, "slot was never interned");
+  return JY_OK;
+}
+
+int32_t jy_gcount_converge(jy_engine* eng, uint64_t n, const uint32_t* slot, const uint16_t* col,
+                           const uint64_t* val, int32_t mem) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (n == 0) return JY_OK;
+  JY_TRY(slots_check(eng, JY_GCOUNT, n, slot, mem));
+  JY_TRY(counter_cols_check(eng, 0, n, col, mem));
+  const void *ds, *dc, *dv;
+  JY_TRY(stage_begin(eng));
+  JY_TRY(jy_stage(eng, 0, slot, n * 4, mem, &ds));
+  JY_TRY(jy_stage(eng, 1, col, n * 2, mem, &dc));
+  JY_TRY(jy_stage(eng, 2, val, n * 8, mem, &dv));
+  JY_TRY(stage_end(eng));
+  return jy_counter_coo(eng, 0, 0, n, (const u32*)ds, (const u16*)dc, (const u64*)dv);
+}
+
+int32_t jy_gcount_converge_block(jy_engine* eng, uint32_t ncols, const uint16_t* cols, uint32_t slot0,
+                                 uint32_t nslots, const uint64_t* vals, int32_t mem) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (ncols == 0 || nslots == 0) return JY_OK;
+  if ((u64)slot0 + nslots > eng->nkeys[JY_GCOUNT]) return eng->fail(JY_ERANGE, "slot run was never interned");
+  JY_TRY(counter_cols_check(eng, 0, ncols, cols, JY_HOST));
+  const void* dv;
+  const u16* dc;
+  JY_TRY(cols_to_device(eng, ncols, cols, &dc));
+  JY_TRY(stage_begin(eng));
+  JY_TRY(jy_stage(eng, 2, vals, (u64)ncols * nslots * 8, mem, &dv));
+  JY_TRY(stage_end(eng));
+  return jy_counter_block(eng, 0, ncols, dc, slot0, nslots, (const u64*)dv, nullptr);
+}
+
+static int32_t counter_get(jy_engine* eng, int which, int32_t type, uint64_t n, const uint32_t* slots,
+                           uint64_t* out, int32_t mem) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (n == 0) return JY_OK;
+  const void* ds;
+  JY_TRY(stage_begin(eng));
+  JY_TRY(jy_stage(eng, 0, slots, n * 4, mem, &ds));
+  JY_TRY(stage_end(eng));
+  u64* dout = out;
+  if (mem == JY_HOST) {
+    void* p;
+    JY_TRY(jy_scratch(eng, 3, n * 8, &p));
+    dout = static_cast<u64*>(p);
+  }
+  JY_TRY(jy_counter_sum(eng, which, n, (const u32*)ds, dout));
+  if (mem == JY_HOST) {
+    JY_HIP(eng, hipMemcpyAsync(out, dout, n * 8, hipMemcpyDeviceToHost, eng->stream));
+    JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  }
+  (void)type;
+  return JY_OK;
+}
+
+int32_t jy_gcount_get(jy_engine* eng, uint64_t n, const uint32_t* slots, uint64_t* out, int32_t mem) {
+  return counter_get(eng, 0, JY_GCOUNT, n, slots, out, mem);
+}
+
+int32_t jy_pncount_converge(jy_engine* eng, uint64_t np, const uint32_t* pslot, const uint16_t* pcol,
+                            const uint64_t* pval, uint64_t nn, const uint32_t* nslot, const uint16_t* ncol,
+                            const uint64_t* nval, int32_t mem) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  JY_TRY(slots_check(eng, JY_PNCOUNT, np, pslot, mem));
+  JY_TRY(slots_check(eng, JY_PNCOUNT, nn, nslot, mem));
+  JY_TRY(counter_cols_check(eng, 1, np, pcol, mem));
+  JY_TRY(counter_cols_check(eng, 1, nn, ncol, mem));
+  if (np) {
+    const void *ds, *dc, *dv;
+    JY_TRY(stage_begin(eng));
+    JY_TRY(jy_stage(eng, 0, pslot, np * 4, mem, &ds));
+    JY_TRY(jy_stage(eng, 1, pcol, np * 2, mem, &dc));
+    JY_TRY(jy_stage(eng, 2, pval, np * 8, mem, &dv));
+    JY_TRY(stage_end(eng));
+    JY_TRY(jy_counter_coo(eng, 1, 0, np, (const u32*)ds, (const u16*)dc, (const u64*)dv));
+  }
+  if (nn) {
+    const void *ds, *dc, *dv;
+    JY_TRY(stage_begin(eng));
+    JY_TRY(jy_stage(eng, 4, nslot, nn * 4, mem, &ds));
+    JY_TRY(jy_stage(eng, 5, ncol, nn * 2, mem, &dc));
+    JY_TRY(jy_stage(eng, 6, nval, nn * 8, mem, &dv));
+    JY_TRY(stage_end(eng));
+    JY_TRY(jy_counter_coo(eng, 1, 1, nn, (const u32*)ds, (const u16*)dc, (const u64*)dv));
+  }
+  return JY_OK;
+}
+
+int32_t jy_pncount_converge_block(jy_engine* eng, uint32_t ncols, const uint16_t* cols, uint32_t slot0,
+                                  uint32_t nslots, const uint64_t* vp, const uint64_t* vn, int32_t mem) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (ncols == 0 || nslots == 0) return JY_OK;
+  if ((u64)slot0 + nslots > eng->nkeys[JY_PNCOUNT]) return eng->fail(JY_ERANGE, "slot run was never interned");
+  JY_TRY(counter_cols_check(eng, 1, ncols, cols, JY_HOST));
+  const void *dp, *dn;
+  const u16* dc;
+  JY_TRY(cols_to_device(eng, ncols, cols, &dc));
+  JY_TRY(stage_begin(eng));
+  JY_TRY(jy_stage(eng, 2, vp, (u64)ncols * nslots * 8, mem, &dp));
+  JY_TRY(jy_stage(eng, 6, vn, (u64)ncols * nslots * 8, mem, &dn));
+  JY_TRY(stage_end(eng));
+  return jy_counter_block(eng, 1, ncols, dc, slot0, nslots, (const u64*)dp, (const u64*)dn);
+}
+
+int32_t jy_pncount_get(jy_engine* eng, uint64_t n, const uint32_t* slots, int64_t* out, int32_t mem) {
+  return counter_get(eng, 1, JY_PNCOUNT, n, slots, reinterpret_cast<uint64_t*>(out), mem);
+}
+
+int32_t jy_counter_export(jy_engine* eng, int32_t type, uint32_t ncols, uint32_t slot0, uint32_t nslots,
+                          uint64_t* out) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (type != JY_GCOUNT && type != JY_PNCOUNT) return eng->fail(JY_ETYPE, "not a counter type");
+  int w = type == JY_GCOUNT ? 0 : 1;
+  CounterState& c = eng->cnt[w];
+  if (ncols > c.ccap || (u64)slot0 + nslots > c.kcap) return eng->fail(JY_ERANGE, "export out of range");
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  int nsigns = w + 1;
+  for (int s = 0; s < nsigns; s++)
+    for (u32 col = 0; col < ncols; col++) {
+      const u64* src = c.slab + ((u64)s * c.ccap + col) * c.kcap + slot0;
+      JY_HIP(eng, hipMemcpy(out + ((u64)s * ncols + col) * nslots, src, (u64)nslots * 8, hipMemcpyDeviceToHost));
+    }
+  return JY_OK;
+}
+
+// ---- TREG ----
+int32_t jy_treg_converge(jy_engine* eng, uint64_t n, const uint32_t* slot, const uint64_t* ts, const uint64_t* pre,
+                         const uint64_t* lr, int32_t mem) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (n == 0) return JY_OK;
+  JY_TRY(slots_check(eng, JY_TREG, n, slot, mem));
+  if (mem == JY_HOST) {
+    // one delta per key per call (Map semantics); split repeated keys into rounds
+    std::unordered_map<u32, u32> seen;
+    std::vector<u32> round(n);
+    u32 rounds = 1;
+    bool dup = false;
+    {
+      std::vector<uint8_t> mark(eng->nkeys[JY_TREG], 0);
+      for (u64 i = 0; i < n; i++) {
+        if (mark[slot[i]]) dup = true;
+        mark[slot[i]] = 1;
+      }
+    }
+    if (dup) {
+      for (u64 i = 0; i < n; i++) {
+        u32 r = seen[slot[i]]++;
+        round[i] = r;
+        rounds = std::max(rounds, r + 1);
+      }
+      for (u32 r = 0; r < rounds; r++) {
+        std::vector<u32> s;
+        std::vector<u64> t, p, l;
+        for (u64 i = 0; i < n; i++)
+          if (round[i] == r) {
+            s.push_back(slot[i]);
+            t.push_back(ts[i]);
+            p.push_back(pre[i]);
+            l.push_back(lr[i]);
+          }
+        JY_TRY(jy_treg_converge(eng, s.size(), s.data(), t.data(), p.data(), l.data(), JY_HOST));
+      }
+      return JY_OK;
+    }
+    u64 alen = eng->arena[JY_TREG].len;
+    for (u64 i = 0; i < n; i++)
+      if ((lr[i] & JY_LR_LEN_MASK) > 8 && (lr[i] >> JY_LR_LEN_BITS) + (lr[i] & JY_LR_LEN_MASK) > alen)
+        return eng->fail(JY_ERANGE, "value handle outside the arena");
+  }
+  const void *ds, *dt, *dp, *dl;
+  JY_TRY(stage_begin(eng));
+  JY_TRY(jy_stage(eng, 0, slot, n * 4, mem, &ds));
+  JY_TRY(jy_stage(eng, 1, ts, n * 8, mem, &dt));
+  JY_TRY(jy_stage(eng, 2, pre, n * 8, mem, &dp));
+  JY_TRY(jy_stage(eng, 3, lr, n * 8, mem, &dl));
+  JY_TRY(stage_end(eng));
+  return jy_treg_merge(eng, n, (const u32*)ds, (const u64*)dt, (const u64*)dp, (const u64*)dl);
+}
+
+int32_t jy_treg_read(jy_engine* eng, uint64_t n, const uint32_t* slots, uint64_t* ts, uint64_t* pre,
+                     uint64_t* lr) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (n == 0) return JY_OK;
+  JY_TRY(slots_check(eng, JY_TREG, n, slots, JY_HOST));
+  const void* ds;
+  JY_TRY(stage_begin(eng));
+  JY_TRY(jy_stage(eng, 0, slots, n * 4, JY_HOST, &ds));
+  JY_TRY(stage_end(eng));
+  void* o;
+  JY_TRY(jy_scratch(eng, 1, n * 24, &o));
+  u64* d = static_cast<u64*>(o);
+  JY_TRY(jy_treg_gather(eng, n, (const u32*)ds, d, d + n, d + 2 * n));
+  JY_HIP(eng, hipMemcpyAsync(ts, d, n * 8, hipMemcpyDeviceToHost, eng->stream));
+  JY_HIP(eng, hipMemcpyAsync(pre, d + n, n * 8, hipMemcpyDeviceToHost, eng->stream));
+  JY_HIP(eng, hipMemcpyAsync(lr, d + 2 * n, n * 8, hipMemcpyDeviceToHost, eng->stream));
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  return JY_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,189 @@
+// jy_internal.hpp -- engine internals shared by the HIP translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/jylis_gpu.h"
+
+typedef uint64_t u64;
+typedef uint32_t u32;
+typedef uint16_t u16;
+
+#define JY_LR_LEN_BITS 24
+#define JY_LR_LEN_MASK ((1ull << JY_LR_LEN_BITS) - 1)
+#define JY_MAX_VALUE_LEN JY_LR_LEN_MASK
+#define JY_DOT_SEQ_BITS 48
+#define JY_DOT_SEQ_MASK ((1ull << JY_DOT_SEQ_BITS) - 1)
+
+// ---------------------------------------------------------------------------
+// Device-side helpers
+
+// Pony String order on (prefix, lr) handles: unsigned bytewise, then length.
+// prefix = first 8 bytes big-endian zero-padded, so unsigned prefix order is
+// bytewise order of the first min(8, len) bytes up to zero padding; the
+// arena holds the whole value when len > 8.
+__device__ __forceinline__ int jy_value_cmp(u64 pa, u64 la, u64 pb, u64 lb, const uint8_t* __restrict__ arena) {
+  if (pa != pb) return pa < pb ? -1 : 1;
+  const u64 na = la & JY_LR_LEN_MASK, nb = lb & JY_LR_LEN_MASK;
+  if (na > 8 && nb > 8) {
+    const uint8_t* a = arena + (la >> JY_LR_LEN_BITS);
+    const uint8_t* b = arena + (lb >> JY_LR_LEN_BITS);
+    const u64 n = na < nb ? na : nb;
+    for (u64 i = 8; i < n; i++) {
+      const uint8_t x = a[i], y = b[i];
+      if (x != y) return x < y ? -1 : 1;
+    }
+  }
+  // equal prefix and (one side <= 8 bytes, or equal common bytes):
+  // the shorter one is a prefix of the other
+  if (na == nb) return 0;
+  return na < nb ? -1 : 1;
+}
+
+// ---------------------------------------------------------------------------
+// Host-side engine state
+
+struct DevArray {
+  void* p = nullptr;
+  u64 bytes = 0;
+};
+
+struct KeyIndex {
+  std::unordered_map<std::string, u32> map;
+};
+
+struct CounterState {  // GCOUNT (nsigns 1) / PNCOUNT (nsigns 2): slab [sign][col][kcap]
+  u64* slab = nullptr;
+  u32 ccap = 0;  // column capacity
+  u64 kcap = 0;  // slot capacity (column pitch, even)
+};
+
+struct TregState {  // SoA per slot
+  u64* ts = nullptr;
+  u64* pre = nullptr;
+  u64* lr = nullptr;
+  u64 kcap = 0;
+};
+
+struct TlogState {  // CSR, double-buffered entries
+  u64* off[2] = {nullptr, nullptr};  // [kcap + 1]
+  u64* ts[2] = {nullptr, nullptr};
+  u64* pre[2] = {nullptr, nullptr};
+  u64* lr[2] = {nullptr, nullptr};
+  u64 ecap[2] = {0, 0};
+  int cur = 0;
+  u64* cutoff = nullptr;  // [kcap]
+  u64 kcap = 0;
+  u64 nent_bound = 0;  // host upper bound of live entries
+};
+
+struct UjsonState {  // CSR elements + CSR cloud (double-buffered), dense vv
+  u64* eoff[2] = {nullptr, nullptr};  // [kcap + 1]
+  u64* dots[2] = {nullptr, nullptr};
+  u64* elems[2] = {nullptr, nullptr};
+  u64 ecap[2] = {0, 0};
+  u64* coff[2] = {nullptr, nullptr};  // [kcap + 1]
+  u64* cloud[2] = {nullptr, nullptr};
+  u64 ccap[2] = {0, 0};
+  int cur = 0;
+  u64* vv = nullptr;  // [kcap][R]
+  u32 R = 0;
+  u64 kcap = 0;
+  u64 nel_bound = 0, ncloud_bound = 0;
+};
+
+struct Arena {
+  uint8_t* p = nullptr;
+  u64 len = 0, cap = 0;
+};
+
+struct jy_engine {
+  jy_config cfg;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t own_stream = nullptr;
+  std::string err;
+  u64 skipped_host = 0;
+  u64* skipped_dev = nullptr;  // device counter of skipped entries
+
+  std::unordered_map<u64, u32> rep_col;
+  std::vector<u64> rep_id;
+
+  KeyIndex keys[JY_NTYPES];
+  u64 nkeys[JY_NTYPES] = {0, 0, 0, 0, 0};
+  Arena arena[JY_NTYPES];
+
+  CounterState cnt[2];  // [0] GCOUNT, [1] PNCOUNT
+  TregState treg;
+  TlogState tlog;
+  UjsonState ujson;
+
+  // scratch (device) reused across calls, stream-ordered
+  DevArray scratch[8];
+  // column list of the last block merge, kept resident (a peer set rarely changes)
+  std::vector<u16> cols_cache;
+  u16* cols_dev = nullptr;
+  u64 cols_dev_cap = 0;
+  // pinned host staging
+  void* pin = nullptr;
+  u64 pin_bytes = 0;
+  u64 pin_cursor = 0;
+  bool pin_used = false;
+  hipEvent_t pin_ready = nullptr;  // staging may be overwritten once this fired
+  u64* pin_total = nullptr;        // pinned u64[4] for async totals
+  hipEvent_t total_ready = nullptr;
+
+  int32_t fail(int32_t code, const std::string& msg) {
+    err = msg;
+    return code;
+  }
+};
+
+#define JY_HIP(eng, call)                                                                       \
+  do {                                                                                          \
+    hipError_t e_ = (call);                                                                     \
+    if (e_ != hipSuccess)                                                                       \
+      return (eng)->fail(JY_EHIP, std::string(#call) + ": " + hipGetErrorString(e_));        \
+  } while (0)
+
+#define JY_TRY(expr)            \
+  do {                          \
+    int32_t rc_ = (expr);       \
+    if (rc_ != JY_OK) return rc_; \
+  } while (0)
+
+// engine.hip helpers used by the kernel translation units
+int32_t jy_scratch(jy_engine* eng, int idx, u64 bytes, void** out);
+// copy a borrowed input into device memory if it is on the host; returns a
+// device pointer valid in stream order (scratch slot `idx`)
+int32_t jy_stage(jy_engine* eng, int idx, const void* src, u64 bytes, int32_t mem, const void** dev_out);
+int32_t jy_ensure_slots(jy_engine* eng, int32_t type, u64 nkeys);
+int32_t jy_realloc(jy_engine* eng, void** p, u64 old_bytes, u64 new_bytes, bool zero_tail);
+
+// kernel-side entry points (k_*.hip)
+int32_t jy_counter_grow(jy_engine* eng, int which, u32 need_cols, u64 need_slots);
+int32_t jy_counter_coo(jy_engine* eng, int which, int sign, u64 n, const u32* slot, const u16* col, const u64* val);
+int32_t jy_counter_block(jy_engine* eng, int which, u32 ncols, const u16* cols_dev, u32 slot0, u32 nslots,
+                         const u64* vals_p, const u64* vals_n);
+int32_t jy_counter_sum(jy_engine* eng, int which, u64 n, const u32* slots_dev, u64* out_dev);
+
+int32_t jy_treg_grow(jy_engine* eng, u64 need_slots);
+int32_t jy_treg_merge(jy_engine* eng, u64 n, const u32* slot, const u64* ts, const u64* pre, const u64* lr);
+int32_t jy_treg_gather(jy_engine* eng, u64 n, const u32* slots, u64* ts, u64* pre, u64* lr);
+
+int32_t jy_tlog_grow(jy_engine* eng, u64 need_slots);
+int32_t jy_tlog_merge(jy_engine* eng, u64 nkeys, const u32* slot, const u64* cutoff, const u64* offs, u64 nent,
+                      const u64* ts, const u64* pre, const u64* lr);
+
+int32_t jy_ujson_grow(jy_engine* eng, u64 need_slots);
+int32_t jy_ujson_merge(jy_engine* eng, u64 ndocs, const u32* slot, const u64* eoffs, u64 nel, const u64* dots,
+                       const u64* elems, const u64* vvoffs, u64 nvv, const u64* vv, const u64* coffs, u64 ncloud,
+                       const u64* cloud);
+
+// device exclusive scan of n u64 counts into out[0..n] (out[n] = total)
+int32_t jy_scan_u64(jy_engine* eng, const u64* in, u64* out, u64 n);

@@ -1,0 +1,206 @@
+// k_counter.hip -- GCOUNT / PNCOUNT kernels for gfx950.
+//
+// Semantics (bit-exact with the oracle, oracle/jy_oracle.cpp GCounter):
+//   converge: s[slot][col] = max(s[slot][col], v)         gcount.md:45-47,
+//             PNCOUNT: P and N separately                  pncount.md:51-55
+//   value:    sum_col s[slot][col] mod 2^64;  PNCOUNT sum P - sum N, as i64
+//             (repo_gcount.pony:53-55, repo_pncount.pony:55-57)
+//
+// HBM layout: one slab per type, [sign][column][slot] (replica-major).  A
+// flushed peer batch is one replica column, so the dense merge of a peer
+// batch streams one contiguous column; the per-key sum reads across
+// columns with lanes on consecutive slots (coalesced).  Absent replica
+// entries are 0, which is indistinguishable from absent under max and sum.
+//
+// Roofline: HBM.  Block merge moves 24 B per cell (8 delta read, 8 state
+// read, 8 state write); sum-read 8 B per cell + 8 B per key.
+
+#include <algorithm>
+
+#include "jy_internal.hpp"
+
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kUnroll = 4;                          // 16-B vectors in flight per lane
+constexpr u64 kTileCells = kThreads * 2 * kUnroll;  // 2048 cells per tile
+
+// Dense column-block max-merge, 16 B per lane per access, kUnroll
+// independent vectors per lane.  Tiles are walked grid-stride; a tile lies
+// in one (sign, column) row so every access is contiguous.
+__global__ __launch_bounds__(kThreads) void k_block_max_v2(u64* __restrict__ slab, u64 row_pitch, u64 sign_pitch,
+                                                           const u16* __restrict__ cols, u32 ncols, u64 slot0,
+                                                           u64 nslots, const u64* __restrict__ vp,
+                                                           const u64* __restrict__ vn, u64 tiles_per_row,
+                                                           u64 ntiles) {
+  for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const u64 row = t / tiles_per_row;
+    const u64 tile = t - row * tiles_per_row;
+    const u32 sign = (u32)(row / ncols);
+    const u32 c = (u32)(row - (u64)sign * ncols);
+    u64* __restrict__ s = slab + sign * sign_pitch + (u64)cols[c] * row_pitch + slot0;
+    const u64* __restrict__ d = (sign ? vn : vp) + (u64)c * nslots;
+    const u64 base = tile * kTileCells + (u64)threadIdx.x * 2;
+    u64x2 dv[kUnroll], sv[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; u++) {
+      const u64 i = base + (u64)u * (kThreads * 2);
+      if (i < nslots) {
+        dv[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(d + i));
+        sv[u] = *reinterpret_cast<const u64x2*>(s + i);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; u++) {
+      const u64 i = base + (u64)u * (kThreads * 2);
+      if (i < nslots) {
+        u64x2 r;
+        r.x = dv[u].x > sv[u].x ? dv[u].x : sv[u].x;
+        r.y = dv[u].y > sv[u].y ? dv[u].y : sv[u].y;
+        *reinterpret_cast<u64x2*>(s + i) = r;
+      }
+    }
+  }
+}
+
+// Scalar variant for odd slot runs / pitches.
+__global__ __launch_bounds__(kThreads) void k_block_max_v1(u64* __restrict__ slab, u64 row_pitch, u64 sign_pitch,
+                                                           const u16* __restrict__ cols, u32 ncols, u64 slot0,
+                                                           u64 nslots, const u64* __restrict__ vp,
+                                                           const u64* __restrict__ vn, u64 tiles_per_row,
+                                                           u64 ntiles) {
+  for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const u64 row = t / tiles_per_row;
+    const u64 tile = t - row * tiles_per_row;
+    const u32 sign = (u32)(row / ncols);
+    const u32 c = (u32)(row - (u64)sign * ncols);
+    u64* __restrict__ s = slab + sign * sign_pitch + (u64)cols[c] * row_pitch + slot0;
+    const u64* __restrict__ d = (sign ? vn : vp) + (u64)c * nslots;
+    const u64 base = tile * kTileCells + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < 2 * kUnroll; u++) {
+      const u64 i = base + (u64)u * kThreads;
+      if (i < nslots) {
+        const u64 dv = d[i], sv = s[i];
+        s[i] = dv > sv ? dv : sv;
+      }
+    }
+  }
+}
+
+// Sparse COO max-merge.  Cells of one call may repeat (several deltas for
+// one key, or a delta naming a replica twice): the 64-bit atomic max keeps
+// the join exact in any order.
+__global__ __launch_bounds__(kThreads) void k_coo_max(u64* __restrict__ slab, u64 row_pitch,
+                                                      const u32* __restrict__ slot, const u16* __restrict__ col,
+                                                      const u64* __restrict__ val, u64 n) {
+  const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  u64* p = slab + (u64)col[i] * row_pitch + slot[i];
+  const u64 v = val[i];
+  if (v > *p) __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// value(): wrapping sum over the used replica columns; PNCOUNT subtracts N.
+__global__ __launch_bounds__(kThreads) void k_sum(const u64* __restrict__ slab, u64 row_pitch, u64 sign_pitch,
+                                                  u32 ncols, u32 nsigns, const u32* __restrict__ slots, u64 n,
+                                                  u64* __restrict__ out) {
+  const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const u64 s = slots ? (u64)slots[i] : i;
+  u64 acc = 0;
+  const u64* p = slab + s;
+#pragma unroll 8
+  for (u32 c = 0; c < ncols; c++) acc += p[(u64)c * row_pitch];
+  if (nsigns == 2) {
+    const u64* q = slab + sign_pitch + s;
+#pragma unroll 8
+    for (u32 c = 0; c < ncols; c++) acc -= q[(u64)c * row_pitch];
+  }
+  out[i] = acc;
+}
+
+u64 grid_for(u64 ntiles) {
+  // 256 CUs x 8 resident 256-thread blocks; grid-stride beyond that
+  return std::max<u64>(1, std::min<u64>(ntiles, 256ull * 8));
+}
+
+}  // namespace
+
+int32_t jy_counter_grow(jy_engine* eng, int which, u32 need_cols, u64 need_slots) {
+  CounterState& c = eng->cnt[which];
+  const u32 nsigns = which + 1;
+  u32 ncap = c.ccap;
+  u64 nk = c.kcap;
+  if (need_cols > ncap) ncap = std::max<u32>(need_cols, ncap ? std::min<u32>(ncap * 2, 0xFFFF) : need_cols);
+  if (need_slots > nk) nk = std::max<u64>(need_slots, nk ? nk * 2 : need_slots);
+  nk = (nk + 63) & ~63ull;  // 512-B aligned column pitch
+  if (ncap == 0) ncap = eng->cfg.counter_columns;
+  if (ncap == c.ccap && nk == c.kcap && c.slab) return JY_OK;
+  void* p = nullptr;
+  const u64 bytes = (u64)nsigns * ncap * nk * 8;
+  hipError_t e = hipMalloc(&p, bytes);
+  if (e != hipSuccess)
+    return eng->fail(JY_ENOMEM, "counter slab hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
+  JY_HIP(eng, hipMemsetAsync(p, 0, bytes, eng->stream));
+  if (c.slab) {
+    for (u32 s = 0; s < nsigns; s++) {
+      u64* dst = static_cast<u64*>(p) + (u64)s * ncap * nk;
+      const u64* src = c.slab + (u64)s * c.ccap * c.kcap;
+      JY_HIP(eng, hipMemcpy2DAsync(dst, nk * 8, src, c.kcap * 8, c.kcap * 8, c.ccap, hipMemcpyDeviceToDevice,
+                                   eng->stream));
+    }
+    JY_HIP(eng, hipStreamSynchronize(eng->stream));
+    JY_HIP(eng, hipFree(c.slab));
+  }
+  c.slab = static_cast<u64*>(p);
+  c.ccap = ncap;
+  c.kcap = nk;
+  return JY_OK;
+}
+
+int32_t jy_counter_coo(jy_engine* eng, int which, int sign, u64 n, const u32* slot, const u16* col, const u64* val) {
+  if (n == 0) return JY_OK;
+  CounterState& c = eng->cnt[which];
+  u64* base = c.slab + (u64)sign * c.ccap * c.kcap;
+  const u64 blocks = (n + kThreads - 1) / kThreads;
+  hipLaunchKernelGGL(k_coo_max, dim3((u32)blocks), dim3(kThreads), 0, eng->stream, base, c.kcap, slot, col, val, n);
+  JY_HIP(eng, hipGetLastError());
+  return JY_OK;
+}
+
+int32_t jy_counter_block(jy_engine* eng, int which, u32 ncols, const u16* cols_dev, u32 slot0, u32 nslots,
+                         const u64* vp, const u64* vn) {
+  CounterState& c = eng->cnt[which];
+  const u32 nsigns = which + 1;
+  const void* dcols = cols_dev;
+  const u64 rows = (u64)nsigns * ncols;
+  const u64 tiles_per_row = (nslots + kTileCells - 1) / kTileCells;
+  const u64 ntiles = rows * tiles_per_row;
+  const bool vec = (slot0 % 2 == 0) && (nslots % 2 == 0) && (c.kcap % 2 == 0) &&
+                   (reinterpret_cast<uintptr_t>(vp) % 16 == 0) && (!vn || reinterpret_cast<uintptr_t>(vn) % 16 == 0);
+  const u64 grid = grid_for(ntiles);
+  if (vec)
+    hipLaunchKernelGGL(k_block_max_v2, dim3((u32)grid), dim3(kThreads), 0, eng->stream, c.slab, c.kcap,
+                       (u64)c.ccap * c.kcap, static_cast<const u16*>(dcols), ncols, (u64)slot0, (u64)nslots, vp,
+                       vn, tiles_per_row, ntiles);
+  else
+    hipLaunchKernelGGL(k_block_max_v1, dim3((u32)grid), dim3(kThreads), 0, eng->stream, c.slab, c.kcap,
+                       (u64)c.ccap * c.kcap, static_cast<const u16*>(dcols), ncols, (u64)slot0, (u64)nslots, vp,
+                       vn, tiles_per_row, ntiles);
+  JY_HIP(eng, hipGetLastError());
+  return JY_OK;
+}
+
+int32_t jy_counter_sum(jy_engine* eng, int which, u64 n, const u32* slots_dev, u64* out_dev) {
+  if (n == 0) return JY_OK;
+  CounterState& c = eng->cnt[which];
+  const u32 ncols = std::min<u32>((u32)eng->rep_id.size(), c.ccap);
+  const u64 blocks = (n + kThreads - 1) / kThreads;
+  hipLaunchKernelGGL(k_sum, dim3((u32)blocks), dim3(kThreads), 0, eng->stream, c.slab, c.kcap,
+                     (u64)c.ccap * c.kcap, ncols, (u32)(which + 1), slots_dev, n, out_dev);
+  JY_HIP(eng, hipGetLastError());
+  return JY_OK;
+}

@@ -1,0 +1,92 @@
+// k_treg.hip -- TREG last-writer-wins compare-select for gfx950.
+//
+// Semantics (oracle/jy_oracle.cpp TReg; treg.md:58-63): the delta (v, t)
+// replaces the state (v_s, t_s) iff t > t_s, or t == t_s and v > v_s in
+// Pony String order.  A fresh slot is ("", 0) (repo_treg.pony:37-42).
+//
+// HBM layout (SoA per slot): ts u64, pre u64 (first 8 value bytes,
+// big-endian, zero padded), lr u64 (arena offset << 24 | length).  Values
+// longer than 8 bytes also live whole in the type's arena; the byte loop
+// runs only on (timestamp, prefix) ties of two long values.
+//
+// Roofline: HBM.  Per delta entry: 28 B delta read (slot + ts/pre/lr) +
+// 8 B state ts read (pre/lr only on timestamp ties) + 24 B winner write.
+
+#include <algorithm>
+
+#include "jy_internal.hpp"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__global__ __launch_bounds__(kThreads) void k_treg_lww(u64* __restrict__ ts, u64* __restrict__ pre,
+                                                       u64* __restrict__ lr, const uint8_t* __restrict__ arena,
+                                                       const u32* __restrict__ slot, const u64* __restrict__ dts,
+                                                       const u64* __restrict__ dpre, const u64* __restrict__ dlr,
+                                                       u64 n) {
+  const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const u64 s = slot[i];
+  const u64 t = __builtin_nontemporal_load(dts + i);
+  const u64 p = __builtin_nontemporal_load(dpre + i);
+  const u64 l = __builtin_nontemporal_load(dlr + i);
+  const u64 t0 = ts[s];
+  bool win = t > t0;
+  if (t == t0) win = jy_value_cmp(p, l, pre[s], lr[s], arena) > 0;
+  if (win) {
+    ts[s] = t;
+    pre[s] = p;
+    lr[s] = l;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_treg_gather(const u64* __restrict__ ts, const u64* __restrict__ pre,
+                                                          const u64* __restrict__ lr, const u32* __restrict__ slots,
+                                                          u64 n, u64* __restrict__ ots, u64* __restrict__ opre,
+                                                          u64* __restrict__ olr) {
+  const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const u64 s = slots[i];
+  ots[i] = ts[s];
+  opre[i] = pre[s];
+  olr[i] = lr[s];
+}
+
+}  // namespace
+
+int32_t jy_treg_grow(jy_engine* eng, u64 need) {
+  TregState& t = eng->treg;
+  if (need <= t.kcap && t.ts) return JY_OK;
+  u64 nk = std::max<u64>(need, t.kcap ? t.kcap * 2 : need);
+  nk = std::max<u64>((nk + 63) & ~63ull, 64);
+  void *a = t.ts, *b = t.pre, *c = t.lr;
+  JY_TRY(jy_realloc(eng, &a, t.kcap * 8, nk * 8, true));
+  JY_TRY(jy_realloc(eng, &b, t.kcap * 8, nk * 8, true));
+  JY_TRY(jy_realloc(eng, &c, t.kcap * 8, nk * 8, true));
+  t.ts = static_cast<u64*>(a);
+  t.pre = static_cast<u64*>(b);
+  t.lr = static_cast<u64*>(c);
+  t.kcap = nk;
+  return JY_OK;
+}
+
+int32_t jy_treg_merge(jy_engine* eng, u64 n, const u32* slot, const u64* ts, const u64* pre, const u64* lr) {
+  if (n == 0) return JY_OK;
+  TregState& t = eng->treg;
+  const u64 blocks = (n + kThreads - 1) / kThreads;
+  hipLaunchKernelGGL(k_treg_lww, dim3((u32)blocks), dim3(kThreads), 0, eng->stream, t.ts, t.pre, t.lr,
+                     eng->arena[JY_TREG].p, slot, ts, pre, lr, n);
+  JY_HIP(eng, hipGetLastError());
+  return JY_OK;
+}
+
+int32_t jy_treg_gather(jy_engine* eng, u64 n, const u32* slots, u64* ots, u64* opre, u64* olr) {
+  if (n == 0) return JY_OK;
+  TregState& t = eng->treg;
+  const u64 blocks = (n + kThreads - 1) / kThreads;
+  hipLaunchKernelGGL(k_treg_gather, dim3((u32)blocks), dim3(kThreads), 0, eng->stream, t.ts, t.pre, t.lr, slots, n,
+                     ots, opre, olr);
+  JY_HIP(eng, hipGetLastError());
+  return JY_OK;
+}

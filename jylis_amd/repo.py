@@ -1,0 +1,197 @@
+"""GPU-backed Repo* mirrors: the host side of the drop-in boundary.
+
+Each class stands where the reference's RepoGCOUNT / RepoPNCOUNT / RepoTREG /
+RepoTLOG / RepoUJSON stand (jylis/repo_*.pony) and exposes the same converge
+surface as RepoAny (jylis/repo_manager.pony:5-10):
+
+  converge(key, delta)        one (key, delta) pair   (repo_*.pony `converge`)
+  converge_deltas(batch)      a whole decoded batch   (repo_manager.pony:92-93)
+
+but the batch form marshals the whole Array[(String, Any box)] into
+structure-of-arrays and makes ONE engine call, which is the change
+INTEGRATION.md describes for the Pony host.  Batches use the table layout of
+oracle/oracle.py (key_bytes/key_offs + per-type CSR columns), the decoded
+form of a MsgPushDeltas payload (jylis/msg.pony:20-24).
+
+Error behaviour follows the reference: a batch of the wrong type is ignored
+(the `delta' as T box` downcast fails inside `try ... end`,
+repo_gcount.pony:50-51).
+"""
+import numpy as np
+
+from . import engine as E
+from ._lib import GCOUNT, PNCOUNT, TLOG, TREG, UJSON
+
+
+def _keys_of(table):
+    return np.ascontiguousarray(table["key_bytes"], np.uint8), np.ascontiguousarray(table["key_offs"], np.uint64)
+
+
+class _GpuRepo:
+    ctype = None
+
+    def __init__(self, eng):
+        self.eng = eng
+        self.names = []  # slot -> key bytes (the engine interns; the host keeps names for reads)
+
+    def _intern(self, table):
+        kb, ko = _keys_of(table)
+        before = self.eng.nkeys(self.ctype)
+        slots = self.eng.intern(self.ctype, (kb, ko))
+        after = self.eng.nkeys(self.ctype)
+        if after > before:
+            fresh = np.nonzero(slots >= before)[0]
+            order = np.argsort(slots[fresh], kind="stable")
+            seen = set()
+            for i in fresh[order]:
+                s = int(slots[i])
+                if s not in seen:
+                    seen.add(s)
+                    self.names.append(bytes(kb[ko[i]:ko[i + 1]]))
+        return slots
+
+    def slots_of(self, keys):
+        return self.eng.lookup(self.ctype, keys)
+
+    def converge(self, key, delta_table_row):
+        """RepoXXX.converge(key, delta') for one pair (delta given as a 1-key table)."""
+        t = dict(delta_table_row)
+        kb = key.encode() if isinstance(key, str) else bytes(key)
+        t["key_bytes"] = np.frombuffer(kb, np.uint8)
+        t["key_offs"] = np.array([0, len(kb)], np.uint64)
+        self.converge_deltas(t)
+
+    def _sorted_slots(self):
+        order = sorted(range(len(self.names)), key=lambda s: self.names[s])
+        return np.array(order, dtype=np.uint32)
+
+    def _keys_table(self, slots):
+        names = [self.names[s] for s in slots]
+        kb, ko = E.encode_keys(names)
+        return {"key_bytes": kb, "key_offs": ko}
+
+
+class RepoGCOUNT(_GpuRepo):
+    """repo_gcount.pony: GCounter per key, per-replica max-merge."""
+    ctype = GCOUNT
+
+    def converge_deltas(self, batch, ctype=GCOUNT):
+        if ctype != self.ctype:
+            return
+        slots = self._intern(batch)
+        offs = np.asarray(batch["offs"], np.uint64)
+        ids = np.asarray(batch["ids"], np.uint64)
+        if len(ids) == 0:
+            return
+        cols = self.eng.replica_cols(ids.tolist())
+        cell_slot = np.repeat(slots, np.diff(offs).astype(np.int64))
+        self.eng.gcount_converge(cell_slot, cols, np.asarray(batch["vals"], np.uint64))
+
+    def get(self, keys):
+        """GCOUNT GET (repo_gcount.pony:53-55): missing key -> 0"""
+        slots = self.slots_of(keys)
+        out = np.zeros(len(slots), np.uint64)
+        have = slots != E._lib.JY_NO_SLOT
+        if have.any():
+            out[have] = self.eng.gcount_get(slots[have])
+        return out
+
+    def state(self):
+        """oracle-format state table (absent replica entries == 0 are dropped)"""
+        slots = self._sorted_slots()
+        t = self._keys_table(slots)
+        t.update(_counter_table(self.eng, GCOUNT, slots, "", 0))
+        return t
+
+
+class RepoPNCOUNT(_GpuRepo):
+    """repo_pncount.pony: PNCounter per key (two GCounters)."""
+    ctype = PNCOUNT
+
+    def converge_deltas(self, batch, ctype=PNCOUNT):
+        if ctype != self.ctype:
+            return
+        slots = self._intern(batch)
+        parts = []
+        for pre in ("p_", "n_"):
+            offs = np.asarray(batch[pre + "offs"], np.uint64)
+            ids = np.asarray(batch[pre + "ids"], np.uint64)
+            if len(ids) == 0:
+                parts.append(None)
+                continue
+            cols = self.eng.replica_cols(ids.tolist())
+            parts.append((np.repeat(slots, np.diff(offs).astype(np.int64)), cols,
+                          np.asarray(batch[pre + "vals"], np.uint64)))
+        self.eng.pncount_converge(parts[0], parts[1])
+
+    def get(self, keys):
+        """PNCOUNT GET (repo_pncount.pony:55-57): (sum P - sum N) as i64, missing -> 0"""
+        slots = self.slots_of(keys)
+        out = np.zeros(len(slots), np.int64)
+        have = slots != E._lib.JY_NO_SLOT
+        if have.any():
+            out[have] = self.eng.pncount_get(slots[have])
+        return out
+
+    def state(self):
+        slots = self._sorted_slots()
+        t = self._keys_table(slots)
+        t.update(_counter_table(self.eng, PNCOUNT, slots, "p_", 0))
+        t.update(_counter_table(self.eng, PNCOUNT, slots, "n_", 1))
+        return t
+
+
+def _counter_table(eng, ctype, slots, prefix, sign):
+    ncols = eng.replica_count()
+    nk = eng.nkeys(ctype)
+    if nk == 0 or ncols == 0:
+        return {prefix + "offs": np.zeros(len(slots) + 1, np.uint64), prefix + "ids": np.zeros(0, np.uint64),
+                prefix + "vals": np.zeros(0, np.uint64)}
+    dump = eng.counter_export(ctype, ncols, 0, nk)[sign]  # [col][slot]
+    ids_of_col = np.array([eng.replica_id(c) for c in range(ncols)], np.uint64)
+    order = np.argsort(ids_of_col, kind="stable")
+    offs = [0]
+    ids, vals = [], []
+    for s in slots:
+        col_vals = dump[order, s]
+        nz = col_vals != 0
+        ids.append(ids_of_col[order][nz])
+        vals.append(col_vals[nz])
+        offs.append(offs[-1] + int(nz.sum()))
+    return {prefix + "offs": np.array(offs, np.uint64),
+            prefix + "ids": np.concatenate(ids) if ids else np.zeros(0, np.uint64),
+            prefix + "vals": np.concatenate(vals) if vals else np.zeros(0, np.uint64)}
+
+
+class RepoTREG(_GpuRepo):
+    """repo_treg.pony: TRegString per key, LWW by (timestamp, value)."""
+    ctype = TREG
+
+    def converge_deltas(self, batch, ctype=TREG):
+        if ctype != self.ctype:
+            return
+        slots = self._intern(batch)
+        if len(slots) == 0:
+            return
+        pre, lr = self.eng.pack_values(TREG, (batch["val_bytes"], batch["val_offs"]))
+        self.eng.treg_converge(slots, np.asarray(batch["ts"], np.uint64), pre, lr)
+
+    def get(self, key):
+        """TREG GET (repo_treg.pony:54-63): (value, ts), or None if never touched"""
+        s = int(self.slots_of([key])[0])
+        if s == E._lib.JY_NO_SLOT:
+            return None
+        ts, pre, lr = self.eng.treg_read(np.array([s], np.uint32))
+        return self.eng.value_bytes(TREG, pre[0], lr[0]), int(ts[0])
+
+    def state(self):
+        slots = self._sorted_slots()
+        t = self._keys_table(slots)
+        ts, pre, lr = self.eng.treg_read(slots) if len(slots) else (np.zeros(0, np.uint64),) * 3
+        vals = [self.eng.value_bytes(TREG, p, l) for p, l in zip(pre, lr)]
+        vb, vo = E.encode_keys(vals)
+        t.update({"ts": ts, "val_bytes": vb, "val_offs": vo})
+        return t
+
+
+REPOS = {GCOUNT: RepoGCOUNT, PNCOUNT: RepoPNCOUNT, TREG: RepoTREG}

@@ -1,0 +1,87 @@
+"""Shared test helpers: oracle-driven delta streams and state comparison."""
+import numpy as np
+
+
+def strip_zero_counters(t, prefixes):
+    """GCounter entries holding 0 are unobservable (value() and max-merge treat
+    absent == 0); the engine stores replica columns densely, so compare with
+    zero entries removed."""
+    t = dict(t)
+    n = len(t["key_offs"]) - 1
+    for p in prefixes:
+        offs, ids, vals = t[p + "offs"], t[p + "ids"], t[p + "vals"]
+        keep = vals != 0
+        new_offs = np.zeros(n + 1, np.uint64)
+        if len(offs) > 1:
+            cnt = np.add.reduceat(keep.astype(np.uint64), offs[:-1].astype(np.int64)) if len(vals) else np.zeros(n)
+            # reduceat misreports empty segments: fix them
+            seg = np.diff(offs.astype(np.int64))
+            cnt = np.where(seg == 0, 0, cnt)
+            new_offs[1:] = np.cumsum(cnt, dtype=np.uint64)
+        t[p + "offs"], t[p + "ids"], t[p + "vals"] = new_offs, ids[keep], vals[keep]
+    return t
+
+
+COUNTER_PREFIXES = {0: ("",), 1: ("p_", "n_")}
+
+
+def assert_state_equal(ctype, want, got):
+    if ctype in COUNTER_PREFIXES:
+        want = strip_zero_counters(want, COUNTER_PREFIXES[ctype])
+        got = strip_zero_counters(got, COUNTER_PREFIXES[ctype])
+    assert set(want) == set(got), (sorted(want), sorted(got))
+    for k in want:
+        np.testing.assert_array_equal(np.asarray(want[k]), np.asarray(got[k]), err_msg=f"field {k}")
+
+
+def random_history(O, ctype, seed, nrep=4, nops=300, nkeys=12, val_len=14, gossip=0.25):
+    """Run random writes on `nrep` oracle replicas with partial gossip and
+    return every flushed batch (tables), in emission order."""
+    rng = np.random.default_rng(seed)
+    reps = [O.Repo(ctype, int(rng.integers(1, 2**63)) * 2 + 1) for _ in range(nrep)]
+    keys = [f"k{i}" for i in range(nkeys)]
+    batches = []
+
+    def rstr():
+        n = int(rng.integers(0, val_len))
+        # small alphabet -> many shared prefixes / ties
+        return bytes(rng.choice(np.frombuffer(b"aab\x00\xff", np.uint8), size=n))
+
+    for _ in range(nops):
+        r = reps[rng.integers(nrep)]
+        k = keys[rng.integers(nkeys)]
+        if ctype == O.GCOUNT:
+            r.gcount_inc(k, int(rng.integers(0, 1 << 62)))
+        elif ctype == O.PNCOUNT:
+            v = int(rng.integers(-(1 << 62), 1 << 62))
+            (r.pncount_inc if rng.random() < 0.5 else r.pncount_dec)(k, v)
+        elif ctype == O.TREG:
+            r.treg_set(k, rstr(), int(rng.integers(0, 6)))
+        elif ctype == O.TLOG:
+            x = rng.random()
+            if x < 0.8:
+                r.tlog_ins(k, rstr(), int(rng.integers(0, 40)))
+            elif x < 0.9:
+                r.tlog_trimat(k, int(rng.integers(0, 30)))
+            elif x < 0.97:
+                r.tlog_trim(k, int(rng.integers(0, 8)))
+            else:
+                r.tlog_clr(k)
+        elif ctype == O.UJSON:
+            x = rng.random()
+            if x < 0.65:
+                r.ujson_ins(k, int(rng.integers(1, 8)))
+            elif x < 0.9:
+                r.ujson_rm(k, int(rng.integers(1, 8)))
+            else:
+                r.ujson_clr(k)
+        if rng.random() < gossip:
+            b = r.flush().table()
+            batches.append(b)
+            for o in reps:
+                if o is not r and rng.random() < 0.5:
+                    o.converge(b)
+    for r in reps:
+        batches.append(r.flush().table())
+        batches.append(r.state())  # full-state deltas too
+    return batches

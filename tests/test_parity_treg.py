@@ -1,0 +1,103 @@
+"""TREG: the HIP LWW select against the CPU oracle (bit-exact).
+
+Edge cases: timestamp ties broken by Pony String order (bytewise unsigned,
+then shorter-is-less), values sharing 8-byte prefixes, embedded NULs and
+0xFF bytes, empty values, keys created by converge but never set (GET shows
+("", 0), not nil: repo_treg.pony:52,55-61)."""
+import numpy as np
+import pytest
+
+from helpers import assert_state_equal, random_history
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_history_parity(oracle_mod, engine, seed):
+    from jylis_amd.repo import RepoTREG
+    O = oracle_mod
+    want = O.Repo(O.TREG)
+    got = RepoTREG(engine)
+    for b in random_history(O, O.TREG, seed, val_len=20):
+        want.converge(b)
+        got.converge_deltas(b)
+    assert_state_equal(O.TREG, want.state(), got.state())
+
+
+def _batch(keys, vals, ts):
+    from jylis_amd.engine import encode_keys
+    kb, ko = encode_keys(keys)
+    vb, vo = encode_keys(vals)
+    return {"key_bytes": kb, "key_offs": ko, "ts": np.array(ts, np.uint64), "val_bytes": vb, "val_offs": vo}
+
+
+TIES = [  # (state, delta) at equal timestamps
+    (b"", b"a"), (b"a", b""), (b"abc", b"abd"), (b"abcdefgh", b"abcdefgh\x00"),
+    (b"abcdefghij", b"abcdefghik"), (b"abcdefghijk", b"abcdefghij"), (b"\xff", b"\x00\x00"),
+    (b"same-long-value!", b"same-long-value!"), (b"a\x00", b"a"), (b"zzzzzzzzzzzzzzzzzzzz1", b"zzzzzzzzzzzzzzzzzzzz2"),
+]
+
+
+def test_tie_break_order(oracle_mod, engine):
+    from jylis_amd.repo import RepoTREG
+    O = oracle_mod
+    want = O.Repo(O.TREG)
+    got = RepoTREG(engine)
+    keys = [f"t{i}" for i in range(len(TIES))]
+    s = _batch(keys, [a for a, _ in TIES], [7] * len(TIES))
+    d = _batch(keys, [b for _, b in TIES], [7] * len(TIES))
+    for b in (s, d):
+        want.converge(b)
+        got.converge_deltas(b)
+    assert_state_equal(O.TREG, want.state(), got.state())
+    for k, (a, b) in zip(keys, TIES):
+        assert got.get(k) == (max(a, b), 7)  # python bytes order == Pony String order
+
+
+def test_existence_and_nil(oracle_mod, engine):
+    from jylis_amd.repo import RepoTREG
+    got = RepoTREG(engine)
+    got.converge_deltas(_batch(["e"], [b""], [0]))  # ("", 0) delta still creates the key
+    assert got.get("e") == (b"", 0)
+    assert got.get("never") is None
+
+
+def test_repeated_key_in_one_batch(oracle_mod, engine):
+    """several deltas for one key in one call are split into rounds (exact LWW join)"""
+    from jylis_amd.repo import RepoTREG
+    O = oracle_mod
+    want = O.Repo(O.TREG)
+    got = RepoTREG(engine)
+    b = _batch(["k", "k", "j", "k"], [b"x", b"zz", b"q", b"y"], [3, 3, 1, 2])
+    want.converge(b)
+    got.converge_deltas(b)
+    assert_state_equal(O.TREG, want.state(), got.state())
+    assert got.get("k") == (b"zz", 3)
+
+
+def test_large_random(oracle_mod, engine):
+    """50k keys, dense timestamp ties, ~20% shared 8-byte prefixes"""
+    from jylis_amd.repo import RepoTREG
+    O = oracle_mod
+    rng = np.random.default_rng(5)
+    n = 50000
+    keys = [f"r{i}" for i in range(n)]
+    prefixes = [bytes(rng.integers(0, 256, 8).astype(np.uint8)) for _ in range(16)]
+
+    def vals():
+        out = []
+        for _ in range(n):
+            L = int(rng.integers(1, 17))
+            if rng.random() < 0.2:
+                out.append((prefixes[rng.integers(16)] + bytes(rng.integers(0, 256, 8).astype(np.uint8)))[:max(L, 9)])
+            else:
+                out.append(bytes(rng.integers(0, 256, L).astype(np.uint8)))
+        return out
+
+    want = O.Repo(O.TREG)
+    got = RepoTREG(engine)
+    for _ in range(3):
+        b = _batch(keys, vals(), rng.integers(0, 4, n))
+        want.converge(b)
+        got.converge_deltas(b)
+    assert_state_equal(O.TREG, want.state(), got.state())
