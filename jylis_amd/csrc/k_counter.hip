@@ -27,64 +27,51 @@ constexpr int kThreads = 256;
 constexpr int kUnroll = 4;                          // 16-B vectors in flight per lane
 constexpr u64 kTileCells = kThreads * 2 * kUnroll;  // 2048 cells per tile
 
-// Dense column-block max-merge, 16 B per lane per access, kUnroll
-// independent vectors per lane.  Tiles are walked grid-stride; a tile lies
-// in one (sign, column) row so every access is contiguous.
-__global__ __launch_bounds__(kThreads) void k_block_max_v2(u64* __restrict__ slab, u64 row_pitch, u64 sign_pitch,
-                                                           const u16* __restrict__ cols, u32 ncols, u64 slot0,
-                                                           u64 nslots, const u64* __restrict__ vp,
-                                                           const u64* __restrict__ vn, u64 tiles_per_row,
-                                                           u64 ntiles) {
-  for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const u64 row = t / tiles_per_row;
-    const u64 tile = t - row * tiles_per_row;
+// Dense column-block max-merge.  Grid: x = 2048-cell tile of a row, y = row
+// (sign, column); one tile per workgroup (the dispatcher keeps 256 CUs fed
+// better than a grid-stride loop here: tools/mb_stream.hip).  16 B per lane
+// per access, kUnroll independent vectors in flight per lane; every stream
+// is touched once, so loads and stores are nontemporal.
+template <bool kVec>
+__global__ __launch_bounds__(kThreads) void k_block_max(u64* __restrict__ slab, u64 row_pitch, u64 sign_pitch,
+                                                        const u16* __restrict__ cols, u32 ncols, u64 slot0,
+                                                        u64 nslots, const u64* __restrict__ vp,
+                                                        const u64* __restrict__ vn, u64 rows) {
+  for (u64 row = blockIdx.y; row < rows; row += gridDim.y) {
     const u32 sign = (u32)(row / ncols);
     const u32 c = (u32)(row - (u64)sign * ncols);
     u64* __restrict__ s = slab + sign * sign_pitch + (u64)cols[c] * row_pitch + slot0;
     const u64* __restrict__ d = (sign ? vn : vp) + (u64)c * nslots;
-    const u64 base = tile * kTileCells + (u64)threadIdx.x * 2;
-    u64x2 dv[kUnroll], sv[kUnroll];
+    if (kVec) {
+      const u64 base = (u64)blockIdx.x * kTileCells + (u64)threadIdx.x * 2;
+      u64x2 dv[kUnroll], sv[kUnroll];
 #pragma unroll
-    for (int u = 0; u < kUnroll; u++) {
-      const u64 i = base + (u64)u * (kThreads * 2);
-      if (i < nslots) {
-        dv[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(d + i));
-        sv[u] = *reinterpret_cast<const u64x2*>(s + i);
+      for (int u = 0; u < kUnroll; u++) {
+        const u64 i = base + (u64)u * (kThreads * 2);
+        if (i < nslots) {
+          dv[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(d + i));
+          sv[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(s + i));
+        }
       }
-    }
 #pragma unroll
-    for (int u = 0; u < kUnroll; u++) {
-      const u64 i = base + (u64)u * (kThreads * 2);
-      if (i < nslots) {
-        u64x2 r;
-        r.x = dv[u].x > sv[u].x ? dv[u].x : sv[u].x;
-        r.y = dv[u].y > sv[u].y ? dv[u].y : sv[u].y;
-        *reinterpret_cast<u64x2*>(s + i) = r;
+      for (int u = 0; u < kUnroll; u++) {
+        const u64 i = base + (u64)u * (kThreads * 2);
+        if (i < nslots) {
+          u64x2 r;
+          r.x = dv[u].x > sv[u].x ? dv[u].x : sv[u].x;
+          r.y = dv[u].y > sv[u].y ? dv[u].y : sv[u].y;
+          __builtin_nontemporal_store(r, reinterpret_cast<u64x2*>(s + i));
+        }
       }
-    }
-  }
-}
-
-// Scalar variant for odd slot runs / pitches.
-__global__ __launch_bounds__(kThreads) void k_block_max_v1(u64* __restrict__ slab, u64 row_pitch, u64 sign_pitch,
-                                                           const u16* __restrict__ cols, u32 ncols, u64 slot0,
-                                                           u64 nslots, const u64* __restrict__ vp,
-                                                           const u64* __restrict__ vn, u64 tiles_per_row,
-                                                           u64 ntiles) {
-  for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const u64 row = t / tiles_per_row;
-    const u64 tile = t - row * tiles_per_row;
-    const u32 sign = (u32)(row / ncols);
-    const u32 c = (u32)(row - (u64)sign * ncols);
-    u64* __restrict__ s = slab + sign * sign_pitch + (u64)cols[c] * row_pitch + slot0;
-    const u64* __restrict__ d = (sign ? vn : vp) + (u64)c * nslots;
-    const u64 base = tile * kTileCells + threadIdx.x;
+    } else {  // odd slot runs / misaligned inputs
+      const u64 base = (u64)blockIdx.x * kTileCells + threadIdx.x;
 #pragma unroll
-    for (int u = 0; u < 2 * kUnroll; u++) {
-      const u64 i = base + (u64)u * kThreads;
-      if (i < nslots) {
-        const u64 dv = d[i], sv = s[i];
-        s[i] = dv > sv ? dv : sv;
+      for (int u = 0; u < 2 * kUnroll; u++) {
+        const u64 i = base + (u64)u * kThreads;
+        if (i < nslots) {
+          const u64 dv = d[i], sv = s[i];
+          s[i] = dv > sv ? dv : sv;
+        }
       }
     }
   }
@@ -120,11 +107,6 @@ __global__ __launch_bounds__(kThreads) void k_sum(const u64* __restrict__ slab, 
     for (u32 c = 0; c < ncols; c++) acc -= q[(u64)c * row_pitch];
   }
   out[i] = acc;
-}
-
-u64 grid_for(u64 ntiles) {
-  // 256 CUs x 8 resident 256-thread blocks; grid-stride beyond that
-  return std::max<u64>(1, std::min<u64>(ntiles, 256ull * 8));
 }
 
 }  // namespace
@@ -178,18 +160,17 @@ int32_t jy_counter_block(jy_engine* eng, int which, u32 ncols, const u16* cols_d
   const void* dcols = cols_dev;
   const u64 rows = (u64)nsigns * ncols;
   const u64 tiles_per_row = (nslots + kTileCells - 1) / kTileCells;
-  const u64 ntiles = rows * tiles_per_row;
   const bool vec = (slot0 % 2 == 0) && (nslots % 2 == 0) && (c.kcap % 2 == 0) &&
                    (reinterpret_cast<uintptr_t>(vp) % 16 == 0) && (!vn || reinterpret_cast<uintptr_t>(vn) % 16 == 0);
-  const u64 grid = grid_for(ntiles);
+  const dim3 grid((u32)tiles_per_row, (u32)std::min<u64>(rows, 65535));
   if (vec)
-    hipLaunchKernelGGL(k_block_max_v2, dim3((u32)grid), dim3(kThreads), 0, eng->stream, c.slab, c.kcap,
+    hipLaunchKernelGGL(k_block_max<true>, grid, dim3(kThreads), 0, eng->stream, c.slab, c.kcap,
                        (u64)c.ccap * c.kcap, static_cast<const u16*>(dcols), ncols, (u64)slot0, (u64)nslots, vp,
-                       vn, tiles_per_row, ntiles);
+                       vn, rows);
   else
-    hipLaunchKernelGGL(k_block_max_v1, dim3((u32)grid), dim3(kThreads), 0, eng->stream, c.slab, c.kcap,
+    hipLaunchKernelGGL(k_block_max<false>, grid, dim3(kThreads), 0, eng->stream, c.slab, c.kcap,
                        (u64)c.ccap * c.kcap, static_cast<const u16*>(dcols), ncols, (u64)slot0, (u64)nslots, vp,
-                       vn, tiles_per_row, ntiles);
+                       vn, rows);
   JY_HIP(eng, hipGetLastError());
   return JY_OK;
 }
