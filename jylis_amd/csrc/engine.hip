@@ -70,6 +70,9 @@ static int32_t stage_end(jy_engine* eng) {
   return JY_OK;
 }
 
+int32_t jy_stage_begin(jy_engine* eng) { return stage_begin(eng); }
+int32_t jy_stage_end(jy_engine* eng) { return stage_end(eng); }
+
 int32_t jy_stage(jy_engine* eng, int idx, const void* src, u64 bytes, int32_t mem, const void** dev_out) {
   if (mem == JY_DEVICE || bytes == 0) {
     *dev_out = src;
@@ -300,6 +303,9 @@ int32_t jy_keys_intern(jy_engine* eng, int32_t type, uint64_t n, const uint8_t* 
     slots[i] = r.first->second;
   }
   JY_TRY(jy_ensure_slots(eng, type, nk));
+  const u64 before = eng->nkeys[type];
+  if (type == JY_TLOG) JY_TRY(jy_tlog_extend(eng, before, nk));
+  if (type == JY_UJSON) JY_TRY(jy_ujson_extend(eng, before, nk));
   eng->nkeys[type] = nk;
   return JY_OK;
 }
@@ -616,3 +622,7 @@ int32_t jy_treg_read(jy_engine* eng, uint64_t n, const uint32_t* slots, uint64_t
 }
 
 }  // extern "C"
+
+int32_t jy_slots_check(jy_engine* eng, int32_t type, u64 n, const u32* slot, int32_t mem) {
+  return slots_check(eng, type, n, slot, mem);
+}

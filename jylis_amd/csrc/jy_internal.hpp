@@ -79,7 +79,8 @@ struct TlogState {  // CSR, double-buffered entries
   int cur = 0;
   u64* cutoff = nullptr;  // [kcap]
   u64 kcap = 0;
-  u64 nent_bound = 0;  // host upper bound of live entries
+  u64 nent_bound = 0;       // host upper bound of live entries
+  bool nent_known = false;  // pin_total[0] holds the live total after a merge
 };
 
 struct UjsonState {  // CSR elements + CSR cloud (double-buffered), dense vv
@@ -95,6 +96,7 @@ struct UjsonState {  // CSR elements + CSR cloud (double-buffered), dense vv
   u32 R = 0;
   u64 kcap = 0;
   u64 nel_bound = 0, ncloud_bound = 0;
+  bool known = false;  // pin_total[1..2] hold the live totals after a merge
 };
 
 struct Arena {
@@ -124,7 +126,8 @@ struct jy_engine {
   UjsonState ujson;
 
   // scratch (device) reused across calls, stream-ordered
-  DevArray scratch[8];
+  // 0-7 staged inputs, 8-14 merge temporaries, 15 scan temp storage
+  DevArray scratch[16];
   // column list of the last block merge, kept resident (a peer set rarely changes)
   std::vector<u16> cols_cache;
   u16* cols_dev = nullptr;
@@ -162,6 +165,10 @@ int32_t jy_scratch(jy_engine* eng, int idx, u64 bytes, void** out);
 // copy a borrowed input into device memory if it is on the host; returns a
 // device pointer valid in stream order (scratch slot `idx`)
 int32_t jy_stage(jy_engine* eng, int idx, const void* src, u64 bytes, int32_t mem, const void** dev_out);
+// bracket the jy_stage calls of one API call (pinned staging reuse)
+int32_t jy_stage_begin(jy_engine* eng);
+int32_t jy_stage_end(jy_engine* eng);
+int32_t jy_slots_check(jy_engine* eng, int32_t type, u64 n, const u32* slot, int32_t mem);
 int32_t jy_ensure_slots(jy_engine* eng, int32_t type, u64 nkeys);
 int32_t jy_realloc(jy_engine* eng, void** p, u64 old_bytes, u64 new_bytes, bool zero_tail);
 
@@ -177,10 +184,17 @@ int32_t jy_treg_merge(jy_engine* eng, u64 n, const u32* slot, const u64* ts, con
 int32_t jy_treg_gather(jy_engine* eng, u64 n, const u32* slots, u64* ts, u64* pre, u64* lr);
 
 int32_t jy_tlog_grow(jy_engine* eng, u64 need_slots);
+int32_t jy_tlog_extend(jy_engine* eng, u64 from, u64 to);
+int32_t jy_tlog_sizes(jy_engine* eng, u64 n, const u32* slots, u64* len, u64* cut);
+int32_t jy_tlog_gather(jy_engine* eng, u64 n, const u32* slots, const u64* ooff, u64* ts, u64* pre, u64* lr);
 int32_t jy_tlog_merge(jy_engine* eng, u64 nkeys, const u32* slot, const u64* cutoff, const u64* offs, u64 nent,
                       const u64* ts, const u64* pre, const u64* lr);
 
 int32_t jy_ujson_grow(jy_engine* eng, u64 need_slots);
+int32_t jy_ujson_extend(jy_engine* eng, u64 from, u64 to);
+int32_t jy_ujson_sizes(jy_engine* eng, u64 n, const u32* slots, u64* ne, u64* nc);
+int32_t jy_ujson_gather(jy_engine* eng, u64 n, const u32* slots, const u64* oeoff, const u64* ocoff, u64* odots,
+                        u64* oelems, u64* ovv, u64* ocloud);
 int32_t jy_ujson_merge(jy_engine* eng, u64 ndocs, const u32* slot, const u64* eoffs, u64 nel, const u64* dots,
                        const u64* elems, const u64* vvoffs, u64 nvv, const u64* vv, const u64* coffs, u64 ncloud,
                        const u64* cloud);

@@ -194,4 +194,131 @@ class RepoTREG(_GpuRepo):
         return t
 
 
-REPOS = {GCOUNT: RepoGCOUNT, PNCOUNT: RepoPNCOUNT, TREG: RepoTREG}
+class RepoTLOG(_GpuRepo):
+    """repo_tlog.pony: TLog[String] per key (sorted log with grow-only cutoff)."""
+    ctype = TLOG
+
+    def converge_deltas(self, batch, ctype=TLOG):
+        if ctype != self.ctype:
+            return
+        slots = self._intern(batch)
+        if len(slots) == 0:
+            return
+        pre, lr = self.eng.pack_values(TLOG, (batch["val_bytes"], batch["val_offs"]))
+        self.eng.tlog_converge(slots, np.asarray(batch["cutoff"], np.uint64), np.asarray(batch["ent_offs"], np.uint64),
+                               np.asarray(batch["ts"], np.uint64), pre, lr)
+
+    def get(self, key, count=None):
+        """TLOG GET key [count] (repo_tlog.pony:69-83): [(value, ts)], newest first"""
+        s = int(self.slots_of([key])[0])
+        if s == E._lib.JY_NO_SLOT:
+            return []
+        cut, offs, ts, pre, lr = self.eng.tlog_read(np.array([s], np.uint32))
+        n = len(ts) if count is None else min(count, len(ts))
+        return [(self.eng.value_bytes(TLOG, pre[j], lr[j]), int(ts[j])) for j in range(n)]
+
+    def size(self, key):
+        s = int(self.slots_of([key])[0])
+        return 0 if s == E._lib.JY_NO_SLOT else len(self.eng.tlog_read(np.array([s], np.uint32))[2])
+
+    def cutoff(self, key):
+        s = int(self.slots_of([key])[0])
+        return 0 if s == E._lib.JY_NO_SLOT else int(self.eng.tlog_read(np.array([s], np.uint32))[0][0])
+
+    def state(self):
+        slots = self._sorted_slots()
+        t = self._keys_table(slots)
+        if len(slots) == 0:
+            t.update({"cutoff": np.zeros(0, np.uint64), "ent_offs": np.zeros(1, np.uint64),
+                      "ts": np.zeros(0, np.uint64), "val_bytes": np.zeros(0, np.uint8),
+                      "val_offs": np.zeros(1, np.uint64)})
+            return t
+        cut, offs, ts, pre, lr = self.eng.tlog_read(slots)
+        vals = [self.eng.value_bytes(TLOG, p, l) for p, l in zip(pre, lr)]
+        vb, vo = E.encode_keys(vals)
+        t.update({"cutoff": cut, "ent_offs": offs, "ts": ts, "val_bytes": vb, "val_offs": vo})
+        return t
+
+
+def _seg_ids(offs):
+    offs = np.asarray(offs, np.int64)
+    return np.repeat(np.arange(len(offs) - 1), np.diff(offs))
+
+
+class RepoUJSON(_GpuRepo):
+    """repo_ujson.pony: UJSON per key (dot kernel over interned (path, value) leaves)."""
+    ctype = UJSON
+
+    def _pack(self, ids, seqs):
+        ids = np.asarray(ids, np.uint64)
+        cols = self.eng.replica_cols(ids.tolist()).astype(np.uint64) if len(ids) else np.zeros(0, np.uint64)
+        if len(seqs) and (np.asarray(seqs, np.uint64) >> np.uint64(E.DOT_SEQ_BITS)).any():
+            raise ValueError("dot sequence numbers must stay below 2^48")
+        return E.pack_dot(cols, seqs)
+
+    @staticmethod
+    def _sort_segments(offs, packed, *payload):
+        seg = _seg_ids(offs)
+        order = np.lexsort((packed, seg))
+        return (packed[order],) + tuple(np.asarray(p)[order] for p in payload)
+
+    def converge_deltas(self, batch, ctype=UJSON):
+        if ctype != self.ctype:
+            return
+        slots = self._intern(batch)
+        if len(slots) == 0:
+            return
+        eo, vo, co = (np.asarray(batch[k], np.uint64) for k in ("el_offs", "vv_offs", "cloud_offs"))
+        dots, elems = self._sort_segments(eo, self._pack(batch["dot_ids"], batch["dot_seqs"]),
+                                          np.asarray(batch["elems"], np.uint64))
+        (vv,) = self._sort_segments(vo, self._pack(batch["vv_ids"], batch["vv_seqs"]))
+        (cloud,) = self._sort_segments(co, self._pack(batch["cloud_ids"], batch["cloud_seqs"]))
+        self.eng.ujson_converge(slots, eo, dots, elems, vo, vv, co, cloud)
+
+    def elements(self, key):
+        """the observable element set of a doc (what GET renders, repo_ujson.pony:68-72)"""
+        s = int(self.slots_of([key])[0])
+        if s == E._lib.JY_NO_SLOT:
+            return set()
+        return set(int(x) for x in self.eng.ujson_read(np.array([s], np.uint32))[2])
+
+    def state(self):
+        slots = self._sorted_slots()
+        t = self._keys_table(slots)
+        n = len(slots)
+        out = {k: [] for k in ("dot_ids", "dot_seqs", "elems", "vv_ids", "vv_seqs", "cloud_ids", "cloud_seqs")}
+        eoffs, voffs, coffs = [0], [0], [0]
+        if n:
+            eo, dots, elems, vv, co, cloud = self.eng.ujson_read(slots)
+            R = vv.shape[1]
+            ids = np.array([self.eng.replica_id(c) for c in range(self.eng.replica_count())] or [0], np.uint64)
+            for i in range(n):
+                c, q = E.unpack_dot(dots[eo[i]:eo[i + 1]])
+                di = ids[c]
+                order = np.lexsort((q, di))
+                out["dot_ids"].append(di[order])
+                out["dot_seqs"].append(q[order])
+                out["elems"].append(elems[eo[i]:eo[i + 1]][order])
+                eoffs.append(eoffs[-1] + len(order))
+                nz = np.nonzero(vv[i])[0]
+                vi = ids[nz] if len(nz) else np.zeros(0, np.uint64)
+                order = np.argsort(vi, kind="stable")
+                out["vv_ids"].append(vi[order])
+                out["vv_seqs"].append(vv[i][nz][order])
+                voffs.append(voffs[-1] + len(nz))
+                c, q = E.unpack_dot(cloud[co[i]:co[i + 1]])
+                ci = ids[c]
+                order = np.lexsort((q, ci))
+                out["cloud_ids"].append(ci[order])
+                out["cloud_seqs"].append(q[order])
+                coffs.append(coffs[-1] + len(order))
+                assert R == self.eng.ujson_columns
+        for k, v in out.items():
+            t[k] = np.concatenate(v).astype(np.uint64) if v else np.zeros(0, np.uint64)
+        t["el_offs"] = np.array(eoffs, np.uint64)
+        t["vv_offs"] = np.array(voffs, np.uint64)
+        t["cloud_offs"] = np.array(coffs, np.uint64)
+        return t
+
+
+REPOS = {GCOUNT: RepoGCOUNT, PNCOUNT: RepoPNCOUNT, TREG: RepoTREG, TLOG: RepoTLOG, UJSON: RepoUJSON}

@@ -156,6 +156,191 @@ def counter_rows_torch(out, seed, rnd=None, prev=None, wrap_frac=True):
     return out
 
 
+def _excl_cumsum(x):
+    out = np.zeros(len(x) + 1, np.uint64)
+    out[1:] = np.cumsum(x, dtype=np.uint64)
+    return out
+
+
+def gather_bytes(vb, vo, idx):
+    """bytes of entries idx of (vb, vo) -> (bytes, offs)"""
+    idx = np.asarray(idx, np.int64)
+    lens = (vo[idx + 1] - vo[idx]).astype(np.int64)
+    offs = _excl_cumsum(lens)
+    total = int(offs[-1])
+    if total == 0:
+        return np.zeros(0, np.uint8), offs
+    pos = np.repeat(vo[idx].astype(np.int64) - offs[:-1].astype(np.int64), lens) + np.arange(total)
+    return vb[pos], offs
+
+
+def random_values(rng, n, lo=1, hi=16):
+    lens = rng.integers(lo, hi + 1, n)
+    offs = _excl_cumsum(lens)
+    return rng.integers(0, 256, int(offs[-1]), dtype=np.uint8), offs
+
+
+def _concat_values(parts):
+    """[(bytes, offs)] -> (bytes, offs)"""
+    vbs = [p[0] for p in parts]
+    lens = np.concatenate([np.diff(p[1].astype(np.int64)) for p in parts])
+    return (np.concatenate(vbs) if vbs else np.zeros(0, np.uint8)), _excl_cumsum(lens)
+
+
+def tlog_tables(K, seed, rounds=1, mean_state=8, cap=64, mean_delta=2, key_prefix=b"l"):
+    """Config-4 stream: K logs with state lengths ~ Geom(mean 8,
+    cap 64), then `rounds` delta batches with lengths ~ Geom(mean 2): newer
+    entries, ~10% duplicates of a state entry, ~5% same-timestamp different-value
+    ties, 5% of keys raising the cutoff to a state entry's timestamp.  Every
+    segment is canonical (strictly descending).  Returns (state, [deltas])."""
+    rng = np.random.default_rng(seed)
+    kb, ko = counter_keys(K, prefix=key_prefix)
+    Ls = np.minimum(rng.geometric(1.0 / mean_state, K), cap).astype(np.int64)
+    soff = _excl_cumsum(Ls)
+    N = int(soff[-1])
+    seg = np.repeat(np.arange(K), Ls)
+    newest = rng.integers(1 << 20, 1 << 40, K).astype(np.uint64)
+    gaps = rng.integers(1, 1000, N).astype(np.uint64)
+    cg = np.cumsum(gaps, dtype=np.uint64)
+    first = soff[:-1].astype(np.int64)
+    w = cg - gaps - (cg[first] - gaps[first])[seg]
+    sts = newest[seg] - w
+    svb, svo = random_values(rng, N)
+    state = {"key_bytes": kb, "key_offs": ko, "cutoff": np.zeros(K, np.uint64), "ent_offs": soff, "ts": sts,
+             "val_bytes": svb, "val_offs": svo}
+    deltas = []
+    top = newest.copy()
+    for _ in range(rounds):
+        Ld = np.minimum(rng.geometric(1.0 / mean_delta, K), cap).astype(np.int64)
+        step = rng.integers(1, 100, K).astype(np.uint64)
+        # new entries, newest first
+        nkey = np.repeat(np.arange(K), Ld)
+        rank = np.arange(int(Ld.sum())) - np.repeat(_excl_cumsum(Ld)[:-1].astype(np.int64), Ld)
+        nts = top[nkey] + (Ld[nkey] - rank).astype(np.uint64) * step[nkey]
+        nval = random_values(rng, len(nkey))
+        # a duplicate of one state entry (20% of keys) and a timestamp tie with
+        # another (10% of keys with >= 2 entries), appended oldest-last
+        i1 = (rng.random(K) * Ls).astype(np.int64)
+        i2 = (i1 + 1 + (rng.random(K) * np.maximum(Ls - 1, 1)).astype(np.int64)) % Ls
+        has_dup = rng.random(K) < 0.2
+        has_tie = (rng.random(K) < 0.1) & (Ls >= 2)
+        dkeys = np.nonzero(has_dup)[0]
+        tkeys = np.nonzero(has_tie)[0]
+        didx = soff[dkeys].astype(np.int64) + i1[dkeys]
+        tidx = soff[tkeys].astype(np.int64) + i2[tkeys]
+        dval = gather_bytes(svb, svo, didx)
+        tval = random_values(rng, len(tkeys))
+        keys = np.concatenate([nkey, dkeys, tkeys])
+        ts = np.concatenate([nts, sts[didx], sts[tidx]])
+        # order inside a segment: new entries first (they are newer), then the
+        # older pair by descending timestamp
+        grp = np.concatenate([np.zeros(len(nkey)), np.ones(len(dkeys) + len(tkeys))])
+        r2 = np.concatenate([rank, np.zeros(len(dkeys) + len(tkeys), np.int64)])
+        order = np.lexsort((r2, -ts.astype(np.float64) * grp, grp, keys))
+        vb, vo = _concat_values([nval, dval, tval])
+        ent_vb, ent_vo = gather_bytes(vb, vo, order)
+        offs = _excl_cumsum(np.bincount(keys, minlength=K))
+        cut = np.zeros(K, np.uint64)
+        ck = np.nonzero(rng.random(K) < 0.05)[0]
+        cut[ck] = sts[soff[ck].astype(np.int64) + (rng.random(len(ck)) * Ls[ck]).astype(np.int64)]
+        deltas.append({"key_bytes": kb, "key_offs": ko, "cutoff": cut, "ent_offs": offs, "ts": ts[order],
+                       "val_bytes": ent_vb, "val_offs": ent_vo})
+        top = top + (Ld + 1).astype(np.uint64) * step + np.uint64(1)
+    return state, deltas
+
+
+def ujson_tables(D, seed, rounds=1, R=16, leaves=8, zipf=1.1, ops_per_round=None, key_prefix=b"u"):
+    """Config-5 stream: D docs with ~`leaves` elements over R
+    replicas, then `rounds` delta batches whose ops (70% INS, 20% RM, 10% CLR)
+    hit docs with Zipf(zipf) popularity; ops on one doc fold into one delta.
+    Tables use replica ids (oracle layout).  Returns (state, [deltas])."""
+    rng = np.random.default_rng(seed)
+    ids = replica_ids(R, seed)
+    kb, ko = counter_keys(D, prefix=key_prefix)
+    docs = []
+    for d in range(D):
+        vv = rng.integers(0, 24, R)
+        live = np.nonzero(vv)[0]
+        els = {}
+        for _ in range(min(int(rng.poisson(leaves)), 40)):
+            if len(live) == 0:
+                break
+            c = int(rng.choice(live))
+            q = int(rng.integers(1, vv[c] + 1))
+            els[(c, q)] = int(rng.integers(1, 64))
+        cloud = set()
+        if rng.random() < 0.25:
+            for _ in range(int(rng.integers(1, 4))):
+                c = int(rng.integers(R))
+                q = int(vv[c]) + 2 + int(rng.integers(0, 5))
+                cloud.add((c, q))
+                if rng.random() < 0.5:
+                    els[(c, q)] = int(rng.integers(1, 64))
+        docs.append((vv, els, cloud))
+
+    def table(entries):
+        t = {"key_bytes": kb, "key_offs": ko}
+        cols = {k: [] for k in ("dot_ids", "dot_seqs", "elems", "vv_ids", "vv_seqs", "cloud_ids", "cloud_seqs")}
+        eo, vo, co = [0], [0], [0]
+        sel = []
+        for d, (vv, els, cloud) in entries:
+            sel.append(d)
+            for (c, q), e in sorted(els.items()):
+                cols["dot_ids"].append(ids[c])
+                cols["dot_seqs"].append(q)
+                cols["elems"].append(e)
+            eo.append(eo[-1] + len(els))
+            nz = [(c, int(vv[c])) for c in range(R) if vv[c]]
+            for c, q in nz:
+                cols["vv_ids"].append(ids[c])
+                cols["vv_seqs"].append(q)
+            vo.append(vo[-1] + len(nz))
+            for c, q in sorted(cloud):
+                cols["cloud_ids"].append(ids[c])
+                cols["cloud_seqs"].append(q)
+            co.append(co[-1] + len(cloud))
+        sel = np.array(sel, np.int64)
+        t["key_bytes"], t["key_offs"] = gather_bytes(kb, ko, sel) if len(sel) else (np.zeros(0, np.uint8),
+                                                                                   np.zeros(1, np.uint64))
+        for k, v in cols.items():
+            t[k] = np.array(v, np.uint64)
+        t["el_offs"], t["vv_offs"], t["cloud_offs"] = (np.array(x, np.uint64) for x in (eo, vo, co))
+        return t
+
+    state = table(list(enumerate(docs)))
+    perm = rng.permutation(D)
+    deltas = []
+    nops = ops_per_round or max(1, D // 2)
+    for _ in range(rounds):
+        hit = perm[(rng.zipf(zipf, nops) - 1) % D]
+        kinds = rng.random(nops)
+        folded = {}
+        for d, x in zip(hit.tolist(), kinds.tolist()):
+            vv, els, cloud = docs[d]
+            dvv, dels, dcl = folded.setdefault(d, (np.zeros(R, np.int64), {}, set()))
+            r = int(rng.integers(R))
+            if x < 0.7:  # INS: a fresh dot of replica r (sometimes past a gap)
+                top = max([int(vv[r])] + [q for (c, q) in cloud | dcl | set(dels) if c == r])
+                q = top + 1 + (int(rng.integers(1, 3)) if rng.random() < 0.2 else 0)
+                dels[(r, q)] = int(rng.integers(1, 64))
+                dcl.add((r, q))
+            elif x < 0.9:  # RM one element value: every dot holding it
+                if els:
+                    e = list(els.values())[int(rng.integers(len(els)))]
+                    dcl.update(k for k, v in els.items() if v == e)
+            else:  # CLR
+                dcl.update(els.keys())
+            if rng.random() < 0.1:  # carry a version-vector entry too
+                c = int(rng.integers(R))
+                dvv[c] = max(dvv[c], int(vv[c]))
+            if rng.random() < 0.05 and els:  # re-send an element the state holds
+                k = list(els)[int(rng.integers(len(els)))]
+                dels[k] = els[k]
+                dcl.add(k)
+        deltas.append(table(sorted(folded.items())))
+    return state, deltas
+
+
 def counter_batch_tables(state_or_delta, replica_id_list, key_tab, prefix=""):
     """[R][K] (GCOUNT) or [2][R][K] (PNCOUNT) array -> per-replica oracle batch tables
     (one flushed peer batch per replica column, every key carrying that column)"""

@@ -1,0 +1,137 @@
+"""TLOG: the HIP segmented merge against the CPU oracle (bit-exact).
+
+Edge cases: (ts, value) duplicates across state and delta, timestamp ties
+broken by Pony String order (long values sharing 8-byte prefixes), cutoffs
+that drop state entries / delta entries / everything, CLR at ts 2^64-1
+(cutoff wraps to 0: no-op), TRIM past the end, keys with a cutoff but no
+entries, repeated keys in one batch, malformed (unsorted) delta segments."""
+import numpy as np
+import pytest
+
+from helpers import assert_state_equal, random_history
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4, 5])
+def test_history_parity(oracle_mod, engine, seed):
+    from jylis_amd.repo import RepoTLOG
+    O = oracle_mod
+    want = O.Repo(O.TLOG)
+    got = RepoTLOG(engine)
+    for b in random_history(O, O.TLOG, seed, nops=400, val_len=20):
+        want.converge(b)
+        got.converge_deltas(b)
+    assert_state_equal(O.TLOG, want.state(), got.state())
+
+
+def _log_batch(logs):
+    """logs: list of (key, cutoff, [(value, ts), ...]) -> batch table (entries as given)"""
+    from jylis_amd.engine import encode_keys
+    kb, ko = encode_keys([k for k, _, _ in logs])
+    vals, ts, offs = [], [], [0]
+    for _, _, ents in logs:
+        for v, t in ents:
+            vals.append(v)
+            ts.append(t)
+        offs.append(len(vals))
+    vb, vo = encode_keys(vals)
+    return {"key_bytes": kb, "key_offs": ko, "cutoff": np.array([c for _, c, _ in logs], np.uint64),
+            "ent_offs": np.array(offs, np.uint64), "ts": np.array(ts, np.uint64), "val_bytes": vb, "val_offs": vo}
+
+
+def _canon(ents):
+    """sort + dedupe as a pony TLog would hold them (later ts, then greater value first)"""
+    return sorted(set(ents), key=lambda e: (e[1], e[0]), reverse=True)
+
+
+def test_edge_cases(oracle_mod, engine):
+    from jylis_amd.repo import RepoTLOG
+    O = oracle_mod
+    big = (1 << 64) - 1
+    P = b"prefix!!"  # 8-byte shared prefix
+    state = [
+        ("dup", 0, _canon([(b"a", 5), (b"b", 5), (b"c", 4)])),
+        ("tie", 0, _canon([(P + b"zz", 9), (P + b"a", 9), (P, 9), (b"x", 1)])),
+        ("cut", 0, _canon([(b"v%d" % i, i) for i in range(10)])),
+        ("cutall", 0, _canon([(b"q", 3), (b"r", 2)])),
+        ("wrap", 0, _canon([(b"max", big), (b"low", 1)])),
+        ("onlycut", 7, []),
+        ("empty", 0, []),
+    ]
+    delta = [
+        ("dup", 0, _canon([(b"b", 5), (b"c", 4), (b"d", 4)])),
+        ("tie", 0, _canon([(P + b"zy", 9), (P + b"\x00", 9), (P + b"zz", 9)])),
+        ("cut", 6, _canon([(b"v9", 9), (b"new", 7), (b"old", 2)])),
+        ("cutall", 100, []),
+        ("wrap", 0, []),
+        ("onlycut", 3, _canon([(b"late", 8), (b"early", 2)])),
+        ("fresh", 0, _canon([(b"", 0), (b"\xff" * 12, 0)])),
+    ]
+    want = O.Repo(O.TLOG)
+    got = RepoTLOG(engine)
+    for logs in (state, delta, state):
+        b = _log_batch(logs)
+        want.converge(b)
+        got.converge_deltas(b)
+    assert_state_equal(O.TLOG, want.state(), got.state())
+    assert got.cutoff("cutall") == 100 and got.size("cutall") == 0
+    assert got.get("tie", 2) == [(P + b"zz", 9), (P + b"zy", 9)]
+    assert got.get("missing") == [] and got.size("missing") == 0 and got.cutoff("missing") == 0
+
+
+def test_clr_at_max_timestamp_and_trim_past_end(oracle_mod, engine):
+    """CLR with newest ts 2^64-1 sets cutoff ts+1 = 0 (U64 wrap): no effect;
+    TRIM n > size raises nothing (repo_tlog.pony:103-111; parity unpinned)"""
+    from jylis_amd.repo import RepoTLOG
+    O = oracle_mod
+    w = O.Repo(O.TLOG, 1)
+    w.tlog_ins("k", b"top", (1 << 64) - 1)
+    w.tlog_ins("k", b"x", 10)
+    w.tlog_clr("k")
+    w.tlog_trim("k", 50)
+    w.tlog_ins("j", b"y", 3)
+    w.tlog_trim("j", 1)
+    got = RepoTLOG(engine)
+    want = O.Repo(O.TLOG)
+    for b in (w.flush().table(), w.state()):
+        want.converge(b)
+        got.converge_deltas(b)
+    assert_state_equal(O.TLOG, want.state(), got.state())
+    assert got.size("k") == 2
+
+
+def test_repeated_keys_in_one_batch(oracle_mod, engine):
+    from jylis_amd.repo import RepoTLOG
+    O = oracle_mod
+    logs = [("k", 0, _canon([(b"a", 1)])), ("k", 2, _canon([(b"b", 3)])), ("j", 0, []), ("k", 0, _canon([(b"c", 2)]))]
+    want = O.Repo(O.TLOG)
+    got = RepoTLOG(engine)
+    b = _log_batch(logs)
+    want.converge(b)
+    got.converge_deltas(b)
+    assert_state_equal(O.TLOG, want.state(), got.state())
+
+
+def test_malformed_segment_is_skipped(engine):
+    """an unsorted delta log is not a TLog: the key is left untouched and the
+    entry counted as skipped (the reference swallows converge errors)"""
+    from jylis_amd.repo import RepoTLOG
+    got = RepoTLOG(engine)
+    got.converge_deltas(_log_batch([("k", 0, [(b"a", 1), (b"b", 5)]), ("ok", 0, [(b"z", 1)])]))
+    assert engine.skipped() == 1
+    assert got.get("k") == [] and got.get("ok") == [(b"z", 1)]
+
+
+def test_large_synthetic(oracle_mod, engine):
+    """config-4 shaped stream at 20k keys (geometric lengths, dups, ties, cutoffs)"""
+    from jylis_amd import synth as S
+    from jylis_amd.repo import RepoTLOG
+    O = oracle_mod
+    st, dl = S.tlog_tables(20000, seed=S.BASE_SEED + 4, rounds=2)
+    want = O.Repo(O.TLOG)
+    got = RepoTLOG(engine)
+    for b in [st] + dl:
+        want.converge(b)
+        got.converge_deltas(b)
+    assert_state_equal(O.TLOG, want.state(), got.state())

@@ -1,0 +1,115 @@
+"""UJSON: the HIP dot-kernel join against the CPU oracle (bit-exact on the
+canonical state: element dots, version vector, compacted cloud).
+
+Edge cases: concurrent INS/RM of one value (add wins, ujson.md:61,103),
+CLR racing INS, re-delivered deltas (idempotence), clouds that compact into
+the version vector, equal dots in state and delta, repeated docs in one
+batch, malformed deltas (unsorted dots, column beyond the vv width)."""
+import numpy as np
+import pytest
+
+from helpers import assert_state_equal, random_history
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4, 5])
+def test_history_parity(oracle_mod, engine, seed):
+    from jylis_amd.repo import RepoUJSON
+    O = oracle_mod
+    want = O.Repo(O.UJSON, 5)
+    got = RepoUJSON(engine)
+    for b in random_history(O, O.UJSON, seed, nops=400):
+        want.converge(b)
+        got.converge_deltas(b)
+    assert_state_equal(O.UJSON, want.state(), got.state())
+
+
+def test_add_wins_and_redelivery(oracle_mod, engine):
+    """replica a removes value 7 while replica b concurrently re-inserts it:
+    after exchange both see 7 (add wins); re-delivering every delta is a no-op"""
+    from jylis_amd.repo import RepoUJSON
+    O = oracle_mod
+    a, b = O.Repo(O.UJSON, 11), O.Repo(O.UJSON, 22)
+    a.ujson_ins("doc", 7)
+    a.ujson_ins("doc", 8)
+    d0 = a.flush().table()
+    b.converge(d0)
+    a.ujson_rm("doc", 7)
+    b.ujson_ins("doc", 7)
+    b.ujson_clr("other")  # no key creation on CLR of a missing doc
+    da, db = a.flush().table(), b.flush().table()
+    want = O.Repo(O.UJSON, 33)
+    got = RepoUJSON(engine)
+    for t in (d0, da, db, da, d0, db):
+        want.converge(t)
+        got.converge_deltas(t)
+    assert_state_equal(O.UJSON, want.state(), got.state())
+    assert got.elements("doc") == {7, 8}
+
+
+def test_repeated_docs_in_one_batch(oracle_mod, engine):
+    from jylis_amd.repo import RepoUJSON
+    O = oracle_mod
+    r = O.Repo(O.UJSON, 3)
+    parts = []
+    for e in (1, 2, 3):
+        r.ujson_ins("k", e)
+        parts.append(r.flush().table())
+    r.ujson_rm("k", 2)
+    parts.append(r.flush().table())
+    # concatenate the four 1-doc batches into one batch naming "k" four times
+    cat = {}
+    for k in parts[0]:
+        if k.endswith("offs"):
+            acc = [np.zeros(1, np.uint64)]
+            base = 0
+            for p in parts:
+                acc.append(p[k][1:] + np.uint64(base))
+                base = int(acc[-1][-1]) if len(acc[-1]) else base
+            cat[k] = np.concatenate(acc)
+        else:
+            cat[k] = np.concatenate([p[k] for p in parts])
+    want = O.Repo(O.UJSON, 9)
+    got = RepoUJSON(engine)
+    want.converge(cat)
+    got.converge_deltas(cat)
+    assert_state_equal(O.UJSON, want.state(), got.state())
+    assert got.elements("k") == {1, 3}
+
+
+def test_malformed_delta_is_skipped(engine):
+    from jylis_amd.engine import pack_dot
+    engine.intern(4, ["good", "bad"])
+    slots = np.array([0, 1], np.uint32)
+    eo = np.array([0, 1, 3], np.uint64)
+    dots = np.concatenate([pack_dot([0], [1]), pack_dot([0, 0], [5, 2])])  # second doc unsorted
+    elems = np.array([10, 11, 12], np.uint64)
+    vo = np.zeros(3, np.uint64)
+    co = np.array([0, 1, 2], np.uint64)
+    cloud = np.concatenate([pack_dot([0], [1]), pack_dot([0], [9])])
+    engine.ujson_converge(slots, eo, dots, elems, vo, np.zeros(0, np.uint64), co, cloud)
+    assert engine.skipped() == 1
+    eoffs, d, e, vv, coffs, cl = engine.ujson_read(slots)
+    assert list(e) == [10] and vv[0][0] == 1 and len(cl) == 0  # dot (0,1) compacted into vv
+    assert vv[1].sum() == 0
+
+
+@pytest.mark.parametrize("R", [16, 4])
+def test_synthetic_zipf(oracle_mod, R):
+    """config-5 shaped stream at 3000 docs: Zipf(1.1) popularity, INS/RM/CLR mix"""
+    from jylis_amd import synth as S
+    from jylis_amd.engine import Engine
+    from jylis_amd.repo import RepoUJSON
+    O = oracle_mod
+    eng = Engine(device=0, ujson_columns=R)
+    try:
+        st, dl = S.ujson_tables(3000, seed=S.BASE_SEED + 5, rounds=3, R=R)
+        want = O.Repo(O.UJSON, 1)
+        got = RepoUJSON(eng)
+        for b in [st] + dl:
+            want.converge(b)
+            got.converge_deltas(b)
+        assert_state_equal(O.UJSON, want.state(), got.state())
+    finally:
+        eng.close()
