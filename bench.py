@@ -40,7 +40,34 @@ def parse():
     ap.add_argument("--cpu-rounds", type=int, default=6, help="cpu_baseline sample: peer-batch rounds")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=None, help="per-launch HBM bytes from a PMC run (json)")
+    ap.add_argument("--type", default="pncount", choices=["pncount", "gcount", "treg", "tlog", "ujson"],
+                    help="pncount = the BASELINE metric line; the others measure SURVEY 8d configs 1,3,4,5")
+    ap.add_argument("--route", action="store_true", help="treg: run the routing exchange even on 1 GPU")
     return ap.parse_args()
+
+
+def other_mode(args, rank, world, local, dist):
+    """bench_modes.py: one JSON line for a non-default CRDT type"""
+    import torch
+
+    import bench_modes
+    from jylis_amd.engine import Engine
+    dev = torch.device("cuda", local)
+    eng = Engine(device=local, counter_columns=16)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    eng.set_stream(stream.cuda_stream)
+    if args.keys == 16 * 1024 * 1024:
+        args.keys = 0  # per-mode default size
+    res = bench_modes.MODES[args.type](args, eng, dev, dist, rank, world)
+    if rank == 0:
+        line = {"metric": f"{args.type.upper()} delta converge throughput (SURVEY 8d)", "value": res.pop("value"),
+                "unit": res.pop("unit_of_work") + "s/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": res.pop("ms_per_step"), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic (jylis_amd/synth.py)",
+                "config": {"workload": res.pop("workload")}, **res}
+        print(json.dumps(line), flush=True)
+    eng.close()
 
 
 def cpu_baseline(args, seed):
@@ -88,6 +115,11 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if args.type != "pncount":
+        other_mode(args, rank, world, local, dist)
+        if dist:
+            dist.destroy_process_group()
+        return
 
     from jylis_amd import synth as S
     from jylis_amd.engine import Engine

@@ -1,0 +1,335 @@
+"""Per-type bench modes behind `bench.py --type {gcount,treg,tlog,ujson}`.
+
+The default bench line is PNCOUNT (BASELINE.json configs[1]); these modes
+measure the other SURVEY.md 8d configs on the same engine and report their
+own roofline (algorithmic bytes per converge / converge time, HIP events on
+the engine stream).  Inputs are synthetic (jylis_amd/synth.py); the first
+converge of every mode is checked against an independent recomputation.
+"""
+import time
+
+import numpy as np
+
+HBM_PEAK_GBS = 8000.0
+
+
+def _timed(steps, warmup, step, dist, dev):
+    """warmup, then exactly `steps` steps bracketed by barrier + synchronize;
+    per-step HIP events on the current (engine) stream"""
+    import torch
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        evs[i][0].record()
+        step(warmup + i)
+        evs[i][1].record()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    return elapsed, [a.elapsed_time(b) / 1e3 for a, b in evs]
+
+
+def _max_over_ranks(x, dist, dev):
+    import torch
+    if not dist:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0])
+
+
+def _to_dev(a, dev, dtype=None):
+    import torch
+    a = np.ascontiguousarray(a)
+    if a.dtype == np.uint64:
+        a = a.view(np.int64)
+    elif a.dtype == np.uint32:
+        a = a.view(np.int32)
+    t = torch.from_numpy(a).to(dev)
+    return t if dtype is None else t.to(dtype)
+
+
+# ---- GCOUNT (config 1: 1M keys x 16 replicas) --------------------------------
+
+def bench_gcount(args, eng, dev, dist, rank, world):
+    import torch
+    from jylis_amd import synth as S
+    K, R = args.keys or (1 << 20), 16
+    seed = S.BASE_SEED + 1
+    kb, ko = S.counter_keys(K, prefix=f"s{rank}:g".encode(), width=7)
+    eng.intern(0, (kb, ko))
+    cols = eng.replica_cols(S.replica_ids(R, seed).tolist())
+    st = torch.empty((1, R, K), dtype=torch.int64, device=dev)
+    S.counter_rows_torch(st, seed, wrap_frac=False)
+    eng.gcount_converge_block(cols, 0, st[0])
+    nb = max(1, args.batches)
+    ds, prev = [], st
+    for j in range(nb):
+        d = torch.empty_like(st)
+        S.counter_rows_torch(d, seed, rnd=j, prev=prev)
+        ds.append(d)
+        prev = d
+    elapsed, kt = _timed(args.steps, args.warmup, lambda i: eng.gcount_converge_block(cols, 0, ds[i % nb][0]),
+                         dist, dev)
+    t = _max_over_ranks(elapsed, dist, dev)
+    cells = R * K
+    k = float(np.mean(kt))
+    return {"workload": f"GCOUNT converge: {K} keys x {R} replicas per GPU, one full delta batch "
+                        f"({R} peer batches) per step (SURVEY 8d config 1)",
+            "unit_of_work": "cell merge", "units_per_step_per_gpu": cells,
+            "value": world * cells * args.steps / t, "ms_per_step": t / args.steps * 1e3,
+            "roofline": {"bound": "hbm", "achieved": 24 * cells / k / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": 24 * cells / k / 1e9 / HBM_PEAK_GBS, "kernel": "k_block_max<true>",
+                         "kernel_ms_avg": k * 1e3, "bytes_per_unit": 24,
+                         "note": "state (128 MiB) + delta fit the 256 MiB Infinity Cache"}}
+
+
+# ---- TREG (config 3: 64M keys over 8 GPUs = 8M per GPU) -----------------------
+
+def _treg_values(rng, n):
+    """random 1-16 byte values, ~20% sharing one of 16 8-byte prefixes"""
+    from jylis_amd import synth as S
+    vb, vo = S.random_values(rng, n, 1, 16)
+    lens = np.diff(vo.astype(np.int64))
+    share = (rng.random(n) < 0.2) & (lens >= 8)
+    prefixes = rng.integers(0, 256, (16, 8), dtype=np.uint8)
+    pick = rng.integers(0, 16, n)
+    starts = vo[:-1].astype(np.int64)
+    for j in range(8):
+        idx = starts[share] + j
+        vb[idx] = prefixes[pick[share], j]
+    return vb, vo
+
+
+def bench_treg(args, eng, dev, dist, rank, world):
+    """Routed TREG converge: every rank ingests 1/world of the global key space
+    per step and routes records + long value bytes to their owners (RCCL
+    all-to-all), which LWW-merge them.  At world 1 the exchange is skipped
+    unless --route (then it runs the same kernels against itself)."""
+    import torch
+    from jylis_amd import synth as S
+    from jylis_amd._lib import TREG
+    from jylis_amd.route import ShardRouter, TregRouter
+    Kper = args.keys or (8 << 20)
+    G = Kper * world
+    rng = np.random.default_rng(S.BASE_SEED + 3 + 1000 * rank)
+    # ingest share of this rank: global keys k = rank, rank + world, ...
+    idx = np.arange(rank, G, world, dtype=np.uint64)
+    kb, ko = _key_strings(idx, b"t")
+    routed = world > 1 or args.route
+    t0 = time.perf_counter()
+    if routed:
+        import torch.distributed as tdist
+        cpu_group = tdist.new_group(backend="gloo") if world > 1 else None
+        router = ShardRouter(rank, world, lambda tab: eng.intern(TREG, tab), dist=tdist if world > 1 else None,
+                             group=cpu_group)
+        own, slot = router.resolve(kb, ko)
+        tr = TregRouter(eng, tdist if world > 1 else None)
+    else:
+        slot = eng.intern(TREG, (kb, ko))
+        own = np.zeros(len(slot), np.uint32)
+    setup_s = time.perf_counter() - t0
+    n = len(slot)
+    batches = []
+    for j in range(max(1, args.batches) + 1):  # batch 0 = initial state
+        vb, vo = _treg_values(rng, n)
+        pre, lr = eng.pack_values(TREG, (vb, vo))
+        ts = rng.integers(0, 1 << 20, n).astype(np.uint64)
+        batches.append(tuple(_to_dev(a, dev) for a in (own, slot, ts, pre, lr)))
+    win = []
+
+    def step_of(b):
+        o, s, ts, pre, lr = b
+        if routed:
+            tr.exchange_and_converge(o, s, ts, pre, lr)
+        else:
+            eng.treg_converge(s, ts, pre, lr)
+
+    step_of(batches[0])
+    # winners per step from timestamps (ties need the value compare: rare)
+    cur = batches[0][2].clone() if not routed else None
+    nb = max(1, args.batches)
+    elapsed, kt = _timed(args.steps, args.warmup, lambda i: step_of(batches[1 + i % nb]), dist, dev)
+    if cur is not None:
+        for i in range(args.warmup + args.steps):
+            t = batches[1 + i % nb][2]
+            w = (t > cur)
+            if i >= args.warmup:
+                win.append(float(w.float().mean()))
+            cur = torch.where(w, t, cur)
+    t = _max_over_ranks(elapsed, dist, dev)
+    k = float(np.mean(kt))
+    wf = float(np.mean(win)) if win else 0.5
+    bytes_per_key = 4 + 24 + 8 + 24 * wf
+    out = {"workload": f"TREG LWW converge: {G} keys over {world} GPU(s) ({Kper} per GPU), one delta per key "
+                       f"per step{' routed by owner (all-to-all)' if routed else ''} (SURVEY 8d config 3)",
+           "unit_of_work": "key LWW select", "units_per_step_per_gpu": n,
+           "value": world * n * args.steps / t, "ms_per_step": t / args.steps * 1e3, "setup_s": setup_s,
+           "winner_fraction": wf}
+    if not routed:
+        out["roofline"] = {"bound": "hbm", "achieved": bytes_per_key * n / k / 1e9, "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": bytes_per_key * n / k / 1e9 / HBM_PEAK_GBS,
+                           "kernel": "k_treg_lww", "kernel_ms_avg": k * 1e3, "bytes_per_unit": bytes_per_key,
+                           "bytes_note": "4 slot + 24 delta + 8 state ts + 24 x winner fraction"}
+    else:
+        out["step_ms_avg_events"] = k * 1e3
+    return out
+
+
+def _key_strings(idx, prefix):
+    """global key indices -> fixed-width keys (bytes, offs)"""
+    n = len(idx)
+    width = 10
+    digits = np.empty((n, width), np.uint8)
+    v = np.asarray(idx, np.uint64).copy()
+    for j in range(width - 1, -1, -1):
+        digits[:, j] = (v % np.uint64(10)).astype(np.uint8) + ord("0")
+        v //= np.uint64(10)
+    pre = np.frombuffer(prefix, np.uint8)
+    rows = np.concatenate([np.broadcast_to(pre, (n, len(pre))), digits], axis=1)
+    return np.ascontiguousarray(rows).reshape(-1), np.arange(n + 1, dtype=np.uint64) * np.uint64(rows.shape[1])
+
+
+# ---- TLOG (config 4: 4M keys) --------------------------------------------------
+
+def bench_tlog(args, eng, dev, dist, rank, world):
+    import torch
+    from jylis_amd import synth as S
+    from jylis_amd._lib import TLOG
+    K = args.keys or (4 << 20)
+    nb = max(1, args.batches)
+    st, dl = S.tlog_tables(K, seed=S.BASE_SEED + 4 + 1000 * rank, rounds=nb)
+    slots = eng.intern(TLOG, (st["key_bytes"], st["key_offs"]))
+    assert (slots == np.arange(K)).all()
+    dev_batches = []
+    for b in [st] + dl:
+        pre, lr = eng.pack_values(TLOG, (b["val_bytes"], b["val_offs"]))
+        dev_batches.append(tuple(_to_dev(a, dev) for a in (slots, b["cutoff"], b["ent_offs"], b["ts"], pre, lr)))
+    eng.tlog_converge(*dev_batches[0])
+    eng.sync()
+    n_state0 = len(st["ts"])
+
+    def step(i):
+        eng.tlog_converge(*dev_batches[1 + i % nb])
+
+    elapsed, kt = _timed(args.steps, args.warmup, step, dist, dev)
+    t = _max_over_ranks(elapsed, dist, dev)
+    # replay the same sequence on a fresh engine pass to get exact in/out
+    # entry counts per step: state entries are the running total (the engine
+    # keeps it), so re-run step by step outside the timed region
+    from jylis_amd.engine import Engine
+    e2 = Engine(device=eng.device, key_capacity=[1024, 1024, 1024, K, 1024])
+    e2.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    e2.intern(TLOG, (st["key_bytes"], st["key_offs"]))
+    b2 = []
+    for b in [st] + dl:
+        pre, lr = e2.pack_values(TLOG, (b["val_bytes"], b["val_offs"]))
+        b2.append(tuple(_to_dev(a, dev) for a in (slots, b["cutoff"], b["ent_offs"], b["ts"], pre, lr)))
+    e2.tlog_converge(*b2[0])
+    byts, ins = [], []
+    prev = _tlog_total(e2)
+    for i in range(args.warmup + args.steps):
+        bt = b2[1 + i % nb]
+        e2.tlog_converge(*bt)
+        now = _tlog_total(e2)
+        nd = int(bt[3].numel())
+        if i >= args.warmup:
+            byts.append(24 * (prev + nd) + 24 * now + 24 * K)
+            ins.append(prev + nd)
+        prev = now
+    e2.close()
+    k = float(np.mean(kt))
+    avg_b = float(np.mean(byts))
+    units = float(np.mean(ins))
+    return {"workload": f"TLOG converge: {K} logs, state ~Geom(8, cap 64) entries, delta ~Geom(2) per key "
+                        f"per step, dups/ties/cutoffs (SURVEY 8d config 4); {n_state0} initial entries",
+            "unit_of_work": "log entry (input)", "value": world * units * args.steps / t,
+            "ms_per_step": t / args.steps * 1e3,
+            "roofline": {"bound": "hbm", "achieved": avg_b / k / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": avg_b / k / 1e9 / HBM_PEAK_GBS,
+                         "kernel": "k_tlog_count + scan + k_tlog_write (whole converge)",
+                         "converge_ms_avg": k * 1e3, "bytes_per_converge": avg_b,
+                         "bytes_note": "24 B per input entry (state + delta) + 24 B per output entry + 24 B per key"}}
+
+
+def _tlog_total(eng):
+    """live TLOG entries (sum of all slot lengths)"""
+    n = eng.nkeys(3)
+    if n == 0:
+        return 0
+    lens = np.empty(n, np.uint64)
+    cut = np.empty(n, np.uint64)
+    s = np.arange(n, dtype=np.uint32)
+    eng._check(eng.lib.jy_tlog_read_sizes(eng.h, n, s.ctypes.data, lens.ctypes.data, cut.ctypes.data))
+    return int(lens.sum())
+
+
+# ---- UJSON (config 5: 1M docs, Zipf) --------------------------------------------
+
+def bench_ujson(args, eng, dev, dist, rank, world):
+    import torch
+    from jylis_amd import synth as S
+    from jylis_amd._lib import UJSON
+    from jylis_amd.repo import RepoUJSON
+    D = args.keys or (1 << 20)
+    nb = max(1, args.batches)
+    t0 = time.perf_counter()
+    st, dl = S.ujson_tables(D, seed=S.BASE_SEED + 5 + 1000 * rank, rounds=nb, R=16)
+    gen_s = time.perf_counter() - t0
+    repo = RepoUJSON(eng)
+    repo.converge_deltas(st)
+    dev_batches = []
+    for b in dl:
+        slots = eng.lookup(UJSON, (b["key_bytes"], b["key_offs"]))
+        eo, vo, co = (np.asarray(b[k], np.uint64) for k in ("el_offs", "vv_offs", "cloud_offs"))
+        dots, elems = repo._sort_segments(eo, repo._pack(b["dot_ids"], b["dot_seqs"]), np.asarray(b["elems"]))
+        (vv,) = repo._sort_segments(vo, repo._pack(b["vv_ids"], b["vv_seqs"]))
+        (cloud,) = repo._sort_segments(co, repo._pack(b["cloud_ids"], b["cloud_seqs"]))
+        dev_batches.append((tuple(_to_dev(a, dev) for a in (slots, eo, dots, elems, vo, vv, co, cloud)),
+                            len(slots), len(dots), len(cloud)))
+    eng.sync()
+    n_el0 = len(st["elems"])
+    n_cl0 = len(st["cloud_ids"])
+
+    def step(i):
+        eng.ujson_converge(*dev_batches[i % nb][0])
+
+    elapsed, kt = _timed(args.steps, args.warmup, step, dist, dev)
+    t = _max_over_ranks(elapsed, dist, dev)
+    k = float(np.mean(kt))
+    # live sizes: average of the initial and final state (they drift slowly)
+    s = np.arange(eng.nkeys(UJSON), dtype=np.uint32)
+    ne, nc = np.empty(len(s), np.uint64), np.empty(len(s), np.uint64)
+    eng._check(eng.lib.jy_ujson_read_sizes(eng.h, len(s), s.ctypes.data, ne.ctypes.data, nc.ctypes.data))
+    n_el0 = (n_el0 + int(ne.sum())) / 2
+    n_cl0 = (n_cl0 + int(nc.sum())) / 2
+    # bytes: every doc's elements and cloud are read and rewritten (CSR rebuild),
+    # the vv row is read for every doc; delta dots / cloud read once
+    nd_docs = float(np.mean([b[1] for b in dev_batches]))
+    nd_el = float(np.mean([b[2] for b in dev_batches]))
+    nd_cl = float(np.mean([b[3] for b in dev_batches]))
+    R = 16
+    bytes_conv = 16 * n_el0 * 2 + 8 * n_cl0 * 2 + 16 * nd_el + 8 * nd_cl + 16 * D + 8 * R * nd_docs * 2
+    dots_examined = 2 * n_el0 + nd_el
+    return {"workload": f"UJSON converge: {D} docs (~8 leaves, R=16), Zipf(1.1) delta docs per step "
+                        f"({int(nd_docs)} docs, {int(nd_el)} dots, {int(nd_cl)} cloud dots), "
+                        f"70/20/10 INS/RM/CLR (SURVEY 8d config 5)",
+            "unit_of_work": "dot examined", "value": world * dots_examined * args.steps / t,
+            "ms_per_step": t / args.steps * 1e3, "generate_s": gen_s,
+            "roofline": {"bound": "hbm", "achieved": bytes_conv / k / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": bytes_conv / k / 1e9 / HBM_PEAK_GBS,
+                         "kernel": "k_uj_count + 2 scans + k_uj_write (whole converge)",
+                         "converge_ms_avg": k * 1e3, "bytes_per_converge": bytes_conv,
+                         "bytes_note": "16 B per element read+written, 8 B per cloud dot read+written, "
+                                       "8R B vv per delta doc read+write, 16 B per doc offsets"}}
+
+
+MODES = {"gcount": bench_gcount, "treg": bench_treg, "tlog": bench_tlog, "ujson": bench_ujson}

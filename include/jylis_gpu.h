@@ -157,6 +157,28 @@ int32_t jy_ujson_read(jy_engine* eng, uint64_t n, const uint32_t* slots, const u
                       uint64_t* dots_out, uint64_t* elems_out, uint64_t* vv_out,
                       const uint64_t* cloud_offs, uint64_t* cloud_out);
 
+/* ---- multi-GPU routing: the exchange step of a key-hash-sharded node ----
+ * Replaces nothing in the reference (every node holds every key there); it is
+ * the intra-node analogue of Cluster.broadcast_deltas (cluster.pony:209-213).
+ * A TREG batch ingested on one GPU is partitioned by owner shard into u64[4]
+ * records {slot on owner, ts, pre, lr'} plus the bytes of values > 8 bytes
+ * (lr' offsets are relative to the destination's byte run).  The host moves
+ * both with an all-to-all(v) (RCCL) and each owner converges its runs. */
+void jy_keys_owner(uint64_t n, const uint8_t* key_bytes, const uint64_t* key_offs, uint32_t nshards,
+                   uint32_t* owner_out);
+/* records / value bytes per destination (host out, nshards each) */
+int32_t jy_treg_route_count(jy_engine* eng, uint64_t n, const uint32_t* owner, const uint64_t* lr,
+                            uint32_t nshards, int32_t mem, uint64_t* rec_counts, uint64_t* byte_counts);
+/* scatter into caller-provided device buffers (records u64[n][4], bytes) laid
+ * out destination by destination in the order of the counts */
+int32_t jy_treg_route_scatter(jy_engine* eng, uint64_t n, const uint32_t* owner, const uint32_t* slot,
+                              const uint64_t* ts, const uint64_t* pre, const uint64_t* lr, uint32_t nshards,
+                              const uint64_t* rec_counts, const uint64_t* byte_counts, int32_t mem,
+                              uint64_t* recs_dev, uint8_t* bytes_dev);
+/* owner side: converge nsrc received runs (device buffers, counts on host) */
+int32_t jy_treg_converge_routed(jy_engine* eng, uint32_t nsrc, const uint64_t* rec_counts,
+                                const uint64_t* byte_counts, const uint64_t* recs_dev, const uint8_t* bytes_dev);
+
 #ifdef __cplusplus
 }
 #endif

@@ -68,6 +68,10 @@ SIGNATURES = {
     "jy_ujson_converge": (I32, [P, U64, P, P, U64, P, P, P, U64, P, P, U64, P, I32]),
     "jy_ujson_read_sizes": (I32, [P, U64, P, P, P]),
     "jy_ujson_read": (I32, [P, U64, P, P, P, P, P, P, P]),
+    "jy_keys_owner": (None, [U64, P, P, U32, P]),
+    "jy_treg_route_count": (I32, [P, U64, P, P, U32, I32, P, P]),
+    "jy_treg_route_scatter": (I32, [P, U64, P, P, P, P, P, U32, P, P, I32, P, P]),
+    "jy_treg_converge_routed": (I32, [P, U32, P, P, P, P]),
 }
 
 _lib = None

@@ -1,0 +1,218 @@
+// k_route.hip -- routing delta batches to owner shards (the exchange step).
+//
+// Keys are hash-sharded over S engines (jy_key_owner).  A peer batch that
+// lands on one GPU is partitioned by owner into contiguous per-destination
+// runs, exchanged with one all-to-all(v) (RCCL over xGMI; the host side
+// drives it), and each owner converges what it received, one call per
+// source run (a run holds each key at most once, as the sender's Map did).
+// This is the intra-node analogue of Cluster.broadcast_deltas
+// (jylis/cluster.pony:209-213); the reference replicates instead.
+//
+// TREG record: u64[4] = {slot on owner, ts, pre, lr'}, lr' = (byte offset
+// inside the destination's byte run << 24 | length) for values > 8 bytes,
+// whose bytes travel in a second all-to-all.
+//
+// Roofline: HBM.  Partition reads 4+4+24 B per entry (+ long value bytes),
+// writes 32 B per record; the receiver reads 32 B per record + state.
+
+#include <algorithm>
+
+#include "jy_internal.hpp"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr u32 kMaxShards = 64;
+
+__global__ __launch_bounds__(kThreads) void k_route_count(const u32* __restrict__ owner, const u64* __restrict__ lr,
+                                                          u64 n, u32 S, unsigned long long* __restrict__ counts) {
+  __shared__ unsigned long long lrec[kMaxShards], lbyte[kMaxShards];
+  for (u32 i = threadIdx.x; i < S; i += kThreads) lrec[i] = lbyte[i] = 0;
+  __syncthreads();
+  const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
+  if (i < n) {
+    const u32 o = owner[i];
+    const u64 len = lr[i] & JY_LR_LEN_MASK;
+    atomicAdd(&lrec[o], 1ull);
+    if (len > 8) atomicAdd(&lbyte[o], (unsigned long long)len);
+  }
+  __syncthreads();
+  for (u32 d = threadIdx.x; d < S; d += kThreads) {
+    if (lrec[d]) atomicAdd(&counts[d], lrec[d]);
+    if (lbyte[d]) atomicAdd(&counts[S + d], lbyte[d]);
+  }
+}
+
+// cursors[0..S) record cursors, [S..2S) byte cursors, initialised to the
+// destination bases; bases[S..2S) = byte bases (for relative offsets)
+__global__ __launch_bounds__(kThreads) void k_route_scatter_treg(
+    const u32* __restrict__ owner, const u32* __restrict__ slot, const u64* __restrict__ ts,
+    const u64* __restrict__ pre, const u64* __restrict__ lr, const uint8_t* __restrict__ arena, u64 n, u32 S,
+    unsigned long long* __restrict__ cursors, const u64* __restrict__ byte_base, u64* __restrict__ recs,
+    uint8_t* __restrict__ bytes) {
+  __shared__ unsigned long long lrec[kMaxShards], lbyte[kMaxShards], grec[kMaxShards], gbyte[kMaxShards];
+  for (u32 d = threadIdx.x; d < S; d += kThreads) lrec[d] = lbyte[d] = 0;
+  __syncthreads();
+  const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
+  u32 o = 0;
+  u64 len = 0, my_rec = 0, my_byte = 0, l = 0;
+  if (i < n) {
+    o = owner[i];
+    l = lr[i];
+    len = l & JY_LR_LEN_MASK;
+    my_rec = atomicAdd(&lrec[o], 1ull);
+    if (len > 8) my_byte = atomicAdd(&lbyte[o], (unsigned long long)len);
+  }
+  __syncthreads();
+  for (u32 d = threadIdx.x; d < S; d += kThreads) {
+    grec[d] = lrec[d] ? atomicAdd(&cursors[d], lrec[d]) : 0;
+    gbyte[d] = lbyte[d] ? atomicAdd(&cursors[S + d], lbyte[d]) : 0;
+  }
+  __syncthreads();
+  if (i >= n) return;
+  const u64 pos = grec[o] + my_rec;
+  u64 out_lr = l;
+  if (len > 8) {
+    const u64 bpos = gbyte[o] + my_byte;
+    const uint8_t* src = arena + (l >> JY_LR_LEN_BITS);
+    for (u64 j = 0; j < len; j++) bytes[bpos + j] = src[j];
+    out_lr = ((bpos - byte_base[o]) << JY_LR_LEN_BITS) | len;
+  }
+  u64* r = recs + pos * 4;
+  r[0] = slot[i];
+  r[1] = ts[i];
+  r[2] = pre[i];
+  r[3] = out_lr;
+}
+
+// receiver: LWW-merge one source run of records; long values are rebased
+// onto the arena region where this run's bytes were appended
+__global__ __launch_bounds__(kThreads) void k_treg_lww_records(u64* __restrict__ ts, u64* __restrict__ pre,
+                                                               u64* __restrict__ lr,
+                                                               const uint8_t* __restrict__ arena,
+                                                               const u64* __restrict__ recs, u64 n, u64 base) {
+  const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const u64* r = recs + i * 4;
+  const u64 s = r[0], t = r[1], p = r[2];
+  u64 l = r[3];
+  if ((l & JY_LR_LEN_MASK) > 8) l = (((l >> JY_LR_LEN_BITS) + base) << JY_LR_LEN_BITS) | (l & JY_LR_LEN_MASK);
+  const u64 t0 = ts[s];
+  bool win = t > t0;
+  if (t == t0) win = jy_value_cmp(p, l, pre[s], lr[s], arena) > 0;
+  if (win) {
+    ts[s] = t;
+    pre[s] = p;
+    lr[s] = l;
+  }
+}
+
+u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kThreads - 1) / kThreads); }
+
+}  // namespace
+
+extern "C" {
+
+void jy_keys_owner(uint64_t n, const uint8_t* kb, const uint64_t* ko, uint32_t nshards, uint32_t* out) {
+  for (u64 i = 0; i < n; i++) out[i] = jy_key_owner(kb + ko[i], ko[i + 1] - ko[i], nshards);
+}
+
+int32_t jy_treg_route_count(jy_engine* eng, uint64_t n, const uint32_t* owner, const uint64_t* lr, uint32_t nshards,
+                            int32_t mem, uint64_t* rec_counts, uint64_t* byte_counts) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (nshards == 0 || nshards > kMaxShards) return eng->fail(JY_ERANGE, "nshards must be in [1, 64]");
+  if (mem == JY_HOST)
+    for (u64 i = 0; i < n; i++)
+      if (owner[i] >= nshards) return eng->fail(JY_ERANGE, "owner outside [0, nshards)");
+  const void *dow, *dlr;
+  JY_TRY(jy_stage_begin(eng));
+  JY_TRY(jy_stage(eng, 0, owner, n * 4, mem, &dow));
+  JY_TRY(jy_stage(eng, 4, lr, n * 8, mem, &dlr));
+  JY_TRY(jy_stage_end(eng));
+  void* c;
+  JY_TRY(jy_scratch(eng, 12, 2 * nshards * 8, &c));
+  JY_HIP(eng, hipMemsetAsync(c, 0, 2 * nshards * 8, eng->stream));
+  if (n)
+    hipLaunchKernelGGL(k_route_count, dim3(blocks_for(n)), dim3(kThreads), 0, eng->stream,
+                       static_cast<const u32*>(dow), static_cast<const u64*>(dlr), n, nshards,
+                       static_cast<unsigned long long*>(c));
+  JY_HIP(eng, hipGetLastError());
+  std::vector<u64> h(2 * nshards);
+  JY_HIP(eng, hipMemcpyAsync(h.data(), c, 2 * nshards * 8, hipMemcpyDeviceToHost, eng->stream));
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  std::copy(h.begin(), h.begin() + nshards, rec_counts);
+  std::copy(h.begin() + nshards, h.end(), byte_counts);
+  return JY_OK;
+}
+
+int32_t jy_treg_route_scatter(jy_engine* eng, uint64_t n, const uint32_t* owner, const uint32_t* slot,
+                              const uint64_t* ts, const uint64_t* pre, const uint64_t* lr, uint32_t nshards,
+                              const uint64_t* rec_counts, const uint64_t* byte_counts, int32_t mem,
+                              uint64_t* recs_dev, uint8_t* bytes_dev) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (nshards == 0 || nshards > kMaxShards) return eng->fail(JY_ERANGE, "nshards must be in [1, 64]");
+  if (n == 0) return JY_OK;
+  std::vector<u64> init(2 * nshards), bbase(nshards);
+  u64 r = 0, b = 0;
+  for (u32 d = 0; d < nshards; d++) {
+    init[d] = r;
+    init[nshards + d] = b;
+    bbase[d] = b;
+    r += rec_counts[d];
+    b += byte_counts[d];
+  }
+  if (r != n) return eng->fail(JY_EINVAL, "record counts do not add up to n");
+  const void *dow, *dsl, *dts, *dpre, *dlr, *dinit, *dbb;
+  JY_TRY(jy_stage_begin(eng));
+  JY_TRY(jy_stage(eng, 0, owner, n * 4, mem, &dow));
+  JY_TRY(jy_stage(eng, 1, slot, n * 4, mem, &dsl));
+  JY_TRY(jy_stage(eng, 2, ts, n * 8, mem, &dts));
+  JY_TRY(jy_stage(eng, 3, pre, n * 8, mem, &dpre));
+  JY_TRY(jy_stage(eng, 4, lr, n * 8, mem, &dlr));
+  JY_TRY(jy_stage(eng, 5, init.data(), init.size() * 8, JY_HOST, &dinit));
+  JY_TRY(jy_stage(eng, 6, bbase.data(), bbase.size() * 8, JY_HOST, &dbb));
+  JY_TRY(jy_stage_end(eng));
+  // the cursors are updated in place: use a private copy of the bases
+  void* cur;
+  JY_TRY(jy_scratch(eng, 13, 2 * nshards * 8, &cur));
+  JY_HIP(eng, hipMemcpyAsync(cur, dinit, 2 * nshards * 8, hipMemcpyDeviceToDevice, eng->stream));
+  hipLaunchKernelGGL(k_route_scatter_treg, dim3(blocks_for(n)), dim3(kThreads), 0, eng->stream,
+                     static_cast<const u32*>(dow), static_cast<const u32*>(dsl), static_cast<const u64*>(dts),
+                     static_cast<const u64*>(dpre), static_cast<const u64*>(dlr), eng->arena[JY_TREG].p, n, nshards,
+                     static_cast<unsigned long long*>(cur), static_cast<const u64*>(dbb), recs_dev, bytes_dev);
+  JY_HIP(eng, hipGetLastError());
+  return JY_OK;
+}
+
+int32_t jy_treg_converge_routed(jy_engine* eng, uint32_t nsrc, const uint64_t* rec_counts,
+                                const uint64_t* byte_counts, const uint64_t* recs_dev, const uint8_t* bytes_dev) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  u64 total_bytes = 0;
+  for (u32 s = 0; s < nsrc; s++) total_bytes += byte_counts[s];
+  Arena& a = eng->arena[JY_TREG];
+  if (total_bytes) {
+    if (a.len + total_bytes > a.cap) {
+      u64 nc = std::max<u64>(std::max<u64>(a.cap * 2, a.len + total_bytes), 1 << 16);
+      void* p = a.p;
+      JY_TRY(jy_realloc(eng, &p, a.len, nc, false));
+      a.p = static_cast<uint8_t*>(p);
+      a.cap = nc;
+    }
+    if ((a.len + total_bytes) >> (64 - JY_LR_LEN_BITS)) return eng->fail(JY_ERANGE, "arena offset overflow");
+    JY_HIP(eng, hipMemcpyAsync(a.p + a.len, bytes_dev, total_bytes, hipMemcpyDeviceToDevice, eng->stream));
+  }
+  TregState& t = eng->treg;
+  u64 rec_off = 0, byte_off = a.len;
+  for (u32 s = 0; s < nsrc; s++) {
+    if (rec_counts[s])
+      hipLaunchKernelGGL(k_treg_lww_records, dim3(blocks_for(rec_counts[s])), dim3(kThreads), 0, eng->stream, t.ts,
+                         t.pre, t.lr, a.p, recs_dev + rec_off * 4, rec_counts[s], byte_off);
+    rec_off += rec_counts[s];
+    byte_off += byte_counts[s];
+  }
+  JY_HIP(eng, hipGetLastError());
+  a.len += total_bytes;
+  return JY_OK;
+}
+
+}  // extern "C"

@@ -257,49 +257,64 @@ def ujson_tables(D, seed, rounds=1, R=16, leaves=8, zipf=1.1, ops_per_round=None
     rng = np.random.default_rng(seed)
     ids = replica_ids(R, seed)
     kb, ko = counter_keys(D, prefix=key_prefix)
-    docs = []
-    for d in range(D):
-        vv = rng.integers(0, 24, R)
-        live = np.nonzero(vv)[0]
-        els = {}
-        for _ in range(min(int(rng.poisson(leaves)), 40)):
-            if len(live) == 0:
-                break
-            c = int(rng.choice(live))
-            q = int(rng.integers(1, vv[c] + 1))
-            els[(c, q)] = int(rng.integers(1, 64))
-        cloud = set()
-        if rng.random() < 0.25:
-            for _ in range(int(rng.integers(1, 4))):
-                c = int(rng.integers(R))
-                q = int(vv[c]) + 2 + int(rng.integers(0, 5))
-                cloud.add((c, q))
-                if rng.random() < 0.5:
-                    els[(c, q)] = int(rng.integers(1, 64))
-        docs.append((vv, els, cloud))
+    # ---- state, vectorised: vv, elements under seen dots, gapped cloud dots
+    vv = rng.integers(0, 24, (D, R)).astype(np.int64)
+    ne = np.minimum(rng.poisson(leaves, D), 40)
+    ed = np.repeat(np.arange(D), ne)
+    ec = rng.integers(0, R, len(ed))
+    top = vv[ed, ec]
+    keep = top > 0
+    ed, ec, top = ed[keep], ec[keep], top[keep]
+    eq = 1 + (rng.random(len(ed)) * top).astype(np.int64)
+    nk = rng.integers(1, 4, D) * (rng.random(D) < 0.25)
+    cd = np.repeat(np.arange(D), nk)
+    cc = rng.integers(0, R, len(cd))
+    cq = vv[cd, cc] + 2 + rng.integers(0, 5, len(cd))
+    _, first = np.unique((cd * R + cc) * 64 + cq, return_index=True)
+    cd, cc, cq = cd[first], cc[first], cq[first]
+    ce = rng.random(len(cd)) < 0.5
+    ed, ec, eq = (np.concatenate([x, y[ce]]) for x, y in ((ed, cd), (ec, cc), (eq, cq)))
+    _, first = np.unique((ed * R + ec) * 64 + eq, return_index=True)
+    ed, ec, eq = ed[first], ec[first], eq[first]
+    ee = rng.integers(1, 64, len(ed))
+    e_off = _excl_cumsum(np.bincount(ed, minlength=D)).astype(np.int64)
+    c_off = _excl_cumsum(np.bincount(cd, minlength=D)).astype(np.int64)
+    vd, vc = np.nonzero(vv)
+    state = {"key_bytes": kb, "key_offs": ko,
+             "el_offs": e_off.astype(np.uint64), "dot_ids": ids[ec], "dot_seqs": eq.astype(np.uint64),
+             "elems": ee.astype(np.uint64),
+             "vv_offs": _excl_cumsum(np.bincount(vd, minlength=D)), "vv_ids": ids[vc],
+             "vv_seqs": vv[vd, vc].astype(np.uint64),
+             "cloud_offs": c_off.astype(np.uint64), "cloud_ids": ids[cc], "cloud_seqs": cq.astype(np.uint64)}
+    # highest seq any context of a doc has seen per column (fresh dots go above)
+    seen = vv.copy()
+    np.maximum.at(seen, (cd, cc), cq)
 
-    def table(entries):
-        t = {"key_bytes": kb, "key_offs": ko}
+    def doc_elems(d):
+        lo, hi = e_off[d], e_off[d + 1]
+        return list(zip(ec[lo:hi].tolist(), eq[lo:hi].tolist(), ee[lo:hi].tolist()))
+
+    def table(folded):
+        docs = sorted(folded)
         cols = {k: [] for k in ("dot_ids", "dot_seqs", "elems", "vv_ids", "vv_seqs", "cloud_ids", "cloud_seqs")}
         eo, vo, co = [0], [0], [0]
-        sel = []
-        for d, (vv, els, cloud) in entries:
-            sel.append(d)
-            for (c, q), e in sorted(els.items()):
+        for d in docs:
+            dvv, dels, dcl = folded[d]
+            for (c, q), e in sorted(dels.items()):
                 cols["dot_ids"].append(ids[c])
                 cols["dot_seqs"].append(q)
                 cols["elems"].append(e)
-            eo.append(eo[-1] + len(els))
-            nz = [(c, int(vv[c])) for c in range(R) if vv[c]]
-            for c, q in nz:
+            eo.append(eo[-1] + len(dels))
+            for c, q in sorted(dvv.items()):
                 cols["vv_ids"].append(ids[c])
                 cols["vv_seqs"].append(q)
-            vo.append(vo[-1] + len(nz))
-            for c, q in sorted(cloud):
+            vo.append(vo[-1] + len(dvv))
+            for c, q in sorted(dcl):
                 cols["cloud_ids"].append(ids[c])
                 cols["cloud_seqs"].append(q)
-            co.append(co[-1] + len(cloud))
-        sel = np.array(sel, np.int64)
+            co.append(co[-1] + len(dcl))
+        sel = np.array(docs, np.int64)
+        t = {}
         t["key_bytes"], t["key_offs"] = gather_bytes(kb, ko, sel) if len(sel) else (np.zeros(0, np.uint8),
                                                                                    np.zeros(1, np.uint64))
         for k, v in cols.items():
@@ -307,37 +322,38 @@ def ujson_tables(D, seed, rounds=1, R=16, leaves=8, zipf=1.1, ops_per_round=None
         t["el_offs"], t["vv_offs"], t["cloud_offs"] = (np.array(x, np.uint64) for x in (eo, vo, co))
         return t
 
-    state = table(list(enumerate(docs)))
     perm = rng.permutation(D)
     deltas = []
     nops = ops_per_round or max(1, D // 2)
     for _ in range(rounds):
-        hit = perm[(rng.zipf(zipf, nops) - 1) % D]
-        kinds = rng.random(nops)
+        hit = perm[(rng.zipf(zipf, nops) - 1) % D].tolist()
+        kinds = rng.random(nops).tolist()
+        reps = rng.integers(0, R, nops).tolist()
+        u = rng.random((nops, 4)).tolist()
         folded = {}
-        for d, x in zip(hit.tolist(), kinds.tolist()):
-            vv, els, cloud = docs[d]
-            dvv, dels, dcl = folded.setdefault(d, (np.zeros(R, np.int64), {}, set()))
-            r = int(rng.integers(R))
+        for d, x, r, (u0, u1, u2, u3) in zip(hit, kinds, reps, u):
+            dvv, dels, dcl = folded.setdefault(d, ({}, {}, set()))
+            els = doc_elems(d)
             if x < 0.7:  # INS: a fresh dot of replica r (sometimes past a gap)
-                top = max([int(vv[r])] + [q for (c, q) in cloud | dcl | set(dels) if c == r])
-                q = top + 1 + (int(rng.integers(1, 3)) if rng.random() < 0.2 else 0)
-                dels[(r, q)] = int(rng.integers(1, 64))
+                q = int(seen[d, r]) + 1 + (1 + int(u1 * 2) if u0 < 0.2 else 0)
+                seen[d, r] = q
+                dels[(r, q)] = 1 + int(u2 * 63)
                 dcl.add((r, q))
             elif x < 0.9:  # RM one element value: every dot holding it
                 if els:
-                    e = list(els.values())[int(rng.integers(len(els)))]
-                    dcl.update(k for k, v in els.items() if v == e)
+                    e = els[int(u1 * len(els))][2]
+                    dcl.update((c, q) for c, q, v in els if v == e)
             else:  # CLR
-                dcl.update(els.keys())
-            if rng.random() < 0.1:  # carry a version-vector entry too
-                c = int(rng.integers(R))
-                dvv[c] = max(dvv[c], int(vv[c]))
-            if rng.random() < 0.05 and els:  # re-send an element the state holds
-                k = list(els)[int(rng.integers(len(els)))]
-                dels[k] = els[k]
-                dcl.add(k)
-        deltas.append(table(sorted(folded.items())))
+                dcl.update((c, q) for c, q, _ in els)
+            if u3 < 0.1:  # carry a version-vector entry too
+                c = int(u2 * R)
+                if vv[d, c]:
+                    dvv[c] = max(dvv.get(c, 0), int(vv[d, c]))
+            if u3 > 0.95 and els:  # re-send an element the state holds
+                c, q, v = els[int(u0 * len(els))]
+                dels[(c, q)] = v
+                dcl.add((c, q))
+        deltas.append(table(folded))
     return state, deltas
 
 
