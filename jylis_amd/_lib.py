@@ -86,6 +86,15 @@ def load(path=LIB_PATH):
         raise RuntimeError(
             f"{path} is missing: build it with `make -C jylis_amd` (hipcc, gfx950); "
             "there is no CPU fallback for the converge path")
+    # PyTorch-ROCm ships its own libamdhip64 / libhsa-runtime64 under the same
+    # sonames as /opt/rocm.  Whichever loads first serves the whole process;
+    # if the engine's copy initialises first, torch sees no GPU.  Load torch's
+    # runtime first (when torch is installed) so the engine and torch share
+    # one HIP runtime and device pointers pass between them.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
