@@ -221,6 +221,9 @@ void jy_engine_destroy(jy_engine* eng) {
     F(eng->ujson.elems[b]);
     F(eng->ujson.coff[b]);
     F(eng->ujson.cloud[b]);
+    F(eng->ujson.eseg[b]);
+    F(eng->tlog.seg[b]);
+    F(eng->ujson.cseg[b]);
   }
   F(eng->tlog.cutoff);
   F(eng->ujson.vv);

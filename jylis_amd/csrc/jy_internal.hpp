@@ -75,6 +75,7 @@ struct TlogState {  // CSR, double-buffered entries
   u64* ts[2] = {nullptr, nullptr};
   u64* pre[2] = {nullptr, nullptr};
   u64* lr[2] = {nullptr, nullptr};
+  u32* seg[2] = {nullptr, nullptr};  // slot of each entry
   u64 ecap[2] = {0, 0};
   int cur = 0;
   u64* cutoff = nullptr;  // [kcap]
@@ -87,9 +88,11 @@ struct UjsonState {  // CSR elements + CSR cloud (double-buffered), dense vv
   u64* eoff[2] = {nullptr, nullptr};  // [kcap + 1]
   u64* dots[2] = {nullptr, nullptr};
   u64* elems[2] = {nullptr, nullptr};
+  u32* eseg[2] = {nullptr, nullptr};  // slot of each element
   u64 ecap[2] = {0, 0};
   u64* coff[2] = {nullptr, nullptr};  // [kcap + 1]
   u64* cloud[2] = {nullptr, nullptr};
+  u32* cseg[2] = {nullptr, nullptr};  // slot of each cloud dot
   u64 ccap[2] = {0, 0};
   int cur = 0;
   u64* vv = nullptr;  // [kcap][R]
@@ -126,8 +129,8 @@ struct jy_engine {
   UjsonState ujson;
 
   // scratch (device) reused across calls, stream-ordered
-  // 0-7 staged inputs, 8-14 merge temporaries, 15 scan temp storage
-  DevArray scratch[16];
+  // 0-7 staged inputs, 8-14 and 16-23 merge temporaries, 15 scan temp storage
+  DevArray scratch[24];
   // column list of the last block merge, kept resident (a peer set rarely changes)
   std::vector<u16> cols_cache;
   u16* cols_dev = nullptr;

@@ -2,25 +2,33 @@
 //
 // Semantics (oracle/jy_oracle.cpp TLog; tlog.md:116-133, repo_tlog.pony:66-67):
 //   cutoff' = max(cutoff_s, cutoff_d)
-//   entries' = dedupe(state U delta) restricted to ts >= cutoff', sorted with
+//   entries' = dedupe(state U delta) restricted to ts >= cutoff', ordered with
 //              the later timestamp first, then the greater value first
 //              (Pony String order); (ts, value) duplicates collapse.
 //
-// HBM layout: per type, CSR over slots -- off[kcap+1] (u64), entries SoA
-// ts / pre / lr (u64 each, value handle as in TREG: 8-byte big-endian prefix
-// + arena offset/length), cutoff[kcap].  Entries are double-buffered: a
-// converge rewrites the whole CSR into the other buffer in three passes
-//   1. count  : per slot, size of the merged log       (thread per slot)
-//   2. scan   : exclusive prefix sum -> new offsets     (hipcub)
-//   3. write  : per slot, merge into the new buffer     (thread per slot)
-// Slots without a delta in the batch are copied.  Delta segments must be
-// canonical (strictly descending); a malformed segment leaves its key
-// untouched and is counted in jy_skipped (the reference swallows converge
-// errors, repo_tlog.pony:67).
+// HBM layout: per type, CSR over slots -- off[kcap+1] (u64); entries SoA
+// ts / pre / lr (u64 each; value handle as in TREG: 8-byte big-endian prefix
+// + arena offset/length) and seg (u32 slot of the entry); cutoff[kcap].
+// Entries are double-buffered: a converge rewrites the CSR into the other
+// buffer.
 //
-// Roofline: HBM.  Per batch: 24 B read per input entry (state + delta;
-// count pass re-reads 8 B ts per entry), 24 B written per output entry,
-// plus 8 B offset + 8 B cutoff read/write per slot.
+// Parallel shape: one thread per ENTRY (state or delta), coalesced, with
+// merge-path positions -- no per-key loops, so long or skewed logs cost the
+// same per entry as short ones:
+//   keep(state e)  = ts >= cutoff'
+//   keep(delta e)  = ts >= cutoff' and no equal entry in the state segment
+//   pos(e) = new_off[key] + #kept own-side entries before e
+//                         + #kept other-side entries ordered before e
+// the counts coming from exclusive scans of the keep flags and one binary
+// search (entry order, value bytes compared only on (ts, prefix) ties) into
+// the other side's sorted segment.  A delta segment that is not strictly
+// ordered is not a TLog: its key is left untouched and counted (the
+// reference swallows converge errors, repo_tlog.pony:67).
+//
+// Roofline: HBM.  Per input entry: 24 B read (+4 B seg, state side) and
+// 28 B written per output entry; per key 16 B offsets + 16 B cutoff; keep
+// flags and their scans add 24 B per input entry (u64 flag, scan write +
+// read); see DESIGN.md.
 
 #include <hipcub/hipcub.hpp>
 
@@ -33,62 +41,39 @@ namespace {
 constexpr int kThreads = 256;
 constexpr u32 kNone = 0xFFFFFFFFu;
 
-struct Seg {  // a view of one sorted log
-  const u64* ts;
-  const u64* pre;
-  const u64* lr;
-  u64 lo, hi;
-};
+__device__ __forceinline__ u64 gid() { return (u64)blockIdx.x * kThreads + threadIdx.x; }
 
-// > 0 if entry (ta, pa, la) sorts before (tb, pb, lb)
+// > 0 if (ta, pa, la) is ordered before (tb, pb, lb): later ts, then greater value
 __device__ __forceinline__ int entry_cmp(u64 ta, u64 pa, u64 la, u64 tb, u64 pb, u64 lb,
                                          const uint8_t* __restrict__ arena) {
   if (ta != tb) return ta > tb ? 1 : -1;
   return jy_value_cmp(pa, la, pb, lb, arena);
 }
 
-__device__ __forceinline__ bool seg_canonical(const Seg& s, const uint8_t* __restrict__ arena) {
-  for (u64 j = s.lo + 1; j < s.hi; j++)
-    if (entry_cmp(s.ts[j - 1], s.pre[j - 1], s.lr[j - 1], s.ts[j], s.pre[j], s.lr[j], arena) <= 0) return false;
-  return true;
-}
+struct Ent {
+  u64 t, p, l;
+};
 
-// drop the tail below the cutoff (entries are in non-increasing ts order)
-__device__ __forceinline__ void seg_cut(Seg& s, u64 c) {
-  while (s.hi > s.lo && s.ts[s.hi - 1] < c) s.hi--;
-}
-
-// Merge two canonical logs; emit(ts, pre, lr) for each output entry in order.
-template <class Emit>
-__device__ __forceinline__ void merge_logs(Seg a, Seg b, const uint8_t* __restrict__ arena, Emit emit) {
-  u64 i = a.lo, j = b.lo;
-  while (i < a.hi && j < b.hi) {
-    const u64 ta = a.ts[i], tb = b.ts[j];
-    int c;
-    if (ta != tb) {
-      c = ta > tb ? 1 : -1;
-    } else {
-      c = jy_value_cmp(a.pre[i], a.lr[i], b.pre[j], b.lr[j], arena);
-    }
-    if (c > 0) {
-      emit(ta, a.pre[i], a.lr[i]);
-      i++;
-    } else if (c < 0) {
-      emit(tb, b.pre[j], b.lr[j]);
-      j++;
-    } else {  // (ts, value) duplicate: keep the state's copy
-      emit(ta, a.pre[i], a.lr[i]);
-      i++;
-      j++;
-    }
+// first index in [lo, hi) of a sorted log whose entry is NOT ordered before x
+__device__ __forceinline__ u64 lower_bound_entry(const u64* __restrict__ ts, const u64* __restrict__ pre,
+                                                 const u64* __restrict__ lr, u64 lo, u64 hi, const Ent& x,
+                                                 const uint8_t* __restrict__ arena) {
+  while (lo < hi) {
+    const u64 m = (lo + hi) >> 1;
+    if (entry_cmp(ts[m], pre[m], lr[m], x.t, x.p, x.l, arena) > 0) lo = m + 1;
+    else hi = m;
   }
-  for (; i < a.hi; i++) emit(a.ts[i], a.pre[i], a.lr[i]);
-  for (; j < b.hi; j++) emit(b.ts[j], b.pre[j], b.lr[j]);
+  return lo;
 }
 
-__global__ __launch_bounds__(kThreads) void k_scatter_ptr(u32* __restrict__ dptr, const u32* __restrict__ slot, u64 n) {
-  const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
-  if (i < n) dptr[slot[i]] = (u32)i;
+__device__ __forceinline__ u32 seg_of(const u64* __restrict__ offs, u64 n, u64 j) {
+  u64 lo = 0, hi = n;
+  while (hi - lo > 1) {
+    const u64 m = (lo + hi) >> 1;
+    if (offs[m] <= j) lo = m;
+    else hi = m;
+  }
+  return (u32)lo;
 }
 
 struct TlogArgs {
@@ -97,94 +82,151 @@ struct TlogArgs {
   const u64* ts;
   const u64* pre;
   const u64* lr;
+  const u32* seg;
   u64* cutoff;
+  u64 nkeys, na;
   // delta batch
-  const u32* dptr;
+  u64 nd, nb;
+  const u32* slot;
+  u32* dptr;
   const u64* dcut;
   const u64* doff;
   const u64* dts;
   const u64* dpre;
   const u64* dlr;
   const uint8_t* arena;
-  u64 nkeys;
+  // temporaries
+  u32* bad;   // [nd]
+  u64* cut;   // [nd] merged cutoff
+  u64* flag_a;
+  u64* scan_a;
+  u64* flag_b;
+  u64* scan_b;
 };
 
-// resolve slot s: its state segment, its delta segment (if any, canonical),
-// and the merged cutoff.  Returns false for "copy unchanged".
-__device__ __forceinline__ bool tlog_resolve(const TlogArgs& A, u64 s, Seg& a, Seg& b, u64& c, bool& bad) {
-  a = Seg{A.ts, A.pre, A.lr, A.off[s], A.off[s + 1]};
-  bad = false;
-  const u32 i = A.dptr[s];
-  if (i == kNone) return false;
-  b = Seg{A.dts, A.dpre, A.dlr, A.doff[i], A.doff[i + 1]};
-  if (!seg_canonical(b, A.arena)) {
-    bad = true;
-    return false;
-  }
-  const u64 cs = A.cutoff[s], cd = A.dcut[i];
-  c = cs > cd ? cs : cd;
-  seg_cut(a, c);
-  seg_cut(b, c);
-  return true;
+__global__ __launch_bounds__(kThreads) void k_tlog_prep(TlogArgs A) {
+  const u64 k = gid();
+  if (k >= A.nd) return;
+  const u64 s = A.slot[k];
+  A.dptr[s] = (u32)k;
+  A.bad[k] = 0;
+  const u64 cs = A.cutoff[s], cd = A.dcut[k];
+  A.cut[k] = cs > cd ? cs : cd;
 }
 
-__global__ __launch_bounds__(kThreads) void k_tlog_count(TlogArgs A, u64* __restrict__ cnt,
-                                                         unsigned long long* __restrict__ skipped) {
-  const u64 s = (u64)blockIdx.x * kThreads + threadIdx.x;
+__global__ __launch_bounds__(kThreads) void k_tlog_validate(TlogArgs A) {
+  const u64 j = gid();
+  if (j >= A.nb) return;
+  const u32 k = seg_of(A.doff, A.nd, j);
+  if (j > A.doff[k] &&
+      entry_cmp(A.dts[j - 1], A.dpre[j - 1], A.dlr[j - 1], A.dts[j], A.dpre[j], A.dlr[j], A.arena) <= 0)
+    A.bad[k] = 1;
+}
+
+__global__ __launch_bounds__(kThreads) void k_tlog_drop_bad(TlogArgs A, unsigned long long* __restrict__ skipped) {
+  const u64 k = gid();
+  if (k >= A.nd) return;
+  if (A.bad[k]) {
+    A.dptr[A.slot[k]] = kNone;
+    atomicAdd(skipped, 1ull);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_tlog_flag_a(TlogArgs A) {
+  const u64 i = gid();
+  if (i > A.na) return;
+  if (i == A.na) {
+    A.flag_a[i] = 0;
+    return;
+  }
+  const u32 k = A.dptr[A.seg[i]];
+  A.flag_a[i] = (k == kNone) ? 1 : (A.ts[i] >= A.cut[k]);
+}
+
+__global__ __launch_bounds__(kThreads) void k_tlog_flag_b(TlogArgs A) {
+  const u64 j = gid();
+  if (j > A.nb) return;
+  if (j == A.nb) {
+    A.flag_b[j] = 0;
+    return;
+  }
+  const u32 k = seg_of(A.doff, A.nd, j);
+  const u64 s = A.slot[k];
+  u64 keep = 0;
+  if (A.dptr[s] == k && A.dts[j] >= A.cut[k]) {
+    const Ent x{A.dts[j], A.dpre[j], A.dlr[j]};
+    const u64 hi = A.off[s + 1];
+    const u64 p = lower_bound_entry(A.ts, A.pre, A.lr, A.off[s], hi, x, A.arena);
+    keep = !(p < hi && entry_cmp(A.ts[p], A.pre[p], A.lr[p], x.t, x.p, x.l, A.arena) == 0);
+  }
+  A.flag_b[j] = keep;
+}
+
+__global__ __launch_bounds__(kThreads) void k_tlog_sizes_out(TlogArgs A, u64* __restrict__ cnt) {
+  const u64 s = gid();
   if (s > A.nkeys) return;
   if (s == A.nkeys) {
     cnt[s] = 0;
     return;
   }
-  Seg a, b;
-  u64 c;
-  bool bad;
-  if (!tlog_resolve(A, s, a, b, c, bad)) {
-    cnt[s] = a.hi - a.lo;
-    if (bad) atomicAdd(skipped, 1ull);
-    return;
-  }
-  u64 n = 0;
-  merge_logs(a, b, A.arena, [&](u64, u64, u64) { n++; });
+  const u32 k = A.dptr[s];
+  u64 n = A.scan_a[A.off[s + 1]] - A.scan_a[A.off[s]];
+  if (k != kNone) n += A.scan_b[A.doff[k + 1]] - A.scan_b[A.doff[k]];
   cnt[s] = n;
 }
 
-__global__ __launch_bounds__(kThreads) void k_tlog_write(TlogArgs A, const u64* __restrict__ noff,
-                                                         u64* __restrict__ ots, u64* __restrict__ opre,
-                                                         u64* __restrict__ olr) {
-  const u64 s = (u64)blockIdx.x * kThreads + threadIdx.x;
-  if (s >= A.nkeys) return;
-  Seg a, b;
-  u64 c;
-  bool bad;
-  u64 o = noff[s];
-  if (!tlog_resolve(A, s, a, b, c, bad)) {
-    for (u64 j = a.lo; j < a.hi; j++, o++) {
-      ots[o] = a.ts[j];
-      opre[o] = a.pre[j];
-      olr[o] = a.lr[j];
-    }
-    return;
+__global__ __launch_bounds__(kThreads) void k_tlog_scatter_a(TlogArgs A, const u64* __restrict__ noff,
+                                                             u64* __restrict__ ots, u64* __restrict__ opre,
+                                                             u64* __restrict__ olr, u32* __restrict__ oseg) {
+  const u64 i = gid();
+  if (i >= A.na || !A.flag_a[i]) return;
+  const u64 s = A.seg[i];
+  const u32 k = A.dptr[s];
+  const Ent x{A.ts[i], A.pre[i], A.lr[i]};
+  u64 pos = noff[s] + (A.scan_a[i] - A.scan_a[A.off[s]]);
+  if (k != kNone) {
+    const u64 lo = A.doff[k];
+    pos += A.scan_b[lower_bound_entry(A.dts, A.dpre, A.dlr, lo, A.doff[k + 1], x, A.arena)] - A.scan_b[lo];
   }
-  merge_logs(a, b, A.arena, [&](u64 t, u64 p, u64 l) {
-    ots[o] = t;
-    opre[o] = p;
-    olr[o] = l;
-    o++;
-  });
-  A.cutoff[s] = c;
+  ots[pos] = x.t;
+  opre[pos] = x.p;
+  olr[pos] = x.l;
+  oseg[pos] = (u32)s;
+}
+
+__global__ __launch_bounds__(kThreads) void k_tlog_scatter_b(TlogArgs A, const u64* __restrict__ noff,
+                                                             u64* __restrict__ ots, u64* __restrict__ opre,
+                                                             u64* __restrict__ olr, u32* __restrict__ oseg) {
+  const u64 j = gid();
+  if (j >= A.nb || !A.flag_b[j]) return;
+  const u32 k = seg_of(A.doff, A.nd, j);
+  const u64 s = A.slot[k];
+  const Ent x{A.dts[j], A.dpre[j], A.dlr[j]};
+  const u64 lo = A.off[s];
+  const u64 p = lower_bound_entry(A.ts, A.pre, A.lr, lo, A.off[s + 1], x, A.arena);
+  const u64 pos = noff[s] + (A.scan_b[j] - A.scan_b[A.doff[k]]) + (A.scan_a[p] - A.scan_a[lo]);
+  ots[pos] = x.t;
+  opre[pos] = x.p;
+  olr[pos] = x.l;
+  oseg[pos] = (u32)s;
+}
+
+__global__ __launch_bounds__(kThreads) void k_tlog_cut_store(TlogArgs A) {
+  const u64 k = gid();
+  if (k >= A.nd || A.bad[k]) return;
+  A.cutoff[A.slot[k]] = A.cut[k];
 }
 
 __global__ __launch_bounds__(kThreads) void k_fill_tail(u64* __restrict__ off, u64 from, u64 to) {
   // off[from+1 .. to] = off[from]  (new, empty slots)
-  const u64 i = from + 1 + (u64)blockIdx.x * kThreads + threadIdx.x;
+  const u64 i = from + 1 + gid();
   if (i <= to) off[i] = off[from];
 }
 
 __global__ __launch_bounds__(kThreads) void k_tlog_sizes(const u64* __restrict__ off, const u64* __restrict__ cutoff,
                                                          const u32* __restrict__ slots, u64 n, u64* __restrict__ len,
                                                          u64* __restrict__ cut) {
-  const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
+  const u64 i = gid();
   if (i >= n) return;
   const u64 s = slots[i];
   len[i] = off[s + 1] - off[s];
@@ -196,7 +238,7 @@ __global__ __launch_bounds__(kThreads) void k_tlog_gather(const u64* __restrict_
                                                           const u32* __restrict__ slots, const u64* __restrict__ ooff,
                                                           u64 n, u64* __restrict__ ots, u64* __restrict__ opre,
                                                           u64* __restrict__ olr) {
-  const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
+  const u64 i = gid();
   if (i >= n) return;
   const u64 s = slots[i];
   u64 o = ooff[i];
@@ -208,6 +250,23 @@ __global__ __launch_bounds__(kThreads) void k_tlog_gather(const u64* __restrict_
 }
 
 u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kThreads - 1) / kThreads); }
+
+#define LAUNCH(k, n, ...)                                                                          \
+  do {                                                                                             \
+    hipLaunchKernelGGL(k, dim3(blocks_for(n)), dim3(kThreads), 0, eng->stream, __VA_ARGS__);     \
+    JY_HIP(eng, hipGetLastError());                                                                \
+  } while (0)
+
+int32_t realloc_dead(jy_engine* eng, void** p, u64 bytes) {
+  if (*p) {
+    JY_HIP(eng, hipStreamSynchronize(eng->stream));
+    JY_HIP(eng, hipFree(*p));
+    *p = nullptr;
+  }
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) return eng->fail(JY_ENOMEM, std::string("tlog entries: ") + hipGetErrorString(e));
+  return JY_OK;
+}
 
 }  // namespace
 
@@ -225,17 +284,9 @@ int32_t jy_scan_u64(jy_engine* eng, const u64* in, u64* out, u64 n) {
 static int32_t ensure_entries(jy_engine* eng, int buf, u64 need) {
   TlogState& t = eng->tlog;
   if (need <= t.ecap[buf] && t.ts[buf]) return JY_OK;
-  u64 nc = std::max<u64>(std::max<u64>(need + need / 2, eng->cfg.entry_capacity[JY_TLOG]), 1024);
-  // contents of the target buffer are dead (it is rewritten): free, then allocate
-  for (u64** p : {&t.ts[buf], &t.pre[buf], &t.lr[buf]}) {
-    if (*p) {
-      JY_HIP(eng, hipStreamSynchronize(eng->stream));
-      JY_HIP(eng, hipFree(*p));
-      *p = nullptr;
-    }
-    hipError_t e = hipMalloc(reinterpret_cast<void**>(p), nc * 8);
-    if (e != hipSuccess) return eng->fail(JY_ENOMEM, std::string("tlog entries: ") + hipGetErrorString(e));
-  }
+  const u64 nc = std::max<u64>(std::max<u64>(need + need / 2, eng->cfg.entry_capacity[JY_TLOG]), 1024);
+  for (u64** p : {&t.ts[buf], &t.pre[buf], &t.lr[buf]}) JY_TRY(realloc_dead(eng, reinterpret_cast<void**>(p), nc * 8));
+  JY_TRY(realloc_dead(eng, reinterpret_cast<void**>(&t.seg[buf]), nc * 4));
   t.ecap[buf] = nc;
   return JY_OK;
 }
@@ -245,7 +296,6 @@ int32_t jy_tlog_grow(jy_engine* eng, u64 need) {
   if (need <= t.kcap && t.cutoff) return JY_OK;
   u64 nk = std::max<u64>(need, t.kcap ? t.kcap * 2 : need);
   nk = std::max<u64>((nk + 63) & ~63ull, 64);
-  const u64 live = eng->nkeys[JY_TLOG];
   void* c = t.cutoff;
   JY_TRY(jy_realloc(eng, &c, t.kcap * 8, nk * 8, true));
   t.cutoff = static_cast<u64*>(c);
@@ -254,7 +304,6 @@ int32_t jy_tlog_grow(jy_engine* eng, u64 need) {
     JY_TRY(jy_realloc(eng, &o, t.kcap ? (t.kcap + 1) * 8 : 0, (nk + 1) * 8, true));
     t.off[b] = static_cast<u64*>(o);
   }
-  (void)live;
   t.kcap = nk;
   for (int b = 0; b < 2; b++) JY_TRY(ensure_entries(eng, b, 1));
   return JY_OK;
@@ -264,9 +313,7 @@ int32_t jy_tlog_grow(jy_engine* eng, u64 need) {
 int32_t jy_tlog_extend(jy_engine* eng, u64 from, u64 to) {
   if (to <= from) return JY_OK;
   TlogState& t = eng->tlog;
-  hipLaunchKernelGGL(k_fill_tail, dim3(blocks_for(to - from)), dim3(kThreads), 0, eng->stream, t.off[t.cur], from,
-                     to);
-  JY_HIP(eng, hipGetLastError());
+  LAUNCH(k_fill_tail, to - from, t.off[t.cur], from, to);
   return JY_OK;
 }
 
@@ -275,49 +322,75 @@ int32_t jy_tlog_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* dcut, 
   TlogState& t = eng->tlog;
   const u64 nk = eng->nkeys[JY_TLOG];
   if (nd == 0 || nk == 0) return JY_OK;
-  // live entry count of the current buffer: the previous merge's total
+  // exact live entry count of the current buffer: the previous merge's total
   JY_HIP(eng, hipEventSynchronize(eng->total_ready));
-  const u64 live = t.nent_known ? eng->pin_total[0] : t.nent_bound;
+  const u64 na = t.nent_known ? eng->pin_total[0] : 0;
   const int cur = t.cur, nxt = 1 - cur;
-  JY_TRY(ensure_entries(eng, nxt, live + nent));
+  JY_TRY(ensure_entries(eng, nxt, na + nent));
 
-  void *dptr, *cnt;
-  JY_TRY(jy_scratch(eng, 8, nk * 4, &dptr));
-  JY_TRY(jy_scratch(eng, 9, (nk + 1) * 8, &cnt));
-  JY_HIP(eng, hipMemsetAsync(dptr, 0xFF, nk * 4, eng->stream));
-  hipLaunchKernelGGL(k_scatter_ptr, dim3(blocks_for(nd)), dim3(kThreads), 0, eng->stream, static_cast<u32*>(dptr),
-                     slot, nd);
-  TlogArgs A{t.off[cur], t.ts[cur], t.pre[cur], t.lr[cur], t.cutoff, static_cast<const u32*>(dptr), dcut, doff,
-             dts, dpre, dlr, eng->arena[JY_TLOG].p, nk};
-  hipLaunchKernelGGL(k_tlog_count, dim3(blocks_for(nk + 1)), dim3(kThreads), 0, eng->stream, A,
-                     static_cast<u64*>(cnt), reinterpret_cast<unsigned long long*>(eng->skipped_dev));
-  JY_HIP(eng, hipGetLastError());
-  JY_TRY(jy_scan_u64(eng, static_cast<const u64*>(cnt), t.off[nxt], nk));
-  hipLaunchKernelGGL(k_tlog_write, dim3(blocks_for(nk)), dim3(kThreads), 0, eng->stream, A, t.off[nxt], t.ts[nxt],
-                     t.pre[nxt], t.lr[nxt]);
-  JY_HIP(eng, hipGetLastError());
+  TlogArgs A{};
+  A.off = t.off[cur];
+  A.ts = t.ts[cur];
+  A.pre = t.pre[cur];
+  A.lr = t.lr[cur];
+  A.seg = t.seg[cur];
+  A.cutoff = t.cutoff;
+  A.nkeys = nk;
+  A.na = na;
+  A.nd = nd;
+  A.nb = nent;
+  A.slot = slot;
+  A.dcut = dcut;
+  A.doff = doff;
+  A.dts = dts;
+  A.dpre = dpre;
+  A.dlr = dlr;
+  A.arena = eng->arena[JY_TLOG].p;
+  void* p;
+  JY_TRY(jy_scratch(eng, 8, nk * 4, &p));
+  A.dptr = static_cast<u32*>(p);
+  JY_TRY(jy_scratch(eng, 9, nd * 12, &p));
+  A.cut = static_cast<u64*>(p);
+  A.bad = reinterpret_cast<u32*>(A.cut + nd);
+  JY_TRY(jy_scratch(eng, 11, (na + 1) * 16, &p));
+  A.flag_a = static_cast<u64*>(p);
+  A.scan_a = A.flag_a + na + 1;
+  JY_TRY(jy_scratch(eng, 12, (nent + 1) * 16, &p));
+  A.flag_b = static_cast<u64*>(p);
+  A.scan_b = A.flag_b + nent + 1;
+  JY_TRY(jy_scratch(eng, 16, (nk + 1) * 8, &p));
+  u64* cnt = static_cast<u64*>(p);
+
+  JY_HIP(eng, hipMemsetAsync(A.dptr, 0xFF, nk * 4, eng->stream));
+  LAUNCH(k_tlog_prep, nd, A);
+  if (nent) LAUNCH(k_tlog_validate, nent, A);
+  LAUNCH(k_tlog_drop_bad, nd, A, reinterpret_cast<unsigned long long*>(eng->skipped_dev));
+  LAUNCH(k_tlog_flag_a, na + 1, A);
+  LAUNCH(k_tlog_flag_b, nent + 1, A);
+  JY_TRY(jy_scan_u64(eng, A.flag_a, A.scan_a, na));
+  JY_TRY(jy_scan_u64(eng, A.flag_b, A.scan_b, nent));
+  LAUNCH(k_tlog_sizes_out, nk + 1, A, cnt);
+  JY_TRY(jy_scan_u64(eng, cnt, t.off[nxt], nk));
+  if (na) LAUNCH(k_tlog_scatter_a, na, A, t.off[nxt], t.ts[nxt], t.pre[nxt], t.lr[nxt], t.seg[nxt]);
+  if (nent) LAUNCH(k_tlog_scatter_b, nent, A, t.off[nxt], t.ts[nxt], t.pre[nxt], t.lr[nxt], t.seg[nxt]);
+  LAUNCH(k_tlog_cut_store, nd, A);
   // publish the new total for the next call (read back asynchronously)
   JY_HIP(eng, hipMemcpyAsync(eng->pin_total, t.off[nxt] + nk, 8, hipMemcpyDeviceToHost, eng->stream));
   JY_HIP(eng, hipEventRecord(eng->total_ready, eng->stream));
   t.nent_known = true;
-  t.nent_bound = live + nent;
   t.cur = nxt;
   return JY_OK;
 }
 
 int32_t jy_tlog_sizes(jy_engine* eng, u64 n, const u32* slots, u64* len, u64* cut) {
   TlogState& t = eng->tlog;
-  hipLaunchKernelGGL(k_tlog_sizes, dim3(blocks_for(n)), dim3(kThreads), 0, eng->stream, t.off[t.cur], t.cutoff,
-                     slots, n, len, cut);
-  JY_HIP(eng, hipGetLastError());
+  LAUNCH(k_tlog_sizes, n, t.off[t.cur], t.cutoff, slots, n, len, cut);
   return JY_OK;
 }
 
 int32_t jy_tlog_gather(jy_engine* eng, u64 n, const u32* slots, const u64* ooff, u64* ts, u64* pre, u64* lr) {
   TlogState& t = eng->tlog;
   const int c = t.cur;
-  hipLaunchKernelGGL(k_tlog_gather, dim3(blocks_for(n)), dim3(kThreads), 0, eng->stream, t.off[c], t.ts[c],
-                     t.pre[c], t.lr[c], slots, ooff, n, ts, pre, lr);
-  JY_HIP(eng, hipGetLastError());
+  LAUNCH(k_tlog_gather, n, t.off[c], t.ts[c], t.pre[c], t.lr[c], slots, ooff, n, ts, pre, lr);
   return JY_OK;
 }
