@@ -204,3 +204,5 @@ int32_t jy_ujson_merge(jy_engine* eng, u64 ndocs, const u32* slot, const u64* eo
 
 // device exclusive scan of n u64 counts into out[0..n] (out[n] = total)
 int32_t jy_scan_u64(jy_engine* eng, const u64* in, u64* out, u64 n);
+// segment id (u32) of each of the n items of a CSR offs[0..nseg]
+int32_t jy_seg_ids(jy_engine* eng, const u64* offs, u64 nseg, u64 n, u32* out);

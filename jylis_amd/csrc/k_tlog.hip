@@ -66,16 +66,6 @@ __device__ __forceinline__ u64 lower_bound_entry(const u64* __restrict__ ts, con
   return lo;
 }
 
-__device__ __forceinline__ u32 seg_of(const u64* __restrict__ offs, u64 n, u64 j) {
-  u64 lo = 0, hi = n;
-  while (hi - lo > 1) {
-    const u64 m = (lo + hi) >> 1;
-    if (offs[m] <= j) lo = m;
-    else hi = m;
-  }
-  return (u32)lo;
-}
-
 struct TlogArgs {
   // state (current buffer)
   const u64* off;
@@ -95,11 +85,11 @@ struct TlogArgs {
   const u64* dpre;
   const u64* dlr;
   const uint8_t* arena;
+  const u32* dseg;  // [nb] delta key of each delta entry
   // temporaries
-  u32* bad;   // [nd]
-  u64* cut;   // [nd] merged cutoff
-  u64* flag_a;
-  u64* scan_a;
+  u32* bad;     // [nd]
+  u64* cut;     // [nd] merged cutoff
+  u64* keep_a;  // [nkeys] surviving state entries: a prefix of every log
   u64* flag_b;
   u64* scan_b;
 };
@@ -117,7 +107,7 @@ __global__ __launch_bounds__(kThreads) void k_tlog_prep(TlogArgs A) {
 __global__ __launch_bounds__(kThreads) void k_tlog_validate(TlogArgs A) {
   const u64 j = gid();
   if (j >= A.nb) return;
-  const u32 k = seg_of(A.doff, A.nd, j);
+  const u32 k = A.dseg[j];
   if (j > A.doff[k] &&
       entry_cmp(A.dts[j - 1], A.dpre[j - 1], A.dlr[j - 1], A.dts[j], A.dpre[j], A.dlr[j], A.arena) <= 0)
     A.bad[k] = 1;
@@ -132,17 +122,6 @@ __global__ __launch_bounds__(kThreads) void k_tlog_drop_bad(TlogArgs A, unsigned
   }
 }
 
-__global__ __launch_bounds__(kThreads) void k_tlog_flag_a(TlogArgs A) {
-  const u64 i = gid();
-  if (i > A.na) return;
-  if (i == A.na) {
-    A.flag_a[i] = 0;
-    return;
-  }
-  const u32 k = A.dptr[A.seg[i]];
-  A.flag_a[i] = (k == kNone) ? 1 : (A.ts[i] >= A.cut[k]);
-}
-
 __global__ __launch_bounds__(kThreads) void k_tlog_flag_b(TlogArgs A) {
   const u64 j = gid();
   if (j > A.nb) return;
@@ -150,7 +129,7 @@ __global__ __launch_bounds__(kThreads) void k_tlog_flag_b(TlogArgs A) {
     A.flag_b[j] = 0;
     return;
   }
-  const u32 k = seg_of(A.doff, A.nd, j);
+  const u32 k = A.dseg[j];
   const u64 s = A.slot[k];
   u64 keep = 0;
   if (A.dptr[s] == k && A.dts[j] >= A.cut[k]) {
@@ -170,7 +149,21 @@ __global__ __launch_bounds__(kThreads) void k_tlog_sizes_out(TlogArgs A, u64* __
     return;
   }
   const u32 k = A.dptr[s];
-  u64 n = A.scan_a[A.off[s + 1]] - A.scan_a[A.off[s]];
+  const u64 lo = A.off[s];
+  u64 hi = A.off[s + 1];
+  if (k != kNone) {
+    // entries are in non-increasing ts order: the cutoff drops a suffix
+    const u64 c = A.cut[k];
+    u64 a = lo;
+    while (a < hi) {
+      const u64 m = (a + hi) >> 1;
+      if (A.ts[m] >= c) a = m + 1;
+      else hi = m;
+    }
+    hi = a;
+  }
+  A.keep_a[s] = hi - lo;
+  u64 n = hi - lo;
   if (k != kNone) n += A.scan_b[A.doff[k + 1]] - A.scan_b[A.doff[k]];
   cnt[s] = n;
 }
@@ -179,11 +172,13 @@ __global__ __launch_bounds__(kThreads) void k_tlog_scatter_a(TlogArgs A, const u
                                                              u64* __restrict__ ots, u64* __restrict__ opre,
                                                              u64* __restrict__ olr, u32* __restrict__ oseg) {
   const u64 i = gid();
-  if (i >= A.na || !A.flag_a[i]) return;
+  if (i >= A.na) return;
   const u64 s = A.seg[i];
+  const u64 r = i - A.off[s];
+  if (r >= A.keep_a[s]) return;
   const u32 k = A.dptr[s];
   const Ent x{A.ts[i], A.pre[i], A.lr[i]};
-  u64 pos = noff[s] + (A.scan_a[i] - A.scan_a[A.off[s]]);
+  u64 pos = noff[s] + r;
   if (k != kNone) {
     const u64 lo = A.doff[k];
     pos += A.scan_b[lower_bound_entry(A.dts, A.dpre, A.dlr, lo, A.doff[k + 1], x, A.arena)] - A.scan_b[lo];
@@ -199,12 +194,13 @@ __global__ __launch_bounds__(kThreads) void k_tlog_scatter_b(TlogArgs A, const u
                                                              u64* __restrict__ olr, u32* __restrict__ oseg) {
   const u64 j = gid();
   if (j >= A.nb || !A.flag_b[j]) return;
-  const u32 k = seg_of(A.doff, A.nd, j);
+  const u32 k = A.dseg[j];
   const u64 s = A.slot[k];
   const Ent x{A.dts[j], A.dpre[j], A.dlr[j]};
   const u64 lo = A.off[s];
+  // state entries ordered before x all survive the cutoff (x itself does)
   const u64 p = lower_bound_entry(A.ts, A.pre, A.lr, lo, A.off[s + 1], x, A.arena);
-  const u64 pos = noff[s] + (A.scan_b[j] - A.scan_b[A.doff[k]]) + (A.scan_a[p] - A.scan_a[lo]);
+  const u64 pos = noff[s] + (A.scan_b[j] - A.scan_b[A.doff[k]]) + (p - lo);
   ots[pos] = x.t;
   opre[pos] = x.p;
   olr[pos] = x.l;
@@ -249,6 +245,11 @@ __global__ __launch_bounds__(kThreads) void k_tlog_gather(const u64* __restrict_
   }
 }
 
+__global__ __launch_bounds__(kThreads) void k_seg_starts(const u64* __restrict__ offs, u64 nseg, u32* __restrict__ out) {
+  const u64 k = gid();
+  if (k < nseg && offs[k] < offs[k + 1]) out[offs[k]] = (u32)k;
+}
+
 u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kThreads - 1) / kThreads); }
 
 #define LAUNCH(k, n, ...)                                                                          \
@@ -278,6 +279,20 @@ int32_t jy_scan_u64(jy_engine* eng, const u64* in, u64* out, u64 n) {
   void* t;
   JY_TRY(jy_scratch(eng, 15, tmp, &t));
   JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(t, tmp, in, out, (int)(n + 1), eng->stream));
+  return JY_OK;
+}
+
+// segment id of every item of a CSR (offs[0..nseg], n items): mark each
+// non-empty segment's first item, then an inclusive max-scan carries it on
+int32_t jy_seg_ids(jy_engine* eng, const u64* offs, u64 nseg, u64 n, u32* out) {
+  if (n == 0) return JY_OK;
+  JY_HIP(eng, hipMemsetAsync(out, 0, n * 4, eng->stream));
+  LAUNCH(k_seg_starts, nseg, offs, nseg, out);
+  size_t tmp = 0;
+  JY_HIP(eng, hipcub::DeviceScan::InclusiveScan(nullptr, tmp, out, out, hipcub::Max(), (int)n, eng->stream));
+  void* t;
+  JY_TRY(jy_scratch(eng, 15, tmp, &t));
+  JY_HIP(eng, hipcub::DeviceScan::InclusiveScan(t, tmp, out, out, hipcub::Max(), (int)n, eng->stream));
   return JY_OK;
 }
 
@@ -352,22 +367,22 @@ int32_t jy_tlog_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* dcut, 
   JY_TRY(jy_scratch(eng, 9, nd * 12, &p));
   A.cut = static_cast<u64*>(p);
   A.bad = reinterpret_cast<u32*>(A.cut + nd);
-  JY_TRY(jy_scratch(eng, 11, (na + 1) * 16, &p));
-  A.flag_a = static_cast<u64*>(p);
-  A.scan_a = A.flag_a + na + 1;
+  JY_TRY(jy_scratch(eng, 11, nk * 8, &p));
+  A.keep_a = static_cast<u64*>(p);
   JY_TRY(jy_scratch(eng, 12, (nent + 1) * 16, &p));
   A.flag_b = static_cast<u64*>(p);
   A.scan_b = A.flag_b + nent + 1;
   JY_TRY(jy_scratch(eng, 16, (nk + 1) * 8, &p));
   u64* cnt = static_cast<u64*>(p);
+  JY_TRY(jy_scratch(eng, 17, std::max<u64>(nent, 1) * 4, &p));
+  A.dseg = static_cast<const u32*>(p);
+  JY_TRY(jy_seg_ids(eng, doff, nd, nent, static_cast<u32*>(p)));
 
   JY_HIP(eng, hipMemsetAsync(A.dptr, 0xFF, nk * 4, eng->stream));
   LAUNCH(k_tlog_prep, nd, A);
   if (nent) LAUNCH(k_tlog_validate, nent, A);
   LAUNCH(k_tlog_drop_bad, nd, A, reinterpret_cast<unsigned long long*>(eng->skipped_dev));
-  LAUNCH(k_tlog_flag_a, na + 1, A);
   LAUNCH(k_tlog_flag_b, nent + 1, A);
-  JY_TRY(jy_scan_u64(eng, A.flag_a, A.scan_a, na));
   JY_TRY(jy_scan_u64(eng, A.flag_b, A.scan_b, nent));
   LAUNCH(k_tlog_sizes_out, nk + 1, A, cnt);
   JY_TRY(jy_scan_u64(eng, cnt, t.off[nxt], nk));

@@ -20,24 +20,41 @@ namespace {
 
 constexpr int kThreads = 256;
 
+// kUnroll keys per lane, lanes on consecutive keys for every unroll step:
+// all delta loads (coalesced, nontemporal) and the dependent state-ts
+// gathers of the kUnroll keys are in flight together before any decision.
+constexpr int kUnroll = 4;
+
 __global__ __launch_bounds__(kThreads) void k_treg_lww(u64* __restrict__ ts, u64* __restrict__ pre,
                                                        u64* __restrict__ lr, const uint8_t* __restrict__ arena,
                                                        const u32* __restrict__ slot, const u64* __restrict__ dts,
                                                        const u64* __restrict__ dpre, const u64* __restrict__ dlr,
                                                        u64 n) {
-  const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= n) return;
-  const u64 s = slot[i];
-  const u64 t = __builtin_nontemporal_load(dts + i);
-  const u64 p = __builtin_nontemporal_load(dpre + i);
-  const u64 l = __builtin_nontemporal_load(dlr + i);
-  const u64 t0 = ts[s];
-  bool win = t > t0;
-  if (t == t0) win = jy_value_cmp(p, l, pre[s], lr[s], arena) > 0;
-  if (win) {
-    ts[s] = t;
-    pre[s] = p;
-    lr[s] = l;
+  const u64 base = (u64)blockIdx.x * (kThreads * kUnroll) + threadIdx.x;
+  u64 s[kUnroll], t[kUnroll], p[kUnroll], l[kUnroll], t0[kUnroll];
+#pragma unroll
+  for (int u = 0; u < kUnroll; u++) {
+    const u64 i = base + (u64)u * kThreads;
+    if (i < n) {
+      s[u] = slot[i];
+      t[u] = __builtin_nontemporal_load(dts + i);
+      p[u] = __builtin_nontemporal_load(dpre + i);
+      l[u] = __builtin_nontemporal_load(dlr + i);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kUnroll; u++)
+    if (base + (u64)u * kThreads < n) t0[u] = ts[s[u]];
+#pragma unroll
+  for (int u = 0; u < kUnroll; u++) {
+    if (base + (u64)u * kThreads >= n) continue;
+    bool win = t[u] > t0[u];
+    if (t[u] == t0[u]) win = jy_value_cmp(p[u], l[u], pre[s[u]], lr[s[u]], arena) > 0;
+    if (win) {
+      ts[s[u]] = t[u];
+      pre[s[u]] = p[u];
+      lr[s[u]] = l[u];
+    }
   }
 }
 
@@ -74,7 +91,7 @@ int32_t jy_treg_grow(jy_engine* eng, u64 need) {
 int32_t jy_treg_merge(jy_engine* eng, u64 n, const u32* slot, const u64* ts, const u64* pre, const u64* lr) {
   if (n == 0) return JY_OK;
   TregState& t = eng->treg;
-  const u64 blocks = (n + kThreads - 1) / kThreads;
+  const u64 blocks = (n + kThreads * kUnroll - 1) / (kThreads * kUnroll);
   hipLaunchKernelGGL(k_treg_lww, dim3((u32)blocks), dim3(kThreads), 0, eng->stream, t.ts, t.pre, t.lr,
                      eng->arena[JY_TREG].p, slot, ts, pre, lr, n);
   JY_HIP(eng, hipGetLastError());

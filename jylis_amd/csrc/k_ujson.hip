@@ -58,17 +58,6 @@ __device__ __forceinline__ bool contains(const u64* __restrict__ a, u64 lo, u64 
   const u64 i = lower_bound(a, lo, hi, x);
   return i < hi && a[i] == x;
 }
-// segment of item j in a CSR offs[0..n]: the k with offs[k] <= j < offs[k+1]
-__device__ __forceinline__ u32 seg_of(const u64* __restrict__ offs, u64 n, u64 j) {
-  u64 lo = 0, hi = n;  // invariant: offs[lo] <= j, answer in [lo, hi)
-  while (hi - lo > 1) {
-    const u64 m = (lo + hi) >> 1;
-    if (offs[m] <= j) lo = m;
-    else hi = m;
-  }
-  return (u32)lo;
-}
-
 struct UjArgs {
   // state (current buffers)
   const u64* eoff;
@@ -92,6 +81,8 @@ struct UjArgs {
   const u64* dvv;
   const u64* dcoff;
   const u64* dcloud;
+  const u32* dseg;   // [nb] delta doc of each delta element
+  const u32* dcseg;  // [cb] delta doc of each delta cloud dot
   // merge temporaries
   u32* bad;     // [nd]
   u64* vvm;     // [nd][R] max(vv_A, vv_B)
@@ -155,11 +146,12 @@ __global__ __launch_bounds__(kThreads) void k_uj_prep(UjArgs A) {
 }
 
 // ---- P1: validate delta dots / cloud (strictly ascending, col < R, seq >= 1)
-__global__ __launch_bounds__(kThreads) void k_uj_validate(UjArgs A, const u64* __restrict__ offs,
-                                                          const u64* __restrict__ a, u64 n) {
+__global__ __launch_bounds__(kThreads) void k_uj_validate(UjArgs A, const u32* __restrict__ seg,
+                                                          const u64* __restrict__ offs, const u64* __restrict__ a,
+                                                          u64 n) {
   const u64 j = gid();
   if (j >= n) return;
-  const u32 k = seg_of(offs, A.nd, j);
+  const u32 k = seg[j];
   const u64 x = a[j];
   bool ok = dcol(x) < A.R && dseq(x) >= 1;
   if (j > offs[k] && a[j - 1] >= x) ok = false;
@@ -201,7 +193,7 @@ __global__ __launch_bounds__(kThreads) void k_uj_flag_b(UjArgs A) {
     A.flag_b[j] = 0;
     return;
   }
-  const u32 k = seg_of(A.deoff, A.nd, j);
+  const u32 k = A.dseg[j];
   const u64 s = A.slot[k];
   u64 keep = 0;
   if (A.dptr[s] == k) {
@@ -258,7 +250,7 @@ __global__ __launch_bounds__(kThreads) void k_uj_scatter_b(UjArgs A, const u64* 
                                                            u32* __restrict__ oseg) {
   const u64 j = gid();
   if (j >= A.nb || !A.flag_b[j]) return;
-  const u32 k = seg_of(A.deoff, A.nd, j);
+  const u32 k = A.dseg[j];
   const u64 s = A.slot[k];
   const u64 d = A.ddots[j];
   const u64 lo = A.eoff[s];
@@ -277,7 +269,7 @@ __global__ __launch_bounds__(kThreads) void k_uj_cloud_dedupe(UjArgs A) {
     A.cflag_b[j] = 0;
     return;
   }
-  const u32 k = seg_of(A.dcoff, A.nd, j);
+  const u32 k = A.dcseg[j];
   const u64 s = A.slot[k];
   u64 f = 0;
   if (A.dptr[s] == k) f = !contains(A.cloud, A.coff[s], A.coff[s + 1], A.dcloud[j]);
@@ -329,7 +321,7 @@ __global__ __launch_bounds__(kThreads) void k_uj_compact_b(UjArgs A) {
   }
   u64 keep = 0;
   if (A.cflag_b[j]) {
-    const u32 k = seg_of(A.dcoff, A.nd, j);
+    const u32 k = A.dcseg[j];
     const u64 s = A.slot[k];
     const u64 x = A.dcloud[j];
     const u32 c = dcol(x);
@@ -372,7 +364,7 @@ __global__ __launch_bounds__(kThreads) void k_uj_cscatter_b(UjArgs A, const u64*
                                                             u64* __restrict__ ocloud, u32* __restrict__ oseg) {
   const u64 j = gid();
   if (j >= A.cb || !A.keep_cb[j]) return;
-  const u32 k = seg_of(A.dcoff, A.nd, j);
+  const u32 k = A.dcseg[j];
   const u64 s = A.slot[k];
   const u64 x = A.dcloud[j];
   const u64 lo = A.coff[s];
@@ -574,10 +566,17 @@ int32_t jy_ujson_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* deoff
   u64* ne = static_cast<u64*>(p);
   u64* nc = ne + nk + 1;
 
+  JY_TRY(jy_scratch(eng, 17, std::max<u64>(nel, 1) * 4, &p));
+  A.dseg = static_cast<const u32*>(p);
+  JY_TRY(jy_seg_ids(eng, deoff, nd, nel, static_cast<u32*>(p)));
+  JY_TRY(jy_scratch(eng, 18, std::max<u64>(ncloud, 1) * 4, &p));
+  A.dcseg = static_cast<const u32*>(p);
+  JY_TRY(jy_seg_ids(eng, dcoff, nd, ncloud, static_cast<u32*>(p)));
+
   JY_HIP(eng, hipMemsetAsync(A.dptr, 0xFF, nk * 4, eng->stream));
   LAUNCH(k_uj_prep, nd, A);
-  if (nel) LAUNCH(k_uj_validate, nel, A, deoff, ddots, nel);
-  if (ncloud) LAUNCH(k_uj_validate, ncloud, A, dcoff, dcloud, ncloud);
+  if (nel) LAUNCH(k_uj_validate, nel, A, A.dseg, deoff, ddots, nel);
+  if (ncloud) LAUNCH(k_uj_validate, ncloud, A, A.dcseg, dcoff, dcloud, ncloud);
   LAUNCH(k_uj_drop_bad, nd, A, reinterpret_cast<unsigned long long*>(eng->skipped_dev));
   // elements
   LAUNCH(k_uj_flag_a, na + 1, A);
