@@ -119,30 +119,34 @@ __device__ __forceinline__ bool in_delta_ctx(const UjArgs& A, u32 k, u64 d) {
 
 __device__ __forceinline__ u64 gid() { return (u64)blockIdx.x * kThreads + threadIdx.x; }
 
-// ---- P0: per delta doc: scatter, vv max, vv validity --------------------------
+// ---- P0: per delta doc scatter; per (doc, column) vv init; per delta vv entry max
 __global__ __launch_bounds__(kThreads) void k_uj_prep(UjArgs A) {
   const u64 k = gid();
   if (k >= A.nd) return;
-  const u64 s = A.slot[k];
-  A.dptr[s] = (u32)k;
+  A.dptr[A.slot[k]] = (u32)k;
   A.bad[k] = 0;
-  u64* m = A.vvm + k * A.R;
-  u64* n = A.vvn + k * A.R;
-  for (u32 c = 0; c < A.R; c++) m[c] = A.vv[s * A.R + c];
-  bool ok = true;
-  u32 prev = 0;
-  for (u64 j = A.dvoff[k]; j < A.dvoff[k + 1]; j++) {
-    const u64 x = A.dvv[j];
-    const u32 c = dcol(x);
-    if (c >= A.R || (j > A.dvoff[k] && c <= prev)) {
-      ok = false;
-      break;
-    }
-    prev = c;
-    if (dseq(x) > m[c]) m[c] = dseq(x);
+}
+
+__global__ __launch_bounds__(kThreads) void k_uj_vv_init(UjArgs A) {
+  const u64 t = gid();
+  if (t >= A.nd * A.R) return;
+  const u64 k = t / A.R;
+  const u32 c = (u32)(t - k * A.R);
+  A.vvm[t] = A.vv[(u64)A.slot[k] * A.R + c];
+}
+
+// delta vv entries (col << 48 | n), strictly ascending columns per doc
+__global__ __launch_bounds__(kThreads) void k_uj_vv_delta(UjArgs A, const u32* __restrict__ vseg, u64 nvv) {
+  const u64 j = gid();
+  if (j >= nvv) return;
+  const u32 k = vseg[j];
+  const u64 x = A.dvv[j];
+  const u32 c = dcol(x);
+  if (c >= A.R || (j > A.dvoff[k] && dcol(A.dvv[j - 1]) >= c)) {
+    A.bad[k] = 1;
+    return;
   }
-  for (u32 c = 0; c < A.R; c++) n[c] = m[c];
-  if (!ok) A.bad[k] = 1;
+  __hip_atomic_fetch_max(&A.vvm[(u64)k * A.R + c], dseq(x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---- P1: validate delta dots / cloud (strictly ascending, col < R, seq >= 1)
@@ -573,8 +577,15 @@ int32_t jy_ujson_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* deoff
   A.dcseg = static_cast<const u32*>(p);
   JY_TRY(jy_seg_ids(eng, dcoff, nd, ncloud, static_cast<u32*>(p)));
 
+  JY_TRY(jy_scratch(eng, 19, std::max<u64>(nvv, 1) * 4, &p));
+  const u32* vseg = static_cast<const u32*>(p);
+  JY_TRY(jy_seg_ids(eng, dvoff, nd, nvv, static_cast<u32*>(p)));
+
   JY_HIP(eng, hipMemsetAsync(A.dptr, 0xFF, nk * 4, eng->stream));
   LAUNCH(k_uj_prep, nd, A);
+  LAUNCH(k_uj_vv_init, nd * R, A);
+  if (nvv) LAUNCH(k_uj_vv_delta, nvv, A, vseg, nvv);
+  JY_HIP(eng, hipMemcpyAsync(A.vvn, A.vvm, nd * R * 8, hipMemcpyDeviceToDevice, eng->stream));
   if (nel) LAUNCH(k_uj_validate, nel, A, A.dseg, deoff, ddots, nel);
   if (ncloud) LAUNCH(k_uj_validate, ncloud, A, A.dcseg, dcoff, dcloud, ncloud);
   LAUNCH(k_uj_drop_bad, nd, A, reinterpret_cast<unsigned long long*>(eng->skipped_dev));
