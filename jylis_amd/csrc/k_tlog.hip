@@ -8,27 +8,27 @@
 //
 // HBM layout: per type, CSR over slots -- off[kcap+1] (u64); entries SoA
 // ts / pre / lr (u64 each; value handle as in TREG: 8-byte big-endian prefix
-// + arena offset/length); cutoff[kcap].  Entries are double-buffered: a
-// converge rewrites the CSR into the other buffer.
+// + arena offset/length) and seg (u32 slot of the entry); cutoff[kcap].
+// Entries are double-buffered: a converge rewrites the CSR into the other
+// buffer.
 //
-// Parallel shape: a workgroup owns a tile of kTile consecutive slots (one
-// lane per slot).  The tile's state entries are one contiguous CSR range:
-// the workgroup stages it into LDS with coalesced loads, then every lane
-// merges its own log out of LDS against its delta segment (short, read from
-// HBM) and streams the result to the new CSR.  Two passes -- count (ts only,
-// value bytes on ties) and write -- around a scan of per-slot sizes.  A tile
-// whose state range exceeds the LDS budget reads HBM directly (same code).
-// Logs are short (state ~Geom(8) capped at 64, deltas ~Geom(2): SURVEY 8d
-// config 4), so lanes stay balanced; unbounded skew is UJSON's problem
-// (per-element design there).
+// Parallel shape: one thread per ENTRY (state or delta), coalesced, with
+// merge-path positions -- no per-key loops, so long or skewed logs cost the
+// same per entry as short ones:
+//   keep(state e)  = ts >= cutoff'
+//   keep(delta e)  = ts >= cutoff' and no equal entry in the state segment
+//   pos(e) = new_off[key] + #kept own-side entries before e
+//                         + #kept other-side entries ordered before e
+// the counts coming from exclusive scans of the keep flags and one binary
+// search (entry order, value bytes compared only on (ts, prefix) ties) into
+// the other side's sorted segment.  A delta segment that is not strictly
+// ordered is not a TLog: its key is left untouched and counted (the
+// reference swallows converge errors, repo_tlog.pony:67).
 //
-// A delta segment that is not strictly ordered is not a TLog: its key is
-// left untouched and counted (the reference swallows converge errors,
-// repo_tlog.pony:67).
-//
-// Roofline: HBM.  Count pass 8 B per input entry; write pass 24 B per input
-// entry + 24 B per output entry; per slot 8 B offsets in + 8 B out + 16 B
-// cutoff.
+// Roofline: HBM.  Per input entry: 24 B read (+4 B seg, state side) and
+// 28 B written per output entry; per key 16 B offsets + 16 B cutoff; keep
+// flags and their scans add 24 B per input entry (u64 flag, scan write +
+// read); see DESIGN.md.
 
 #include <hipcub/hipcub.hpp>
 
@@ -38,15 +38,53 @@
 
 namespace {
 
-constexpr int kTile = 128;      // slots (lanes) per workgroup
-constexpr u32 kStage = 2048;    // state entries staged in LDS per tile (48 KiB)
+constexpr int kThreads = 256;
 constexpr u32 kNone = 0xFFFFFFFFu;
 
+__device__ __forceinline__ u64 gid() { return (u64)blockIdx.x * kThreads + threadIdx.x; }
+
+// > 0 if (ta, pa, la) is ordered before (tb, pb, lb): later ts, then greater value
 __device__ __forceinline__ int entry_cmp(u64 ta, u64 pa, u64 la, u64 tb, u64 pb, u64 lb,
                                          const uint8_t* __restrict__ arena) {
   if (ta != tb) return ta > tb ? 1 : -1;
   return jy_value_cmp(pa, la, pb, lb, arena);
 }
+
+struct Ent {
+  u64 t, p, l;
+};
+
+// > 0 if log entry m is ordered before x; value handles are read only on a
+// timestamp tie
+__device__ __forceinline__ int cmp_at(const u64* __restrict__ ts, const u64* __restrict__ pre,
+                                      const u64* __restrict__ lr, u64 m, const Ent& x,
+                                      const uint8_t* __restrict__ arena) {
+  const u64 t = ts[m];
+  if (t != x.t) return t > x.t ? 1 : -1;
+  return jy_value_cmp(pre[m], lr[m], x.p, x.l, arena);
+}
+
+// first index in [lo, hi) of a sorted log whose entry is NOT ordered before x
+__device__ __forceinline__ u64 lower_bound_entry(const u64* __restrict__ ts, const u64* __restrict__ pre,
+                                                 const u64* __restrict__ lr, u64 lo, u64 hi, const Ent& x,
+                                                 const uint8_t* __restrict__ arena) {
+  while (lo < hi) {
+    const u64 m = (lo + hi) >> 1;
+    if (cmp_at(ts, pre, lr, m, x, arena) > 0) lo = m + 1;
+    else hi = m;
+  }
+  return lo;
+}
+
+// per-key record for the state-side scatter: one cache line instead of six
+// scattered per-key arrays
+struct KeyInfo {
+  u64 shift;     // new_off[s] - off[s]
+  u64 keep_end;  // off[s] + surviving prefix length
+  u64 blo, bhi;  // delta segment (empty if none)
+  u64 scan_lo;   // scan_b[blo]
+  u64 pad;
+};
 
 struct TlogArgs {
   // state (current buffer)
@@ -54,142 +92,181 @@ struct TlogArgs {
   const u64* ts;
   const u64* pre;
   const u64* lr;
+  const u32* seg;
   u64* cutoff;
-  u64 nkeys;
+  u64 nkeys, na;
   // delta batch
-  u64 nd;
+  u64 nd, nb;
   const u32* slot;
-  const u32* dptr;
+  u32* dptr;
   const u64* dcut;
   const u64* doff;
   const u64* dts;
   const u64* dpre;
   const u64* dlr;
   const uint8_t* arena;
-  u32* bad;  // [nd] malformed delta segment (set by the count pass)
+  const u32* dseg;  // [nb] delta key of each delta entry
+  // temporaries
+  u32* bad;     // [nd]
+  u64* cut;     // [nd] merged cutoff
+  u64* keep_a;  // [nkeys] surviving state entries: a prefix of every log
+  u64* flag_b;
+  u64* scan_b;
+  KeyInfo* info;  // [nkeys]
 };
 
-__global__ __launch_bounds__(256) void k_scatter_ptr(u32* __restrict__ dptr, const u32* __restrict__ slot, u64 n) {
-  const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) dptr[slot[i]] = (u32)i;
+__global__ __launch_bounds__(kThreads) void k_tlog_prep(TlogArgs A) {
+  const u64 k = gid();
+  if (k >= A.nd) return;
+  const u64 s = A.slot[k];
+  A.dptr[s] = (u32)k;
+  A.bad[k] = 0;
+  const u64 cs = A.cutoff[s], cd = A.dcut[k];
+  A.cut[k] = cs > cd ? cs : cd;
 }
 
-// kWrite = false: count pass (cnt[s]); true: write pass (entries + cutoff)
-template <bool kWrite>
-__global__ __launch_bounds__(kTile) void k_tlog_tile(TlogArgs A, u64* __restrict__ cnt, const u64* __restrict__ noff,
-                                                     u64* __restrict__ ots, u64* __restrict__ opre,
-                                                     u64* __restrict__ olr, unsigned long long* __restrict__ skipped) {
-  __shared__ u64 sts[kStage];
-  __shared__ u64 spre[kWrite ? kStage : 1];
-  __shared__ u64 slr[kWrite ? kStage : 1];
-  const u64 s0 = (u64)blockIdx.x * kTile;
-  const u64 s = s0 + threadIdx.x;
-  const u64 s1 = min(s0 + (u64)kTile, A.nkeys);
-  const u64 a0 = A.off[s0], a1 = A.off[s1];
-  const bool staged = (a1 - a0) <= kStage;
-  if (staged) {
-    for (u64 j = threadIdx.x; j < a1 - a0; j += kTile) {
-      sts[j] = A.ts[a0 + j];
-      if (kWrite) {
-        spre[j] = A.pre[a0 + j];
-        slr[j] = A.lr[a0 + j];
-      }
-    }
+__global__ __launch_bounds__(kThreads) void k_tlog_validate(TlogArgs A) {
+  const u64 j = gid();
+  if (j >= A.nb) return;
+  const u32 k = A.dseg[j];
+  if (j > A.doff[k] &&
+      entry_cmp(A.dts[j - 1], A.dpre[j - 1], A.dlr[j - 1], A.dts[j], A.dpre[j], A.dlr[j], A.arena) <= 0)
+    A.bad[k] = 1;
+}
+
+__global__ __launch_bounds__(kThreads) void k_tlog_drop_bad(TlogArgs A, unsigned long long* __restrict__ skipped) {
+  const u64 k = gid();
+  if (k >= A.nd) return;
+  if (A.bad[k]) {
+    A.dptr[A.slot[k]] = kNone;
+    atomicAdd(skipped, 1ull);
   }
-  __syncthreads();
-  if (!kWrite && s == A.nkeys) cnt[s] = 0;  // scan sentinel
-  if (s >= A.nkeys) return;
-  // this lane's state log: LDS when staged, else HBM
-  const u64 lo = A.off[s], hi0 = A.off[s + 1];
-  const u64* ta = staged ? sts + (lo - a0) : A.ts + lo;
-  const u64* pa = kWrite ? (staged ? spre + (lo - a0) : A.pre + lo) : A.pre + lo;
-  const u64* la = kWrite ? (staged ? slr + (lo - a0) : A.lr + lo) : A.lr + lo;
-  u64 na = hi0 - lo;
+}
+
+__global__ __launch_bounds__(kThreads) void k_tlog_flag_b(TlogArgs A) {
+  const u64 j = gid();
+  if (j > A.nb) return;
+  if (j == A.nb) {
+    A.flag_b[j] = 0;
+    return;
+  }
+  const u32 k = A.dseg[j];
+  const u64 s = A.slot[k];
+  u64 keep = 0;
+  if (A.dptr[s] == k && A.dts[j] >= A.cut[k]) {
+    const Ent x{A.dts[j], A.dpre[j], A.dlr[j]};
+    const u64 hi = A.off[s + 1];
+    const u64 p = lower_bound_entry(A.ts, A.pre, A.lr, A.off[s], hi, x, A.arena);
+    keep = !(p < hi && cmp_at(A.ts, A.pre, A.lr, p, x, A.arena) == 0);
+  }
+  A.flag_b[j] = keep;
+}
+
+__global__ __launch_bounds__(kThreads) void k_tlog_sizes_out(TlogArgs A, u64* __restrict__ cnt) {
+  const u64 s = gid();
+  if (s > A.nkeys) return;
+  if (s == A.nkeys) {
+    cnt[s] = 0;
+    return;
+  }
   const u32 k = A.dptr[s];
-  u64 b = 0, nb = 0, c = A.cutoff[s];
-  bool merge = false;
+  const u64 lo = A.off[s];
+  u64 hi = A.off[s + 1];
   if (k != kNone) {
-    b = A.doff[k];
-    nb = A.doff[k + 1] - b;
-    if (!kWrite) {
-      bool ok = true;
-      for (u64 j = 1; j < nb && ok; j++)
-        ok = entry_cmp(A.dts[b + j - 1], A.dpre[b + j - 1], A.dlr[b + j - 1], A.dts[b + j], A.dpre[b + j],
-                       A.dlr[b + j], A.arena) > 0;
-      if (!ok) {
-        A.bad[k] = 1;
-        atomicAdd(skipped, 1ull);
-      }
-      merge = ok;
-    } else {
-      merge = !A.bad[k];
+    // entries are in non-increasing ts order: the cutoff drops a suffix
+    const u64 c = A.cut[k];
+    u64 a = lo;
+    while (a < hi) {
+      const u64 m = (a + hi) >> 1;
+      if (A.ts[m] >= c) a = m + 1;
+      else hi = m;
     }
+    hi = a;
   }
-  if (merge) {
-    const u64 cd = A.dcut[k];
-    c = c > cd ? c : cd;
-    while (na > 0 && ta[na - 1] < c) na--;  // the cutoff drops a suffix
-    while (nb > 0 && A.dts[b + nb - 1] < c) nb--;
-  } else {
-    nb = 0;
-  }
-  u64 o = kWrite ? noff[s] : 0;
-  u64 n = 0;
-  u64 i = 0, j = 0;
-  while (i < na || j < nb) {
-    int cmp;
-    if (j >= nb) cmp = 1;
-    else if (i >= na) cmp = -1;
-    else {
-      const u64 x = ta[i], y = A.dts[b + j];
-      cmp = x != y ? (x > y ? 1 : -1) : jy_value_cmp(pa[i], la[i], A.dpre[b + j], A.dlr[b + j], A.arena);
-    }
-    if (kWrite) {
-      if (cmp >= 0) {
-        ots[o] = ta[i];
-        opre[o] = pa[i];
-        olr[o] = la[i];
-      } else {
-        ots[o] = A.dts[b + j];
-        opre[o] = A.dpre[b + j];
-        olr[o] = A.dlr[b + j];
-      }
-      o++;
-    }
-    n++;
-    if (cmp > 0) i++;
-    else if (cmp < 0) j++;
-    else {  // (ts, value) duplicate: the state's copy stays
-      i++;
-      j++;
-    }
-  }
-  if (!kWrite) cnt[s] = n;
-  if (kWrite && merge) A.cutoff[s] = c;
+  A.keep_a[s] = hi - lo;
+  u64 n = hi - lo;
+  if (k != kNone) n += A.scan_b[A.doff[k + 1]] - A.scan_b[A.doff[k]];
+  cnt[s] = n;
 }
 
-__global__ __launch_bounds__(256) void k_fill_tail(u64* __restrict__ off, u64 from, u64 to) {
+__global__ __launch_bounds__(kThreads) void k_tlog_info(TlogArgs A, const u64* __restrict__ noff) {
+  const u64 s = gid();
+  if (s >= A.nkeys) return;
+  const u32 k = A.dptr[s];
+  KeyInfo I;
+  I.shift = noff[s] - A.off[s];
+  I.keep_end = A.off[s] + A.keep_a[s];
+  I.blo = k == kNone ? 0 : A.doff[k];
+  I.bhi = k == kNone ? 0 : A.doff[k + 1];
+  I.scan_lo = A.scan_b[I.blo];
+  I.pad = 0;
+  A.info[s] = I;
+}
+
+__global__ __launch_bounds__(kThreads) void k_tlog_scatter_a(TlogArgs A, const u64* __restrict__ noff,
+                                                             u64* __restrict__ ots, u64* __restrict__ opre,
+                                                             u64* __restrict__ olr, u32* __restrict__ oseg) {
+  const u64 i = gid();
+  if (i >= A.na) return;
+  const u32 s = A.seg[i];
+  const KeyInfo I = A.info[s];
+  if (i >= I.keep_end) return;
+  const Ent x{A.ts[i], A.pre[i], A.lr[i]};
+  u64 pos = i + I.shift;
+  if (I.bhi > I.blo) pos += A.scan_b[lower_bound_entry(A.dts, A.dpre, A.dlr, I.blo, I.bhi, x, A.arena)] - I.scan_lo;
+  (void)noff;
+  ots[pos] = x.t;
+  opre[pos] = x.p;
+  olr[pos] = x.l;
+  oseg[pos] = (u32)s;
+}
+
+__global__ __launch_bounds__(kThreads) void k_tlog_scatter_b(TlogArgs A, const u64* __restrict__ noff,
+                                                             u64* __restrict__ ots, u64* __restrict__ opre,
+                                                             u64* __restrict__ olr, u32* __restrict__ oseg) {
+  const u64 j = gid();
+  if (j >= A.nb || !A.flag_b[j]) return;
+  const u32 k = A.dseg[j];
+  const u64 s = A.slot[k];
+  const Ent x{A.dts[j], A.dpre[j], A.dlr[j]};
+  const u64 lo = A.off[s];
+  // state entries ordered before x all survive the cutoff (x itself does)
+  const u64 p = lower_bound_entry(A.ts, A.pre, A.lr, lo, A.off[s + 1], x, A.arena);
+  const u64 pos = noff[s] + (A.scan_b[j] - A.scan_b[A.doff[k]]) + (p - lo);
+  ots[pos] = x.t;
+  opre[pos] = x.p;
+  olr[pos] = x.l;
+  oseg[pos] = (u32)s;
+}
+
+__global__ __launch_bounds__(kThreads) void k_tlog_cut_store(TlogArgs A) {
+  const u64 k = gid();
+  if (k >= A.nd || A.bad[k]) return;
+  A.cutoff[A.slot[k]] = A.cut[k];
+}
+
+__global__ __launch_bounds__(kThreads) void k_fill_tail(u64* __restrict__ off, u64 from, u64 to) {
   // off[from+1 .. to] = off[from]  (new, empty slots)
-  const u64 i = from + 1 + (u64)blockIdx.x * 256 + threadIdx.x;
+  const u64 i = from + 1 + gid();
   if (i <= to) off[i] = off[from];
 }
 
-__global__ __launch_bounds__(256) void k_tlog_sizes(const u64* __restrict__ off, const u64* __restrict__ cutoff,
-                                                    const u32* __restrict__ slots, u64 n, u64* __restrict__ len,
-                                                    u64* __restrict__ cut) {
-  const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(kThreads) void k_tlog_sizes(const u64* __restrict__ off, const u64* __restrict__ cutoff,
+                                                         const u32* __restrict__ slots, u64 n, u64* __restrict__ len,
+                                                         u64* __restrict__ cut) {
+  const u64 i = gid();
   if (i >= n) return;
   const u64 s = slots[i];
   len[i] = off[s + 1] - off[s];
   cut[i] = cutoff[s];
 }
 
-__global__ __launch_bounds__(256) void k_tlog_gather(const u64* __restrict__ off, const u64* __restrict__ ts,
-                                                     const u64* __restrict__ pre, const u64* __restrict__ lr,
-                                                     const u32* __restrict__ slots, const u64* __restrict__ ooff,
-                                                     u64 n, u64* __restrict__ ots, u64* __restrict__ opre,
-                                                     u64* __restrict__ olr) {
-  const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(kThreads) void k_tlog_gather(const u64* __restrict__ off, const u64* __restrict__ ts,
+                                                          const u64* __restrict__ pre, const u64* __restrict__ lr,
+                                                          const u32* __restrict__ slots, const u64* __restrict__ ooff,
+                                                          u64 n, u64* __restrict__ ots, u64* __restrict__ opre,
+                                                          u64* __restrict__ olr) {
+  const u64 i = gid();
   if (i >= n) return;
   const u64 s = slots[i];
   u64 o = ooff[i];
@@ -200,16 +277,16 @@ __global__ __launch_bounds__(256) void k_tlog_gather(const u64* __restrict__ off
   }
 }
 
-__global__ __launch_bounds__(256) void k_seg_starts(const u64* __restrict__ offs, u64 nseg, u32* __restrict__ out) {
-  const u64 k = (u64)blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(kThreads) void k_seg_starts(const u64* __restrict__ offs, u64 nseg, u32* __restrict__ out) {
+  const u64 k = gid();
   if (k < nseg && offs[k] < offs[k + 1]) out[offs[k]] = (u32)k;
 }
 
-u32 blocks_for(u64 n, u64 per = 256) { return (u32)std::max<u64>(1, (n + per - 1) / per); }
+u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kThreads - 1) / kThreads); }
 
 #define LAUNCH(k, n, ...)                                                                          \
   do {                                                                                             \
-    hipLaunchKernelGGL(k, dim3(blocks_for(n)), dim3(256), 0, eng->stream, __VA_ARGS__);          \
+    hipLaunchKernelGGL(k, dim3(blocks_for(n)), dim3(kThreads), 0, eng->stream, __VA_ARGS__);     \
     JY_HIP(eng, hipGetLastError());                                                                \
   } while (0)
 
@@ -256,6 +333,7 @@ static int32_t ensure_entries(jy_engine* eng, int buf, u64 need) {
   if (need <= t.ecap[buf] && t.ts[buf]) return JY_OK;
   const u64 nc = std::max<u64>(std::max<u64>(need + need / 2, eng->cfg.entry_capacity[JY_TLOG]), 1024);
   for (u64** p : {&t.ts[buf], &t.pre[buf], &t.lr[buf]}) JY_TRY(realloc_dead(eng, reinterpret_cast<void**>(p), nc * 8));
+  JY_TRY(realloc_dead(eng, reinterpret_cast<void**>(&t.seg[buf]), nc * 4));
   t.ecap[buf] = nc;
   return JY_OK;
 }
@@ -264,7 +342,7 @@ int32_t jy_tlog_grow(jy_engine* eng, u64 need) {
   TlogState& t = eng->tlog;
   if (need <= t.kcap && t.cutoff) return JY_OK;
   u64 nk = std::max<u64>(need, t.kcap ? t.kcap * 2 : need);
-  nk = std::max<u64>((nk + 127) & ~127ull, 128);  // whole tiles
+  nk = std::max<u64>((nk + 63) & ~63ull, 64);
   void* c = t.cutoff;
   JY_TRY(jy_realloc(eng, &c, t.kcap * 8, nk * 8, true));
   t.cutoff = static_cast<u64*>(c);
@@ -302,9 +380,12 @@ int32_t jy_tlog_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* dcut, 
   A.ts = t.ts[cur];
   A.pre = t.pre[cur];
   A.lr = t.lr[cur];
+  A.seg = t.seg[cur];
   A.cutoff = t.cutoff;
   A.nkeys = nk;
+  A.na = na;
   A.nd = nd;
+  A.nb = nent;
   A.slot = slot;
   A.dcut = dcut;
   A.doff = doff;
@@ -312,24 +393,37 @@ int32_t jy_tlog_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* dcut, 
   A.dpre = dpre;
   A.dlr = dlr;
   A.arena = eng->arena[JY_TLOG].p;
-  void *dptr, *bad, *cnt;
-  JY_TRY(jy_scratch(eng, 8, nk * 4, &dptr));
-  JY_TRY(jy_scratch(eng, 9, nd * 4, &bad));
-  JY_TRY(jy_scratch(eng, 16, (nk + 1) * 8, &cnt));
-  A.dptr = static_cast<const u32*>(dptr);
-  A.bad = static_cast<u32*>(bad);
-  JY_HIP(eng, hipMemsetAsync(dptr, 0xFF, nk * 4, eng->stream));
-  JY_HIP(eng, hipMemsetAsync(bad, 0, nd * 4, eng->stream));
-  LAUNCH(k_scatter_ptr, nd, static_cast<u32*>(dptr), slot, nd);
-  auto* skipped = reinterpret_cast<unsigned long long*>(eng->skipped_dev);
-  const u32 tiles = blocks_for(nk + 1, kTile);  // +1: the scan sentinel lane
-  hipLaunchKernelGGL(k_tlog_tile<false>, dim3(tiles), dim3(kTile), 0, eng->stream, A, static_cast<u64*>(cnt),
-                     (const u64*)nullptr, (u64*)nullptr, (u64*)nullptr, (u64*)nullptr, skipped);
-  JY_HIP(eng, hipGetLastError());
-  JY_TRY(jy_scan_u64(eng, static_cast<const u64*>(cnt), t.off[nxt], nk));
-  hipLaunchKernelGGL(k_tlog_tile<true>, dim3(blocks_for(nk, kTile)), dim3(kTile), 0, eng->stream, A,
-                     static_cast<u64*>(cnt), t.off[nxt], t.ts[nxt], t.pre[nxt], t.lr[nxt], skipped);
-  JY_HIP(eng, hipGetLastError());
+  void* p;
+  JY_TRY(jy_scratch(eng, 8, nk * 4, &p));
+  A.dptr = static_cast<u32*>(p);
+  JY_TRY(jy_scratch(eng, 9, nd * 12, &p));
+  A.cut = static_cast<u64*>(p);
+  A.bad = reinterpret_cast<u32*>(A.cut + nd);
+  JY_TRY(jy_scratch(eng, 11, nk * 8, &p));
+  A.keep_a = static_cast<u64*>(p);
+  JY_TRY(jy_scratch(eng, 12, (nent + 1) * 16, &p));
+  A.flag_b = static_cast<u64*>(p);
+  A.scan_b = A.flag_b + nent + 1;
+  JY_TRY(jy_scratch(eng, 16, (nk + 1) * 8, &p));
+  u64* cnt = static_cast<u64*>(p);
+  JY_TRY(jy_scratch(eng, 18, nk * sizeof(KeyInfo), &p));
+  A.info = static_cast<KeyInfo*>(p);
+  JY_TRY(jy_scratch(eng, 17, std::max<u64>(nent, 1) * 4, &p));
+  A.dseg = static_cast<const u32*>(p);
+  JY_TRY(jy_seg_ids(eng, doff, nd, nent, static_cast<u32*>(p)));
+
+  JY_HIP(eng, hipMemsetAsync(A.dptr, 0xFF, nk * 4, eng->stream));
+  LAUNCH(k_tlog_prep, nd, A);
+  if (nent) LAUNCH(k_tlog_validate, nent, A);
+  LAUNCH(k_tlog_drop_bad, nd, A, reinterpret_cast<unsigned long long*>(eng->skipped_dev));
+  LAUNCH(k_tlog_flag_b, nent + 1, A);
+  JY_TRY(jy_scan_u64(eng, A.flag_b, A.scan_b, nent));
+  LAUNCH(k_tlog_sizes_out, nk + 1, A, cnt);
+  JY_TRY(jy_scan_u64(eng, cnt, t.off[nxt], nk));
+  LAUNCH(k_tlog_info, nk, A, t.off[nxt]);
+  if (na) LAUNCH(k_tlog_scatter_a, na, A, t.off[nxt], t.ts[nxt], t.pre[nxt], t.lr[nxt], t.seg[nxt]);
+  if (nent) LAUNCH(k_tlog_scatter_b, nent, A, t.off[nxt], t.ts[nxt], t.pre[nxt], t.lr[nxt], t.seg[nxt]);
+  LAUNCH(k_tlog_cut_store, nd, A);
   // publish the new total for the next call (read back asynchronously)
   JY_HIP(eng, hipMemcpyAsync(eng->pin_total, t.off[nxt] + nk, 8, hipMemcpyDeviceToHost, eng->stream));
   JY_HIP(eng, hipEventRecord(eng->total_ready, eng->stream));
