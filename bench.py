@@ -60,6 +60,8 @@ def other_mode(args, rank, world, local, dist):
     if args.keys == 16 * 1024 * 1024:
         args.keys = 0  # per-mode default size
     res = bench_modes.MODES[args.type](args, eng, dev, dist, rank, world)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = bench_modes.cpu_baseline(args.type)
     if rank == 0:
         line = {"metric": f"{args.type.upper()} delta converge throughput (SURVEY 8d)", "value": res.pop("value"),
                 "unit": res.pop("unit_of_work") + "s/s", "n_gpus": world, "steps": args.steps,

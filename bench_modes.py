@@ -46,6 +46,85 @@ def _max_over_ranks(x, dist, dev):
     return float(t[0])
 
 
+def cpu_baseline(mode, rounds=2):
+    """The oracle (oracle/jy_oracle.cpp: the reference's Map[String, CRDT] +
+    per-key converge loop, repo_manager.pony:92-93) timed single-threaded on a
+    bounded sample of the same synthetic stream; only the converge of the
+    delta batches is timed (decode excluded).  Units match the GPU mode."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "oracle"))
+    import oracle as O
+    from jylis_amd import synth as S
+    t_conv, units, sample = 0.0, 0, ""
+    if mode == "gcount":
+        K, R = 262144, 16
+        seed = S.BASE_SEED + 1
+        kb, ko = S.counter_keys(K, prefix=b"g", width=7)
+        rids = S.replica_ids(R, seed)
+        st = S.counter_state_np(K, R, 1, seed, wrap_frac=False)[0]
+        repo = O.Repo(O.GCOUNT, 1)
+        for t in S.counter_batch_tables(st, rids, (kb, ko)):
+            repo.converge(t)
+        cur = st
+        for r in range(rounds):
+            cur = S.counter_delta_np(cur, r, seed)
+            bs = [O.Batch(O.GCOUNT, t) for t in S.counter_batch_tables(cur, rids, (kb, ko))]
+            t0 = time.perf_counter()
+            for b in bs:
+                repo.converge(b)
+            t_conv += time.perf_counter() - t0
+        units = K * R * rounds
+        sample = f"GCOUNT {K} keys x {R} replicas x {rounds} rounds of {R} peer batches"
+    elif mode == "treg":
+        K = 1 << 20
+        rng = np.random.default_rng(S.BASE_SEED + 3)
+        from bench_modes import _key_strings, _treg_values
+        kb, ko = _key_strings(np.arange(K, dtype=np.uint64), b"t")
+        repo = O.Repo(O.TREG)
+        bs = []
+        for j in range(rounds + 1):
+            vb, vo = _treg_values(rng, K)
+            bs.append(O.Batch(O.TREG, {"key_bytes": kb, "key_offs": ko, "val_bytes": vb, "val_offs": vo,
+                                       "ts": rng.integers(0, 1 << 20, K).astype(np.uint64)}))
+        repo.converge(bs[0])
+        t0 = time.perf_counter()
+        for b in bs[1:]:
+            repo.converge(b)
+        t_conv = time.perf_counter() - t0
+        units = K * rounds
+        sample = f"TREG {K} keys x {rounds} delta batches"
+    elif mode == "tlog":
+        K = 1 << 18
+        st, dl = S.tlog_tables(K, seed=S.BASE_SEED + 4, rounds=rounds)
+        repo = O.Repo(O.TLOG)
+        repo.converge(st)
+        n_state = len(st["ts"])
+        for d in dl:
+            b = O.Batch(O.TLOG, d)
+            units += n_state + len(d["ts"])
+            t0 = time.perf_counter()
+            repo.converge(b)
+            t_conv += time.perf_counter() - t0
+            n_state = len(repo.state()["ts"])
+        sample = f"TLOG {K} logs, {rounds} delta batches"
+    elif mode == "ujson":
+        D = 1 << 17
+        st, dl = S.ujson_tables(D, seed=S.BASE_SEED + 5, rounds=rounds, R=16)
+        repo = O.Repo(O.UJSON, 1)
+        repo.converge(st)
+        n_el = len(st["elems"])
+        for d in dl:
+            b = O.Batch(O.UJSON, d)
+            units += 2 * n_el + len(d["elems"])
+            t0 = time.perf_counter()
+            repo.converge(b)
+            t_conv += time.perf_counter() - t0
+        sample = f"UJSON {D} docs, Zipf(1.1), {rounds} delta batches"
+    return {"value": units / t_conv, "unit": "same as value", "cores": 1, "kind": "port",
+            "sample": f"{sample} ({units} units, {t_conv:.2f} s converge, oracle/jy_oracle.cpp, 1 thread)"}
+
+
 def _to_dev(a, dev, dtype=None):
     import torch
     a = np.ascontiguousarray(a)
