@@ -25,6 +25,57 @@ constexpr int kThreads = 256;
 // gathers of the kUnroll keys are in flight together before any decision.
 constexpr int kUnroll = 4;
 
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void lww_one(u64* __restrict__ ts, u64* __restrict__ pre, u64* __restrict__ lr,
+                                        const uint8_t* __restrict__ arena, u64 s, u64 t, u64 p, u64 l, u64 t0) {
+  bool win = t > t0;
+  if (t == t0) win = jy_value_cmp(p, l, pre[s], lr[s], arena) > 0;
+  if (win) {
+    ts[s] = t;
+    pre[s] = p;
+    lr[s] = l;
+  }
+}
+
+// Vector form: every lane owns PAIRS of consecutive delta entries, so the
+// delta streams move 16 B per lane per load (8 B for the slot pair).  n is
+// even and the delta arrays are 16-B aligned (checked by the launcher).
+__global__ __launch_bounds__(kThreads) void k_treg_lww_v2(u64* __restrict__ ts, u64* __restrict__ pre,
+                                                          u64* __restrict__ lr, const uint8_t* __restrict__ arena,
+                                                          const u32* __restrict__ slot, const u64* __restrict__ dts,
+                                                          const u64* __restrict__ dpre,
+                                                          const u64* __restrict__ dlr, u64 npairs) {
+  constexpr int U = 2;  // pairs per lane
+  const u64 base = (u64)blockIdx.x * (kThreads * U) + threadIdx.x;
+  u32x2 s[U];
+  u64x2 t[U], p[U], l[U], t0[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const u64 q = base + (u64)u * kThreads;
+    if (q < npairs) {
+      s[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(slot) + q);
+      t[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(dts) + q);
+      p[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(dpre) + q);
+      l[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(dlr) + q);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    if (base + (u64)u * kThreads < npairs) {
+      t0[u].x = ts[s[u].x];
+      t0[u].y = ts[s[u].y];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    if (base + (u64)u * kThreads >= npairs) continue;
+    lww_one(ts, pre, lr, arena, s[u].x, t[u].x, p[u].x, l[u].x, t0[u].x);
+    lww_one(ts, pre, lr, arena, s[u].y, t[u].y, p[u].y, l[u].y, t0[u].y);
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void k_treg_lww(u64* __restrict__ ts, u64* __restrict__ pre,
                                                        u64* __restrict__ lr, const uint8_t* __restrict__ arena,
                                                        const u32* __restrict__ slot, const u64* __restrict__ dts,
@@ -91,9 +142,21 @@ int32_t jy_treg_grow(jy_engine* eng, u64 need) {
 int32_t jy_treg_merge(jy_engine* eng, u64 n, const u32* slot, const u64* ts, const u64* pre, const u64* lr) {
   if (n == 0) return JY_OK;
   TregState& t = eng->treg;
-  const u64 blocks = (n + kThreads * kUnroll - 1) / (kThreads * kUnroll);
-  hipLaunchKernelGGL(k_treg_lww, dim3((u32)blocks), dim3(kThreads), 0, eng->stream, t.ts, t.pre, t.lr,
-                     eng->arena[JY_TREG].p, slot, ts, pre, lr, n);
+  auto al16 = [](const void* q) { return reinterpret_cast<uintptr_t>(q) % 16 == 0; };
+  u64 done = 0;
+  if (n >= 2 && al16(ts) && al16(pre) && al16(lr) && reinterpret_cast<uintptr_t>(slot) % 8 == 0) {
+    const u64 npairs = n / 2;
+    const u64 blocks = (npairs + kThreads * 2 - 1) / (kThreads * 2);
+    hipLaunchKernelGGL(k_treg_lww_v2, dim3((u32)blocks), dim3(kThreads), 0, eng->stream, t.ts, t.pre, t.lr,
+                       eng->arena[JY_TREG].p, slot, ts, pre, lr, npairs);
+    done = npairs * 2;
+  }
+  if (done < n) {
+    const u64 rest = n - done;
+    const u64 blocks = (rest + kThreads * kUnroll - 1) / (kThreads * kUnroll);
+    hipLaunchKernelGGL(k_treg_lww, dim3((u32)blocks), dim3(kThreads), 0, eng->stream, t.ts, t.pre, t.lr,
+                       eng->arena[JY_TREG].p, slot + done, ts + done, pre + done, lr + done, rest);
+  }
   JY_HIP(eng, hipGetLastError());
   return JY_OK;
 }
