@@ -74,6 +74,18 @@ SIGNATURES = {
     "jy_treg_converge_routed": (I32, [P, U32, P, P, P, P]),
 }
 
+# include/jylis_host.h: the C++ host mirror (Database / RepoManagerCore / Repo*)
+HOST_SIGNATURES = {
+    "jyh_db_create": (I32, [I32, U64, P]),
+    "jyh_db_destroy": (None, [P]),
+    "jyh_db_error": (C.c_char_p, [P]),
+    "jyh_db_apply": (I32, [P, U32, P, P, P, U64, P]),
+    "jyh_db_flush": (I32, [P, P, P]),
+    "jyh_db_converge": (I32, [P, P, U64]),
+    "jyh_db_shutdown": (I32, [P]),
+    "jyh_free": (None, [P]),
+}
+
 _lib = None
 
 
@@ -96,7 +108,7 @@ def load(path=LIB_PATH):
     except ImportError:
         pass
     lib = C.CDLL(path)
-    for name, (res, args) in SIGNATURES.items():
+    for name, (res, args) in list(SIGNATURES.items()) + list(HOST_SIGNATURES.items()):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -42,6 +42,15 @@ def test_python_binding_covers_the_header():
     assert set(declared_symbols()) == set(_lib.SIGNATURES)
 
 
+def test_host_mirror_symbols(lib):
+    """include/jylis_host.h (the C++ Database / RepoManagerCore mirror)"""
+    from jylis_amd import _lib
+    text = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "jylis_host.h")).read(), flags=re.S)
+    syms = sorted(set(re.findall(r"\b(jyh_[a-z0-9_]+)\s*\(", text)))
+    assert syms and set(syms) == set(_lib.HOST_SIGNATURES)
+    assert all(hasattr(lib, s) for s in syms)
+
+
 def test_no_gpu_fails_loudly():
     """Without a GPU the engine refuses to start: no silent CPU fallback."""
     import torch
