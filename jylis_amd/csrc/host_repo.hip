@@ -231,32 +231,53 @@ struct Repo {
   }
 };
 
-// GCOUNT (repo_gcount.pony): own column kept on the host for INC, sums on the GPU
+// Counters keep THIS replica's own entry on the host, with the reference's
+// rules: INC assigns own + v (wrapping, GCounter.increment) and a converged
+// echo of our id max-merges into it.  The engine max-merges every column,
+// own included, so after a wrapping INC its own cell can exceed the
+// reference's; GET therefore reads the engine sum and swaps in the host's own
+// entry: sum - engine_cell(own) + own (all mod 2^64).  Every other column --
+// the converge path -- is exactly the engine's.
+struct OwnCol {
+  std::unordered_map<std::string, u64> own;
+  u64 get(const std::string& k) const {
+    auto it = own.find(k);
+    return it == own.end() ? 0 : it->second;
+  }
+  void echo(const std::string& k, u64 v) {  // converge of our id: max-merge
+    u64& t = own[k];
+    if (v > t) t = v;
+  }
+};
+
+// GCOUNT (repo_gcount.pony)
 struct RepoGCOUNT : Repo {
-  std::unordered_map<std::string, u64> own;    // this replica's totals (only we write them)
-  std::map<std::string, u64> deltas;           // _deltas: key -> our total
+  OwnCol mine;
+  std::map<std::string, u64> deltas;  // _deltas: key -> our total at the last INC
   const char* datatype() const override { return "GCOUNT"; }
   std::vector<std::pair<std::string, std::string>> commands() const override {
     return {{"GET", "key"}, {"INC", "key value"}};
   }
   bool apply(Respond& r, Cmd& c) override {
     const std::string op = c.next();
-    if (op == "GET") {
+    if (op == "GET") {  // repo_gcount.pony:53-55
       const std::string k = c.next();
       u32 s;
       u64 v = 0;
-      if (eng->lookup(JY_GCOUNT, k, s)) eng->ck(jy_gcount_get(eng->e, 1, &s, &v, JY_HOST));
+      if (eng->lookup(JY_GCOUNT, k, s)) {
+        eng->ck(jy_gcount_get(eng->e, 1, &s, &v, JY_HOST));
+        v = v - eng->cell(JY_GCOUNT, s, eng->col(identity), 0) + mine.get(k);
+      }
       r.u64v(v);
       return false;
     }
-    if (op == "INC") {
+    if (op == "INC") {  // repo_gcount.pony:57-60
       const std::string k = c.next();
       const u64 v = parse_u64(c.next());
       const u32 s = eng->intern(JY_GCOUNT, k);
       const u16 col = eng->col(identity);
-      // our own entry as the engine holds it (a converged echo may have raised it)
-      u64& t = own[k];
-      t = std::max(t, eng->cell(JY_GCOUNT, s, col, 0)) + v;  // GCounter.increment: wrapping add
+      u64& t = mine.own[k];
+      t += v;
       deltas[k] = t;
       eng->ck(jy_gcount_converge(eng->e, 1, &s, &col, &t, JY_HOST));
       r.ok();
@@ -282,6 +303,7 @@ struct RepoGCOUNT : Repo {
     std::vector<u64> cv;
     for (size_t i = 0; i < b.keys.size(); i++)
       for (auto& e : b.g[i]) {
+        if (e.first == identity) mine.echo(b.keys[i], e.second);
         cs.push_back(slots[i]);
         cc.push_back(eng->col(e.first));
         cv.push_back(e.second);
@@ -292,32 +314,42 @@ struct RepoGCOUNT : Repo {
 
 // PNCOUNT (repo_pncount.pony): INC/DEC parse i64 and bit-cast to u64 (:36,60,65)
 struct RepoPNCOUNT : Repo {
-  std::unordered_map<std::string, u64> own_p, own_n;
+  OwnCol mp, mn;
   std::map<std::string, std::pair<bool, bool>> touched;  // which of P / N a delta carries
+  std::map<std::string, std::pair<u64, u64>> dval;       // their values at the last INC / DEC
   const char* datatype() const override { return "PNCOUNT"; }
   std::vector<std::pair<std::string, std::string>> commands() const override {
     return {{"GET", "key"}, {"INC", "key value"}, {"DEC", "key value"}};
   }
   bool apply(Respond& r, Cmd& c) override {
     const std::string op = c.next();
-    if (op == "GET") {
+    if (op == "GET") {  // repo_pncount.pony:55-57
       const std::string k = c.next();
       u32 s;
       i64 v = 0;
-      if (eng->lookup(JY_PNCOUNT, k, s)) eng->ck(jy_pncount_get(eng->e, 1, &s, &v, JY_HOST));
+      if (eng->lookup(JY_PNCOUNT, k, s)) {
+        eng->ck(jy_pncount_get(eng->e, 1, &s, &v, JY_HOST));
+        const u16 col = eng->col(identity);
+        u64 u = (u64)v;
+        u = u - eng->cell(JY_PNCOUNT, s, col, 0) + mp.get(k);
+        u = u + eng->cell(JY_PNCOUNT, s, col, 1) - mn.get(k);
+        v = (i64)u;
+      }
       r.i64v(v);
       return false;
     }
-    if (op == "INC" || op == "DEC") {
+    if (op == "INC" || op == "DEC") {  // repo_pncount.pony:59-67
       const std::string k = c.next();
       const u64 v = (u64)parse_i64(c.next());
       const bool inc = op == "INC";
       const u32 s = eng->intern(JY_PNCOUNT, k);
       const u16 col = eng->col(identity);
-      u64& t = (inc ? own_p : own_n)[k];
-      t = std::max(t, eng->cell(JY_PNCOUNT, s, col, inc ? 0 : 1)) + v;
+      u64& t = (inc ? mp : mn).own[k];
+      t += v;
       auto& tt = touched[k];
+      auto& dv = dval[k];
       (inc ? tt.first : tt.second) = true;
+      (inc ? dv.first : dv.second) = t;
       if (inc) eng->ck(jy_pncount_converge(eng->e, 1, &s, &col, &t, 0, nullptr, nullptr, nullptr, JY_HOST));
       else eng->ck(jy_pncount_converge(eng->e, 0, nullptr, nullptr, nullptr, 1, &s, &col, &t, JY_HOST));
       r.ok();
@@ -333,10 +365,12 @@ struct RepoPNCOUNT : Repo {
       b.keys.push_back(kv.first);
       b.g.push_back({});
       b.n.push_back({});
-      if (kv.second.first) b.g.back().push_back({identity, own_p[kv.first]});
-      if (kv.second.second) b.n.back().push_back({identity, own_n[kv.first]});
+      const auto& dv = dval[kv.first];
+      if (kv.second.first) b.g.back().push_back({identity, dv.first});
+      if (kv.second.second) b.n.back().push_back({identity, dv.second});
     }
     touched.clear();
+    dval.clear();
     return b;
   }
   void converge_batch(const Batch& b) override {
@@ -346,11 +380,13 @@ struct RepoPNCOUNT : Repo {
     std::vector<u64> pv, nv;
     for (size_t i = 0; i < b.keys.size(); i++) {
       for (auto& e : b.g[i]) {
+        if (e.first == identity) mp.echo(b.keys[i], e.second);
         ps.push_back(slots[i]);
         pc.push_back(eng->col(e.first));
         pv.push_back(e.second);
       }
       for (auto& e : b.n[i]) {
+        if (e.first == identity) mn.echo(b.keys[i], e.second);
         ns.push_back(slots[i]);
         nc.push_back(eng->col(e.first));
         nv.push_back(e.second);
