@@ -284,7 +284,8 @@ def bench_tlog(args, eng, dev, dist, rank, world):
     from jylis_amd import synth as S
     from jylis_amd._lib import TLOG
     K = args.keys or (4 << 20)
-    nb = max(1, args.batches)
+    # a distinct batch for every step: a replayed batch is all duplicates
+    nb = max(1, args.batches, args.warmup + args.steps)
     st, dl = S.tlog_tables(K, seed=S.BASE_SEED + 4 + 1000 * rank, rounds=nb)
     slots = eng.intern(TLOG, (st["key_bytes"], st["key_offs"]))
     assert (slots == np.arange(K)).all()
@@ -334,7 +335,7 @@ def bench_tlog(args, eng, dev, dist, rank, world):
             "ms_per_step": t / args.steps * 1e3,
             "roofline": {"bound": "hbm", "achieved": avg_b / k / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": avg_b / k / 1e9 / HBM_PEAK_GBS,
-                         "kernel": "k_tlog_count + scan + k_tlog_write (whole converge)",
+                         "kernel": "TLOG merge path (k_tlog_*, whole converge)",
                          "converge_ms_avg": k * 1e3, "bytes_per_converge": avg_b,
                          "bytes_note": "24 B per input entry (state + delta) + 24 B per output entry + 24 B per key"}}
 
@@ -359,7 +360,7 @@ def bench_ujson(args, eng, dev, dist, rank, world):
     from jylis_amd._lib import UJSON
     from jylis_amd.repo import RepoUJSON
     D = args.keys or (1 << 20)
-    nb = max(1, args.batches)
+    nb = max(1, args.batches, args.warmup + args.steps)
     t0 = time.perf_counter()
     st, dl = S.ujson_tables(D, seed=S.BASE_SEED + 5 + 1000 * rank, rounds=nb, R=16)
     gen_s = time.perf_counter() - t0
@@ -405,7 +406,7 @@ def bench_ujson(args, eng, dev, dist, rank, world):
             "ms_per_step": t / args.steps * 1e3, "generate_s": gen_s,
             "roofline": {"bound": "hbm", "achieved": bytes_conv / k / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": bytes_conv / k / 1e9 / HBM_PEAK_GBS,
-                         "kernel": "k_uj_count + 2 scans + k_uj_write (whole converge)",
+                         "kernel": "UJSON merge path (k_uj_*, whole converge)",
                          "converge_ms_avg": k * 1e3, "bytes_per_converge": bytes_conv,
                          "bytes_note": "16 B per element read+written, 8 B per cloud dot read+written, "
                                        "8R B vv per delta doc read+write, 16 B per doc offsets"}}

@@ -213,16 +213,12 @@ void jy_engine_destroy(jy_engine* eng) {
   F(eng->treg.lr);
   for (int b = 0; b < 2; b++) {
     F(eng->tlog.off[b]);
-    F(eng->tlog.ts[b]);
-    F(eng->tlog.pre[b]);
-    F(eng->tlog.lr[b]);
+    F(eng->tlog.rec[b]);
     F(eng->ujson.eoff[b]);
-    F(eng->ujson.dots[b]);
-    F(eng->ujson.elems[b]);
+    F(eng->ujson.rec[b]);
     F(eng->ujson.coff[b]);
     F(eng->ujson.cloud[b]);
     F(eng->ujson.eseg[b]);
-    F(eng->tlog.seg[b]);
     F(eng->ujson.cseg[b]);
   }
   F(eng->tlog.cutoff);

@@ -70,12 +70,16 @@ struct TregState {  // SoA per slot
   u64 kcap = 0;
 };
 
-struct TlogState {  // CSR, double-buffered entries
+// one TLOG entry: 32 B so a lane moves it with two 16-B accesses
+struct alignas(16) TRec {
+  u64 ts, pre, lr;
+  u32 seg;  // slot of the entry
+  u32 pad;
+};
+
+struct TlogState {  // CSR over slots, double-buffered entry records
   u64* off[2] = {nullptr, nullptr};  // [kcap + 1]
-  u64* ts[2] = {nullptr, nullptr};
-  u64* pre[2] = {nullptr, nullptr};
-  u64* lr[2] = {nullptr, nullptr};
-  u32* seg[2] = {nullptr, nullptr};  // slot of each entry
+  TRec* rec[2] = {nullptr, nullptr};
   u64 ecap[2] = {0, 0};
   int cur = 0;
   u64* cutoff = nullptr;  // [kcap]
@@ -84,10 +88,14 @@ struct TlogState {  // CSR, double-buffered entries
   bool nent_known = false;  // pin_total[0] holds the live total after a merge
 };
 
+// one UJSON element: (dot, element handle), moved with one 16-B access
+struct alignas(16) URec {
+  u64 dot, elem;
+};
+
 struct UjsonState {  // CSR elements + CSR cloud (double-buffered), dense vv
   u64* eoff[2] = {nullptr, nullptr};  // [kcap + 1]
-  u64* dots[2] = {nullptr, nullptr};
-  u64* elems[2] = {nullptr, nullptr};
+  URec* rec[2] = {nullptr, nullptr};
   u32* eseg[2] = {nullptr, nullptr};  // slot of each element
   u64 ecap[2] = {0, 0};
   u64* coff[2] = {nullptr, nullptr};  // [kcap + 1]

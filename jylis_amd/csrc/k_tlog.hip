@@ -6,11 +6,11 @@
 //              the later timestamp first, then the greater value first
 //              (Pony String order); (ts, value) duplicates collapse.
 //
-// HBM layout: per type, CSR over slots -- off[kcap+1] (u64); entries SoA
-// ts / pre / lr (u64 each; value handle as in TREG: 8-byte big-endian prefix
-// + arena offset/length) and seg (u32 slot of the entry); cutoff[kcap].
-// Entries are double-buffered: a converge rewrites the CSR into the other
-// buffer.
+// HBM layout: per type, CSR over slots -- off[kcap+1] (u64); entries are
+// 32-B records {ts, pre, lr, seg} (value handle as in TREG: 8-byte big-endian
+// prefix + arena offset/length; seg = slot of the entry), so the streaming
+// passes move them with 16-B accesses; cutoff[kcap].  Entries are
+// double-buffered: a converge rewrites the CSR into the other buffer.
 //
 // Parallel shape: one thread per ENTRY (state or delta), coalesced, with
 // merge-path positions -- no per-key loops, so long or skewed logs cost the
@@ -19,16 +19,17 @@
 //   keep(delta e)  = ts >= cutoff' and no equal entry in the state segment
 //   pos(e) = new_off[key] + #kept own-side entries before e
 //                         + #kept other-side entries ordered before e
-// the counts coming from exclusive scans of the keep flags and one binary
-// search (entry order, value bytes compared only on (ts, prefix) ties) into
-// the other side's sorted segment.  A delta segment that is not strictly
+// the counts coming from an exclusive scan of the delta keep flags and one
+// binary search per delta entry (entry order, value bytes compared only on
+// (ts, prefix) ties) into the state segment.  That search's result (the
+// entry's state rank, prel) is kept, so the state side finds its count by a
+// search over small integers and the delta side needs no second search.  A delta segment that is not strictly
 // ordered is not a TLog: its key is left untouched and counted (the
 // reference swallows converge errors, repo_tlog.pony:67).
 //
-// Roofline: HBM.  Per input entry: 24 B read (+4 B seg, state side) and
-// 28 B written per output entry; per key 16 B offsets + 16 B cutoff; keep
-// flags and their scans add 24 B per input entry (u64 flag, scan write +
-// read); see DESIGN.md.
+// Roofline: HBM.  Per state entry 32 B read; per delta entry 24 B read;
+// 32 B written per output entry; per key 16 B offsets + 16 B cutoff; delta
+// keep flags, their scan and prel add ~28 B per delta entry; see DESIGN.md.
 
 #include <hipcub/hipcub.hpp>
 
@@ -56,43 +57,72 @@ struct Ent {
 
 // > 0 if log entry m is ordered before x; value handles are read only on a
 // timestamp tie
-__device__ __forceinline__ int cmp_at(const u64* __restrict__ ts, const u64* __restrict__ pre,
-                                      const u64* __restrict__ lr, u64 m, const Ent& x,
+__device__ __forceinline__ int cmp_at(const TRec* __restrict__ rec, u64 m, const Ent& x,
                                       const uint8_t* __restrict__ arena) {
-  const u64 t = ts[m];
+  const u64 t = rec[m].ts;
   if (t != x.t) return t > x.t ? 1 : -1;
-  return jy_value_cmp(pre[m], lr[m], x.p, x.l, arena);
+  return jy_value_cmp(rec[m].pre, rec[m].lr, x.p, x.l, arena);
 }
 
 // first index in [lo, hi) of a sorted log whose entry is NOT ordered before x
-__device__ __forceinline__ u64 lower_bound_entry(const u64* __restrict__ ts, const u64* __restrict__ pre,
-                                                 const u64* __restrict__ lr, u64 lo, u64 hi, const Ent& x,
+__device__ __forceinline__ u64 lower_bound_entry(const TRec* __restrict__ rec, u64 lo, u64 hi, const Ent& x,
                                                  const uint8_t* __restrict__ arena) {
   while (lo < hi) {
     const u64 m = (lo + hi) >> 1;
-    if (cmp_at(ts, pre, lr, m, x, arena) > 0) lo = m + 1;
+    if (cmp_at(rec, m, x, arena) > 0) lo = m + 1;
     else hi = m;
   }
   return lo;
 }
 
-// per-key record for the state-side scatter: one cache line instead of six
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ TRec load_rec(const TRec* __restrict__ p) {
+  const u64x2* q = reinterpret_cast<const u64x2*>(p);
+  const u64x2 a = __builtin_nontemporal_load(q), b = __builtin_nontemporal_load(q + 1);
+  TRec r;
+  r.ts = a.x;
+  r.pre = a.y;
+  r.lr = b.x;
+  r.seg = (u32)b.y;
+  r.pad = (u32)(b.y >> 32);
+  return r;
+}
+
+__device__ __forceinline__ void store_rec(TRec* __restrict__ p, u64 ts, u64 pre, u64 lr, u32 seg) {
+  u64x2* q = reinterpret_cast<u64x2*>(p);
+  u64x2 a, b;
+  a.x = ts;
+  a.y = pre;
+  b.x = lr;
+  b.y = seg;
+  __builtin_nontemporal_store(a, q);
+  __builtin_nontemporal_store(b, q + 1);
+}
+
+// per-key record for the state-side scatter: one line instead of six
 // scattered per-key arrays
 struct KeyInfo {
   u64 shift;     // new_off[s] - off[s]
   u64 keep_end;  // off[s] + surviving prefix length
+  u64 lo;        // off[s]
   u64 blo, bhi;  // delta segment (empty if none)
   u64 scan_lo;   // scan_b[blo]
-  u64 pad;
+};
+
+// per delta key: its state segment, merged cutoff and whether it merges
+struct DInfo {
+  u64 lo, hi;  // state segment [off[s], off[s+1])
+  u64 cut;     // max(state cutoff, delta cutoff)
+  u32 s;       // slot
+  u32 raised;  // the delta raises the cutoff (else no state entry drops:
+               // every state entry already has ts >= the state cutoff)
 };
 
 struct TlogArgs {
   // state (current buffer)
   const u64* off;
-  const u64* ts;
-  const u64* pre;
-  const u64* lr;
-  const u32* seg;
+  const TRec* rec;
   u64* cutoff;
   u64 nkeys, na;
   // delta batch
@@ -108,10 +138,11 @@ struct TlogArgs {
   const u32* dseg;  // [nb] delta key of each delta entry
   // temporaries
   u32* bad;     // [nd]
-  u64* cut;     // [nd] merged cutoff
+  DInfo* dinfo;  // [nd]
   u64* keep_a;  // [nkeys] surviving state entries: a prefix of every log
-  u64* flag_b;
-  u64* scan_b;
+  u64* flag_b;  // [nb + 1]
+  u64* scan_b;  // [nb + 1]
+  u32* prel;    // [nb] state entries of the key ordered before the delta entry
   KeyInfo* info;  // [nkeys]
 };
 
@@ -122,7 +153,13 @@ __global__ __launch_bounds__(kThreads) void k_tlog_prep(TlogArgs A) {
   A.dptr[s] = (u32)k;
   A.bad[k] = 0;
   const u64 cs = A.cutoff[s], cd = A.dcut[k];
-  A.cut[k] = cs > cd ? cs : cd;
+  DInfo D;
+  D.lo = A.off[s];
+  D.hi = A.off[s + 1];
+  D.cut = cs > cd ? cs : cd;
+  D.s = (u32)s;
+  D.raised = cd > cs;
+  A.dinfo[k] = D;
 }
 
 __global__ __launch_bounds__(kThreads) void k_tlog_validate(TlogArgs A) {
@@ -134,15 +171,16 @@ __global__ __launch_bounds__(kThreads) void k_tlog_validate(TlogArgs A) {
     A.bad[k] = 1;
 }
 
-__global__ __launch_bounds__(kThreads) void k_tlog_drop_bad(TlogArgs A, unsigned long long* __restrict__ skipped) {
-  const u64 k = gid();
-  if (k >= A.nd) return;
-  if (A.bad[k]) {
-    A.dptr[A.slot[k]] = kNone;
-    atomicAdd(skipped, 1ull);
-  }
+// the delta key that merges into slot s, or kNone (no delta, or a malformed
+// one: the reference swallows the error and leaves the key untouched)
+__device__ __forceinline__ u32 merging_key(const TlogArgs& A, u64 s) {
+  const u32 k = A.dptr[s];
+  return (k != kNone && !A.bad[k]) ? k : kNone;
 }
 
+// keep flag of every delta entry and its rank among the state entries.
+// prel is non-decreasing along a delta segment: entries dropped by the
+// cutoff are its tail and take the segment length.
 __global__ __launch_bounds__(kThreads) void k_tlog_flag_b(TlogArgs A) {
   const u64 j = gid();
   if (j > A.nb) return;
@@ -151,15 +189,27 @@ __global__ __launch_bounds__(kThreads) void k_tlog_flag_b(TlogArgs A) {
     return;
   }
   const u32 k = A.dseg[j];
-  const u64 s = A.slot[k];
+  const DInfo D = A.dinfo[k];
   u64 keep = 0;
-  if (A.dptr[s] == k && A.dts[j] >= A.cut[k]) {
-    const Ent x{A.dts[j], A.dpre[j], A.dlr[j]};
-    const u64 hi = A.off[s + 1];
-    const u64 p = lower_bound_entry(A.ts, A.pre, A.lr, A.off[s], hi, x, A.arena);
-    keep = !(p < hi && cmp_at(A.ts, A.pre, A.lr, p, x, A.arena) == 0);
+  const u64 lo = D.lo, hi = D.hi;
+  u64 p = hi;
+  const u64 t = A.dts[j];
+  if (t >= D.cut && !A.bad[k] && A.dptr[D.s] == k) {
+    const Ent x{t, A.dpre[j], A.dlr[j]};
+    // fast path: new log entries are usually newer than the whole state
+    const int c0 = lo < hi ? cmp_at(A.rec, lo, x, A.arena) : -1;
+    if (c0 < 0) {
+      p = lo;
+      keep = 1;
+    } else if (c0 == 0) {
+      p = lo;
+    } else {
+      p = lower_bound_entry(A.rec, lo + 1, hi, x, A.arena);
+      keep = !(p < hi && cmp_at(A.rec, p, x, A.arena) == 0);
+    }
   }
   A.flag_b[j] = keep;
+  A.prel[j] = (u32)(p - lo);
 }
 
 __global__ __launch_bounds__(kThreads) void k_tlog_sizes_out(TlogArgs A, u64* __restrict__ cnt) {
@@ -169,16 +219,16 @@ __global__ __launch_bounds__(kThreads) void k_tlog_sizes_out(TlogArgs A, u64* __
     cnt[s] = 0;
     return;
   }
-  const u32 k = A.dptr[s];
+  const u32 k = merging_key(A, s);
   const u64 lo = A.off[s];
   u64 hi = A.off[s + 1];
-  if (k != kNone) {
+  if (k != kNone && A.dinfo[k].raised && lo < hi && A.rec[hi - 1].ts < A.dinfo[k].cut) {
     // entries are in non-increasing ts order: the cutoff drops a suffix
-    const u64 c = A.cut[k];
+    const u64 c = A.dinfo[k].cut;
     u64 a = lo;
     while (a < hi) {
       const u64 m = (a + hi) >> 1;
-      if (A.ts[m] >= c) a = m + 1;
+      if (A.rec[m].ts >= c) a = m + 1;
       else hi = m;
     }
     hi = a;
@@ -189,60 +239,61 @@ __global__ __launch_bounds__(kThreads) void k_tlog_sizes_out(TlogArgs A, u64* __
   cnt[s] = n;
 }
 
-__global__ __launch_bounds__(kThreads) void k_tlog_info(TlogArgs A, const u64* __restrict__ noff) {
+// per slot: the state-side scatter record; merged cutoff stored; malformed
+// deltas counted
+__global__ __launch_bounds__(kThreads) void k_tlog_info(TlogArgs A, const u64* __restrict__ noff,
+                                                        unsigned long long* __restrict__ skipped) {
   const u64 s = gid();
   if (s >= A.nkeys) return;
-  const u32 k = A.dptr[s];
+  u32 k = A.dptr[s];
+  if (k != kNone) {
+    if (A.bad[k]) {
+      atomicAdd(skipped, 1ull);
+      k = kNone;
+    } else {
+      A.cutoff[s] = A.dinfo[k].cut;
+    }
+  }
   KeyInfo I;
-  I.shift = noff[s] - A.off[s];
-  I.keep_end = A.off[s] + A.keep_a[s];
+  I.lo = A.off[s];
+  I.shift = noff[s] - I.lo;
+  I.keep_end = I.lo + A.keep_a[s];
   I.blo = k == kNone ? 0 : A.doff[k];
   I.bhi = k == kNone ? 0 : A.doff[k + 1];
   I.scan_lo = A.scan_b[I.blo];
-  I.pad = 0;
   A.info[s] = I;
 }
 
-__global__ __launch_bounds__(kThreads) void k_tlog_scatter_a(TlogArgs A, const u64* __restrict__ noff,
-                                                             u64* __restrict__ ots, u64* __restrict__ opre,
-                                                             u64* __restrict__ olr, u32* __restrict__ oseg) {
+// every surviving state entry: new position = old + key shift + kept delta
+// entries ordered before it (those whose state rank is <= its own)
+__global__ __launch_bounds__(kThreads) void k_tlog_scatter_a(TlogArgs A, TRec* __restrict__ out) {
   const u64 i = gid();
   if (i >= A.na) return;
-  const u32 s = A.seg[i];
-  const KeyInfo I = A.info[s];
+  const TRec r = load_rec(A.rec + i);
+  const KeyInfo I = A.info[r.seg];
   if (i >= I.keep_end) return;
-  const Ent x{A.ts[i], A.pre[i], A.lr[i]};
   u64 pos = i + I.shift;
-  if (I.bhi > I.blo) pos += A.scan_b[lower_bound_entry(A.dts, A.dpre, A.dlr, I.blo, I.bhi, x, A.arena)] - I.scan_lo;
-  (void)noff;
-  ots[pos] = x.t;
-  opre[pos] = x.p;
-  olr[pos] = x.l;
-  oseg[pos] = (u32)s;
+  if (I.bhi > I.blo) {
+    const u32 rr = (u32)(i - I.lo);
+    u64 lo = I.blo, hi = I.bhi;
+    while (lo < hi) {
+      const u64 m = (lo + hi) >> 1;
+      if (A.prel[m] <= rr) lo = m + 1;
+      else hi = m;
+    }
+    pos += A.scan_b[lo] - I.scan_lo;
+  }
+  store_rec(out + pos, r.ts, r.pre, r.lr, r.seg);
 }
 
 __global__ __launch_bounds__(kThreads) void k_tlog_scatter_b(TlogArgs A, const u64* __restrict__ noff,
-                                                             u64* __restrict__ ots, u64* __restrict__ opre,
-                                                             u64* __restrict__ olr, u32* __restrict__ oseg) {
+                                                             TRec* __restrict__ out) {
   const u64 j = gid();
   if (j >= A.nb || !A.flag_b[j]) return;
   const u32 k = A.dseg[j];
-  const u64 s = A.slot[k];
-  const Ent x{A.dts[j], A.dpre[j], A.dlr[j]};
-  const u64 lo = A.off[s];
-  // state entries ordered before x all survive the cutoff (x itself does)
-  const u64 p = lower_bound_entry(A.ts, A.pre, A.lr, lo, A.off[s + 1], x, A.arena);
-  const u64 pos = noff[s] + (A.scan_b[j] - A.scan_b[A.doff[k]]) + (p - lo);
-  ots[pos] = x.t;
-  opre[pos] = x.p;
-  olr[pos] = x.l;
-  oseg[pos] = (u32)s;
-}
-
-__global__ __launch_bounds__(kThreads) void k_tlog_cut_store(TlogArgs A) {
-  const u64 k = gid();
-  if (k >= A.nd || A.bad[k]) return;
-  A.cutoff[A.slot[k]] = A.cut[k];
+  const u32 s = A.dinfo[k].s;
+  const u64 pos = noff[s] + (A.scan_b[j] - A.scan_b[A.doff[k]]) + A.prel[j];
+  store_rec(out + pos, A.dts[j], A.dpre[j], A.dlr[j], s);
 }
 
 __global__ __launch_bounds__(kThreads) void k_fill_tail(u64* __restrict__ off, u64 from, u64 to) {
@@ -261,8 +312,7 @@ __global__ __launch_bounds__(kThreads) void k_tlog_sizes(const u64* __restrict__
   cut[i] = cutoff[s];
 }
 
-__global__ __launch_bounds__(kThreads) void k_tlog_gather(const u64* __restrict__ off, const u64* __restrict__ ts,
-                                                          const u64* __restrict__ pre, const u64* __restrict__ lr,
+__global__ __launch_bounds__(kThreads) void k_tlog_gather(const u64* __restrict__ off, const TRec* __restrict__ rec,
                                                           const u32* __restrict__ slots, const u64* __restrict__ ooff,
                                                           u64 n, u64* __restrict__ ots, u64* __restrict__ opre,
                                                           u64* __restrict__ olr) {
@@ -271,9 +321,9 @@ __global__ __launch_bounds__(kThreads) void k_tlog_gather(const u64* __restrict_
   const u64 s = slots[i];
   u64 o = ooff[i];
   for (u64 j = off[s]; j < off[s + 1]; j++, o++) {
-    ots[o] = ts[j];
-    opre[o] = pre[j];
-    olr[o] = lr[j];
+    ots[o] = rec[j].ts;
+    opre[o] = rec[j].pre;
+    olr[o] = rec[j].lr;
   }
 }
 
@@ -330,10 +380,9 @@ int32_t jy_seg_ids(jy_engine* eng, const u64* offs, u64 nseg, u64 n, u32* out) {
 
 static int32_t ensure_entries(jy_engine* eng, int buf, u64 need) {
   TlogState& t = eng->tlog;
-  if (need <= t.ecap[buf] && t.ts[buf]) return JY_OK;
+  if (need <= t.ecap[buf] && t.rec[buf]) return JY_OK;
   const u64 nc = std::max<u64>(std::max<u64>(need + need / 2, eng->cfg.entry_capacity[JY_TLOG]), 1024);
-  for (u64** p : {&t.ts[buf], &t.pre[buf], &t.lr[buf]}) JY_TRY(realloc_dead(eng, reinterpret_cast<void**>(p), nc * 8));
-  JY_TRY(realloc_dead(eng, reinterpret_cast<void**>(&t.seg[buf]), nc * 4));
+  JY_TRY(realloc_dead(eng, reinterpret_cast<void**>(&t.rec[buf]), nc * sizeof(TRec)));
   t.ecap[buf] = nc;
   return JY_OK;
 }
@@ -377,10 +426,7 @@ int32_t jy_tlog_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* dcut, 
 
   TlogArgs A{};
   A.off = t.off[cur];
-  A.ts = t.ts[cur];
-  A.pre = t.pre[cur];
-  A.lr = t.lr[cur];
-  A.seg = t.seg[cur];
+  A.rec = t.rec[cur];
   A.cutoff = t.cutoff;
   A.nkeys = nk;
   A.na = na;
@@ -396,14 +442,15 @@ int32_t jy_tlog_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* dcut, 
   void* p;
   JY_TRY(jy_scratch(eng, 8, nk * 4, &p));
   A.dptr = static_cast<u32*>(p);
-  JY_TRY(jy_scratch(eng, 9, nd * 12, &p));
-  A.cut = static_cast<u64*>(p);
-  A.bad = reinterpret_cast<u32*>(A.cut + nd);
+  JY_TRY(jy_scratch(eng, 9, nd * (sizeof(DInfo) + 4), &p));
+  A.dinfo = static_cast<DInfo*>(p);
+  A.bad = reinterpret_cast<u32*>(A.dinfo + nd);
   JY_TRY(jy_scratch(eng, 11, nk * 8, &p));
   A.keep_a = static_cast<u64*>(p);
-  JY_TRY(jy_scratch(eng, 12, (nent + 1) * 16, &p));
+  JY_TRY(jy_scratch(eng, 12, (nent + 1) * 20, &p));
   A.flag_b = static_cast<u64*>(p);
   A.scan_b = A.flag_b + nent + 1;
+  A.prel = reinterpret_cast<u32*>(A.scan_b + nent + 1);
   JY_TRY(jy_scratch(eng, 16, (nk + 1) * 8, &p));
   u64* cnt = static_cast<u64*>(p);
   JY_TRY(jy_scratch(eng, 18, nk * sizeof(KeyInfo), &p));
@@ -415,15 +462,13 @@ int32_t jy_tlog_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* dcut, 
   JY_HIP(eng, hipMemsetAsync(A.dptr, 0xFF, nk * 4, eng->stream));
   LAUNCH(k_tlog_prep, nd, A);
   if (nent) LAUNCH(k_tlog_validate, nent, A);
-  LAUNCH(k_tlog_drop_bad, nd, A, reinterpret_cast<unsigned long long*>(eng->skipped_dev));
   LAUNCH(k_tlog_flag_b, nent + 1, A);
   JY_TRY(jy_scan_u64(eng, A.flag_b, A.scan_b, nent));
   LAUNCH(k_tlog_sizes_out, nk + 1, A, cnt);
   JY_TRY(jy_scan_u64(eng, cnt, t.off[nxt], nk));
-  LAUNCH(k_tlog_info, nk, A, t.off[nxt]);
-  if (na) LAUNCH(k_tlog_scatter_a, na, A, t.off[nxt], t.ts[nxt], t.pre[nxt], t.lr[nxt], t.seg[nxt]);
-  if (nent) LAUNCH(k_tlog_scatter_b, nent, A, t.off[nxt], t.ts[nxt], t.pre[nxt], t.lr[nxt], t.seg[nxt]);
-  LAUNCH(k_tlog_cut_store, nd, A);
+  LAUNCH(k_tlog_info, nk, A, t.off[nxt], reinterpret_cast<unsigned long long*>(eng->skipped_dev));
+  if (na) LAUNCH(k_tlog_scatter_a, na, A, t.rec[nxt]);
+  if (nent) LAUNCH(k_tlog_scatter_b, nent, A, t.off[nxt], t.rec[nxt]);
   // publish the new total for the next call (read back asynchronously)
   JY_HIP(eng, hipMemcpyAsync(eng->pin_total, t.off[nxt] + nk, 8, hipMemcpyDeviceToHost, eng->stream));
   JY_HIP(eng, hipEventRecord(eng->total_ready, eng->stream));
@@ -441,6 +486,6 @@ int32_t jy_tlog_sizes(jy_engine* eng, u64 n, const u32* slots, u64* len, u64* cu
 int32_t jy_tlog_gather(jy_engine* eng, u64 n, const u32* slots, const u64* ooff, u64* ts, u64* pre, u64* lr) {
   TlogState& t = eng->tlog;
   const int c = t.cur;
-  LAUNCH(k_tlog_gather, n, t.off[c], t.ts[c], t.pre[c], t.lr[c], slots, ooff, n, ts, pre, lr);
+  LAUNCH(k_tlog_gather, n, t.off[c], t.rec[c], slots, ooff, n, ts, pre, lr);
   return JY_OK;
 }
