@@ -6,6 +6,8 @@ own roofline (algorithmic bytes per converge / converge time, HIP events on
 the engine stream).  Inputs are synthetic (jylis_amd/synth.py); the first
 converge of every mode is checked against an independent recomputation.
 """
+import os
+import sys
 import time
 
 import numpy as np
@@ -24,16 +26,21 @@ def _timed(steps, warmup, step, dist, dev):
         dist.barrier()
     torch.cuda.synchronize(dev)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    host = []
     t0 = time.perf_counter()
     for i in range(steps):
         evs[i][0].record()
+        h0 = time.perf_counter()
         step(warmup + i)
+        host.append(time.perf_counter() - h0)
         evs[i][1].record()
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    if os.environ.get("JY_TRACE"):
+        print("host s per step:", " ".join(f"{h * 1e3:.3f}ms" for h in host), file=sys.stderr)
     return elapsed, [a.elapsed_time(b) / 1e3 for a, b in evs]
 
 

@@ -80,6 +80,15 @@ int32_t jy_keys_intern(jy_engine* eng, int32_t type, uint64_t n, const uint8_t* 
                        const uint64_t* key_offs, uint32_t* slots_out);
 int32_t jy_keys_lookup(const jy_engine* eng, int32_t type, uint64_t n, const uint8_t* key_bytes,
                        const uint64_t* key_offs, uint32_t* slots_out);
+/* The key directory lives in HBM (hash table + key bytes, k_keys.hip); the
+ * host-pointer calls above consult a host cache first and send the misses to
+ * it.  The _mem forms take key_bytes / key_offs / slots_out in HBM when
+ * mem = JY_DEVICE (bulk interning with no host round trip per key).  Slots
+ * are dense, per type, handed out in order of first occurrence. */
+int32_t jy_keys_intern_mem(jy_engine* eng, int32_t type, uint64_t n, const uint8_t* key_bytes,
+                           const uint64_t* key_offs, uint32_t* slots_out, int32_t mem);
+int32_t jy_keys_lookup_mem(jy_engine* eng, int32_t type, uint64_t n, const uint8_t* key_bytes,
+                           const uint64_t* key_offs, uint32_t* slots_out, int32_t mem);
 uint64_t jy_keys_count(const jy_engine* eng, int32_t type);
 int32_t jy_keys_reserve(jy_engine* eng, int32_t type, uint64_t key_capacity);
 /* owner shard of a key when keys are hash-sharded over `nshards` engines */

@@ -48,6 +48,8 @@ SIGNATURES = {
     "jy_replica_count": (U32, [P]),
     "jy_keys_intern": (I32, [P, I32, U64, P, P, P]),
     "jy_keys_lookup": (I32, [P, I32, U64, P, P, P]),
+    "jy_keys_intern_mem": (I32, [P, I32, U64, P, P, P, I32]),
+    "jy_keys_lookup_mem": (I32, [P, I32, U64, P, P, P, I32]),
     "jy_keys_count": (U64, [P, I32]),
     "jy_keys_reserve": (I32, [P, I32, U64]),
     "jy_key_owner": (U32, [P, U64, U32]),

@@ -26,20 +26,31 @@ int32_t check_type(jy_engine* eng, int32_t type) {
 // ---------------------------------------------------------------------------
 // memory helpers
 
+// Engine buffers come from the stream-ordered allocator: growing a buffer
+// never waits for queued kernels that still read the old one (they finish
+// before the stream-ordered free takes effect), so the host can enqueue the
+// next merge while the GPU runs the previous one.
+int32_t jy_dev_alloc(jy_engine* eng, void** p, u64 bytes, const char* what) {
+  hipError_t e = hipMallocAsync(p, bytes ? bytes : 8, eng->stream);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return eng->fail(JY_ENOMEM, std::string(what) + " hipMallocAsync(" + std::to_string(bytes) + "): " +
+                                    hipGetErrorString(e));
+  }
+  return JY_OK;
+}
+void jy_dev_free(jy_engine* eng, void* p) {
+  if (p) hipFreeAsync(p, eng->stream);
+}
+
 int32_t jy_realloc(jy_engine* eng, void** p, u64 old_bytes, u64 new_bytes, bool zero_tail) {
   if (new_bytes <= old_bytes && *p) return JY_OK;
   void* np = nullptr;
-  hipError_t e = hipMalloc(&np, new_bytes ? new_bytes : 8);
-  if (e != hipSuccess)
-    return eng->fail(JY_ENOMEM, "hipMalloc(" + std::to_string(new_bytes) + "): " + hipGetErrorString(e));
+  JY_TRY(jy_dev_alloc(eng, &np, new_bytes, "realloc"));
   if (*p && old_bytes) JY_HIP(eng, hipMemcpyAsync(np, *p, old_bytes, hipMemcpyDeviceToDevice, eng->stream));
   if (zero_tail && new_bytes > old_bytes)
     JY_HIP(eng, hipMemsetAsync(static_cast<uint8_t*>(np) + old_bytes, 0, new_bytes - old_bytes, eng->stream));
-  if (*p) {
-    // the old buffer may still be read by queued work: free in stream order
-    JY_HIP(eng, hipStreamSynchronize(eng->stream));
-    JY_HIP(eng, hipFree(*p));
-  }
+  jy_dev_free(eng, *p);
   *p = np;
   return JY_OK;
 }
@@ -47,14 +58,13 @@ int32_t jy_realloc(jy_engine* eng, void** p, u64 old_bytes, u64 new_bytes, bool 
 int32_t jy_scratch(jy_engine* eng, int idx, u64 bytes, void** out) {
   DevArray& a = eng->scratch[idx];
   if (a.bytes < bytes) {
-    u64 nb = std::max<u64>(round_up(bytes + bytes / 4, 256), 4096);
-    if (a.p) {
-      JY_HIP(eng, hipStreamSynchronize(eng->stream));
-      JY_HIP(eng, hipFree(a.p));
-      a.p = nullptr;
-    }
-    hipError_t e = hipMalloc(&a.p, nb);
-    if (e != hipSuccess) return eng->fail(JY_ENOMEM, std::string("scratch hipMalloc: ") + hipGetErrorString(e));
+    JY_TRACE("scratch %d grows %llu -> %llu", idx, (unsigned long long)a.bytes, (unsigned long long)bytes);
+    // grow by at least 2x: growing states should not realloc every call
+    u64 nb = std::max<u64>(round_up(std::max<u64>(bytes + bytes / 4, 2 * a.bytes), 256), 4096);
+    jy_dev_free(eng, a.p);
+    a.p = nullptr;
+    a.bytes = 0;
+    JY_TRY(jy_dev_alloc(eng, &a.p, nb, "scratch"));
     a.bytes = nb;
   }
   *out = a.p;
@@ -204,9 +214,7 @@ void jy_engine_destroy(jy_engine* eng) {
   if (!eng) return;
   hipSetDevice(eng->device);
   if (eng->stream) hipStreamSynchronize(eng->stream);
-  auto F = [](void* p) {
-    if (p) hipFree(p);
-  };
+  auto F = [eng](void* p) { jy_dev_free(eng, p); };
   for (int w = 0; w < 2; w++) F(eng->cnt[w].slab);
   F(eng->treg.ts);
   F(eng->treg.pre);
@@ -222,11 +230,14 @@ void jy_engine_destroy(jy_engine* eng) {
     F(eng->ujson.cseg[b]);
   }
   F(eng->tlog.cutoff);
+  F(eng->tlog.newest);
+  for (auto& k : eng->kdir) jy_keydir_free(eng, k);
   F(eng->ujson.vv);
   for (auto& a : eng->arena) F(a.p);
   for (auto& s : eng->scratch) F(s.p);
-  F(eng->skipped_dev);
-  F(eng->cols_dev);
+  if (eng->stream) hipStreamSynchronize(eng->stream);
+  if (eng->skipped_dev) hipFree(eng->skipped_dev);
+  if (eng->cols_dev) hipFree(eng->cols_dev);
   if (eng->pin) hipHostFree(eng->pin);
   if (eng->pin_total) hipHostFree(eng->pin_total);
   if (eng->pin_ready) hipEventDestroy(eng->pin_ready);
@@ -285,39 +296,93 @@ int32_t jy_replica_id(const jy_engine* eng, uint32_t col, uint64_t* id) {
 uint32_t jy_replica_count(const jy_engine* eng) { return (uint32_t)eng->rep_id.size(); }
 
 // ---- keys ----
-int32_t jy_keys_intern(jy_engine* eng, int32_t type, uint64_t n, const uint8_t* kb, const uint64_t* ko,
-                       uint32_t* slots) {
-  JY_TRY(check_type(eng, type));
-  JY_HIP(eng, hipSetDevice(eng->device));
-  KeyIndex& ix = eng->keys[type];
-  u64 nk = eng->nkeys[type];
-  if (ix.map.empty()) ix.map.reserve(std::max<u64>(n, 1024));
-  for (u64 i = 0; i < n; i++) {
-    std::string k(reinterpret_cast<const char*>(kb) + ko[i], ko[i + 1] - ko[i]);
-    auto r = ix.map.emplace(std::move(k), (u32)nk);
-    if (r.second) {
-      if (nk >= 0xFFFFFFFEull) return eng->fail(JY_ERANGE, "slot space exhausted");
-      nk++;
-    }
-    slots[i] = r.first->second;
-  }
+// The device key directory (k_keys.hip) is authoritative; eng->keys is a
+// host cache filled by small host-pointer calls.
+static constexpr u64 kCacheFill = 1 << 16;  // bulk calls do not fill the cache
+
+static int32_t keys_created(jy_engine* eng, int32_t type, u64 created) {
+  if (created == 0) return JY_OK;
+  const u64 before = eng->nkeys[type], nk = before + created;
   JY_TRY(jy_ensure_slots(eng, type, nk));
-  const u64 before = eng->nkeys[type];
   if (type == JY_TLOG) JY_TRY(jy_tlog_extend(eng, before, nk));
   if (type == JY_UJSON) JY_TRY(jy_ujson_extend(eng, before, nk));
   eng->nkeys[type] = nk;
   return JY_OK;
 }
 
-int32_t jy_keys_lookup(const jy_engine* eng, int32_t type, uint64_t n, const uint8_t* kb, const uint64_t* ko,
-                       uint32_t* slots) {
-  if (type < 0 || type >= JY_NTYPES) return JY_ETYPE;
-  const KeyIndex& ix = eng->keys[type];
+// host keys: cache first, the misses go to the device directory in one call
+static int32_t keys_host(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, const u64* ko, u32* slots,
+                         bool create) {
+  KeyIndex& ix = eng->keys[type];
+  std::vector<u64> miss;
   for (u64 i = 0; i < n; i++) {
     auto it = ix.map.find(std::string(reinterpret_cast<const char*>(kb) + ko[i], ko[i + 1] - ko[i]));
-    slots[i] = it == ix.map.end() ? JY_NO_SLOT : it->second;
+    if (it != ix.map.end()) slots[i] = it->second;
+    else miss.push_back(i);
+  }
+  if (miss.empty()) return JY_OK;
+  const u64 m = miss.size();
+  std::vector<u64> mo(m + 1, 0);
+  for (u64 j = 0; j < m; j++) {
+    const u64 len = ko[miss[j] + 1] - ko[miss[j]];
+    if (len > JY_LR_LEN_MASK) return eng->fail(JY_ERANGE, "key longer than 16 MiB");
+    mo[j + 1] = mo[j] + len;
+  }
+  std::vector<uint8_t> mb(mo[m]);
+  for (u64 j = 0; j < m; j++) std::memcpy(mb.data() + mo[j], kb + ko[miss[j]], mo[j + 1] - mo[j]);
+  const void* db;
+  const void* dofs;
+  JY_TRY(stage_begin(eng));
+  JY_TRY(jy_stage(eng, 0, mb.data(), mb.size(), JY_HOST, &db));
+  JY_TRY(jy_stage(eng, 1, mo.data(), (m + 1) * 8, JY_HOST, &dofs));
+  JY_TRY(stage_end(eng));
+  void* ds;
+  JY_TRY(jy_scratch(eng, 2, m * 4, &ds));
+  u64 created = 0;
+  JY_TRY(jy_keydir_run(eng, type, m, static_cast<const uint8_t*>(db), static_cast<const u64*>(dofs),
+                       static_cast<u32*>(ds), create, &created));
+  std::vector<u32> ms(m);
+  JY_HIP(eng, hipMemcpyAsync(ms.data(), ds, m * 4, hipMemcpyDeviceToHost, eng->stream));
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  JY_TRY(keys_created(eng, type, created));
+  const bool fill = m <= kCacheFill;
+  for (u64 j = 0; j < m; j++) {
+    slots[miss[j]] = ms[j];
+    if (fill && ms[j] != JY_NO_SLOT)
+      ix.map.emplace(std::string(reinterpret_cast<const char*>(mb.data()) + mo[j], mo[j + 1] - mo[j]), ms[j]);
   }
   return JY_OK;
+}
+
+int32_t jy_keys_intern(jy_engine* eng, int32_t type, uint64_t n, const uint8_t* kb, const uint64_t* ko,
+                       uint32_t* slots) {
+  return jy_keys_intern_mem(eng, type, n, kb, ko, slots, JY_HOST);
+}
+
+int32_t jy_keys_lookup(const jy_engine* eng, int32_t type, uint64_t n, const uint8_t* kb, const uint64_t* ko,
+                       uint32_t* slots) {
+  return jy_keys_lookup_mem(const_cast<jy_engine*>(eng), type, n, kb, ko, slots, JY_HOST);
+}
+
+int32_t jy_keys_intern_mem(jy_engine* eng, int32_t type, uint64_t n, const uint8_t* kb, const uint64_t* ko,
+                           uint32_t* slots, int32_t mem) {
+  JY_TRY(check_type(eng, type));
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (mem == JY_HOST) return keys_host(eng, type, n, kb, ko, slots, true);
+  if (mem != JY_DEVICE) return eng->fail(JY_EINVAL, "mem must be JY_HOST or JY_DEVICE");
+  u64 created = 0;
+  JY_TRY(jy_keydir_run(eng, type, n, kb, reinterpret_cast<const u64*>(ko), slots, true, &created));
+  return keys_created(eng, type, created);
+}
+
+int32_t jy_keys_lookup_mem(jy_engine* eng, int32_t type, uint64_t n, const uint8_t* kb, const uint64_t* ko,
+                           uint32_t* slots, int32_t mem) {
+  JY_TRY(check_type(eng, type));
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (mem == JY_HOST) return keys_host(eng, type, n, kb, ko, slots, false);
+  if (mem != JY_DEVICE) return eng->fail(JY_EINVAL, "mem must be JY_HOST or JY_DEVICE");
+  u64 created = 0;
+  return jy_keydir_run(eng, type, n, kb, reinterpret_cast<const u64*>(ko), slots, false, &created);
 }
 
 uint64_t jy_keys_count(const jy_engine* eng, int32_t type) {
@@ -327,7 +392,7 @@ uint64_t jy_keys_count(const jy_engine* eng, int32_t type) {
 int32_t jy_keys_reserve(jy_engine* eng, int32_t type, uint64_t cap) {
   JY_TRY(check_type(eng, type));
   JY_HIP(eng, hipSetDevice(eng->device));
-  eng->keys[type].map.reserve(cap);
+  JY_TRY(jy_keydir_reserve(eng, type, cap));
   return jy_ensure_slots(eng, type, cap);
 }
 

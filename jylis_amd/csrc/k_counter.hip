@@ -123,9 +123,7 @@ int32_t jy_counter_grow(jy_engine* eng, int which, u32 need_cols, u64 need_slots
   if (ncap == c.ccap && nk == c.kcap && c.slab) return JY_OK;
   void* p = nullptr;
   const u64 bytes = (u64)nsigns * ncap * nk * 8;
-  hipError_t e = hipMalloc(&p, bytes);
-  if (e != hipSuccess)
-    return eng->fail(JY_ENOMEM, "counter slab hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
+  JY_TRY(jy_dev_alloc(eng, &p, bytes, "counter slab"));
   JY_HIP(eng, hipMemsetAsync(p, 0, bytes, eng->stream));
   if (c.slab) {
     for (u32 s = 0; s < nsigns; s++) {
@@ -134,8 +132,7 @@ int32_t jy_counter_grow(jy_engine* eng, int which, u32 need_cols, u64 need_slots
       JY_HIP(eng, hipMemcpy2DAsync(dst, nk * 8, src, c.kcap * 8, c.kcap * 8, c.ccap, hipMemcpyDeviceToDevice,
                                    eng->stream));
     }
-    JY_HIP(eng, hipStreamSynchronize(eng->stream));
-    JY_HIP(eng, hipFree(c.slab));
+    jy_dev_free(eng, c.slab);
   }
   c.slab = static_cast<u64*>(p);
   c.ccap = ncap;

@@ -1,0 +1,375 @@
+// k_keys.hip -- device key directory: String key -> dense slot, gfx950.
+//
+// Replaces the per-type `Map[String, CRDT]` probe of `_data_for(key)`
+// (repo_gcount.pony:36-41; same in every repo_*.pony) -- create on miss --
+// and `_data(key)?` (repo_gcount.pony:53-55) -- look up only.  SURVEY 8f #1.
+//
+// HBM layout per type (KeyDir):
+//   bytes[]      key bytes, appended in slot order
+//   kref[slot]   (byte offset << 24) | length
+//   khash[slot]  64-bit table hash (kept for rehashing)
+//   table[tcap]  open addressing, linear probing, tcap a power of two kept
+//                >= 2x the keys: entry = tag32 << 32 | slot, EMPTY = ~0.
+//                The slot position is the top bits of the hash, the tag its
+//                low 32 bits, so most probes of a foreign key stop at the tag.
+//
+// Interning n keys is deterministic and lock-free (no thread ever waits on
+// another):
+//   K1 probe      every key; found -> its slot; misses counted (+ their bytes)
+//   K2 claim      each missing key probes again; at an EMPTY entry it CASes in
+//                 a PENDING entry carrying its own input index.  A key that
+//                 meets a PENDING entry with its tag compares bytes with that
+//                 input key (input bytes, already in HBM) and joins its group.
+//   K3 first      atomicMin of the input index per group: slots are handed
+//                 out in order of first occurrence in the input, as the host
+//                 map would, whatever order the CASes landed in
+//   scan          ranks of first occurrences, byte offsets of their keys
+//   K4 commit     slot = old count + rank; first occurrences copy their bytes
+//                 and fill kref / khash; claimers turn PENDING into final
+//
+// Roofline: HBM/latency.  Per key: its bytes read twice (hash, compare), one
+// table probe chain (8 B entries), 4 B slot out; a new key adds its bytes +
+// 16 B written.
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "jy_internal.hpp"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr u64 kEmpty = ~0ull;
+constexpr u32 kMiss = 0xFFFFFFFFu;
+constexpr u64 kPending = 0x80000000ull;
+constexpr u64 kIdxMask = 0x7FFFFFFFull;
+
+__device__ __forceinline__ u64 gid() { return (u64)blockIdx.x * kThreads + threadIdx.x; }
+
+// jy_key_owner's hash (FNV-1a 64 + splitmix64 finaliser), remixed so the
+// table position is independent of the owner shard (owner = h mod S would
+// otherwise pin the low bits of every key of a shard)
+__device__ __forceinline__ u64 table_hash(const uint8_t* __restrict__ p, u64 len) {
+  u64 h = 0xCBF29CE484222325ull;
+  for (u64 i = 0; i < len; i++) {
+    h ^= p[i];
+    h *= 0x100000001B3ull;
+  }
+  h ^= h >> 30;
+  h *= 0xBF58476D1CE4E5B9ull;
+  h ^= h >> 27;
+  h *= 0x94D049BB133111EBull;
+  h ^= h >> 31;
+  h += 0x9E3779B97F4A7C15ull;
+  h ^= h >> 30;
+  h *= 0xBF58476D1CE4E5B9ull;
+  h ^= h >> 27;
+  h *= 0x94D049BB133111EBull;
+  h ^= h >> 31;
+  return h;
+}
+
+__device__ __forceinline__ bool bytes_equal(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, u64 n) {
+  for (u64 i = 0; i < n; i++)
+    if (a[i] != b[i]) return false;
+  return true;
+}
+
+struct Dir {
+  const uint8_t* bytes;
+  u64* kref;
+  u64* khash;
+  u64* table;
+  u64 mask;
+  u32 shift;  // 64 - log2(tcap)
+};
+
+struct In {
+  const uint8_t* kb;
+  const u64* ko;
+  u64 n;
+};
+
+__device__ __forceinline__ u32 tag_of(u64 t) { return (u32)t; }
+
+// K1: look every key up; misses counted with their bytes
+__global__ __launch_bounds__(kThreads) void k_key_probe(In I, Dir D, u32* __restrict__ res, u64* __restrict__ th,
+                                                        u64* __restrict__ counts) {
+  const u64 i = gid();
+  if (i >= I.n) return;
+  const uint8_t* k = I.kb + I.ko[i];
+  const u64 len = I.ko[i + 1] - I.ko[i];
+  const u64 t = table_hash(k, len);
+  th[i] = t;
+  u64 p = t >> D.shift;
+  u32 slot = kMiss;
+  for (;;) {
+    const u64 e = D.table[p];
+    if (e == kEmpty) break;
+    if ((u32)(e >> 32) == tag_of(t) && !(e & kPending)) {
+      const u32 s = (u32)(e & kIdxMask);
+      const u64 r = D.kref[s];
+      if ((r & JY_LR_LEN_MASK) == len && bytes_equal(D.bytes + (r >> JY_LR_LEN_BITS), k, len)) {
+        slot = s;
+        break;
+      }
+    }
+    p = (p + 1) & D.mask;
+  }
+  res[i] = slot;
+  if (slot == kMiss) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(counts), 1ull);
+    atomicAdd(reinterpret_cast<unsigned long long*>(counts + 1), (unsigned long long)len);
+    if (len > JY_LR_LEN_MASK) atomicAdd(reinterpret_cast<unsigned long long*>(counts + 2), 1ull);
+  }
+}
+
+// K2: claim an EMPTY entry (PENDING | own index) or join the group of an
+// equal key that claimed first
+__global__ __launch_bounds__(kThreads) void k_key_claim(In I, Dir D, const u32* __restrict__ res,
+                                                        const u64* __restrict__ th, u32* __restrict__ owner,
+                                                        u64* __restrict__ pos) {
+  const u64 i = gid();
+  if (i >= I.n || res[i] != kMiss) return;
+  const uint8_t* k = I.kb + I.ko[i];
+  const u64 len = I.ko[i + 1] - I.ko[i];
+  const u64 t = th[i];
+  const u64 mine = ((u64)tag_of(t) << 32) | kPending | i;
+  u64 p = t >> D.shift;
+  u64 e = D.table[p];
+  for (;;) {
+    if (e == kEmpty) {
+      const u64 prev = atomicCAS(reinterpret_cast<unsigned long long*>(D.table + p), kEmpty, mine);
+      if (prev == kEmpty) {
+        owner[i] = (u32)i;
+        pos[i] = p;
+        return;
+      }
+      e = prev;  // look at what landed here
+      continue;
+    }
+    if ((u32)(e >> 32) == tag_of(t) && (e & kPending)) {
+      const u64 j = e & kIdxMask;
+      const u64 lj = I.ko[j + 1] - I.ko[j];
+      if (lj == len && bytes_equal(I.kb + I.ko[j], k, len)) {
+        owner[i] = (u32)j;
+        return;
+      }
+    }
+    p = (p + 1) & D.mask;
+    e = D.table[p];
+  }
+}
+
+// K3: the first input index of every group
+__global__ __launch_bounds__(kThreads) void k_key_first(u64 n, const u32* __restrict__ res,
+                                                        const u32* __restrict__ owner, u32* __restrict__ first) {
+  const u64 i = gid();
+  if (i >= n || res[i] != kMiss) return;
+  atomicMin(first + owner[i], (u32)i);
+}
+
+__global__ __launch_bounds__(kThreads) void k_key_flags(In I, const u32* __restrict__ res,
+                                                        const u32* __restrict__ owner, const u32* __restrict__ first,
+                                                        u32* __restrict__ flag, u64* __restrict__ blen) {
+  const u64 i = gid();
+  if (i > I.n) return;
+  u32 f = 0;
+  u64 b = 0;
+  if (i < I.n && res[i] == kMiss && first[owner[i]] == (u32)i) {
+    f = 1;
+    b = I.ko[i + 1] - I.ko[i];
+  }
+  flag[i] = f;
+  blen[i] = b;
+}
+
+// K4: slots out; first occurrences store their key; claimers publish
+__global__ __launch_bounds__(kThreads) void k_key_commit(In I, Dir D, uint8_t* __restrict__ dbytes, u64 base_slot,
+                                                         u64 base_byte, const u32* __restrict__ res,
+                                                         const u64* __restrict__ th, const u32* __restrict__ owner,
+                                                         const u64* __restrict__ pos, const u32* __restrict__ first,
+                                                         const u32* __restrict__ rank, const u64* __restrict__ boff,
+                                                         u32* __restrict__ slots) {
+  const u64 i = gid();
+  if (i >= I.n) return;
+  if (res[i] != kMiss) {
+    slots[i] = res[i];
+    return;
+  }
+  const u32 o = owner[i];
+  const u32 f = first[o];
+  const u64 slot = base_slot + rank[f];
+  slots[i] = (u32)slot;
+  if (f == (u32)i) {
+    const u64 len = I.ko[i + 1] - I.ko[i];
+    const u64 at = base_byte + boff[i];
+    const uint8_t* src = I.kb + I.ko[i];
+    for (u64 b = 0; b < len; b++) dbytes[at + b] = src[b];
+    D.kref[slot] = (at << JY_LR_LEN_BITS) | len;
+    D.khash[slot] = th[i];
+  }
+  if (o == (u32)i) D.table[pos[i]] = ((u64)tag_of(th[i]) << 32) | slot;
+}
+
+// lookup only: slots of present keys, JY_NO_SLOT otherwise
+__global__ __launch_bounds__(kThreads) void k_key_copy_res(u64 n, const u32* __restrict__ res, u32* __restrict__ out) {
+  const u64 i = gid();
+  if (i < n) out[i] = res[i];
+}
+
+// rebuild the table from the per-slot hashes
+__global__ __launch_bounds__(kThreads) void k_key_rehash(Dir D, u64 nk) {
+  const u64 s = gid();
+  if (s >= nk) return;
+  const u64 t = D.khash[s];
+  const u64 e = ((u64)tag_of(t) << 32) | s;
+  u64 p = t >> D.shift;
+  while (atomicCAS(reinterpret_cast<unsigned long long*>(D.table + p), kEmpty, e) != kEmpty) p = (p + 1) & D.mask;
+}
+
+u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kThreads - 1) / kThreads); }
+
+#define LAUNCH(k, n, ...)                                                                          \
+  do {                                                                                             \
+    hipLaunchKernelGGL(k, dim3(blocks_for(n)), dim3(kThreads), 0, eng->stream, __VA_ARGS__);     \
+    JY_HIP(eng, hipGetLastError());                                                                \
+  } while (0)
+
+Dir dir_of(KeyDir& K) {
+  Dir D;
+  D.bytes = K.bytes;
+  D.kref = K.kref;
+  D.khash = K.khash;
+  D.table = K.table;
+  D.mask = K.tcap - 1;
+  D.shift = 64 - K.lg;
+  return D;
+}
+
+int32_t grow_table(jy_engine* eng, KeyDir& K, u64 need_keys) {
+  u64 want = 1024;
+  u32 lg = 10;
+  while (want < 2 * need_keys) {
+    want <<= 1;
+    lg++;
+  }
+  if (K.table && want <= K.tcap) return JY_OK;
+  jy_dev_free(eng, K.table);
+  K.table = nullptr;
+  JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&K.table), want * 8, "key table"));
+  K.tcap = want;
+  K.lg = lg;
+  JY_HIP(eng, hipMemsetAsync(K.table, 0xFF, want * 8, eng->stream));
+  if (K.n) LAUNCH(k_key_rehash, K.n, dir_of(K), K.n);
+  return JY_OK;
+}
+
+int32_t grow_slots(jy_engine* eng, KeyDir& K, u64 need) {
+  if (need <= K.scap && K.kref) return JY_OK;
+  const u64 nc = std::max<u64>(std::max<u64>(need, K.scap * 2), 1024);
+  void* a = K.kref;
+  JY_TRY(jy_realloc(eng, &a, K.n * 8, nc * 8, false));
+  K.kref = static_cast<u64*>(a);
+  void* b = K.khash;
+  JY_TRY(jy_realloc(eng, &b, K.n * 8, nc * 8, false));
+  K.khash = static_cast<u64*>(b);
+  K.scap = nc;
+  return JY_OK;
+}
+
+int32_t grow_bytes(jy_engine* eng, KeyDir& K, u64 need) {
+  if (need <= K.bcap && K.bytes) return JY_OK;
+  const u64 nc = std::max<u64>(std::max<u64>(need, K.bcap * 2), 1 << 16);
+  void* a = K.bytes;
+  JY_TRY(jy_realloc(eng, &a, K.blen, nc, false));
+  K.bytes = static_cast<uint8_t*>(a);
+  K.bcap = nc;
+  return JY_OK;
+}
+
+}  // namespace
+
+int32_t jy_keydir_reserve(jy_engine* eng, int32_t type, u64 cap) {
+  KeyDir& K = eng->kdir[type];
+  JY_TRY(grow_slots(eng, K, cap));
+  return grow_table(eng, K, cap);
+}
+
+void jy_keydir_free(jy_engine* eng, KeyDir& K) {
+  for (void* p : {static_cast<void*>(K.bytes), static_cast<void*>(K.kref), static_cast<void*>(K.khash),
+                  static_cast<void*>(K.table)})
+    jy_dev_free(eng, p);
+  K = KeyDir{};
+}
+
+// Device interning / lookup of n keys (device pointers).  Returns the number
+// of keys created in *created.  Synchronises (the host must know the new
+// key count before any call sizes work by it).
+int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, const u64* ko, u32* slots, bool create,
+                      u64* created) {
+  *created = 0;
+  if (n == 0) return JY_OK;
+  if (n >= kIdxMask) return eng->fail(JY_ERANGE, "too many keys in one call");
+  KeyDir& K = eng->kdir[type];
+  JY_TRY(grow_slots(eng, K, std::max<u64>(K.n, 1)));
+  JY_TRY(grow_table(eng, K, std::max<u64>(K.n, 1)));
+  void* p;
+  JY_TRY(jy_scratch(eng, 20, n * 4 + n * 8 + 64, &p));
+  u32* res = static_cast<u32*>(p);
+  u64* th = reinterpret_cast<u64*>((reinterpret_cast<uintptr_t>(res + n) + 15) & ~uintptr_t(15));
+  u64* counts = th + n;  // [3] misses, their bytes, oversized keys
+  In I{kb, ko, n};
+  JY_HIP(eng, hipMemsetAsync(counts, 0, 24, eng->stream));
+  LAUNCH(k_key_probe, n, I, dir_of(K), res, th, counts);
+  u64 hc[3];
+  JY_HIP(eng, hipMemcpyAsync(hc, counts, 24, hipMemcpyDeviceToHost, eng->stream));
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  const u64 m = hc[0], mbytes = hc[1];
+  if (!create || m == 0) {
+    LAUNCH(k_key_copy_res, n, n, res, slots);
+    return JY_OK;
+  }
+  if (hc[2]) return eng->fail(JY_ERANGE, "key longer than 16 MiB");
+  if (K.n + m >= kIdxMask) return eng->fail(JY_ERANGE, "slot space exhausted");
+  JY_TRY(grow_table(eng, K, K.n + m));
+  JY_TRY(grow_slots(eng, K, K.n + m));
+  JY_TRY(grow_bytes(eng, K, K.blen + mbytes));
+  JY_TRY(jy_scratch(eng, 21, n * 16 + 64, &p));
+  u32* owner = static_cast<u32*>(p);
+  u32* first = owner + n;
+  u64* pos = reinterpret_cast<u64*>((reinterpret_cast<uintptr_t>(first + n) + 15) & ~uintptr_t(15));
+  JY_TRY(jy_scratch(eng, 22, (n + 1) * 8 + 64, &p));
+  u32* flag = static_cast<u32*>(p);
+  u32* rank = flag + n + 1;
+  JY_TRY(jy_scratch(eng, 23, (n + 1) * 16 + 64, &p));
+  u64* blen = static_cast<u64*>(p);
+  u64* boff = blen + n + 1;
+  const Dir D = dir_of(K);
+  JY_HIP(eng, hipMemsetAsync(first, 0xFF, n * 4, eng->stream));
+  LAUNCH(k_key_claim, n, I, D, res, th, owner, pos);
+  LAUNCH(k_key_first, n, n, res, owner, first);
+  LAUNCH(k_key_flags, n + 1, I, res, owner, first, flag, blen);
+  size_t tmp = 0;
+  JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, flag, rank, (int)(n + 1), eng->stream));
+  JY_TRY(jy_scratch(eng, 15, tmp, &p));
+  JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(p, tmp, flag, rank, (int)(n + 1), eng->stream));
+  tmp = 0;
+  JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, blen, boff, (int)(n + 1), eng->stream));
+  JY_TRY(jy_scratch(eng, 15, tmp, &p));
+  JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(p, tmp, blen, boff, (int)(n + 1), eng->stream));
+  LAUNCH(k_key_commit, n, I, D, K.bytes, K.n, K.blen, res, th, owner, pos, first, rank, boff, slots);
+  u32 nnew = 0;
+  u64 nbytes = 0;
+  JY_HIP(eng, hipMemcpyAsync(&nnew, rank + n, 4, hipMemcpyDeviceToHost, eng->stream));
+  JY_HIP(eng, hipMemcpyAsync(&nbytes, boff + n, 8, hipMemcpyDeviceToHost, eng->stream));
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  K.n += nnew;
+  K.blen += nbytes;
+  *created = nnew;
+  return JY_OK;
+}

@@ -103,17 +103,17 @@ __device__ __forceinline__ void store_rec(TRec* __restrict__ p, u64 ts, u64 pre,
 // per-key record for the state-side scatter: one line instead of six
 // scattered per-key arrays
 struct KeyInfo {
-  u64 shift;     // new_off[s] - off[s]
-  u64 keep_end;  // off[s] + surviving prefix length
-  u64 lo;        // off[s]
+  u64 lo;        // off[s]: the state segment (its surviving prefix is what the output holds)
   u64 blo, bhi;  // delta segment (empty if none)
-  u64 scan_lo;   // scan_b[blo]
+  u32 scan_lo;   // scan_b[blo]
+  u32 front;     // every delta entry is kept and precedes the whole state
 };
 
 // per delta key: its state segment, merged cutoff and whether it merges
 struct DInfo {
   u64 lo, hi;  // state segment [off[s], off[s+1])
   u64 cut;     // max(state cutoff, delta cutoff)
+  u64 newest;  // ts of the state's first (newest) entry (any value if empty)
   u32 s;       // slot
   u32 raised;  // the delta raises the cutoff (else no state entry drops:
                // every state entry already has ts >= the state cutoff)
@@ -124,6 +124,7 @@ struct TlogArgs {
   const u64* off;
   const TRec* rec;
   u64* cutoff;
+  u64* newest;
   u64 nkeys, na;
   // delta batch
   u64 nd, nb;
@@ -140,23 +141,33 @@ struct TlogArgs {
   u32* bad;     // [nd]
   DInfo* dinfo;  // [nd]
   u64* keep_a;  // [nkeys] surviving state entries: a prefix of every log
-  u64* flag_b;  // [nb + 1]
-  u64* scan_b;  // [nb + 1]
+  u32* flag_b;  // [nb + 1]
+  u32* scan_b;  // [nb + 1]
   u32* prel;    // [nb] state entries of the key ordered before the delta entry
+  u32* slow;       // [nb] 1: the delta entry needs the full search
+  u32* slow_list;  // [nb] those entries, compacted (count at slow_n)
+  u32* slow_n;
   KeyInfo* info;  // [nkeys]
 };
 
+// per delta key.  A slot named twice in one device batch breaks the
+// one-delta-per-key contract: both deltas are skipped (counted), the key is
+// left untouched.  bad[] and dptr[] are cleared before this launch.
 __global__ __launch_bounds__(kThreads) void k_tlog_prep(TlogArgs A) {
   const u64 k = gid();
   if (k >= A.nd) return;
   const u64 s = A.slot[k];
-  A.dptr[s] = (u32)k;
-  A.bad[k] = 0;
+  const u32 prev = atomicCAS(A.dptr + s, kNone, (u32)k);
+  if (prev != kNone) {
+    A.bad[k] = 1;
+    A.bad[prev] = 1;
+  }
   const u64 cs = A.cutoff[s], cd = A.dcut[k];
   DInfo D;
   D.lo = A.off[s];
   D.hi = A.off[s + 1];
   D.cut = cs > cd ? cs : cd;
+  D.newest = A.newest[s];
   D.s = (u32)s;
   D.raised = cd > cs;
   A.dinfo[k] = D;
@@ -181,6 +192,10 @@ __device__ __forceinline__ u32 merging_key(const TlogArgs& A, u64 s) {
 // keep flag of every delta entry and its rank among the state entries.
 // prel is non-decreasing along a delta segment: entries dropped by the
 // cutoff are its tail and take the segment length.
+// keep flag and state rank of every delta entry.  The usual entry is newer
+// than its whole log: rank 0, kept, no search.  Entries that need the full
+// search (ties with the newest entry, older entries, duplicates) go to a
+// worklist so waves of the common case never wait on a searching lane.
 __global__ __launch_bounds__(kThreads) void k_tlog_flag_b(TlogArgs A) {
   const u64 j = gid();
   if (j > A.nb) return;
@@ -190,26 +205,35 @@ __global__ __launch_bounds__(kThreads) void k_tlog_flag_b(TlogArgs A) {
   }
   const u32 k = A.dseg[j];
   const DInfo D = A.dinfo[k];
-  u64 keep = 0;
-  const u64 lo = D.lo, hi = D.hi;
-  u64 p = hi;
   const u64 t = A.dts[j];
-  if (t >= D.cut && !A.bad[k] && A.dptr[D.s] == k) {
-    const Ent x{t, A.dpre[j], A.dlr[j]};
-    // fast path: new log entries are usually newer than the whole state
-    const int c0 = lo < hi ? cmp_at(A.rec, lo, x, A.arena) : -1;
-    if (c0 < 0) {
-      p = lo;
+  bool slow = false;
+  u32 keep = 0;
+  u64 p = D.hi;
+  if (t >= D.cut && !A.bad[k]) {
+    if (D.lo == D.hi || t > D.newest) {
+      p = D.lo;
       keep = 1;
-    } else if (c0 == 0) {
-      p = lo;
     } else {
-      p = lower_bound_entry(A.rec, lo + 1, hi, x, A.arena);
-      keep = !(p < hi && cmp_at(A.rec, p, x, A.arena) == 0);
+      slow = true;
     }
   }
-  A.flag_b[j] = keep;
-  A.prel[j] = (u32)(p - lo);
+  A.slow[j] = slow;  // compacted into the worklist by DeviceSelect
+  if (!slow) {
+    A.flag_b[j] = keep;
+    A.prel[j] = (u32)(p - D.lo);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_tlog_flag_slow(TlogArgs A) {
+  const u32 n = *A.slow_n;
+  for (u64 w = gid(); w < n; w += (u64)gridDim.x * kThreads) {
+    const u32 j = A.slow_list[w];
+    const DInfo D = A.dinfo[A.dseg[j]];
+    const Ent x{A.dts[j], A.dpre[j], A.dlr[j]};
+    const u64 p = lower_bound_entry(A.rec, D.lo, D.hi, x, A.arena);
+    A.flag_b[j] = !(p < D.hi && cmp_at(A.rec, p, x, A.arena) == 0);
+    A.prel[j] = (u32)(p - D.lo);
+  }
 }
 
 __global__ __launch_bounds__(kThreads) void k_tlog_sizes_out(TlogArgs A, u64* __restrict__ cnt) {
@@ -241,8 +265,7 @@ __global__ __launch_bounds__(kThreads) void k_tlog_sizes_out(TlogArgs A, u64* __
 
 // per slot: the state-side scatter record; merged cutoff stored; malformed
 // deltas counted
-__global__ __launch_bounds__(kThreads) void k_tlog_info(TlogArgs A, const u64* __restrict__ noff,
-                                                        unsigned long long* __restrict__ skipped) {
+__global__ __launch_bounds__(kThreads) void k_tlog_info(TlogArgs A, unsigned long long* __restrict__ skipped) {
   const u64 s = gid();
   if (s >= A.nkeys) return;
   u32 k = A.dptr[s];
@@ -256,44 +279,110 @@ __global__ __launch_bounds__(kThreads) void k_tlog_info(TlogArgs A, const u64* _
   }
   KeyInfo I;
   I.lo = A.off[s];
-  I.shift = noff[s] - I.lo;
-  I.keep_end = I.lo + A.keep_a[s];
   I.blo = k == kNone ? 0 : A.doff[k];
   I.bhi = k == kNone ? 0 : A.doff[k + 1];
   I.scan_lo = A.scan_b[I.blo];
+  I.front = I.bhi > I.blo && A.prel[I.bhi - 1] == 0 && A.scan_b[I.bhi] - I.scan_lo == I.bhi - I.blo;
   A.info[s] = I;
 }
 
-// every surviving state entry: new position = old + key shift + kept delta
-// entries ordered before it (those whose state rank is <= its own)
-__global__ __launch_bounds__(kThreads) void k_tlog_scatter_a(TlogArgs A, TRec* __restrict__ out) {
-  const u64 i = gid();
-  if (i >= A.na) return;
-  const TRec r = load_rec(A.rec + i);
-  const KeyInfo I = A.info[r.seg];
-  if (i >= I.keep_end) return;
-  u64 pos = i + I.shift;
-  if (I.bhi > I.blo) {
-    const u32 rr = (u32)(i - I.lo);
-    u64 lo = I.blo, hi = I.bhi;
+// Output-parallel write of the merged logs.  A workgroup owns a fixed range
+// of kTileOut output positions (so a skewed log costs its size, never a
+// straggler), finds the keys of its range once (noff staged in LDS), and
+// every lane resolves its output position r of key s to its source:
+//   o_j = (kept deltas before j) + prel_j is non-decreasing over the key's
+//   delta segment; c = #kept deltas with o_j <= r.  Position r holds the
+//   kept delta of kept-rank c-1 if that one has o == r, else state entry
+//   r - c (always inside the surviving prefix).
+// Writes are one contiguous 32-B record stream per workgroup.
+constexpr u32 kTileOut = 4096;
+constexpr u32 kTileKeys = 2048;
+
+__global__ __launch_bounds__(kThreads) void k_tlog_gather_out(TlogArgs A, const u64* __restrict__ noff,
+                                                              TRec* __restrict__ out) {
+  __shared__ u64 loff[kTileKeys + 2];
+  __shared__ u64 sb_sh, se_sh;
+  const u64 nk = A.nkeys;
+  const u64 total = noff[nk];
+  const u64 t0 = (u64)blockIdx.x * kTileOut;
+  if (t0 >= total) return;
+  const u64 t1 = t0 + kTileOut < total ? t0 + kTileOut : total;
+  if (threadIdx.x == 0) {
+    // last s with noff[s] <= x, over [0, nk]
+    u64 lo = 0, hi = nk + 1;
     while (lo < hi) {
       const u64 m = (lo + hi) >> 1;
-      if (A.prel[m] <= rr) lo = m + 1;
+      if (noff[m] <= t0) lo = m + 1;
       else hi = m;
     }
-    pos += A.scan_b[lo] - I.scan_lo;
+    sb_sh = lo - 1;
+    hi = nk + 1;
+    while (lo < hi) {
+      const u64 m = (lo + hi) >> 1;
+      if (noff[m] <= t1 - 1) lo = m + 1;
+      else hi = m;
+    }
+    se_sh = lo - 1;
   }
-  store_rec(out + pos, r.ts, r.pre, r.lr, r.seg);
-}
-
-__global__ __launch_bounds__(kThreads) void k_tlog_scatter_b(TlogArgs A, const u64* __restrict__ noff,
-                                                             TRec* __restrict__ out) {
-  const u64 j = gid();
-  if (j >= A.nb || !A.flag_b[j]) return;
-  const u32 k = A.dseg[j];
-  const u32 s = A.dinfo[k].s;
-  const u64 pos = noff[s] + (A.scan_b[j] - A.scan_b[A.doff[k]]) + A.prel[j];
-  store_rec(out + pos, A.dts[j], A.dpre[j], A.dlr[j], s);
+  __syncthreads();
+  const u64 sb = sb_sh, se = se_sh;
+  const bool local = se - sb + 2 <= kTileKeys + 2;
+  if (local)
+    for (u64 q = threadIdx.x; q < se - sb + 2; q += kThreads) loff[q] = noff[sb + q];
+  __syncthreads();
+  for (u64 t = t0 + threadIdx.x; t < t1; t += kThreads) {
+    u64 lo = 0, hi = se - sb + 1;  // last q in [0, se-sb] with off(q) <= t
+    while (lo < hi) {
+      const u64 m = (lo + hi + 1) >> 1;
+      const u64 v = local ? loff[m] : noff[sb + m];
+      if (v <= t) lo = m;
+      else hi = m - 1;
+    }
+    const u64 s = sb + lo;
+    const u64 r = t - (local ? loff[lo] : noff[s]);
+    const KeyInfo I = A.info[s];
+    u64 a = r;
+    if (I.front) {
+      // every delta entry kept, all before the state: deltas, then the state
+      const u64 K = I.bhi - I.blo;
+      if (r < K) {
+        const u64 j = I.blo + r;
+        if (r == 0) A.newest[s] = A.dts[j];
+        store_rec(out + t, A.dts[j], A.dpre[j], A.dlr[j], (u32)s);
+        continue;
+      }
+      a = r - K;
+    } else if (I.bhi > I.blo) {
+      u64 l = I.blo, h = I.bhi;  // jj: first j with o_j > r
+      while (l < h) {
+        const u64 m = (l + h) >> 1;
+        if ((u64)(A.scan_b[m] - (u32)I.scan_lo) + A.prel[m] <= r) l = m + 1;
+        else h = m;
+      }
+      const u64 jj = l;
+      const u64 c = A.scan_b[jj] - (u32)I.scan_lo;
+      if (c > 0) {
+        // the kept delta of kept-rank c-1: last j in [blo, jj) with scan_b[j] < scan_lo + c
+        l = I.blo;
+        h = jj;
+        while (l < h) {
+          const u64 m = (l + h) >> 1;
+          if ((u64)(A.scan_b[m] - (u32)I.scan_lo) < c) l = m + 1;
+          else h = m;
+        }
+        const u64 jk = l - 1;
+        if (c - 1 + A.prel[jk] == r) {
+          if (r == 0) A.newest[s] = A.dts[jk];
+          store_rec(out + t, A.dts[jk], A.dpre[jk], A.dlr[jk], (u32)s);
+          continue;
+        }
+      }
+      a = r - c;
+    }
+    const TRec x = load_rec(A.rec + I.lo + a);
+    if (r == 0) A.newest[s] = x.ts;
+    store_rec(out + t, x.ts, x.pre, x.lr, (u32)s);
+  }
 }
 
 __global__ __launch_bounds__(kThreads) void k_fill_tail(u64* __restrict__ off, u64 from, u64 to) {
@@ -341,14 +430,11 @@ u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kThreads - 1) / kThrea
   } while (0)
 
 int32_t realloc_dead(jy_engine* eng, void** p, u64 bytes) {
-  if (*p) {
-    JY_HIP(eng, hipStreamSynchronize(eng->stream));
-    JY_HIP(eng, hipFree(*p));
-    *p = nullptr;
-  }
-  hipError_t e = hipMalloc(p, bytes);
-  if (e != hipSuccess) return eng->fail(JY_ENOMEM, std::string("tlog entries: ") + hipGetErrorString(e));
-  return JY_OK;
+  // the buffer's contents are dead (it is rewritten): stream-ordered free
+  JY_TRACE("tlog entries realloc %llu bytes", (unsigned long long)bytes);
+  jy_dev_free(eng, *p);
+  *p = nullptr;
+  return jy_dev_alloc(eng, p, bytes, "tlog entries");
 }
 
 }  // namespace
@@ -395,6 +481,9 @@ int32_t jy_tlog_grow(jy_engine* eng, u64 need) {
   void* c = t.cutoff;
   JY_TRY(jy_realloc(eng, &c, t.kcap * 8, nk * 8, true));
   t.cutoff = static_cast<u64*>(c);
+  void* w = t.newest;
+  JY_TRY(jy_realloc(eng, &w, t.kcap * 8, nk * 8, true));
+  t.newest = static_cast<u64*>(w);
   for (int b = 0; b < 2; b++) {
     void* o = t.off[b];
     JY_TRY(jy_realloc(eng, &o, t.kcap ? (t.kcap + 1) * 8 : 0, (nk + 1) * 8, true));
@@ -418,9 +507,20 @@ int32_t jy_tlog_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* dcut, 
   TlogState& t = eng->tlog;
   const u64 nk = eng->nkeys[JY_TLOG];
   if (nd == 0 || nk == 0) return JY_OK;
-  // exact live entry count of the current buffer: the previous merge's total
-  JY_HIP(eng, hipEventSynchronize(eng->total_ready));
-  const u64 na = t.nent_known ? eng->pin_total[0] : 0;
+  if (nent >= (1ull << 31)) return eng->fail(JY_ERANGE, "tlog converge: more than 2^31 entries in one call");
+  // live entries of the current buffer: exact when the previous merge's
+  // total has landed (non-blocking query), else the host upper bound; the
+  // kernels take the exact count from off[nkeys] in HBM.  The host never
+  // waits for the GPU here, so merges queue back to back.
+  const double t_enter = jy_tracing() ? jy_now_us() : 0;
+  u64 na = 0;
+  if (t.nent_known) {
+    const hipError_t q = hipEventQuery(eng->total_ready);
+    if (q == hipSuccess) na = eng->pin_total[0];
+    else if (q == hipErrorNotReady) na = t.nent_bound;
+    else JY_HIP(eng, q);
+  }
+  const double t_synced = jy_tracing() ? jy_now_us() : 0;
   const int cur = t.cur, nxt = 1 - cur;
   JY_TRY(ensure_entries(eng, nxt, na + nent));
 
@@ -428,6 +528,7 @@ int32_t jy_tlog_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* dcut, 
   A.off = t.off[cur];
   A.rec = t.rec[cur];
   A.cutoff = t.cutoff;
+  A.newest = t.newest;
   A.nkeys = nk;
   A.na = na;
   A.nd = nd;
@@ -447,10 +548,13 @@ int32_t jy_tlog_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* dcut, 
   A.bad = reinterpret_cast<u32*>(A.dinfo + nd);
   JY_TRY(jy_scratch(eng, 11, nk * 8, &p));
   A.keep_a = static_cast<u64*>(p);
-  JY_TRY(jy_scratch(eng, 12, (nent + 1) * 20, &p));
-  A.flag_b = static_cast<u64*>(p);
+  JY_TRY(jy_scratch(eng, 12, (nent + 1) * 20 + 16, &p));
+  A.flag_b = static_cast<u32*>(p);
   A.scan_b = A.flag_b + nent + 1;
-  A.prel = reinterpret_cast<u32*>(A.scan_b + nent + 1);
+  A.prel = A.scan_b + nent + 1;
+  A.slow = A.prel + nent + 1;
+  A.slow_list = A.slow + nent + 1;
+  A.slow_n = A.slow_list + nent + 1;
   JY_TRY(jy_scratch(eng, 16, (nk + 1) * 8, &p));
   u64* cnt = static_cast<u64*>(p);
   JY_TRY(jy_scratch(eng, 18, nk * sizeof(KeyInfo), &p));
@@ -460,19 +564,43 @@ int32_t jy_tlog_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* dcut, 
   JY_TRY(jy_seg_ids(eng, doff, nd, nent, static_cast<u32*>(p)));
 
   JY_HIP(eng, hipMemsetAsync(A.dptr, 0xFF, nk * 4, eng->stream));
+  JY_HIP(eng, hipMemsetAsync(A.bad, 0, nd * 4, eng->stream));
   LAUNCH(k_tlog_prep, nd, A);
   if (nent) LAUNCH(k_tlog_validate, nent, A);
   LAUNCH(k_tlog_flag_b, nent + 1, A);
-  JY_TRY(jy_scan_u64(eng, A.flag_b, A.scan_b, nent));
+  if (nent) {
+    size_t tmp = 0;
+    hipcub::CountingInputIterator<u32> idx(0);
+    JY_HIP(eng, hipcub::DeviceSelect::Flagged(nullptr, tmp, idx, A.slow, A.slow_list, A.slow_n, (int)nent,
+                                              eng->stream));
+    JY_TRY(jy_scratch(eng, 15, tmp, &p));
+    JY_HIP(eng, hipcub::DeviceSelect::Flagged(p, tmp, idx, A.slow, A.slow_list, A.slow_n, (int)nent, eng->stream));
+    const u32 g = (u32)std::min<u64>(2048, (nent + kThreads - 1) / kThreads);
+    hipLaunchKernelGGL(k_tlog_flag_slow, dim3(g), dim3(kThreads), 0, eng->stream, A);
+    JY_HIP(eng, hipGetLastError());
+  }
+  {
+    size_t tmp = 0;
+    JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, A.flag_b, A.scan_b, (int)(nent + 1), eng->stream));
+    JY_TRY(jy_scratch(eng, 15, tmp, &p));
+    JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(p, tmp, A.flag_b, A.scan_b, (int)(nent + 1), eng->stream));
+  }
   LAUNCH(k_tlog_sizes_out, nk + 1, A, cnt);
   JY_TRY(jy_scan_u64(eng, cnt, t.off[nxt], nk));
-  LAUNCH(k_tlog_info, nk, A, t.off[nxt], reinterpret_cast<unsigned long long*>(eng->skipped_dev));
-  if (na) LAUNCH(k_tlog_scatter_a, na, A, t.rec[nxt]);
-  if (nent) LAUNCH(k_tlog_scatter_b, nent, A, t.off[nxt], t.rec[nxt]);
+  LAUNCH(k_tlog_info, nk, A, reinterpret_cast<unsigned long long*>(eng->skipped_dev));
+  {
+    // output size bound: surviving state + kept delta <= na + nent
+    const u64 nout = na + nent;
+    const u32 tiles = (u32)std::max<u64>(1, (nout + kTileOut - 1) / kTileOut);
+    hipLaunchKernelGGL(k_tlog_gather_out, dim3(tiles), dim3(kThreads), 0, eng->stream, A, t.off[nxt], t.rec[nxt]);
+    JY_HIP(eng, hipGetLastError());
+  }
   // publish the new total for the next call (read back asynchronously)
   JY_HIP(eng, hipMemcpyAsync(eng->pin_total, t.off[nxt] + nk, 8, hipMemcpyDeviceToHost, eng->stream));
   JY_HIP(eng, hipEventRecord(eng->total_ready, eng->stream));
+  if (jy_tracing()) JY_TRACE("tlog merge host: wait %.1f us, issue %.1f us", t_synced - t_enter, jy_now_us() - t_synced);
   t.nent_known = true;
+  t.nent_bound = na + nent;
   t.cur = nxt;
   return JY_OK;
 }

@@ -220,7 +220,7 @@ __global__ __launch_bounds__(kThreads) void k_uj_drop_bad(UjArgs A) {
 
 // ---- P3: keep flags: state elements, delta elements, delta cloud dedupe ------------
 __device__ __forceinline__ void flag_a(const UjArgs& A, u64 i) {
-  if (i == A.na) {
+  if (i >= A.eoff[A.nkeys]) {  // A.na is a host bound; eoff[nkeys] is exact
     A.flag_a[i] = 0;
     return;
   }
@@ -274,7 +274,7 @@ __global__ __launch_bounds__(kThreads) void k_uj_flags(UjArgs A, Ranges G) {
 // union rank of x (column c, seq q) above v: state dots of c in (v, q) plus
 // de-duplicated delta dots of c in (v, q)
 __device__ __forceinline__ void compact_a(const UjArgs& A, u64 i) {
-  if (i == A.ca) {
+  if (i >= A.coff[A.nkeys]) {  // A.ca is a host bound; coff[nkeys] is exact
     A.keep_ca[i] = 0;
     return;
   }
@@ -501,15 +501,11 @@ __global__ __launch_bounds__(kThreads) void k_uj_gather(const u64* __restrict__ 
 u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kThreads - 1) / kThreads); }
 
 int32_t realloc_dead(jy_engine* eng, void** p, u64 bytes) {
-  // the target buffer's contents are dead (it is rewritten)
-  if (*p) {
-    JY_HIP(eng, hipStreamSynchronize(eng->stream));
-    JY_HIP(eng, hipFree(*p));
-    *p = nullptr;
-  }
-  hipError_t e = hipMalloc(p, bytes);
-  if (e != hipSuccess) return eng->fail(JY_ENOMEM, std::string("ujson buffers: ") + hipGetErrorString(e));
-  return JY_OK;
+  // the buffer's contents are dead (it is rewritten): stream-ordered free
+  JY_TRACE("ujson buffers realloc %llu bytes", (unsigned long long)bytes);
+  jy_dev_free(eng, *p);
+  *p = nullptr;
+  return jy_dev_alloc(eng, p, bytes, "ujson buffers");
 }
 
 int32_t ensure_elems(jy_engine* eng, int b, u64 need) {
@@ -594,12 +590,27 @@ int32_t jy_ujson_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* deoff
   const u64 nk = eng->nkeys[JY_UJSON];
   if (nd == 0 || nk == 0) return JY_OK;
   if (nd >= (1ull << kSegBits)) return eng->fail(JY_ERANGE, "ujson converge: more than 2^28 documents in one call");
-  // exact live sizes of the current buffers (the previous merge's totals)
-  JY_HIP(eng, hipEventSynchronize(eng->total_ready));
-  const u64 na = u.known ? eng->pin_total[1] : 0;
-  const u64 ca = u.known ? eng->pin_total[2] : 0;
-  if (na + nel + ncloud + 3 >= (1ull << 32) || ca + ncloud + 2 >= (1ull << 32))
-    return eng->fail(JY_ERANGE, "ujson converge: more than 2^32 elements in one shard");
+  // live sizes of the current buffers: exact when the previous merge's
+  // totals have landed (non-blocking query), else host upper bounds; the
+  // kernels take the exact counts from eoff/coff[nkeys] in HBM, so the host
+  // never waits for the GPU here
+  const double t_enter = jy_tracing() ? jy_now_us() : 0;
+  u64 na = 0, ca = 0;
+  if (u.known) {
+    const hipError_t q = hipEventQuery(eng->total_ready);
+    if (q == hipSuccess) {
+      na = eng->pin_total[1];
+      ca = eng->pin_total[2];
+    } else if (q == hipErrorNotReady) {
+      na = u.nel_bound;
+      ca = u.ncloud_bound;
+    } else {
+      JY_HIP(eng, q);
+    }
+  }
+  const double t_synced = jy_tracing() ? jy_now_us() : 0;
+  if (na + nel + ncloud + 3 >= (1ull << 31) || ca + ncloud + 2 >= (1ull << 31))
+    return eng->fail(JY_ERANGE, "ujson converge: more than 2^31 elements in one shard");
   const int cur = u.cur, nxt = 1 - cur;
   JY_TRY(ensure_elems(eng, nxt, na + nel));
   JY_TRY(ensure_cloud(eng, nxt, ca + ncloud));
@@ -710,7 +721,10 @@ int32_t jy_ujson_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* deoff
   JY_TRY(launch_ranges(k_uj_scatter, ranges({nd * R, na, nel, ca, ncloud}), A, O));
   JY_HIP(eng, hipMemcpyAsync(eng->pin_total + 1, totals_dev, 16, hipMemcpyDeviceToHost, eng->stream));
   JY_HIP(eng, hipEventRecord(eng->total_ready, eng->stream));
+  if (jy_tracing()) JY_TRACE("ujson merge host: wait %.1f us, issue %.1f us", t_synced - t_enter, jy_now_us() - t_synced);
   u.known = true;
+  u.nel_bound = na + nel;
+  u.ncloud_bound = ca + ncloud;
   u.cur = nxt;
   return JY_OK;
 }

@@ -156,6 +156,16 @@ class Engine:
         self._check(self.lib.jy_keys_lookup(self.h, ctype, n, kb.ctypes.data, ko.ctypes.data, out.ctypes.data))
         return out
 
+    def intern_device(self, ctype, key_bytes, key_offs, create=True):
+        """bulk interning with keys already in HBM: key_bytes (uint8) and
+        key_offs (int64/uint64, n+1) CUDA tensors -> int32 CUDA tensor of slots"""
+        import torch
+        n = int(key_offs.numel()) - 1
+        out = torch.empty(max(n, 1), dtype=torch.int32, device=key_offs.device)
+        fn = self.lib.jy_keys_intern_mem if create else self.lib.jy_keys_lookup_mem
+        self._check(fn(self.h, ctype, n, key_bytes.data_ptr(), key_offs.data_ptr(), out.data_ptr(), DEVICE))
+        return out[:n]
+
     def nkeys(self, ctype):
         return int(self.lib.jy_keys_count(self.h, ctype))
 
