@@ -15,9 +15,11 @@ import numpy as np
 HBM_PEAK_GBS = 8000.0
 
 
-def _timed(steps, warmup, step, dist, dev):
-    """warmup, then exactly `steps` steps bracketed by barrier + synchronize;
-    per-step HIP events on the current (engine) stream"""
+def _timed(steps, warmup, step, dist, dev, eng=None):
+    """warmup, then exactly `steps` steps bracketed by barrier + synchronize.
+    Per-step device time: with `eng`, the engine's own HIP events around each
+    merge call's device work (jy_timing_enable; host launch gaps excluded),
+    summed per step; otherwise torch events on the current (engine) stream."""
     import torch
     for i in range(warmup):
         step(i)
@@ -26,6 +28,8 @@ def _timed(steps, warmup, step, dist, dev):
         dist.barrier()
     torch.cuda.synchronize(dev)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if eng is not None:
+        eng.timing(True)
     host = []
     t0 = time.perf_counter()
     for i in range(steps):
@@ -41,6 +45,11 @@ def _timed(steps, warmup, step, dist, dev):
     elapsed = time.perf_counter() - t0
     if os.environ.get("JY_TRACE"):
         print("host s per step:", " ".join(f"{h * 1e3:.3f}ms" for h in host), file=sys.stderr)
+    if eng is not None:
+        calls = eng.timing_read()
+        eng.timing(False)
+        per_step = float(np.sum(calls)) / 1e3 / steps
+        return elapsed, [per_step] * steps
     return elapsed, [a.elapsed_time(b) / 1e3 for a, b in evs]
 
 
@@ -164,7 +173,7 @@ def bench_gcount(args, eng, dev, dist, rank, world):
         ds.append(d)
         prev = d
     elapsed, kt = _timed(args.steps, args.warmup, lambda i: eng.gcount_converge_block(cols, 0, ds[i % nb][0]),
-                         dist, dev)
+                         dist, dev, eng=eng)
     t = _max_over_ranks(elapsed, dist, dev)
     cells = R * K
     k = float(np.mean(kt))
@@ -225,10 +234,13 @@ def bench_treg(args, eng, dev, dist, rank, world):
     setup_s = time.perf_counter() - t0
     n = len(slot)
     batches = []
-    for j in range(max(1, args.batches) + 1):  # batch 0 = initial state
+    # batch 0 = initial state; a distinct batch for every step (no replays)
+    for j in range(max(1, args.batches, args.warmup + args.steps) + 1):
         vb, vo = _treg_values(rng, n)
         pre, lr = eng.pack_values(TREG, (vb, vo))
-        ts = rng.integers(0, 1 << 20, n).astype(np.uint64)
+        # fresh writes: batch j's timestamps sit 2^18 above batch j-1's in a
+        # 2^20 window, so ~70% of keys take the delta and ties are dense
+        ts = (rng.integers(0, 1 << 20, n) + (j << 18)).astype(np.uint64)
         batches.append(tuple(_to_dev(a, dev) for a in (own, slot, ts, pre, lr)))
     win = []
 
@@ -242,8 +254,9 @@ def bench_treg(args, eng, dev, dist, rank, world):
     step_of(batches[0])
     # winners per step from timestamps (ties need the value compare: rare)
     cur = batches[0][2].clone() if not routed else None
-    nb = max(1, args.batches)
-    elapsed, kt = _timed(args.steps, args.warmup, lambda i: step_of(batches[1 + i % nb]), dist, dev)
+    nb = len(batches) - 1
+    elapsed, kt = _timed(args.steps, args.warmup, lambda i: step_of(batches[1 + i % nb]), dist, dev,
+                         eng=None if routed else eng)
     if cur is not None:
         for i in range(args.warmup + args.steps):
             t = batches[1 + i % nb][2]
@@ -254,7 +267,11 @@ def bench_treg(args, eng, dev, dist, rank, world):
     t = _max_over_ranks(elapsed, dist, dev)
     k = float(np.mean(kt))
     wf = float(np.mean(win)) if win else 0.5
-    bytes_per_key = 4 + 24 + 8 + 24 * wf
+    # SURVEY 8d prices a key LWW select at 48 B (16 delta + 16 state read +
+    # 16 state write, the write counted unconditionally); what the kernel
+    # actually moves in this layout is reported beside it
+    bytes_per_key = 48
+    moved = 4 + 24 + 8 + 24 * wf
     out = {"workload": f"TREG LWW converge: {G} keys over {world} GPU(s) ({Kper} per GPU), one delta per key "
                        f"per step{' routed by owner (all-to-all)' if routed else ''} (SURVEY 8d config 3)",
            "unit_of_work": "key LWW select", "units_per_step_per_gpu": n,
@@ -264,7 +281,10 @@ def bench_treg(args, eng, dev, dist, rank, world):
         out["roofline"] = {"bound": "hbm", "achieved": bytes_per_key * n / k / 1e9, "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": bytes_per_key * n / k / 1e9 / HBM_PEAK_GBS,
                            "kernel": "k_treg_lww", "kernel_ms_avg": k * 1e3, "bytes_per_unit": bytes_per_key,
-                           "bytes_note": "4 slot + 24 delta + 8 state ts + 24 x winner fraction"}
+                           "bytes_note": "SURVEY 8d: 16 delta + 16 state read + 16 state write per key",
+                           "bytes_moved_per_unit": moved,
+                           "bytes_moved_note": "4 slot + 24 delta (ts, pre, lr) + 8 state ts + 24 state write x "
+                                               "winner fraction"}
     else:
         out["step_ms_avg_events"] = k * 1e3
     return out
@@ -307,7 +327,7 @@ def bench_tlog(args, eng, dev, dist, rank, world):
     def step(i):
         eng.tlog_converge(*dev_batches[1 + i % nb])
 
-    elapsed, kt = _timed(args.steps, args.warmup, step, dist, dev)
+    elapsed, kt = _timed(args.steps, args.warmup, step, dist, dev, eng=eng)
     t = _max_over_ranks(elapsed, dist, dev)
     # replay the same sequence on a fresh engine pass to get exact in/out
     # entry counts per step: state entries are the running total (the engine
@@ -389,7 +409,7 @@ def bench_ujson(args, eng, dev, dist, rank, world):
     def step(i):
         eng.ujson_converge(*dev_batches[i % nb][0])
 
-    elapsed, kt = _timed(args.steps, args.warmup, step, dist, dev)
+    elapsed, kt = _timed(args.steps, args.warmup, step, dist, dev, eng=eng)
     t = _max_over_ranks(elapsed, dist, dev)
     k = float(np.mean(kt))
     # live sizes: average of the initial and final state (they drift slowly)

@@ -68,6 +68,13 @@ uint64_t jy_skipped(const jy_engine* eng);      /* malformed entries skipped so 
 int32_t jy_set_stream(jy_engine* eng, void* hip_stream); /* NULL: engine-owned stream */
 void* jy_get_stream(jy_engine* eng);
 int32_t jy_sync(jy_engine* eng);
+/* measurement (not on the reference's surface; bench.py and rocprof
+ * cross-checks): while enabled, every merge call brackets its device work
+ * (first to last launch, host staging excluded) with HIP events on the
+ * engine stream.  jy_timing_read waits for them, writes up to `cap`
+ * per-call durations in ms, returns the count in *n_out and clears them. */
+int32_t jy_timing_enable(jy_engine* eng, int32_t on);
+int32_t jy_timing_read(jy_engine* eng, uint64_t cap, double* ms_out, uint64_t* n_out);
 
 /* ---- replica dictionary: u64 identity <-> dense column ---- */
 int32_t jy_replica_col(jy_engine* eng, uint64_t replica_id, uint32_t* col_out);

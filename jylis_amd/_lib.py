@@ -43,6 +43,8 @@ SIGNATURES = {
     "jy_set_stream": (I32, [P, P]),
     "jy_get_stream": (P, [P]),
     "jy_sync": (I32, [P]),
+    "jy_timing_enable": (I32, [P, I32]),
+    "jy_timing_read": (I32, [P, U64, P, P]),
     "jy_replica_col": (I32, [P, U64, P]),
     "jy_replica_id": (I32, [P, U32, P]),
     "jy_replica_count": (U32, [P]),

@@ -217,8 +217,7 @@ void jy_engine_destroy(jy_engine* eng) {
   auto F = [eng](void* p) { jy_dev_free(eng, p); };
   for (int w = 0; w < 2; w++) F(eng->cnt[w].slab);
   F(eng->treg.ts);
-  F(eng->treg.pre);
-  F(eng->treg.lr);
+  F(eng->treg.val);
   for (int b = 0; b < 2; b++) {
     F(eng->tlog.off[b]);
     F(eng->tlog.rec[b]);
@@ -240,6 +239,10 @@ void jy_engine_destroy(jy_engine* eng) {
   if (eng->cols_dev) hipFree(eng->cols_dev);
   if (eng->pin) hipHostFree(eng->pin);
   if (eng->pin_total) hipHostFree(eng->pin_total);
+  for (auto& ev : eng->tm_ev) {
+    hipEventDestroy(ev.first);
+    hipEventDestroy(ev.second);
+  }
   if (eng->pin_ready) hipEventDestroy(eng->pin_ready);
   if (eng->total_ready) hipEventDestroy(eng->total_ready);
   if (eng->own_stream) hipStreamDestroy(eng->own_stream);
@@ -271,6 +274,28 @@ void* jy_get_stream(jy_engine* eng) { return eng->stream; }
 int32_t jy_sync(jy_engine* eng) {
   JY_HIP(eng, hipSetDevice(eng->device));
   JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  return JY_OK;
+}
+
+int32_t jy_timing_enable(jy_engine* eng, int32_t on) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  eng->timing = on != 0;
+  eng->tm_used = 0;
+  eng->tm_depth = 0;
+  return JY_OK;
+}
+
+int32_t jy_timing_read(jy_engine* eng, uint64_t cap, double* ms_out, uint64_t* n_out) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  const u64 n = eng->tm_used;
+  for (u64 i = 0; i < n; i++) {
+    JY_HIP(eng, hipEventSynchronize(eng->tm_ev[i].second));
+    float ms = 0;
+    JY_HIP(eng, hipEventElapsedTime(&ms, eng->tm_ev[i].first, eng->tm_ev[i].second));
+    if (i < cap && ms_out) ms_out[i] = ms;
+  }
+  if (n_out) *n_out = n;
+  eng->tm_used = 0;
   return JY_OK;
 }
 

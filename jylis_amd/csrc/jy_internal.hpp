@@ -86,10 +86,14 @@ struct CounterState {  // GCOUNT (nsigns 1) / PNCOUNT (nsigns 2): slab [sign][co
   u64 kcap = 0;  // slot capacity (column pitch, even)
 };
 
-struct TregState {  // SoA per slot
+// TREG value handle of one slot: first 8 value bytes (big-endian) + arena ref
+struct alignas(16) TVal {
+  u64 pre, lr;
+};
+
+struct TregState {  // per slot: ts u64 (read by every merge) + TVal (written by winners)
   u64* ts = nullptr;
-  u64* pre = nullptr;
-  u64* lr = nullptr;
+  TVal* val = nullptr;
   u64 kcap = 0;
 };
 
@@ -177,9 +181,36 @@ struct jy_engine {
   u64* pin_total = nullptr;        // pinned u64[4] for async totals
   hipEvent_t total_ready = nullptr;
 
+  // jy_timing_enable: event pairs around the device work of merge calls
+  bool timing = false;
+  int tm_depth = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> tm_ev;
+  size_t tm_used = 0;
+
   int32_t fail(int32_t code, const std::string& msg) {
     err = msg;
     return code;
+  }
+};
+
+// scope guard: records the start/stop events of one timed merge call (the
+// outermost guard of nested ones wins)
+struct JyTimed {
+  jy_engine* eng;
+  bool on = false;
+  explicit JyTimed(jy_engine* e) : eng(e) {
+    if (!eng->timing || eng->tm_depth++ > 0) return;
+    if (eng->tm_used == eng->tm_ev.size()) {
+      std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+      if (hipEventCreate(&ev.first) != hipSuccess || hipEventCreate(&ev.second) != hipSuccess) return;
+      eng->tm_ev.push_back(ev);
+    }
+    on = hipEventRecord(eng->tm_ev[eng->tm_used].first, eng->stream) == hipSuccess;
+  }
+  ~JyTimed() {
+    if (!eng->timing) return;
+    eng->tm_depth--;
+    if (on && hipEventRecord(eng->tm_ev[eng->tm_used].second, eng->stream) == hipSuccess) eng->tm_used++;
   }
 };
 
@@ -238,6 +269,8 @@ int32_t jy_counter_sum(jy_engine* eng, int which, u64 n, const u32* slots_dev, u
 int32_t jy_treg_grow(jy_engine* eng, u64 need_slots);
 int32_t jy_treg_merge(jy_engine* eng, u64 n, const u32* slot, const u64* ts, const u64* pre, const u64* lr);
 int32_t jy_treg_gather(jy_engine* eng, u64 n, const u32* slots, u64* ts, u64* pre, u64* lr);
+// routed records (slot, ts, pre, lr) x n, long values rebased by `base`
+int32_t jy_treg_merge_records(jy_engine* eng, const u64* recs, u64 n, u64 base);
 
 int32_t jy_tlog_grow(jy_engine* eng, u64 need_slots);
 int32_t jy_tlog_extend(jy_engine* eng, u64 from, u64 to);

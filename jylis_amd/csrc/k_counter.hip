@@ -142,6 +142,7 @@ int32_t jy_counter_grow(jy_engine* eng, int which, u32 need_cols, u64 need_slots
 
 int32_t jy_counter_coo(jy_engine* eng, int which, int sign, u64 n, const u32* slot, const u16* col, const u64* val) {
   if (n == 0) return JY_OK;
+  JyTimed tm(eng);
   CounterState& c = eng->cnt[which];
   u64* base = c.slab + (u64)sign * c.ccap * c.kcap;
   const u64 blocks = (n + kThreads - 1) / kThreads;
@@ -152,6 +153,7 @@ int32_t jy_counter_coo(jy_engine* eng, int which, int sign, u64 n, const u32* sl
 
 int32_t jy_counter_block(jy_engine* eng, int which, u32 ncols, const u16* cols_dev, u32 slot0, u32 nslots,
                          const u64* vp, const u64* vn) {
+  JyTimed tm(eng);
   CounterState& c = eng->cnt[which];
   const u32 nsigns = which + 1;
   const void* dcols = cols_dev;

@@ -85,28 +85,6 @@ __global__ __launch_bounds__(kThreads) void k_route_scatter_treg(
   r[3] = out_lr;
 }
 
-// receiver: LWW-merge one source run of records; long values are rebased
-// onto the arena region where this run's bytes were appended
-__global__ __launch_bounds__(kThreads) void k_treg_lww_records(u64* __restrict__ ts, u64* __restrict__ pre,
-                                                               u64* __restrict__ lr,
-                                                               const uint8_t* __restrict__ arena,
-                                                               const u64* __restrict__ recs, u64 n, u64 base) {
-  const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= n) return;
-  const u64* r = recs + i * 4;
-  const u64 s = r[0], t = r[1], p = r[2];
-  u64 l = r[3];
-  if ((l & JY_LR_LEN_MASK) > 8) l = (((l >> JY_LR_LEN_BITS) + base) << JY_LR_LEN_BITS) | (l & JY_LR_LEN_MASK);
-  const u64 t0 = ts[s];
-  bool win = t > t0;
-  if (t == t0) win = jy_value_cmp(p, l, pre[s], lr[s], arena) > 0;
-  if (win) {
-    ts[s] = t;
-    pre[s] = p;
-    lr[s] = l;
-  }
-}
-
 u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kThreads - 1) / kThreads); }
 
 }  // namespace
@@ -187,6 +165,7 @@ int32_t jy_treg_route_scatter(jy_engine* eng, uint64_t n, const uint32_t* owner,
 int32_t jy_treg_converge_routed(jy_engine* eng, uint32_t nsrc, const uint64_t* rec_counts,
                                 const uint64_t* byte_counts, const uint64_t* recs_dev, const uint8_t* bytes_dev) {
   JY_HIP(eng, hipSetDevice(eng->device));
+  JyTimed tm(eng);
   u64 total_bytes = 0;
   for (u32 s = 0; s < nsrc; s++) total_bytes += byte_counts[s];
   Arena& a = eng->arena[JY_TREG];
@@ -201,16 +180,12 @@ int32_t jy_treg_converge_routed(jy_engine* eng, uint32_t nsrc, const uint64_t* r
     if ((a.len + total_bytes) >> (64 - JY_LR_LEN_BITS)) return eng->fail(JY_ERANGE, "arena offset overflow");
     JY_HIP(eng, hipMemcpyAsync(a.p + a.len, bytes_dev, total_bytes, hipMemcpyDeviceToDevice, eng->stream));
   }
-  TregState& t = eng->treg;
   u64 rec_off = 0, byte_off = a.len;
   for (u32 s = 0; s < nsrc; s++) {
-    if (rec_counts[s])
-      hipLaunchKernelGGL(k_treg_lww_records, dim3(blocks_for(rec_counts[s])), dim3(kThreads), 0, eng->stream, t.ts,
-                         t.pre, t.lr, a.p, recs_dev + rec_off * 4, rec_counts[s], byte_off);
+    if (rec_counts[s]) JY_TRY(jy_treg_merge_records(eng, recs_dev + rec_off * 4, rec_counts[s], byte_off));
     rec_off += rec_counts[s];
     byte_off += byte_counts[s];
   }
-  JY_HIP(eng, hipGetLastError());
   a.len += total_bytes;
   return JY_OK;
 }

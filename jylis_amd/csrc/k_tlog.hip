@@ -504,6 +504,7 @@ int32_t jy_tlog_extend(jy_engine* eng, u64 from, u64 to) {
 
 int32_t jy_tlog_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* dcut, const u64* doff, u64 nent,
                       const u64* dts, const u64* dpre, const u64* dlr) {
+  JyTimed tm(eng);
   TlogState& t = eng->tlog;
   const u64 nk = eng->nkeys[JY_TLOG];
   if (nd == 0 || nk == 0) return JY_OK;

@@ -586,6 +586,7 @@ int32_t jy_ujson_extend(jy_engine* eng, u64 from, u64 to) {
 int32_t jy_ujson_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* deoff, u64 nel, const u64* ddots,
                        const u64* delems, const u64* dvoff, u64 nvv, const u64* dvv, const u64* dcoff, u64 ncloud,
                        const u64* dcloud) {
+  JyTimed tm(eng);
   UjsonState& u = eng->ujson;
   const u64 nk = eng->nkeys[JY_UJSON];
   if (nd == 0 || nk == 0) return JY_OK;

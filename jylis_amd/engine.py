@@ -116,6 +116,17 @@ class Engine:
     def stream(self):
         return self.lib.jy_get_stream(self.h)
 
+    def timing(self, on=True):
+        """bracket every merge call's device work with HIP events (jy_timing_enable)"""
+        self._check(self.lib.jy_timing_enable(self.h, 1 if on else 0))
+
+    def timing_read(self, cap=4096):
+        """-> per-call device durations (ms) since the last read"""
+        out = np.zeros(cap, np.float64)
+        n = C.c_uint64()
+        self._check(self.lib.jy_timing_read(self.h, cap, out.ctypes.data, C.byref(n)))
+        return out[:min(n.value, cap)].copy()
+
     def skipped(self):
         return int(self.lib.jy_skipped(self.h))
 
