@@ -341,7 +341,7 @@ def bench_tlog(args, eng, dev, dist, rank, world):
         pre, lr = e2.pack_values(TLOG, (b["val_bytes"], b["val_offs"]))
         b2.append(tuple(_to_dev(a, dev) for a in (slots, b["cutoff"], b["ent_offs"], b["ts"], pre, lr)))
     e2.tlog_converge(*b2[0])
-    byts, ins = [], []
+    byts, ins, moved = [], [], []
     prev = _tlog_total(e2)
     for i in range(args.warmup + args.steps):
         bt = b2[1 + i % nb]
@@ -349,7 +349,10 @@ def bench_tlog(args, eng, dev, dist, rank, world):
         now = _tlog_total(e2)
         nd = int(bt[3].numel())
         if i >= args.warmup:
-            byts.append(24 * (prev + nd) + 24 * now + 24 * K)
+            # 16 B read per input entry + 16 B written per output
+            # entry + 24 B per key; moved: what the append layout touches
+            byts.append(16 * (prev + nd) + 16 * now + 24 * K)
+            moved.append(24 * nd + 32 * max(now - prev, 0) + 64 * int(bt[0].numel()))
             ins.append(prev + nd)
         prev = now
     e2.close()
@@ -362,9 +365,13 @@ def bench_tlog(args, eng, dev, dist, rank, world):
             "ms_per_step": t / args.steps * 1e3,
             "roofline": {"bound": "hbm", "achieved": avg_b / k / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": avg_b / k / 1e9 / HBM_PEAK_GBS,
-                         "kernel": "TLOG merge path (k_tlog_*, whole converge)",
+                         "kernel": "TLOG converge (k_tlog_*, all launches of one call)",
                          "converge_ms_avg": k * 1e3, "bytes_per_converge": avg_b,
-                         "bytes_note": "24 B per input entry (state + delta) + 24 B per output entry + 24 B per key"}}
+                         "bytes_note": "SURVEY 8d: 16 B read per input entry (state + delta) + 16 B written per "
+                                       "output entry + 24 B per key (a whole-state rewrite)",
+                         "min_bytes_moved_per_converge": float(np.mean(moved)),
+                         "min_bytes_moved_note": "append layout lower bound: 24 B per delta entry read + 32 B per "
+                                                 "net new entry written + 64 B meta per delta key"}}
 
 
 def _tlog_total(eng):

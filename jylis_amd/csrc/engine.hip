@@ -219,8 +219,6 @@ void jy_engine_destroy(jy_engine* eng) {
   F(eng->treg.ts);
   F(eng->treg.val);
   for (int b = 0; b < 2; b++) {
-    F(eng->tlog.off[b]);
-    F(eng->tlog.rec[b]);
     F(eng->ujson.eoff[b]);
     F(eng->ujson.rec[b]);
     F(eng->ujson.coff[b]);
@@ -228,8 +226,11 @@ void jy_engine_destroy(jy_engine* eng) {
     F(eng->ujson.eseg[b]);
     F(eng->ujson.cseg[b]);
   }
-  F(eng->tlog.cutoff);
-  F(eng->tlog.newest);
+  F(eng->tlog.meta);
+  F(eng->tlog.pool);
+  F(eng->tlog.ctr);
+  if (eng->tlog.pin) hipHostFree(eng->tlog.pin);
+  if (eng->tlog.ready) hipEventDestroy(eng->tlog.ready);
   for (auto& k : eng->kdir) jy_keydir_free(eng, k);
   F(eng->ujson.vv);
   for (auto& a : eng->arena) F(a.p);

@@ -97,23 +97,35 @@ struct TregState {  // per slot: ts u64 (read by every merge) + TVal (written by
   u64 kcap = 0;
 };
 
-// one TLOG entry: 32 B so a lane moves it with two 16-B accesses
+// one TLOG entry: 32 B so a lane moves it with two 16-B accesses and an
+// entry write is one whole 32-B sector
 struct alignas(16) TRec {
   u64 ts, pre, lr;
-  u32 seg;  // slot of the entry
-  u32 pad;
+  u64 pad;
 };
 
-struct TlogState {  // CSR over slots, double-buffered entry records
-  u64* off[2] = {nullptr, nullptr};  // [kcap + 1]
-  TRec* rec[2] = {nullptr, nullptr};
-  u64 ecap[2] = {0, 0};
-  int cur = 0;
-  u64* cutoff = nullptr;  // [kcap]
-  u64* newest = nullptr;  // [kcap] ts of each log's first (newest) entry; any value when empty
+// per log: a segment of the entry pool, entries OLDEST FIRST (ascending
+// (ts, value)), so the usual delta -- entries newer than the whole log --
+// is an append at the tail; a raised cutoff drops a prefix (base moves up)
+struct alignas(16) TMeta {
+  u64 base;     // pool index of the oldest live entry
+  u32 len;      // live entries
+  u32 cap;      // pool entries reserved from base
+  u64 cut;      // cutoff
+  u64 newest;   // ts of the newest entry (any value when len == 0)
+};
+
+struct TlogState {  // per-slot segments of one entry pool
+  TMeta* meta = nullptr;  // [kcap]
+  TRec* pool = nullptr;   // [pcap]
+  u64 pcap = 0;
+  u64* ctr = nullptr;     // device: [0] pool entries handed out (bump pointer)
+  u64* pin = nullptr;     // pinned readback of ctr[0]
+  hipEvent_t ready = nullptr;
+  bool known = false;     // pin holds the bump pointer after the last merge
+  u64 used_bound = 0;     // host upper bound of ctr[0]
+  u64 live_bound = 0;     // host upper bound of live entries
   u64 kcap = 0;
-  u64 nent_bound = 0;       // host upper bound of live entries
-  bool nent_known = false;  // pin_total[0] holds the live total after a merge
 };
 
 // one UJSON element: (dot, element handle), moved with one 16-B access

@@ -6,30 +6,43 @@
 //              the later timestamp first, then the greater value first
 //              (Pony String order); (ts, value) duplicates collapse.
 //
-// HBM layout: per type, CSR over slots -- off[kcap+1] (u64); entries are
-// 32-B records {ts, pre, lr, seg} (value handle as in TREG: 8-byte big-endian
-// prefix + arena offset/length; seg = slot of the entry), so the streaming
-// passes move them with 16-B accesses; cutoff[kcap].  Entries are
-// double-buffered: a converge rewrites the CSR into the other buffer.
+// HBM layout: one entry pool of 32-B records {ts, pre, lr, pad} (value
+// handle as in TREG: 8-byte big-endian prefix + arena offset/length) and a
+// 32-B TMeta per slot {base, len, cap, cutoff, newest}.  A log is the pool
+// segment [base, base + len), stored OLDEST FIRST, with room up to cap.
+// Reads reverse it into the reference's newest-first order.
 //
-// Parallel shape: one thread per ENTRY (state or delta), coalesced, with
-// merge-path positions -- no per-key loops, so long or skewed logs cost the
-// same per entry as short ones:
-//   keep(state e)  = ts >= cutoff'
-//   keep(delta e)  = ts >= cutoff' and no equal entry in the state segment
-//   pos(e) = new_off[key] + #kept own-side entries before e
-//                         + #kept other-side entries ordered before e
-// the counts coming from an exclusive scan of the delta keep flags and one
-// binary search per delta entry (entry order, value bytes compared only on
-// (ts, prefix) ties) into the state segment.  That search's result (the
-// entry's state rank, prel) is kept, so the state side finds its count by a
-// search over small integers and the delta side needs no second search.  A delta segment that is not strictly
-// ordered is not a TLog: its key is left untouched and counted (the
-// reference swallows converge errors, repo_tlog.pony:67).
+// Why this layout: a peer's delta is almost always entries newer than the
+// whole log (writes carry the current time).  Oldest-first, those are an
+// APPEND at the segment's tail -- the merge writes only the new entries and
+// the key's 32-B meta; the rest of the log is never read or moved.  A raised
+// cutoff drops a prefix: base moves up, nothing is copied.  Only a key whose
+// delta interleaves with its log (an older entry, a timestamp tie) or whose
+// segment is full is REBUILT into fresh pool space (bump allocation,
+// capacity rounded to a power of two) by a merge of the two sorted runs.
+// The pool is compacted (every log rewritten back to back) when its free
+// space cannot cover the worst case of the next merge.
 //
-// Roofline: HBM.  Per state entry 32 B read; per delta entry 24 B read;
-// 32 B written per output entry; per key 16 B offsets + 16 B cutoff; delta
-// keep flags, their scan and prel add ~28 B per delta entry; see DESIGN.md.
+// Per merge, KEY TILES: a workgroup owns 256 consecutive delta keys and
+// their delta entries (contiguous), keys staged in LDS, entries walked in
+// coalesced chunks with lanes on consecutive entries:
+//   k_tlog_prep    repeated slots in the batch (both copies skipped)
+//   k_tlog_tile    validate (strictly newest first), cutoff drop, kept flag
+//                  and state rank per entry (no search for the usual entry,
+//                  newer than the log), append or rebuild per key; appends
+//                  are written at the tail here
+//   k_tlog_commit  publish the new meta; rebuilt keys are written into the
+//                  fresh space the scan of their sizes gave them, one lane
+//                  per output entry (merge-path positions from the ranks)
+// Pool space for rebuilt keys is only known on the device after that scan.
+// The host keeps an upper bound of the bump pointer; when the worst case may
+// not fit, it waits for the scan, reads the exact total and, if the pool is
+// really short, compacts and re-plans (nothing is published before commit).
+//
+// Roofline: HBM.  An append-path delta entry costs 24 B read + 32 B written;
+// per delta key 32 B meta read + 32 B written + a 48-B plan record written
+// and read back.  Rebuilt keys add 32 B read + 32 B written per surviving
+// entry.  See DESIGN.md "TLOG".
 
 #include <hipcub/hipcub.hpp>
 
@@ -44,7 +57,7 @@ constexpr u32 kNone = 0xFFFFFFFFu;
 
 __device__ __forceinline__ u64 gid() { return (u64)blockIdx.x * kThreads + threadIdx.x; }
 
-// > 0 if (ta, pa, la) is ordered before (tb, pb, lb): later ts, then greater value
+// > 0 if (ta, pa, la) is NEWER than (tb, pb, lb): later ts, then greater value
 __device__ __forceinline__ int entry_cmp(u64 ta, u64 pa, u64 la, u64 tb, u64 pb, u64 lb,
                                          const uint8_t* __restrict__ arena) {
   if (ta != tb) return ta > tb ? 1 : -1;
@@ -55,27 +68,26 @@ struct Ent {
   u64 t, p, l;
 };
 
-// > 0 if log entry m is ordered before x; value handles are read only on a
-// timestamp tie
-__device__ __forceinline__ int cmp_at(const TRec* __restrict__ rec, u64 m, const Ent& x,
+// sign of (pool[m] - x) in age order; value handles are read only on a tie
+__device__ __forceinline__ int cmp_at(const TRec* __restrict__ pool, u64 m, const Ent& x,
                                       const uint8_t* __restrict__ arena) {
-  const u64 t = rec[m].ts;
+  const u64 t = pool[m].ts;
   if (t != x.t) return t > x.t ? 1 : -1;
-  return jy_value_cmp(rec[m].pre, rec[m].lr, x.p, x.l, arena);
-}
-
-// first index in [lo, hi) of a sorted log whose entry is NOT ordered before x
-__device__ __forceinline__ u64 lower_bound_entry(const TRec* __restrict__ rec, u64 lo, u64 hi, const Ent& x,
-                                                 const uint8_t* __restrict__ arena) {
-  while (lo < hi) {
-    const u64 m = (lo + hi) >> 1;
-    if (cmp_at(rec, m, x, arena) > 0) lo = m + 1;
-    else hi = m;
-  }
-  return lo;
+  return jy_value_cmp(pool[m].pre, pool[m].lr, x.p, x.l, arena);
 }
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void store_rec(TRec* __restrict__ p, u64 ts, u64 pre, u64 lr) {
+  u64x2* q = reinterpret_cast<u64x2*>(p);
+  u64x2 a, b;
+  a.x = ts;
+  a.y = pre;
+  b.x = lr;
+  b.y = 0;
+  __builtin_nontemporal_store(a, q);
+  __builtin_nontemporal_store(b, q + 1);
+}
 
 __device__ __forceinline__ TRec load_rec(const TRec* __restrict__ p) {
   const u64x2* q = reinterpret_cast<const u64x2*>(p);
@@ -84,335 +96,384 @@ __device__ __forceinline__ TRec load_rec(const TRec* __restrict__ p) {
   r.ts = a.x;
   r.pre = a.y;
   r.lr = b.x;
-  r.seg = (u32)b.y;
-  r.pad = (u32)(b.y >> 32);
+  r.pad = b.y;
   return r;
 }
 
-__device__ __forceinline__ void store_rec(TRec* __restrict__ p, u64 ts, u64 pre, u64 lr, u32 seg) {
-  u64x2* q = reinterpret_cast<u64x2*>(p);
-  u64x2 a, b;
-  a.x = ts;
-  a.y = pre;
-  b.x = lr;
-  b.y = seg;
-  __builtin_nontemporal_store(a, q);
-  __builtin_nontemporal_store(b, q + 1);
-}
+enum : u32 { kSkip = 0, kAppend = 1, kRebuild = 2 };
 
-// per-key record for the state-side scatter: one line instead of six
-// scattered per-key arrays
-struct KeyInfo {
-  u64 lo;        // off[s]: the state segment (its surviving prefix is what the output holds)
-  u64 blo, bhi;  // delta segment (empty if none)
-  u32 scan_lo;   // scan_b[blo]
-  u32 front;     // every delta entry is kept and precedes the whole state
-};
-
-// per delta key: its state segment, merged cutoff and whether it merges
-struct DInfo {
-  u64 lo, hi;  // state segment [off[s], off[s+1])
-  u64 cut;     // max(state cutoff, delta cutoff)
-  u64 newest;  // ts of the state's first (newest) entry (any value if empty)
-  u32 s;       // slot
-  u32 raised;  // the delta raises the cutoff (else no state entry drops:
-               // every state entry already has ts >= the state cutoff)
+// per delta key: what k_tlog_tile decided (k_tlog_commit publishes it)
+struct alignas(16) PInfo {
+  u64 src;      // old base of the log
+  u64 newest;   // newest ts after the merge
+  u64 cut;      // merged cutoff
+  u32 len;      // old length
+  u32 drop;     // state entries dropped by the cutoff (a prefix)
+  u32 newlen;   // entries after the merge
+  u32 cap;      // append: old cap; rebuild: the new segment's capacity
+  u32 mode;
+  u32 s;
 };
 
 struct TlogArgs {
-  // state (current buffer)
-  const u64* off;
-  const TRec* rec;
-  u64* cutoff;
-  u64* newest;
-  u64 nkeys, na;
+  TMeta* meta;
+  const TRec* pool;
+  const uint8_t* arena;
   // delta batch
-  u64 nd, nb;
+  u64 nd;
   const u32* slot;
-  u32* dptr;
   const u64* dcut;
   const u64* doff;
   const u64* dts;
   const u64* dpre;
   const u64* dlr;
-  const uint8_t* arena;
-  const u32* dseg;  // [nb] delta key of each delta entry
   // temporaries
-  u32* bad;     // [nd]
-  DInfo* dinfo;  // [nd]
-  u64* keep_a;  // [nkeys] surviving state entries: a prefix of every log
-  u32* flag_b;  // [nb + 1]
-  u32* scan_b;  // [nb + 1]
-  u32* prel;    // [nb] state entries of the key ordered before the delta entry
-  u32* slow;       // [nb] 1: the delta entry needs the full search
-  u32* slow_list;  // [nb] those entries, compacted (count at slow_n)
-  u32* slow_n;
-  KeyInfo* info;  // [nkeys]
+  u32* dptr;     // [nkeys] delta key merging into each slot
+  u32* bad;      // [nd] repeated slot in the batch
+  PInfo* pinfo;  // [nd]
+  u64* relsz;    // [nd + 1] pool entries a rebuilt key takes (0 otherwise)
 };
 
-// per delta key.  A slot named twice in one device batch breaks the
-// one-delta-per-key contract: both deltas are skipped (counted), the key is
-// left untouched.  bad[] and dptr[] are cleared before this launch.
+// A slot named twice in one device batch breaks the one-delta-per-key
+// contract: both deltas are skipped (counted once), the key is left untouched.
+// dptr[] and bad[] are cleared before this launch.
 __global__ __launch_bounds__(kThreads) void k_tlog_prep(TlogArgs A) {
   const u64 k = gid();
   if (k >= A.nd) return;
-  const u64 s = A.slot[k];
-  const u32 prev = atomicCAS(A.dptr + s, kNone, (u32)k);
+  const u32 prev = atomicCAS(A.dptr + A.slot[k], kNone, (u32)k);
   if (prev != kNone) {
     A.bad[k] = 1;
     A.bad[prev] = 1;
   }
-  const u64 cs = A.cutoff[s], cd = A.dcut[k];
-  DInfo D;
-  D.lo = A.off[s];
-  D.hi = A.off[s + 1];
-  D.cut = cs > cd ? cs : cd;
-  D.newest = A.newest[s];
-  D.s = (u32)s;
-  D.raised = cd > cs;
-  A.dinfo[k] = D;
 }
 
-__global__ __launch_bounds__(kThreads) void k_tlog_validate(TlogArgs A) {
-  const u64 j = gid();
-  if (j >= A.nb) return;
-  const u32 k = A.dseg[j];
-  if (j > A.doff[k] &&
-      entry_cmp(A.dts[j - 1], A.dpre[j - 1], A.dlr[j - 1], A.dts[j], A.dpre[j], A.dlr[j], A.arena) <= 0)
-    A.bad[k] = 1;
+// capacity of a rebuilt segment: room to double by appends, power of two
+__device__ __forceinline__ u32 pow2_cap(u32 n) {
+  const u64 want = 2 * (u64)n + 2;
+  u64 c = 4;
+  while (c < want) c <<= 1;
+  return c > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)c;
 }
 
-// the delta key that merges into slot s, or kNone (no delta, or a malformed
-// one: the reference swallows the error and leaves the key untouched)
-__device__ __forceinline__ u32 merging_key(const TlogArgs& A, u64 s) {
-  const u32 k = A.dptr[s];
-  return (k != kNone && !A.bad[k]) ? k : kNone;
+// last idx in [0, n] with a[idx] <= x (a non-decreasing, a[0] <= x)
+__device__ __forceinline__ u32 lds_last_le(const u64* a, u32 n, u64 x) {
+  u32 lo = 0, hi = n;
+  while (lo < hi) {
+    const u32 m = (lo + hi + 1) >> 1;
+    if (a[m] <= x) lo = m;
+    else hi = m - 1;
+  }
+  return lo;
 }
 
-// keep flag of every delta entry and its rank among the state entries.
-// prel is non-decreasing along a delta segment: entries dropped by the
-// cutoff are its tail and take the segment length.
-// keep flag and state rank of every delta entry.  The usual entry is newer
-// than its whole log: rank 0, kept, no search.  Entries that need the full
-// search (ties with the newest entry, older entries, duplicates) go to a
-// worklist so waves of the common case never wait on a searching lane.
-__global__ __launch_bounds__(kThreads) void k_tlog_flag_b(TlogArgs A) {
-  const u64 j = gid();
-  if (j > A.nb) return;
-  if (j == A.nb) {
-    A.flag_b[j] = 0;
+// key tiles are one wave: no cross-wave barriers, many tiles in flight per CU
+constexpr int kTile = 64;
+typedef hipcub::BlockScan<u32, kTile> BlockScanU32;
+
+constexpr u32 kKept = 0x80000000u;  // eqx: kept flag | # kept entries of the key before this one
+
+// KEY TILES: a workgroup (one wave) owns kTile consecutive delta keys and all their
+// delta entries (contiguous in the batch).  Keys are staged in LDS, entries
+// are walked in coalesced chunks of kTile with lanes on consecutive
+// entries, and per-key facts are gathered with LDS atomics and a block scan:
+//   1. per key (lane = key): log meta, merged cutoff, dropped prefix
+//   2. per entry: order check against the previous entry; kept flag and
+//      rank (# state entries older than it: len for the usual entry, newer
+//      than the log; else a binary search of the log, duplicates dropped);
+//      q = kept entries of the key before it (block scan with carry)
+//   3. per key: append (every kept entry has rank len, room left) or rebuild
+//   4. per entry: kept entries of append keys go to the tail, oldest first
+// rank/q of every entry go to HBM for the rebuild in k_tlog_commit.
+__global__ __launch_bounds__(kTile) void k_tlog_tile(TlogArgs A, TRec* __restrict__ pool, u32* __restrict__ erank,
+                                                        u32* __restrict__ eqx) {
+  __shared__ u64 l_eoff[kTile + 1];
+  __shared__ u64 l_base[kTile], l_newest[kTile], l_cut[kTile];
+  __shared__ u32 l_len[kTile], l_cap[kTile], l_drop[kTile], l_M[kTile], l_minrank[kTile],
+      l_first[kTile], l_bad[kTile], l_gstart[kTile], l_mode[kTile];
+  __shared__ typename BlockScanU32::TempStorage scan_tmp;
+  const u32 tid = threadIdx.x;
+  const u64 k0 = (u64)blockIdx.x * kTile;
+  const u32 nt = (u32)(A.nd - k0 < kTile ? A.nd - k0 : kTile);
+  // 1. keys
+  if (tid < nt) {
+    const u64 k = k0 + tid;
+    const TMeta m = A.meta[A.slot[k]];
+    const u64 cd = A.dcut[k];
+    const u64 cut = m.cut > cd ? m.cut : cd;
+    u32 drop = 0;
+    if (cd > m.cut && m.len > 0 && A.pool[m.base].ts < cut) {
+      u32 l = 0, h = m.len;  // oldest first: the cutoff drops a prefix
+      while (l < h) {
+        const u32 mid = (l + h) >> 1;
+        if (A.pool[m.base + mid].ts < cut) l = mid + 1;
+        else h = mid;
+      }
+      drop = l;
+    }
+    l_eoff[tid] = A.doff[k];
+    l_base[tid] = m.base;
+    l_newest[tid] = m.newest;
+    l_cut[tid] = cut;
+    l_len[tid] = m.len;
+    l_cap[tid] = m.cap;
+    l_drop[tid] = drop;
+    l_bad[tid] = A.bad[k];
+    l_M[tid] = 0;
+    l_minrank[tid] = 0xFFFFFFFFu;
+    l_first[tid] = 0xFFFFFFFFu;
+  }
+  if (tid == 0) l_eoff[nt] = A.doff[k0 + nt];
+  if (blockIdx.x == 0 && tid == 0) A.relsz[A.nd] = 0;
+  __syncthreads();
+  const u64 E0 = l_eoff[0], E1 = l_eoff[nt];
+  // 2. entries
+  u32 carry = 0;
+  for (u64 c0 = E0; c0 < E1; c0 += kTile) {
+    const u64 j = c0 + tid;
+    const bool valid = j < E1;
+    u32 idx = 0, flag = 0, rank = 0;
+    if (valid) {
+      idx = lds_last_le(l_eoff, nt - 1, j);
+      const u64 t = A.dts[j];
+      const Ent x{t, A.dpre[j], A.dlr[j]};
+      if (j > l_eoff[idx] && entry_cmp(A.dts[j - 1], A.dpre[j - 1], A.dlr[j - 1], x.t, x.p, x.l, A.arena) <= 0)
+        atomicOr(&l_bad[idx], 2u);
+      const u32 len = l_len[idx], drop = l_drop[idx];
+      if (t >= l_cut[idx]) {
+        if (len == drop || t > l_newest[idx]) {
+          flag = 1;
+          rank = len;
+        } else {
+          const u64 base = l_base[idx];
+          u32 l = drop, h = len;  // first entry of the log not older than x
+          while (l < h) {
+            const u32 m = (l + h) >> 1;
+            if (cmp_at(A.pool, base + m, x, A.arena) < 0) l = m + 1;
+            else h = m;
+          }
+          rank = l;
+          flag = !(l < len && cmp_at(A.pool, base + l, x, A.arena) == 0);
+        }
+      }
+    }
+    u32 g, agg;
+    BlockScanU32(scan_tmp).ExclusiveSum(flag, g, agg);
+    g += carry;
+    if (valid && j == l_eoff[idx]) l_gstart[idx] = g;
+    __syncthreads();
+    if (valid) {
+      const u32 q = g - l_gstart[idx];
+      erank[j] = rank;
+      eqx[j] = q | (flag ? kKept : 0u);
+      if (flag) {
+        atomicAdd(&l_M[idx], 1u);
+        atomicMin(&l_minrank[idx], rank);
+        atomicMin(&l_first[idx], (u32)(j - E0));
+      }
+    }
+    carry += agg;
+    __syncthreads();  // scan_tmp and l_gstart reuse
+  }
+  // 3. per key decision
+  if (tid < nt) {
+    const u64 k = k0 + tid;
+    PInfo P;
+    P.s = A.slot[k];
+    if (l_bad[tid]) {
+      P.mode = kSkip;
+      A.relsz[k] = 0;
+    } else {
+      const u32 len = l_len[tid], drop = l_drop[tid], M = l_M[tid];
+      const u32 surv = len - drop;
+      const u64 newest = l_newest[tid];
+      u64 nn = newest;
+      if (M > 0) {
+        const u64 tn = A.dts[E0 + l_first[tid]];
+        nn = (surv == 0 || tn > newest) ? tn : newest;
+      }
+      P.src = l_base[tid];
+      P.len = len;
+      P.drop = drop;
+      P.newlen = surv + M;
+      P.cut = l_cut[tid];
+      P.newest = nn;
+      if ((M == 0 || l_minrank[tid] == len) && (u64)len + M <= l_cap[tid]) {
+        P.mode = kAppend;
+        P.cap = l_cap[tid];
+        A.relsz[k] = 0;
+      } else {
+        P.mode = kRebuild;
+        P.cap = pow2_cap(surv + M);
+        A.relsz[k] = P.cap;
+      }
+    }
+    l_mode[tid] = P.mode;
+    A.pinfo[k] = P;
+  }
+  __syncthreads();
+  // 4. appends (the chunk's entries are L2-hot)
+  for (u64 c0 = E0; c0 < E1; c0 += kTile) {
+    const u64 j = c0 + tid;
+    if (j >= E1) continue;
+    const u32 idx = lds_last_le(l_eoff, nt - 1, j);
+    const u32 qx = eqx[j];
+    if (l_mode[idx] != kAppend || !(qx & kKept)) continue;
+    const u64 tail = l_base[idx] + l_len[idx] + l_M[idx] - 1;
+    store_rec(pool + tail - (qx & ~kKept), A.dts[j], A.dpre[j], A.dlr[j]);
+  }
+}
+
+// KEY TILES again, after the scan of rebuilt sizes: publish every key's meta
+// and rebuild the rebuilt keys into their fresh space, one lane per output
+// (state survivors and delta entries of the tile's rebuilt keys, flattened
+// by a block scan):
+//   state entry i (i >= drop): (i - drop) + #kept deltas with rank <= i;
+//     ranks fall along the newest-first delta segment, so that is M - q of
+//     the first entry with rank <= i (binary search)
+//   kept delta entry j: (rank_j - drop) + (M - 1 - q_j)
+__global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __restrict__ roff,
+                                                          const u64* __restrict__ ctr, TRec* __restrict__ pool,
+                                                          const u32* __restrict__ erank, const u32* __restrict__ eqx,
+                                                          unsigned long long* __restrict__ skipped) {
+  __shared__ u64 l_woff[kTile + 1];
+  __shared__ u64 l_src[kTile], l_dst[kTile], l_blo[kTile], l_bhi[kTile];
+  __shared__ u32 l_drop[kTile], l_surv[kTile], l_M[kTile];
+  __shared__ typename BlockScanU32::TempStorage scan_tmp;
+  const u32 tid = threadIdx.x;
+  const u64 k0 = (u64)blockIdx.x * kTile;
+  const u32 nt = (u32)(A.nd - k0 < kTile ? A.nd - k0 : kTile);
+  u32 w = 0;
+  if (tid < nt) {
+    const u64 k = k0 + tid;
+    const PInfo P = A.pinfo[k];
+    if (P.mode == kSkip) {
+      if (A.dptr[P.s] == (u32)k) atomicAdd(skipped, 1ull);  // once per slot
+    } else if (P.mode == kAppend) {
+      A.meta[P.s] = TMeta{P.src + P.drop, P.newlen, P.cap - P.drop, P.cut, P.newest};
+    } else {
+      const u64 dst = ctr[0] + roff[k];
+      A.meta[P.s] = TMeta{dst, P.newlen, P.cap, P.cut, P.newest};
+      const u64 blo = A.doff[k], bhi = A.doff[k + 1];
+      l_src[tid] = P.src;
+      l_dst[tid] = dst;
+      l_blo[tid] = blo;
+      l_bhi[tid] = bhi;
+      l_drop[tid] = P.drop;
+      l_surv[tid] = P.len - P.drop;
+      l_M[tid] = P.newlen - (P.len - P.drop);
+      w = (P.len - P.drop) + (u32)(bhi - blo);
+    }
+  }
+  u32 wo, wtot;
+  BlockScanU32(scan_tmp).ExclusiveSum(w, wo, wtot);
+  if (tid < nt) l_woff[tid] = wo;
+  if (tid == 0) l_woff[nt] = wtot;
+  __syncthreads();
+  for (u32 c0 = 0; c0 < wtot; c0 += kTile) {
+    const u32 item = c0 + tid;
+    if (item >= wtot) continue;
+    u32 idx = 0, hi = nt - 1;  // last idx with woff <= item and w > 0
+    while (idx < hi) {
+      const u32 m = (idx + hi + 1) >> 1;
+      if (l_woff[m] <= item) idx = m;
+      else hi = m - 1;
+    }
+    const u32 r = item - (u32)l_woff[idx];
+    const u32 surv = l_surv[idx], drop = l_drop[idx], M = l_M[idx];
+    const u64 blo = l_blo[idx], bhi = l_bhi[idx];
+    if (r < surv) {
+      const u32 i = drop + r;
+      u64 l = blo, h = bhi;  // first delta entry with rank <= i
+      while (l < h) {
+        const u64 m = (l + h) >> 1;
+        if (erank[m] <= i) h = m;
+        else l = m + 1;
+      }
+      const u32 c = l < bhi ? M - (eqx[l] & ~kKept) : 0;
+      const TRec x = load_rec(A.pool + l_src[idx] + i);
+      store_rec(pool + l_dst[idx] + r + c, x.ts, x.pre, x.lr);
+    } else {
+      const u64 j = blo + (r - surv);
+      const u32 qx = eqx[j];
+      if (!(qx & kKept)) continue;
+      const u64 pos = (u64)(erank[j] - drop) + (M - 1 - (qx & ~kKept));
+      store_rec(pool + l_dst[idx] + pos, A.dts[j], A.dpre[j], A.dlr[j]);
+    }
+  }
+}
+
+__global__ void k_tlog_bump(u64* __restrict__ ctr, const u64* __restrict__ roff, u64 nd) { ctr[0] += roff[nd]; }
+
+constexpr u32 kTileOut = 2048;
+
+// ---- compaction: every log rewritten back to back into a fresh pool ----
+__global__ __launch_bounds__(kThreads) void k_cmp_size(const TMeta* __restrict__ meta, u64 nk, u64* __restrict__ sz,
+                                                       u64* __restrict__ lens) {
+  const u64 s = gid();
+  if (s > nk) return;
+  if (s == nk) {
+    sz[s] = lens[s] = 0;
     return;
   }
-  const u32 k = A.dseg[j];
-  const DInfo D = A.dinfo[k];
-  const u64 t = A.dts[j];
-  bool slow = false;
-  u32 keep = 0;
-  u64 p = D.hi;
-  if (t >= D.cut && !A.bad[k]) {
-    if (D.lo == D.hi || t > D.newest) {
-      p = D.lo;
-      keep = 1;
-    } else {
-      slow = true;
-    }
-  }
-  A.slow[j] = slow;  // compacted into the worklist by DeviceSelect
-  if (!slow) {
-    A.flag_b[j] = keep;
-    A.prel[j] = (u32)(p - D.lo);
-  }
+  const u32 n = meta[s].len;
+  sz[s] = n ? (u64)n + (n / 2 > 2 ? n / 2 : 2) : 0;  // headroom for appends
+  lens[s] = n;
 }
 
-__global__ __launch_bounds__(kThreads) void k_tlog_flag_slow(TlogArgs A) {
-  const u32 n = *A.slow_n;
-  for (u64 w = gid(); w < n; w += (u64)gridDim.x * kThreads) {
-    const u32 j = A.slow_list[w];
-    const DInfo D = A.dinfo[A.dseg[j]];
-    const Ent x{A.dts[j], A.dpre[j], A.dlr[j]};
-    const u64 p = lower_bound_entry(A.rec, D.lo, D.hi, x, A.arena);
-    A.flag_b[j] = !(p < D.hi && cmp_at(A.rec, p, x, A.arena) == 0);
-    A.prel[j] = (u32)(p - D.lo);
-  }
-}
-
-__global__ __launch_bounds__(kThreads) void k_tlog_sizes_out(TlogArgs A, u64* __restrict__ cnt) {
-  const u64 s = gid();
-  if (s > A.nkeys) return;
-  if (s == A.nkeys) {
-    cnt[s] = 0;
-    return;
-  }
-  const u32 k = merging_key(A, s);
-  const u64 lo = A.off[s];
-  u64 hi = A.off[s + 1];
-  if (k != kNone && A.dinfo[k].raised && lo < hi && A.rec[hi - 1].ts < A.dinfo[k].cut) {
-    // entries are in non-increasing ts order: the cutoff drops a suffix
-    const u64 c = A.dinfo[k].cut;
-    u64 a = lo;
-    while (a < hi) {
-      const u64 m = (a + hi) >> 1;
-      if (A.rec[m].ts >= c) a = m + 1;
-      else hi = m;
-    }
-    hi = a;
-  }
-  A.keep_a[s] = hi - lo;
-  u64 n = hi - lo;
-  if (k != kNone) n += A.scan_b[A.doff[k + 1]] - A.scan_b[A.doff[k]];
-  cnt[s] = n;
-}
-
-// per slot: the state-side scatter record; merged cutoff stored; malformed
-// deltas counted
-__global__ __launch_bounds__(kThreads) void k_tlog_info(TlogArgs A, unsigned long long* __restrict__ skipped) {
-  const u64 s = gid();
-  if (s >= A.nkeys) return;
-  u32 k = A.dptr[s];
-  if (k != kNone) {
-    if (A.bad[k]) {
-      atomicAdd(skipped, 1ull);
-      k = kNone;
-    } else {
-      A.cutoff[s] = A.dinfo[k].cut;
-    }
-  }
-  KeyInfo I;
-  I.lo = A.off[s];
-  I.blo = k == kNone ? 0 : A.doff[k];
-  I.bhi = k == kNone ? 0 : A.doff[k + 1];
-  I.scan_lo = A.scan_b[I.blo];
-  I.front = I.bhi > I.blo && A.prel[I.bhi - 1] == 0 && A.scan_b[I.bhi] - I.scan_lo == I.bhi - I.blo;
-  A.info[s] = I;
-}
-
-// Output-parallel write of the merged logs.  A workgroup owns a fixed range
-// of kTileOut output positions (so a skewed log costs its size, never a
-// straggler), finds the keys of its range once (noff staged in LDS), and
-// every lane resolves its output position r of key s to its source:
-//   o_j = (kept deltas before j) + prel_j is non-decreasing over the key's
-//   delta segment; c = #kept deltas with o_j <= r.  Position r holds the
-//   kept delta of kept-rank c-1 if that one has o == r, else state entry
-//   r - c (always inside the surviving prefix).
-// Writes are one contiguous 32-B record stream per workgroup.
-constexpr u32 kTileOut = 4096;
-constexpr u32 kTileKeys = 2048;
-
-__global__ __launch_bounds__(kThreads) void k_tlog_gather_out(TlogArgs A, const u64* __restrict__ noff,
-                                                              TRec* __restrict__ out) {
-  __shared__ u64 loff[kTileKeys + 2];
-  __shared__ u64 sb_sh, se_sh;
-  const u64 nk = A.nkeys;
-  const u64 total = noff[nk];
+__global__ __launch_bounds__(kThreads) void k_cmp_copy(const TMeta* __restrict__ meta, u64 nk,
+                                                       const u64* __restrict__ roff, const TRec* __restrict__ src,
+                                                       TRec* __restrict__ dst) {
+  const u64 total = roff[nk];
   const u64 t0 = (u64)blockIdx.x * kTileOut;
   if (t0 >= total) return;
   const u64 t1 = t0 + kTileOut < total ? t0 + kTileOut : total;
-  if (threadIdx.x == 0) {
-    // last s with noff[s] <= x, over [0, nk]
-    u64 lo = 0, hi = nk + 1;
-    while (lo < hi) {
-      const u64 m = (lo + hi) >> 1;
-      if (noff[m] <= t0) lo = m + 1;
-      else hi = m;
-    }
-    sb_sh = lo - 1;
-    hi = nk + 1;
-    while (lo < hi) {
-      const u64 m = (lo + hi) >> 1;
-      if (noff[m] <= t1 - 1) lo = m + 1;
-      else hi = m;
-    }
-    se_sh = lo - 1;
-  }
-  __syncthreads();
-  const u64 sb = sb_sh, se = se_sh;
-  const bool local = se - sb + 2 <= kTileKeys + 2;
-  if (local)
-    for (u64 q = threadIdx.x; q < se - sb + 2; q += kThreads) loff[q] = noff[sb + q];
-  __syncthreads();
   for (u64 t = t0 + threadIdx.x; t < t1; t += kThreads) {
-    u64 lo = 0, hi = se - sb + 1;  // last q in [0, se-sb] with off(q) <= t
+    u64 lo = 0, hi = nk;
     while (lo < hi) {
       const u64 m = (lo + hi + 1) >> 1;
-      const u64 v = local ? loff[m] : noff[sb + m];
-      if (v <= t) lo = m;
+      if (roff[m] <= t) lo = m;
       else hi = m - 1;
     }
-    const u64 s = sb + lo;
-    const u64 r = t - (local ? loff[lo] : noff[s]);
-    const KeyInfo I = A.info[s];
-    u64 a = r;
-    if (I.front) {
-      // every delta entry kept, all before the state: deltas, then the state
-      const u64 K = I.bhi - I.blo;
-      if (r < K) {
-        const u64 j = I.blo + r;
-        if (r == 0) A.newest[s] = A.dts[j];
-        store_rec(out + t, A.dts[j], A.dpre[j], A.dlr[j], (u32)s);
-        continue;
-      }
-      a = r - K;
-    } else if (I.bhi > I.blo) {
-      u64 l = I.blo, h = I.bhi;  // jj: first j with o_j > r
-      while (l < h) {
-        const u64 m = (l + h) >> 1;
-        if ((u64)(A.scan_b[m] - (u32)I.scan_lo) + A.prel[m] <= r) l = m + 1;
-        else h = m;
-      }
-      const u64 jj = l;
-      const u64 c = A.scan_b[jj] - (u32)I.scan_lo;
-      if (c > 0) {
-        // the kept delta of kept-rank c-1: last j in [blo, jj) with scan_b[j] < scan_lo + c
-        l = I.blo;
-        h = jj;
-        while (l < h) {
-          const u64 m = (l + h) >> 1;
-          if ((u64)(A.scan_b[m] - (u32)I.scan_lo) < c) l = m + 1;
-          else h = m;
-        }
-        const u64 jk = l - 1;
-        if (c - 1 + A.prel[jk] == r) {
-          if (r == 0) A.newest[s] = A.dts[jk];
-          store_rec(out + t, A.dts[jk], A.dpre[jk], A.dlr[jk], (u32)s);
-          continue;
-        }
-      }
-      a = r - c;
-    }
-    const TRec x = load_rec(A.rec + I.lo + a);
-    if (r == 0) A.newest[s] = x.ts;
-    store_rec(out + t, x.ts, x.pre, x.lr, (u32)s);
+    const u64 r = t - roff[lo];
+    const TMeta m = meta[lo];
+    if (r >= m.len) continue;
+    const TRec x = load_rec(src + m.base + r);
+    store_rec(dst + t, x.ts, x.pre, x.lr);
   }
 }
 
-__global__ __launch_bounds__(kThreads) void k_fill_tail(u64* __restrict__ off, u64 from, u64 to) {
-  // off[from+1 .. to] = off[from]  (new, empty slots)
-  const u64 i = from + 1 + gid();
-  if (i <= to) off[i] = off[from];
+__global__ __launch_bounds__(kThreads) void k_cmp_meta(TMeta* __restrict__ meta, u64 nk, const u64* __restrict__ roff) {
+  const u64 s = gid();
+  if (s >= nk) return;
+  meta[s].base = roff[s];
+  meta[s].cap = (u32)(roff[s + 1] - roff[s]);
 }
 
-__global__ __launch_bounds__(kThreads) void k_tlog_sizes(const u64* __restrict__ off, const u64* __restrict__ cutoff,
-                                                         const u32* __restrict__ slots, u64 n, u64* __restrict__ len,
-                                                         u64* __restrict__ cut) {
+// ---- reads ----
+__global__ __launch_bounds__(kThreads) void k_tlog_sizes(const TMeta* __restrict__ meta, const u32* __restrict__ slots,
+                                                         u64 n, u64* __restrict__ len, u64* __restrict__ cut) {
   const u64 i = gid();
   if (i >= n) return;
-  const u64 s = slots[i];
-  len[i] = off[s + 1] - off[s];
-  cut[i] = cutoff[s];
+  const TMeta m = meta[slots[i]];
+  len[i] = m.len;
+  cut[i] = m.cut;
 }
 
-__global__ __launch_bounds__(kThreads) void k_tlog_gather(const u64* __restrict__ off, const TRec* __restrict__ rec,
+// newest first, as GET shows it (repo_tlog.pony:69-83)
+__global__ __launch_bounds__(kThreads) void k_tlog_gather(const TMeta* __restrict__ meta,
+                                                          const TRec* __restrict__ pool,
                                                           const u32* __restrict__ slots, const u64* __restrict__ ooff,
                                                           u64 n, u64* __restrict__ ots, u64* __restrict__ opre,
                                                           u64* __restrict__ olr) {
   const u64 i = gid();
   if (i >= n) return;
-  const u64 s = slots[i];
+  const TMeta m = meta[slots[i]];
   u64 o = ooff[i];
-  for (u64 j = off[s]; j < off[s + 1]; j++, o++) {
-    ots[o] = rec[j].ts;
-    opre[o] = rec[j].pre;
-    olr[o] = rec[j].lr;
+  for (u64 q = m.len; q-- > 0; o++) {
+    const TRec& x = pool[m.base + q];
+    ots[o] = x.ts;
+    opre[o] = x.pre;
+    olr[o] = x.lr;
   }
 }
 
@@ -429,26 +490,63 @@ u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kThreads - 1) / kThrea
     JY_HIP(eng, hipGetLastError());                                                                \
   } while (0)
 
-int32_t realloc_dead(jy_engine* eng, void** p, u64 bytes) {
-  // the buffer's contents are dead (it is rewritten): stream-ordered free
-  JY_TRACE("tlog entries realloc %llu bytes", (unsigned long long)bytes);
-  jy_dev_free(eng, *p);
-  *p = nullptr;
-  return jy_dev_alloc(eng, p, bytes, "tlog entries");
+int32_t scan_excl_u64(jy_engine* eng, const u64* in, u64* out, u64 n_plus_1) {
+  size_t tmp = 0;
+  JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, in, out, (int)n_plus_1, eng->stream));
+  void* t;
+  JY_TRY(jy_scratch(eng, 15, tmp, &t));
+  JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(t, tmp, in, out, (int)n_plus_1, eng->stream));
+  return JY_OK;
+}
+
+// rewrite every log back to back into a fresh pool with `room` free entries
+// after them; synchronises (the new size is read back)
+int32_t tlog_compact(jy_engine* eng, u64 room) {
+  TlogState& t = eng->tlog;
+  const u64 nk = eng->nkeys[JY_TLOG];
+  const double t_enter = jy_tracing() ? jy_now_us() : 0;
+  void* p;
+  JY_TRY(jy_scratch(eng, 16, (nk + 1) * 32, &p));
+  u64* sz = static_cast<u64*>(p);
+  u64* roff = sz + nk + 1;
+  u64* lens = roff + nk + 1;
+  u64* loff = lens + nk + 1;
+  LAUNCH(k_cmp_size, nk + 1, t.meta, nk, sz, lens);
+  JY_TRY(scan_excl_u64(eng, sz, roff, nk + 1));
+  JY_TRY(scan_excl_u64(eng, lens, loff, nk + 1));
+  JY_HIP(eng, hipMemcpyAsync(t.pin, roff + nk, 8, hipMemcpyDeviceToHost, eng->stream));
+  JY_HIP(eng, hipMemcpyAsync(t.pin + 1, loff + nk, 8, hipMemcpyDeviceToHost, eng->stream));
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  const u64 total = t.pin[0], live = t.pin[1];
+  // the next merges' worst case fits several times over before the next sync
+  const u64 ncap = std::max<u64>({total + room, 2 * total, eng->cfg.entry_capacity[JY_TLOG], 1024});
+  TRec* np = nullptr;
+  JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&np), ncap * sizeof(TRec), "tlog pool"));
+  if (total) {
+    const u32 tiles = (u32)std::max<u64>(1, (total + kTileOut - 1) / kTileOut);
+    hipLaunchKernelGGL(k_cmp_copy, dim3(tiles), dim3(kThreads), 0, eng->stream, t.meta, nk, roff, t.pool, np);
+    JY_HIP(eng, hipGetLastError());
+  }
+  if (nk) LAUNCH(k_cmp_meta, nk, t.meta, nk, roff);
+  jy_dev_free(eng, t.pool);
+  t.pool = np;
+  t.pcap = ncap;
+  *t.pin = total;
+  JY_HIP(eng, hipMemcpyAsync(t.ctr, t.pin, 8, hipMemcpyHostToDevice, eng->stream));
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));  // pin is reused right away
+  t.used_bound = total;
+  t.live_bound = live;
+  t.known = false;
+  JY_TRACE("tlog compact: %llu entries, pool %llu, %.1f us", (unsigned long long)total, (unsigned long long)ncap,
+           jy_now_us() - t_enter);
+  return JY_OK;
 }
 
 }  // namespace
 
 // ---------------------------------------------------------------------------
 // device exclusive scan: out[0..n] with out[n] = total (in[n] must be 0)
-int32_t jy_scan_u64(jy_engine* eng, const u64* in, u64* out, u64 n) {
-  size_t tmp = 0;
-  JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, in, out, (int)(n + 1), eng->stream));
-  void* t;
-  JY_TRY(jy_scratch(eng, 15, tmp, &t));
-  JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(t, tmp, in, out, (int)(n + 1), eng->stream));
-  return JY_OK;
-}
+int32_t jy_scan_u64(jy_engine* eng, const u64* in, u64* out, u64 n) { return scan_excl_u64(eng, in, out, n + 1); }
 
 // segment id of every item of a CSR (offs[0..nseg], n items): mark each
 // non-empty segment's first item, then an inclusive max-scan carries it on
@@ -464,43 +562,28 @@ int32_t jy_seg_ids(jy_engine* eng, const u64* offs, u64 nseg, u64 n, u32* out) {
   return JY_OK;
 }
 
-static int32_t ensure_entries(jy_engine* eng, int buf, u64 need) {
-  TlogState& t = eng->tlog;
-  if (need <= t.ecap[buf] && t.rec[buf]) return JY_OK;
-  const u64 nc = std::max<u64>(std::max<u64>(need + need / 2, eng->cfg.entry_capacity[JY_TLOG]), 1024);
-  JY_TRY(realloc_dead(eng, reinterpret_cast<void**>(&t.rec[buf]), nc * sizeof(TRec)));
-  t.ecap[buf] = nc;
-  return JY_OK;
-}
-
 int32_t jy_tlog_grow(jy_engine* eng, u64 need) {
   TlogState& t = eng->tlog;
-  if (need <= t.kcap && t.cutoff) return JY_OK;
+  if (!t.ctr) {
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.ctr), 64, "tlog counters"));
+    JY_HIP(eng, hipMemsetAsync(t.ctr, 0, 64, eng->stream));
+    JY_HIP(eng, hipHostMalloc(reinterpret_cast<void**>(&t.pin), 64, hipHostMallocDefault));
+    JY_HIP(eng, hipEventCreateWithFlags(&t.ready, hipEventDisableTiming));
+    t.pcap = std::max<u64>(eng->cfg.entry_capacity[JY_TLOG], 1024);
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.pool), t.pcap * sizeof(TRec), "tlog pool"));
+  }
+  if (need <= t.kcap && t.meta) return JY_OK;
   u64 nk = std::max<u64>(need, t.kcap ? t.kcap * 2 : need);
   nk = std::max<u64>((nk + 63) & ~63ull, 64);
-  void* c = t.cutoff;
-  JY_TRY(jy_realloc(eng, &c, t.kcap * 8, nk * 8, true));
-  t.cutoff = static_cast<u64*>(c);
-  void* w = t.newest;
-  JY_TRY(jy_realloc(eng, &w, t.kcap * 8, nk * 8, true));
-  t.newest = static_cast<u64*>(w);
-  for (int b = 0; b < 2; b++) {
-    void* o = t.off[b];
-    JY_TRY(jy_realloc(eng, &o, t.kcap ? (t.kcap + 1) * 8 : 0, (nk + 1) * 8, true));
-    t.off[b] = static_cast<u64*>(o);
-  }
+  void* m = t.meta;
+  JY_TRY(jy_realloc(eng, &m, t.kcap * sizeof(TMeta), nk * sizeof(TMeta), true));  // empty logs
+  t.meta = static_cast<TMeta*>(m);
   t.kcap = nk;
-  for (int b = 0; b < 2; b++) JY_TRY(ensure_entries(eng, b, 1));
   return JY_OK;
 }
 
-// new slots [from, to) start as empty logs: off[from+1..to] = off[from]
-int32_t jy_tlog_extend(jy_engine* eng, u64 from, u64 to) {
-  if (to <= from) return JY_OK;
-  TlogState& t = eng->tlog;
-  LAUNCH(k_fill_tail, to - from, t.off[t.cur], from, to);
-  return JY_OK;
-}
+// new slots start as empty logs: their meta is zeroed when it is allocated
+int32_t jy_tlog_extend(jy_engine*, u64, u64) { return JY_OK; }
 
 int32_t jy_tlog_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* dcut, const u64* doff, u64 nent,
                       const u64* dts, const u64* dpre, const u64* dlr) {
@@ -508,113 +591,84 @@ int32_t jy_tlog_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* dcut, 
   TlogState& t = eng->tlog;
   const u64 nk = eng->nkeys[JY_TLOG];
   if (nd == 0 || nk == 0) return JY_OK;
-  if (nent >= (1ull << 31)) return eng->fail(JY_ERANGE, "tlog converge: more than 2^31 entries in one call");
-  // live entries of the current buffer: exact when the previous merge's
-  // total has landed (non-blocking query), else the host upper bound; the
-  // kernels take the exact count from off[nkeys] in HBM.  The host never
-  // waits for the GPU here, so merges queue back to back.
-  const double t_enter = jy_tracing() ? jy_now_us() : 0;
-  u64 na = 0;
-  if (t.nent_known) {
-    const hipError_t q = hipEventQuery(eng->total_ready);
-    if (q == hipSuccess) na = eng->pin_total[0];
-    else if (q == hipErrorNotReady) na = t.nent_bound;
-    else JY_HIP(eng, q);
-  }
-  const double t_synced = jy_tracing() ? jy_now_us() : 0;
-  const int cur = t.cur, nxt = 1 - cur;
-  JY_TRY(ensure_entries(eng, nxt, na + nent));
+  // worst case of fresh pool space this merge takes: every touched log
+  // rebuilt into pow2_cap(new length) <= 4 * length + 8 entries
+  const u64 need = 4 * (t.live_bound + nent) + 8 * nd + 64;
+  if (t.known && hipEventQuery(t.ready) == hipSuccess) t.used_bound = *t.pin;
 
   TlogArgs A{};
-  A.off = t.off[cur];
-  A.rec = t.rec[cur];
-  A.cutoff = t.cutoff;
-  A.newest = t.newest;
-  A.nkeys = nk;
-  A.na = na;
+  A.arena = eng->arena[JY_TLOG].p;
   A.nd = nd;
-  A.nb = nent;
   A.slot = slot;
   A.dcut = dcut;
   A.doff = doff;
   A.dts = dts;
   A.dpre = dpre;
   A.dlr = dlr;
-  A.arena = eng->arena[JY_TLOG].p;
   void* p;
   JY_TRY(jy_scratch(eng, 8, nk * 4, &p));
   A.dptr = static_cast<u32*>(p);
-  JY_TRY(jy_scratch(eng, 9, nd * (sizeof(DInfo) + 4), &p));
-  A.dinfo = static_cast<DInfo*>(p);
-  A.bad = reinterpret_cast<u32*>(A.dinfo + nd);
-  JY_TRY(jy_scratch(eng, 11, nk * 8, &p));
-  A.keep_a = static_cast<u64*>(p);
-  JY_TRY(jy_scratch(eng, 12, (nent + 1) * 20 + 16, &p));
-  A.flag_b = static_cast<u32*>(p);
-  A.scan_b = A.flag_b + nent + 1;
-  A.prel = A.scan_b + nent + 1;
-  A.slow = A.prel + nent + 1;
-  A.slow_list = A.slow + nent + 1;
-  A.slow_n = A.slow_list + nent + 1;
-  JY_TRY(jy_scratch(eng, 16, (nk + 1) * 8, &p));
-  u64* cnt = static_cast<u64*>(p);
-  JY_TRY(jy_scratch(eng, 18, nk * sizeof(KeyInfo), &p));
-  A.info = static_cast<KeyInfo*>(p);
-  JY_TRY(jy_scratch(eng, 17, std::max<u64>(nent, 1) * 4, &p));
-  A.dseg = static_cast<const u32*>(p);
-  JY_TRY(jy_seg_ids(eng, doff, nd, nent, static_cast<u32*>(p)));
-
+  JY_TRY(jy_scratch(eng, 9, nd * (sizeof(PInfo) + 4) + 64, &p));
+  A.pinfo = static_cast<PInfo*>(p);
+  A.bad = reinterpret_cast<u32*>(A.pinfo + nd);
+  JY_TRY(jy_scratch(eng, 12, std::max<u64>(nent, 1) * 8, &p));
+  u32* erank = static_cast<u32*>(p);
+  u32* eqx = erank + std::max<u64>(nent, 1);
+  const u32 tiles = (u32)((nd + kTile - 1) / kTile);
+  u64* roff = nullptr;
   JY_HIP(eng, hipMemsetAsync(A.dptr, 0xFF, nk * 4, eng->stream));
   JY_HIP(eng, hipMemsetAsync(A.bad, 0, nd * 4, eng->stream));
   LAUNCH(k_tlog_prep, nd, A);
-  if (nent) LAUNCH(k_tlog_validate, nent, A);
-  LAUNCH(k_tlog_flag_b, nent + 1, A);
-  if (nent) {
-    size_t tmp = 0;
-    hipcub::CountingInputIterator<u32> idx(0);
-    JY_HIP(eng, hipcub::DeviceSelect::Flagged(nullptr, tmp, idx, A.slow, A.slow_list, A.slow_n, (int)nent,
-                                              eng->stream));
-    JY_TRY(jy_scratch(eng, 15, tmp, &p));
-    JY_HIP(eng, hipcub::DeviceSelect::Flagged(p, tmp, idx, A.slow, A.slow_list, A.slow_n, (int)nent, eng->stream));
-    const u32 g = (u32)std::min<u64>(2048, (nent + kThreads - 1) / kThreads);
-    hipLaunchKernelGGL(k_tlog_flag_slow, dim3(g), dim3(kThreads), 0, eng->stream, A);
+  for (int attempt = 0;; attempt++) {
+    A.meta = t.meta;
+    A.pool = t.pool;
+    JY_TRY(jy_scratch(eng, 16, (nd + 1) * 16, &p));
+    A.relsz = static_cast<u64*>(p);
+    roff = A.relsz + nd + 1;
+    hipLaunchKernelGGL(k_tlog_tile, dim3(tiles), dim3(kTile), 0, eng->stream, A, t.pool, erank, eqx);
     JY_HIP(eng, hipGetLastError());
+    JY_TRY(scan_excl_u64(eng, A.relsz, roff, nd + 1));
+    if (t.used_bound + need <= t.pcap) {
+      t.used_bound += need;
+      break;
+    }
+    // the worst case may not fit: wait for the exact rebuild size (nothing
+    // is published yet, so a compaction can still move every log)
+    JY_HIP(eng, hipMemcpyAsync(t.pin + 2, roff + nd, 8, hipMemcpyDeviceToHost, eng->stream));
+    JY_HIP(eng, hipMemcpyAsync(t.pin, t.ctr, 8, hipMemcpyDeviceToHost, eng->stream));
+    JY_HIP(eng, hipStreamSynchronize(eng->stream));
+    t.used_bound = t.pin[0];
+    const u64 rebuilt = t.pin[2];
+    if (t.used_bound + rebuilt <= t.pcap) {
+      t.used_bound += rebuilt;
+      break;
+    }
+    if (attempt == 2) return eng->fail(JY_ENOMEM, "tlog pool: no room after compaction");
+    // room for this merge's rebuilds several times over; the last attempt
+    // takes the worst case
+    JY_TRY(tlog_compact(eng, attempt == 0 ? 4 * (rebuilt + nent) : need));
   }
-  {
-    size_t tmp = 0;
-    JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, A.flag_b, A.scan_b, (int)(nent + 1), eng->stream));
-    JY_TRY(jy_scratch(eng, 15, tmp, &p));
-    JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(p, tmp, A.flag_b, A.scan_b, (int)(nent + 1), eng->stream));
-  }
-  LAUNCH(k_tlog_sizes_out, nk + 1, A, cnt);
-  JY_TRY(jy_scan_u64(eng, cnt, t.off[nxt], nk));
-  LAUNCH(k_tlog_info, nk, A, reinterpret_cast<unsigned long long*>(eng->skipped_dev));
-  {
-    // output size bound: surviving state + kept delta <= na + nent
-    const u64 nout = na + nent;
-    const u32 tiles = (u32)std::max<u64>(1, (nout + kTileOut - 1) / kTileOut);
-    hipLaunchKernelGGL(k_tlog_gather_out, dim3(tiles), dim3(kThreads), 0, eng->stream, A, t.off[nxt], t.rec[nxt]);
-    JY_HIP(eng, hipGetLastError());
-  }
-  // publish the new total for the next call (read back asynchronously)
-  JY_HIP(eng, hipMemcpyAsync(eng->pin_total, t.off[nxt] + nk, 8, hipMemcpyDeviceToHost, eng->stream));
-  JY_HIP(eng, hipEventRecord(eng->total_ready, eng->stream));
-  if (jy_tracing()) JY_TRACE("tlog merge host: wait %.1f us, issue %.1f us", t_synced - t_enter, jy_now_us() - t_synced);
-  t.nent_known = true;
-  t.nent_bound = na + nent;
-  t.cur = nxt;
+  t.live_bound += nent;
+  hipLaunchKernelGGL(k_tlog_commit, dim3(tiles), dim3(kTile), 0, eng->stream, A, roff, t.ctr, t.pool, erank,
+                     eqx, reinterpret_cast<unsigned long long*>(eng->skipped_dev));
+  JY_HIP(eng, hipGetLastError());
+  hipLaunchKernelGGL(k_tlog_bump, dim3(1), dim3(1), 0, eng->stream, t.ctr, roff, nd);
+  JY_HIP(eng, hipGetLastError());
+  // publish the bump pointer for the next call (read back asynchronously)
+  JY_HIP(eng, hipMemcpyAsync(t.pin, t.ctr, 8, hipMemcpyDeviceToHost, eng->stream));
+  JY_HIP(eng, hipEventRecord(t.ready, eng->stream));
+  t.known = true;
   return JY_OK;
 }
 
 int32_t jy_tlog_sizes(jy_engine* eng, u64 n, const u32* slots, u64* len, u64* cut) {
   TlogState& t = eng->tlog;
-  LAUNCH(k_tlog_sizes, n, t.off[t.cur], t.cutoff, slots, n, len, cut);
+  LAUNCH(k_tlog_sizes, n, t.meta, slots, n, len, cut);
   return JY_OK;
 }
 
 int32_t jy_tlog_gather(jy_engine* eng, u64 n, const u32* slots, const u64* ooff, u64* ts, u64* pre, u64* lr) {
   TlogState& t = eng->tlog;
-  const int c = t.cur;
-  LAUNCH(k_tlog_gather, n, t.off[c], t.rec[c], slots, ooff, n, ts, pre, lr);
+  LAUNCH(k_tlog_gather, n, t.meta, t.pool, slots, ooff, n, ts, pre, lr);
   return JY_OK;
 }

@@ -135,3 +135,29 @@ def test_large_synthetic(oracle_mod, engine):
         want.converge(b)
         got.converge_deltas(b)
     assert_state_equal(O.TLOG, want.state(), got.state())
+
+
+def test_many_rounds_pool_reuse(oracle_mod):
+    """ten config-4 rounds on a small pool: appends, rebuilds (ties, older
+    entries, full segments), cutoff drops and several pool compactions, with
+    the state compared after every round"""
+    from jylis_amd import synth as S
+    from jylis_amd.engine import Engine
+    from jylis_amd.repo import RepoTLOG
+    O = oracle_mod
+    eng = Engine(device=0, entry_capacity=1024)
+    try:
+        st, dl = S.tlog_tables(3000, seed=S.BASE_SEED + 40, rounds=10, mean_state=3, mean_delta=3)
+        want = O.Repo(O.TLOG)
+        got = RepoTLOG(eng)
+        for b in [st] + dl:
+            want.converge(b)
+            got.converge_deltas(b)
+            assert_state_equal(O.TLOG, want.state(), got.state())
+        # a full-state delta (everything duplicates) leaves the state as is
+        full = want.state()
+        want.converge(full)
+        got.converge_deltas(full)
+        assert_state_equal(O.TLOG, want.state(), got.state())
+    finally:
+        eng.close()
