@@ -129,10 +129,17 @@ def cpu_baseline(mode, rounds=2):
         st, dl = S.ujson_tables(D, seed=S.BASE_SEED + 5, rounds=rounds, R=16)
         repo = O.Repo(O.UJSON, 1)
         repo.converge(st)
-        n_el = len(st["elems"])
         for d in dl:
+            # units as on the GPU line: dots of the touched documents' state
+            # (elements + cloud) plus the delta's dots (untimed bookkeeping)
+            cur = repo.state()
+            eo, co = cur["el_offs"].astype(np.int64), cur["cloud_offs"].astype(np.int64)
+            kb, ko = cur["key_bytes"], cur["key_offs"].astype(np.int64)
+            size = {bytes(kb[ko[i]:ko[i + 1]]): (eo[i + 1] - eo[i]) + (co[i + 1] - co[i]) for i in range(len(ko) - 1)}
+            dkb, dko = d["key_bytes"], d["key_offs"].astype(np.int64)
+            units += sum(int(size.get(bytes(dkb[dko[i]:dko[i + 1]]), 0)) for i in range(len(dko) - 1))
+            units += len(d["elems"]) + len(d["cloud_ids"])
             b = O.Batch(O.UJSON, d)
-            units += 2 * n_el + len(d["elems"])
             t0 = time.perf_counter()
             repo.converge(b)
             t_conv += time.perf_counter() - t0
@@ -410,8 +417,16 @@ def bench_ujson(args, eng, dev, dist, rank, world):
         dev_batches.append((tuple(_to_dev(a, dev) for a in (slots, eo, dots, elems, vo, vv, co, cloud)),
                             len(slots), len(dots), len(cloud)))
     eng.sync()
-    n_el0 = len(st["elems"])
-    n_cl0 = len(st["cloud_ids"])
+    # the documents each batch touches, with their sizes in the state the
+    # steps start from (sizes drift slowly over the steps)
+    s_all = np.arange(eng.nkeys(UJSON), dtype=np.uint32)
+    ne_all, nc_all = np.empty(len(s_all), np.uint64), np.empty(len(s_all), np.uint64)
+    eng._check(eng.lib.jy_ujson_read_sizes(eng.h, len(s_all), s_all.ctypes.data, ne_all.ctypes.data,
+                                           nc_all.ctypes.data))
+    touched = []
+    for b in dl:
+        sl = eng.lookup(UJSON, (b["key_bytes"], b["key_offs"])).astype(np.int64)
+        touched.append((float(ne_all[sl].sum()), float(nc_all[sl].sum())))
 
     def step(i):
         eng.ujson_converge(*dev_batches[i % nb][0])
@@ -419,31 +434,31 @@ def bench_ujson(args, eng, dev, dist, rank, world):
     elapsed, kt = _timed(args.steps, args.warmup, step, dist, dev, eng=eng)
     t = _max_over_ranks(elapsed, dist, dev)
     k = float(np.mean(kt))
-    # live sizes: average of the initial and final state (they drift slowly)
-    s = np.arange(eng.nkeys(UJSON), dtype=np.uint32)
-    ne, nc = np.empty(len(s), np.uint64), np.empty(len(s), np.uint64)
-    eng._check(eng.lib.jy_ujson_read_sizes(eng.h, len(s), s.ctypes.data, ne.ctypes.data, nc.ctypes.data))
-    n_el0 = (n_el0 + int(ne.sum())) / 2
-    n_cl0 = (n_cl0 + int(nc.sum())) / 2
-    # bytes: every doc's elements and cloud are read and rewritten (CSR rebuild),
-    # the vv row is read for every doc; delta dots / cloud read once
-    nd_docs = float(np.mean([b[1] for b in dev_batches]))
-    nd_el = float(np.mean([b[2] for b in dev_batches]))
-    nd_cl = float(np.mean([b[3] for b in dev_batches]))
+    used = [(args.warmup + i) % nb for i in range(args.steps)]
+    nd_docs = float(np.mean([dev_batches[i][1] for i in used]))
+    nd_el = float(np.mean([dev_batches[i][2] for i in used]))
+    nd_cl = float(np.mean([dev_batches[i][3] for i in used]))
+    st_el = float(np.mean([touched[i][0] for i in used]))
+    st_cl = float(np.mean([touched[i][1] for i in used]))
     R = 16
-    bytes_conv = 16 * n_el0 * 2 + 8 * n_cl0 * 2 + 16 * nd_el + 8 * nd_cl + 16 * D + 8 * R * nd_docs * 2
-    dots_examined = 2 * n_el0 + nd_el
+    # 16 B per dot read + 16 B per dot written, 8R B of context
+    # read twice and written once per doc; the dots are those of the touched
+    # documents (state) and of the delta -- untouched documents are not read
+    bytes_conv = 32 * (st_el + nd_el) + 16 * (st_cl + nd_cl) + 24 * R * nd_docs
+    dots_examined = st_el + st_cl + nd_el + nd_cl
     return {"workload": f"UJSON converge: {D} docs (~8 leaves, R=16), Zipf(1.1) delta docs per step "
                         f"({int(nd_docs)} docs, {int(nd_el)} dots, {int(nd_cl)} cloud dots), "
                         f"70/20/10 INS/RM/CLR (SURVEY 8d config 5)",
             "unit_of_work": "dot examined", "value": world * dots_examined * args.steps / t,
             "ms_per_step": t / args.steps * 1e3, "generate_s": gen_s,
+            "delta_docs_per_s": world * nd_docs * args.steps / t,
             "roofline": {"bound": "hbm", "achieved": bytes_conv / k / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": bytes_conv / k / 1e9 / HBM_PEAK_GBS,
-                         "kernel": "UJSON merge path (k_uj_*, whole converge)",
+                         "kernel": "UJSON converge (k_uj_*, all launches of one call)",
                          "converge_ms_avg": k * 1e3, "bytes_per_converge": bytes_conv,
-                         "bytes_note": "16 B per element read+written, 8 B per cloud dot read+written, "
-                                       "8R B vv per delta doc read+write, 16 B per doc offsets"}}
+                         "bytes_note": "SURVEY 8d per dot examined (touched documents' state dots + delta dots): "
+                                       "16 B read + 16 B written per element, 8 + 8 B per cloud dot, 24R B "
+                                       "context per delta doc"}}
 
 
 MODES = {"gcount": bench_gcount, "treg": bench_treg, "tlog": bench_tlog, "ujson": bench_ujson}

@@ -218,14 +218,6 @@ void jy_engine_destroy(jy_engine* eng) {
   for (int w = 0; w < 2; w++) F(eng->cnt[w].slab);
   F(eng->treg.ts);
   F(eng->treg.val);
-  for (int b = 0; b < 2; b++) {
-    F(eng->ujson.eoff[b]);
-    F(eng->ujson.rec[b]);
-    F(eng->ujson.coff[b]);
-    F(eng->ujson.cloud[b]);
-    F(eng->ujson.eseg[b]);
-    F(eng->ujson.cseg[b]);
-  }
   F(eng->tlog.meta);
   F(eng->tlog.pool);
   F(eng->tlog.ctr);
@@ -233,6 +225,11 @@ void jy_engine_destroy(jy_engine* eng) {
   if (eng->tlog.ready) hipEventDestroy(eng->tlog.ready);
   for (auto& k : eng->kdir) jy_keydir_free(eng, k);
   F(eng->ujson.vv);
+  F(eng->ujson.meta);
+  F(eng->ujson.epool);
+  F(eng->ujson.cpool);
+  F(eng->ujson.ctr);
+  if (eng->ujson.pin) hipHostFree(eng->ujson.pin);
   for (auto& a : eng->arena) F(a.p);
   for (auto& s : eng->scratch) F(s.p);
   if (eng->stream) hipStreamSynchronize(eng->stream);

@@ -133,21 +133,26 @@ struct alignas(16) URec {
   u64 dot, elem;
 };
 
-struct UjsonState {  // CSR elements + CSR cloud (double-buffered), dense vv
-  u64* eoff[2] = {nullptr, nullptr};  // [kcap + 1]
-  URec* rec[2] = {nullptr, nullptr};
-  u32* eseg[2] = {nullptr, nullptr};  // slot of each element
-  u64 ecap[2] = {0, 0};
-  u64* coff[2] = {nullptr, nullptr};  // [kcap + 1]
-  u64* cloud[2] = {nullptr, nullptr};
-  u32* cseg[2] = {nullptr, nullptr};  // slot of each cloud dot
-  u64 ccap[2] = {0, 0};
-  int cur = 0;
-  u64* vv = nullptr;  // [kcap][R]
+// per document: its segments of the element pool (records ascending by dot)
+// and of the cloud pool (dots ascending)
+struct alignas(16) UMeta {
+  u64 ebase;
+  u32 elen, ecap;
+  u64 cbase;
+  u32 clen, ccap;
+};
+
+struct UjsonState {  // per-document pool segments + dense vv
+  UMeta* meta = nullptr;  // [kcap]
+  URec* epool = nullptr;  // element pool
+  u64 epcap = 0;
+  u64* cpool = nullptr;   // cloud pool
+  u64 cpcap = 0;
+  u64* ctr = nullptr;     // device: [0] element bump pointer, [1] cloud bump pointer
+  u64* pin = nullptr;     // pinned readback
+  u64* vv = nullptr;      // [kcap][R]
   u32 R = 0;
   u64 kcap = 0;
-  u64 nel_bound = 0, ncloud_bound = 0;
-  bool known = false;  // pin_total[1..2] hold the live totals after a merge
 };
 
 struct Arena {

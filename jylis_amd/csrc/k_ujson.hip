@@ -11,9 +11,20 @@
 //              their column's vv are folded into the vv)
 // Elements are opaque handles (interned (path, value) leaves).
 //
-// HBM layout per type: dots packed (column << 48 | seq); per slot CSR of
-// 16-B element records (dot ascending, elem) + slot-of-element; per slot CSR
-// of cloud dots ascending (+ slot-of-dot); dense vv [kcap][R].
+// HBM layout per type: dots packed (column << 48 | seq); per document a
+// UMeta naming its segment of the element pool (16-B records (dot, elem),
+// ascending by dot) and of the cloud pool (dots ascending); dense vv
+// [kcap][R].
+//
+// A converge touches ONLY the documents of its batch.  Their state segments
+// form the "touched state": flat index spaces over the delta documents (ao /
+// co = exclusive scans of their sizes), merged with the delta by the
+// per-element merge path below; every merged document is written as one
+// fresh run at the pools' bump pointers and its UMeta repointed.  Untouched
+// documents are never read or moved (the Zipf config-5 stream touches ~17 %
+// of them).  The host reads the touched sizes and the bump pointers back once
+// per converge (they size the launches); when a pool cannot hold the touched
+// state plus the delta, every document is first compacted into a new pool.
 //
 // Parallel shape: ONE THREAD PER ELEMENT / CLOUD DOT, not per document.
 // Delta documents follow a Zipf(1.1) popularity: the
@@ -33,8 +44,9 @@
 // concatenated so one scan serves them (positions only ever use differences
 // of scan values inside one side).  A converge is ~20 launches.
 //
-// Roofline: HBM.  Per element: 16 B read + 20 B written (+ 4 B flag, 4 B
-// scan); per cloud dot 8 B read + 12 B written; vv rows of delta docs.
+// Roofline: HBM.  Per touched element: 16 B read + 16 B written (+ 4 B
+// flag, 4 B scan, 4 B doc id); per touched cloud dot 8 B read + 8 B written;
+// vv rows and metas of delta docs.
 
 #include <hipcub/hipcub.hpp>
 
@@ -89,16 +101,22 @@ __device__ __forceinline__ void store_rec(URec* p, u64 d, u64 e) {
 }
 
 struct UjArgs {
-  // state (current buffers)
-  const u64* eoff;
-  const URec* rec;
-  const u32* eseg;
-  const u64* coff;
-  const u64* cloud;
-  const u32* cseg;
+  // state
+  const UMeta* meta;
+  const URec* rec;    // element pool
+  const u64* cloud;   // cloud pool
   u64* vv;
   u32 R;
-  u64 nkeys, na, ca;  // slots, live elements, live cloud dots
+  // touched state: per delta doc its pool segments and flat offsets
+  u64* abase;
+  u64* asz;    // [nd + 1]
+  u64* ao;     // [nd + 1] exclusive scan of asz
+  u64* cbs;
+  u64* csz;    // [nd + 1]
+  u64* co;     // [nd + 1]
+  const u32* aseg;   // [ta] delta doc of each touched state element
+  const u32* acseg;  // [tc] delta doc of each touched state cloud dot
+  u64 ta, tc;
   // delta batch
   u64 nd, nb, cb, nvv;
   const u32* slot;
@@ -114,11 +132,12 @@ struct UjArgs {
   const u32* dcseg;  // [cb] delta doc of each delta cloud dot
   const u32* vseg;   // [nvv] delta doc of each delta vv entry
   // merge temporaries
-  u32* bad;  // [nd]
+  u32* bad;  // [nd] malformed delta or repeated slot: the doc is left untouched
+  u64* vvs;  // [nd][R] the state's vv rows as they were before this converge
   u64* vvd;  // [nd][R] the delta's own vv, dense
   u64* vvm;  // [nd][R] max(vv_A, vv_B)
   u64* vvn;  // [nd][R] after compaction
-  // keep flags, concatenated [flag_a (na+1) | flag_b (nb+1) | cflag_b (cb+1)]
+  // keep flags, concatenated [flag_a (ta+1) | flag_b (nb+1) | cflag_b (cb+1)]
   // and their exclusive scan in the same layout
   u32* flag_a;
   u32* flag_b;
@@ -126,7 +145,7 @@ struct UjArgs {
   const u32* scan_a;
   const u32* scan_b;
   const u32* cscan_b;
-  // cloud compaction survivors [keep_ca (ca+1) | keep_cb (cb+1)] + scan
+  // cloud compaction survivors [keep_ca (tc+1) | keep_cb (cb+1)] + scan
   u32* keep_ca;
   u32* keep_cb;
   const u32* kscan_a;
@@ -134,9 +153,9 @@ struct UjArgs {
   unsigned long long* skipped;
 };
 
-__device__ __forceinline__ bool in_state_ctx(const UjArgs& A, u64 s, u64 d) {
-  if (dseq(d) <= A.vv[s * A.R + dcol(d)]) return true;
-  return contains(A.cloud, A.coff[s], A.coff[s + 1], d);
+__device__ __forceinline__ bool in_state_ctx(const UjArgs& A, u32 k, u64 d) {
+  if (dseq(d) <= A.vvs[(u64)k * A.R + dcol(d)]) return true;
+  return contains(A.cloud, A.cbs[k], A.cbs[k] + A.csz[k], d);
 }
 __device__ __forceinline__ bool in_delta_ctx(const UjArgs& A, u32 k, u64 d) {
   if (dseq(d) <= A.vvd[(u64)k * A.R + dcol(d)]) return true;
@@ -160,7 +179,8 @@ __device__ __forceinline__ int range_of(const Ranges& G, u64& i) {
   return r;
 }
 
-// ---- P0: per (doc, column): dptr, bad, state vv gather, delta vv cleared ---------
+// ---- P0: per (doc, column): repeated slots, touched-state sizes, vv rows ----------
+// dptr[] and bad[] are cleared before this launch.
 __global__ __launch_bounds__(kThreads) void k_uj_prep(UjArgs A) {
   const u64 t = (u64)blockIdx.x * kThreads + threadIdx.x;
   if (t >= A.nd * A.R) return;
@@ -168,10 +188,24 @@ __global__ __launch_bounds__(kThreads) void k_uj_prep(UjArgs A) {
   const u32 c = (u32)(t - k * A.R);
   const u64 s = A.slot[k];
   if (c == 0) {
-    A.dptr[s] = (u32)k;
-    A.bad[k] = 0;
+    const u32 prev = atomicCAS(A.dptr + s, kNone, (u32)k);
+    if (prev != kNone) {  // one delta per doc per call: both copies are skipped
+      A.bad[k] = 1;
+      A.bad[prev] = 1;
+    }
+    const UMeta m = A.meta[s];
+    A.abase[k] = m.ebase;
+    A.asz[k] = m.elen;
+    A.cbs[k] = m.cbase;
+    A.csz[k] = m.clen;
   }
-  A.vvm[t] = A.vv[s * A.R + c];
+  if (t == 0) {
+    A.asz[A.nd] = 0;
+    A.csz[A.nd] = 0;
+  }
+  const u64 v = A.vv[s * A.R + c];
+  A.vvs[t] = v;  // k_uj_scatter overwrites vv while it still tests the state context
+  A.vvm[t] = v;
   A.vvd[t] = 0;
 }
 
@@ -203,7 +237,7 @@ __global__ __launch_bounds__(kThreads) void k_uj_check(UjArgs A, Ranges G) {
   else validate(A, A.dcseg, A.dcoff, A.dcloud, i);
 }
 
-// ---- P2: a malformed delta doc leaves its key untouched (counted); vv max ---------
+// ---- P2: vv max; a malformed delta doc is counted (once per slot) ------------------
 __global__ __launch_bounds__(kThreads) void k_uj_drop_bad(UjArgs A) {
   const u64 t = (u64)blockIdx.x * kThreads + threadIdx.x;
   if (t >= A.nd * A.R) return;
@@ -212,23 +246,19 @@ __global__ __launch_bounds__(kThreads) void k_uj_drop_bad(UjArgs A) {
   A.vvm[t] = m;
   A.vvn[t] = m;
   const u64 k = t / A.R;
-  if (t - k * A.R == 0 && A.bad[k]) {
-    A.dptr[A.slot[k]] = kNone;
-    atomicAdd(A.skipped, 1ull);
-  }
+  if (t - k * A.R == 0 && A.bad[k] && A.dptr[A.slot[k]] == (u32)k) atomicAdd(A.skipped, 1ull);
 }
 
-// ---- P3: keep flags: state elements, delta elements, delta cloud dedupe ------------
+// ---- P3: keep flags: touched state elements, delta elements, delta cloud dedupe ----
 __device__ __forceinline__ void flag_a(const UjArgs& A, u64 i) {
-  if (i >= A.eoff[A.nkeys]) {  // A.na is a host bound; eoff[nkeys] is exact
+  if (i == A.ta) {
     A.flag_a[i] = 0;
     return;
   }
-  const u64 s = A.eseg[i];
-  const u32 k = A.dptr[s];
-  u32 keep = 1;
-  if (k != kNone) {
-    const u64 d = A.rec[i].dot;
+  const u32 k = A.aseg[i];
+  u32 keep = 0;
+  if (!A.bad[k]) {
+    const u64 d = A.rec[A.abase[k] + (i - A.ao[k])].dot;
     keep = contains(A.ddots, A.deoff[k], A.deoff[k + 1], d) || !in_delta_ctx(A, k, d);
   }
   A.flag_a[i] = keep;
@@ -239,13 +269,12 @@ __device__ __forceinline__ void flag_b(const UjArgs& A, u64 j) {
     return;
   }
   const u32 k = A.dseg[j];
-  const u64 s = A.slot[k];
   u32 keep = 0;
-  if (A.dptr[s] == k) {
+  if (!A.bad[k]) {
     const u64 d = A.ddots[j];
-    const u64 lo = A.eoff[s], hi = A.eoff[s + 1];
+    const u64 lo = A.abase[k], hi = lo + A.asz[k];
     const u64 p = lower_bound_rec(A.rec, lo, hi, d);
-    keep = !(p < hi && A.rec[p].dot == d) && !in_state_ctx(A, s, d);
+    keep = !(p < hi && A.rec[p].dot == d) && !in_state_ctx(A, k, d);
   }
   A.flag_b[j] = keep;
 }
@@ -256,9 +285,8 @@ __device__ __forceinline__ void cloud_dedupe(const UjArgs& A, u64 j) {
     return;
   }
   const u32 k = A.dcseg[j];
-  const u64 s = A.slot[k];
   u32 f = 0;
-  if (A.dptr[s] == k) f = !contains(A.cloud, A.coff[s], A.coff[s + 1], A.dcloud[j]);
+  if (!A.bad[k]) f = !contains(A.cloud, A.cbs[k], A.cbs[k] + A.csz[k], A.dcloud[j]);
   A.cflag_b[j] = f;
 }
 __global__ __launch_bounds__(kThreads) void k_uj_flags(UjArgs A, Ranges G) {
@@ -274,23 +302,24 @@ __global__ __launch_bounds__(kThreads) void k_uj_flags(UjArgs A, Ranges G) {
 // union rank of x (column c, seq q) above v: state dots of c in (v, q) plus
 // de-duplicated delta dots of c in (v, q)
 __device__ __forceinline__ void compact_a(const UjArgs& A, u64 i) {
-  if (i >= A.coff[A.nkeys]) {  // A.ca is a host bound; coff[nkeys] is exact
+  if (i == A.tc) {
     A.keep_ca[i] = 0;
     return;
   }
-  const u64 s = A.cseg[i];
-  const u32 k = A.dptr[s];
-  if (k == kNone) {
-    A.keep_ca[i] = 1;
+  const u32 k = A.acseg[i];
+  if (A.bad[k]) {
+    A.keep_ca[i] = 0;
     return;
   }
-  const u64 x = A.cloud[i];
+  const u64 lo0 = A.cbs[k];
+  const u64 pi = lo0 + (i - A.co[k]);
+  const u64 x = A.cloud[pi];
   const u32 c = dcol(x);
   const u64 q = dseq(x), v = A.vvm[(u64)k * A.R + c];
   u32 keep = 0;
   if (q > v) {
     const u64 lo = mkdot(c, v + 1);
-    const u64 ra = i - lower_bound(A.cloud, A.coff[s], i, lo);
+    const u64 ra = pi - lower_bound(A.cloud, lo0, pi, lo);
     const u64 blo = A.dcoff[k], bhi = A.dcoff[k + 1];
     const u64 b0 = lower_bound(A.dcloud, blo, bhi, lo);
     const u64 b1 = lower_bound(A.dcloud, b0, bhi, x);
@@ -309,15 +338,14 @@ __device__ __forceinline__ void compact_b(const UjArgs& A, u64 j) {
     return;
   }
   u32 keep = 0;
-  if (A.cflag_b[j]) {
+  if (A.cflag_b[j]) {  // (0 for malformed docs)
     const u32 k = A.dcseg[j];
-    const u64 s = A.slot[k];
     const u64 x = A.dcloud[j];
     const u32 c = dcol(x);
     const u64 q = dseq(x), v = A.vvm[(u64)k * A.R + c];
     if (q > v) {
       const u64 lo = mkdot(c, v + 1);
-      const u64 alo = A.coff[s], ahi = A.coff[s + 1];
+      const u64 alo = A.cbs[k], ahi = alo + A.csz[k];
       const u64 a0 = lower_bound(A.cloud, alo, ahi, lo);
       const u64 ra = lower_bound(A.cloud, a0, ahi, x) - a0;
       const u64 b0 = lower_bound(A.dcloud, A.dcoff[k], j, lo);
@@ -339,98 +367,79 @@ __global__ __launch_bounds__(kThreads) void k_uj_compact(UjArgs A, Ranges G) {
   else compact_b(A, i);
 }
 
-// ---- P5: per-slot output sizes ------------------------------------------------------
+// ---- P5: per delta doc output sizes ------------------------------------------------
 __global__ __launch_bounds__(kThreads) void k_uj_sizes_out(UjArgs A, u64* __restrict__ ne, u64* __restrict__ nc) {
-  const u64 s = (u64)blockIdx.x * kThreads + threadIdx.x;
-  if (s > A.nkeys) return;
-  if (s == A.nkeys) {
-    ne[s] = 0;
-    nc[s] = 0;
+  const u64 k = (u64)blockIdx.x * kThreads + threadIdx.x;
+  if (k > A.nd) return;
+  if (k == A.nd || A.bad[k]) {
+    ne[k] = 0;
+    nc[k] = 0;
     return;
   }
-  const u32 k = A.dptr[s];
-  u64 e = A.scan_a[A.eoff[s + 1]] - A.scan_a[A.eoff[s]];
-  u64 c = A.kscan_a[A.coff[s + 1]] - A.kscan_a[A.coff[s]];
-  if (k != kNone) {
-    e += A.scan_b[A.deoff[k + 1]] - A.scan_b[A.deoff[k]];
-    c += A.kscan_b[A.dcoff[k + 1]] - A.kscan_b[A.dcoff[k]];
-  }
-  ne[s] = e;
-  nc[s] = c;
+  ne[k] = (A.scan_a[A.ao[k + 1]] - A.scan_a[A.ao[k]]) + (A.scan_b[A.deoff[k + 1]] - A.scan_b[A.deoff[k]]);
+  nc[k] = (A.kscan_a[A.co[k + 1]] - A.kscan_a[A.co[k]]) + (A.kscan_b[A.dcoff[k + 1]] - A.kscan_b[A.dcoff[k]]);
 }
 
-// ---- P6: scatter (merge-path positions) + vv store + live totals --------------------
+// ---- P6: scatter into fresh pool runs (merge-path positions) + vv / meta store -----
 struct Out {
-  const u64* eoff;  // new offsets
-  const u64* coff;
-  URec* rec;
-  u32* eseg;
-  u64* cloud;
-  u32* cseg;
-  u64* totals;  // [2] live elements, live cloud dots
+  const u64* neo;  // exclusive scans of the per-doc output sizes
+  const u64* nco;
+  URec* epool;
+  u64* cpool;
+  UMeta* meta;
+  u64 eb0, cb0;  // bump pointers: this converge's runs start here
 };
 
 __device__ __forceinline__ void scatter_a(const UjArgs& A, const Out& O, u64 i) {
   if (!A.flag_a[i]) return;
-  const u64 s = A.eseg[i];
-  const u32 k = A.dptr[s];
-  const URec x = load_rec(A.rec + i);
+  const u32 k = A.aseg[i];
+  const URec x = load_rec(A.rec + A.abase[k] + (i - A.ao[k]));
   u64 e = x.elem;
-  u64 pos = O.eoff[s] + (A.scan_a[i] - A.scan_a[A.eoff[s]]);
-  if (k != kNone) {
-    const u64 lo = A.deoff[k], hi = A.deoff[k + 1];
-    const u64 p = lower_bound(A.ddots, lo, hi, x.dot);
-    pos += A.scan_b[p] - A.scan_b[lo];
-    if (p < hi && A.ddots[p] == x.dot && !in_state_ctx(A, s, x.dot)) e = A.delems[p];
-  }
-  store_rec(O.rec + pos, x.dot, e);
-  O.eseg[pos] = (u32)s;
+  u64 pos = O.neo[k] + (A.scan_a[i] - A.scan_a[A.ao[k]]);
+  const u64 lo = A.deoff[k], hi = A.deoff[k + 1];
+  const u64 p = lower_bound(A.ddots, lo, hi, x.dot);
+  pos += A.scan_b[p] - A.scan_b[lo];
+  if (p < hi && A.ddots[p] == x.dot && !in_state_ctx(A, k, x.dot)) e = A.delems[p];
+  store_rec(O.epool + O.eb0 + pos, x.dot, e);
 }
 __device__ __forceinline__ void scatter_b(const UjArgs& A, const Out& O, u64 j) {
   if (!A.flag_b[j]) return;
   const u32 k = A.dseg[j];
-  const u64 s = A.slot[k];
   const u64 d = A.ddots[j];
-  const u64 lo = A.eoff[s];
-  const u64 p = lower_bound_rec(A.rec, lo, A.eoff[s + 1], d);
-  const u64 pos = O.eoff[s] + (A.scan_b[j] - A.scan_b[A.deoff[k]]) + (A.scan_a[p] - A.scan_a[lo]);
-  store_rec(O.rec + pos, d, A.delems[j]);
-  O.eseg[pos] = (u32)s;
+  const u64 lo = A.abase[k];
+  const u64 pa = A.ao[k] + (lower_bound_rec(A.rec, lo, lo + A.asz[k], d) - lo);
+  const u64 pos = O.neo[k] + (A.scan_b[j] - A.scan_b[A.deoff[k]]) + (A.scan_a[pa] - A.scan_a[A.ao[k]]);
+  store_rec(O.epool + O.eb0 + pos, d, A.delems[j]);
 }
 __device__ __forceinline__ void cscatter_a(const UjArgs& A, const Out& O, u64 i) {
   if (!A.keep_ca[i]) return;
-  const u64 s = A.cseg[i];
-  const u32 k = A.dptr[s];
-  const u64 x = A.cloud[i];
-  u64 pos = O.coff[s] + (A.kscan_a[i] - A.kscan_a[A.coff[s]]);
-  if (k != kNone) {
-    const u64 lo = A.dcoff[k];
-    pos += A.kscan_b[lower_bound(A.dcloud, lo, A.dcoff[k + 1], x)] - A.kscan_b[lo];
-  }
-  O.cloud[pos] = x;
-  O.cseg[pos] = (u32)s;
+  const u32 k = A.acseg[i];
+  const u64 x = A.cloud[A.cbs[k] + (i - A.co[k])];
+  const u64 lo = A.dcoff[k];
+  const u64 pos = O.nco[k] + (A.kscan_a[i] - A.kscan_a[A.co[k]]) +
+                  (A.kscan_b[lower_bound(A.dcloud, lo, A.dcoff[k + 1], x)] - A.kscan_b[lo]);
+  O.cpool[O.cb0 + pos] = x;
 }
 __device__ __forceinline__ void cscatter_b(const UjArgs& A, const Out& O, u64 j) {
   if (!A.keep_cb[j]) return;
   const u32 k = A.dcseg[j];
-  const u64 s = A.slot[k];
   const u64 x = A.dcloud[j];
-  const u64 lo = A.coff[s];
-  const u64 pos = O.coff[s] + (A.kscan_b[j] - A.kscan_b[A.dcoff[k]]) +
-                  (A.kscan_a[lower_bound(A.cloud, lo, A.coff[s + 1], x)] - A.kscan_a[lo]);
-  O.cloud[pos] = x;
-  O.cseg[pos] = (u32)s;
+  const u64 lo = A.cbs[k];
+  const u64 pa = A.co[k] + (lower_bound(A.cloud, lo, lo + A.csz[k], x) - lo);
+  const u64 pos = O.nco[k] + (A.kscan_b[j] - A.kscan_b[A.dcoff[k]]) + (A.kscan_a[pa] - A.kscan_a[A.co[k]]);
+  O.cpool[O.cb0 + pos] = x;
 }
-// merged + compacted vv rows back into the state; thread 0 publishes totals
+// merged + compacted vv rows back into the state; column 0 repoints the doc
 __device__ __forceinline__ void vv_store(const UjArgs& A, const Out& O, u64 t) {
-  if (t == 0) {
-    O.totals[0] = O.eoff[A.nkeys];
-    O.totals[1] = O.coff[A.nkeys];
-  }
   const u64 k = t / A.R;
   const u32 c = (u32)(t - k * A.R);
   if (A.bad[k]) return;
-  A.vv[(u64)A.slot[k] * A.R + c] = A.vvn[t];
+  const u64 s = A.slot[k];
+  A.vv[s * A.R + c] = A.vvn[t];
+  if (c == 0) {
+    const u32 ne = (u32)(O.neo[k + 1] - O.neo[k]), nc = (u32)(O.nco[k + 1] - O.nco[k]);
+    O.meta[s] = UMeta{O.eb0 + O.neo[k], ne, ne, O.cb0 + O.nco[k], nc, nc};
+  }
 }
 __global__ __launch_bounds__(kThreads) void k_uj_scatter(UjArgs A, Out O, Ranges G) {
   u64 i;
@@ -445,41 +454,83 @@ __global__ __launch_bounds__(kThreads) void k_uj_scatter(UjArgs A, Out O, Ranges
   }
 }
 
-// ---- segment ids of up to 3 CSRs over the same docs, one scan ----------------------
+__global__ void k_uj_bump(u64* __restrict__ ctr, const u64* __restrict__ neo, const u64* __restrict__ nco, u64 nd,
+                          u64 eb0, u64 cb0) {
+  ctr[0] = eb0 + neo[nd];
+  ctr[1] = cb0 + nco[nd];
+}
+
+// ---- segment ids of up to 5 CSRs over the same docs, one scan ----------------------
 // mark the first item of every non-empty segment with (range << 28 | doc);
 // an inclusive max-scan carries it on (each range starts with a mark, and
 // marks grow with the range)
-__global__ __launch_bounds__(kThreads) void k_uj_seg_starts(const u64* __restrict__ o0, const u64* __restrict__ o1,
-                                                            const u64* __restrict__ o2, u64 nseg, u64 n0, u64 n1,
-                                                            u32* __restrict__ out) {
+struct SegSrc {
+  const u64* o[5];
+  u64 base[5];  // first item of each range in the concatenation
+};
+__global__ __launch_bounds__(kThreads) void k_uj_seg_starts(SegSrc S, u64 nseg, u32* __restrict__ out) {
   const u64 k = (u64)blockIdx.x * kThreads + threadIdx.x;
   if (k >= nseg) return;
-  if (o0[k] < o0[k + 1]) out[o0[k]] = (u32)k;
-  if (o1[k] < o1[k + 1]) out[n0 + o1[k]] = (1u << kSegBits) | (u32)k;
-  if (o2[k] < o2[k + 1]) out[n0 + n1 + o2[k]] = (2u << kSegBits) | (u32)k;
+#pragma unroll
+  for (u32 r = 0; r < 5; r++)
+    if (S.o[r][k] < S.o[r][k + 1]) out[S.base[r] + S.o[r][k]] = (r << kSegBits) | (u32)k;
 }
 __global__ __launch_bounds__(kThreads) void k_uj_seg_strip(u32* __restrict__ a, u64 n) {
   const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
   if (i < n) a[i] &= (1u << kSegBits) - 1;
 }
 
-__global__ __launch_bounds__(kThreads) void k_fill_tail(u64* __restrict__ off, u64 from, u64 to) {
-  const u64 i = from + 1 + (u64)blockIdx.x * kThreads + threadIdx.x;
-  if (i <= to) off[i] = off[from];
+// ---- compaction: every document rewritten back to back into fresh pools ------------
+__global__ __launch_bounds__(kThreads) void k_uj_cmp_size(const UMeta* __restrict__ meta, u64 nk,
+                                                          u64* __restrict__ se, u64* __restrict__ sc) {
+  const u64 s = (u64)blockIdx.x * kThreads + threadIdx.x;
+  if (s > nk) return;
+  se[s] = s == nk ? 0 : meta[s].elen;
+  sc[s] = s == nk ? 0 : meta[s].clen;
+}
+constexpr u32 kTileOut = 2048;
+template <bool kElems, typename T>
+__global__ __launch_bounds__(kThreads) void k_uj_cmp_copy(const UMeta* __restrict__ meta, u64 nk,
+                                                          const u64* __restrict__ off, const T* __restrict__ src,
+                                                          T* __restrict__ dst) {
+  const u64 total = off[nk];
+  const u64 t0 = (u64)blockIdx.x * kTileOut;
+  if (t0 >= total) return;
+  const u64 t1 = t0 + kTileOut < total ? t0 + kTileOut : total;
+  for (u64 t = t0 + threadIdx.x; t < t1; t += kThreads) {
+    u64 lo = 0, hi = nk;  // last slot with off <= t
+    while (lo < hi) {
+      const u64 m = (lo + hi + 1) >> 1;
+      if (off[m] <= t) lo = m;
+      else hi = m - 1;
+    }
+    const UMeta m = meta[lo];
+    dst[t] = src[(kElems ? m.ebase : m.cbase) + (t - off[lo])];
+  }
+}
+__global__ __launch_bounds__(kThreads) void k_uj_cmp_meta(UMeta* __restrict__ meta, u64 nk, const u64* __restrict__ eo,
+                                                          const u64* __restrict__ co) {
+  const u64 s = (u64)blockIdx.x * kThreads + threadIdx.x;
+  if (s >= nk) return;
+  UMeta m = meta[s];
+  m.ebase = eo[s];
+  m.ecap = m.elen;
+  m.cbase = co[s];
+  m.ccap = m.clen;
+  meta[s] = m;
 }
 
-__global__ __launch_bounds__(kThreads) void k_uj_sizes(const u64* __restrict__ eoff, const u64* __restrict__ coff,
-                                                       const u32* __restrict__ slots, u64 n, u64* __restrict__ ne,
-                                                       u64* __restrict__ nc) {
+// ---- reads ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void k_uj_sizes(const UMeta* __restrict__ meta, const u32* __restrict__ slots,
+                                                       u64 n, u64* __restrict__ ne, u64* __restrict__ nc) {
   const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
-  const u64 s = slots[i];
-  ne[i] = eoff[s + 1] - eoff[s];
-  nc[i] = coff[s + 1] - coff[s];
+  const UMeta m = meta[slots[i]];
+  ne[i] = m.elen;
+  nc[i] = m.clen;
 }
 
-__global__ __launch_bounds__(kThreads) void k_uj_gather(const u64* __restrict__ eoff, const URec* __restrict__ rec,
-                                                        const u64* __restrict__ coff,
+__global__ __launch_bounds__(kThreads) void k_uj_gather(const UMeta* __restrict__ meta, const URec* __restrict__ rec,
                                                         const u64* __restrict__ cloud, const u64* __restrict__ vv,
                                                         u32 R, const u32* __restrict__ slots, u64 n,
                                                         const u64* __restrict__ oeoff, const u64* __restrict__ ocoff,
@@ -488,61 +539,18 @@ __global__ __launch_bounds__(kThreads) void k_uj_gather(const u64* __restrict__ 
   const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
   const u64 s = slots[i];
+  const UMeta m = meta[s];
   u64 o = oeoff[i];
-  for (u64 j = eoff[s]; j < eoff[s + 1]; j++, o++) {
-    odots[o] = rec[j].dot;
-    oelems[o] = rec[j].elem;
+  for (u64 j = 0; j < m.elen; j++, o++) {
+    odots[o] = rec[m.ebase + j].dot;
+    oelems[o] = rec[m.ebase + j].elem;
   }
   o = ocoff[i];
-  for (u64 j = coff[s]; j < coff[s + 1]; j++, o++) ocloud[o] = cloud[j];
+  for (u64 j = 0; j < m.clen; j++, o++) ocloud[o] = cloud[m.cbase + j];
   for (u32 c = 0; c < R; c++) ovv[i * R + c] = vv[s * R + c];
 }
 
 u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kThreads - 1) / kThreads); }
-
-int32_t realloc_dead(jy_engine* eng, void** p, u64 bytes) {
-  // the buffer's contents are dead (it is rewritten): stream-ordered free
-  JY_TRACE("ujson buffers realloc %llu bytes", (unsigned long long)bytes);
-  jy_dev_free(eng, *p);
-  *p = nullptr;
-  return jy_dev_alloc(eng, p, bytes, "ujson buffers");
-}
-
-int32_t ensure_elems(jy_engine* eng, int b, u64 need) {
-  UjsonState& u = eng->ujson;
-  if (need <= u.ecap[b] && u.rec[b]) return JY_OK;
-  const u64 nc = std::max<u64>(std::max<u64>(need + need / 2, eng->cfg.entry_capacity[JY_UJSON]), 1024);
-  JY_TRY(realloc_dead(eng, reinterpret_cast<void**>(&u.rec[b]), nc * sizeof(URec)));
-  JY_TRY(realloc_dead(eng, reinterpret_cast<void**>(&u.eseg[b]), nc * 4));
-  u.ecap[b] = nc;
-  return JY_OK;
-}
-
-int32_t ensure_cloud(jy_engine* eng, int b, u64 need) {
-  UjsonState& u = eng->ujson;
-  if (need <= u.ccap[b] && u.cloud[b]) return JY_OK;
-  const u64 nc = std::max<u64>(need + need / 2, 1024);
-  JY_TRY(realloc_dead(eng, reinterpret_cast<void**>(&u.cloud[b]), nc * 8));
-  JY_TRY(realloc_dead(eng, reinterpret_cast<void**>(&u.cseg[b]), nc * 4));
-  u.ccap[b] = nc;
-  return JY_OK;
-}
-
-UjArgs state_args(jy_engine* eng) {
-  UjsonState& u = eng->ujson;
-  const int c = u.cur;
-  UjArgs A{};
-  A.eoff = u.eoff[c];
-  A.rec = u.rec[c];
-  A.eseg = u.eseg[c];
-  A.coff = u.coff[c];
-  A.cloud = u.cloud[c];
-  A.cseg = u.cseg[c];
-  A.vv = u.vv;
-  A.R = u.R;
-  A.nkeys = eng->nkeys[JY_UJSON];
-  return A;
-}
 
 #define LAUNCH(k, n, ...)                                                                          \
   do {                                                                                             \
@@ -550,38 +558,82 @@ UjArgs state_args(jy_engine* eng) {
     JY_HIP(eng, hipGetLastError());                                                                \
   } while (0)
 
+// rewrite every document back to back into new pools with `room_e` / `room_c`
+// free entries after them; synchronises (the new sizes are read back)
+int32_t ujson_compact(jy_engine* eng, u64 room_e, u64 room_c) {
+  UjsonState& u = eng->ujson;
+  const u64 nk = eng->nkeys[JY_UJSON];
+  void* p;
+  JY_TRY(jy_scratch(eng, 20, (nk + 1) * 32, &p));
+  u64* se = static_cast<u64*>(p);
+  u64* sc = se + nk + 1;
+  u64* eo = sc + nk + 1;
+  u64* co = eo + nk + 1;
+  LAUNCH(k_uj_cmp_size, nk + 1, u.meta, nk, se, sc);
+  JY_TRY(jy_scan_u64(eng, se, eo, nk));
+  JY_TRY(jy_scan_u64(eng, sc, co, nk));
+  JY_HIP(eng, hipMemcpyAsync(u.pin, eo + nk, 8, hipMemcpyDeviceToHost, eng->stream));
+  JY_HIP(eng, hipMemcpyAsync(u.pin + 1, co + nk, 8, hipMemcpyDeviceToHost, eng->stream));
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  const u64 te = u.pin[0], tc = u.pin[1];
+  // room for many merges like this one before the next compaction
+  const u64 ecap = std::max<u64>({te + 16 * room_e, 3 * te, eng->cfg.entry_capacity[JY_UJSON], 1024});
+  const u64 ccap = std::max<u64>({tc + 16 * room_c, 3 * tc, eng->cfg.entry_capacity[JY_UJSON], 1024});
+  JY_TRACE("ujson compact: %llu elements, %llu cloud dots -> pools %llu / %llu", (unsigned long long)te,
+           (unsigned long long)tc, (unsigned long long)ecap, (unsigned long long)ccap);
+  URec* ne = nullptr;
+  u64* nc = nullptr;
+  JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&ne), ecap * sizeof(URec), "ujson element pool"));
+  JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&nc), ccap * 8, "ujson cloud pool"));
+  if (te)
+    hipLaunchKernelGGL((k_uj_cmp_copy<true, URec>), dim3((u32)((te + kTileOut - 1) / kTileOut)), dim3(kThreads), 0,
+                       eng->stream, u.meta, nk, eo, u.epool, ne);
+  if (tc)
+    hipLaunchKernelGGL((k_uj_cmp_copy<false, u64>), dim3((u32)((tc + kTileOut - 1) / kTileOut)), dim3(kThreads), 0,
+                       eng->stream, u.meta, nk, co, u.cpool, nc);
+  JY_HIP(eng, hipGetLastError());
+  if (nk) LAUNCH(k_uj_cmp_meta, nk, u.meta, nk, eo, co);
+  jy_dev_free(eng, u.epool);
+  jy_dev_free(eng, u.cpool);
+  u.epool = ne;
+  u.cpool = nc;
+  u.epcap = ecap;
+  u.cpcap = ccap;
+  u.pin[0] = te;
+  u.pin[1] = tc;
+  JY_HIP(eng, hipMemcpyAsync(u.ctr, u.pin, 16, hipMemcpyHostToDevice, eng->stream));
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));  // pin is reused right away
+  return JY_OK;
+}
+
 }  // namespace
 
 int32_t jy_ujson_grow(jy_engine* eng, u64 need) {
   UjsonState& u = eng->ujson;
-  if (need <= u.kcap && u.vv) return JY_OK;
   if (u.R == 0) u.R = eng->cfg.ujson_columns;
+  if (!u.ctr) {
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.ctr), 64, "ujson counters"));
+    JY_HIP(eng, hipMemsetAsync(u.ctr, 0, 64, eng->stream));
+    JY_HIP(eng, hipHostMalloc(reinterpret_cast<void**>(&u.pin), 64, hipHostMallocDefault));
+    u.epcap = u.cpcap = std::max<u64>(eng->cfg.entry_capacity[JY_UJSON], 1024);
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.epool), u.epcap * sizeof(URec), "ujson element pool"));
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.cpool), u.cpcap * 8, "ujson cloud pool"));
+  }
+  if (need <= u.kcap && u.vv) return JY_OK;
   u64 nk = std::max<u64>(need, u.kcap ? u.kcap * 2 : need);
   nk = std::max<u64>((nk + 63) & ~63ull, 64);
   void* v = u.vv;
   JY_TRY(jy_realloc(eng, &v, u.kcap * u.R * 8, nk * u.R * 8, true));
   u.vv = static_cast<u64*>(v);
-  for (int b = 0; b < 2; b++) {
-    void* e = u.eoff[b];
-    JY_TRY(jy_realloc(eng, &e, u.kcap ? (u.kcap + 1) * 8 : 0, (nk + 1) * 8, true));
-    u.eoff[b] = static_cast<u64*>(e);
-    void* c = u.coff[b];
-    JY_TRY(jy_realloc(eng, &c, u.kcap ? (u.kcap + 1) * 8 : 0, (nk + 1) * 8, true));
-    u.coff[b] = static_cast<u64*>(c);
-    JY_TRY(ensure_elems(eng, b, 1));
-    JY_TRY(ensure_cloud(eng, b, 1));
-  }
+  void* m = u.meta;
+  JY_TRY(jy_realloc(eng, &m, u.kcap * sizeof(UMeta), nk * sizeof(UMeta), true));  // empty docs
+  u.meta = static_cast<UMeta*>(m);
   u.kcap = nk;
   return JY_OK;
 }
 
-int32_t jy_ujson_extend(jy_engine* eng, u64 from, u64 to) {
-  if (to <= from) return JY_OK;
-  UjsonState& u = eng->ujson;
-  LAUNCH(k_fill_tail, to - from, u.eoff[u.cur], from, to);
-  LAUNCH(k_fill_tail, to - from, u.coff[u.cur], from, to);
-  return JY_OK;
-}
+// new documents are empty: their meta is zeroed when it is allocated
+int32_t jy_ujson_extend(jy_engine*, u64, u64) { return JY_OK; }
 
 int32_t jy_ujson_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* deoff, u64 nel, const u64* ddots,
                        const u64* delems, const u64* dvoff, u64 nvv, const u64* dvv, const u64* dcoff, u64 ncloud,
@@ -591,35 +643,11 @@ int32_t jy_ujson_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* deoff
   const u64 nk = eng->nkeys[JY_UJSON];
   if (nd == 0 || nk == 0) return JY_OK;
   if (nd >= (1ull << kSegBits)) return eng->fail(JY_ERANGE, "ujson converge: more than 2^28 documents in one call");
-  // live sizes of the current buffers: exact when the previous merge's
-  // totals have landed (non-blocking query), else host upper bounds; the
-  // kernels take the exact counts from eoff/coff[nkeys] in HBM, so the host
-  // never waits for the GPU here
-  const double t_enter = jy_tracing() ? jy_now_us() : 0;
-  u64 na = 0, ca = 0;
-  if (u.known) {
-    const hipError_t q = hipEventQuery(eng->total_ready);
-    if (q == hipSuccess) {
-      na = eng->pin_total[1];
-      ca = eng->pin_total[2];
-    } else if (q == hipErrorNotReady) {
-      na = u.nel_bound;
-      ca = u.ncloud_bound;
-    } else {
-      JY_HIP(eng, q);
-    }
-  }
-  const double t_synced = jy_tracing() ? jy_now_us() : 0;
-  if (na + nel + ncloud + 3 >= (1ull << 31) || ca + ncloud + 2 >= (1ull << 31))
-    return eng->fail(JY_ERANGE, "ujson converge: more than 2^31 elements in one shard");
-  const int cur = u.cur, nxt = 1 - cur;
-  JY_TRY(ensure_elems(eng, nxt, na + nel));
-  JY_TRY(ensure_cloud(eng, nxt, ca + ncloud));
   const u32 R = u.R;
 
-  UjArgs A = state_args(eng);
-  A.na = na;
-  A.ca = ca;
+  UjArgs A{};
+  A.R = R;
+  A.vv = u.vv;
   A.nd = nd;
   A.nb = nel;
   A.cb = ncloud;
@@ -638,35 +666,77 @@ int32_t jy_ujson_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* deoff
   A.dptr = static_cast<u32*>(p);
   JY_TRY(jy_scratch(eng, 9, nd * 4 + 16, &p));
   A.bad = static_cast<u32*>(p);
-  u64* totals_dev = reinterpret_cast<u64*>((reinterpret_cast<uintptr_t>(A.bad + nd) + 7) & ~uintptr_t(7));
-  JY_TRY(jy_scratch(eng, 10, nd * R * 24, &p));
+  JY_TRY(jy_scratch(eng, 10, nd * R * 32, &p));
   A.vvm = static_cast<u64*>(p);
   A.vvn = A.vvm + nd * R;
   A.vvd = A.vvn + nd * R;
-  const u64 nf = (na + 1) + (nel + 1) + (ncloud + 1);
+  A.vvs = A.vvd + nd * R;
+  JY_TRY(jy_scratch(eng, 18, (nd + 1) * 48, &p));
+  u64* tb = static_cast<u64*>(p);
+  A.abase = tb;
+  A.asz = tb + (nd + 1);
+  A.ao = tb + 2 * (nd + 1);
+  A.cbs = tb + 3 * (nd + 1);
+  A.csz = tb + 4 * (nd + 1);
+  A.co = tb + 5 * (nd + 1);
+
+  // touched-state sizes and the bump pointers: the one readback of a converge
+  u64 ta = 0, tc = 0, eb0 = 0, cb0 = 0;
+  for (int attempt = 0;; attempt++) {
+    A.meta = u.meta;
+    A.rec = u.epool;
+    A.cloud = u.cpool;
+    JY_HIP(eng, hipMemsetAsync(A.dptr, 0xFF, nk * 4, eng->stream));
+    JY_HIP(eng, hipMemsetAsync(A.bad, 0, nd * 4, eng->stream));
+    LAUNCH(k_uj_prep, nd * R, A);
+    JY_TRY(jy_scan_u64(eng, A.asz, A.ao, nd));
+    JY_TRY(jy_scan_u64(eng, A.csz, A.co, nd));
+    JY_HIP(eng, hipMemcpyAsync(u.pin, A.ao + nd, 8, hipMemcpyDeviceToHost, eng->stream));
+    JY_HIP(eng, hipMemcpyAsync(u.pin + 1, A.co + nd, 8, hipMemcpyDeviceToHost, eng->stream));
+    JY_HIP(eng, hipMemcpyAsync(u.pin + 2, u.ctr, 16, hipMemcpyDeviceToHost, eng->stream));
+    JY_HIP(eng, hipStreamSynchronize(eng->stream));
+    ta = u.pin[0];
+    tc = u.pin[1];
+    eb0 = u.pin[2];
+    cb0 = u.pin[3];
+    if (eb0 + ta + nel <= u.epcap && cb0 + tc + ncloud <= u.cpcap) break;
+    if (attempt == 1) return eng->fail(JY_ENOMEM, "ujson pools: no room after compaction");
+    JY_TRY(ujson_compact(eng, ta + nel, tc + ncloud));  // moves every doc: plan again
+  }
+  if (ta + nel + 3 >= (1ull << 31) || tc + ncloud + 2 >= (1ull << 31))
+    return eng->fail(JY_ERANGE, "ujson converge: more than 2^31 touched elements");
+  A.ta = ta;
+  A.tc = tc;
+
+  const u64 nf = (ta + 1) + (nel + 1) + (ncloud + 1);
   JY_TRY(jy_scratch(eng, 11, nf * 8, &p));
   A.flag_a = static_cast<u32*>(p);
-  A.flag_b = A.flag_a + na + 1;
+  A.flag_b = A.flag_a + ta + 1;
   A.cflag_b = A.flag_b + nel + 1;
   A.scan_a = A.flag_a + nf;
-  A.scan_b = A.scan_a + na + 1;
+  A.scan_b = A.scan_a + ta + 1;
   A.cscan_b = A.scan_b + nel + 1;
-  const u64 nkp = (ca + 1) + (ncloud + 1);
+  const u64 nkp = (tc + 1) + (ncloud + 1);
   JY_TRY(jy_scratch(eng, 14, nkp * 8, &p));
   A.keep_ca = static_cast<u32*>(p);
-  A.keep_cb = A.keep_ca + ca + 1;
+  A.keep_cb = A.keep_ca + tc + 1;
   A.kscan_a = A.keep_ca + nkp;
-  A.kscan_b = A.kscan_a + ca + 1;
-  JY_TRY(jy_scratch(eng, 16, (nk + 1) * 16, &p));
+  A.kscan_b = A.kscan_a + tc + 1;
+  JY_TRY(jy_scratch(eng, 16, (nd + 1) * 32, &p));
   u64* ne = static_cast<u64*>(p);
-  u64* nc = ne + nk + 1;
-  // segment ids of delta elements, cloud dots and vv entries: one buffer
-  const u64 nsg = nel + ncloud + nvv;
+  u64* nc = ne + nd + 1;
+  u64* neo = nc + nd + 1;
+  u64* nco = neo + nd + 1;
+  // segment ids of delta elements, cloud dots, vv entries and the touched
+  // state's elements and cloud dots: one buffer, one scan
+  const u64 nsg = nel + ncloud + nvv + ta + tc;
   JY_TRY(jy_scratch(eng, 17, std::max<u64>(nsg, 1) * 4, &p));
   u32* sg = static_cast<u32*>(p);
   A.dseg = sg;
   A.dcseg = sg + nel;
   A.vseg = sg + nel + ncloud;
+  A.aseg = sg + nel + ncloud + nvv;
+  A.acseg = sg + nel + ncloud + nvv + ta;
 
   auto ranges = [](std::initializer_list<u64> ns) {
     Ranges G{};
@@ -689,58 +759,50 @@ int32_t jy_ujson_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* deoff
   };
 
   if (nsg) {
+    SegSrc S{{deoff, dcoff, dvoff, A.ao, A.co}, {0, nel, nel + ncloud, nel + ncloud + nvv, nel + ncloud + nvv + ta}};
     JY_HIP(eng, hipMemsetAsync(sg, 0, nsg * 4, eng->stream));
-    LAUNCH(k_uj_seg_starts, nd, deoff, dcoff, dvoff, nd, nel, ncloud, sg);
+    LAUNCH(k_uj_seg_starts, nd, S, nd, sg);
     size_t tmp = 0;
     JY_HIP(eng, hipcub::DeviceScan::InclusiveScan(nullptr, tmp, sg, sg, hipcub::Max(), (int)nsg, eng->stream));
     JY_TRY(jy_scratch(eng, 15, tmp, &p));
     JY_HIP(eng, hipcub::DeviceScan::InclusiveScan(p, tmp, sg, sg, hipcub::Max(), (int)nsg, eng->stream));
     LAUNCH(k_uj_seg_strip, nsg, sg, nsg);
   }
-  JY_HIP(eng, hipMemsetAsync(A.dptr, 0xFF, nk * 4, eng->stream));
-  LAUNCH(k_uj_prep, nd * R, A);
   JY_TRY(launch_ranges(k_uj_check, ranges({nvv, nel, ncloud}), A));
   LAUNCH(k_uj_drop_bad, nd * R, A);
-  JY_TRY(launch_ranges(k_uj_flags, ranges({na + 1, nel + 1, ncloud + 1}), A));
+  JY_TRY(launch_ranges(k_uj_flags, ranges({ta + 1, nel + 1, ncloud + 1}), A));
   {
     size_t tmp = 0;
     JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, A.flag_a, A.flag_a + nf, (int)nf, eng->stream));
     JY_TRY(jy_scratch(eng, 15, tmp, &p));
     JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(p, tmp, A.flag_a, A.flag_a + nf, (int)nf, eng->stream));
   }
-  JY_TRY(launch_ranges(k_uj_compact, ranges({ca + 1, ncloud + 1}), A));
+  JY_TRY(launch_ranges(k_uj_compact, ranges({tc + 1, ncloud + 1}), A));
   {
     size_t tmp = 0;
     JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, A.keep_ca, A.keep_ca + nkp, (int)nkp, eng->stream));
     JY_TRY(jy_scratch(eng, 15, tmp, &p));
     JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(p, tmp, A.keep_ca, A.keep_ca + nkp, (int)nkp, eng->stream));
   }
-  LAUNCH(k_uj_sizes_out, nk + 1, A, ne, nc);
-  JY_TRY(jy_scan_u64(eng, ne, u.eoff[nxt], nk));
-  JY_TRY(jy_scan_u64(eng, nc, u.coff[nxt], nk));
-  Out O{u.eoff[nxt], u.coff[nxt], u.rec[nxt], u.eseg[nxt], u.cloud[nxt], u.cseg[nxt], totals_dev};
-  JY_TRY(launch_ranges(k_uj_scatter, ranges({nd * R, na, nel, ca, ncloud}), A, O));
-  JY_HIP(eng, hipMemcpyAsync(eng->pin_total + 1, totals_dev, 16, hipMemcpyDeviceToHost, eng->stream));
-  JY_HIP(eng, hipEventRecord(eng->total_ready, eng->stream));
-  if (jy_tracing()) JY_TRACE("ujson merge host: wait %.1f us, issue %.1f us", t_synced - t_enter, jy_now_us() - t_synced);
-  u.known = true;
-  u.nel_bound = na + nel;
-  u.ncloud_bound = ca + ncloud;
-  u.cur = nxt;
+  LAUNCH(k_uj_sizes_out, nd + 1, A, ne, nc);
+  JY_TRY(jy_scan_u64(eng, ne, neo, nd));
+  JY_TRY(jy_scan_u64(eng, nc, nco, nd));
+  Out O{neo, nco, u.epool, u.cpool, u.meta, eb0, cb0};
+  JY_TRY(launch_ranges(k_uj_scatter, ranges({nd * R, ta, nel, tc, ncloud}), A, O));
+  hipLaunchKernelGGL(k_uj_bump, dim3(1), dim3(1), 0, eng->stream, u.ctr, neo, nco, nd, eb0, cb0);
+  JY_HIP(eng, hipGetLastError());
   return JY_OK;
 }
 
 int32_t jy_ujson_sizes(jy_engine* eng, u64 n, const u32* slots, u64* ne, u64* nc) {
   UjsonState& u = eng->ujson;
-  LAUNCH(k_uj_sizes, n, u.eoff[u.cur], u.coff[u.cur], slots, n, ne, nc);
+  LAUNCH(k_uj_sizes, n, u.meta, slots, n, ne, nc);
   return JY_OK;
 }
 
 int32_t jy_ujson_gather(jy_engine* eng, u64 n, const u32* slots, const u64* oeoff, const u64* ocoff, u64* odots,
                         u64* oelems, u64* ovv, u64* ocloud) {
   UjsonState& u = eng->ujson;
-  const int c = u.cur;
-  LAUNCH(k_uj_gather, n, u.eoff[c], u.rec[c], u.coff[c], u.cloud[c], u.vv, u.R, slots, n, oeoff, ocoff,
-         odots, oelems, ovv, ocloud);
+  LAUNCH(k_uj_gather, n, u.meta, u.epool, u.cpool, u.vv, u.R, slots, n, oeoff, ocoff, odots, oelems, ovv, ocloud);
   return JY_OK;
 }

@@ -113,3 +113,27 @@ def test_synthetic_zipf(oracle_mod, R):
         assert_state_equal(O.UJSON, want.state(), got.state())
     finally:
         eng.close()
+
+
+def test_many_rounds_pool_reuse(oracle_mod):
+    """six Zipf rounds on small pools: only touched documents are rewritten,
+    the pools are compacted several times, state compared after every round"""
+    from jylis_amd import synth as S
+    from jylis_amd.engine import Engine
+    from jylis_amd.repo import RepoUJSON
+    O = oracle_mod
+    eng = Engine(device=0, ujson_columns=8, entry_capacity=1024)
+    try:
+        st, dl = S.ujson_tables(2000, seed=S.BASE_SEED + 50, rounds=6, R=8)
+        want = O.Repo(O.UJSON, 1)
+        got = RepoUJSON(eng)
+        for b in [st] + dl:
+            want.converge(b)
+            got.converge_deltas(b)
+            assert_state_equal(O.UJSON, want.state(), got.state())
+        full = want.state()  # a full-state delta changes nothing
+        want.converge(full)
+        got.converge_deltas(full)
+        assert_state_equal(O.UJSON, want.state(), got.state())
+    finally:
+        eng.close()
