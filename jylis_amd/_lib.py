@@ -7,7 +7,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libjylis_gpu.so")
+# JY_LIB: an alternative build of the same library (kernel A/B experiments)
+LIB_PATH = os.environ.get("JY_LIB") or os.path.join(_HERE, "libjylis_gpu.so")
 
 JY_OK, JY_EINVAL, JY_ENOMEM, JY_EHIP, JY_ERANGE, JY_ETYPE = 0, -1, -2, -3, -4, -5
 JY_NO_SLOT = 0xFFFFFFFF

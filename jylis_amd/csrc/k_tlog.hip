@@ -23,7 +23,7 @@
 // The pool is compacted (every log rewritten back to back) when its free
 // space cannot cover the worst case of the next merge.
 //
-// Per merge, KEY TILES: a workgroup owns 256 consecutive delta keys and
+// Per merge, KEY TILES: a wave owns 64 consecutive delta keys and
 // their delta entries (contiguous), keys staged in LDS, entries walked in
 // coalesced chunks with lanes on consecutive entries:
 //   k_tlog_prep    repeated slots in the batch (both copies skipped)
@@ -56,13 +56,6 @@ constexpr int kThreads = 256;
 constexpr u32 kNone = 0xFFFFFFFFu;
 
 __device__ __forceinline__ u64 gid() { return (u64)blockIdx.x * kThreads + threadIdx.x; }
-
-// > 0 if (ta, pa, la) is NEWER than (tb, pb, lb): later ts, then greater value
-__device__ __forceinline__ int entry_cmp(u64 ta, u64 pa, u64 la, u64 tb, u64 pb, u64 lb,
-                                         const uint8_t* __restrict__ arena) {
-  if (ta != tb) return ta > tb ? 1 : -1;
-  return jy_value_cmp(pa, la, pb, lb, arena);
-}
 
 struct Ent {
   u64 t, p, l;
@@ -168,6 +161,10 @@ __device__ __forceinline__ u32 lds_last_le(const u64* a, u32 n, u64 x) {
 
 // key tiles are one wave: no cross-wave barriers, many tiles in flight per CU
 constexpr int kTile = 64;
+// delta entries per lane per pass of k_tlog_tile (rows of kTile entries; the
+// code is general, 1 measured fastest: 2 and 4 raise VGPRs and cut waves in flight)
+constexpr int kU = 1;
+constexpr int kCU = 1;  // output entries per lane per pass of the rebuild (2: same time)
 typedef hipcub::BlockScan<u32, kTile> BlockScanU32;
 
 constexpr u32 kKept = 0x80000000u;  // eqx: kept flag | # kept entries of the key before this one
@@ -190,7 +187,6 @@ __global__ __launch_bounds__(kTile) void k_tlog_tile(TlogArgs A, TRec* __restric
   __shared__ u64 l_base[kTile], l_newest[kTile], l_cut[kTile];
   __shared__ u32 l_len[kTile], l_cap[kTile], l_drop[kTile], l_M[kTile], l_minrank[kTile],
       l_first[kTile], l_bad[kTile], l_gstart[kTile], l_mode[kTile];
-  __shared__ typename BlockScanU32::TempStorage scan_tmp;
   const u32 tid = threadIdx.x;
   const u64 k0 = (u64)blockIdx.x * kTile;
   const u32 nt = (u32)(A.nd - k0 < kTile ? A.nd - k0 : kTile);
@@ -226,54 +222,111 @@ __global__ __launch_bounds__(kTile) void k_tlog_tile(TlogArgs A, TRec* __restric
   if (blockIdx.x == 0 && tid == 0) A.relsz[A.nd] = 0;
   __syncthreads();
   const u64 E0 = l_eoff[0], E1 = l_eoff[nt];
-  // 2. entries
+  // 2. entries, kU per lane per pass (row u = lanes on consecutive entries):
+  // every load of a pass is issued before any decision, and the binary
+  // searches of the pass advance level by level together
   u32 carry = 0;
-  for (u64 c0 = E0; c0 < E1; c0 += kTile) {
-    const u64 j = c0 + tid;
-    const bool valid = j < E1;
-    u32 idx = 0, flag = 0, rank = 0;
-    if (valid) {
-      idx = lds_last_le(l_eoff, nt - 1, j);
-      const u64 t = A.dts[j];
-      const Ent x{t, A.dpre[j], A.dlr[j]};
-      if (j > l_eoff[idx] && entry_cmp(A.dts[j - 1], A.dpre[j - 1], A.dlr[j - 1], x.t, x.p, x.l, A.arena) <= 0)
-        atomicOr(&l_bad[idx], 2u);
-      const u32 len = l_len[idx], drop = l_drop[idx];
-      if (t >= l_cut[idx]) {
-        if (len == drop || t > l_newest[idx]) {
-          flag = 1;
-          rank = len;
-        } else {
-          const u64 base = l_base[idx];
-          u32 l = drop, h = len;  // first entry of the log not older than x
-          while (l < h) {
-            const u32 m = (l + h) >> 1;
-            if (cmp_at(A.pool, base + m, x, A.arena) < 0) l = m + 1;
-            else h = m;
+  const u64 lanelt = (1ull << tid) - 1;
+  for (u64 c0 = E0; c0 < E1; c0 += (u64)kTile * kU) {
+    u32 idx[kU], flag[kU], rank[kU], lo[kU], hi[kU];
+    u64 t[kU], pp[kU], ll[kU], pt[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const u64 j = c0 + (u64)u * kTile + tid;
+      flag[u] = rank[u] = 0;
+      lo[u] = hi[u] = 0;
+      idx[u] = 0;
+      if (j < E1) {
+        idx[u] = lds_last_le(l_eoff, nt - 1, j);
+        t[u] = A.dts[j];
+        pp[u] = A.dpre[j];
+        ll[u] = A.dlr[j];
+        pt[u] = j > l_eoff[idx[u]] ? A.dts[j - 1] : ~0ull;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const u64 j = c0 + (u64)u * kTile + tid;
+      const u32 i = idx[u];
+      u32 f = 0, r = 0, l = 0, h = 0;
+      if (j < E1) {
+        // strictly newest first; the previous value is read only on a ts tie
+        if (j > l_eoff[i] && (pt[u] < t[u] || (pt[u] == t[u] && jy_value_cmp(A.dpre[j - 1], A.dlr[j - 1], pp[u],
+                                                                             ll[u], A.arena) <= 0)))
+          atomicOr(&l_bad[i], 2u);
+        const u32 len = l_len[i], drop = l_drop[i];
+        if (t[u] >= l_cut[i]) {
+          if (len == drop || t[u] > l_newest[i]) {
+            f = 1;
+            r = len;
+          } else {
+            l = drop;  // search: first entry of the log not older than x
+            h = len;
+            f = 2;     // pending
           }
-          rank = l;
-          flag = !(l < len && cmp_at(A.pool, base + l, x, A.arena) == 0);
         }
       }
+      flag[u] = f;
+      rank[u] = r;
+      lo[u] = l;
+      hi[u] = h;
     }
-    u32 g, agg;
-    BlockScanU32(scan_tmp).ExclusiveSum(flag, g, agg);
-    g += carry;
-    if (valid && j == l_eoff[idx]) l_gstart[idx] = g;
+    // interleaved binary searches: one level of every pending search per round
+    for (;;) {
+      bool any = false;
+      u64 mt[kU];
+#pragma unroll
+      for (int u = 0; u < kU; u++)
+        if (flag[u] == 2 && lo[u] < hi[u]) {
+          mt[u] = A.pool[l_base[idx[u]] + ((lo[u] + hi[u]) >> 1)].ts;
+          any = true;
+        }
+      if (!any) break;
+#pragma unroll
+      for (int u = 0; u < kU; u++)
+        if (flag[u] == 2 && lo[u] < hi[u]) {
+          const u32 m = (lo[u] + hi[u]) >> 1;
+          const Ent x{t[u], pp[u], ll[u]};
+          const int c = mt[u] != x.t ? (mt[u] > x.t ? 1 : -1) : cmp_at(A.pool, l_base[idx[u]] + m, x, A.arena);
+          if (c < 0) lo[u] = m + 1;
+          else hi[u] = m;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++)
+      if (flag[u] == 2) {
+        const Ent x{t[u], pp[u], ll[u]};
+        rank[u] = lo[u];
+        flag[u] = !(lo[u] < l_len[idx[u]] && cmp_at(A.pool, l_base[idx[u]] + lo[u], x, A.arena) == 0);
+      }
+    // kept ranks in entry order: rows in turn (a wave ballot per row)
+    u32 g[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const u64 mask = __ballot(flag[u] != 0);
+      g[u] = carry + (u32)__popcll(mask & lanelt);
+      carry += (u32)__popcll(mask);
+      const u64 j = c0 + (u64)u * kTile + tid;
+      if (j < E1 && j == l_eoff[idx[u]]) l_gstart[idx[u]] = g[u];
+    }
     __syncthreads();
-    if (valid) {
-      const u32 q = g - l_gstart[idx];
-      erank[j] = rank;
-      eqx[j] = q | (flag ? kKept : 0u);
-      if (flag) {
-        atomicAdd(&l_M[idx], 1u);
-        atomicMin(&l_minrank[idx], rank);
-        atomicMin(&l_first[idx], (u32)(j - E0));
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const u64 j = c0 + (u64)u * kTile + tid;
+      if (j >= E1) continue;
+      const u32 i = idx[u];
+      const u32 q = g[u] - l_gstart[i];
+      erank[j] = rank[u];
+      eqx[j] = q | (flag[u] ? kKept : 0u);
+      if (flag[u]) {
+        atomicAdd(&l_M[i], 1u);
+        atomicMin(&l_minrank[i], rank[u]);
+        atomicMin(&l_first[i], (u32)(j - E0));
       }
     }
-    carry += agg;
-    __syncthreads();  // scan_tmp and l_gstart reuse
+    __syncthreads();  // l_gstart reuse
   }
+  (void)lanelt;
   // 3. per key decision
   if (tid < nt) {
     const u64 k = k0 + tid;
@@ -311,7 +364,7 @@ __global__ __launch_bounds__(kTile) void k_tlog_tile(TlogArgs A, TRec* __restric
     A.pinfo[k] = P;
   }
   __syncthreads();
-  // 4. appends (the chunk's entries are L2-hot)
+  // 4. appends: kept entries of append keys go to the tail, oldest first
   for (u64 c0 = E0; c0 < E1; c0 += kTile) {
     const u64 j = c0 + tid;
     if (j >= E1) continue;
@@ -369,35 +422,81 @@ __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __
   if (tid < nt) l_woff[tid] = wo;
   if (tid == 0) l_woff[nt] = wtot;
   __syncthreads();
-  for (u32 c0 = 0; c0 < wtot; c0 += kTile) {
-    const u32 item = c0 + tid;
-    if (item >= wtot) continue;
-    u32 idx = 0, hi = nt - 1;  // last idx with woff <= item and w > 0
-    while (idx < hi) {
-      const u32 m = (idx + hi + 1) >> 1;
-      if (l_woff[m] <= item) idx = m;
-      else hi = m - 1;
-    }
-    const u32 r = item - (u32)l_woff[idx];
-    const u32 surv = l_surv[idx], drop = l_drop[idx], M = l_M[idx];
-    const u64 blo = l_blo[idx], bhi = l_bhi[idx];
-    if (r < surv) {
-      const u32 i = drop + r;
-      u64 l = blo, h = bhi;  // first delta entry with rank <= i
-      while (l < h) {
-        const u64 m = (l + h) >> 1;
-        if (erank[m] <= i) h = m;
-        else l = m + 1;
+  for (u32 c0 = 0; c0 < wtot; c0 += kTile * kCU) {
+    u32 idx[kCU], r[kCU];
+    u64 lo[kCU], hi[kCU];
+    bool st[kCU], live[kCU];
+#pragma unroll
+    for (int u = 0; u < kCU; u++) {
+      const u32 item = c0 + u * kTile + tid;
+      live[u] = item < wtot;
+      st[u] = false;
+      idx[u] = 0;
+      r[u] = 0;
+      lo[u] = hi[u] = 0;
+      if (!live[u]) continue;
+      u32 a = 0, h = nt - 1;  // last idx with woff <= item (a key with items)
+      while (a < h) {
+        const u32 m = (a + h + 1) >> 1;
+        if (l_woff[m] <= item) a = m;
+        else h = m - 1;
       }
-      const u32 c = l < bhi ? M - (eqx[l] & ~kKept) : 0;
-      const TRec x = load_rec(A.pool + l_src[idx] + i);
-      store_rec(pool + l_dst[idx] + r + c, x.ts, x.pre, x.lr);
-    } else {
-      const u64 j = blo + (r - surv);
-      const u32 qx = eqx[j];
-      if (!(qx & kKept)) continue;
-      const u64 pos = (u64)(erank[j] - drop) + (M - 1 - (qx & ~kKept));
-      store_rec(pool + l_dst[idx] + pos, A.dts[j], A.dpre[j], A.dlr[j]);
+      idx[u] = a;
+      r[u] = item - (u32)l_woff[a];
+      st[u] = r[u] < l_surv[a];
+      if (st[u]) {  // first delta entry with rank <= i
+        lo[u] = l_blo[a];
+        hi[u] = l_bhi[a];
+      }
+    }
+    for (;;) {
+      bool any = false;
+      u32 mr[kCU];
+#pragma unroll
+      for (int u = 0; u < kCU; u++)
+        if (st[u] && lo[u] < hi[u]) {
+          mr[u] = erank[(lo[u] + hi[u]) >> 1];
+          any = true;
+        }
+      if (!any) break;
+#pragma unroll
+      for (int u = 0; u < kCU; u++)
+        if (st[u] && lo[u] < hi[u]) {
+          const u64 m = (lo[u] + hi[u]) >> 1;
+          if (mr[u] <= l_drop[idx[u]] + r[u]) hi[u] = m;
+          else lo[u] = m + 1;
+        }
+    }
+    u32 qx[kCU];
+    TRec x[kCU];
+#pragma unroll
+    for (int u = 0; u < kCU; u++) {
+      if (!live[u]) continue;
+      const u32 a = idx[u];
+      if (st[u]) {
+        qx[u] = lo[u] < l_bhi[a] ? eqx[lo[u]] : 0u;
+        x[u] = load_rec(A.pool + l_src[a] + l_drop[a] + r[u]);
+      } else {
+        const u64 j = l_blo[a] + (r[u] - l_surv[a]);
+        qx[u] = eqx[j];
+        x[u].ts = A.dts[j];
+        x[u].pre = A.dpre[j];
+        x[u].lr = A.dlr[j];
+        x[u].pad = erank[j];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kCU; u++) {
+      if (!live[u]) continue;
+      const u32 a = idx[u], M = l_M[a];
+      u64 pos;
+      if (st[u]) {
+        pos = r[u] + (lo[u] < l_bhi[a] ? M - (qx[u] & ~kKept) : 0u);
+      } else {
+        if (!(qx[u] & kKept)) continue;
+        pos = (u64)((u32)x[u].pad - l_drop[a]) + (M - 1 - (qx[u] & ~kKept));
+      }
+      store_rec(pool + l_dst[a] + pos, x[u].ts, x[u].pre, x[u].lr);
     }
   }
 }
