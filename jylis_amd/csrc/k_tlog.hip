@@ -181,12 +181,16 @@ constexpr u32 kKept = 0x80000000u;  // eqx: kept flag | # kept entries of the ke
 //   3. per key: append (every kept entry has rank len, room left) or rebuild
 //   4. per entry: kept entries of append keys go to the tail, oldest first
 // rank/q of every entry go to HBM for the rebuild in k_tlog_commit.
-__global__ __launch_bounds__(kTile) void k_tlog_tile(TlogArgs A, TRec* __restrict__ pool, u32* __restrict__ erank,
+#ifndef JY_TLOG_TILE_ATTR
+// 80 VGPRs: 6 waves per SIMD (81 gave 5; measured 7% faster converges)
+#define JY_TLOG_TILE_ATTR __attribute__((amdgpu_waves_per_eu(6)))
+#endif
+__global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs A, TRec* __restrict__ pool, u32* __restrict__ erank,
                                                         u32* __restrict__ eqx) {
   __shared__ u64 l_eoff[kTile + 1];
-  __shared__ u64 l_base[kTile], l_newest[kTile], l_cut[kTile];
+  __shared__ u64 l_base[kTile], l_newest[kTile], l_cut[kTile], l_tn[kTile];
   __shared__ u32 l_len[kTile], l_cap[kTile], l_drop[kTile], l_M[kTile], l_minrank[kTile],
-      l_first[kTile], l_bad[kTile], l_gstart[kTile], l_mode[kTile];
+      l_bad[kTile], l_gstart[kTile], l_mode[kTile];
   const u32 tid = threadIdx.x;
   const u64 k0 = (u64)blockIdx.x * kTile;
   const u32 nt = (u32)(A.nd - k0 < kTile ? A.nd - k0 : kTile);
@@ -216,7 +220,7 @@ __global__ __launch_bounds__(kTile) void k_tlog_tile(TlogArgs A, TRec* __restric
     l_bad[tid] = A.bad[k];
     l_M[tid] = 0;
     l_minrank[tid] = 0xFFFFFFFFu;
-    l_first[tid] = 0xFFFFFFFFu;
+    l_tn[tid] = 0;
   }
   if (tid == 0) l_eoff[nt] = A.doff[k0 + nt];
   if (blockIdx.x == 0 && tid == 0) A.relsz[A.nd] = 0;
@@ -321,7 +325,7 @@ __global__ __launch_bounds__(kTile) void k_tlog_tile(TlogArgs A, TRec* __restric
       if (flag[u]) {
         atomicAdd(&l_M[i], 1u);
         atomicMin(&l_minrank[i], rank[u]);
-        atomicMin(&l_first[i], (u32)(j - E0));
+        atomicMax((unsigned long long*)&l_tn[i], (unsigned long long)t[u]);  // newest kept
       }
     }
     __syncthreads();  // l_gstart reuse
@@ -341,7 +345,7 @@ __global__ __launch_bounds__(kTile) void k_tlog_tile(TlogArgs A, TRec* __restric
       const u64 newest = l_newest[tid];
       u64 nn = newest;
       if (M > 0) {
-        const u64 tn = A.dts[E0 + l_first[tid]];
+        const u64 tn = l_tn[tid];
         nn = (surv == 0 || tn > newest) ? tn : newest;
       }
       P.src = l_base[tid];
