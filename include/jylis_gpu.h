@@ -133,6 +133,25 @@ int32_t jy_pncount_get(jy_engine* eng, uint64_t n, const uint32_t* slots, int64_
 int32_t jy_counter_export(jy_engine* eng, int32_t type, uint32_t ncols, uint32_t slot0,
                           uint32_t nslots, uint64_t* out);
 
+/* ---- counter write path: the local writes that produce deltas ----
+ * jy_counter_write: n writes of THIS replica, whose column is `col`
+ * (= jy_replica_col(identity)): GCOUNT INC (sign 0, RepoGCOUNT.inc
+ * repo_gcount.pony:57-60), PNCOUNT INC (sign 0) / DEC (sign 1)
+ * (RepoPNCOUNT.inc/dec repo_pncount.pony:59-67; the i64 argument bit-cast to
+ * u64).  s[slot][col] += v (wrapping); each key's pending delta records its
+ * post-write total (GCounter.increment).  Keys may repeat within a batch. */
+int32_t jy_counter_write(jy_engine* eng, int32_t type, int32_t sign, uint32_t col, uint64_t n,
+                         const uint32_t* slot, const uint64_t* val, int32_t mem);
+/* deltas_size() (repo_gcount.pony:16): keys with a pending delta.  Blocks. */
+int32_t jy_counter_deltas_size(jy_engine* eng, int32_t type, uint64_t* n_out);
+/* flush_deltas() (repo_gcount.pony:18-23): every pending key, ascending slot:
+ * slot_out[i]; vals_out[sign * cap + i] = the recorded total (0 where that
+ * sign was not written); mask_out[i] bit s set iff sign s was written.  Clears
+ * the pending set.  *n_out = the count; JY_ERANGE (nothing cleared, *n_out =
+ * the count needed) if cap is smaller.  Blocks. */
+int32_t jy_counter_flush(jy_engine* eng, int32_t type, uint64_t cap, uint32_t* slot_out,
+                         uint64_t* vals_out, uint32_t* mask_out, uint64_t* n_out, int32_t mem);
+
 /* ---- TREG: TRegString.converge (repo_treg.pony:51-52), LWW by (ts, value) ---- */
 int32_t jy_treg_converge(jy_engine* eng, uint64_t n, const uint32_t* slot, const uint64_t* ts,
                          const uint64_t* pre, const uint64_t* lr, int32_t mem);
@@ -140,6 +159,21 @@ int32_t jy_treg_converge(jy_engine* eng, uint64_t n, const uint32_t* slot, const
 int32_t jy_treg_read(jy_engine* eng, uint64_t n, const uint32_t* slots, uint64_t* ts_out,
                      uint64_t* pre_out, uint64_t* lr_out);
 int32_t jy_arena_read(jy_engine* eng, int32_t type, uint64_t offset, uint64_t len, uint8_t* dst);
+
+/* ---- TREG write path: RepoTREG.set (repo_treg.pony:65-68) ----
+ * n local SETs (slot, ts, value handle from jy_values_pack): a SET that wins
+ * against the state (LWW as converge) changes it and is LWW-merged into the
+ * key's pending delta; the key's delta exists even when the SET loses
+ * (_delta_for is evaluated either way).  Host batches may repeat keys (applied
+ * in order); a device batch holds one entry per key. */
+int32_t jy_treg_set(jy_engine* eng, uint64_t n, const uint32_t* slot, const uint64_t* ts,
+                    const uint64_t* pre, const uint64_t* lr, int32_t mem);
+int32_t jy_treg_deltas_size(jy_engine* eng, uint64_t* n_out);  /* deltas_size(); blocks */
+/* flush_deltas() (repo_treg.pony:18-22): every pending key, ascending slot,
+ * with its delta register (ts, pre, lr; a losing-only key reads ("", 0)), then
+ * clears them.  JY_ERANGE (nothing cleared, *n_out = needed) if cap is short. */
+int32_t jy_treg_flush(jy_engine* eng, uint64_t cap, uint32_t* slot_out, uint64_t* ts_out,
+                      uint64_t* pre_out, uint64_t* lr_out, uint64_t* n_out, int32_t mem);
 
 /* ---- TLOG: TLog[String].converge (repo_tlog.pony:66-67) ----
  * nkeys delta logs, CSR: entries of key i are [ent_offs[i], ent_offs[i+1]),

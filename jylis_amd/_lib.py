@@ -64,8 +64,14 @@ SIGNATURES = {
     "jy_pncount_converge_block": (I32, [P, U32, P, U32, U32, P, P, I32]),
     "jy_pncount_get": (I32, [P, U64, P, P, I32]),
     "jy_counter_export": (I32, [P, I32, U32, U32, U32, P]),
+    "jy_counter_write": (I32, [P, I32, I32, U32, U64, P, P, I32]),
+    "jy_counter_deltas_size": (I32, [P, I32, P]),
+    "jy_counter_flush": (I32, [P, I32, U64, P, P, P, P, I32]),
     "jy_treg_converge": (I32, [P, U64, P, P, P, P, I32]),
     "jy_treg_read": (I32, [P, U64, P, P, P, P]),
+    "jy_treg_set": (I32, [P, U64, P, P, P, P, I32]),
+    "jy_treg_deltas_size": (I32, [P, P]),
+    "jy_treg_flush": (I32, [P, U64, P, P, P, P, P, I32]),
     "jy_arena_read": (I32, [P, I32, U64, U64, P]),
     "jy_tlog_converge": (I32, [P, U64, P, P, P, U64, P, P, P, I32]),
     "jy_tlog_read_sizes": (I32, [P, U64, P, P, P]),

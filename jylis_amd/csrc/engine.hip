@@ -215,9 +215,18 @@ void jy_engine_destroy(jy_engine* eng) {
   hipSetDevice(eng->device);
   if (eng->stream) hipStreamSynchronize(eng->stream);
   auto F = [eng](void* p) { jy_dev_free(eng, p); };
-  for (int w = 0; w < 2; w++) F(eng->cnt[w].slab);
+  for (int w = 0; w < 2; w++) {
+    F(eng->cnt[w].slab);
+    F(eng->cnt[w].dflag);
+    F(eng->cnt[w].dval);
+    F(eng->cnt[w].dcount);
+  }
   F(eng->treg.ts);
   F(eng->treg.val);
+  F(eng->treg.dts);
+  F(eng->treg.dval);
+  F(eng->treg.dflag);
+  F(eng->treg.dcount);
   F(eng->tlog.meta);
   F(eng->tlog.pool);
   F(eng->tlog.ctr);
@@ -634,6 +643,68 @@ int32_t jy_counter_export(jy_engine* eng, int32_t type, uint32_t ncols, uint32_t
   return JY_OK;
 }
 
+// ---- counter write path + flush_deltas ----
+int32_t jy_counter_write(jy_engine* eng, int32_t type, int32_t sign, uint32_t col, uint64_t n, const uint32_t* slot,
+                         const uint64_t* val, int32_t mem) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (type != JY_GCOUNT && type != JY_PNCOUNT) return eng->fail(JY_ETYPE, "not a counter type");
+  const int w = type == JY_GCOUNT ? 0 : 1;
+  if (sign < 0 || sign > w) return eng->fail(JY_EINVAL, "sign must be 0 (INC) or, for PNCOUNT, 1 (DEC)");
+  if (col >= eng->rep_id.size()) return eng->fail(JY_ERANGE, "column names no registered replica");
+  if (n == 0) return JY_OK;
+  JY_TRY(slots_check(eng, type, n, slot, mem));
+  JY_TRY(jy_counter_grow(eng, w, (u32)eng->rep_id.size(), eng->nkeys[type]));
+  const void *ds, *dv;
+  JY_TRY(stage_begin(eng));
+  JY_TRY(jy_stage(eng, 0, slot, n * 4, mem, &ds));
+  JY_TRY(jy_stage(eng, 2, val, n * 8, mem, &dv));
+  JY_TRY(stage_end(eng));
+  return jy_cnt_write(eng, w, sign, (u16)col, n, (const u32*)ds, (const u64*)dv);
+}
+
+int32_t jy_counter_deltas_size(jy_engine* eng, int32_t type, uint64_t* n_out) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (type != JY_GCOUNT && type != JY_PNCOUNT) return eng->fail(JY_ETYPE, "not a counter type");
+  return jy_cnt_pending(eng, type == JY_GCOUNT ? 0 : 1, n_out);
+}
+
+int32_t jy_counter_flush(jy_engine* eng, int32_t type, uint64_t cap, uint32_t* slot_out, uint64_t* vals_out,
+                         uint32_t* mask_out, uint64_t* n_out, int32_t mem) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (type != JY_GCOUNT && type != JY_PNCOUNT) return eng->fail(JY_ETYPE, "not a counter type");
+  const int w = type == JY_GCOUNT ? 0 : 1;
+  const u64 nsigns = w + 1;
+  u32 *ds = slot_out, *dm = mask_out;
+  u64* dv = vals_out;
+  u64 pending = 0;
+  JY_TRY(jy_cnt_pending(eng, w, &pending));
+  if (pending > cap) {
+    *n_out = pending;
+    return eng->fail(JY_ERANGE, "flush output capacity is smaller than the pending delta count");
+  }
+  if (mem == JY_HOST && pending) {  // device temporaries sized to the pending count, copied back
+    void *a, *b, *c;
+    JY_TRY(jy_scratch(eng, 8, pending * 4, &a));
+    JY_TRY(jy_scratch(eng, 9, pending * 8 * nsigns, &b));
+    JY_TRY(jy_scratch(eng, 10, pending * 4, &c));
+    ds = static_cast<u32*>(a);
+    dv = static_cast<u64*>(b);
+    dm = static_cast<u32*>(c);
+  }
+  u64 cnt = 0;
+  const u64 dcap = mem == JY_HOST ? pending : cap;
+  JY_TRY(jy_cnt_flush(eng, w, eng->nkeys[type], dcap, ds, dv, dm, &cnt));
+  *n_out = cnt;
+  if (mem == JY_HOST && cnt) {
+    JY_HIP(eng, hipMemcpyAsync(slot_out, ds, cnt * 4, hipMemcpyDeviceToHost, eng->stream));
+    JY_HIP(eng, hipMemcpyAsync(mask_out, dm, cnt * 4, hipMemcpyDeviceToHost, eng->stream));
+    for (u64 g = 0; g < nsigns; g++)
+      JY_HIP(eng, hipMemcpyAsync(vals_out + g * cap, dv + g * dcap, cnt * 8, hipMemcpyDeviceToHost, eng->stream));
+    JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  }
+  return JY_OK;
+}
+
 // ---- TREG ----
 int32_t jy_treg_converge(jy_engine* eng, uint64_t n, const uint32_t* slot, const uint64_t* ts, const uint64_t* pre,
                          const uint64_t* lr, int32_t mem) {
@@ -686,6 +757,93 @@ int32_t jy_treg_converge(jy_engine* eng, uint64_t n, const uint32_t* slot, const
   JY_TRY(jy_stage(eng, 3, lr, n * 8, mem, &dl));
   JY_TRY(stage_end(eng));
   return jy_treg_merge(eng, n, (const u32*)ds, (const u64*)dt, (const u64*)dp, (const u64*)dl);
+}
+
+// local SET batch (RepoTREG.set repo_treg.pony:65-68): pending delta first
+// (against the state as it was), then the state merge.  Host batches that
+// repeat a key run as rounds, in order; a device batch holds one entry per key.
+int32_t jy_treg_set(jy_engine* eng, uint64_t n, const uint32_t* slot, const uint64_t* ts, const uint64_t* pre,
+                    const uint64_t* lr, int32_t mem) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (n == 0) return JY_OK;
+  JY_TRY(slots_check(eng, JY_TREG, n, slot, mem));
+  if (mem == JY_HOST) {
+    std::unordered_map<u32, u32> seen;
+    std::vector<u32> round(n);
+    u32 rounds = 1;
+    for (u64 i = 0; i < n; i++) {
+      round[i] = seen[slot[i]]++;
+      rounds = std::max(rounds, round[i] + 1);
+    }
+    if (rounds > 1) {
+      for (u32 r = 0; r < rounds; r++) {
+        std::vector<u32> s;
+        std::vector<u64> t, p, l;
+        for (u64 i = 0; i < n; i++)
+          if (round[i] == r) {
+            s.push_back(slot[i]);
+            t.push_back(ts[i]);
+            p.push_back(pre[i]);
+            l.push_back(lr[i]);
+          }
+        JY_TRY(jy_treg_set(eng, s.size(), s.data(), t.data(), p.data(), l.data(), JY_HOST));
+      }
+      return JY_OK;
+    }
+    u64 alen = eng->arena[JY_TREG].len;
+    for (u64 i = 0; i < n; i++)
+      if ((lr[i] & JY_LR_LEN_MASK) > 8 && (lr[i] >> JY_LR_LEN_BITS) + (lr[i] & JY_LR_LEN_MASK) > alen)
+        return eng->fail(JY_ERANGE, "value handle outside the arena");
+  }
+  const void *ds, *dt, *dp, *dl;
+  JY_TRY(stage_begin(eng));
+  JY_TRY(jy_stage(eng, 0, slot, n * 4, mem, &ds));
+  JY_TRY(jy_stage(eng, 1, ts, n * 8, mem, &dt));
+  JY_TRY(jy_stage(eng, 2, pre, n * 8, mem, &dp));
+  JY_TRY(jy_stage(eng, 3, lr, n * 8, mem, &dl));
+  JY_TRY(stage_end(eng));
+  JY_TRY(jy_treg_set_pending(eng, n, (const u32*)ds, (const u64*)dt, (const u64*)dp, (const u64*)dl));
+  return jy_treg_merge(eng, n, (const u32*)ds, (const u64*)dt, (const u64*)dp, (const u64*)dl);
+}
+
+int32_t jy_treg_deltas_size(jy_engine* eng, uint64_t* n_out) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  return jy_treg_pending(eng, n_out);
+}
+
+int32_t jy_treg_flush(jy_engine* eng, uint64_t cap, uint32_t* slot_out, uint64_t* ts_out, uint64_t* pre_out,
+                      uint64_t* lr_out, uint64_t* n_out, int32_t mem) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  u64 pending = 0;
+  JY_TRY(jy_treg_pending(eng, &pending));
+  if (pending > cap) {
+    *n_out = pending;
+    return eng->fail(JY_ERANGE, "flush output capacity is smaller than the pending delta count");
+  }
+  u32* ds = slot_out;
+  u64 *dt = ts_out, *dp = pre_out, *dl = lr_out;
+  if (mem == JY_HOST && pending) {
+    void *a, *b, *c, *d;
+    JY_TRY(jy_scratch(eng, 8, pending * 4, &a));
+    JY_TRY(jy_scratch(eng, 9, pending * 8, &b));
+    JY_TRY(jy_scratch(eng, 10, pending * 8, &c));
+    JY_TRY(jy_scratch(eng, 11, pending * 8, &d));
+    ds = static_cast<u32*>(a);
+    dt = static_cast<u64*>(b);
+    dp = static_cast<u64*>(c);
+    dl = static_cast<u64*>(d);
+  }
+  u64 cnt = 0;
+  JY_TRY(jy_treg_flush_dev(eng, eng->nkeys[JY_TREG], mem == JY_HOST ? pending : cap, ds, dt, dp, dl, &cnt));
+  *n_out = cnt;
+  if (mem == JY_HOST && cnt) {
+    JY_HIP(eng, hipMemcpyAsync(slot_out, ds, cnt * 4, hipMemcpyDeviceToHost, eng->stream));
+    JY_HIP(eng, hipMemcpyAsync(ts_out, dt, cnt * 8, hipMemcpyDeviceToHost, eng->stream));
+    JY_HIP(eng, hipMemcpyAsync(pre_out, dp, cnt * 8, hipMemcpyDeviceToHost, eng->stream));
+    JY_HIP(eng, hipMemcpyAsync(lr_out, dl, cnt * 8, hipMemcpyDeviceToHost, eng->stream));
+    JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  }
+  return JY_OK;
 }
 
 int32_t jy_treg_read(jy_engine* eng, uint64_t n, const uint32_t* slots, uint64_t* ts, uint64_t* pre,

@@ -84,6 +84,14 @@ struct CounterState {  // GCOUNT (nsigns 1) / PNCOUNT (nsigns 2): slab [sign][co
   u64* slab = nullptr;
   u32 ccap = 0;  // column capacity
   u64 kcap = 0;  // slot capacity (column pitch, even)
+  // pending local deltas (RepoXXX._deltas, repo_gcount.pony:14): per slot a
+  // flag word (bit s = sign s written since the last flush) and the recorded
+  // post-write totals [sign][dkcap]; dcount = keys with a pending delta
+  u32* dflag = nullptr;
+  u64* dval = nullptr;
+  u64 dkcap = 0;
+  u64* dcount = nullptr;
+  int32_t dcol = -1;  // the writing replica's column while deltas are pending
 };
 
 // TREG value handle of one slot: first 8 value bytes (big-endian) + arena ref
@@ -95,6 +103,14 @@ struct TregState {  // per slot: ts u64 (read by every merge) + TVal (written by
   u64* ts = nullptr;
   TVal* val = nullptr;
   u64 kcap = 0;
+  // pending local deltas (RepoTREG._deltas, repo_treg.pony:14): a TReg per
+  // slot (dts, dval: the LWW max of this replica's winning SETs since the
+  // last flush), a flag per slot and the pending-key count
+  u64* dts = nullptr;
+  TVal* dval = nullptr;
+  u32* dflag = nullptr;
+  u64 dkcap = 0;
+  u64* dcount = nullptr;
 };
 
 // one TLOG entry: 32 B so a lane moves it with two 16-B accesses and an
@@ -282,12 +298,21 @@ int32_t jy_counter_coo(jy_engine* eng, int which, int sign, u64 n, const u32* sl
 int32_t jy_counter_block(jy_engine* eng, int which, u32 ncols, const u16* cols_dev, u32 slot0, u32 nslots,
                          const u64* vals_p, const u64* vals_n);
 int32_t jy_counter_sum(jy_engine* eng, int which, u64 n, const u32* slots_dev, u64* out_dev);
+int32_t jy_cnt_write(jy_engine* eng, int which, int sign, u16 col, u64 n, const u32* slot_dev,
+                         const u64* val_dev);
+int32_t jy_cnt_flush(jy_engine* eng, int which, u64 nkeys, u64 cap, u32* slot_dev, u64* vals_dev,
+                         u32* mask_dev, u64* count_host);
+int32_t jy_cnt_pending(jy_engine* eng, int which, u64* count_host);
 
 int32_t jy_treg_grow(jy_engine* eng, u64 need_slots);
 int32_t jy_treg_merge(jy_engine* eng, u64 n, const u32* slot, const u64* ts, const u64* pre, const u64* lr);
 int32_t jy_treg_gather(jy_engine* eng, u64 n, const u32* slots, u64* ts, u64* pre, u64* lr);
 // routed records (slot, ts, pre, lr) x n, long values rebased by `base`
 int32_t jy_treg_merge_records(jy_engine* eng, const u64* recs, u64 n, u64 base);
+int32_t jy_treg_set_pending(jy_engine* eng, u64 n, const u32* slot, const u64* ts, const u64* pre, const u64* lr);
+int32_t jy_treg_pending(jy_engine* eng, u64* count_host);
+int32_t jy_treg_flush_dev(jy_engine* eng, u64 nkeys, u64 cap, u32* slot_dev, u64* ts_dev, u64* pre_dev, u64* lr_dev,
+                      u64* count_host);
 
 int32_t jy_tlog_grow(jy_engine* eng, u64 need_slots);
 int32_t jy_tlog_extend(jy_engine* eng, u64 from, u64 to);

@@ -17,6 +17,8 @@
 
 #include <algorithm>
 
+#include <hipcub/hipcub.hpp>
+
 #include "jy_internal.hpp"
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
@@ -109,6 +111,51 @@ __global__ __launch_bounds__(kThreads) void k_sum(const u64* __restrict__ slab, 
   out[i] = acc;
 }
 
+// ---- local write path (RepoGCOUNT.inc repo_gcount.pony:57-60, RepoPNCOUNT
+// inc/dec repo_pncount.pony:59-67): s[slot][own] += v, wrapping.  Repeated
+// keys in one batch add atomically (u64 addition mod 2^64 commutes, so the
+// total equals the reference's sequential one).  The first write of a key
+// since the last flush bumps the pending count (deltas_size).
+__global__ __launch_bounds__(kThreads) void k_cnt_add(u64* __restrict__ cell0, u32* __restrict__ dflag, u64* __restrict__ dcount,
+                                                      u32 bit, const u32* __restrict__ slot,
+                                                      const u64* __restrict__ val, u64 n) {
+  const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const u32 s = slot[i];
+  atomicAdd(cell0 + s, val[i]);
+  if (atomicOr(dflag + s, bit) == 0u) atomicAdd(dcount, 1ull);
+}
+
+// the delta records the post-write total (GCounter.increment writes
+// delta[id] = cur).  Within one batch no merge interleaves, so the cell after
+// the whole batch is the total of the key's last write; duplicates store the
+// same value.
+__global__ __launch_bounds__(kThreads) void k_cnt_record(const u64* __restrict__ cell0, u64* __restrict__ dval,
+                                                         u32 nsigns, u32 sign, const u32* __restrict__ slot, u64 n) {
+  const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const u32 s = slot[i];
+  dval[(u64)s * nsigns + sign] = cell0[s];
+}
+
+struct PendingPred {
+  const u32* dflag;
+  __device__ bool operator()(u32 s) const { return dflag[s] != 0; }
+};
+
+// flush_deltas (repo_gcount.pony:18-23): emit every pending key, then clear it
+__global__ __launch_bounds__(kThreads) void k_cnt_flush(u32* __restrict__ dflag, const u64* __restrict__ dval,
+                                                        u32 nsigns, const u32* __restrict__ slots, u64 cnt,
+                                                        u64 cap, u64* __restrict__ vals, u32* __restrict__ mask) {
+  const u64 j = (u64)blockIdx.x * kThreads + threadIdx.x;
+  if (j >= cnt) return;
+  const u32 s = slots[j];
+  const u32 f = dflag[s];
+  mask[j] = f;
+  for (u32 g = 0; g < nsigns; g++) vals[(u64)g * cap + j] = (f >> g) & 1u ? dval[(u64)s * nsigns + g] : 0;
+  dflag[s] = 0;
+}
+
 }  // namespace
 
 int32_t jy_counter_grow(jy_engine* eng, int which, u32 need_cols, u64 need_slots) {
@@ -182,5 +229,78 @@ int32_t jy_counter_sum(jy_engine* eng, int which, u64 n, const u32* slots_dev, u
   hipLaunchKernelGGL(k_sum, dim3((u32)blocks), dim3(kThreads), 0, eng->stream, c.slab, c.kcap,
                      (u64)c.ccap * c.kcap, ncols, (u32)(which + 1), slots_dev, n, out_dev);
   JY_HIP(eng, hipGetLastError());
+  return JY_OK;
+}
+
+// ---- local write path + flush_deltas ----
+static int32_t counter_delta_grow(jy_engine* eng, int which) {
+  CounterState& c = eng->cnt[which];
+  const u32 nsigns = which + 1;
+  if (!c.dcount) {
+    void* p = nullptr;
+    JY_TRY(jy_dev_alloc(eng, &p, 8, "counter pending count"));
+    JY_HIP(eng, hipMemsetAsync(p, 0, 8, eng->stream));
+    c.dcount = static_cast<u64*>(p);
+  }
+  if (c.dkcap >= c.kcap && c.dflag) return JY_OK;
+  void *f = c.dflag, *v = c.dval;
+  JY_TRY(jy_realloc(eng, &f, c.dkcap * 4, c.kcap * 4, true));
+  JY_TRY(jy_realloc(eng, &v, c.dkcap * 8 * nsigns, c.kcap * 8 * nsigns, true));
+  c.dflag = static_cast<u32*>(f);
+  c.dval = static_cast<u64*>(v);
+  c.dkcap = c.kcap;
+  return JY_OK;
+}
+
+int32_t jy_cnt_write(jy_engine* eng, int which, int sign, u16 col, u64 n, const u32* slot, const u64* val) {
+  if (n == 0) return JY_OK;
+  CounterState& c = eng->cnt[which];
+  if (c.dcol >= 0 && c.dcol != col)
+    return eng->fail(JY_EINVAL, "pending deltas were written under another replica column (flush first)");
+  JY_TRY(counter_delta_grow(eng, which));
+  c.dcol = col;
+  JyTimed tm(eng);
+  u64* cell0 = c.slab + (u64)sign * c.ccap * c.kcap + (u64)col * c.kcap;
+  const u32 blocks = (u32)((n + kThreads - 1) / kThreads);
+  hipLaunchKernelGGL(k_cnt_add, dim3(blocks), dim3(kThreads), 0, eng->stream, cell0, c.dflag, c.dcount,
+                     1u << sign, slot, val, n);
+  hipLaunchKernelGGL(k_cnt_record, dim3(blocks), dim3(kThreads), 0, eng->stream, (const u64*)cell0, c.dval,
+                     (u32)(which + 1), (u32)sign, slot, n);
+  JY_HIP(eng, hipGetLastError());
+  return JY_OK;
+}
+
+int32_t jy_cnt_pending(jy_engine* eng, int which, u64* count) {
+  CounterState& c = eng->cnt[which];
+  *count = 0;
+  if (!c.dcount) return JY_OK;
+  JY_HIP(eng, hipMemcpyAsync(eng->pin_total, c.dcount, 8, hipMemcpyDeviceToHost, eng->stream));
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  *count = eng->pin_total[0];
+  return JY_OK;
+}
+
+int32_t jy_cnt_flush(jy_engine* eng, int which, u64 nkeys, u64 cap, u32* slots, u64* vals, u32* mask,
+                         u64* count) {
+  CounterState& c = eng->cnt[which];
+  u64 cnt = 0;
+  JY_TRY(jy_cnt_pending(eng, which, &cnt));
+  *count = cnt;
+  if (cnt == 0) return JY_OK;
+  if (cnt > cap) return eng->fail(JY_ERANGE, "flush output capacity is smaller than the pending delta count");
+  nkeys = std::min<u64>(nkeys, c.dkcap);
+  void *tmp = nullptr, *num = nullptr;
+  size_t tb = 0;
+  hipcub::CountingInputIterator<u32> it(0);
+  PendingPred pred{c.dflag};
+  JY_HIP(eng, hipcub::DeviceSelect::If(nullptr, tb, it, slots, (u32*)nullptr, (int)nkeys, pred, eng->stream));
+  JY_TRY(jy_scratch(eng, 15, tb, &tmp));
+  JY_TRY(jy_scratch(eng, 14, 8, &num));
+  JY_HIP(eng, hipcub::DeviceSelect::If(tmp, tb, it, slots, static_cast<u32*>(num), (int)nkeys, pred, eng->stream));
+  hipLaunchKernelGGL(k_cnt_flush, dim3((u32)((cnt + kThreads - 1) / kThreads)), dim3(kThreads), 0, eng->stream,
+                     c.dflag, (const u64*)c.dval, (u32)(which + 1), (const u32*)slots, cnt, cap, vals, mask);
+  JY_HIP(eng, hipGetLastError());
+  JY_HIP(eng, hipMemsetAsync(c.dcount, 0, 8, eng->stream));
+  c.dcol = -1;
   return JY_OK;
 }

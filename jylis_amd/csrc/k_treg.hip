@@ -23,7 +23,13 @@
 
 #include <algorithm>
 
+#include <hipcub/hipcub.hpp>
+
 #include "jy_internal.hpp"
+
+#ifndef JY_TREG_VARIANT
+#define JY_TREG_VARIANT 0
+#endif
 
 namespace {
 
@@ -31,7 +37,7 @@ constexpr int kThreads = 256;
 // keys per lane; lanes on consecutive keys for every unroll step, so all
 // delta loads and the dependent state-ts gathers of the kUnroll keys are in
 // flight together before any decision
-constexpr int kUnroll = 4;
+constexpr int kUnroll = JY_TREG_VARIANT == 3 ? 8 : 4;
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
@@ -42,6 +48,64 @@ __device__ __forceinline__ bool lww_wins(u64 t, u64 t0, u64 p, u64 l, const TVal
   return jy_value_cmp(p, l, v0.pre, v0.lr, arena) > 0;
 }
 
+#if JY_TREG_VARIANT == 1 || JY_TREG_VARIANT == 2
+// paired lanes: a lane owns two consecutive keys per unroll step, so every
+// delta stream is read with one 16-B (8-B for the slots) load per lane
+#if JY_TREG_VARIANT == 1
+constexpr int kPairs = 2;
+#else
+constexpr int kPairs = 4;
+#endif
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(kThreads) void k_treg_lww(u64* __restrict__ ts, TVal* __restrict__ val,
+                                                       const uint8_t* __restrict__ arena,
+                                                       const u32* __restrict__ slot, const u64* __restrict__ dts,
+                                                       const u64* __restrict__ dpre, const u64* __restrict__ dlr,
+                                                       u64 n) {
+  const u64 base = (u64)blockIdx.x * (kThreads * kPairs) + threadIdx.x;  // pair index
+  u32x2 s[kPairs];
+  u64x2 t[kPairs], p[kPairs], l[kPairs];
+  u64 t0[kPairs][2];
+#pragma unroll
+  for (int u = 0; u < kPairs; u++) {
+    const u64 i = (base + (u64)u * kThreads) * 2;
+    if (i + 1 < n) {
+      s[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(slot + i));
+      t[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(dts + i));
+      p[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(dpre + i));
+      l[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(dlr + i));
+    } else if (i < n) {
+      s[u].x = slot[i];
+      t[u].x = dts[i];
+      p[u].x = dpre[i];
+      l[u].x = dlr[i];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kPairs; u++) {
+    const u64 i = (base + (u64)u * kThreads) * 2;
+    if (i < n) t0[u][0] = ts[s[u].x];
+    if (i + 1 < n) t0[u][1] = ts[s[u].y];
+  }
+#pragma unroll
+  for (int u = 0; u < kPairs; u++) {
+    const u64 i = (base + (u64)u * kThreads) * 2;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      if (i + h >= n) continue;
+      const u32 sh = h ? s[u].y : s[u].x;
+      const u64 th = h ? t[u].y : t[u].x, ph = h ? p[u].y : p[u].x, lh = h ? l[u].y : l[u].x;
+      if (th < t0[u][h]) continue;
+      if (lww_wins(th, t0[u][h], ph, lh, val, sh, arena)) {
+        ts[sh] = th;
+        val[sh] = TVal{ph, lh};
+      }
+    }
+  }
+}
+constexpr int kKeysPerBlock = kThreads * kPairs * 2;
+#else
+constexpr int kKeysPerBlock = kThreads * kUnroll;
 __global__ __launch_bounds__(kThreads) void k_treg_lww(u64* __restrict__ ts, TVal* __restrict__ val,
                                                        const uint8_t* __restrict__ arena,
                                                        const u32* __restrict__ slot, const u64* __restrict__ dts,
@@ -66,13 +130,43 @@ __global__ __launch_bounds__(kThreads) void k_treg_lww(u64* __restrict__ ts, TVa
 #pragma unroll
   for (int u = 0; u < kUnroll; u++) {
     const u64 i = base + (u64)u * kThreads;
-    if (i >= n || t[u] < t0[u]) continue;
+    if (i >= n) continue;
+#if JY_TREG_VARIANT == 4 || JY_TREG_VARIANT == 6
+    // every key rewrites its ts word (losers write back what they read), so
+    // the ts lines leave L2 whole instead of byte-masked
+    const bool w = t[u] >= t0[u] && lww_wins(t[u], t0[u], p[u], l[u], val, s[u], arena);
+#if JY_TREG_VARIANT == 6
+    __builtin_nontemporal_store(w ? t[u] : t0[u], ts + s[u]);
+    if (w) {
+      __builtin_nontemporal_store(p[u], &val[s[u]].pre);
+      __builtin_nontemporal_store(l[u], &val[s[u]].lr);
+    }
+#else
+    ts[s[u]] = w ? t[u] : t0[u];
+    if (w) val[s[u]] = TVal{p[u], l[u]};
+#endif
+#elif JY_TREG_VARIANT == 7
+    // every key rewrites ts and its handle (losers write back what they read)
+    const bool w = t[u] >= t0[u] && lww_wins(t[u], t0[u], p[u], l[u], val, s[u], arena);
+    ts[s[u]] = w ? t[u] : t0[u];
+    const TVal old = w ? TVal{0, 0} : val[s[u]];
+    val[s[u]] = w ? TVal{p[u], l[u]} : old;
+#else
+    if (t[u] < t0[u]) continue;
     if (lww_wins(t[u], t0[u], p[u], l[u], val, s[u], arena)) {
+#if JY_TREG_VARIANT == 5
+      __builtin_nontemporal_store(t[u], ts + s[u]);
+      __builtin_nontemporal_store(p[u], &val[s[u]].pre);
+      __builtin_nontemporal_store(l[u], &val[s[u]].lr);
+#else
       ts[s[u]] = t[u];
       val[s[u]] = TVal{p[u], l[u]};
+#endif
     }
+#endif
   }
 }
+#endif
 
 // receiver side of routing: one 32-B record (slot, ts, pre, lr) per entry,
 // long values rebased onto the arena region this run's bytes went to
@@ -119,6 +213,55 @@ __global__ __launch_bounds__(kThreads) void k_treg_gather(const u64* __restrict_
   olr[i] = v.lr;
 }
 
+// ---- local SET (RepoTREG.set repo_treg.pony:65-68): TReg.update(v, t, delta)
+// changes the state and records the write in the key's pending delta only if
+// it wins against the state; the delta key exists either way
+// (oracle/jy_oracle.cpp or_treg_set).  Run BEFORE the state merge of the same
+// batch (one entry per key): an entry that beats the state as it was is
+// LWW-merged into the pending delta, which equals the reference's sequence.
+__global__ __launch_bounds__(kThreads) void k_treg_set_pending(const u64* __restrict__ ts, const TVal* __restrict__ val,
+                                                               u64* __restrict__ dts, TVal* __restrict__ dval,
+                                                               u32* __restrict__ dflag, u64* __restrict__ dcount,
+                                                               const uint8_t* __restrict__ arena,
+                                                               const u32* __restrict__ slot,
+                                                               const u64* __restrict__ t, const u64* __restrict__ p,
+                                                               const u64* __restrict__ l, u64 n) {
+  const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const u32 s = slot[i];
+  const u64 ti = t[i], pi = p[i], li = l[i];
+  if (atomicOr(dflag + s, 1u) == 0u) atomicAdd(dcount, 1ull);
+  const u64 t0 = ts[s];
+  if (ti < t0 || !lww_wins(ti, t0, pi, li, val, s, arena)) return;
+  const u64 d0 = dts[s];
+  if (ti < d0 || !lww_wins(ti, d0, pi, li, dval, s, arena)) return;
+  dts[s] = ti;
+  dval[s] = TVal{pi, li};
+}
+
+struct TregPendingPred {
+  const u32* dflag;
+  __device__ bool operator()(u32 s) const { return dflag[s] != 0; }
+};
+
+// flush_deltas (repo_treg.pony:18-22): emit each pending key's delta TReg and
+// reset it to the fresh ("", 0)
+__global__ __launch_bounds__(kThreads) void k_treg_flush(u32* __restrict__ dflag, u64* __restrict__ dts,
+                                                         TVal* __restrict__ dval, const u32* __restrict__ slots,
+                                                         u64 cnt, u64* __restrict__ ots, u64* __restrict__ opre,
+                                                         u64* __restrict__ olr) {
+  const u64 j = (u64)blockIdx.x * kThreads + threadIdx.x;
+  if (j >= cnt) return;
+  const u32 s = slots[j];
+  const TVal v = dval[s];
+  ots[j] = dts[s];
+  opre[j] = v.pre;
+  olr[j] = v.lr;
+  dts[s] = 0;
+  dval[s] = TVal{0, 0};
+  dflag[s] = 0;
+}
+
 u32 blocks(u64 n, u64 per) { return (u32)std::max<u64>(1, (n + per - 1) / per); }
 
 }  // namespace
@@ -141,7 +284,7 @@ int32_t jy_treg_merge(jy_engine* eng, u64 n, const u32* slot, const u64* ts, con
   if (n == 0) return JY_OK;
   TregState& t = eng->treg;
   JyTimed tm(eng);
-  hipLaunchKernelGGL(k_treg_lww, dim3(blocks(n, kThreads * kUnroll)), dim3(kThreads), 0, eng->stream, t.ts, t.val,
+  hipLaunchKernelGGL(k_treg_lww, dim3(blocks(n, kKeysPerBlock)), dim3(kThreads), 0, eng->stream, t.ts, t.val,
                      eng->arena[JY_TREG].p, slot, ts, pre, lr, n);
   JY_HIP(eng, hipGetLastError());
   return JY_OK;
@@ -163,5 +306,69 @@ int32_t jy_treg_gather(jy_engine* eng, u64 n, const u32* slots, u64* ots, u64* o
   hipLaunchKernelGGL(k_treg_gather, dim3(blocks(n, kThreads)), dim3(kThreads), 0, eng->stream, t.ts, t.val, slots, n,
                      ots, opre, olr);
   JY_HIP(eng, hipGetLastError());
+  return JY_OK;
+}
+
+static int32_t treg_delta_grow(jy_engine* eng) {
+  TregState& t = eng->treg;
+  if (!t.dcount) {
+    void* p = nullptr;
+    JY_TRY(jy_dev_alloc(eng, &p, 8, "treg pending count"));
+    JY_HIP(eng, hipMemsetAsync(p, 0, 8, eng->stream));
+    t.dcount = static_cast<u64*>(p);
+  }
+  if (t.dkcap >= t.kcap && t.dflag) return JY_OK;
+  void *a = t.dts, *b = t.dval, *f = t.dflag;
+  JY_TRY(jy_realloc(eng, &a, t.dkcap * 8, t.kcap * 8, true));
+  JY_TRY(jy_realloc(eng, &b, t.dkcap * sizeof(TVal), t.kcap * sizeof(TVal), true));
+  JY_TRY(jy_realloc(eng, &f, t.dkcap * 4, t.kcap * 4, true));
+  t.dts = static_cast<u64*>(a);
+  t.dval = static_cast<TVal*>(b);
+  t.dflag = static_cast<u32*>(f);
+  t.dkcap = t.kcap;
+  return JY_OK;
+}
+
+int32_t jy_treg_set_pending(jy_engine* eng, u64 n, const u32* slot, const u64* ts, const u64* pre, const u64* lr) {
+  if (n == 0) return JY_OK;
+  TregState& t = eng->treg;
+  JY_TRY(treg_delta_grow(eng));
+  hipLaunchKernelGGL(k_treg_set_pending, dim3(blocks(n, kThreads)), dim3(kThreads), 0, eng->stream,
+                     (const u64*)t.ts, (const TVal*)t.val, t.dts, t.dval, t.dflag, t.dcount,
+                     eng->arena[JY_TREG].p, slot, ts, pre, lr, n);
+  JY_HIP(eng, hipGetLastError());
+  return JY_OK;
+}
+
+int32_t jy_treg_pending(jy_engine* eng, u64* count) {
+  TregState& t = eng->treg;
+  *count = 0;
+  if (!t.dcount) return JY_OK;
+  JY_HIP(eng, hipMemcpyAsync(eng->pin_total, t.dcount, 8, hipMemcpyDeviceToHost, eng->stream));
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  *count = eng->pin_total[0];
+  return JY_OK;
+}
+
+int32_t jy_treg_flush_dev(jy_engine* eng, u64 nkeys, u64 cap, u32* slots, u64* ots, u64* opre, u64* olr, u64* count) {
+  TregState& t = eng->treg;
+  u64 cnt = 0;
+  JY_TRY(jy_treg_pending(eng, &cnt));
+  *count = cnt;
+  if (cnt == 0) return JY_OK;
+  if (cnt > cap) return eng->fail(JY_ERANGE, "flush output capacity is smaller than the pending delta count");
+  nkeys = std::min<u64>(nkeys, t.dkcap);
+  void *tmp = nullptr, *num = nullptr;
+  size_t tb = 0;
+  hipcub::CountingInputIterator<u32> it(0);
+  TregPendingPred pred{t.dflag};
+  JY_HIP(eng, hipcub::DeviceSelect::If(nullptr, tb, it, slots, (u32*)nullptr, (int)nkeys, pred, eng->stream));
+  JY_TRY(jy_scratch(eng, 15, tb, &tmp));
+  JY_TRY(jy_scratch(eng, 14, 8, &num));
+  JY_HIP(eng, hipcub::DeviceSelect::If(tmp, tb, it, slots, static_cast<u32*>(num), (int)nkeys, pred, eng->stream));
+  hipLaunchKernelGGL(k_treg_flush, dim3(blocks(cnt, kThreads)), dim3(kThreads), 0, eng->stream, t.dflag, t.dts,
+                     t.dval, (const u32*)slots, cnt, ots, opre, olr);
+  JY_HIP(eng, hipGetLastError());
+  JY_HIP(eng, hipMemsetAsync(t.dcount, 0, 8, eng->stream));
   return JY_OK;
 }

@@ -271,6 +271,34 @@ class Engine:
         self._check(self.lib.jy_counter_export(self.h, ctype, ncols, slot0, nslots, out.ctypes.data))
         return out
 
+    # -- counter write path (RepoGCOUNT.inc / RepoPNCOUNT.inc,dec) + flush --
+    def counter_write(self, ctype, sign, col, slot, val):
+        """n local writes under replica column `col`: s[slot][col] += val
+        (wrapping); sign 0 = INC, 1 = DEC (PNCOUNT).  val: uint64 (an i64
+        argument bit-cast, repo_pncount.pony:60,65)"""
+        a, pa, ma = _arg(slot, np.uint32)
+        b, pb, mb = _arg(val if _is_torch(val) else np.asarray(val).astype(np.uint64), np.uint64)
+        mem = _same_mem(ma, mb)
+        self._check(self.lib.jy_counter_write(self.h, ctype, sign, col, len(a), pa, pb, mem))
+
+    def counter_deltas_size(self, ctype):
+        n = C.c_uint64()
+        self._check(self.lib.jy_counter_deltas_size(self.h, ctype, C.byref(n)))
+        return n.value
+
+    def counter_flush(self, ctype):
+        """flush_deltas -> (slots u32[n], vals u64[nsigns][n], mask u32[n])"""
+        nsigns = 1 if ctype == GCOUNT else 2
+        cap = self.counter_deltas_size(ctype)
+        slots = np.zeros(max(cap, 1), np.uint32)
+        vals = np.zeros((nsigns, max(cap, 1)), np.uint64)
+        mask = np.zeros(max(cap, 1), np.uint32)
+        n = C.c_uint64()
+        self._check(self.lib.jy_counter_flush(self.h, ctype, max(cap, 1), slots.ctypes.data, vals.ctypes.data,
+                                              mask.ctypes.data, C.byref(n), HOST))
+        k = n.value
+        return slots[:k].copy(), vals[:, :k].copy(), mask[:k].copy()
+
     # -- TREG --------------------------------------------------------------
     def treg_converge(self, slot, ts, pre, lr):
         a, pa, ma = _arg(slot, np.uint32)
@@ -279,6 +307,31 @@ class Engine:
         d, pd, md = _arg(lr, np.uint64)
         mem = _same_mem(ma, mb, mc, md)
         self._check(self.lib.jy_treg_converge(self.h, len(a), pa, pb, pc, pd, mem))
+
+    def treg_set(self, slot, ts, pre, lr):
+        """local SETs (RepoTREG.set): state LWW + pending delta"""
+        a, pa, ma = _arg(slot, np.uint32)
+        b, pb, mb = _arg(ts, np.uint64)
+        c, pc, mc = _arg(pre, np.uint64)
+        d, pd, md = _arg(lr, np.uint64)
+        mem = _same_mem(ma, mb, mc, md)
+        self._check(self.lib.jy_treg_set(self.h, len(a), pa, pb, pc, pd, mem))
+
+    def treg_deltas_size(self):
+        n = C.c_uint64()
+        self._check(self.lib.jy_treg_deltas_size(self.h, C.byref(n)))
+        return n.value
+
+    def treg_flush(self):
+        """flush_deltas -> (slots, ts, pre, lr) of every pending key"""
+        cap = max(self.treg_deltas_size(), 1)
+        slots = np.zeros(cap, np.uint32)
+        ts, pre, lr = (np.zeros(cap, np.uint64) for _ in range(3))
+        n = C.c_uint64()
+        self._check(self.lib.jy_treg_flush(self.h, cap, slots.ctypes.data, ts.ctypes.data, pre.ctypes.data,
+                                           lr.ctypes.data, C.byref(n), HOST))
+        k = n.value
+        return slots[:k].copy(), ts[:k].copy(), pre[:k].copy(), lr[:k].copy()
 
     def treg_read(self, slots):
         s = np.ascontiguousarray(slots, np.uint32)

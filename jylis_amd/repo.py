@@ -103,6 +103,19 @@ class RepoGCOUNT(_GpuRepo):
         t.update(_counter_table(self.eng, GCOUNT, slots, "", 0))
         return t
 
+    # -- local writes + flush_deltas (on the GPU: jy_counter_write / _flush) --
+    def inc(self, keys, vals, identity):
+        """GCOUNT INC for a batch (repo_gcount.pony:57-60), keys may repeat:
+        s[key][identity] += v (wrapping); the pending delta records the total"""
+        _counter_write(self, keys, vals, identity, 0)
+
+    def deltas_size(self):
+        return self.eng.counter_deltas_size(self.ctype)
+
+    def flush_deltas(self, identity):
+        """flush_deltas (repo_gcount.pony:18-23) -> oracle-format batch table"""
+        return _counter_flush(self, identity, ("",))
+
 
 class RepoPNCOUNT(_GpuRepo):
     """repo_pncount.pony: PNCounter per key (two GCounters)."""
@@ -139,6 +152,42 @@ class RepoPNCOUNT(_GpuRepo):
         t.update(_counter_table(self.eng, PNCOUNT, slots, "p_", 0))
         t.update(_counter_table(self.eng, PNCOUNT, slots, "n_", 1))
         return t
+
+    def inc(self, keys, vals, identity):
+        """PNCOUNT INC (repo_pncount.pony:59-62): i64 values bit-cast to u64"""
+        _counter_write(self, keys, vals, identity, 0)
+
+    def dec(self, keys, vals, identity):
+        """PNCOUNT DEC (repo_pncount.pony:64-67)"""
+        _counter_write(self, keys, vals, identity, 1)
+
+    def deltas_size(self):
+        return self.eng.counter_deltas_size(self.ctype)
+
+    def flush_deltas(self, identity):
+        return _counter_flush(self, identity, ("p_", "n_"))
+
+
+def _counter_write(repo, keys, vals, identity, sign):
+    kb, ko = E.encode_keys(keys)
+    slots = repo._intern({"key_bytes": kb, "key_offs": ko})
+    v = np.asarray(vals)
+    v = v.astype(np.int64).view(np.uint64) if v.dtype.kind == "i" else v.astype(np.uint64)
+    repo.eng.counter_write(repo.ctype, sign, repo.eng.replica_col(identity), slots, v)
+
+
+def _counter_flush(repo, identity, prefixes):
+    slots, vals, mask = repo.eng.counter_flush(repo.ctype)
+    t = repo._keys_table(slots)
+    rid = np.uint64(int(identity) & (2**64 - 1))
+    for g, pre in enumerate(prefixes):
+        has = ((mask >> g) & 1).astype(bool)
+        offs = np.zeros(len(slots) + 1, np.uint64)
+        offs[1:] = np.cumsum(has, dtype=np.uint64)
+        t[pre + "offs"] = offs
+        t[pre + "ids"] = np.full(int(has.sum()), rid, np.uint64)
+        t[pre + "vals"] = vals[g][has]
+    return t
 
 
 def _counter_table(eng, ctype, slots, prefix, sign):
@@ -190,6 +239,25 @@ class RepoTREG(_GpuRepo):
         ts, pre, lr = self.eng.treg_read(slots) if len(slots) else (np.zeros(0, np.uint64),) * 3
         vals = [self.eng.value_bytes(TREG, p, l) for p, l in zip(pre, lr)]
         vb, vo = E.encode_keys(vals)
+        t.update({"ts": ts, "val_bytes": vb, "val_offs": vo})
+        return t
+
+    # -- local writes + flush_deltas (jy_treg_set / _flush) --
+    def set(self, keys, values, ts):
+        """TREG SET for a batch (repo_treg.pony:65-68); keys may repeat (in order)"""
+        kb, ko = E.encode_keys(keys)
+        slots = self._intern({"key_bytes": kb, "key_offs": ko})
+        pre, lr = self.eng.pack_values(TREG, list(values))
+        self.eng.treg_set(slots, np.asarray(ts, np.uint64), pre, lr)
+
+    def deltas_size(self):
+        return self.eng.treg_deltas_size()
+
+    def flush_deltas(self):
+        """flush_deltas (repo_treg.pony:18-22) -> oracle-format batch table"""
+        slots, ts, pre, lr = self.eng.treg_flush()
+        t = self._keys_table(slots)
+        vb, vo = E.encode_keys([self.eng.value_bytes(TREG, p, l) for p, l in zip(pre, lr)])
         t.update({"ts": ts, "val_bytes": vb, "val_offs": vo})
         return t
 

@@ -38,6 +38,19 @@ use @jy_treg_converge[I32](eng: Pointer[None] tag, n: U64, slot: Pointer[U32] ta
   ts: Pointer[U64] tag, pre: Pointer[U64] tag, lr: Pointer[U64] tag, mem: I32)
 use @jy_treg_read[I32](eng: Pointer[None] tag, n: U64, slots: Pointer[U32] tag,
   ts: Pointer[U64] tag, pre: Pointer[U64] tag, lr: Pointer[U64] tag)
+// local writes + flush_deltas (RepoGCOUNT.inc / RepoPNCOUNT.inc,dec /
+// RepoTREG.set and flush_deltas, repo_gcount.pony:18-23,57-60)
+use @jy_counter_write[I32](eng: Pointer[None] tag, ty: I32, sign: I32, col: U32, n: U64,
+  slot: Pointer[U32] tag, value: Pointer[U64] tag, mem: I32)
+use @jy_counter_deltas_size[I32](eng: Pointer[None] tag, ty: I32, n_out: Pointer[U64] tag)
+use @jy_counter_flush[I32](eng: Pointer[None] tag, ty: I32, cap: U64, slot_out: Pointer[U32] tag,
+  vals_out: Pointer[U64] tag, mask_out: Pointer[U32] tag, n_out: Pointer[U64] tag, mem: I32)
+use @jy_treg_set[I32](eng: Pointer[None] tag, n: U64, slot: Pointer[U32] tag,
+  ts: Pointer[U64] tag, pre: Pointer[U64] tag, lr: Pointer[U64] tag, mem: I32)
+use @jy_treg_deltas_size[I32](eng: Pointer[None] tag, n_out: Pointer[U64] tag)
+use @jy_treg_flush[I32](eng: Pointer[None] tag, cap: U64, slot_out: Pointer[U32] tag,
+  ts_out: Pointer[U64] tag, pre_out: Pointer[U64] tag, lr_out: Pointer[U64] tag,
+  n_out: Pointer[U64] tag, mem: I32)
 use @jy_tlog_converge[I32](eng: Pointer[None] tag, n: U64, slot: Pointer[U32] tag,
   cutoff: Pointer[U64] tag, ent_offs: Pointer[U64] tag, nent: U64,
   ts: Pointer[U64] tag, pre: Pointer[U64] tag, lr: Pointer[U64] tag, mem: I32)
