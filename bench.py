@@ -38,6 +38,9 @@ def parse():
     ap.add_argument("--batches", type=int, default=4, help="distinct delta batches held in HBM")
     ap.add_argument("--cpu-keys", type=int, default=65536, help="cpu_baseline sample: keys (x replicas x 2)")
     ap.add_argument("--cpu-rounds", type=int, default=6, help="cpu_baseline sample: peer-batch rounds")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="key-partitioned CPU baseline threads (the GPU box's CPU share); 1 = off")
+    ap.add_argument("--cpu-keys-per-thread", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=None, help="per-launch HBM bytes from a PMC run (json)")
     ap.add_argument("--type", default="pncount", choices=["pncount", "gcount", "treg", "tlog", "ujson"],
@@ -104,6 +107,50 @@ def cpu_baseline(args, seed):
             "sample": f"PNCOUNT {K} keys x {R} replicas x 2 signs x {args.cpu_rounds} rounds of {R} peer batches "
                       f"({cells} cell merges, {dt:.2f} s, oracle/jy_oracle.cpp unordered_map path, 1 thread)",
             "host_cpus": os.cpu_count()}
+
+
+def cpu_baseline_parallel(args, seed):
+    """The stronger CPU baseline of SURVEY 8d: the oracle key-partitioned over
+    `cpu_threads` threads, each converging its own partition's peer batches
+    into its own Repo (one unordered_map per thread, no sharing; the ctypes
+    calls release the GIL).  Same stream shape as cpu_baseline."""
+    import sys
+    import threading
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "oracle"))
+    import oracle as O
+    from jylis_amd import synth as S
+    T, kt, R, rounds = args.cpu_threads, args.cpu_keys_per_thread, args.replicas, 2
+    rids = S.replica_ids(R, seed)
+    repos, batches = [], []
+    for t in range(T):
+        keys = S.counter_keys(kt, prefix=b"c", start=t * kt)
+        st = S.counter_state_np(kt, R, 2, seed + t)
+        repo = O.Repo(O.PNCOUNT, 1)
+        for tab in S.counter_batch_tables(st, rids, keys):
+            repo.converge(tab)
+        mine = []
+        cur = st
+        for r in range(rounds):
+            cur = S.counter_delta_np(cur, r, seed + t)
+            mine += [O.Batch(O.PNCOUNT, tab) for tab in S.counter_batch_tables(cur, rids, keys)]
+        repos.append(repo)
+        batches.append(mine)
+
+    def work(t):
+        for b in batches[t]:
+            repos[t].converge(b)
+
+    threads = [threading.Thread(target=work, args=(t,)) for t in range(T)]
+    t0 = time.perf_counter()
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    dt = time.perf_counter() - t0
+    cells = T * kt * R * 2 * rounds
+    return {"value": cells / dt, "unit": "merges/s", "cores": T, "kind": "port",
+            "sample": f"PNCOUNT {T} key partitions x {kt} keys x {R} replicas x 2 signs x {rounds} rounds of {R} "
+                      f"peer batches ({cells} cell merges, {dt:.2f} s, oracle/jy_oracle.cpp, {T} threads)"}
 
 
 def main():
@@ -222,9 +269,10 @@ def main():
         except Exception:
             traffic = None
 
-    cpu = None
+    cpu = cpu_par = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, seed)
+        cpu_par = cpu_baseline_parallel(args, seed) if args.cpu_threads > 1 else None
 
     if rank == 0:
         line = {
@@ -249,6 +297,7 @@ def main():
                          "kernel": "k_block_max<true>", "kernel_ms_avg": avg_kern_s * 1e3,
                          "bytes_per_cell": BYTES_PER_CELL},
             "cpu_baseline": cpu,
+            "cpu_baseline_parallel": cpu_par,
             "verified": ok,
         }
         print(json.dumps(line), flush=True)

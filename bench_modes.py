@@ -278,7 +278,8 @@ def bench_treg(args, eng, dev, dist, rank, world):
     # 16 state write, the write counted unconditionally); what the kernel
     # actually moves in this layout is reported beside it
     bytes_per_key = 48
-    moved = 4 + 24 + 8 + 24 * wf
+    whole = n * 24 > (256 << 20)  # k_treg_lww<true>: state over the Infinity Cache
+    moved = 4 + 24 + 8 + 8 + (16 if whole else 16 * wf) + (16 * (1 - wf) if whole else 0)
     out = {"workload": f"TREG LWW converge: {G} keys over {world} GPU(s) ({Kper} per GPU), one delta per key "
                        f"per step{' routed by owner (all-to-all)' if routed else ''} (SURVEY 8d config 3)",
            "unit_of_work": "key LWW select", "units_per_step_per_gpu": n,
@@ -290,8 +291,9 @@ def bench_treg(args, eng, dev, dist, rank, world):
                            "kernel": "k_treg_lww", "kernel_ms_avg": k * 1e3, "bytes_per_unit": bytes_per_key,
                            "bytes_note": "SURVEY 8d: 16 delta + 16 state read + 16 state write per key",
                            "bytes_moved_per_unit": moved,
-                           "bytes_moved_note": "4 slot + 24 delta (ts, pre, lr) + 8 state ts + 24 state write x "
-                                               "winner fraction"}
+                           "bytes_moved_note": "4 slot + 24 delta (ts, pre, lr) + 8 state ts read + 8 ts rewritten "
+                                               "+ 16 handle write x winner fraction (a state over the 256 MiB "
+                                               "MALL: every handle written, losers' read)"}
     else:
         out["step_ms_avg_events"] = k * 1e3
     return out

@@ -19,7 +19,9 @@
 // + 16 state write).  What this kernel moves per delta entry: 28 B delta
 // (slot, ts, pre, lr; all coalesced, loaded up front with the state-ts
 // gather -- loading the handle lazily for winners only measured slower at
-// winner fractions >= 0.2) + 8 B state ts, and per winner 24 B state write.
+// winner fractions >= 0.2) + 8 B state ts read + 8 B ts rewritten, and per
+// winner a 16-B handle write (a state over the MALL also rewrites losers'
+// handles, 32 B more per loser: see k_treg_lww).
 
 #include <algorithm>
 
@@ -27,17 +29,14 @@
 
 #include "jy_internal.hpp"
 
-#ifndef JY_TREG_VARIANT
-#define JY_TREG_VARIANT 0
-#endif
-
 namespace {
 
 constexpr int kThreads = 256;
 // keys per lane; lanes on consecutive keys for every unroll step, so all
 // delta loads and the dependent state-ts gathers of the kUnroll keys are in
 // flight together before any decision
-constexpr int kUnroll = JY_TREG_VARIANT == 3 ? 8 : 4;
+constexpr int kUnroll = 4;
+constexpr u64 kMallBytes = 256ull << 20;  // MI355X Infinity Cache (MALL)
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
@@ -48,64 +47,18 @@ __device__ __forceinline__ bool lww_wins(u64 t, u64 t0, u64 p, u64 l, const TVal
   return jy_value_cmp(p, l, v0.pre, v0.lr, arena) > 0;
 }
 
-#if JY_TREG_VARIANT == 1 || JY_TREG_VARIANT == 2
-// paired lanes: a lane owns two consecutive keys per unroll step, so every
-// delta stream is read with one 16-B (8-B for the slots) load per lane
-#if JY_TREG_VARIANT == 1
-constexpr int kPairs = 2;
-#else
-constexpr int kPairs = 4;
-#endif
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-__global__ __launch_bounds__(kThreads) void k_treg_lww(u64* __restrict__ ts, TVal* __restrict__ val,
-                                                       const uint8_t* __restrict__ arena,
-                                                       const u32* __restrict__ slot, const u64* __restrict__ dts,
-                                                       const u64* __restrict__ dpre, const u64* __restrict__ dlr,
-                                                       u64 n) {
-  const u64 base = (u64)blockIdx.x * (kThreads * kPairs) + threadIdx.x;  // pair index
-  u32x2 s[kPairs];
-  u64x2 t[kPairs], p[kPairs], l[kPairs];
-  u64 t0[kPairs][2];
-#pragma unroll
-  for (int u = 0; u < kPairs; u++) {
-    const u64 i = (base + (u64)u * kThreads) * 2;
-    if (i + 1 < n) {
-      s[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(slot + i));
-      t[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(dts + i));
-      p[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(dpre + i));
-      l[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(dlr + i));
-    } else if (i < n) {
-      s[u].x = slot[i];
-      t[u].x = dts[i];
-      p[u].x = dpre[i];
-      l[u].x = dlr[i];
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < kPairs; u++) {
-    const u64 i = (base + (u64)u * kThreads) * 2;
-    if (i < n) t0[u][0] = ts[s[u].x];
-    if (i + 1 < n) t0[u][1] = ts[s[u].y];
-  }
-#pragma unroll
-  for (int u = 0; u < kPairs; u++) {
-    const u64 i = (base + (u64)u * kThreads) * 2;
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      if (i + h >= n) continue;
-      const u32 sh = h ? s[u].y : s[u].x;
-      const u64 th = h ? t[u].y : t[u].x, ph = h ? p[u].y : p[u].x, lh = h ? l[u].y : l[u].x;
-      if (th < t0[u][h]) continue;
-      if (lww_wins(th, t0[u][h], ph, lh, val, sh, arena)) {
-        ts[sh] = th;
-        val[sh] = TVal{ph, lh};
-      }
-    }
-  }
-}
-constexpr int kKeysPerBlock = kThreads * kPairs * 2;
-#else
-constexpr int kKeysPerBlock = kThreads * kUnroll;
+// kRewriteAll = false: every key rewrites its ts word (a loser writes back
+//   the timestamp it read, so ts lines leave L2 whole instead of byte-masked:
+//   no extra bytes), winners write their 16-B handle.
+// kRewriteAll = true: losers also read and rewrite their handle, so every
+//   handle line is written whole.  A byte-masked line that misses the
+//   Infinity Cache costs HBM a read-modify-write; when the state outruns the
+//   256 MiB MALL the explicit rewrite is cheaper (64M keys: 0.84 vs 0.96 ms),
+//   while a cache-resident state prefers the leaner form (8M keys: 84 vs
+//   94 us).  jy_treg_merge picks by state size.
+// Both need one entry per slot per launch (the C ABI's contract; host
+// batches that repeat a key are split into rounds).
+template <bool kRewriteAll>
 __global__ __launch_bounds__(kThreads) void k_treg_lww(u64* __restrict__ ts, TVal* __restrict__ val,
                                                        const uint8_t* __restrict__ arena,
                                                        const u32* __restrict__ slot, const u64* __restrict__ dts,
@@ -131,42 +84,16 @@ __global__ __launch_bounds__(kThreads) void k_treg_lww(u64* __restrict__ ts, TVa
   for (int u = 0; u < kUnroll; u++) {
     const u64 i = base + (u64)u * kThreads;
     if (i >= n) continue;
-#if JY_TREG_VARIANT == 4 || JY_TREG_VARIANT == 6
-    // every key rewrites its ts word (losers write back what they read), so
-    // the ts lines leave L2 whole instead of byte-masked
-    const bool w = t[u] >= t0[u] && lww_wins(t[u], t0[u], p[u], l[u], val, s[u], arena);
-#if JY_TREG_VARIANT == 6
-    __builtin_nontemporal_store(w ? t[u] : t0[u], ts + s[u]);
-    if (w) {
-      __builtin_nontemporal_store(p[u], &val[s[u]].pre);
-      __builtin_nontemporal_store(l[u], &val[s[u]].lr);
-    }
-#else
-    ts[s[u]] = w ? t[u] : t0[u];
-    if (w) val[s[u]] = TVal{p[u], l[u]};
-#endif
-#elif JY_TREG_VARIANT == 7
-    // every key rewrites ts and its handle (losers write back what they read)
     const bool w = t[u] >= t0[u] && lww_wins(t[u], t0[u], p[u], l[u], val, s[u], arena);
     ts[s[u]] = w ? t[u] : t0[u];
-    const TVal old = w ? TVal{0, 0} : val[s[u]];
-    val[s[u]] = w ? TVal{p[u], l[u]} : old;
-#else
-    if (t[u] < t0[u]) continue;
-    if (lww_wins(t[u], t0[u], p[u], l[u], val, s[u], arena)) {
-#if JY_TREG_VARIANT == 5
-      __builtin_nontemporal_store(t[u], ts + s[u]);
-      __builtin_nontemporal_store(p[u], &val[s[u]].pre);
-      __builtin_nontemporal_store(l[u], &val[s[u]].lr);
-#else
-      ts[s[u]] = t[u];
+    if (kRewriteAll) {
+      const TVal old = w ? TVal{0, 0} : val[s[u]];
+      val[s[u]] = w ? TVal{p[u], l[u]} : old;
+    } else if (w) {
       val[s[u]] = TVal{p[u], l[u]};
-#endif
     }
-#endif
   }
 }
-#endif
 
 // receiver side of routing: one 32-B record (slot, ts, pre, lr) per entry,
 // long values rebased onto the arena region this run's bytes went to
@@ -284,8 +211,14 @@ int32_t jy_treg_merge(jy_engine* eng, u64 n, const u32* slot, const u64* ts, con
   if (n == 0) return JY_OK;
   TregState& t = eng->treg;
   JyTimed tm(eng);
-  hipLaunchKernelGGL(k_treg_lww, dim3(blocks(n, kKeysPerBlock)), dim3(kThreads), 0, eng->stream, t.ts, t.val,
-                     eng->arena[JY_TREG].p, slot, ts, pre, lr, n);
+  // state larger than the Infinity Cache: write whole lines (see k_treg_lww)
+  const bool whole = t.kcap * (8 + sizeof(TVal)) > kMallBytes;
+  if (whole)
+    hipLaunchKernelGGL(k_treg_lww<true>, dim3(blocks(n, kThreads * kUnroll)), dim3(kThreads), 0, eng->stream, t.ts,
+                       t.val, eng->arena[JY_TREG].p, slot, ts, pre, lr, n);
+  else
+    hipLaunchKernelGGL(k_treg_lww<false>, dim3(blocks(n, kThreads * kUnroll)), dim3(kThreads), 0, eng->stream,
+                       t.ts, t.val, eng->arena[JY_TREG].p, slot, ts, pre, lr, n);
   JY_HIP(eng, hipGetLastError());
   return JY_OK;
 }
