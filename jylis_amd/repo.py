@@ -32,7 +32,9 @@ class _GpuRepo:
 
     def __init__(self, eng):
         self.eng = eng
-        self.names = []  # slot -> key bytes (the engine interns; the host keeps names for reads)
+        # slot -> key bytes (the engine interns; the host keeps names for reads),
+        # one list per engine and type: every repo over the engine shares its slots
+        self.names = eng.__dict__.setdefault("_slot_names", {}).setdefault(self.ctype, [])
 
     def _intern(self, table):
         kb, ko = _keys_of(table)
