@@ -219,7 +219,7 @@ void jy_keys_owner(uint64_t n, const uint8_t* key_bytes, const uint64_t* key_off
 /* records / value bytes per destination (host out, nshards each) */
 int32_t jy_treg_route_count(jy_engine* eng, uint64_t n, const uint32_t* owner, const uint64_t* lr,
                             uint32_t nshards, int32_t mem, uint64_t* rec_counts, uint64_t* byte_counts);
-/* scatter into caller-provided device buffers (records u64[n][4], bytes) laid
+/* scatter into caller-provided device buffers (records u64[n][4], 16-B aligned; bytes) laid
  * out destination by destination in the order of the counts */
 int32_t jy_treg_route_scatter(jy_engine* eng, uint64_t n, const uint32_t* owner, const uint32_t* slot,
                               const uint64_t* ts, const uint64_t* pre, const uint64_t* lr, uint32_t nshards,

@@ -22,20 +22,74 @@
 namespace {
 
 constexpr int kThreads = 256;
+constexpr int kPer = 8;  // entries per lane: one tile of 2048 entries per workgroup
+constexpr u64 kTile = (u64)kThreads * kPer;
 constexpr u32 kMaxShards = 64;
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
+// Per-owner counts without same-address atomics per lane: a wave walks the
+// distinct owners among its lanes (one ballot each), and its leader adds the
+// wave's count and long-value bytes to the workgroup's LDS counters once.
+// `rank`/`brank` (scatter only) receive each lane's position inside the
+// workgroup's run for its owner.  All lanes of the wave call this together.
+template <bool kRanks>
+__device__ __forceinline__ void wave_aggregate(bool valid, u32 o, u32 blen, unsigned long long* lrec,
+                                               unsigned long long* lbyte, u64* rank, u64* brank) {
+  const int lane = __lane_id();
+  const u64 lt = (1ull << lane) - 1;
+  u64 pending = __ballot(valid);
+  while (pending) {
+    const int leader = __ffsll((unsigned long long)pending) - 1;
+    const u32 d = __shfl(o, leader);
+    const bool mine = valid && o == d;
+    const u64 m = __ballot(mine);
+    // inclusive scan of the long-value bytes of this owner's lanes (a value
+    // is < 2^24 bytes, so a wave's sum fits 32 bits); skipped when none is long
+    u32 x = mine ? blen : 0;
+    u32 bsum = 0;
+    if (__ballot(x != 0)) {
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const u32 y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+      }
+      bsum = __shfl(x, 63);
+    }
+    unsigned long long rb = 0, bb = 0;
+    if (lane == leader) {
+      rb = atomicAdd(&lrec[d], (unsigned long long)__popcll(m));
+      if (bsum) bb = atomicAdd(&lbyte[d], (unsigned long long)bsum);
+    }
+    if (kRanks) {
+      rb = __shfl(rb, leader);
+      bb = __shfl(bb, leader);
+      if (mine) {
+        *rank = rb + __popcll(m & lt);
+        *brank = bb + x - blen;
+      }
+    }
+    pending &= ~m;
+  }
+}
 
 __global__ __launch_bounds__(kThreads) void k_route_count(const u32* __restrict__ owner, const u64* __restrict__ lr,
                                                           u64 n, u32 S, unsigned long long* __restrict__ counts) {
   __shared__ unsigned long long lrec[kMaxShards], lbyte[kMaxShards];
   for (u32 i = threadIdx.x; i < S; i += kThreads) lrec[i] = lbyte[i] = 0;
   __syncthreads();
-  const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
-  if (i < n) {
-    const u32 o = owner[i];
-    const u64 len = lr[i] & JY_LR_LEN_MASK;
-    atomicAdd(&lrec[o], 1ull);
-    if (len > 8) atomicAdd(&lbyte[o], (unsigned long long)len);
+  const u64 base = (u64)blockIdx.x * kTile + threadIdx.x;
+  u32 o[kPer];
+  u64 len[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {  // every load in flight before the first ballot
+    const u64 i = base + (u64)u * kThreads;
+    o[u] = i < n ? owner[i] : 0;
+    len[u] = i < n ? (lr[i] & JY_LR_LEN_MASK) : 0;
   }
+#pragma unroll
+  for (int u = 0; u < kPer; u++)
+    wave_aggregate<false>(base + (u64)u * kThreads < n, o[u], len[u] > 8 ? (u32)len[u] : 0u, lrec, lbyte, nullptr,
+                          nullptr);
   __syncthreads();
   for (u32 d = threadIdx.x; d < S; d += kThreads) {
     if (lrec[d]) atomicAdd(&counts[d], lrec[d]);
@@ -53,39 +107,52 @@ __global__ __launch_bounds__(kThreads) void k_route_scatter_treg(
   __shared__ unsigned long long lrec[kMaxShards], lbyte[kMaxShards], grec[kMaxShards], gbyte[kMaxShards];
   for (u32 d = threadIdx.x; d < S; d += kThreads) lrec[d] = lbyte[d] = 0;
   __syncthreads();
-  const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
-  u32 o = 0;
-  u64 len = 0, my_rec = 0, my_byte = 0, l = 0;
-  if (i < n) {
-    o = owner[i];
-    l = lr[i];
-    len = l & JY_LR_LEN_MASK;
-    my_rec = atomicAdd(&lrec[o], 1ull);
-    if (len > 8) my_byte = atomicAdd(&lbyte[o], (unsigned long long)len);
+  const u64 base = (u64)blockIdx.x * kTile + threadIdx.x;
+  u32 o[kPer], sl[kPer];
+  u64 l[kPer], t[kPer], p[kPer], rk[kPer], brk[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {  // every load in flight before the first ballot
+    const u64 i = base + (u64)u * kThreads;
+    const bool valid = i < n;
+    o[u] = valid ? owner[i] : 0;
+    l[u] = valid ? lr[i] : 0;
+    sl[u] = valid ? slot[i] : 0;
+    t[u] = valid ? ts[i] : 0;
+    p[u] = valid ? pre[i] : 0;
+  }
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {
+    const u64 len = l[u] & JY_LR_LEN_MASK;
+    rk[u] = brk[u] = 0;
+    wave_aggregate<true>(base + (u64)u * kThreads < n, o[u], len > 8 ? (u32)len : 0u, lrec, lbyte, &rk[u], &brk[u]);
   }
   __syncthreads();
+  // one global reservation per (workgroup, owner)
   for (u32 d = threadIdx.x; d < S; d += kThreads) {
     grec[d] = lrec[d] ? atomicAdd(&cursors[d], lrec[d]) : 0;
     gbyte[d] = lbyte[d] ? atomicAdd(&cursors[S + d], lbyte[d]) : 0;
   }
   __syncthreads();
-  if (i >= n) return;
-  const u64 pos = grec[o] + my_rec;
-  u64 out_lr = l;
-  if (len > 8) {
-    const u64 bpos = gbyte[o] + my_byte;
-    const uint8_t* src = arena + (l >> JY_LR_LEN_BITS);
-    for (u64 j = 0; j < len; j++) bytes[bpos + j] = src[j];
-    out_lr = ((bpos - byte_base[o]) << JY_LR_LEN_BITS) | len;
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {
+    const u64 i = base + (u64)u * kThreads;
+    if (i >= n) continue;
+    const u64 pos = grec[o[u]] + rk[u];
+    const u64 len = l[u] & JY_LR_LEN_MASK;
+    u64 out_lr = l[u];
+    if (len > 8) {
+      const u64 bpos = gbyte[o[u]] + brk[u];
+      const uint8_t* src = arena + (l[u] >> JY_LR_LEN_BITS);
+      for (u64 j = 0; j < len; j++) bytes[bpos + j] = src[j];
+      out_lr = ((bpos - byte_base[o[u]]) << JY_LR_LEN_BITS) | len;
+    }
+    u64x2* r = reinterpret_cast<u64x2*>(recs + pos * 4);  // 32-B records, two 16-B stores
+    r[0] = u64x2{(u64)sl[u], t[u]};
+    r[1] = u64x2{p[u], out_lr};
   }
-  u64* r = recs + pos * 4;
-  r[0] = slot[i];
-  r[1] = ts[i];
-  r[2] = pre[i];
-  r[3] = out_lr;
 }
 
-u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kThreads - 1) / kThreads); }
+u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kTile - 1) / kTile); }
 
 }  // namespace
 
@@ -140,6 +207,7 @@ int32_t jy_treg_route_scatter(jy_engine* eng, uint64_t n, const uint32_t* owner,
     b += byte_counts[d];
   }
   if (r != n) return eng->fail(JY_EINVAL, "record counts do not add up to n");
+  if (reinterpret_cast<uintptr_t>(recs_dev) % 16) return eng->fail(JY_EINVAL, "recs_dev must be 16-B aligned");
   const void *dow, *dsl, *dts, *dpre, *dlr, *dinit, *dbb;
   JY_TRY(jy_stage_begin(eng));
   JY_TRY(jy_stage(eng, 0, owner, n * 4, mem, &dow));
