@@ -59,6 +59,7 @@ namespace {
 constexpr int kThreads = 256;
 constexpr u32 kNone = 0xFFFFFFFFu;
 constexpr u32 kSegBits = 28;  // seg-id encoding (range << 28 | doc)
+constexpr u32 kSegMask = (1u << kSegBits) - 1;  // readers strip the range bits
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
@@ -187,31 +188,32 @@ __global__ __launch_bounds__(kThreads) void k_uj_prep(UjArgs A) {
   const u64 k = t / A.R;
   const u32 c = (u32)(t - k * A.R);
   const u64 s = A.slot[k];
+  // the vv row and the meta are loaded before the claim's atomic round trip
+  const u64 v = A.vv[s * A.R + c];
+  A.vvs[t] = v;  // k_uj_scatter overwrites vv while it still tests the state context
+  A.vvm[t] = v;
+  A.vvd[t] = 0;
   if (c == 0) {
-    const u32 prev = atomicCAS(A.dptr + s, kNone, (u32)k);
-    if (prev != kNone) {  // one delta per doc per call: both copies are skipped
-      A.bad[k] = 1;
-      A.bad[prev] = 1;
-    }
     const UMeta m = A.meta[s];
     A.abase[k] = m.ebase;
     A.asz[k] = m.elen;
     A.cbs[k] = m.cbase;
     A.csz[k] = m.clen;
+    const u32 prev = atomicCAS(A.dptr + s, kNone, (u32)k);
+    if (prev != kNone) {  // one delta per doc per call: both copies are skipped
+      A.bad[k] = 1;
+      A.bad[prev] = 1;
+    }
   }
   if (t == 0) {
     A.asz[A.nd] = 0;
     A.csz[A.nd] = 0;
   }
-  const u64 v = A.vv[s * A.R + c];
-  A.vvs[t] = v;  // k_uj_scatter overwrites vv while it still tests the state context
-  A.vvm[t] = v;
-  A.vvd[t] = 0;
 }
 
 // ---- P1: delta vv scattered dense + validation of vv / dots / cloud ---------------
 __device__ __forceinline__ void vv_delta(const UjArgs& A, u64 j) {
-  const u32 k = A.vseg[j];
+  const u32 k = A.vseg[j] & kSegMask;
   const u64 x = A.dvv[j];
   const u32 c = dcol(x);
   if (c >= A.R || (j > A.dvoff[k] && dcol(A.dvv[j - 1]) >= c)) {
@@ -222,7 +224,7 @@ __device__ __forceinline__ void vv_delta(const UjArgs& A, u64 j) {
 }
 // strictly ascending, col < R, seq >= 1
 __device__ __forceinline__ void validate(const UjArgs& A, const u32* seg, const u64* offs, const u64* a, u64 j) {
-  const u32 k = seg[j];
+  const u32 k = seg[j] & kSegMask;
   const u64 x = a[j];
   bool ok = dcol(x) < A.R && dseq(x) >= 1;
   if (j > offs[k] && a[j - 1] >= x) ok = false;
@@ -255,7 +257,7 @@ __device__ __forceinline__ void flag_a(const UjArgs& A, u64 i) {
     A.flag_a[i] = 0;
     return;
   }
-  const u32 k = A.aseg[i];
+  const u32 k = A.aseg[i] & kSegMask;
   u32 keep = 0;
   if (!A.bad[k]) {
     const u64 d = A.rec[A.abase[k] + (i - A.ao[k])].dot;
@@ -268,7 +270,7 @@ __device__ __forceinline__ void flag_b(const UjArgs& A, u64 j) {
     A.flag_b[j] = 0;
     return;
   }
-  const u32 k = A.dseg[j];
+  const u32 k = A.dseg[j] & kSegMask;
   u32 keep = 0;
   if (!A.bad[k]) {
     const u64 d = A.ddots[j];
@@ -284,7 +286,7 @@ __device__ __forceinline__ void cloud_dedupe(const UjArgs& A, u64 j) {
     A.cflag_b[j] = 0;
     return;
   }
-  const u32 k = A.dcseg[j];
+  const u32 k = A.dcseg[j] & kSegMask;
   u32 f = 0;
   if (!A.bad[k]) f = !contains(A.cloud, A.cbs[k], A.cbs[k] + A.csz[k], A.dcloud[j]);
   A.cflag_b[j] = f;
@@ -306,7 +308,7 @@ __device__ __forceinline__ void compact_a(const UjArgs& A, u64 i) {
     A.keep_ca[i] = 0;
     return;
   }
-  const u32 k = A.acseg[i];
+  const u32 k = A.acseg[i] & kSegMask;
   if (A.bad[k]) {
     A.keep_ca[i] = 0;
     return;
@@ -339,7 +341,7 @@ __device__ __forceinline__ void compact_b(const UjArgs& A, u64 j) {
   }
   u32 keep = 0;
   if (A.cflag_b[j]) {  // (0 for malformed docs)
-    const u32 k = A.dcseg[j];
+    const u32 k = A.dcseg[j] & kSegMask;
     const u64 x = A.dcloud[j];
     const u32 c = dcol(x);
     const u64 q = dseq(x), v = A.vvm[(u64)k * A.R + c];
@@ -392,7 +394,7 @@ struct Out {
 
 __device__ __forceinline__ void scatter_a(const UjArgs& A, const Out& O, u64 i) {
   if (!A.flag_a[i]) return;
-  const u32 k = A.aseg[i];
+  const u32 k = A.aseg[i] & kSegMask;
   const URec x = load_rec(A.rec + A.abase[k] + (i - A.ao[k]));
   u64 e = x.elem;
   u64 pos = O.neo[k] + (A.scan_a[i] - A.scan_a[A.ao[k]]);
@@ -404,7 +406,7 @@ __device__ __forceinline__ void scatter_a(const UjArgs& A, const Out& O, u64 i) 
 }
 __device__ __forceinline__ void scatter_b(const UjArgs& A, const Out& O, u64 j) {
   if (!A.flag_b[j]) return;
-  const u32 k = A.dseg[j];
+  const u32 k = A.dseg[j] & kSegMask;
   const u64 d = A.ddots[j];
   const u64 lo = A.abase[k];
   const u64 pa = A.ao[k] + (lower_bound_rec(A.rec, lo, lo + A.asz[k], d) - lo);
@@ -413,7 +415,7 @@ __device__ __forceinline__ void scatter_b(const UjArgs& A, const Out& O, u64 j) 
 }
 __device__ __forceinline__ void cscatter_a(const UjArgs& A, const Out& O, u64 i) {
   if (!A.keep_ca[i]) return;
-  const u32 k = A.acseg[i];
+  const u32 k = A.acseg[i] & kSegMask;
   const u64 x = A.cloud[A.cbs[k] + (i - A.co[k])];
   const u64 lo = A.dcoff[k];
   const u64 pos = O.nco[k] + (A.kscan_a[i] - A.kscan_a[A.co[k]]) +
@@ -422,7 +424,7 @@ __device__ __forceinline__ void cscatter_a(const UjArgs& A, const Out& O, u64 i)
 }
 __device__ __forceinline__ void cscatter_b(const UjArgs& A, const Out& O, u64 j) {
   if (!A.keep_cb[j]) return;
-  const u32 k = A.dcseg[j];
+  const u32 k = A.dcseg[j] & kSegMask;
   const u64 x = A.dcloud[j];
   const u64 lo = A.cbs[k];
   const u64 pa = A.co[k] + (lower_bound(A.cloud, lo, lo + A.csz[k], x) - lo);
@@ -474,10 +476,6 @@ __global__ __launch_bounds__(kThreads) void k_uj_seg_starts(SegSrc S, u64 nseg, 
 #pragma unroll
   for (u32 r = 0; r < 5; r++)
     if (S.o[r][k] < S.o[r][k + 1]) out[S.base[r] + S.o[r][k]] = (r << kSegBits) | (u32)k;
-}
-__global__ __launch_bounds__(kThreads) void k_uj_seg_strip(u32* __restrict__ a, u64 n) {
-  const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
-  if (i < n) a[i] &= (1u << kSegBits) - 1;
 }
 
 // ---- compaction: every document rewritten back to back into fresh pools ------------
@@ -766,7 +764,6 @@ int32_t jy_ujson_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* deoff
     JY_HIP(eng, hipcub::DeviceScan::InclusiveScan(nullptr, tmp, sg, sg, hipcub::Max(), (int)nsg, eng->stream));
     JY_TRY(jy_scratch(eng, 15, tmp, &p));
     JY_HIP(eng, hipcub::DeviceScan::InclusiveScan(p, tmp, sg, sg, hipcub::Max(), (int)nsg, eng->stream));
-    LAUNCH(k_uj_seg_strip, nsg, sg, nsg);
   }
   JY_TRY(launch_ranges(k_uj_check, ranges({nvv, nel, ncloud}), A));
   LAUNCH(k_uj_drop_bad, nd * R, A);
