@@ -478,6 +478,56 @@ __global__ __launch_bounds__(kThreads) void k_uj_seg_starts(SegSrc S, u64 nseg, 
     if (S.o[r][k] < S.o[r][k + 1]) out[S.base[r] + S.o[r][k]] = (r << kSegBits) | (u32)k;
 }
 
+// The max-scan that carries the marks on, one 4096-item tile per workgroup
+// with no inter-tile pass: a tile's carry-in is the segment of its first
+// item, found by one binary search over that range's offsets (the last
+// document whose segment starts at or before it), so every tile scans alone.
+constexpr int kFillPer = 16;
+constexpr u64 kFillTile = (u64)kThreads * kFillPer;
+__global__ __launch_bounds__(kThreads) void k_uj_seg_fill(SegSrc S, u64 nseg, u32* __restrict__ a, u64 n) {
+  typedef hipcub::BlockScan<u32, kThreads> Scan;
+  typedef hipcub::BlockLoad<u32, kThreads, kFillPer, hipcub::BLOCK_LOAD_WARP_TRANSPOSE> Load;
+  typedef hipcub::BlockStore<u32, kThreads, kFillPer, hipcub::BLOCK_STORE_WARP_TRANSPOSE> Store;
+  __shared__ union {
+    typename Scan::TempStorage scan;
+    typename Load::TempStorage load;
+    typename Store::TempStorage store;
+  } tmp;
+  __shared__ u32 carry;
+  const u64 t0 = (u64)blockIdx.x * kFillTile;
+  if (threadIdx.x < 64) {
+    // 64-ary search by the first wave: each round every lane tests one
+    // candidate and a ballot keeps the last one that passes (3 dependent
+    // loads for 2^18 documents instead of 18)
+    u32 r = 4;
+    while (r > 0 && S.base[r] > t0) r--;
+    const u64 local = t0 - S.base[r];
+    const u64* o = S.o[r];
+    const u32 lane = threadIdx.x;
+    u64 lo = 0, hi = nseg;  // the last doc k with o[k] <= local lies in [lo, hi]
+    while (lo < hi) {
+      const u64 step = (hi - lo + 63) / 64;
+      const u64 c = lo + (u64)(lane + 1) * step;
+      const u64 pass = __ballot(c <= hi && o[c] <= local);  // a prefix of the lanes
+      const u64 nlo = lo + (u64)__popcll(pass) * step;
+      hi = nlo + step - 1 < hi ? nlo + step - 1 : hi;
+      lo = nlo;
+    }
+    if (lane == 0) carry = (r << kSegBits) | (u32)lo;
+  }
+  // coalesced tile load, transposed through LDS into a blocked arrangement
+  u32 v[kFillPer];
+  const int valid = (int)(n - t0 < kFillTile ? n - t0 : kFillTile);
+  Load(tmp.load).Load(a + t0, v, valid, 0u);
+  __syncthreads();
+  Scan(tmp.scan).InclusiveScan(v, v, hipcub::Max());
+  __syncthreads();
+  const u32 c = carry;
+#pragma unroll
+  for (int u = 0; u < kFillPer; u++) v[u] = v[u] > c ? v[u] : c;
+  Store(tmp.store).Store(a + t0, v, valid);
+}
+
 // ---- compaction: every document rewritten back to back into fresh pools ------------
 __global__ __launch_bounds__(kThreads) void k_uj_cmp_size(const UMeta* __restrict__ meta, u64 nk,
                                                           u64* __restrict__ se, u64* __restrict__ sc) {
@@ -760,10 +810,9 @@ int32_t jy_ujson_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* deoff
     SegSrc S{{deoff, dcoff, dvoff, A.ao, A.co}, {0, nel, nel + ncloud, nel + ncloud + nvv, nel + ncloud + nvv + ta}};
     JY_HIP(eng, hipMemsetAsync(sg, 0, nsg * 4, eng->stream));
     LAUNCH(k_uj_seg_starts, nd, S, nd, sg);
-    size_t tmp = 0;
-    JY_HIP(eng, hipcub::DeviceScan::InclusiveScan(nullptr, tmp, sg, sg, hipcub::Max(), (int)nsg, eng->stream));
-    JY_TRY(jy_scratch(eng, 15, tmp, &p));
-    JY_HIP(eng, hipcub::DeviceScan::InclusiveScan(p, tmp, sg, sg, hipcub::Max(), (int)nsg, eng->stream));
+    hipLaunchKernelGGL(k_uj_seg_fill, dim3((u32)((nsg + kFillTile - 1) / kFillTile)), dim3(kThreads), 0, eng->stream,
+                       S, nd, sg, nsg);
+    JY_HIP(eng, hipGetLastError());
   }
   JY_TRY(launch_ranges(k_uj_check, ranges({nvv, nel, ncloud}), A));
   LAUNCH(k_uj_drop_bad, nd * R, A);
