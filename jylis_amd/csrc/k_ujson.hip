@@ -528,69 +528,62 @@ __global__ __launch_bounds__(kThreads) void k_uj_seg_fill(SegSrc S, u64 nseg, u3
   Store(tmp.store).Store(a + t0, v, valid);
 }
 
-// ---- two exclusive u64 scans in one pass (the per-document size pairs) ---------------
-// reduce-then-scan: k_pair_tile_sums sums each 4096-item tile of both arrays;
-// k_pair_scan adds up the sums of the tiles before its own (a few hundred at
-// most for these batches) and scans its tile.  Two launches for both arrays
-// instead of two rocprim launches per array.
-typedef hipcub::BlockReduce<u64, kThreads> PairReduce;
-__global__ __launch_bounds__(kThreads) void k_pair_tile_sums(const u64* __restrict__ a, const u64* __restrict__ b,
-                                                             u64 n, u64* __restrict__ sums) {
-  __shared__ typename PairReduce::TempStorage tmp;
+// ---- exclusive scans by tiles (the per-document size pairs, the keep flags) ---------
+// reduce-then-scan: k_tile_sums sums each 4096-item tile of every array;
+// k_tile_scan adds up the sums of the tiles before its own (a few hundred at
+// most for these batches) and scans its tile.  Two launches for up to two
+// arrays, against two rocprim launches per array.
+template <typename T>
+struct ScanJob {
+  const T* in[2];
+  T* out[2];
+};
+template <typename T, int NA>
+__global__ __launch_bounds__(kThreads) void k_tile_sums(ScanJob<T> J, u64 n, T* __restrict__ sums) {
+  typedef hipcub::BlockReduce<T, kThreads> Red;
+  __shared__ typename Red::TempStorage tmp;
   const u64 t0 = (u64)blockIdx.x * kFillTile;
-  u64 sa = 0, sb = 0;
+#pragma unroll
+  for (int x = 0; x < NA; x++) {
+    T acc = 0;
 #pragma unroll 4
-  for (u64 i = t0 + threadIdx.x; i < t0 + kFillTile && i < n; i += kThreads) {
-    sa += a[i];
-    sb += b[i];
-  }
-  sa = PairReduce(tmp).Sum(sa);
-  __syncthreads();
-  sb = PairReduce(tmp).Sum(sb);
-  if (threadIdx.x == 0) {
-    sums[2 * blockIdx.x] = sa;
-    sums[2 * blockIdx.x + 1] = sb;
+    for (u64 i = t0 + threadIdx.x; i < t0 + kFillTile && i < n; i += kThreads) acc += J.in[x][i];
+    acc = Red(tmp).Sum(acc);
+    if (threadIdx.x == 0) sums[(u64)NA * blockIdx.x + x] = acc;
+    __syncthreads();
   }
 }
-__global__ __launch_bounds__(kThreads) void k_pair_scan(const u64* __restrict__ a, const u64* __restrict__ b,
-                                                        u64* __restrict__ oa, u64* __restrict__ ob, u64 n,
-                                                        const u64* __restrict__ sums) {
-  typedef hipcub::BlockScan<u64, kThreads> Scan;
-  typedef hipcub::BlockLoad<u64, kThreads, kFillPer, hipcub::BLOCK_LOAD_WARP_TRANSPOSE> Load;
-  typedef hipcub::BlockStore<u64, kThreads, kFillPer, hipcub::BLOCK_STORE_WARP_TRANSPOSE> Store;
+template <typename T, int NA>
+__global__ __launch_bounds__(kThreads) void k_tile_scan(ScanJob<T> J, u64 n, const T* __restrict__ sums) {
+  typedef hipcub::BlockReduce<T, kThreads> Red;
+  typedef hipcub::BlockScan<T, kThreads> Scan;
+  typedef hipcub::BlockLoad<T, kThreads, kFillPer, hipcub::BLOCK_LOAD_WARP_TRANSPOSE> Load;
+  typedef hipcub::BlockStore<T, kThreads, kFillPer, hipcub::BLOCK_STORE_WARP_TRANSPOSE> Store;
   __shared__ union {
-    typename PairReduce::TempStorage red;
+    typename Red::TempStorage red;
     typename Scan::TempStorage scan;
     typename Load::TempStorage load;
     typename Store::TempStorage store;
   } tmp;
-  __shared__ u64 carry[2];
-  u64 ca = 0, cb = 0;
-  for (u32 j = threadIdx.x; j < blockIdx.x; j += kThreads) {
-    ca += sums[2 * j];
-    cb += sums[2 * j + 1];
-  }
-  ca = PairReduce(tmp.red).Sum(ca);
-  __syncthreads();
-  cb = PairReduce(tmp.red).Sum(cb);
-  if (threadIdx.x == 0) {
-    carry[0] = ca;
-    carry[1] = cb;
-  }
-  __syncthreads();
+  __shared__ T carry;
   const u64 t0 = (u64)blockIdx.x * kFillTile;
   const int valid = (int)(n - t0 < kFillTile ? n - t0 : kFillTile);
-  u64 v[kFillPer];
 #pragma unroll
-  for (int side = 0; side < 2; side++) {
-    Load(tmp.load).Load((side ? b : a) + t0, v, valid, (u64)0);
+  for (int x = 0; x < NA; x++) {
+    T c = 0;
+    for (u32 j = threadIdx.x; j < blockIdx.x; j += kThreads) c += sums[(u64)NA * j + x];
+    c = Red(tmp.red).Sum(c);
+    if (threadIdx.x == 0) carry = c;
+    __syncthreads();
+    c = carry;
+    T v[kFillPer];
+    Load(tmp.load).Load(J.in[x] + t0, v, valid, (T)0);
     __syncthreads();
     Scan(tmp.scan).ExclusiveSum(v, v);
     __syncthreads();
-    const u64 c = carry[side];
 #pragma unroll
     for (int u = 0; u < kFillPer; u++) v[u] += c;
-    Store(tmp.store).Store((side ? ob : oa) + t0, v, valid);
+    Store(tmp.store).Store(J.out[x] + t0, v, valid);
     __syncthreads();
   }
 }
@@ -675,17 +668,22 @@ u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kThreads - 1) / kThrea
 
 // rewrite every document back to back into new pools with `room_e` / `room_c`
 // free entries after them; synchronises (the new sizes are read back)
-// exclusive scans of a[0..n] -> oa and b[0..n] -> ob (oa[n], ob[n] = totals)
-static int32_t uj_scan2(jy_engine* eng, const u64* a, u64* oa, const u64* b, u64* ob, u64 n) {
-  const u64 n1 = n + 1;
-  const u32 tiles = (u32)((n1 + kFillTile - 1) / kFillTile);
+// exclusive scans of n items of one or two arrays (in -> out, not in place)
+template <typename T, int NA>
+static int32_t uj_tile_scan(jy_engine* eng, ScanJob<T> J, u64 n) {
+  if (n == 0) return JY_OK;
+  const u32 tiles = (u32)((n + kFillTile - 1) / kFillTile);
   void* p;
-  JY_TRY(jy_scratch(eng, 19, (u64)tiles * 16, &p));
-  u64* sums = static_cast<u64*>(p);
-  hipLaunchKernelGGL(k_pair_tile_sums, dim3(tiles), dim3(kThreads), 0, eng->stream, a, b, n1, sums);
-  hipLaunchKernelGGL(k_pair_scan, dim3(tiles), dim3(kThreads), 0, eng->stream, a, b, oa, ob, n1, (const u64*)sums);
+  JY_TRY(jy_scratch(eng, 19, (u64)tiles * NA * sizeof(T), &p));
+  T* sums = static_cast<T*>(p);
+  hipLaunchKernelGGL((k_tile_sums<T, NA>), dim3(tiles), dim3(kThreads), 0, eng->stream, J, n, sums);
+  hipLaunchKernelGGL((k_tile_scan<T, NA>), dim3(tiles), dim3(kThreads), 0, eng->stream, J, n, (const T*)sums);
   JY_HIP(eng, hipGetLastError());
   return JY_OK;
+}
+// a[0..n] -> oa and b[0..n] -> ob (oa[n], ob[n] = the totals)
+static int32_t uj_scan2(jy_engine* eng, const u64* a, u64* oa, const u64* b, u64* ob, u64 n) {
+  return uj_tile_scan<u64, 2>(eng, ScanJob<u64>{{a, b}, {oa, ob}}, n + 1);
 }
 
 int32_t ujson_compact(jy_engine* eng, u64 room_e, u64 room_c) {
@@ -896,19 +894,9 @@ int32_t jy_ujson_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* deoff
   JY_TRY(launch_ranges(k_uj_check, ranges({nvv, nel, ncloud}), A));
   LAUNCH(k_uj_drop_bad, nd * R, A);
   JY_TRY(launch_ranges(k_uj_flags, ranges({ta + 1, nel + 1, ncloud + 1}), A));
-  {
-    size_t tmp = 0;
-    JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, A.flag_a, A.flag_a + nf, (int)nf, eng->stream));
-    JY_TRY(jy_scratch(eng, 15, tmp, &p));
-    JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(p, tmp, A.flag_a, A.flag_a + nf, (int)nf, eng->stream));
-  }
+  JY_TRY((uj_tile_scan<u32, 1>(eng, ScanJob<u32>{{A.flag_a, nullptr}, {A.flag_a + nf, nullptr}}, nf)));
   JY_TRY(launch_ranges(k_uj_compact, ranges({tc + 1, ncloud + 1}), A));
-  {
-    size_t tmp = 0;
-    JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, A.keep_ca, A.keep_ca + nkp, (int)nkp, eng->stream));
-    JY_TRY(jy_scratch(eng, 15, tmp, &p));
-    JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(p, tmp, A.keep_ca, A.keep_ca + nkp, (int)nkp, eng->stream));
-  }
+  JY_TRY((uj_tile_scan<u32, 1>(eng, ScanJob<u32>{{A.keep_ca, nullptr}, {A.keep_ca + nkp, nullptr}}, nkp)));
   LAUNCH(k_uj_sizes_out, nd + 1, A, ne, nc);
   JY_TRY(uj_scan2(eng, ne, neo, nc, nco, nd));
   Out O{neo, nco, u.epool, u.cpool, u.meta, eb0, cb0};
