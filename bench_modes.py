@@ -230,11 +230,14 @@ def bench_treg(args, eng, dev, dist, rank, world):
     t0 = time.perf_counter()
     if routed:
         import torch.distributed as tdist
+
+        from jylis_amd.route import DistFabric, LocalFabric
         cpu_group = tdist.new_group(backend="gloo") if world > 1 else None
         router = ShardRouter(rank, world, lambda tab: eng.intern(TREG, tab), dist=tdist if world > 1 else None,
                              group=cpu_group)
         own, slot = router.resolve(kb, ko)
-        tr = TregRouter(eng, tdist if world > 1 else None)
+        fabric = DistFabric(tdist, cpu_group=cpu_group) if world > 1 else LocalFabric(1)
+        tr = TregRouter([eng], fabric)
     else:
         slot = eng.intern(TREG, (kb, ko))
         own = np.zeros(len(slot), np.uint32)
@@ -248,13 +251,14 @@ def bench_treg(args, eng, dev, dist, rank, world):
         # fresh writes: batch j's timestamps sit 2^18 above batch j-1's in a
         # 2^20 window, so ~70% of keys take the delta and ties are dense
         ts = (rng.integers(0, 1 << 20, n) + (j << 18)).astype(np.uint64)
-        batches.append(tuple(_to_dev(a, dev) for a in (own, slot, ts, pre, lr)))
+        lens = lr & np.uint64((1 << 24) - 1)
+        batches.append(tuple(_to_dev(a, dev) for a in (own, slot, ts, pre, lr)) + (int(lens[lens > 8].sum()),))
     win = []
 
     def step_of(b):
-        o, s, ts, pre, lr = b
+        o, s, ts, pre, lr, nbytes = b
         if routed:
-            tr.exchange_and_converge(o, s, ts, pre, lr)
+            tr.step([b])
         else:
             eng.treg_converge(s, ts, pre, lr)
 

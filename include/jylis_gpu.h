@@ -49,11 +49,15 @@ enum { JY_HOST = 0, JY_DEVICE = 1 };
 
 typedef struct jy_engine jy_engine;
 
+/* jy_config.flags: test switches that force a kernel form the engine would
+ * otherwise pick by state size (the parity tests reach every form) */
+#define JY_CFG_TREG_WHOLE_LINES 1u /* k_treg_lww<true>: every handle line rewritten */
+
 typedef struct jy_config {
   int32_t device;            /* HIP device ordinal                                   */
   uint32_t counter_columns;  /* initial replica-column capacity of GCOUNT/PNCOUNT    */
   uint32_t ujson_columns;    /* version-vector width of UJSON contexts (fixed)       */
-  uint32_t reserved;
+  uint32_t flags;            /* JY_CFG_* switches; 0 in production                   */
   uint64_t key_capacity[JY_NTYPES];   /* initial slots per type (grows by doubling)  */
   uint64_t entry_capacity[JY_NTYPES]; /* initial TLOG entries / UJSON dots            */
   uint64_t arena_capacity[JY_NTYPES]; /* initial string arena bytes (TREG, TLOG)      */
@@ -210,24 +214,31 @@ int32_t jy_ujson_read(jy_engine* eng, uint64_t n, const uint32_t* slots, const u
 /* ---- multi-GPU routing: the exchange step of a key-hash-sharded node ----
  * Replaces nothing in the reference (every node holds every key there); it is
  * the intra-node analogue of Cluster.broadcast_deltas (cluster.pony:209-213).
- * A TREG batch ingested on one GPU is partitioned by owner shard into u64[4]
- * records {slot on owner, ts, pre, lr'} plus the bytes of values > 8 bytes
- * (lr' offsets are relative to the destination's byte run).  The host moves
- * both with an all-to-all(v) (RCCL) and each owner converges its runs. */
+ * Runs have a FIXED capacity per destination, so the all-to-all is an
+ * equal-split collective and the counts travel on the device with the data:
+ * no host round trip per batch.
+ *
+ * Sender: jy_treg_route_part partitions n ingested TREG entries (owner
+ * shard, slot on the owner, ts, pre, lr) into nshards runs:
+ *   recs_dev  u64[nshards][cap][4] {slot, ts, pre, lr'}, 16-B aligned; lr' of a
+ *             value > 8 bytes addresses the run's own bytes
+ *   bytes_dev u8[nshards][cap_byte]
+ *   hdr_dev   u64[nshards][2]: records / value bytes reserved per destination
+ *             (ZERO on entry; may end above the capacities)
+ *   ovf_dev   u32[1 + n]: [0] = entries that did not fit (ZERO on entry), then
+ *             their input indices -- the caller sends those in a later round.
+ * Receiver: jy_treg_converge_routed merges nsrc received runs (the same
+ * layout, source-major, each source's hdr row) in one launch; a key named by
+ * several sources is exact (LWW join).  All pointers are device memory
+ * except the `mem`-tagged inputs; both calls only enqueue. */
 void jy_keys_owner(uint64_t n, const uint8_t* key_bytes, const uint64_t* key_offs, uint32_t nshards,
                    uint32_t* owner_out);
-/* records / value bytes per destination (host out, nshards each) */
-int32_t jy_treg_route_count(jy_engine* eng, uint64_t n, const uint32_t* owner, const uint64_t* lr,
-                            uint32_t nshards, int32_t mem, uint64_t* rec_counts, uint64_t* byte_counts);
-/* scatter into caller-provided device buffers (records u64[n][4], 16-B aligned; bytes) laid
- * out destination by destination in the order of the counts */
-int32_t jy_treg_route_scatter(jy_engine* eng, uint64_t n, const uint32_t* owner, const uint32_t* slot,
-                              const uint64_t* ts, const uint64_t* pre, const uint64_t* lr, uint32_t nshards,
-                              const uint64_t* rec_counts, const uint64_t* byte_counts, int32_t mem,
-                              uint64_t* recs_dev, uint8_t* bytes_dev);
-/* owner side: converge nsrc received runs (device buffers, counts on host) */
-int32_t jy_treg_converge_routed(jy_engine* eng, uint32_t nsrc, const uint64_t* rec_counts,
-                                const uint64_t* byte_counts, const uint64_t* recs_dev, const uint8_t* bytes_dev);
+int32_t jy_treg_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, const uint32_t* slot,
+                           const uint64_t* ts, const uint64_t* pre, const uint64_t* lr, uint32_t nshards,
+                           uint64_t cap, uint64_t cap_byte, int32_t mem, uint64_t* recs_dev, uint8_t* bytes_dev,
+                           uint64_t* hdr_dev, uint32_t* ovf_dev);
+int32_t jy_treg_converge_routed(jy_engine* eng, uint32_t nsrc, uint64_t cap, uint64_t cap_byte,
+                                const uint64_t* recs_dev, const uint8_t* bytes_dev, const uint64_t* hdr_dev);
 
 #ifdef __cplusplus
 }

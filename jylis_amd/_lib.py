@@ -15,6 +15,7 @@ JY_NO_SLOT = 0xFFFFFFFF
 GCOUNT, PNCOUNT, TREG, TLOG, UJSON = 0, 1, 2, 3, 4
 TYPE_NAMES = {"GCOUNT": GCOUNT, "PNCOUNT": PNCOUNT, "TREG": TREG, "TLOG": TLOG, "UJSON": UJSON}
 HOST, DEVICE = 0, 1
+CFG_TREG_WHOLE_LINES = 1
 
 
 class JyConfig(C.Structure):
@@ -22,7 +23,7 @@ class JyConfig(C.Structure):
         ("device", C.c_int32),
         ("counter_columns", C.c_uint32),
         ("ujson_columns", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("flags", C.c_uint32),
         ("key_capacity", C.c_uint64 * 5),
         ("entry_capacity", C.c_uint64 * 5),
         ("arena_capacity", C.c_uint64 * 5),
@@ -80,9 +81,8 @@ SIGNATURES = {
     "jy_ujson_read_sizes": (I32, [P, U64, P, P, P]),
     "jy_ujson_read": (I32, [P, U64, P, P, P, P, P, P, P]),
     "jy_keys_owner": (None, [U64, P, P, U32, P]),
-    "jy_treg_route_count": (I32, [P, U64, P, P, U32, I32, P, P]),
-    "jy_treg_route_scatter": (I32, [P, U64, P, P, P, P, P, U32, P, P, I32, P, P]),
-    "jy_treg_converge_routed": (I32, [P, U32, P, P, P, P]),
+    "jy_treg_route_part": (I32, [P, U64, P, P, P, P, P, U32, U64, U64, I32, P, P, P, P]),
+    "jy_treg_converge_routed": (I32, [P, U32, U64, U64, P, P, P]),
 }
 
 # include/jylis_host.h: the C++ host mirror (Database / RepoManagerCore / Repo*)

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstring>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "jy_internal.hpp"
@@ -23,14 +24,16 @@ bool csr_ok(const u64* offs, u64 n, u64 total) {
 }
 
 // occurrence index of each slot inside the call; returns the number of rounds
-u32 rounds_of(jy_engine* eng, int32_t type, u64 n, const u32* slot, std::vector<u32>& occ) {
-  std::vector<uint8_t> mark(eng->nkeys[type], 0);
-  bool dup = false;
-  for (u64 i = 0; i < n && !dup; i++) {
-    if (mark[slot[i]]) dup = true;
-    mark[slot[i]] = 1;
+// (a hash set sized to the call, not to the interned keys: the host mirror
+// makes many one-key calls)
+u32 rounds_of(u64 n, const u32* slot, std::vector<u32>& occ) {
+  {
+    std::unordered_set<u32> mark;
+    mark.reserve(n * 2);
+    bool dup = false;
+    for (u64 i = 0; i < n && !dup; i++) dup = !mark.insert(slot[i]).second;
+    if (!dup) return 1;
   }
-  if (!dup) return 1;
   std::unordered_map<u32, u32> seen;
   occ.resize(n);
   u32 rounds = 1;
@@ -78,7 +81,7 @@ int32_t jy_tlog_converge(jy_engine* eng, uint64_t n, const uint32_t* slot, const
       if ((lr[j] & JY_LR_LEN_MASK) > 8 && (lr[j] >> JY_LR_LEN_BITS) + (lr[j] & JY_LR_LEN_MASK) > alen)
         return eng->fail(JY_ERANGE, "value handle outside the arena");
     std::vector<u32> occ;
-    const u32 rounds = rounds_of(eng, JY_TLOG, n, slot, occ);
+    const u32 rounds = rounds_of(n, slot, occ);
     if (rounds > 1) {
       for (u32 r = 0; r < rounds; r++) {
         std::vector<u64> idx;
@@ -163,7 +166,7 @@ int32_t jy_ujson_converge(jy_engine* eng, uint64_t n, const uint32_t* slot, cons
     if (!csr_ok(eoffs, n, nel) || !csr_ok(voffs, n, nvv) || !csr_ok(coffs, n, ncloud))
       return eng->fail(JY_EINVAL, "element / vv / cloud offsets are not CSRs of their totals");
     std::vector<u32> occ;
-    const u32 rounds = rounds_of(eng, JY_UJSON, n, slot, occ);
+    const u32 rounds = rounds_of(n, slot, occ);
     if (rounds > 1) {
       for (u32 r = 0; r < rounds; r++) {
         std::vector<u64> idx;

@@ -706,104 +706,50 @@ int32_t jy_counter_flush(jy_engine* eng, int32_t type, uint64_t cap, uint32_t* s
 }
 
 // ---- TREG ----
+// A key repeated inside one call (host or device memory) is exact: the
+// device folds the repeats in after the wide merge (k_treg.hip), and LWW
+// is a join, so SET batches and converges need no host-side rounds.
+static int32_t treg_handles_check(jy_engine* eng, u64 n, const u64* lr) {
+  const u64 alen = eng->arena[JY_TREG].len;
+  for (u64 i = 0; i < n; i++)
+    if ((lr[i] & JY_LR_LEN_MASK) > 8 && (lr[i] >> JY_LR_LEN_BITS) + (lr[i] & JY_LR_LEN_MASK) > alen)
+      return eng->fail(JY_ERANGE, "value handle outside the arena");
+  return JY_OK;
+}
+
+static int32_t treg_stage(jy_engine* eng, uint64_t n, const uint32_t* slot, const uint64_t* ts, const uint64_t* pre,
+                          const uint64_t* lr, int32_t mem, const void** ds, const void** dt, const void** dp,
+                          const void** dl) {
+  JY_TRY(slots_check(eng, JY_TREG, n, slot, mem));
+  if (mem == JY_HOST) JY_TRY(treg_handles_check(eng, n, lr));
+  JY_TRY(stage_begin(eng));
+  JY_TRY(jy_stage(eng, 0, slot, n * 4, mem, ds));
+  JY_TRY(jy_stage(eng, 1, ts, n * 8, mem, dt));
+  JY_TRY(jy_stage(eng, 2, pre, n * 8, mem, dp));
+  JY_TRY(jy_stage(eng, 3, lr, n * 8, mem, dl));
+  return stage_end(eng);
+}
+
 int32_t jy_treg_converge(jy_engine* eng, uint64_t n, const uint32_t* slot, const uint64_t* ts, const uint64_t* pre,
                          const uint64_t* lr, int32_t mem) {
   JY_HIP(eng, hipSetDevice(eng->device));
   if (n == 0) return JY_OK;
-  JY_TRY(slots_check(eng, JY_TREG, n, slot, mem));
-  if (mem == JY_HOST) {
-    // one delta per key per call (Map semantics); split repeated keys into rounds
-    std::unordered_map<u32, u32> seen;
-    std::vector<u32> round(n);
-    u32 rounds = 1;
-    bool dup = false;
-    {
-      std::vector<uint8_t> mark(eng->nkeys[JY_TREG], 0);
-      for (u64 i = 0; i < n; i++) {
-        if (mark[slot[i]]) dup = true;
-        mark[slot[i]] = 1;
-      }
-    }
-    if (dup) {
-      for (u64 i = 0; i < n; i++) {
-        u32 r = seen[slot[i]]++;
-        round[i] = r;
-        rounds = std::max(rounds, r + 1);
-      }
-      for (u32 r = 0; r < rounds; r++) {
-        std::vector<u32> s;
-        std::vector<u64> t, p, l;
-        for (u64 i = 0; i < n; i++)
-          if (round[i] == r) {
-            s.push_back(slot[i]);
-            t.push_back(ts[i]);
-            p.push_back(pre[i]);
-            l.push_back(lr[i]);
-          }
-        JY_TRY(jy_treg_converge(eng, s.size(), s.data(), t.data(), p.data(), l.data(), JY_HOST));
-      }
-      return JY_OK;
-    }
-    u64 alen = eng->arena[JY_TREG].len;
-    for (u64 i = 0; i < n; i++)
-      if ((lr[i] & JY_LR_LEN_MASK) > 8 && (lr[i] >> JY_LR_LEN_BITS) + (lr[i] & JY_LR_LEN_MASK) > alen)
-        return eng->fail(JY_ERANGE, "value handle outside the arena");
-  }
+  if (n >= 0xFFFFFFFFull) return eng->fail(JY_ERANGE, "more than 2^32 - 1 entries in one call");
   const void *ds, *dt, *dp, *dl;
-  JY_TRY(stage_begin(eng));
-  JY_TRY(jy_stage(eng, 0, slot, n * 4, mem, &ds));
-  JY_TRY(jy_stage(eng, 1, ts, n * 8, mem, &dt));
-  JY_TRY(jy_stage(eng, 2, pre, n * 8, mem, &dp));
-  JY_TRY(jy_stage(eng, 3, lr, n * 8, mem, &dl));
-  JY_TRY(stage_end(eng));
+  JY_TRY(treg_stage(eng, n, slot, ts, pre, lr, mem, &ds, &dt, &dp, &dl));
   return jy_treg_merge(eng, n, (const u32*)ds, (const u64*)dt, (const u64*)dp, (const u64*)dl);
 }
 
-// local SET batch (RepoTREG.set repo_treg.pony:65-68): pending delta first
-// (against the state as it was), then the state merge.  Host batches that
-// repeat a key run as rounds, in order; a device batch holds one entry per key.
+// local SET batch (RepoTREG.set repo_treg.pony:65-68): the state merge and
+// the pending delta in one pass (k_treg.hip set_one)
 int32_t jy_treg_set(jy_engine* eng, uint64_t n, const uint32_t* slot, const uint64_t* ts, const uint64_t* pre,
                     const uint64_t* lr, int32_t mem) {
   JY_HIP(eng, hipSetDevice(eng->device));
   if (n == 0) return JY_OK;
-  JY_TRY(slots_check(eng, JY_TREG, n, slot, mem));
-  if (mem == JY_HOST) {
-    std::unordered_map<u32, u32> seen;
-    std::vector<u32> round(n);
-    u32 rounds = 1;
-    for (u64 i = 0; i < n; i++) {
-      round[i] = seen[slot[i]]++;
-      rounds = std::max(rounds, round[i] + 1);
-    }
-    if (rounds > 1) {
-      for (u32 r = 0; r < rounds; r++) {
-        std::vector<u32> s;
-        std::vector<u64> t, p, l;
-        for (u64 i = 0; i < n; i++)
-          if (round[i] == r) {
-            s.push_back(slot[i]);
-            t.push_back(ts[i]);
-            p.push_back(pre[i]);
-            l.push_back(lr[i]);
-          }
-        JY_TRY(jy_treg_set(eng, s.size(), s.data(), t.data(), p.data(), l.data(), JY_HOST));
-      }
-      return JY_OK;
-    }
-    u64 alen = eng->arena[JY_TREG].len;
-    for (u64 i = 0; i < n; i++)
-      if ((lr[i] & JY_LR_LEN_MASK) > 8 && (lr[i] >> JY_LR_LEN_BITS) + (lr[i] & JY_LR_LEN_MASK) > alen)
-        return eng->fail(JY_ERANGE, "value handle outside the arena");
-  }
+  if (n >= 0xFFFFFFFFull) return eng->fail(JY_ERANGE, "more than 2^32 - 1 entries in one call");
   const void *ds, *dt, *dp, *dl;
-  JY_TRY(stage_begin(eng));
-  JY_TRY(jy_stage(eng, 0, slot, n * 4, mem, &ds));
-  JY_TRY(jy_stage(eng, 1, ts, n * 8, mem, &dt));
-  JY_TRY(jy_stage(eng, 2, pre, n * 8, mem, &dp));
-  JY_TRY(jy_stage(eng, 3, lr, n * 8, mem, &dl));
-  JY_TRY(stage_end(eng));
-  JY_TRY(jy_treg_set_pending(eng, n, (const u32*)ds, (const u64*)dt, (const u64*)dp, (const u64*)dl));
-  return jy_treg_merge(eng, n, (const u32*)ds, (const u64*)dt, (const u64*)dp, (const u64*)dl);
+  JY_TRY(treg_stage(eng, n, slot, ts, pre, lr, mem, &ds, &dt, &dp, &dl));
+  return jy_treg_set_batch(eng, n, (const u32*)ds, (const u64*)dt, (const u64*)dp, (const u64*)dl);
 }
 
 int32_t jy_treg_deltas_size(jy_engine* eng, uint64_t* n_out) {

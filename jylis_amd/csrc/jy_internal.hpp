@@ -54,6 +54,70 @@ __device__ __forceinline__ int jy_value_cmp(u64 pa, u64 la, u64 pb, u64 lb, cons
   return na < nb ? -1 : 1;
 }
 
+__device__ __forceinline__ u32 jy_wave_or(u32 x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x |= __shfl_xor(x, o);
+  return x;
+}
+
+// ---- first-occurrence claims: exact handling of a slot named twice in one launch
+// `bits` holds one bit per slot and is zero before the launch.  For each of
+// the U rows of a wave (one entry per lane per row), first[u] is true iff the
+// lane's entry is the FIRST entry of its slot in the whole launch: the one
+// whose atomicOr set the slot's bit.  Every lane of the wave calls this
+// together.  A batch in slot order (a flush, a routed run) puts a row's 64
+// entries on two or three bitmap words, so the row's distinct words are
+// walked with ballots (at most kAgg) and each is claimed by ONE atomicOr of
+// the OR of its lanes' bits; lanes left over (scattered slots, or two lanes
+// of a row on one slot) claim with one atomicOr each -- the memory side
+// orders those, so exactly one entry of a slot sees its bit clear.  Every
+// atomic of all U rows is issued before any result is consumed.
+template <int U, int kAgg = 3>
+__device__ __forceinline__ void jy_claim_rows(const bool (&valid)[U], const u32 (&s)[U], u32* __restrict__ bits,
+                                              bool (&first)[U]) {
+  const int lane = __lane_id();
+  u32 ret[U][kAgg], own[U];
+  int grp[U], ldr[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const u32 w = s[u] >> 5, b = 1u << (s[u] & 31);
+    grp[u] = -1;
+    ldr[u] = 0;
+    u64 pending = __ballot(valid[u]);
+#pragma unroll
+    for (int k = 0; k < kAgg; k++) {
+      ret[u][k] = 0;
+      if (pending) {  // wave-uniform
+        const int leader = __ffsll((unsigned long long)pending) - 1;
+        const u32 d = __shfl(w, leader);
+        const bool mine = ((pending >> lane) & 1) && w == d;
+        const u64 m = __ballot(mine);
+        const u32 orv = jy_wave_or(mine ? b : 0u);
+        if ((u32)__popc(orv) == (u32)__popcll(m)) {  // no two lanes of the group on one slot
+          if (lane == leader) ret[u][k] = atomicOr(bits + d, orv);
+          if (mine) {
+            grp[u] = k;
+            ldr[u] = leader;
+          }
+        }
+        pending &= ~m;
+      }
+    }
+    own[u] = 0;
+    if (valid[u] && grp[u] < 0) own[u] = atomicOr(bits + w, b);
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    u32 old = own[u];
+#pragma unroll
+    for (int k = 0; k < kAgg; k++) {
+      const u32 v = __shfl(ret[u][k], ldr[u]);
+      if (grp[u] == k) old = v;
+    }
+    first[u] = valid[u] && !(old & (1u << (s[u] & 31)));
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Host-side engine state
 
@@ -111,6 +175,10 @@ struct TregState {  // per slot: ts u64 (read by every merge) + TVal (written by
   u32* dflag = nullptr;
   u64 dkcap = 0;
   u64* dcount = nullptr;
+  // first-occurrence claim bitmap (one bit per slot, zero between launches)
+  // followed by the launch's duplicate counter; see jy_claim_rows
+  u32* seen = nullptr;
+  u64 seen_words = 0;  // bitmap words (the counter is word seen_words)
 };
 
 // one TLOG entry: 32 B so a lane moves it with two 16-B accesses and an
@@ -307,9 +375,13 @@ int32_t jy_cnt_pending(jy_engine* eng, int which, u64* count_host);
 int32_t jy_treg_grow(jy_engine* eng, u64 need_slots);
 int32_t jy_treg_merge(jy_engine* eng, u64 n, const u32* slot, const u64* ts, const u64* pre, const u64* lr);
 int32_t jy_treg_gather(jy_engine* eng, u64 n, const u32* slots, u64* ts, u64* pre, u64* lr);
-// routed records (slot, ts, pre, lr) x n, long values rebased by `base`
-int32_t jy_treg_merge_records(jy_engine* eng, const u64* recs, u64 n, u64 base);
-int32_t jy_treg_set_pending(jy_engine* eng, u64 n, const u32* slot, const u64* ts, const u64* pre, const u64* lr);
+// routed runs: S sources x cap records (slot, ts, pre, lr'), counts in hdr
+// (device, 2 u64 per source); source src's value bytes at arena offset
+// rebase + src * cap_byte
+int32_t jy_treg_merge_routed(jy_engine* eng, u32 S, u64 cap, u64 cap_byte, const u64* recs, const u64* hdr,
+                             u64 rebase);
+// local SETs: state LWW + pending delta, repeated keys exact
+int32_t jy_treg_set_batch(jy_engine* eng, u64 n, const u32* slot, const u64* ts, const u64* pre, const u64* lr);
 int32_t jy_treg_pending(jy_engine* eng, u64* count_host);
 int32_t jy_treg_flush_dev(jy_engine* eng, u64 nkeys, u64 cap, u32* slot_dev, u64* ts_dev, u64* pre_dev, u64* lr_dev,
                       u64* count_host);

@@ -1,16 +1,18 @@
 // k_route.hip -- routing delta batches to owner shards (the exchange step).
 //
 // Keys are hash-sharded over S engines (jy_key_owner).  A peer batch that
-// lands on one GPU is partitioned by owner into contiguous per-destination
-// runs, exchanged with one all-to-all(v) (RCCL over xGMI; the host side
-// drives it), and each owner converges what it received, one call per
-// source run (a run holds each key at most once, as the sender's Map did).
+// lands on one GPU is partitioned by owner into per-destination runs of a
+// FIXED capacity, exchanged with one equal-split all-to-all (RCCL over
+// xGMI; the host side drives it) together with a small header of counts,
+// and each owner converges every received run in one launch, reading the
+// counts from device memory -- no host round trip per batch.  Entries that
+// do not fit their run are listed for a later round (jylis_amd/route.py).
 // This is the intra-node analogue of Cluster.broadcast_deltas
 // (jylis/cluster.pony:209-213); the reference replicates instead.
 //
 // TREG record: u64[4] = {slot on owner, ts, pre, lr'}, lr' = (byte offset
 // inside the destination's byte run << 24 | length) for values > 8 bytes,
-// whose bytes travel in a second all-to-all.
+// whose bytes travel in a second run.
 //
 // Roofline: HBM.  Partition reads 4+4+24 B per entry (+ long value bytes),
 // writes 32 B per record; the receiver reads 32 B per record + state.
@@ -72,38 +74,19 @@ __device__ __forceinline__ void wave_aggregate(bool valid, u32 o, u32 blen, unsi
   }
 }
 
-__global__ __launch_bounds__(kThreads) void k_route_count(const u32* __restrict__ owner, const u64* __restrict__ lr,
-                                                          u64 n, u32 S, unsigned long long* __restrict__ counts) {
-  __shared__ unsigned long long lrec[kMaxShards], lbyte[kMaxShards];
-  for (u32 i = threadIdx.x; i < S; i += kThreads) lrec[i] = lbyte[i] = 0;
-  __syncthreads();
-  const u64 base = (u64)blockIdx.x * kTile + threadIdx.x;
-  u32 o[kPer];
-  u64 len[kPer];
-#pragma unroll
-  for (int u = 0; u < kPer; u++) {  // every load in flight before the first ballot
-    const u64 i = base + (u64)u * kThreads;
-    o[u] = i < n ? owner[i] : 0;
-    len[u] = i < n ? (lr[i] & JY_LR_LEN_MASK) : 0;
-  }
-#pragma unroll
-  for (int u = 0; u < kPer; u++)
-    wave_aggregate<false>(base + (u64)u * kThreads < n, o[u], len[u] > 8 ? (u32)len[u] : 0u, lrec, lbyte, nullptr,
-                          nullptr);
-  __syncthreads();
-  for (u32 d = threadIdx.x; d < S; d += kThreads) {
-    if (lrec[d]) atomicAdd(&counts[d], lrec[d]);
-    if (lbyte[d]) atomicAdd(&counts[S + d], lbyte[d]);
-  }
-}
-
-// cursors[0..S) record cursors, [S..2S) byte cursors, initialised to the
-// destination bases; bases[S..2S) = byte bases (for relative offsets)
-__global__ __launch_bounds__(kThreads) void k_route_scatter_treg(
+// One pass: per-owner ranks inside the workgroup (wave_aggregate), one
+// global reservation per (workgroup, owner) on the header cursors, then
+// every entry that fits its owner's run is written there.  An entry past
+// the run's record capacity, or whose long value would pass the run's byte
+// capacity, is listed in ovf (input index) -- a record slot it took is left
+// as a hole (slot ~0) the receiver skips.  hdr[2d] / hdr[2d + 1] end as the
+// records / bytes reserved for owner d, which may pass the capacities; the
+// receiver clamps.
+__global__ __launch_bounds__(kThreads) void k_route_part_treg(
     const u32* __restrict__ owner, const u32* __restrict__ slot, const u64* __restrict__ ts,
-    const u64* __restrict__ pre, const u64* __restrict__ lr, const uint8_t* __restrict__ arena, u64 n, u32 S,
-    unsigned long long* __restrict__ cursors, const u64* __restrict__ byte_base, u64* __restrict__ recs,
-    uint8_t* __restrict__ bytes) {
+    const u64* __restrict__ pre, const u64* __restrict__ lr, const uint8_t* __restrict__ arena, u64 n, u32 S, u64 cap,
+    u64 cap_byte, unsigned long long* __restrict__ hdr, u64* __restrict__ recs, uint8_t* __restrict__ bytes,
+    u32* __restrict__ ovf) {
   __shared__ unsigned long long lrec[kMaxShards], lbyte[kMaxShards], grec[kMaxShards], gbyte[kMaxShards];
   for (u32 d = threadIdx.x; d < S; d += kThreads) lrec[d] = lbyte[d] = 0;
   __syncthreads();
@@ -127,10 +110,9 @@ __global__ __launch_bounds__(kThreads) void k_route_scatter_treg(
     wave_aggregate<true>(base + (u64)u * kThreads < n, o[u], len > 8 ? (u32)len : 0u, lrec, lbyte, &rk[u], &brk[u]);
   }
   __syncthreads();
-  // one global reservation per (workgroup, owner)
   for (u32 d = threadIdx.x; d < S; d += kThreads) {
-    grec[d] = lrec[d] ? atomicAdd(&cursors[d], lrec[d]) : 0;
-    gbyte[d] = lbyte[d] ? atomicAdd(&cursors[S + d], lbyte[d]) : 0;
+    grec[d] = lrec[d] ? atomicAdd(&hdr[2 * d], lrec[d]) : 0;
+    gbyte[d] = lbyte[d] ? atomicAdd(&hdr[2 * d + 1], lbyte[d]) : 0;
   }
   __syncthreads();
 #pragma unroll
@@ -139,14 +121,22 @@ __global__ __launch_bounds__(kThreads) void k_route_scatter_treg(
     if (i >= n) continue;
     const u64 pos = grec[o[u]] + rk[u];
     const u64 len = l[u] & JY_LR_LEN_MASK;
-    u64 out_lr = l[u];
-    if (len > 8) {
-      const u64 bpos = gbyte[o[u]] + brk[u];
-      const uint8_t* src = arena + (l[u] >> JY_LR_LEN_BITS);
-      for (u64 j = 0; j < len; j++) bytes[bpos + j] = src[j];
-      out_lr = ((bpos - byte_base[o[u]]) << JY_LR_LEN_BITS) | len;
+    const u64 bpos = gbyte[o[u]] + brk[u];
+    const bool long_v = len > 8;
+    const bool fits = pos < cap && (!long_v || bpos + len <= cap_byte);
+    u64x2* r = reinterpret_cast<u64x2*>(recs + ((u64)o[u] * cap + pos) * 4);  // 32-B records, two 16-B stores
+    if (!fits) {
+      ovf[1 + atomicAdd(ovf, 1u)] = (u32)i;
+      if (pos < cap) r[0] = u64x2{~0ull, 0};  // hole
+      continue;
     }
-    u64x2* r = reinterpret_cast<u64x2*>(recs + pos * 4);  // 32-B records, two 16-B stores
+    u64 out_lr = l[u];
+    if (long_v) {
+      uint8_t* dst = bytes + (u64)o[u] * cap_byte + bpos;
+      const uint8_t* src = arena + (l[u] >> JY_LR_LEN_BITS);
+      for (u64 j = 0; j < len; j++) dst[j] = src[j];
+      out_lr = (bpos << JY_LR_LEN_BITS) | len;
+    }
     r[0] = u64x2{(u64)sl[u], t[u]};
     r[1] = u64x2{p[u], out_lr};
   }
@@ -162,81 +152,44 @@ void jy_keys_owner(uint64_t n, const uint8_t* kb, const uint64_t* ko, uint32_t n
   for (u64 i = 0; i < n; i++) out[i] = jy_key_owner(kb + ko[i], ko[i + 1] - ko[i], nshards);
 }
 
-int32_t jy_treg_route_count(jy_engine* eng, uint64_t n, const uint32_t* owner, const uint64_t* lr, uint32_t nshards,
-                            int32_t mem, uint64_t* rec_counts, uint64_t* byte_counts) {
-  JY_HIP(eng, hipSetDevice(eng->device));
-  if (nshards == 0 || nshards > kMaxShards) return eng->fail(JY_ERANGE, "nshards must be in [1, 64]");
-  if (mem == JY_HOST)
-    for (u64 i = 0; i < n; i++)
-      if (owner[i] >= nshards) return eng->fail(JY_ERANGE, "owner outside [0, nshards)");
-  const void *dow, *dlr;
-  JY_TRY(jy_stage_begin(eng));
-  JY_TRY(jy_stage(eng, 0, owner, n * 4, mem, &dow));
-  JY_TRY(jy_stage(eng, 4, lr, n * 8, mem, &dlr));
-  JY_TRY(jy_stage_end(eng));
-  void* c;
-  JY_TRY(jy_scratch(eng, 12, 2 * nshards * 8, &c));
-  JY_HIP(eng, hipMemsetAsync(c, 0, 2 * nshards * 8, eng->stream));
-  if (n)
-    hipLaunchKernelGGL(k_route_count, dim3(blocks_for(n)), dim3(kThreads), 0, eng->stream,
-                       static_cast<const u32*>(dow), static_cast<const u64*>(dlr), n, nshards,
-                       static_cast<unsigned long long*>(c));
-  JY_HIP(eng, hipGetLastError());
-  std::vector<u64> h(2 * nshards);
-  JY_HIP(eng, hipMemcpyAsync(h.data(), c, 2 * nshards * 8, hipMemcpyDeviceToHost, eng->stream));
-  JY_HIP(eng, hipStreamSynchronize(eng->stream));
-  std::copy(h.begin(), h.begin() + nshards, rec_counts);
-  std::copy(h.begin() + nshards, h.end(), byte_counts);
-  return JY_OK;
-}
-
-int32_t jy_treg_route_scatter(jy_engine* eng, uint64_t n, const uint32_t* owner, const uint32_t* slot,
-                              const uint64_t* ts, const uint64_t* pre, const uint64_t* lr, uint32_t nshards,
-                              const uint64_t* rec_counts, const uint64_t* byte_counts, int32_t mem,
-                              uint64_t* recs_dev, uint8_t* bytes_dev) {
+int32_t jy_treg_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, const uint32_t* slot, const uint64_t* ts,
+                           const uint64_t* pre, const uint64_t* lr, uint32_t nshards, uint64_t cap, uint64_t cap_byte,
+                           int32_t mem, uint64_t* recs_dev, uint8_t* bytes_dev, uint64_t* hdr_dev,
+                           uint32_t* ovf_dev) {
   JY_HIP(eng, hipSetDevice(eng->device));
   if (nshards == 0 || nshards > kMaxShards) return eng->fail(JY_ERANGE, "nshards must be in [1, 64]");
   if (n == 0) return JY_OK;
-  std::vector<u64> init(2 * nshards), bbase(nshards);
-  u64 r = 0, b = 0;
-  for (u32 d = 0; d < nshards; d++) {
-    init[d] = r;
-    init[nshards + d] = b;
-    bbase[d] = b;
-    r += rec_counts[d];
-    b += byte_counts[d];
-  }
-  if (r != n) return eng->fail(JY_EINVAL, "record counts do not add up to n");
+  if (n >= 0xFFFFFFFFull) return eng->fail(JY_ERANGE, "more than 2^32 - 1 entries in one call");
   if (reinterpret_cast<uintptr_t>(recs_dev) % 16) return eng->fail(JY_EINVAL, "recs_dev must be 16-B aligned");
-  const void *dow, *dsl, *dts, *dpre, *dlr, *dinit, *dbb;
+  if (mem == JY_HOST)
+    for (u64 i = 0; i < n; i++)
+      if (owner[i] >= nshards) return eng->fail(JY_ERANGE, "owner outside [0, nshards)");
+  const void *dow, *dsl, *dts, *dpre, *dlr;
   JY_TRY(jy_stage_begin(eng));
   JY_TRY(jy_stage(eng, 0, owner, n * 4, mem, &dow));
   JY_TRY(jy_stage(eng, 1, slot, n * 4, mem, &dsl));
   JY_TRY(jy_stage(eng, 2, ts, n * 8, mem, &dts));
   JY_TRY(jy_stage(eng, 3, pre, n * 8, mem, &dpre));
   JY_TRY(jy_stage(eng, 4, lr, n * 8, mem, &dlr));
-  JY_TRY(jy_stage(eng, 5, init.data(), init.size() * 8, JY_HOST, &dinit));
-  JY_TRY(jy_stage(eng, 6, bbase.data(), bbase.size() * 8, JY_HOST, &dbb));
   JY_TRY(jy_stage_end(eng));
-  // the cursors are updated in place: use a private copy of the bases
-  void* cur;
-  JY_TRY(jy_scratch(eng, 13, 2 * nshards * 8, &cur));
-  JY_HIP(eng, hipMemcpyAsync(cur, dinit, 2 * nshards * 8, hipMemcpyDeviceToDevice, eng->stream));
-  hipLaunchKernelGGL(k_route_scatter_treg, dim3(blocks_for(n)), dim3(kThreads), 0, eng->stream,
+  hipLaunchKernelGGL(k_route_part_treg, dim3(blocks_for(n)), dim3(kThreads), 0, eng->stream,
                      static_cast<const u32*>(dow), static_cast<const u32*>(dsl), static_cast<const u64*>(dts),
                      static_cast<const u64*>(dpre), static_cast<const u64*>(dlr), eng->arena[JY_TREG].p, n, nshards,
-                     static_cast<unsigned long long*>(cur), static_cast<const u64*>(dbb), recs_dev, bytes_dev);
+                     cap, cap_byte, reinterpret_cast<unsigned long long*>(hdr_dev), recs_dev, bytes_dev, ovf_dev);
   JY_HIP(eng, hipGetLastError());
   return JY_OK;
 }
 
-int32_t jy_treg_converge_routed(jy_engine* eng, uint32_t nsrc, const uint64_t* rec_counts,
-                                const uint64_t* byte_counts, const uint64_t* recs_dev, const uint8_t* bytes_dev) {
+int32_t jy_treg_converge_routed(jy_engine* eng, uint32_t nsrc, uint64_t cap, uint64_t cap_byte,
+                                const uint64_t* recs_dev, const uint8_t* bytes_dev, const uint64_t* hdr_dev) {
   JY_HIP(eng, hipSetDevice(eng->device));
-  JyTimed tm(eng);
-  u64 total_bytes = 0;
-  for (u32 s = 0; s < nsrc; s++) total_bytes += byte_counts[s];
+  if (nsrc == 0 || cap == 0) return JY_OK;
+  // the sources' byte runs go to the arena whole (nsrc x cap_byte); the
+  // records address them relative to their run
+  const u64 total_bytes = (u64)nsrc * cap_byte;
   Arena& a = eng->arena[JY_TREG];
+  if ((a.len + total_bytes) >> (64 - JY_LR_LEN_BITS)) return eng->fail(JY_ERANGE, "arena offset overflow");
+  const u64 rebase = a.len;
   if (total_bytes) {
     if (a.len + total_bytes > a.cap) {
       u64 nc = std::max<u64>(std::max<u64>(a.cap * 2, a.len + total_bytes), 1 << 16);
@@ -245,17 +198,10 @@ int32_t jy_treg_converge_routed(jy_engine* eng, uint32_t nsrc, const uint64_t* r
       a.p = static_cast<uint8_t*>(p);
       a.cap = nc;
     }
-    if ((a.len + total_bytes) >> (64 - JY_LR_LEN_BITS)) return eng->fail(JY_ERANGE, "arena offset overflow");
     JY_HIP(eng, hipMemcpyAsync(a.p + a.len, bytes_dev, total_bytes, hipMemcpyDeviceToDevice, eng->stream));
+    a.len += total_bytes;
   }
-  u64 rec_off = 0, byte_off = a.len;
-  for (u32 s = 0; s < nsrc; s++) {
-    if (rec_counts[s]) JY_TRY(jy_treg_merge_records(eng, recs_dev + rec_off * 4, rec_counts[s], byte_off));
-    rec_off += rec_counts[s];
-    byte_off += byte_counts[s];
-  }
-  a.len += total_bytes;
-  return JY_OK;
+  return jy_treg_merge_routed(eng, nsrc, cap, cap_byte, recs_dev, hdr_dev, rebase);
 }
 
 }  // extern "C"

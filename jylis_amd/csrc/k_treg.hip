@@ -15,6 +15,14 @@
 // winner dirties one 8-B ts word and one 16-B handle instead of three
 // scattered 8-B words (DESIGN.md "TREG").
 //
+// A slot named twice in one launch (a device batch that breaks the
+// one-delta-per-key contract, or routed runs of two sources touching one
+// key) is resolved EXACTLY: the first entry of each slot (jy_claim_rows, one
+// bit per slot) is merged by the wide kernel, the others are appended to a
+// list that one wave folds in afterwards -- LWW is a join, so the fold order
+// does not change the result.  A batch in slot order costs the claim ~3
+// atomics per wave row.
+//
 // Roofline: HBM.  SURVEY 8d prices a key at 48 B (16 delta + 16 state read
 // + 16 state write).  What this kernel moves per delta entry: 28 B delta
 // (slot, ts, pre, lr; all coalesced, loaded up front with the state-ts
@@ -40,11 +48,56 @@ constexpr u64 kMallBytes = 256ull << 20;  // MI355X Infinity Cache (MALL)
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
+// kCoh: loads that bypass the CU's L1 (the one-wave duplicate fold reads
+// what other lanes of its wave stored a round earlier)
+template <bool kCoh>
+__device__ __forceinline__ u64 ld64(const u64* p) {
+  return kCoh ? __hip_atomic_load(const_cast<u64*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
+}
+
+template <bool kCoh = false>
 __device__ __forceinline__ bool lww_wins(u64 t, u64 t0, u64 p, u64 l, const TVal* __restrict__ val, u64 s,
                                          const uint8_t* __restrict__ arena) {
   if (t != t0) return t > t0;
-  const TVal v0 = val[s];
-  return jy_value_cmp(p, l, v0.pre, v0.lr, arena) > 0;
+  const u64 pre0 = ld64<kCoh>(&val[s].pre), lr0 = ld64<kCoh>(&val[s].lr);
+  return jy_value_cmp(p, l, pre0, lr0, arena) > 0;
+}
+
+// state + (SET path) pending-delta registers + the launch's claim state
+struct TregK {
+  u64* ts;
+  TVal* val;
+  const uint8_t* arena;
+  u32* seen;     // claim bitmap; seen[seen_words] = duplicate count
+  u32* dupn;
+  u32* duplist;  // entry indices of the non-first entries
+  // RepoTREG._deltas (SET path only)
+  u64* pts;
+  TVal* pval;
+  u32* pflag;
+  u64* pcount;
+};
+
+// SET semantics of one entry whose slot nobody else touches right now:
+// TReg.update(v, t, delta) (repo_treg.pony:65-68) changes the state and
+// records the write in the key's pending delta only if it wins against the
+// state; the delta key exists either way (oracle/jy_oracle.cpp or_treg_set)
+template <bool kCoh = false>
+__device__ __forceinline__ void set_one(const TregK& K, u32 s, u64 t, u64 p, u64 l) {
+  if (atomicOr(K.pflag + s, 1u) == 0u) atomicAdd(K.pcount, 1ull);
+  const u64 t0 = ld64<kCoh>(K.ts + s);
+  if (t < t0 || !lww_wins<kCoh>(t, t0, p, l, K.val, s, K.arena)) return;
+  K.ts[s] = t;
+  K.val[s] = TVal{p, l};
+  const u64 d0 = ld64<kCoh>(K.pts + s);
+  if (t < d0 || !lww_wins<kCoh>(t, d0, p, l, K.pval, s, K.arena)) return;
+  K.pts[s] = t;
+  K.pval[s] = TVal{p, l};
+}
+
+__device__ __forceinline__ void push_dup(const TregK& K, u64 i) {
+  const u32 at = atomicAdd(K.dupn, 1u);
+  K.duplist[at] = (u32)i;
 }
 
 // kRewriteAll = false: every key rewrites its ts word (a loser writes back
@@ -56,74 +109,175 @@ __device__ __forceinline__ bool lww_wins(u64 t, u64 t0, u64 p, u64 l, const TVal
 //   256 MiB MALL the explicit rewrite is cheaper (64M keys: 0.84 vs 0.96 ms),
 //   while a cache-resident state prefers the leaner form (8M keys: 84 vs
 //   94 us).  jy_treg_merge picks by state size.
-// Both need one entry per slot per launch (the C ABI's contract; host
-// batches that repeat a key are split into rounds).
-template <bool kRewriteAll>
-__global__ __launch_bounds__(kThreads) void k_treg_lww(u64* __restrict__ ts, TVal* __restrict__ val,
-                                                       const uint8_t* __restrict__ arena,
-                                                       const u32* __restrict__ slot, const u64* __restrict__ dts,
-                                                       const u64* __restrict__ dpre, const u64* __restrict__ dlr,
-                                                       u64 n) {
+// kSet: local SETs (RepoTREG.set): the pending delta is updated with the
+//   state (set_one); the wide form is used for cache-friendly batches.
+template <bool kRewriteAll, bool kSet>
+__global__ __launch_bounds__(kThreads) void k_treg_lww(TregK K, const u32* __restrict__ slot,
+                                                       const u64* __restrict__ dts, const u64* __restrict__ dpre,
+                                                       const u64* __restrict__ dlr, u64 n) {
   const u64 base = (u64)blockIdx.x * (kThreads * kUnroll) + threadIdx.x;
   u32 s[kUnroll];
   u64 t[kUnroll], t0[kUnroll], p[kUnroll], l[kUnroll];
+  bool valid[kUnroll], first[kUnroll];
 #pragma unroll
   for (int u = 0; u < kUnroll; u++) {
     const u64 i = base + (u64)u * kThreads;
-    if (i < n) {
+    valid[u] = i < n;
+    s[u] = 0;
+    if (valid[u]) {
       s[u] = __builtin_nontemporal_load(slot + i);
       t[u] = __builtin_nontemporal_load(dts + i);
       p[u] = __builtin_nontemporal_load(dpre + i);
       l[u] = __builtin_nontemporal_load(dlr + i);
     }
   }
+  if (!kSet) {
 #pragma unroll
-  for (int u = 0; u < kUnroll; u++)
-    if (base + (u64)u * kThreads < n) t0[u] = ts[s[u]];
+    for (int u = 0; u < kUnroll; u++)
+      if (valid[u]) t0[u] = K.ts[s[u]];
+  }
+  jy_claim_rows<kUnroll>(valid, s, K.seen, first);
 #pragma unroll
   for (int u = 0; u < kUnroll; u++) {
     const u64 i = base + (u64)u * kThreads;
-    if (i >= n) continue;
-    const bool w = t[u] >= t0[u] && lww_wins(t[u], t0[u], p[u], l[u], val, s[u], arena);
-    ts[s[u]] = w ? t[u] : t0[u];
+    if (!valid[u]) continue;
+    if (!first[u]) {
+      push_dup(K, i);
+      continue;
+    }
+    if (kSet) {
+      set_one(K, s[u], t[u], p[u], l[u]);
+      continue;
+    }
+    const bool w = t[u] >= t0[u] && lww_wins(t[u], t0[u], p[u], l[u], K.val, s[u], K.arena);
+    K.ts[s[u]] = w ? t[u] : t0[u];
     if (kRewriteAll) {
-      const TVal old = w ? TVal{0, 0} : val[s[u]];
-      val[s[u]] = w ? TVal{p[u], l[u]} : old;
+      const TVal old = w ? TVal{0, 0} : K.val[s[u]];
+      K.val[s[u]] = w ? TVal{p[u], l[u]} : old;
     } else if (w) {
-      val[s[u]] = TVal{p[u], l[u]};
+      K.val[s[u]] = TVal{p[u], l[u]};
     }
   }
 }
 
-// receiver side of routing: one 32-B record (slot, ts, pre, lr) per entry,
-// long values rebased onto the arena region this run's bytes went to
-__global__ __launch_bounds__(kThreads) void k_treg_lww_records(u64* __restrict__ ts, TVal* __restrict__ val,
-                                                               const uint8_t* __restrict__ arena,
-                                                               const u64* __restrict__ recs, u64 n, u64 rebase) {
+// Routed runs (receiver side of the exchange, k_route.hip): S source runs
+// of 32-B records {slot on this owner, ts, pre, lr'} at recs[src * cap ..],
+// each holding hdr[2 * src] records (counts travel with the data: no host
+// round trip).  A hole (slot ~0) is a record whose value bytes overflowed
+// the sender's byte run; a slot this shard never handed out is counted as
+// skipped.  lr' offsets are relative to the source's byte run, which sits at
+// arena offset rebase + src * cap_byte.
+struct RoutedIn {
+  const u64* recs;
+  const u64* hdr;
+  u32 S;
+  u64 cap, cap_byte, rebase, nslots;
+  unsigned long long* skipped;
+};
+
+__device__ __forceinline__ bool routed_get(const RoutedIn& R, u64 i, u32& s, u64& t, u64& p, u64& l) {
+  const u64 src = i / R.cap, j = i - src * R.cap;
+  const u64 cnt = R.hdr[2 * src];
+  if (j >= (cnt < R.cap ? cnt : R.cap)) return false;
+  const u64x2 a = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(R.recs + i * 4));
+  const u64x2 b = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(R.recs + i * 4) + 1);
+  if (a.x == ~0ull) return false;  // hole
+  if (a.x >= R.nslots) {
+    atomicAdd(R.skipped, 1ull);
+    return false;
+  }
+  s = (u32)a.x;
+  t = a.y;
+  p = b.x;
+  l = b.y;
+  if ((l & JY_LR_LEN_MASK) > 8)
+    l = (((l >> JY_LR_LEN_BITS) + R.rebase + src * R.cap_byte) << JY_LR_LEN_BITS) | (l & JY_LR_LEN_MASK);
+  return true;
+}
+
+__global__ __launch_bounds__(kThreads) void k_treg_lww_routed(TregK K, RoutedIn R) {
   constexpr int U = 2;
   const u64 base = (u64)blockIdx.x * (kThreads * U) + threadIdx.x;
-  u64x2 a[U], b[U];
-  u64 t0[U];
+  const u64 n = (u64)R.S * R.cap;
+  u32 s[U];
+  u64 t[U], p[U], l[U], t0[U];
+  bool valid[U], first[U];
 #pragma unroll
   for (int u = 0; u < U; u++) {
     const u64 i = base + (u64)u * kThreads;
-    if (i < n) {
-      a[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(recs + i * 4));
-      b[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(recs + i * 4) + 1);
-    }
+    s[u] = 0;
+    valid[u] = i < n && routed_get(R, i, s[u], t[u], p[u], l[u]);
   }
 #pragma unroll
   for (int u = 0; u < U; u++)
-    if (base + (u64)u * kThreads < n) t0[u] = ts[a[u].x];
+    if (valid[u]) t0[u] = K.ts[s[u]];
+  jy_claim_rows<U>(valid, s, K.seen, first);
 #pragma unroll
   for (int u = 0; u < U; u++) {
-    if (base + (u64)u * kThreads >= n) continue;
-    const u64 s = a[u].x, t = a[u].y, p = b[u].x;
-    u64 l = b[u].y;
-    if ((l & JY_LR_LEN_MASK) > 8) l = (((l >> JY_LR_LEN_BITS) + rebase) << JY_LR_LEN_BITS) | (l & JY_LR_LEN_MASK);
-    if (t >= t0[u] && lww_wins(t, t0[u], p, l, val, s, arena)) {
-      ts[s] = t;
-      val[s] = TVal{p, l};
+    if (!valid[u]) continue;
+    if (!first[u]) {
+      push_dup(K, base + (u64)u * kThreads);
+      continue;
+    }
+    if (t[u] >= t0[u] && lww_wins(t[u], t0[u], p[u], l[u], K.val, s[u], K.arena)) {
+      K.ts[s[u]] = t[u];
+      K.val[s[u]] = TVal{p[u], l[u]};
+    }
+  }
+}
+
+// The non-first entries of a launch, folded in by ONE wave after it: a chunk
+// of 64 entries per pass (lane = entry); entries of one slot inside a chunk
+// run in rounds by their rank among the chunk's entries of that slot, so no
+// two lanes touch a slot at once and chunks run in list order.
+struct SoaIn {
+  const u32* slot;
+  const u64* ts;
+  const u64* pre;
+  const u64* lr;
+};
+__device__ __forceinline__ bool dup_get(const SoaIn& A, u64 i, u32& s, u64& t, u64& p, u64& l) {
+  s = A.slot[i];
+  t = A.ts[i];
+  p = A.pre[i];
+  l = A.lr[i];
+  return true;
+}
+__device__ __forceinline__ bool dup_get(const RoutedIn& R, u64 i, u32& s, u64& t, u64& p, u64& l) {
+  return routed_get(R, i, s, t, p, l);
+}
+
+template <bool kSet, typename In>
+__global__ __launch_bounds__(64) void k_treg_dups(TregK K, In in) {
+  const u32 n = *K.dupn;
+  const int lane = threadIdx.x;
+  for (u32 j0 = 0; j0 < n; j0 += 64) {
+    const u32 j = j0 + lane;
+    u32 s = 0xFFFFFFFFu;
+    u64 t = 0, p = 0, l = 0;
+    bool live = j < n && dup_get(in, K.duplist[j], s, t, p, l);
+    if (!live) s = 0xFFFFFFFFu;
+    u32 rank = 0;
+    for (int k = 0; k < 64; k++) {
+      const u32 sk = __shfl(s, k);
+      if (k < lane && sk == s) rank++;
+    }
+    u32 rounds = live ? rank + 1 : 0;
+    for (int o = 32; o > 0; o >>= 1) rounds = max(rounds, (u32)__shfl_xor(rounds, o));
+    for (u32 r = 0; r < rounds; r++) {
+      if (live && rank == r) {
+        if (kSet) {
+          set_one<true>(K, s, t, p, l);
+        } else {
+          const u64 t0 = ld64<true>(K.ts + s);
+          if (t >= t0 && lww_wins<true>(t, t0, p, l, K.val, s, K.arena)) {
+            K.ts[s] = t;
+            K.val[s] = TVal{p, l};
+          }
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0);  // this round's stores land before the next round reads
+      __syncthreads();
     }
   }
 }
@@ -138,32 +292,6 @@ __global__ __launch_bounds__(kThreads) void k_treg_gather(const u64* __restrict_
   ots[i] = ts[s];
   opre[i] = v.pre;
   olr[i] = v.lr;
-}
-
-// ---- local SET (RepoTREG.set repo_treg.pony:65-68): TReg.update(v, t, delta)
-// changes the state and records the write in the key's pending delta only if
-// it wins against the state; the delta key exists either way
-// (oracle/jy_oracle.cpp or_treg_set).  Run BEFORE the state merge of the same
-// batch (one entry per key): an entry that beats the state as it was is
-// LWW-merged into the pending delta, which equals the reference's sequence.
-__global__ __launch_bounds__(kThreads) void k_treg_set_pending(const u64* __restrict__ ts, const TVal* __restrict__ val,
-                                                               u64* __restrict__ dts, TVal* __restrict__ dval,
-                                                               u32* __restrict__ dflag, u64* __restrict__ dcount,
-                                                               const uint8_t* __restrict__ arena,
-                                                               const u32* __restrict__ slot,
-                                                               const u64* __restrict__ t, const u64* __restrict__ p,
-                                                               const u64* __restrict__ l, u64 n) {
-  const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= n) return;
-  const u32 s = slot[i];
-  const u64 ti = t[i], pi = p[i], li = l[i];
-  if (atomicOr(dflag + s, 1u) == 0u) atomicAdd(dcount, 1ull);
-  const u64 t0 = ts[s];
-  if (ti < t0 || !lww_wins(ti, t0, pi, li, val, s, arena)) return;
-  const u64 d0 = dts[s];
-  if (ti < d0 || !lww_wins(ti, d0, pi, li, dval, s, arena)) return;
-  dts[s] = ti;
-  dval[s] = TVal{pi, li};
 }
 
 struct TregPendingPred {
@@ -191,6 +319,27 @@ __global__ __launch_bounds__(kThreads) void k_treg_flush(u32* __restrict__ dflag
 
 u32 blocks(u64 n, u64 per) { return (u32)std::max<u64>(1, (n + per - 1) / per); }
 
+// claim state of one launch over `n` entries: the bitmap (zero), the
+// duplicate counter (zero) and a duplicate list of n entries
+int32_t claim_begin(jy_engine* eng, u64 n, TregK& K) {
+  TregState& t = eng->treg;
+  K.ts = t.ts;
+  K.val = t.val;
+  K.arena = eng->arena[JY_TREG].p;
+  K.seen = t.seen;
+  K.dupn = t.seen + t.seen_words;
+  void* p;
+  JY_TRY(jy_scratch(eng, 23, std::max<u64>(n, 1) * 4, &p));
+  K.duplist = static_cast<u32*>(p);
+  return JY_OK;
+}
+// the bitmap and the counter go back to zero for the next launch
+int32_t claim_end(jy_engine* eng) {
+  TregState& t = eng->treg;
+  JY_HIP(eng, hipMemsetAsync(t.seen, 0, (t.seen_words + 1) * 4, eng->stream));
+  return JY_OK;
+}
+
 }  // namespace
 
 int32_t jy_treg_grow(jy_engine* eng, u64 need) {
@@ -204,6 +353,13 @@ int32_t jy_treg_grow(jy_engine* eng, u64 need) {
   t.ts = static_cast<u64*>(a);
   t.val = static_cast<TVal*>(b);
   t.kcap = nk;
+  // claim bitmap: one bit per slot + the duplicate counter, all zero
+  jy_dev_free(eng, t.seen);
+  t.seen_words = (nk + 31) / 32;
+  void* sp = nullptr;
+  JY_TRY(jy_dev_alloc(eng, &sp, (t.seen_words + 16) * 4, "treg claim bitmap"));
+  t.seen = static_cast<u32*>(sp);
+  JY_HIP(eng, hipMemsetAsync(t.seen, 0, (t.seen_words + 16) * 4, eng->stream));
   return JY_OK;
 }
 
@@ -211,26 +367,36 @@ int32_t jy_treg_merge(jy_engine* eng, u64 n, const u32* slot, const u64* ts, con
   if (n == 0) return JY_OK;
   TregState& t = eng->treg;
   JyTimed tm(eng);
-  // state larger than the Infinity Cache: write whole lines (see k_treg_lww)
-  const bool whole = t.kcap * (8 + sizeof(TVal)) > kMallBytes;
+  TregK K{};
+  JY_TRY(claim_begin(eng, n, K));
+  // state larger than the Infinity Cache: write whole lines (see k_treg_lww);
+  // config flag JY_CFG_TREG_WHOLE_LINES forces that form (tests)
+  const bool whole =
+      t.kcap * (8 + sizeof(TVal)) > kMallBytes || (eng->cfg.flags & JY_CFG_TREG_WHOLE_LINES) != 0;
   if (whole)
-    hipLaunchKernelGGL(k_treg_lww<true>, dim3(blocks(n, kThreads * kUnroll)), dim3(kThreads), 0, eng->stream, t.ts,
-                       t.val, eng->arena[JY_TREG].p, slot, ts, pre, lr, n);
+    hipLaunchKernelGGL((k_treg_lww<true, false>), dim3(blocks(n, kThreads * kUnroll)), dim3(kThreads), 0,
+                       eng->stream, K, slot, ts, pre, lr, n);
   else
-    hipLaunchKernelGGL(k_treg_lww<false>, dim3(blocks(n, kThreads * kUnroll)), dim3(kThreads), 0, eng->stream,
-                       t.ts, t.val, eng->arena[JY_TREG].p, slot, ts, pre, lr, n);
+    hipLaunchKernelGGL((k_treg_lww<false, false>), dim3(blocks(n, kThreads * kUnroll)), dim3(kThreads), 0,
+                       eng->stream, K, slot, ts, pre, lr, n);
+  hipLaunchKernelGGL((k_treg_dups<false, SoaIn>), dim3(1), dim3(64), 0, eng->stream, K, SoaIn{slot, ts, pre, lr});
   JY_HIP(eng, hipGetLastError());
-  return JY_OK;
+  return claim_end(eng);
 }
 
-int32_t jy_treg_merge_records(jy_engine* eng, const u64* recs, u64 n, u64 base) {
+int32_t jy_treg_merge_routed(jy_engine* eng, u32 S, u64 cap, u64 cap_byte, const u64* recs, const u64* hdr,
+                             u64 rebase) {
+  const u64 n = (u64)S * cap;
   if (n == 0) return JY_OK;
-  TregState& t = eng->treg;
   JyTimed tm(eng);
-  hipLaunchKernelGGL(k_treg_lww_records, dim3(blocks(n, kThreads * 2)), dim3(kThreads), 0, eng->stream, t.ts, t.val,
-                     eng->arena[JY_TREG].p, recs, n, base);
+  TregK K{};
+  JY_TRY(claim_begin(eng, n, K));
+  RoutedIn R{recs, hdr, S, cap, cap_byte, rebase, eng->nkeys[JY_TREG],
+             reinterpret_cast<unsigned long long*>(eng->skipped_dev)};
+  hipLaunchKernelGGL(k_treg_lww_routed, dim3(blocks(n, kThreads * 2)), dim3(kThreads), 0, eng->stream, K, R);
+  hipLaunchKernelGGL((k_treg_dups<false, RoutedIn>), dim3(1), dim3(64), 0, eng->stream, K, R);
   JY_HIP(eng, hipGetLastError());
-  return JY_OK;
+  return claim_end(eng);
 }
 
 int32_t jy_treg_gather(jy_engine* eng, u64 n, const u32* slots, u64* ots, u64* opre, u64* olr) {
@@ -262,15 +428,25 @@ static int32_t treg_delta_grow(jy_engine* eng) {
   return JY_OK;
 }
 
-int32_t jy_treg_set_pending(jy_engine* eng, u64 n, const u32* slot, const u64* ts, const u64* pre, const u64* lr) {
+// local SET batch (RepoTREG.set repo_treg.pony:65-68): every entry updates
+// the state and, if it wins there, the key's pending delta; repeated keys are
+// exact (the first entry of a slot in the wide kernel, the rest folded after)
+int32_t jy_treg_set_batch(jy_engine* eng, u64 n, const u32* slot, const u64* ts, const u64* pre, const u64* lr) {
   if (n == 0) return JY_OK;
   TregState& t = eng->treg;
   JY_TRY(treg_delta_grow(eng));
-  hipLaunchKernelGGL(k_treg_set_pending, dim3(blocks(n, kThreads)), dim3(kThreads), 0, eng->stream,
-                     (const u64*)t.ts, (const TVal*)t.val, t.dts, t.dval, t.dflag, t.dcount,
-                     eng->arena[JY_TREG].p, slot, ts, pre, lr, n);
+  JyTimed tm(eng);
+  TregK K{};
+  JY_TRY(claim_begin(eng, n, K));
+  K.pts = t.dts;
+  K.pval = t.dval;
+  K.pflag = t.dflag;
+  K.pcount = t.dcount;
+  hipLaunchKernelGGL((k_treg_lww<false, true>), dim3(blocks(n, kThreads * kUnroll)), dim3(kThreads), 0, eng->stream,
+                     K, slot, ts, pre, lr, n);
+  hipLaunchKernelGGL((k_treg_dups<true, SoaIn>), dim3(1), dim3(64), 0, eng->stream, K, SoaIn{slot, ts, pre, lr});
   JY_HIP(eng, hipGetLastError());
-  return JY_OK;
+  return claim_end(eng);
 }
 
 int32_t jy_treg_pending(jy_engine* eng, u64* count) {

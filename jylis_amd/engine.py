@@ -72,13 +72,14 @@ class Engine:
     """One engine = one GPU = one key shard."""
 
     def __init__(self, device=0, counter_columns=16, ujson_columns=16, key_capacity=1024,
-                 entry_capacity=8192, arena_capacity=1 << 16):
+                 entry_capacity=8192, arena_capacity=1 << 16, flags=0):
         self.lib = _lib.load()
         cfg = _lib.JyConfig()
         self.lib.jy_config_default(C.byref(cfg))
         cfg.device = device
         cfg.counter_columns = counter_columns
         cfg.ujson_columns = ujson_columns
+        cfg.flags = flags
         for t in range(5):
             cfg.key_capacity[t] = key_capacity if np.isscalar(key_capacity) else key_capacity[t]
             cfg.entry_capacity[t] = entry_capacity

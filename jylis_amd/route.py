@@ -6,19 +6,34 @@ shards that own its keys.  The reference has no counterpart (every Jylis node
 holds every key); this is the intra-node analogue of Cluster.broadcast_deltas
 (jylis/cluster.pony:209-213).
 
-Control plane (host, gloo): a key's slot lives on its owner.  The first time
-a rank ingests a key owned elsewhere, it sends the key bytes to the owner,
-which interns it and answers with the slot (`ShardRouter.resolve`); the
-answer is cached.  Data plane (device, RCCL over xGMI): records and long
-value bytes move with two all_to_all_single calls per batch.
+Control plane (host): a key's slot lives on its owner.  The first time a rank
+ingests a key owned elsewhere, it sends the key bytes to the owner, which
+interns it and answers with the slot (`ShardRouter.resolve`); the answer is
+cached.
 
-Everything here runs in every rank (collective calls).
+Data plane (device): runs of a FIXED capacity per destination, so every
+all-to-all is an equal-split collective (RCCL over xGMI) and the per-run
+counts travel as a small device header beside the data -- the host never
+reads a count back per batch.  What does not fit a run (a skewed batch) is
+listed on the device and sent in a drain round, decided one step later from
+an asynchronously read global maximum, so no step waits for the GPU.
+
+`Fabric` is the medium: `DistFabric` (one rank per process: RCCL for CUDA
+tensors, or gloo through host memory) or `LocalFabric` (S engines in one
+process, for single-GPU tests).  Routers take lists of per-rank engines and
+batches: one per process with a DistFabric, S with a LocalFabric.
 """
 import ctypes as C
 
 import numpy as np
 
 from . import _lib
+
+# run capacity: the expected share of a balanced hash partition plus slack
+CAP_SLACK = 1.125
+CAP_MARGIN = 256
+BYTE_SLACK = 1.25
+BYTE_MARGIN = 4096
 
 
 def owners(kb, ko, nshards):
@@ -31,8 +46,310 @@ def owners(kb, ko, nshards):
     return out
 
 
+def run_caps(n_max, bytes_max, world):
+    """(records, value bytes) per destination run for batches of at most
+    n_max entries / bytes_max long-value bytes per rank"""
+    if world == 1:
+        return max(n_max, 1), max(bytes_max, 1)
+    cap = min(max(n_max, 1), int(np.ceil(n_max / world * CAP_SLACK)) + CAP_MARGIN)
+    capb = min(max(bytes_max, 1), int(np.ceil(bytes_max / world * BYTE_SLACK)) + BYTE_MARGIN)
+    return cap, capb
+
+
+# ---- fabrics ------------------------------------------------------------------
+
+class _Done:
+    def wait(self):
+        pass
+
+
+class LocalFabric:
+    """S shards hosted by one process (tests on one GPU): the all-to-all is a
+    set of device copies on the current stream."""
+
+    def __init__(self, world):
+        self.world = world
+        self.ranks = list(range(world))
+
+    def a2a(self, outs, ins, async_op=False):
+        S = self.world
+        for r in range(S):
+            cr = outs[r].numel() // S
+            for s in range(S):
+                cs = ins[s].numel() // S
+                assert cs == cr, "equal-split all-to-all: every rank sends the same chunk size"
+                outs[r].view(-1)[s * cr:(s + 1) * cr].copy_(ins[s].view(-1)[r * cs:(r + 1) * cs])
+        return _Done()
+
+    def max_all(self, ts):
+        """in place: every tensor becomes the max over ranks"""
+        import torch
+        m = torch.stack([t.view(-1) for t in ts]).max(0).values
+        for t in ts:
+            t.view(-1).copy_(m)
+        return _Done()
+
+    def host_max(self, vals):
+        m = np.max(np.asarray(vals, np.int64), axis=0)
+        return [m.copy() for _ in vals]
+
+
+class DistFabric:
+    """One rank per process over torch.distributed.  With the nccl backend
+    (RCCL on ROCm) CUDA tensors move GPU to GPU over xGMI; with gloo they go
+    through host memory (multi-process tests on one GPU).  `cpu_group` (gloo)
+    carries the host-side control values."""
+
+    def __init__(self, dist, group=None, cpu_group=None):
+        self.dist = dist
+        self.group = group
+        self.cpu_group = cpu_group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.ranks = [self.rank]
+        self.staged = dist.get_backend(group) == "gloo"
+
+    def a2a(self, outs, ins, async_op=False):
+        (out,), (inp,) = outs, ins
+        if self.staged:
+            o = out.view(-1).cpu()
+            self.dist.all_to_all_single(o, inp.view(-1).cpu(), group=self.group)
+            out.view(-1).copy_(o)
+            return _Done()
+        w = self.dist.all_to_all_single(out.view(-1), inp.view(-1), group=self.group, async_op=async_op)
+        return w if async_op else _Done()
+
+    def max_all(self, ts):
+        (t,) = ts
+        if self.staged:
+            c = t.cpu()
+            self.dist.all_reduce(c, op=self.dist.ReduceOp.MAX, group=self.group)
+            t.copy_(c)
+            return _Done()
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+        return _Done()
+
+    def host_max(self, vals):
+        import torch
+        (v,) = vals
+        t = torch.tensor(np.asarray(v, np.int64))
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.cpu_group)
+        return [t.numpy()]
+
+
+def _bind_streams(engines):
+    """every engine enqueues on torch's current stream of its device, so the
+    collectives (issued by torch against that stream) and the engine's
+    launches are ordered, and tensors the caching allocator recycles are
+    stream-ordered with the engine's reads of them.  The engine cannot name
+    the legacy default stream (NULL selects its own stream), so a router
+    bound while torch is on the default stream moves torch to a new stream."""
+    import torch
+    for e in engines:
+        dev = torch.device("cuda", e.device)
+        if torch.cuda.current_stream(dev).cuda_stream == 0:
+            torch.cuda.synchronize(dev)
+            torch.cuda.set_stream(torch.cuda.Stream(dev))
+        cur = torch.cuda.current_stream(dev).cuda_stream
+        if e.stream() != cur:
+            e.set_stream(cur)
+
+
+def _check_streams(engines):
+    import torch
+    for e in engines:
+        if e.stream() != torch.cuda.current_stream(e.device).cuda_stream:
+            raise RuntimeError("the engine stream is not torch's current stream: call router.bind() after "
+                               "switching streams")
+
+
+# ---- TREG ---------------------------------------------------------------------
+
+class TregRouter:
+    """Routes TREG delta batches between the shards of one node.
+
+    `step(batches)`: batches[i] = (owner, slot, ts, pre, lr, long_bytes) for
+    local rank i (CUDA tensors; owner/slot int32, the rest int64 bits;
+    long_bytes = total bytes of its values longer than 8 bytes, a host int).
+    Partition -> header + records + bytes all-to-all -> one merge of every
+    received run.  Entries that overflowed a run are sent by a drain round
+    at the next step (or `drain()`), decided from a global maximum read back
+    without stalling the GPU."""
+
+    def __init__(self, engines, fabric):
+        self.engs = list(engines)
+        self.fabric = fabric
+        self.S = fabric.world
+        assert len(self.engs) == len(fabric.ranks)
+        self.pending = None  # (batches, ovf tensors, pinned global max, event)
+        self.routed = 0
+        self.drains = 0
+        self.bind()
+
+    def bind(self):
+        _bind_streams(self.engs)
+
+    def step(self, batches):
+        _check_streams(self.engs)
+        self._settle(wait=True)
+        ovfs = self._round(batches)
+        self._publish(batches, ovfs)
+
+    def drain(self):
+        """route everything still pending (a collective: every rank calls it)"""
+        _check_streams(self.engs)
+        while self.pending is not None:
+            self._settle(wait=True)
+
+    # one exchange round over the given per-rank batches
+    def _round(self, batches, caps=None):
+        import torch
+        S, fab = self.S, self.fabric
+        if caps is None:
+            nb = [np.array([int(b[0].numel()), int(b[5])], np.int64) for b in batches]
+            m = fab.host_max(nb)[0]
+            caps = run_caps(int(m[0]), int(m[1]), S)
+        cap, capb = caps
+        sends, ovfs = [], []
+        for eng, b in zip(self.engs, batches):
+            own, slot, ts, pre, lr = b[:5]
+            n = int(own.numel())
+            dev = torch.device("cuda", eng.device)
+            recs = torch.empty((S * cap, 4), dtype=torch.int64, device=dev)
+            byts = torch.empty(S * capb, dtype=torch.uint8, device=dev)
+            hdr = torch.zeros((S, 2), dtype=torch.int64, device=dev)
+            ovf = torch.zeros(n + 1, dtype=torch.int32, device=dev)
+            if n:
+                for t in (own, slot, ts, pre, lr):
+                    assert t.is_cuda and t.is_contiguous() and t.numel() == n
+                eng._check(eng.lib.jy_treg_route_part(
+                    eng.h, n, own.data_ptr(), slot.data_ptr(), ts.data_ptr(), pre.data_ptr(), lr.data_ptr(), S, cap,
+                    capb, _lib.DEVICE, C.c_void_p(recs.data_ptr()), C.c_void_p(byts.data_ptr()),
+                    C.c_void_p(hdr.data_ptr()), C.c_void_p(ovf.data_ptr())))
+            sends.append((recs, byts, hdr))
+            ovfs.append(ovf)
+        if S == 1:
+            recvs = sends
+        else:
+            recvs = [tuple(torch.empty_like(x) for x in snd) for snd in sends]
+            for k in (2, 0, 1):  # header, records, bytes
+                fab.a2a([r[k] for r in recvs], [s[k] for s in sends])
+        for eng, (recs, byts, hdr) in zip(self.engs, recvs):
+            eng._check(eng.lib.jy_treg_converge_routed(eng.h, S, cap, capb, C.c_void_p(recs.data_ptr()),
+                                                       C.c_void_p(byts.data_ptr()), C.c_void_p(hdr.data_ptr())))
+        self.routed += 1
+        return ovfs
+
+    def _publish(self, batches, ovfs):
+        """global max of the overflow counts, copied to pinned memory behind an event"""
+        import torch
+        gm = [o[:1].clone() for o in ovfs]
+        self.fabric.max_all(gm)
+        pins = []
+        for eng, g, o in zip(self.engs, gm, ovfs):
+            p = torch.empty(2, dtype=torch.int32, pin_memory=True)
+            p[0:1].copy_(g, non_blocking=True)
+            p[1:2].copy_(o[:1], non_blocking=True)
+            pins.append(p)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.pending = (batches, ovfs, pins, ev)
+
+    def _settle(self, wait):
+        """check the last round's overflow; run a drain round if any rank overflowed"""
+        if self.pending is None:
+            return
+        batches, ovfs, pins, ev = self.pending
+        if not wait and not ev.query():
+            return
+        ev.synchronize()
+        self.pending = None
+        gmax = int(pins[0][0])
+        if gmax == 0:
+            return
+        import torch
+        sub = []
+        for b, o, p in zip(batches, ovfs, pins):
+            k = int(p[1])
+            idx = o[1:1 + k].long()
+            own, slot, ts, pre, lr = (t.index_select(0, idx) for t in b[:5])
+            lens = lr & ((1 << 24) - 1)
+            nbytes = int(torch.where(lens > 8, lens, torch.zeros_like(lens)).sum())
+            sub.append((own.contiguous(), slot.contiguous(), ts.contiguous(), pre.contiguous(), lr.contiguous(),
+                        nbytes))
+        m = self.fabric.host_max([np.array([int(s[0].numel()), int(s[5])], np.int64) for s in sub])[0]
+        # capacity = the whole overflow of the largest sender: nothing can overflow again
+        ovfs2 = self._round(sub, caps=(max(int(m[0]), 1), max(int(m[1]), 1)))
+        self.drains += 1
+        self._publish(sub, ovfs2)
+
+
+# ---- counters (dense column blocks) --------------------------------------------
+
+class CounterRouter:
+    """Routes dense GCOUNT / PNCOUNT peer batches between the shards of a node.
+
+    A peer replica that runs the same sharding flushes shard by shard, so
+    its batch for one replica column arrives grouped by owner: K slots for
+    owner 0, then owner 1, ... (each owner's run in that owner's slot
+    order).  Rank r ingests C peer columns: `ingest` is an int64 CUDA tensor
+    [nsigns][C][S][K] and `cols[r]` the engine columns of r's peers.  Chunk c
+    of the exchange moves column c of every rank to its owners (an
+    equal-split all-to-all); the owner merges the S received columns with one
+    block converge while chunk c + 1 is in flight (double-buffered)."""
+
+    def __init__(self, engines, fabric, ctype):
+        self.engs = list(engines)
+        self.fabric = fabric
+        self.S = fabric.world
+        self.ctype = ctype
+        self.bind()
+
+    def bind(self):
+        _bind_streams(self.engs)
+
+    def step(self, ingests, cols):
+        """ingests[i]: local rank i's [nsigns][C][S][K] batch; cols[r][c]: the
+        engine column of rank r's c-th peer (every rank knows every rank's)"""
+        import torch
+        _check_streams(self.engs)
+        S, fab = self.S, self.fabric
+        nsigns, Cn, S_, K = ingests[0].shape
+        assert S_ == S
+        merge = [self._merge_fn(e) for e in self.engs]
+        if S == 1:
+            for eng, m, ing in zip(self.engs, merge, ingests):
+                m(np.asarray(cols[0], np.uint16), ing[:, :, 0])
+            return
+        bufs = [[torch.empty((nsigns, S, K), dtype=torch.int64, device=ing.device) for _ in range(2)]
+                for ing in ingests]
+        works = [None, None]
+
+        def issue(c):
+            b = c & 1
+            works[b] = [fab.a2a([bf[b][g] for bf in bufs], [ing[g, c] for ing in ingests], async_op=True)
+                        for g in range(nsigns)]
+
+        issue(0)
+        for c in range(Cn):
+            for w in works[c & 1]:
+                w.wait()
+            if c + 1 < Cn:
+                issue(c + 1)
+            colc = np.array([cols[s][c] for s in range(S)], np.uint16)
+            for m, bf in zip(merge, bufs):
+                m(colc, bf[c & 1])
+
+    def _merge_fn(self, eng):
+        if self.ctype == _lib.PNCOUNT:
+            return lambda cols, v: eng.pncount_converge_block(cols, 0, v[0], v[1])
+        return lambda cols, v: eng.gcount_converge_block(cols, 0, v[0])
+
+
+# ---- control plane ----------------------------------------------------------------
+
 def _a2a_host(dist, group, send, send_counts):
-    """variable all-to-all of a 1-D int64 / uint8 numpy array over `group`"""
+    """variable all-to-all of a 1-D int64 / uint8 numpy array over `group` (host)"""
     import torch
     world = dist.get_world_size(group)
     sc = torch.tensor(np.asarray(send_counts, np.int64))
@@ -113,61 +430,3 @@ def _pick_keys(kb, ko, idx):
     total = int(offs[-1])
     pos = np.repeat(ko[idx].astype(np.int64) - offs[:-1].astype(np.int64), lens) + np.arange(total)
     return kb[pos], offs
-
-
-# ---- data plane -------------------------------------------------------------
-
-def partition_counts_np(owner, lr, world):
-    """records and long-value bytes per destination (numpy restatement of k_route_count)"""
-    lens = np.asarray(lr, np.uint64) & np.uint64((1 << 24) - 1)
-    rec = np.bincount(owner, minlength=world).astype(np.uint64)
-    byt = np.bincount(owner, weights=np.where(lens > 8, lens, 0).astype(np.float64), minlength=world)
-    return rec, byt.astype(np.uint64)
-
-
-class TregRouter:
-    """Routes TREG delta batches between the engines of one node (RCCL)."""
-
-    def __init__(self, eng, dist, group=None):
-        self.eng = eng
-        self.dist = dist
-        self.group = group
-        self.world = dist.get_world_size(group) if dist else 1
-
-    def exchange_and_converge(self, owner, slot, ts, pre, lr):
-        """one routed converge: partition -> all-to-all(v) -> converge each source run.
-        Arguments are CUDA tensors (or numpy) of one ingested batch; every rank calls."""
-        import torch
-        eng, S = self.eng, self.world
-        lib = eng.lib
-        from .engine import _arg, _same_mem
-        args = [_arg(owner, np.uint32), _arg(slot, np.uint32), _arg(ts, np.uint64), _arg(pre, np.uint64),
-                _arg(lr, np.uint64)]
-        mem = _same_mem(*[m for (_, _, m) in args])
-        n = len(args[0][0])
-        rc = np.zeros(S, np.uint64)
-        bc = np.zeros(S, np.uint64)
-        eng._check(lib.jy_treg_route_count(eng.h, n, args[0][1], args[4][1], S, mem, rc.ctypes.data, bc.ctypes.data))
-        dev = torch.device("cuda", eng.device)
-        recs = torch.empty((max(n, 1), 4), dtype=torch.int64, device=dev)
-        byts = torch.empty(max(int(bc.sum()), 1), dtype=torch.uint8, device=dev)
-        eng._check(lib.jy_treg_route_scatter(eng.h, n, args[0][1], args[1][1], args[2][1], args[3][1], args[4][1],
-                                             S, rc.ctypes.data, bc.ctypes.data, mem,
-                                             C.c_void_p(recs.data_ptr()), C.c_void_p(byts.data_ptr())))
-        if S > 1:
-            cnt = torch.tensor(np.concatenate([rc, bc]).astype(np.int64), device=dev).view(2, S).t().contiguous()
-            rcnt = torch.empty_like(cnt)
-            self.dist.all_to_all_single(rcnt, cnt, group=self.group)
-            rcnt = rcnt.cpu().numpy()
-            rrc, rbc = rcnt[:, 0].astype(np.uint64), rcnt[:, 1].astype(np.uint64)
-            rrecs = torch.empty((max(int(rrc.sum()), 1), 4), dtype=torch.int64, device=dev)
-            rbyts = torch.empty(max(int(rbc.sum()), 1), dtype=torch.uint8, device=dev)
-            self.dist.all_to_all_single(rrecs[:int(rrc.sum())], recs[:n], rrc.astype(np.int64).tolist(),
-                                        rc.astype(np.int64).tolist(), group=self.group)
-            self.dist.all_to_all_single(rbyts[:int(rbc.sum())], byts[:int(bc.sum())], rbc.astype(np.int64).tolist(),
-                                        bc.astype(np.int64).tolist(), group=self.group)
-        else:
-            rrc, rbc, rrecs, rbyts = rc, bc, recs, byts
-        eng._check(lib.jy_treg_converge_routed(eng.h, S, rrc.ctypes.data, rbc.ctypes.data,
-                                               C.c_void_p(rrecs.data_ptr()), C.c_void_p(rbyts.data_ptr())))
-        return int(rrc.sum())

@@ -85,3 +85,35 @@ def random_history(O, ctype, seed, nrep=4, nops=300, nkeys=12, val_len=14, gossi
         batches.append(r.flush().table())
         batches.append(r.state())  # full-state deltas too
     return batches
+
+
+def collect(procs, q, n, deadline_s=150.0):
+    """n messages from worker processes; fail fast on an ("error", rank,
+    traceback) message or a dead worker, and kill the rest (a rank stuck in
+    a collective its peer never joins would otherwise hang the test)"""
+    import queue
+    import time
+    msgs = []
+    t_end = time.time() + deadline_s
+    try:
+        while len(msgs) < n:
+            try:
+                m = q.get(timeout=2.0)
+            except queue.Empty:
+                dead = [p for p in procs if p.exitcode not in (None, 0)]
+                if dead:
+                    raise AssertionError(f"worker exited with {dead[0].exitcode} before sending its results")
+                if time.time() > t_end:
+                    raise AssertionError(f"timed out with {len(msgs)} of {n} messages")
+                continue
+            if m[0] == "error":
+                raise AssertionError(f"rank {m[1]} failed:\n{m[2]}")
+            msgs.append(m)
+    finally:
+        if len(msgs) < n:
+            for p in procs:
+                if p.is_alive():
+                    p.kill()
+        for p in procs:
+            p.join(timeout=30)
+    return msgs

@@ -1,88 +1,295 @@
-"""Routing kernels on the GPU (one process): the HIP partition's counts equal
-the numpy restatement, and converging the partitioned runs of a batch equals
-converging the batch directly (records and long-value bytes both travel)."""
+"""The routing data plane on the GPU: partition kernels, the fixed-capacity
+all-to-all and the routed merge, with S shards hosted in one process
+(route.LocalFabric: S engines on cuda:0, the all-to-all as device copies).
+
+After routing, the union of the shards must equal ONE oracle repo that
+converged every ingested batch (TREG: repo_treg.pony:51-52; counters:
+repo_pncount.pony:52-53) -- bit-exact, including overflowing runs (drain
+rounds), keys several sources send in the same step, and long values whose
+bytes travel in their own run."""
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 
-def _treg_batch(rng, n, keyspace):
+def _treg_batch(rng, n, keyspace, ts_hi=4):
     from jylis_amd.engine import encode_keys
     keys = [f"rk{int(x)}" for x in rng.choice(keyspace, n, replace=False)]
     vals = []
     for _ in keys:
         L = int(rng.integers(0, 24))
         vals.append(bytes(rng.integers(0, 256, L).astype(np.uint8)) if rng.random() < 0.7
-                    else b"shared-prefix" [:min(L, 13)] + bytes(rng.integers(97, 99, max(L - 13, 0)).astype(np.uint8)))
-    ts = rng.integers(0, 4, n).astype(np.uint64)
+                    else b"shared-prefix"[:min(L, 13)] + bytes(rng.integers(97, 99, max(L - 13, 0)).astype(np.uint8)))
+    ts = rng.integers(0, ts_hi, n).astype(np.uint64)
     kb, ko = encode_keys(keys)
     vb, vo = encode_keys(vals)
     return {"key_bytes": kb, "key_offs": ko, "ts": ts, "val_bytes": vb, "val_offs": vo}
 
 
-@pytest.mark.parametrize("S", [1, 3, 8])
-def test_partition_and_routed_converge(oracle_mod, engine, S):
-    import ctypes as C
+def _dev(a, dtype):
+    import torch
+    a = np.ascontiguousarray(a)
+    return torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a.view(np.int32)).to("cuda:0")
 
+
+class _Node:
+    """S engines on one GPU + per-shard slot directories (the control plane's
+    role: owner hash, owner-side interning)"""
+
+    def __init__(self, S):
+        from jylis_amd.engine import Engine
+        from jylis_amd.repo import RepoTREG
+        self.S = S
+        self.engs = [Engine(device=0) for _ in range(S)]
+        self.repos = [RepoTREG(e) for e in self.engs]
+
+    def close(self):
+        for e in self.engs:
+            e.close()
+
+    def ingest(self, rank, b):
+        """(owner, owner slot, ts, pre, lr, long bytes) of a batch landing on `rank`"""
+        from jylis_amd._lib import TREG
+        from jylis_amd.route import owners
+        own = owners(b["key_bytes"], b["key_offs"], self.S)
+        slot = np.zeros(len(own), np.uint32)
+        for d in range(self.S):
+            idx = np.nonzero(own == d)[0]
+            if len(idx):
+                from jylis_amd.route import _pick_keys
+                kb, ko = _pick_keys(np.asarray(b["key_bytes"], np.uint8), np.asarray(b["key_offs"], np.uint64), idx)
+                slot[idx] = self.repos[d]._intern({"key_bytes": kb, "key_offs": ko})
+        pre, lr = self.engs[rank].pack_values(TREG, (b["val_bytes"], b["val_offs"]))
+        lens = lr & np.uint64((1 << 24) - 1)
+        nbytes = int(lens[lens > 8].sum())
+        return (_dev(own, np.uint32), _dev(slot, np.uint32), _dev(b["ts"], np.uint64), _dev(pre, np.uint64),
+                _dev(lr, np.uint64), nbytes)
+
+    def union_state(self):
+        """merged state tables of the shards (each shard holds only its own keys)"""
+        from jylis_amd.route import owners
+        out = {}
+        for d, r in enumerate(self.repos):
+            st = r.state()
+            kb, ko = st["key_bytes"], st["key_offs"]
+            for i in range(len(ko) - 1):
+                k = bytes(kb[ko[i]:ko[i + 1]])
+                assert owners(np.frombuffer(k, np.uint8), np.array([0, len(k)], np.uint64), self.S)[0] == d
+                out[k] = (int(st["ts"][i]), bytes(st["val_bytes"][st["val_offs"][i]:st["val_offs"][i + 1]]))
+        return out
+
+
+def _oracle_dict(O, batches):
+    ref = O.Repo(O.TREG)
+    for b in batches:
+        ref.converge(b)
+    st = ref.state()
+    return {k: (int(t), bytes(st["val_bytes"][st["val_offs"][i]:st["val_offs"][i + 1]]))
+            for i, (k, t) in enumerate(zip(O.split_keys(st), st["ts"]))}
+
+
+@pytest.mark.parametrize("S", [1, 2, 3])
+def test_treg_routed_local_fabric(oracle_mod, S):
+    """every rank ingests its own batch over a shared key space; keys that
+    several ranks ingest in the same step meet in one merge launch"""
+    from jylis_amd.route import LocalFabric, TregRouter
+    rng = np.random.default_rng(40 + S)
+    node = _Node(S)
+    try:
+        router = TregRouter(node.engs, LocalFabric(S))
+        seen = []
+        for _ in range(4):
+            bs = [_treg_batch(rng, 2500, 4000) for _ in range(S)]
+            seen += bs
+            router.step([node.ingest(r, b) for r, b in enumerate(bs)])
+        router.drain()
+        for e in node.engs:
+            e.sync()
+        assert node.union_state() == _oracle_dict(oracle_mod, seen)
+    finally:
+        node.close()
+
+
+def test_treg_routed_overflow_drains(oracle_mod):
+    """a batch whose keys all belong to one owner overflows its run: the
+    overflow is listed on the device and routed by a drain round"""
+    from jylis_amd.engine import encode_keys
+    from jylis_amd.route import LocalFabric, TregRouter, owners
+    S = 2
+    rng = np.random.default_rng(7)
+    cand = [f"ov{i}" for i in range(20000)]
+    kb, ko = encode_keys(cand)
+    own = owners(kb, ko, S)
+    hot = [k for k, o in zip(cand, own) if o == 1][:6000]
+    node = _Node(S)
+    try:
+        router = TregRouter(node.engs, LocalFabric(S))
+        seen = []
+        for rnd in range(2):
+            bs = []
+            for r in range(S):
+                keys = [hot[int(i)] for i in rng.choice(len(hot), 5000, replace=False)]
+                vals = [bytes(rng.integers(97, 123, int(rng.integers(0, 20))).astype(np.uint8)) for _ in keys]
+                kb2, ko2 = encode_keys(keys)
+                vb, vo = encode_keys(vals)
+                bs.append({"key_bytes": kb2, "key_offs": ko2, "ts": rng.integers(0, 3, 5000).astype(np.uint64),
+                           "val_bytes": vb, "val_offs": vo})
+            seen += bs
+            router.step([node.ingest(r, b) for r, b in enumerate(bs)])
+        router.drain()
+        assert router.drains >= 1
+        assert node.union_state() == _oracle_dict(oracle_mod, seen)
+    finally:
+        node.close()
+
+
+@pytest.mark.parametrize("flags", [0, 1])
+def test_treg_device_batch_repeated_keys(oracle_mod, flags):
+    """a device batch naming keys several times (ADVICE: k_treg_lww had no
+    in-launch duplicate handling) converges exactly, in both kernel forms
+    (flags=1 forces k_treg_lww<true>, the >MALL whole-line form)"""
     import torch
 
     from helpers import assert_state_equal
     from jylis_amd._lib import TREG
+    from jylis_amd.engine import Engine
     from jylis_amd.repo import RepoTREG
-    from jylis_amd.route import owners, partition_counts_np
     O = oracle_mod
-    rng = np.random.default_rng(S)
-    want = O.Repo(O.TREG)
-    got = RepoTREG(engine)
-    lib = engine.lib
-    dev = torch.device("cuda", 0)
-    for _ in range(4):
-        b = _treg_batch(rng, 3000, 5000)
-        want.converge(b)
-        # every "shard" is this engine: slots are this engine's, owners are hashed over S
-        slots = got._intern(b)
-        own = owners(b["key_bytes"], b["key_offs"], S)
-        pre, lr = engine.pack_values(TREG, (b["val_bytes"], b["val_offs"]))
-        n = len(slots)
-        rc, bc = np.zeros(S, np.uint64), np.zeros(S, np.uint64)
-        engine._check(lib.jy_treg_route_count(engine.h, n, own.ctypes.data, lr.ctypes.data, S, 0,
-                                              rc.ctypes.data, bc.ctypes.data))
-        erc, ebc = partition_counts_np(own, lr, S)
-        assert rc.tolist() == erc.tolist() and bc.tolist() == ebc.tolist()
-        recs = torch.empty((n, 4), dtype=torch.int64, device=dev)
-        byts = torch.empty(max(int(bc.sum()), 1), dtype=torch.uint8, device=dev)
-        ts = np.asarray(b["ts"], np.uint64)
-        engine._check(lib.jy_treg_route_scatter(engine.h, n, own.ctypes.data, slots.ctypes.data, ts.ctypes.data,
-                                                pre.ctypes.data, lr.ctypes.data, S, rc.ctypes.data, bc.ctypes.data,
-                                                0, C.c_void_p(recs.data_ptr()), C.c_void_p(byts.data_ptr())))
-        engine.sync()
-        # every run holds exactly its owner's records
-        r = recs.cpu().numpy().view(np.uint64)
-        bounds = np.concatenate([[0], np.cumsum(rc)]).astype(np.int64)
-        for d in range(S):
-            run = r[bounds[d]:bounds[d + 1]]
-            assert sorted(run[:, 0].tolist()) == sorted(slots[own == d].tolist())
-        engine._check(lib.jy_treg_converge_routed(engine.h, S, rc.ctypes.data, bc.ctypes.data,
-                                                  C.c_void_p(recs.data_ptr()), C.c_void_p(byts.data_ptr())))
-    assert_state_equal(O.TREG, want.state(), got.state())
+    rng = np.random.default_rng(11 + flags)
+    eng = Engine(device=0, flags=flags)
+    try:
+        got = RepoTREG(eng)
+        want = O.Repo(O.TREG)
+        for rnd in range(5):
+            b = _treg_batch(rng, 3000, 4000)
+            # repeat ~30% of the entries at random positions (some several times)
+            rep = rng.integers(0, 3000, 1500)
+            order = rng.permutation(3000 + 1500)
+            keys = O.split_keys(b) + [O.split_keys(b)[i] for i in rep]
+            vb, vo = b["val_bytes"], b["val_offs"]
+            vals = [bytes(vb[vo[i]:vo[i + 1]]) for i in range(3000)]
+            vals += [bytes(rng.integers(97, 100, int(rng.integers(0, 20))).astype(np.uint8)) for _ in rep]
+            ts = np.concatenate([b["ts"], rng.integers(0, 4, len(rep)).astype(np.uint64)])
+            keys = [keys[i] for i in order]
+            vals = [vals[i] for i in order]
+            ts = ts[order]
+            from jylis_amd.engine import encode_keys
+            kb, ko = encode_keys(keys)
+            for k, v, t in zip(keys, vals, ts):
+                want.converge({"key_bytes": np.frombuffer(k, np.uint8), "key_offs": np.array([0, len(k)], np.uint64),
+                               "ts": np.array([t], np.uint64), "val_bytes": np.frombuffer(v, np.uint8),
+                               "val_offs": np.array([0, len(v)], np.uint64)})
+            slots = got._intern({"key_bytes": kb, "key_offs": ko})
+            pre, lr = eng.pack_values(TREG, vals)
+            eng.treg_converge(_dev(slots, np.uint32), _dev(ts, np.uint64), _dev(pre, np.uint64), _dev(lr, np.uint64))
+            torch.cuda.synchronize()
+        assert_state_equal(O.TREG, want.state(), got.state())
+    finally:
+        eng.close()
 
 
-def test_router_world_one(oracle_mod, engine):
-    """TregRouter with no process group: partition -> (self) -> converge"""
+def test_treg_whole_line_kernel_matches_oracle(oracle_mod):
+    """k_treg_lww<true> (picked for states over the 256 MiB MALL, ~11.2M+
+    slots) on the config-shaped stream: fresh timestamps, dense ties, shared
+    prefixes, long values"""
     from helpers import assert_state_equal
-    from jylis_amd._lib import TREG
+    from jylis_amd._lib import CFG_TREG_WHOLE_LINES, TREG
+    from jylis_amd.engine import Engine
     from jylis_amd.repo import RepoTREG
-    from jylis_amd.route import TregRouter
     O = oracle_mod
-    rng = np.random.default_rng(9)
-    want = O.Repo(O.TREG)
-    got = RepoTREG(engine)
-    router = TregRouter(engine, None)
-    for _ in range(3):
-        b = _treg_batch(rng, 2000, 2500)
-        want.converge(b)
-        slots = got._intern(b)
-        pre, lr = engine.pack_values(TREG, (b["val_bytes"], b["val_offs"]))
-        router.exchange_and_converge(np.zeros(len(slots), np.uint32), slots, np.asarray(b["ts"], np.uint64), pre, lr)
-    assert_state_equal(O.TREG, want.state(), got.state())
+    rng = np.random.default_rng(3)
+    eng = Engine(device=0, flags=CFG_TREG_WHOLE_LINES)
+    try:
+        got = RepoTREG(eng)
+        want = O.Repo(O.TREG)
+        for j in range(4):
+            b = _treg_batch(rng, 20000, 20000, ts_hi=1 << 3)
+            b["ts"] = b["ts"] + np.uint64(j * 2)
+            want.converge(b)
+            got.converge_deltas(b)
+        assert_state_equal(O.TREG, want.state(), got.state())
+    finally:
+        eng.close()
+
+
+def test_treg_set_repeated_keys_device(oracle_mod):
+    """local SETs on the device with repeated keys: state and flushed delta
+    equal the oracle's sequential RepoTREG.set (repo_treg.pony:65-68)"""
+    import torch
+
+    from jylis_amd._lib import TREG
+    from jylis_amd.engine import Engine, encode_keys
+    from jylis_amd.repo import RepoTREG
+    from helpers import assert_state_equal
+    O = oracle_mod
+    rng = np.random.default_rng(5)
+    eng = Engine(device=0)
+    try:
+        got = RepoTREG(eng)
+        want = O.Repo(O.TREG, 5)
+        keys = [f"s{int(i)}" for i in rng.integers(0, 300, 2000)]
+        vals = [bytes(rng.integers(97, 100, int(rng.integers(0, 14))).astype(np.uint8)) for _ in keys]
+        ts = rng.integers(0, 5, len(keys)).astype(np.uint64)
+        for k, v, t in zip(keys, vals, ts):
+            want.treg_set(k, v, int(t))
+        kb, ko = encode_keys(keys)
+        slots = got._intern({"key_bytes": kb, "key_offs": ko})
+        pre, lr = eng.pack_values(TREG, vals)
+        eng.treg_set(_dev(slots, np.uint32), _dev(ts, np.uint64), _dev(pre, np.uint64), _dev(lr, np.uint64))
+        torch.cuda.synchronize()
+        assert_state_equal(O.TREG, want.state(), got.state())
+
+        def by_key(t):
+            return {k: (int(x), bytes(t["val_bytes"][t["val_offs"][i]:t["val_offs"][i + 1]]))
+                    for i, (k, x) in enumerate(zip(O.split_keys(t), t["ts"]))}
+        assert by_key(got.flush_deltas()) == by_key(want.flush().table())
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("S", [2, 3])
+def test_pncount_routed_local_fabric(S):
+    """dense PNCOUNT peer batches grouped by owner, exchanged column by
+    column (double-buffered) and block-merged on the owners; checked against
+    a numpy max over everything ingested"""
+    import torch
+
+    from jylis_amd._lib import PNCOUNT
+    from jylis_amd.engine import Engine
+    from jylis_amd.route import CounterRouter, LocalFabric
+    from jylis_amd import synth as Sy
+    K, Cn = 4096, 3
+    engs = [Engine(device=0, counter_columns=S * Cn) for _ in range(S)]
+    try:
+        for r, e in enumerate(engs):
+            e.intern(PNCOUNT, Sy.counter_keys(K, prefix=f"o{r}:".encode()))
+        rids = Sy.replica_ids(S * Cn, 77)
+        cols = []
+        for e in engs:
+            cols.append(e.replica_cols(rids.tolist()))
+        assert all((c == cols[0]).all() for c in cols)  # one registration order on every shard
+        peer_cols = [[int(cols[0][r * Cn + c]) for c in range(Cn)] for r in range(S)]
+        router = CounterRouter(engs, LocalFabric(S), PNCOUNT)
+        rng = np.random.default_rng(S)
+        want = [np.zeros((2, S * Cn, K), np.uint64) for _ in range(S)]
+        for rnd in range(3):
+            ing = []
+            for r in range(S):
+                v = rng.integers(0, 1 << 62, (2, Cn, S, K), dtype=np.uint64)
+                v[:, :, :, :7] = np.uint64(2**64 - 3)  # wrap edge
+                ing.append(torch.from_numpy(v.view(np.int64)).to("cuda:0"))
+                for d in range(S):
+                    for c in range(Cn):
+                        w = want[d][:, peer_cols[r][c]]
+                        np.maximum(w, v[:, c, d], out=w)
+            router.step(ing, peer_cols)
+        for d, e in enumerate(engs):
+            got = e.counter_export(PNCOUNT, S * Cn, 0, K)
+            np.testing.assert_array_equal(got, want[d])
+            sums = e.pncount_get(np.arange(K, dtype=np.uint32))
+            exp = (want[d][0].sum(axis=0, dtype=np.uint64) - want[d][1].sum(axis=0, dtype=np.uint64)).view(np.int64)
+            np.testing.assert_array_equal(sums, exp)
+    finally:
+        for e in engs:
+            e.close()
