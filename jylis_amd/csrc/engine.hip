@@ -227,6 +227,10 @@ void jy_engine_destroy(jy_engine* eng) {
   F(eng->treg.dval);
   F(eng->treg.dflag);
   F(eng->treg.dcount);
+  F(eng->treg.seen[0]);
+  F(eng->treg.seen[1]);
+  F(eng->treg.dupn);
+  F(eng->treg.dups);
   F(eng->tlog.meta);
   F(eng->tlog.pool);
   F(eng->tlog.ctr);

@@ -72,10 +72,48 @@ __device__ __forceinline__ u32 jy_wave_or(u32 x) {
 // of a row on one slot) claim with one atomicOr each -- the memory side
 // orders those, so exactly one entry of a slot sees its bit clear.  Every
 // atomic of all U rows is issued before any result is consumed.
+// JY_CLAIM_MODE (build-time A/B switch, tools/ and DESIGN.md): 2 = walk the
+// row's words (default), 1 = one atomicOr per lane, 0 = no claim (UNSAFE:
+// measures the claim's cost only; never shipped)
+#ifndef JY_CLAIM_MODE
+#define JY_CLAIM_MODE 2
+#endif
 template <int U, int kAgg = 3>
 __device__ __forceinline__ void jy_claim_rows(const bool (&valid)[U], const u32 (&s)[U], u32* __restrict__ bits,
                                               bool (&first)[U]) {
+  if (JY_CLAIM_MODE == 0) {
+#pragma unroll
+    for (int u = 0; u < U; u++) first[u] = valid[u];
+    return;
+  }
   const int lane = __lane_id();
+  // Fast path: callers lay a wave's rows out as U consecutive runs of 64
+  // entries (row u, lane l = entry wave_base + 64u + l).  When those U * 64
+  // entries name the consecutive slots s0 .. s0 + 64U - 1 (a dense batch in
+  // slot order: a flush, the bench), their bitmap words and masks follow
+  // from s0 alone: one atomicOr instruction with one lane per word.
+  {
+    const u32 s0 = __shfl(s[0], 0);
+    bool contig = true;
+#pragma unroll
+    for (int u = 0; u < U; u++) contig = contig && valid[u] && s[u] == s0 + (u32)(u * 64 + lane);
+    if (__ballot(!contig) == 0) {
+      const u32 last = s0 + (u32)(U * 64 - 1), w0 = s0 >> 5;
+      u32 old = 0;
+      if ((u32)lane <= (last >> 5) - w0) {
+        const u32 w = w0 + lane;
+        const u32 lo = (s0 > w * 32 ? s0 - w * 32 : 0), hi = (last < w * 32 + 31 ? last - w * 32 : 31);
+        const u32 mask = (hi == 31 ? 0xFFFFFFFFu : ((1u << (hi + 1)) - 1)) & ~((1u << lo) - 1);
+        old = atomicOr(bits + w, mask);
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const u32 o = __shfl(old, (int)((s[u] >> 5) - w0));
+        first[u] = !(o & (1u << (s[u] & 31)));
+      }
+      return;
+    }
+  }
   u32 ret[U][kAgg], own[U];
   int grp[U], ldr[U];
 #pragma unroll
@@ -83,7 +121,7 @@ __device__ __forceinline__ void jy_claim_rows(const bool (&valid)[U], const u32 
     const u32 w = s[u] >> 5, b = 1u << (s[u] & 31);
     grp[u] = -1;
     ldr[u] = 0;
-    u64 pending = __ballot(valid[u]);
+    u64 pending = JY_CLAIM_MODE == 2 ? __ballot(valid[u]) : 0;
 #pragma unroll
     for (int k = 0; k < kAgg; k++) {
       ret[u][k] = 0;
@@ -175,10 +213,17 @@ struct TregState {  // per slot: ts u64 (read by every merge) + TVal (written by
   u32* dflag = nullptr;
   u64 dkcap = 0;
   u64* dcount = nullptr;
-  // first-occurrence claim bitmap (one bit per slot, zero between launches)
-  // followed by the launch's duplicate counter; see jy_claim_rows
-  u32* seen = nullptr;
-  u64 seen_words = 0;  // bitmap words (the counter is word seen_words)
+  // first-occurrence claims (jy_claim_rows): two bitmaps of one bit per slot
+  // used by alternate launches (each launch clears the other one), and the
+  // list of non-first entries not yet folded in: count (device), 32-B
+  // records, host capacity and an upper bound of the records it holds
+  u32* seen[2] = {nullptr, nullptr};
+  u64 seen_words = 0;
+  int parity = 0;
+  u32* dupn = nullptr;
+  u64* dups = nullptr;
+  u64 dup_cap = 0;
+  u64 dup_bound = 0;
 };
 
 // one TLOG entry: 32 B so a lane moves it with two 16-B accesses and an

@@ -18,10 +18,13 @@
 // A slot named twice in one launch (a device batch that breaks the
 // one-delta-per-key contract, or routed runs of two sources touching one
 // key) is resolved EXACTLY: the first entry of each slot (jy_claim_rows, one
-// bit per slot) is merged by the wide kernel, the others are appended to a
-// list that one wave folds in afterwards -- LWW is a join, so the fold order
-// does not change the result.  A batch in slot order costs the claim ~3
-// atomics per wave row.
+// bit per slot) is merged by the wide kernel; the others are copied into a
+// duplicate list that one wave folds in later -- before the next read or
+// SET of the register file, since LWW is a join and the fold's timing and
+// order do not change the result.  A dense batch in slot order costs the
+// claim one atomic instruction per wave.  Two claim bitmaps alternate: each
+// launch clears the other one, slice by slice, so no launch is spent on
+// resetting them.
 //
 // Roofline: HBM.  SURVEY 8d prices a key at 48 B (16 delta + 16 state read
 // + 16 state write).  What this kernel moves per delta entry: 28 B delta
@@ -68,9 +71,11 @@ struct TregK {
   u64* ts;
   TVal* val;
   const uint8_t* arena;
-  u32* seen;     // claim bitmap; seen[seen_words] = duplicate count
-  u32* dupn;
-  u32* duplist;  // entry indices of the non-first entries
+  u32* seen;     // this launch's claim bitmap
+  u32* clear;    // the other bitmap (cleared by this launch), or null
+  u64 clear_bytes;
+  u32* dupn;     // duplicate list: count, then 32-B records {slot, ts, pre, lr}
+  u64* dups;
   // RepoTREG._deltas (SET path only)
   u64* pts;
   TVal* pval;
@@ -95,9 +100,21 @@ __device__ __forceinline__ void set_one(const TregK& K, u32 s, u64 t, u64 p, u64
   K.pval[s] = TVal{p, l};
 }
 
-__device__ __forceinline__ void push_dup(const TregK& K, u64 i) {
+__device__ __forceinline__ void push_dup(const TregK& K, u32 s, u64 t, u64 p, u64 l) {
   const u32 at = atomicAdd(K.dupn, 1u);
-  K.duplist[at] = (u32)i;
+  u64x2* r = reinterpret_cast<u64x2*>(K.dups + (u64)at * 4);
+  r[0] = u64x2{(u64)s, t};
+  r[1] = u64x2{p, l};
+}
+
+// this workgroup's slice of the other claim bitmap (16-B stores)
+__device__ __forceinline__ void clear_slice(const TregK& K) {
+  if (!K.clear) return;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u64 per = ((K.clear_bytes + gridDim.x - 1) / gridDim.x + 15) & ~15ull;
+  const u64 b0 = (u64)blockIdx.x * per, b1 = b0 + per < K.clear_bytes ? b0 + per : K.clear_bytes;
+  uint8_t* base = reinterpret_cast<uint8_t*>(K.clear);
+  for (u64 o = b0 + threadIdx.x * 16; o < b1; o += blockDim.x * 16) *reinterpret_cast<u32x4*>(base + o) = u32x4{0, 0, 0, 0};
 }
 
 // kRewriteAll = false: every key rewrites its ts word (a loser writes back
@@ -115,13 +132,14 @@ template <bool kRewriteAll, bool kSet>
 __global__ __launch_bounds__(kThreads) void k_treg_lww(TregK K, const u32* __restrict__ slot,
                                                        const u64* __restrict__ dts, const u64* __restrict__ dpre,
                                                        const u64* __restrict__ dlr, u64 n) {
-  const u64 base = (u64)blockIdx.x * (kThreads * kUnroll) + threadIdx.x;
+  // a wave's rows are kUnroll consecutive runs of 64 entries (jy_claim_rows)
+  const u64 base = (u64)blockIdx.x * (kThreads * kUnroll) + (threadIdx.x >> 6) * (64 * kUnroll) + (threadIdx.x & 63);
   u32 s[kUnroll];
   u64 t[kUnroll], t0[kUnroll], p[kUnroll], l[kUnroll];
   bool valid[kUnroll], first[kUnroll];
 #pragma unroll
   for (int u = 0; u < kUnroll; u++) {
-    const u64 i = base + (u64)u * kThreads;
+    const u64 i = base + (u64)u * 64;
     valid[u] = i < n;
     s[u] = 0;
     if (valid[u]) {
@@ -137,12 +155,12 @@ __global__ __launch_bounds__(kThreads) void k_treg_lww(TregK K, const u32* __res
       if (valid[u]) t0[u] = K.ts[s[u]];
   }
   jy_claim_rows<kUnroll>(valid, s, K.seen, first);
+  clear_slice(K);
 #pragma unroll
   for (int u = 0; u < kUnroll; u++) {
-    const u64 i = base + (u64)u * kThreads;
     if (!valid[u]) continue;
     if (!first[u]) {
-      push_dup(K, i);
+      push_dup(K, s[u], t[u], p[u], l[u]);
       continue;
     }
     if (kSet) {
@@ -197,14 +215,14 @@ __device__ __forceinline__ bool routed_get(const RoutedIn& R, u64 i, u32& s, u64
 
 __global__ __launch_bounds__(kThreads) void k_treg_lww_routed(TregK K, RoutedIn R) {
   constexpr int U = 2;
-  const u64 base = (u64)blockIdx.x * (kThreads * U) + threadIdx.x;
+  const u64 base = (u64)blockIdx.x * (kThreads * U) + (threadIdx.x >> 6) * (64 * U) + (threadIdx.x & 63);
   const u64 n = (u64)R.S * R.cap;
   u32 s[U];
   u64 t[U], p[U], l[U], t0[U];
   bool valid[U], first[U];
 #pragma unroll
   for (int u = 0; u < U; u++) {
-    const u64 i = base + (u64)u * kThreads;
+    const u64 i = base + (u64)u * 64;
     s[u] = 0;
     valid[u] = i < n && routed_get(R, i, s[u], t[u], p[u], l[u]);
   }
@@ -212,11 +230,12 @@ __global__ __launch_bounds__(kThreads) void k_treg_lww_routed(TregK K, RoutedIn 
   for (int u = 0; u < U; u++)
     if (valid[u]) t0[u] = K.ts[s[u]];
   jy_claim_rows<U>(valid, s, K.seen, first);
+  clear_slice(K);
 #pragma unroll
   for (int u = 0; u < U; u++) {
     if (!valid[u]) continue;
     if (!first[u]) {
-      push_dup(K, base + (u64)u * kThreads);
+      push_dup(K, s[u], t[u], p[u], l[u]);
       continue;
     }
     if (t[u] >= t0[u] && lww_wins(t[u], t0[u], p[u], l[u], K.val, s[u], K.arena)) {
@@ -226,37 +245,27 @@ __global__ __launch_bounds__(kThreads) void k_treg_lww_routed(TregK K, RoutedIn 
   }
 }
 
-// The non-first entries of a launch, folded in by ONE wave after it: a chunk
-// of 64 entries per pass (lane = entry); entries of one slot inside a chunk
-// run in rounds by their rank among the chunk's entries of that slot, so no
-// two lanes touch a slot at once and chunks run in list order.
-struct SoaIn {
-  const u32* slot;
-  const u64* ts;
-  const u64* pre;
-  const u64* lr;
-};
-__device__ __forceinline__ bool dup_get(const SoaIn& A, u64 i, u32& s, u64& t, u64& p, u64& l) {
-  s = A.slot[i];
-  t = A.ts[i];
-  p = A.pre[i];
-  l = A.lr[i];
-  return true;
-}
-__device__ __forceinline__ bool dup_get(const RoutedIn& R, u64 i, u32& s, u64& t, u64& p, u64& l) {
-  return routed_get(R, i, s, t, p, l);
-}
-
-template <bool kSet, typename In>
-__global__ __launch_bounds__(64) void k_treg_dups(TregK K, In in) {
+// The duplicate list, folded in by ONE wave: a chunk of 64 records per pass
+// (lane = record); records of one slot inside a chunk run in rounds by their
+// rank among the chunk's records of that slot, so no two lanes touch a slot
+// at once and chunks run in list order.  Resets the list.
+template <bool kSet>
+__global__ __launch_bounds__(64) void k_treg_fold(TregK K) {
   const u32 n = *K.dupn;
   const int lane = threadIdx.x;
   for (u32 j0 = 0; j0 < n; j0 += 64) {
     const u32 j = j0 + lane;
+    const bool live = j < n;
     u32 s = 0xFFFFFFFFu;
     u64 t = 0, p = 0, l = 0;
-    bool live = j < n && dup_get(in, K.duplist[j], s, t, p, l);
-    if (!live) s = 0xFFFFFFFFu;
+    if (live) {
+      const u64x2 a = reinterpret_cast<const u64x2*>(K.dups + (u64)j * 4)[0];
+      const u64x2 b = reinterpret_cast<const u64x2*>(K.dups + (u64)j * 4)[1];
+      s = (u32)a.x;
+      t = a.y;
+      p = b.x;
+      l = b.y;
+    }
     u32 rank = 0;
     for (int k = 0; k < 64; k++) {
       const u32 sk = __shfl(s, k);
@@ -277,9 +286,10 @@ __global__ __launch_bounds__(64) void k_treg_dups(TregK K, In in) {
         }
       }
       __builtin_amdgcn_s_waitcnt(0);  // this round's stores land before the next round reads
-      __syncthreads();
+      __builtin_amdgcn_wave_barrier();
     }
   }
+  if (lane == 0) *K.dupn = 0;
 }
 
 __global__ __launch_bounds__(kThreads) void k_treg_gather(const u64* __restrict__ ts, const TVal* __restrict__ val,
@@ -319,24 +329,58 @@ __global__ __launch_bounds__(kThreads) void k_treg_flush(u32* __restrict__ dflag
 
 u32 blocks(u64 n, u64 per) { return (u32)std::max<u64>(1, (n + per - 1) / per); }
 
-// claim state of one launch over `n` entries: the bitmap (zero), the
-// duplicate counter (zero) and a duplicate list of n entries
-int32_t claim_begin(jy_engine* eng, u64 n, TregK& K) {
+TregK state_of(jy_engine* eng) {
   TregState& t = eng->treg;
+  TregK K{};
   K.ts = t.ts;
   K.val = t.val;
   K.arena = eng->arena[JY_TREG].p;
-  K.seen = t.seen;
-  K.dupn = t.seen + t.seen_words;
-  void* p;
-  JY_TRY(jy_scratch(eng, 23, std::max<u64>(n, 1) * 4, &p));
-  K.duplist = static_cast<u32*>(p);
+  K.dupn = t.dupn;
+  K.dups = t.dups;
+  return K;
+}
+
+// fold the pending duplicates (converge paths) now: before a read, a SET
+// batch (whose pending-delta test must see them) or an arena move
+int32_t fold_now(jy_engine* eng) {
+  TregState& t = eng->treg;
+  if (t.dup_bound == 0) return JY_OK;
+  hipLaunchKernelGGL((k_treg_fold<false>), dim3(1), dim3(64), 0, eng->stream, state_of(eng));
+  JY_HIP(eng, hipGetLastError());
+  t.dup_bound = 0;
   return JY_OK;
 }
-// the bitmap and the counter go back to zero for the next launch
-int32_t claim_end(jy_engine* eng) {
+
+// claim state of one launch over n entries: room for n more duplicates
+// (folding the list first when the bound says it might overflow), this
+// launch's bitmap and the other one to clear
+int32_t claim_begin(jy_engine* eng, u64 n, u32 nblocks, TregK& K) {
   TregState& t = eng->treg;
-  JY_HIP(eng, hipMemsetAsync(t.seen, 0, (t.seen_words + 1) * 4, eng->stream));
+  if (t.dup_bound + n > t.dup_cap) {
+    JY_TRY(fold_now(eng));
+    if (n > t.dup_cap) {
+      const u64 cap = std::max<u64>(4 * n, 1 << 16);
+      jy_dev_free(eng, t.dups);
+      t.dups = nullptr;
+      t.dup_cap = 0;
+      JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.dups), cap * 32, "treg duplicate list"));
+      t.dup_cap = cap;
+    }
+  }
+  K = state_of(eng);
+  K.seen = t.seen[t.parity];
+  const u64 bytes = ((t.seen_words * 4 + 15) & ~15ull);
+  // a grid too small to clear the other bitmap cheaply leaves it to a memset
+  if (bytes > (u64)nblocks * 4096) {
+    JY_HIP(eng, hipMemsetAsync(t.seen[t.parity ^ 1], 0, bytes, eng->stream));
+    K.clear = nullptr;
+    K.clear_bytes = 0;
+  } else {
+    K.clear = t.seen[t.parity ^ 1];
+    K.clear_bytes = bytes;
+  }
+  t.parity ^= 1;
+  t.dup_bound += n;
   return JY_OK;
 }
 
@@ -353,13 +397,21 @@ int32_t jy_treg_grow(jy_engine* eng, u64 need) {
   t.ts = static_cast<u64*>(a);
   t.val = static_cast<TVal*>(b);
   t.kcap = nk;
-  // claim bitmap: one bit per slot + the duplicate counter, all zero
-  jy_dev_free(eng, t.seen);
+  // the pending duplicates hold slots of the old capacity: fold them first;
+  // then two claim bitmaps (one bit per slot), both zero
+  JY_TRY(fold_now(eng));
+  for (auto& b : t.seen) jy_dev_free(eng, b);
   t.seen_words = (nk + 31) / 32;
-  void* sp = nullptr;
-  JY_TRY(jy_dev_alloc(eng, &sp, (t.seen_words + 16) * 4, "treg claim bitmap"));
-  t.seen = static_cast<u32*>(sp);
-  JY_HIP(eng, hipMemsetAsync(t.seen, 0, (t.seen_words + 16) * 4, eng->stream));
+  for (auto& b : t.seen) {
+    void* sp = nullptr;
+    JY_TRY(jy_dev_alloc(eng, &sp, (t.seen_words + 16) * 4, "treg claim bitmap"));
+    b = static_cast<u32*>(sp);
+    JY_HIP(eng, hipMemsetAsync(b, 0, (t.seen_words + 16) * 4, eng->stream));
+  }
+  if (!t.dupn) {
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.dupn), 64, "treg duplicate count"));
+    JY_HIP(eng, hipMemsetAsync(t.dupn, 0, 64, eng->stream));
+  }
   return JY_OK;
 }
 
@@ -367,21 +419,21 @@ int32_t jy_treg_merge(jy_engine* eng, u64 n, const u32* slot, const u64* ts, con
   if (n == 0) return JY_OK;
   TregState& t = eng->treg;
   JyTimed tm(eng);
+  const u32 grid = blocks(n, kThreads * kUnroll);
   TregK K{};
-  JY_TRY(claim_begin(eng, n, K));
+  JY_TRY(claim_begin(eng, n, grid, K));
   // state larger than the Infinity Cache: write whole lines (see k_treg_lww);
   // config flag JY_CFG_TREG_WHOLE_LINES forces that form (tests)
   const bool whole =
       t.kcap * (8 + sizeof(TVal)) > kMallBytes || (eng->cfg.flags & JY_CFG_TREG_WHOLE_LINES) != 0;
   if (whole)
-    hipLaunchKernelGGL((k_treg_lww<true, false>), dim3(blocks(n, kThreads * kUnroll)), dim3(kThreads), 0,
+    hipLaunchKernelGGL((k_treg_lww<true, false>), dim3(grid), dim3(kThreads), 0,
                        eng->stream, K, slot, ts, pre, lr, n);
   else
-    hipLaunchKernelGGL((k_treg_lww<false, false>), dim3(blocks(n, kThreads * kUnroll)), dim3(kThreads), 0,
+    hipLaunchKernelGGL((k_treg_lww<false, false>), dim3(grid), dim3(kThreads), 0,
                        eng->stream, K, slot, ts, pre, lr, n);
-  hipLaunchKernelGGL((k_treg_dups<false, SoaIn>), dim3(1), dim3(64), 0, eng->stream, K, SoaIn{slot, ts, pre, lr});
   JY_HIP(eng, hipGetLastError());
-  return claim_end(eng);
+  return JY_OK;
 }
 
 int32_t jy_treg_merge_routed(jy_engine* eng, u32 S, u64 cap, u64 cap_byte, const u64* recs, const u64* hdr,
@@ -389,19 +441,20 @@ int32_t jy_treg_merge_routed(jy_engine* eng, u32 S, u64 cap, u64 cap_byte, const
   const u64 n = (u64)S * cap;
   if (n == 0) return JY_OK;
   JyTimed tm(eng);
+  const u32 grid = blocks(n, kThreads * 2);
   TregK K{};
-  JY_TRY(claim_begin(eng, n, K));
+  JY_TRY(claim_begin(eng, n, grid, K));
   RoutedIn R{recs, hdr, S, cap, cap_byte, rebase, eng->nkeys[JY_TREG],
              reinterpret_cast<unsigned long long*>(eng->skipped_dev)};
-  hipLaunchKernelGGL(k_treg_lww_routed, dim3(blocks(n, kThreads * 2)), dim3(kThreads), 0, eng->stream, K, R);
-  hipLaunchKernelGGL((k_treg_dups<false, RoutedIn>), dim3(1), dim3(64), 0, eng->stream, K, R);
+  hipLaunchKernelGGL(k_treg_lww_routed, dim3(grid), dim3(kThreads), 0, eng->stream, K, R);
   JY_HIP(eng, hipGetLastError());
-  return claim_end(eng);
+  return JY_OK;
 }
 
 int32_t jy_treg_gather(jy_engine* eng, u64 n, const u32* slots, u64* ots, u64* opre, u64* olr) {
   if (n == 0) return JY_OK;
   TregState& t = eng->treg;
+  JY_TRY(fold_now(eng));
   hipLaunchKernelGGL(k_treg_gather, dim3(blocks(n, kThreads)), dim3(kThreads), 0, eng->stream, t.ts, t.val, slots, n,
                      ots, opre, olr);
   JY_HIP(eng, hipGetLastError());
@@ -429,24 +482,28 @@ static int32_t treg_delta_grow(jy_engine* eng) {
 }
 
 // local SET batch (RepoTREG.set repo_treg.pony:65-68): every entry updates
-// the state and, if it wins there, the key's pending delta; repeated keys are
-// exact (the first entry of a slot in the wide kernel, the rest folded after)
+// the state and, if it wins there, the key's pending delta.  A SET's pending
+// test must see the state as the reference would, so converge duplicates
+// still pending are folded first, and the batch's own repeated keys are
+// folded right after it (SET semantics) rather than later.
 int32_t jy_treg_set_batch(jy_engine* eng, u64 n, const u32* slot, const u64* ts, const u64* pre, const u64* lr) {
   if (n == 0) return JY_OK;
   TregState& t = eng->treg;
   JY_TRY(treg_delta_grow(eng));
   JyTimed tm(eng);
+  JY_TRY(fold_now(eng));
+  const u32 grid = blocks(n, kThreads * kUnroll);
   TregK K{};
-  JY_TRY(claim_begin(eng, n, K));
+  JY_TRY(claim_begin(eng, n, grid, K));
   K.pts = t.dts;
   K.pval = t.dval;
   K.pflag = t.dflag;
   K.pcount = t.dcount;
-  hipLaunchKernelGGL((k_treg_lww<false, true>), dim3(blocks(n, kThreads * kUnroll)), dim3(kThreads), 0, eng->stream,
-                     K, slot, ts, pre, lr, n);
-  hipLaunchKernelGGL((k_treg_dups<true, SoaIn>), dim3(1), dim3(64), 0, eng->stream, K, SoaIn{slot, ts, pre, lr});
+  hipLaunchKernelGGL((k_treg_lww<false, true>), dim3(grid), dim3(kThreads), 0, eng->stream, K, slot, ts, pre, lr, n);
+  hipLaunchKernelGGL((k_treg_fold<true>), dim3(1), dim3(64), 0, eng->stream, K);
   JY_HIP(eng, hipGetLastError());
-  return claim_end(eng);
+  t.dup_bound = 0;
+  return JY_OK;
 }
 
 int32_t jy_treg_pending(jy_engine* eng, u64* count) {
