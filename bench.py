@@ -3,16 +3,27 @@
 
 Workload (BASELINE.json configs[1]): PNCOUNT,
 16M keys x 64 replicas x {P, N} per GPU shard.  One step = converge one full
-delta batch (64 flushed peer batches, one per replica column, each covering
-every key of the shard, both signs) = 2^31 cell merges, in ONE engine call
-(jy_pncount_converge_block) on HBM-resident input.  Keys are hash-sharded:
-every rank owns its own 16M keys (weak scaling, no data-path collective --
-the merge itself exchanges nothing; see DESIGN.md for the routed variant).
+delta batch: 64 flushed peer batches (one per replica column, each covering
+every key, both signs) = 2^31 cell merges per shard, HBM-resident input.
 
-Inputs: seeded splitmix64 streams generated in HBM (jylis_amd/synth.py);
-state starts from a synthetic full state; `--batches` distinct delta batches
-(a monotone chain, 75% advanced / 25% stale cells) are cycled through, so
-every step performs real state changes on fresh input.
+Keys are hash-sharded over the N GPUs (weak scaling: 16M keys per GPU).  At
+N = 1 a step is ONE engine call (jy_pncount_converge_block) over the 64
+columns.  At N > 1 the peer batches are ROUTED (north_star): rank
+r ingests the 64/N peer columns c with c % N == r, each covering the keys of
+every owner (grouped by owner, as a peer running the same sharding flushes
+them), and route.CounterRouter moves them to their owners with equal-split
+RCCL all-to-alls over xGMI, one column per rank at a time, double-buffered so
+chunk c+1 is in flight while the owners merge chunk c.  `value` counts the
+cells merged on all ranks per wall second including the exchange; the
+roofline line prices the merge kernel alone.
+
+Inputs: seeded splitmix64 streams generated in HBM (jylis_amd/synth.py); the
+state starts from a synthetic full state and `--batches` distinct delta
+batches (a monotone chain, 75% of cells advanced / 25% stale) are cycled.
+After the first cycle the state already dominates every batch, so later
+steps change no cell -- the kernel's traffic is the same (it reads both
+operands and stores the max unconditionally), and `first_cycle_changes`
+reports how many cells the first application changed.
 
 Prints ONE JSON line on rank 0.
 """
@@ -46,6 +57,9 @@ def parse():
     ap.add_argument("--type", default="pncount", choices=["pncount", "gcount", "treg", "tlog", "ujson"],
                     help="pncount = the BASELINE metric line; the others measure SURVEY 8d configs 1,3,4,5")
     ap.add_argument("--route", action="store_true", help="treg: run the routing exchange even on 1 GPU")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1 collectives: nccl (RCCL over xGMI); gloo only rehearses the routed path "
+                         "with several ranks on one GPU")
     return ap.parse_args()
 
 
@@ -153,17 +167,27 @@ def cpu_baseline_parallel(args, seed):
                       f"peer batches ({cells} cell merges, {dt:.2f} s, oracle/jy_oracle.cpp, {T} threads)"}
 
 
+def _owner_seed(seed, owner):
+    return seed + owner * 7919  # owner 0 keeps the single-GPU stream
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
     import torch
+    if args.backend == "gloo":  # rehearsal: several ranks may share one GPU
+        local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
-    dist = None
+    dist = cpu_group = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+        cpu_group = dist.new_group(backend="gloo")
     if args.type != "pncount":
         other_mode(args, rank, world, local, dist)
         if dist:
@@ -171,77 +195,95 @@ def main():
         return
 
     from jylis_amd import synth as S
+    from jylis_amd._lib import PNCOUNT
     from jylis_amd.engine import Engine
+    from jylis_amd.route import CounterRouter, DistFabric, LocalFabric
     K, R = args.keys, args.replicas
+    assert R % world == 0, "the replica columns are split evenly over the ranks"
+    Cn = R // world  # peer columns ingested per rank
     seed = S.BASE_SEED + 2  # config 2
+    seed_me = _owner_seed(seed, rank)
     dev = torch.device("cuda", local)
     eng = Engine(device=local, counter_columns=R, key_capacity=[1024, K, 1024, 1024, 1024])
-    # one non-default stream shared by torch (generation, timing events) and the
-    # engine, so the HIP events bracket exactly the engine's launches
+    # one non-default stream shared by torch (generation, collectives, timing
+    # events) and the engine, so the HIP events bracket the engine's launches
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     eng.set_stream(stream.cuda_stream)
 
     # key shard of this rank: interned on the host like any key (s<rank>:p########)
     kb, ko = S.counter_keys(K, prefix=f"s{rank}:p".encode())
-    slots = eng.intern(1, (kb, ko))
+    slots = eng.intern(PNCOUNT, (kb, ko))
     assert slots[0] == 0 and slots[-1] == K - 1
     del kb, ko, slots
     cols = eng.replica_cols(S.replica_ids(R, seed).tolist())
+    assert (cols == np.arange(R)).all()
+    peer = [[r + c * world for c in range(Cn)] for r in range(world)]  # global column of rank r's c-th peer
 
-    # initial state and the delta chain, generated in HBM
-    shape = (2, R, K)
-    tmp = torch.empty(shape, dtype=torch.int64, device=dev)
-    S.counter_rows_torch(tmp, seed)
-    eng.pncount_converge_block(cols, 0, tmp[0], tmp[1])  # load: max(0, s) = s
+    # initial state of this shard, generated in HBM and loaded (max(0, s) = s)
+    tmp = torch.empty((2, R, K), dtype=torch.int64, device=dev)
+    S.counter_rows_torch(tmp, seed_me)
+    eng.pncount_converge_block(cols, 0, tmp[0], tmp[1])
+    del tmp
+    # the delta chain this rank ingests: [sign][c][owner][K] per batch
     nb = max(1, args.batches)
-    deltas = []
-    prev = tmp
-    for j in range(nb):
-        d = torch.empty(shape, dtype=torch.int64, device=dev)
-        S.counter_rows_torch(d, seed, rnd=j, prev=prev)
-        deltas.append(d)
-        prev = d
-    del tmp, prev
+    ingests = [torch.empty((2, Cn, world, K), dtype=torch.int64, device=dev) for _ in range(nb)]
+    for d in range(world):
+        seed_d = _owner_seed(seed, d)
+        for c in range(Cn):
+            g = peer[rank][c]
+            prev = torch.empty((2, 1, K), dtype=torch.int64, device=dev)
+            S.counter_rows_torch(prev, seed_d, col_offset=g, col_total=R)
+            for j in range(nb):
+                cur = torch.empty_like(prev)
+                S.counter_rows_torch(cur, seed_d, rnd=j, prev=prev, col_offset=g, col_total=R)
+                ingests[j][:, c, d].copy_(cur[:, 0])
+                prev = cur
     torch.cuda.synchronize(dev)
+    fabric = DistFabric(dist, cpu_group=cpu_group) if world > 1 else LocalFabric(1)
+    router = CounterRouter([eng], fabric, PNCOUNT)
 
     def step(i):
-        d = deltas[i % nb]
-        eng.pncount_converge_block(cols, 0, d[0], d[1])
+        router.step([ingests[i % nb]], peer)
 
+    changed = None
     for i in range(args.warmup):
+        if i == 0:
+            before = eng.counter_export(PNCOUNT, R, 0, min(K, 1 << 16))
         step(i)
+        if i == 0:
+            changed = int((eng.counter_export(PNCOUNT, R, 0, min(K, 1 << 16)) != before).sum())
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    eng.timing(True)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        evs[i][0].record()
         step(args.warmup + i)
-        evs[i][1].record()
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kern_ms = [a.elapsed_time(b) for a, b in evs]
+    calls = eng.timing_read(cap=1 << 16)
+    eng.timing(False)
+    merge_ms_per_step = float(np.sum(calls)) / args.steps
 
-    # correctness spot-check on sampled cells: state == max(initial, applied batches)
+    # correctness spot-check on sampled cells of this shard: state == max(initial, applied batches)
     applied = sorted({(args.warmup + i) % nb for i in range(args.steps)} | {i % nb for i in range(args.warmup)})
     rng = np.random.default_rng(rank)
     s0 = int(rng.integers(0, K - 64))
     cells = (np.arange(2)[:, None, None] * R * K + np.arange(R)[None, :, None] * K
              + (s0 + np.arange(64))[None, None, :]).astype(np.uint64)
-    exp = S.counter_state_np(K, R, 2, seed, cells=cells)
+    exp = S.counter_state_np(K, R, 2, seed_me, cells=cells)
     chain = exp.copy()
     best = exp.copy()
     for j in range(nb):
-        chain = S.counter_delta_np(chain, j, seed, cells=cells)
+        chain = S.counter_delta_np(chain, j, seed_me, cells=cells)
         if j in applied:
             best = np.maximum(best, chain)
-    got = eng.counter_export(1, R, s0, 64)
+    got = eng.counter_export(PNCOUNT, R, s0, 64)
     ok = bool((got == best).all())
     sums = eng.pncount_get(np.arange(s0, s0 + 64, dtype=np.uint32))
     exp_sum = (best[0].sum(axis=0, dtype=np.uint64) - best[1].sum(axis=0, dtype=np.uint64)).view(np.int64)
@@ -249,13 +291,13 @@ def main():
 
     t_max = elapsed
     if dist:
-        tt = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed, 0.0 if ok else 1.0, merge_ms_per_step], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_max, bad = float(tt[0]), float(tt[1])
+        t_max, bad, merge_ms_per_step = float(tt[0]), float(tt[1]), float(tt[2])
         ok = bad == 0.0
     cells_per_step = 2 * R * K
     value = world * cells_per_step * args.steps / t_max
-    avg_kern_s = float(np.mean(kern_ms)) / 1e3
+    avg_kern_s = merge_ms_per_step / 1e3
     achieved = BYTES_PER_CELL * cells_per_step / avg_kern_s / 1e9
 
     traffic = None
@@ -275,6 +317,7 @@ def main():
         cpu_par = cpu_baseline_parallel(args, seed) if args.cpu_threads > 1 else None
 
     if rank == 0:
+        xbytes = 2 * Cn * (world - 1) * K * 8  # sent (= received) per rank per step
         line = {
             "metric": METRIC,
             "value": value,
@@ -288,18 +331,24 @@ def main():
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (seeded splitmix64 in HBM; SURVEY.md 8d config 2)",
-            "config": {"workload": "PNCOUNT converge: 16M keys x 64 replicas x {P,N} per GPU shard, "
-                                   "one full delta batch (64 peer batches) per step",
+            "config": {"workload": f"PNCOUNT converge: {K // (1 << 20)}M keys x {R} replicas x {{P,N}} per GPU shard, "
+                                   f"one full delta batch ({R} peer batches) per step"
+                                   + (", peer batches routed to owners (RCCL all-to-all)" if world > 1 else ""),
                        "keys_per_gpu": K, "replicas": R, "signs": 2, "cells_per_step_per_gpu": cells_per_step,
-                       "parallelism": f"key-sharded x{world}", "distinct_batches": nb},
+                       "parallelism": f"key-sharded x{world}", "distinct_batches": nb,
+                       "routed": world > 1, "exchange_bytes_per_gpu_per_step": xbytes},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_block_max<true>", "kernel_ms_avg": avg_kern_s * 1e3,
+                         "merge_launches_per_step": len(calls) // max(args.steps, 1),
                          "bytes_per_cell": BYTES_PER_CELL},
             "cpu_baseline": cpu,
             "cpu_baseline_parallel": cpu_par,
+            "first_cycle_changes": {"cells_changed": changed, "cells_sampled": 2 * R * min(K, 1 << 16)},
             "verified": ok,
         }
+        if world > 1:
+            line["exchange_GBps_per_gpu"] = xbytes / (t_max / args.steps) / 1e9
         print(json.dumps(line), flush=True)
     eng.close()
     if dist:

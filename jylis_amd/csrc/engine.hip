@@ -76,7 +76,7 @@ static int32_t stage_begin(jy_engine* eng) {
   return JY_OK;
 }
 static int32_t stage_end(jy_engine* eng) {
-  if (eng->pin_used) JY_HIP(eng, hipEventRecord(eng->pin_ready, eng->stream));
+  if (eng->pin_used) JY_HIP(eng, hipEventRecord(eng->pins[eng->pin_slot].ready, eng->stream));
   return JY_OK;
 }
 
@@ -97,47 +97,63 @@ int32_t jy_stage(jy_engine* eng, int idx, const void* src, u64 bytes, int32_t me
   void* d;
   JY_TRY(jy_scratch(eng, idx, bytes, &d));
   if (!eng->pin_used) {
-    // the previous call's staging copies must have drained before reuse
-    JY_HIP(eng, hipEventSynchronize(eng->pin_ready));
+    // next region of the ring: its copies (kPinRing calls ago) must have drained
+    eng->pin_slot = (eng->pin_slot + 1) % jy_engine::kPinRing;
+    JY_HIP(eng, hipEventSynchronize(eng->pins[eng->pin_slot].ready));
     eng->pin_cursor = 0;
     eng->pin_used = true;
   }
+  jy_engine::PinSlot& ps = eng->pins[eng->pin_slot];
   u64 need = round_up(eng->pin_cursor, 256) + bytes;
-  if (need > eng->pin_bytes) {
-    // grow: drain everything that may read the old pinned region
+  if (need > ps.bytes) {
+    // grow this region: drain everything that may read it
     JY_HIP(eng, hipStreamSynchronize(eng->stream));
-    if (eng->pin) JY_HIP(eng, hipHostFree(eng->pin));
-    eng->pin = nullptr;
     u64 nb = std::max<u64>(need * 2, 1ull << 20);
-    JY_HIP(eng, hipHostMalloc(&eng->pin, nb, hipHostMallocDefault));
-    eng->pin_bytes = nb;
-    eng->pin_cursor = 0;
+    void* np = nullptr;
+    JY_HIP(eng, hipHostMalloc(&np, nb, hipHostMallocDefault));
+    if (ps.p) {
+      std::memcpy(np, ps.p, eng->pin_cursor);  // earlier inputs of this call stay valid
+      JY_HIP(eng, hipHostFree(ps.p));
+    }
+    ps.p = np;
+    ps.bytes = nb;
   }
   u64 at = round_up(eng->pin_cursor, 256);
-  std::memcpy(static_cast<uint8_t*>(eng->pin) + at, src, bytes);
-  JY_HIP(eng, hipMemcpyAsync(d, static_cast<uint8_t*>(eng->pin) + at, bytes, hipMemcpyHostToDevice, eng->stream));
+  std::memcpy(static_cast<uint8_t*>(ps.p) + at, src, bytes);
+  JY_HIP(eng, hipMemcpyAsync(d, static_cast<uint8_t*>(ps.p) + at, bytes, hipMemcpyHostToDevice, eng->stream));
   eng->pin_cursor = at + bytes;
   *dev_out = d;
   return JY_OK;
 }
 
-// Device copy of a block merge's column list; re-uploaded only when it changes.
+// Device copy of a block merge's column list, cached by content (a routed
+// step cycles through a few lists); a new list is uploaded asynchronously
+// from a pinned copy kept with it, so no call waits for the stream.
 static int32_t cols_to_device(jy_engine* eng, u32 ncols, const u16* cols, const u16** out) {
-  if (eng->cols_cache.size() == ncols && eng->cols_dev &&
-      std::equal(eng->cols_cache.begin(), eng->cols_cache.end(), cols)) {
-    *out = eng->cols_dev;
+  std::vector<u16> key(cols, cols + ncols);
+  auto it = eng->cols_cache.find(key);
+  if (it != eng->cols_cache.end()) {
+    *out = it->second.dev;
     return JY_OK;
   }
-  JY_HIP(eng, hipStreamSynchronize(eng->stream));  // queued merges may still read the old list
-  if (ncols > eng->cols_dev_cap) {
-    if (eng->cols_dev) JY_HIP(eng, hipFree(eng->cols_dev));
-    eng->cols_dev = nullptr;
-    JY_HIP(eng, hipMalloc(reinterpret_cast<void**>(&eng->cols_dev), std::max<u64>(ncols, 64) * 2));
-    eng->cols_dev_cap = std::max<u64>(ncols, 64);
+  if (eng->cols_cache.size() >= 256) {  // rare: drop the cache once its uploads and readers are done
+    JY_HIP(eng, hipStreamSynchronize(eng->stream));
+    for (auto& kv : eng->cols_cache) {
+      hipFree(kv.second.dev);
+      hipHostFree(kv.second.pin);
+    }
+    eng->cols_cache.clear();
   }
-  JY_HIP(eng, hipMemcpy(eng->cols_dev, cols, (u64)ncols * 2, hipMemcpyHostToDevice));
-  eng->cols_cache.assign(cols, cols + ncols);
-  *out = eng->cols_dev;
+  jy_engine::ColList c;
+  JY_HIP(eng, hipHostMalloc(reinterpret_cast<void**>(&c.pin), std::max<u64>(ncols, 1) * 2, hipHostMallocDefault));
+  std::memcpy(c.pin, cols, (u64)ncols * 2);
+  if (hipMalloc(reinterpret_cast<void**>(&c.dev), std::max<u64>(ncols, 1) * 2) != hipSuccess) {
+    hipHostFree(c.pin);
+    return eng->fail(JY_ENOMEM, "column list allocation");
+  }
+  JY_HIP(eng, hipMemcpyAsync(c.dev, c.pin, (u64)ncols * 2, hipMemcpyHostToDevice, eng->stream));
+  eng->cols_cache.emplace(std::move(key), c);
+  *out = c.dev;
   return JY_OK;
 }
 
@@ -185,7 +201,7 @@ int32_t jy_engine_create(const jy_config* cfg, jy_engine** out) {
   }
   if (hipSetDevice(eng->device) != hipSuccess ||
       hipStreamCreateWithFlags(&eng->own_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&eng->pin_ready, hipEventDisableTiming) != hipSuccess ||
+
       hipEventCreateWithFlags(&eng->total_ready, hipEventDisableTiming) != hipSuccess ||
       hipMalloc(&eng->skipped_dev, 8) != hipSuccess || hipMemset(eng->skipped_dev, 0, 8) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&eng->pin_total), 64, hipHostMallocDefault) != hipSuccess) {
@@ -194,7 +210,13 @@ int32_t jy_engine_create(const jy_config* cfg, jy_engine** out) {
   }
   eng->stream = eng->own_stream;
   std::memset(eng->pin_total, 0, 64);
-  hipEventRecord(eng->pin_ready, eng->stream);
+  for (auto& ps : eng->pins) {
+    if (hipEventCreateWithFlags(&ps.ready, hipEventDisableTiming) != hipSuccess) {
+      jy_engine_destroy(eng);
+      return JY_EHIP;
+    }
+    hipEventRecord(ps.ready, eng->stream);
+  }
   hipEventRecord(eng->total_ready, eng->stream);
   int32_t rc = JY_OK;
   for (int t = 0; t < JY_NTYPES && rc == JY_OK; t++) rc = jy_ensure_slots(eng, t, eng->cfg.key_capacity[t]);
@@ -247,14 +269,19 @@ void jy_engine_destroy(jy_engine* eng) {
   for (auto& s : eng->scratch) F(s.p);
   if (eng->stream) hipStreamSynchronize(eng->stream);
   if (eng->skipped_dev) hipFree(eng->skipped_dev);
-  if (eng->cols_dev) hipFree(eng->cols_dev);
-  if (eng->pin) hipHostFree(eng->pin);
+  for (auto& kv : eng->cols_cache) {
+    hipFree(kv.second.dev);
+    hipHostFree(kv.second.pin);
+  }
+  for (auto& ps : eng->pins) {
+    if (ps.p) hipHostFree(ps.p);
+    if (ps.ready) hipEventDestroy(ps.ready);
+  }
   if (eng->pin_total) hipHostFree(eng->pin_total);
   for (auto& ev : eng->tm_ev) {
     hipEventDestroy(ev.first);
     hipEventDestroy(ev.second);
   }
-  if (eng->pin_ready) hipEventDestroy(eng->pin_ready);
   if (eng->total_ready) hipEventDestroy(eng->total_ready);
   if (eng->own_stream) hipStreamDestroy(eng->own_stream);
   delete eng;
@@ -276,7 +303,7 @@ int32_t jy_set_stream(jy_engine* eng, void* s) {
   JY_HIP(eng, hipStreamSynchronize(eng->stream));
   eng->stream = s ? static_cast<hipStream_t>(s) : eng->own_stream;
   // events recorded on the previous stream are complete (synchronised above)
-  JY_HIP(eng, hipEventRecord(eng->pin_ready, eng->stream));
+  for (auto& ps : eng->pins) JY_HIP(eng, hipEventRecord(ps.ready, eng->stream));
   JY_HIP(eng, hipEventRecord(eng->total_ready, eng->stream));
   return JY_OK;
 }

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <map>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -314,16 +315,25 @@ struct jy_engine {
   // scratch (device) reused across calls, stream-ordered
   // 0-7 staged inputs, 8-14 and 16-23 merge temporaries, 15 scan temp storage
   DevArray scratch[24];
-  // column list of the last block merge, kept resident (a peer set rarely changes)
-  std::vector<u16> cols_cache;
-  u16* cols_dev = nullptr;
-  u64 cols_dev_cap = 0;
-  // pinned host staging
-  void* pin = nullptr;
-  u64 pin_bytes = 0;
+  // column lists of block merges, kept resident: a routed step cycles
+  // through a few lists, and uploading one must not stall the stream
+  struct ColList {
+    u16* dev = nullptr;
+    u16* pin = nullptr;  // the pinned source of the async upload, kept with it
+  };
+  std::map<std::vector<u16>, ColList> cols_cache;
+  // pinned host staging: a ring of regions, so a call only waits for the
+  // copies of the call kRing calls ago
+  static constexpr int kPinRing = 4;
+  struct PinSlot {
+    void* p = nullptr;
+    u64 bytes = 0;
+    hipEvent_t ready = nullptr;  // the region may be overwritten once this fired
+  };
+  PinSlot pins[kPinRing];
+  int pin_slot = 0;
   u64 pin_cursor = 0;
   bool pin_used = false;
-  hipEvent_t pin_ready = nullptr;  // staging may be overwritten once this fired
   u64* pin_total = nullptr;        // pinned u64[4] for async totals
   hipEvent_t total_ready = nullptr;
 

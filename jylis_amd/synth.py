@@ -130,15 +130,18 @@ def counter_delta_torch(prev, rnd, seed, out=None):
     return r
 
 
-def counter_rows_torch(out, seed, rnd=None, prev=None, wrap_frac=True):
+def counter_rows_torch(out, seed, rnd=None, prev=None, wrap_frac=True, col_offset=0, col_total=None):
     """Fill out[nsigns][R][K] (int64 bits of u64) row by row, bounding temporaries:
-    rnd None -> initial state; else the round-`rnd` delta from `prev`."""
+    rnd None -> initial state; else the round-`rnd` delta from `prev`.
+    Rows are columns col_offset .. col_offset + R - 1 of a [nsigns][col_total][K]
+    stream (default: the whole stream), so any slice of it can be generated alone."""
     import torch
     nsigns, R, K = out.shape
+    RT = R if col_total is None else col_total
     ar = torch.arange(K, dtype=torch.int64, device=out.device)
     for s in range(nsigns):
         for c in range(R):
-            cell = ar + (s * R + c) * K
+            cell = ar + (s * RT + col_offset + c) * K
             if rnd is None:
                 h = splitmix64_torch(cell * _s64(GOLDEN) + _s64(seed))
                 v = _srl(h, 24)
