@@ -263,8 +263,17 @@ void jy_engine_destroy(jy_engine* eng) {
   F(eng->ujson.meta);
   F(eng->ujson.epool);
   F(eng->ujson.cpool);
+  F(eng->ujson.spare_e);
+  F(eng->ujson.spare_c);
   F(eng->ujson.ctr);
+  F(eng->ujson.dptr);
+  F(eng->ujson.bad);
+  F(eng->ujson.vvd);
+  F(eng->ujson.tick);
+  for (auto& a : eng->ujson.st) F(a.p);
   if (eng->ujson.pin) hipHostFree(eng->ujson.pin);
+  for (hipEvent_t e : eng->ujson.ready)
+    if (e) hipEventDestroy(e);
   for (auto& a : eng->arena) F(a.p);
   for (auto& s : eng->scratch) F(s.p);
   if (eng->stream) hipStreamSynchronize(eng->stream);

@@ -278,11 +278,35 @@ struct UjsonState {  // per-document pool segments + dense vv
   u64 epcap = 0;
   u64* cpool = nullptr;   // cloud pool
   u64 cpcap = 0;
+  URec* spare_e = nullptr;  // the pools a compaction wrote out of (reused by the next one)
+  u64 spare_ecap = 0;
+  u64* spare_c = nullptr;
+  u64 spare_ccap = 0;
   u64* ctr = nullptr;     // device: [0] element bump pointer, [1] cloud bump pointer
   u64* pin = nullptr;     // pinned readback
   u64* vv = nullptr;      // [kcap][R]
   u32 R = 0;
   u64 kcap = 0;
+  // converge pipeline (k_ujson.hip): epoch-tagged claims and bad marks (no
+  // reset between converges), a zero-between-converges dense delta vv, the
+  // launches' tickets, and the host's bounds of pool use
+  u32 epoch = 0;
+  u64* dptr = nullptr;     // [kcap] epoch << 32 | first delta doc of the slot
+  u32* bad = nullptr;      // [dcap] == epoch: the delta doc is skipped
+  u64* vvd = nullptr;      // [dcap][R], zero between converges
+  u64 dcap = 0;
+  u32* tick = nullptr;     // [8] ticket counters of the launches
+  u64* pin_dev = nullptr;  // device view of pin: [8 + 2j ..] bump pointers after converge j (mod kRing)
+  // converges in flight: converge j records ready[j % kRing] and its worst-
+  // case pool use; the host absorbs the newest finished one's exact bump
+  // pointers, so it waits only when the pools may really be short
+  static constexpr int kRing = 4;
+  hipEvent_t ready[kRing] = {};
+  u64 ring_e[kRing] = {}, ring_c[kRing] = {};
+  u64 seq = 0, done = 0;               // converges issued / absorbed
+  u64 used_e = 0, used_c = 0;          // bump pointers after converge done - 1 (exact)
+  u64 live_e = 0, live_c = 0;          // upper bounds of live elements / cloud dots
+  DevArray st[6];                      // look-back status words of the scans (zeroed once)
 };
 
 struct Arena {

@@ -16,50 +16,60 @@
 // ascending by dot) and of the cloud pool (dots ascending); dense vv
 // [kcap][R].
 //
-// A converge touches ONLY the documents of its batch.  Their state segments
-// form the "touched state": flat index spaces over the delta documents (ao /
-// co = exclusive scans of their sizes), merged with the delta by the
-// per-element merge path below; every merged document is written as one
-// fresh run at the pools' bump pointers and its UMeta repointed.  Untouched
-// documents are never read or moved (the Zipf config-5 stream touches ~17 %
-// of them).  The host reads the touched sizes and the bump pointers back once
-// per converge (they size the launches); when a pool cannot hold the touched
-// state plus the delta, every document is first compacted into a new pool.
+// A converge touches ONLY the documents of its batch; every merged document
+// is written as one fresh run at the pools' bump pointers and its UMeta
+// repointed.  Untouched documents are never read or moved.
 //
-// Parallel shape: ONE THREAD PER ELEMENT / CLOUD DOT, not per document.
-// Delta documents follow a Zipf(1.1) popularity: the
-// hottest document of a batch carries tens of thousands of dots, and a
-// thread-per-document join serialises on it (measured: 415 ms for 1M docs).
-// Every decision is local to one element given binary searches into the
-// other side's sorted segment; output positions come from merge-path ranks:
-//   pos(x) = out_off[doc] + #kept own-side before x + #kept other-side < x
-// with the kept counts from exclusive scans of keep flags.  Compaction of a
-// cloud dot x of column c above the merged vv v: x folds into the vv iff
-// seq(x) == v + 1 + |union dots of c in (v, seq(x))|, the union rank being
-// two lower_bounds (state side) plus a scan over de-duplicated delta dots.
+// Parallel shape: ONE THREAD PER ELEMENT / CLOUD DOT (the Zipf config-5
+// stream puts tens of thousands of dots on its hottest documents, so a
+// thread- or wave-per-document join serialises on them).  Every decision is
+// local to one item given binary searches into the other side's sorted
+// segment; output positions come from merge-path ranks,
+//   pos(x) = out_off[doc] + #kept own-side before x + #kept other-side < x,
+// with the kept counts from scans of keep flags.  A cloud dot x of column c
+// above the merged vv v folds into the vv iff seq(x) == v + 1 + |union dots
+// of c in (v, seq(x))|.
 //
-// Launch shape: independent per-item jobs of one phase share ONE launch
-// (block-uniform ranges: e.g. state-side scatter, delta-side scatter, both
-// cloud scatters and the vv store), and the keep flags of all sides are
-// concatenated so one scan serves them (positions only ever use differences
-// of scan values inside one side).  A converge is ~20 launches.
+// FIVE launches per converge and no host round trip:
+//   U1 k_uj_docs     per delta doc: slot claim, meta, state vv rows, scans of
+//                    the touched-state sizes; per delta item: validation and
+//                    the dense delta vv
+//   U2 k_uj_flags    keep flags of state / delta elements and delta cloud
+//                    dedupe, scanned; merged vv
+//   U3 k_uj_compact  cloud compaction against the merged vv, scanned
+//   U4 k_uj_sizes    per-document output sizes, scanned; the pools' bump
+//                    pointers move on the device
+//   U5 k_uj_scatter  every kept item to its merge-path position; vv rows and
+//                    metas; the next converge's zero state
+// Scans are single-pass (jy_scan.hpp: tickets + decoupled look-back), item
+// launches are persistent grids that read their sizes from device memory,
+// and each tile finds the documents of its items with one search over the
+// CSR offsets staged in LDS -- no segment-id arrays.  Claims (a slot named
+// twice in one batch: both copies skipped) and bad marks carry the
+// converge's epoch, so nothing is reset with a memset.  The host reads pool
+// use back only through a mapped pinned word written by U4 and checks it
+// when a later converge's worst case might not fit (then it compacts).
 //
 // Roofline: HBM.  Per touched element: 16 B read + 16 B written (+ 4 B
-// flag, 4 B scan, 4 B doc id); per touched cloud dot 8 B read + 8 B written;
-// vv rows and metas of delta docs.
-
-#include <hipcub/hipcub.hpp>
+// scan value, written and read); per touched cloud dot 8 B read + 8 B
+// written (+ 4 B); vv rows and metas of delta docs.
 
 #include <algorithm>
+#include <cstring>
 
 #include "jy_internal.hpp"
+#include "jy_scan.hpp"
 
 namespace {
 
 constexpr int kThreads = 256;
-constexpr u32 kNone = 0xFFFFFFFFu;
-constexpr u32 kSegBits = 28;  // seg-id encoding (range << 28 | doc)
-constexpr u32 kSegMask = (1u << kSegBits) - 1;  // readers strip the range bits
+constexpr int kPer = 4;                         // items per thread in item tiles
+constexpr u64 kTile1 = (u64)kThreads * kPer;    // U1 item tiles: 1024 items
+constexpr u64 kTile = kThreads;                 // U2 / U3 / U5 item tiles: one item per thread
+constexpr u64 kDocTile = kThreads;              // docs per doc tile
+constexpr u64 kLdsDocs = 1023;                  // docs a tile stages in LDS for its search
+
+enum { T_U1 = 0, T_U2, T_U3, T_U4, T_U5 };  // ticket counters
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
@@ -67,27 +77,36 @@ __device__ __forceinline__ u32 dcol(u64 d) { return (u32)(d >> JY_DOT_SEQ_BITS);
 __device__ __forceinline__ u64 dseq(u64 d) { return d & JY_DOT_SEQ_MASK; }
 __device__ __forceinline__ u64 mkdot(u64 c, u64 q) { return (c << JY_DOT_SEQ_BITS) | q; }
 
-// first index in [lo, hi) with a[i] >= x
-__device__ __forceinline__ u64 lower_bound(const u64* __restrict__ a, u64 lo, u64 hi, u64 x) {
-  while (lo < hi) {
+// first index in [lo, hi) with a[i] >= x (a sorted): bisect down to 8
+// candidates, then load those at once and count -- one round trip for the
+// short segments of a typical document instead of one per level
+template <bool kRec>
+__device__ __forceinline__ u64 dot_at(const void* src, u64 i) {
+  return kRec ? static_cast<const URec*>(src)[i].dot : static_cast<const u64*>(src)[i];
+}
+template <bool kRec>
+__device__ __forceinline__ u64 lb_g(const void* src, u64 lo, u64 hi, u64 x) {
+  while (hi - lo > 8) {
     const u64 m = (lo + hi) >> 1;
-    if (a[m] < x) lo = m + 1;
+    if (dot_at<kRec>(src, m) < x) lo = m + 1;
     else hi = m;
   }
-  return lo;
+  if (lo >= hi) return lo;
+  const u64 n = hi - lo;
+  u32 c = 0;
+#pragma unroll
+  for (u32 j = 0; j < 8; j++) {
+    const u64 v = dot_at<kRec>(src, lo + (j < n ? j : 0));
+    c += (j < n) & (v < x);
+  }
+  return lo + c;
+}
+__device__ __forceinline__ u64 lower_bound(const u64* __restrict__ a, u64 lo, u64 hi, u64 x) {
+  return lb_g<false>(a, lo, hi, x);
 }
 __device__ __forceinline__ bool contains(const u64* __restrict__ a, u64 lo, u64 hi, u64 x) {
   const u64 i = lower_bound(a, lo, hi, x);
   return i < hi && a[i] == x;
-}
-// the same over the dots of element records
-__device__ __forceinline__ u64 lower_bound_rec(const URec* __restrict__ a, u64 lo, u64 hi, u64 x) {
-  while (lo < hi) {
-    const u64 m = (lo + hi) >> 1;
-    if (a[m].dot < x) lo = m + 1;
-    else hi = m;
-  }
-  return lo;
 }
 
 __device__ __forceinline__ URec load_rec(const URec* p) {
@@ -103,25 +122,23 @@ __device__ __forceinline__ void store_rec(URec* p, u64 d, u64 e) {
 
 struct UjArgs {
   // state
-  const UMeta* meta;
-  const URec* rec;    // element pool
-  const u64* cloud;   // cloud pool
+  UMeta* meta;
+  const URec* rec;   // element pool
+  const u64* cloud;  // cloud pool
   u64* vv;
+  URec* epool_out;
+  u64* cpool_out;
+  u64* ctr;          // bump pointers (device)
+  u64* pin;          // mapped pinned: [2..3] bump pointers after this converge
   u32 R;
-  // touched state: per delta doc its pool segments and flat offsets
-  u64* abase;
-  u64* asz;    // [nd + 1]
-  u64* ao;     // [nd + 1] exclusive scan of asz
-  u64* cbs;
-  u64* csz;    // [nd + 1]
-  u64* co;     // [nd + 1]
-  const u32* aseg;   // [ta] delta doc of each touched state element
-  const u32* acseg;  // [tc] delta doc of each touched state cloud dot
-  u64 ta, tc;
+  u32 epoch;
+  u64* dptr;         // [kcap] epoch << 32 | first delta doc of the slot
+  u32* bad;          // [nd] == epoch: skipped
+  unsigned long long* skipped;
+  u32* tick;
   // delta batch
   u64 nd, nb, cb, nvv;
   const u32* slot;
-  u32* dptr;
   const u64* deoff;
   const u64* ddots;
   const u64* delems;
@@ -129,462 +146,587 @@ struct UjArgs {
   const u64* dvv;
   const u64* dcoff;
   const u64* dcloud;
-  const u32* dseg;   // [nb] delta doc of each delta element
-  const u32* dcseg;  // [cb] delta doc of each delta cloud dot
-  const u32* vseg;   // [nvv] delta doc of each delta vv entry
-  // merge temporaries
-  u32* bad;  // [nd] malformed delta or repeated slot: the doc is left untouched
-  u64* vvs;  // [nd][R] the state's vv rows as they were before this converge
-  u64* vvd;  // [nd][R] the delta's own vv, dense
-  u64* vvm;  // [nd][R] max(vv_A, vv_B)
-  u64* vvn;  // [nd][R] after compaction
-  // keep flags, concatenated [flag_a (ta+1) | flag_b (nb+1) | cflag_b (cb+1)]
-  // and their exclusive scan in the same layout
-  u32* flag_a;
-  u32* flag_b;
-  u32* cflag_b;
-  const u32* scan_a;
-  const u32* scan_b;
-  const u32* cscan_b;
-  // cloud compaction survivors [keep_ca (tc+1) | keep_cb (cb+1)] + scan
-  u32* keep_ca;
-  u32* keep_cb;
-  const u32* kscan_a;
-  const u32* kscan_b;
-  unsigned long long* skipped;
+  // per delta doc
+  u64* abase;  // [nd] state element segment base
+  u64* cbs;    // [nd] state cloud segment base
+  u64* ao;     // [nd + 1] exclusive scan of the touched state element counts (ao[nd] = ta)
+  u64* co;     // [nd + 1] ... of the touched state cloud counts (co[nd] = tc)
+  u64* neo;    // [nd + 1] output offsets (elements)
+  u64* nco;    // [nd + 1] output offsets (cloud)
+  u64* base;   // [2] this converge's pool bases
+  u64* vvs;    // [nd][R] state vv rows as they were
+  u64* vvd;    // [nd][R] the delta's vv, dense (zero between converges)
+  u64* vvm;    // [nd][R] max(vvs, vvd)
+  u64* vvn;    // [nd][R] after compaction
+  // scans: sc over [state elements | delta elements | delta cloud], ksc over
+  // [state cloud | delta cloud]; tile-local exclusive prefixes (see ScanSp)
+  u32* sc;
+  u32* ksc;
+  // cross ranks (U2 / U3 -> U5): each item's merge position on the other
+  // side, relative to that side's segment start, so U5 needs no search
+  u32* xr;  // over the sc space
+  u32* kr;  // over the ksc space
+  // look-back status words
+  u64* st_ao;
+  u64* st_co;
+  // the doc of every item, per item space (written by U1's doc tiles):
+  // state elements, delta elements, state cloud, delta cloud
+  u32* sidA;
+  u32* sidB;
+  u32* sidC;
+  u32* sidD;
+  u64* tp;   // [tiles + 1] sc tile aggregates -> exclusive tile prefixes (U2 -> k_uj_tscan)
+  u64* ktp;  // ... of ksc
+  u64* st_ne;
+  u64* st_nc;
 };
 
-__device__ __forceinline__ bool in_state_ctx(const UjArgs& A, u32 k, u64 d) {
-  if (dseq(d) <= A.vvs[(u64)k * A.R + dcol(d)]) return true;
-  return contains(A.cloud, A.cbs[k], A.cbs[k] + A.csz[k], d);
-}
-__device__ __forceinline__ bool in_delta_ctx(const UjArgs& A, u32 k, u64 d) {
-  if (dseq(d) <= A.vvd[(u64)k * A.R + dcol(d)]) return true;
-  return contains(A.dcloud, A.dcoff[k], A.dcoff[k + 1], d);
-}
+__device__ __forceinline__ bool is_bad(const UjArgs& A, u64 k) { return A.bad[k] == A.epoch; }
+__device__ __forceinline__ void mark_bad(const UjArgs& A, u64 k) { A.bad[k] = A.epoch; }  // same value from every writer
 
-// ---- multi-range launches ---------------------------------------------------------
-// Up to 6 independent item ranges in one grid; each block belongs to one
-// range (block-uniform branch).
-struct Ranges {
-  u64 n[6];
-  u32 b0[7];  // first block of each range; b0[cnt] = grid size
-  int cnt;
+// A scan space of up to three kinds laid back to back, each cut into kTile
+// tiles from its own start.  U2 / U3 write each item's exclusive prefix
+// WITHIN its tile (loc) and each tile's total (tp); k_uj_tscan turns tp into
+// exclusive tile prefixes.  No tile waits for another (a decoupled look-back
+// would make every tile wait for its slowest predecessor's searches).
+__device__ __forceinline__ u64 cdiv(u64 a) { return (a + kTile - 1) / kTile; }
+struct ScanSp {
+  const u32* loc;
+  const u64* tp;
+  u64 b1, b2, n;   // kinds [0, b1) [b1, b2) [b2, n)
+  u64 t1, t2, tn;  // their first tiles; tile count
+  __device__ __forceinline__ u64 at(u64 j) const {  // global exclusive prefix at j (j <= n)
+    if (j >= n) return tp[tn];
+    const u64 t = j < b1 ? j / kTile : j < b2 ? t1 + (j - b1) / kTile : t2 + (j - b2) / kTile;
+    return tp[t] + loc[j];
+  }
 };
-
-__device__ __forceinline__ int range_of(const Ranges& G, u64& i) {
-  const u32 b = blockIdx.x;
-  int r = 0;
-  while (r + 1 < G.cnt && b >= G.b0[r + 1]) r++;
-  i = (u64)(b - G.b0[r]) * kThreads + threadIdx.x;
-  return r;
+__device__ __forceinline__ ScanSp sc_space(const UjArgs& A) {
+  const u64 ta = A.ao[A.nd];
+  const u64 t1 = cdiv(ta), t2 = t1 + cdiv(A.nb);
+  return ScanSp{A.sc, A.tp, ta, ta + A.nb, ta + A.nb + A.cb, t1, t2, t2 + cdiv(A.cb)};
+}
+__device__ __forceinline__ ScanSp ksc_space(const UjArgs& A) {
+  const u64 tc = A.co[A.nd];
+  const u64 t1 = cdiv(tc), tn = t1 + cdiv(A.cb);
+  return ScanSp{A.ksc, A.ktp, tc, tc + A.cb, tc + A.cb, t1, tn, tn};
 }
 
-// ---- P0: per (doc, column): repeated slots, touched-state sizes, vv rows ----------
-// dptr[] and bad[] are cleared before this launch.
-__global__ __launch_bounds__(kThreads) void k_uj_prep(UjArgs A) {
-  const u64 t = (u64)blockIdx.x * kThreads + threadIdx.x;
-  if (t >= A.nd * A.R) return;
-  const u64 k = t / A.R;
-  const u32 c = (u32)(t - k * A.R);
-  const u64 s = A.slot[k];
-  // the vv row and the meta are loaded before the claim's atomic round trip
-  const u64 v = A.vv[s * A.R + c];
-  A.vvs[t] = v;  // k_uj_scatter overwrites vv while it still tests the state context
-  A.vvm[t] = v;
-  A.vvd[t] = 0;
-  if (c == 0) {
-    const UMeta m = A.meta[s];
-    A.abase[k] = m.ebase;
-    A.asz[k] = m.elen;
-    A.cbs[k] = m.cbase;
-    A.csz[k] = m.clen;
-    const u32 prev = atomicCAS(A.dptr + s, kNone, (u32)k);
-    if (prev != kNone) {  // one delta per doc per call: both copies are skipped
-      A.bad[k] = 1;
-      A.bad[prev] = 1;
+__device__ __forceinline__ bool in_state_ctx(const UjArgs& A, u64 k, u64 d) {
+  if (dseq(d) <= A.vvs[k * A.R + dcol(d)]) return true;
+  return contains(A.cloud, A.cbs[k], A.cbs[k] + (A.co[k + 1] - A.co[k]), d);
+}
+
+// ---- tiles: the documents of an item range [i0, i1) of a CSR offs[0..nd],
+// staged in LDS (first wave searches; everyone loads); doc_of() per item
+struct TileDocs {
+  u64 k0, cnt;  // docs k0 .. k0 + cnt - 1 cover the range
+  bool lds;     // their offsets are staged in LDS
+};
+// waves 0 and 1 search the first and the last doc at once
+template <u64 kCap>
+__device__ __forceinline__ TileDocs tile_docs(const u64* offs, u64 nd, u64 i0, u64 i1, u64* lds, u64* sh) {
+  if (threadIdx.x < 128) {
+    const u64 k = jyscan::wave_last_le(offs, nd, threadIdx.x < 64 ? i0 : i1 - 1);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = k;
+  }
+  __syncthreads();
+  TileDocs T{sh[0], sh[1] - sh[0] + 1, sh[1] - sh[0] + 1 <= kCap};
+  if (T.lds)
+    for (u64 j = threadIdx.x; j <= T.cnt; j += kThreads) lds[j] = offs[T.k0 + j];
+  __syncthreads();
+  return T;
+}
+__device__ __forceinline__ u64 doc_of(const TileDocs& T, const u64* offs, const u64* lds, u64 i) {
+  if (T.lds) {
+    u32 lo = 0, hi = (u32)T.cnt - 1;
+    while (lo < hi) {
+      const u32 m = (lo + hi + 1) >> 1;
+      if (lds[m] <= i) lo = m;
+      else hi = m - 1;
     }
+    return T.k0 + lo;
   }
-  if (t == 0) {
-    A.asz[A.nd] = 0;
-    A.csz[A.nd] = 0;
+  u64 lo = T.k0, hi = T.k0 + T.cnt - 1;
+  while (lo < hi) {
+    const u64 m = (lo + hi + 1) >> 1;
+    if (offs[m] <= i) lo = m;
+    else hi = m - 1;
   }
+  return lo;
 }
 
-// ---- P1: delta vv scattered dense + validation of vv / dots / cloud ---------------
-__device__ __forceinline__ void vv_delta(const UjArgs& A, u64 j) {
-  const u32 k = A.vseg[j] & kSegMask;
-  const u64 x = A.dvv[j];
-  const u32 c = dcol(x);
-  if (c >= A.R || (j > A.dvoff[k] && dcol(A.dvv[j - 1]) >= c)) {
-    A.bad[k] = 1;
-    return;
-  }
-  A.vvd[(u64)k * A.R + c] = dseq(x);  // columns are unique in a well-formed doc
-}
-// strictly ascending, col < R, seq >= 1
-__device__ __forceinline__ void validate(const UjArgs& A, const u32* seg, const u64* offs, const u64* a, u64 j) {
-  const u32 k = seg[j] & kSegMask;
-  const u64 x = a[j];
-  bool ok = dcol(x) < A.R && dseq(x) >= 1;
-  if (j > offs[k] && a[j - 1] >= x) ok = false;
-  if (!ok) A.bad[k] = 1;
-}
-__global__ __launch_bounds__(kThreads) void k_uj_check(UjArgs A, Ranges G) {
-  u64 i;
-  const int r = range_of(G, i);
-  if (i >= G.n[r]) return;
-  if (r == 0) vv_delta(A, i);
-  else if (r == 1) validate(A, A.dseg, A.deoff, A.ddots, i);
-  else validate(A, A.dcseg, A.dcoff, A.dcloud, i);
+struct Shared {
+  u64 offs[kLdsDocs + 1];  // the CSR offsets of a tile's docs
+  u64 rng[8];
+  u64 sh[2];
+  u64 red[kThreads / 64];
+  u64 pre;
+  u32 tk;
+};
+
+// item kernels U2 / U3 / U5: one item per thread, a tile of kTile items per
+// workgroup, nothing staged -- full occupancy hides the searches' latency
+constexpr int kItemThreads = (int)kTile;
+
+// tile-local exclusive scan of one flag per thread; returns the tile total
+__device__ __forceinline__ u64 item_scan(u64 f, u64* red, u64& tot) {
+  return jyscan::block_excl<kItemThreads, u64>(f, red, tot);
 }
 
-// ---- P2: vv max; a malformed delta doc is counted (once per slot) ------------------
-__global__ __launch_bounds__(kThreads) void k_uj_drop_bad(UjArgs A) {
-  const u64 t = (u64)blockIdx.x * kThreads + threadIdx.x;
-  if (t >= A.nd * A.R) return;
-  const u64 a = A.vvm[t], b = A.vvd[t];
-  const u64 m = a > b ? a : b;
-  A.vvm[t] = m;
-  A.vvn[t] = m;
-  const u64 k = t / A.R;
-  if (t - k * A.R == 0 && A.bad[k] && A.dptr[A.slot[k]] == (u32)k) atomicAdd(A.skipped, 1ull);
+// exclusive scan of the tile totals of U2 (`which` 0) or U3 (1), in place,
+// total appended; one workgroup of 1024
+__global__ __launch_bounds__(1024) void k_uj_tscan(UjArgs A, int which) {
+  __shared__ u64 red[16];
+  const ScanSp sp = which == 0 ? sc_space(A) : ksc_space(A);
+  u64* tp = which == 0 ? A.tp : A.ktp;
+  const u64 n = sp.tn;
+  u64 carry = 0;
+  for (u64 c0 = 0; c0 < n; c0 += 1024 * 4) {
+    u64 v[4], sum = 0;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const u64 j = c0 + threadIdx.x * 4 + u;
+      v[u] = j < n ? tp[j] : 0;
+      sum += v[u];
+    }
+    u64 tot;
+    u64 off = jyscan::block_excl<1024, u64>(sum, red, tot) + carry;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const u64 j = c0 + threadIdx.x * 4 + u;
+      if (j < n) tp[j] = off;
+      off += v[u];
+    }
+    carry += tot;
+  }
+  if (threadIdx.x == 0) tp[n] = carry;
 }
 
-// ---- P3: keep flags: touched state elements, delta elements, delta cloud dedupe ----
-__device__ __forceinline__ void flag_a(const UjArgs& A, u64 i) {
-  if (i == A.ta) {
-    A.flag_a[i] = 0;
-    return;
+#ifdef JY_UJ_PROBE  // A/B only: per-tile clocks of U2..U4 (wall clock, 100 MHz)
+constexpr u32 kProbe = 32768;
+__device__ u64 g_probe[kProbe][6];
+__device__ u32 g_probe_n;
+__device__ __forceinline__ void probe(u32 kern, u32 kind, u32 t, u64 c0, u64 c1, u64 c2, u64 ca = 0, u64 cb = 0) {
+  if (threadIdx.x != 0) return;
+  const u32 j = atomicAdd(&g_probe_n, 1u);
+  if (j < kProbe) {
+    g_probe[j][0] = ((u64)kern << 56) | ((u64)kind << 48) | t;
+    g_probe[j][1] = c0;
+    g_probe[j][2] = c1;
+    g_probe[j][3] = c2;
+    g_probe[j][4] = ca;
+    g_probe[j][5] = cb;
   }
-  const u32 k = A.aseg[i] & kSegMask;
-  u32 keep = 0;
-  if (!A.bad[k]) {
-    const u64 d = A.rec[A.abase[k] + (i - A.ao[k])].dot;
-    keep = contains(A.ddots, A.deoff[k], A.deoff[k + 1], d) || !in_delta_ctx(A, k, d);
-  }
-  A.flag_a[i] = keep;
 }
-__device__ __forceinline__ void flag_b(const UjArgs& A, u64 j) {
-  if (j == A.nb) {
-    A.flag_b[j] = 0;
-    return;
-  }
-  const u32 k = A.dseg[j] & kSegMask;
-  u32 keep = 0;
-  if (!A.bad[k]) {
-    const u64 d = A.ddots[j];
-    const u64 lo = A.abase[k], hi = lo + A.asz[k];
-    const u64 p = lower_bound_rec(A.rec, lo, hi, d);
-    keep = !(p < hi && A.rec[p].dot == d) && !in_state_ctx(A, k, d);
-  }
-  A.flag_b[j] = keep;
-}
-// delta cloud dots that the state cloud also holds are dropped
-__device__ __forceinline__ void cloud_dedupe(const UjArgs& A, u64 j) {
-  if (j == A.cb) {
-    A.cflag_b[j] = 0;
-    return;
-  }
-  const u32 k = A.dcseg[j] & kSegMask;
-  u32 f = 0;
-  if (!A.bad[k]) f = !contains(A.cloud, A.cbs[k], A.cbs[k] + A.csz[k], A.dcloud[j]);
-  A.cflag_b[j] = f;
-}
-__global__ __launch_bounds__(kThreads) void k_uj_flags(UjArgs A, Ranges G) {
-  u64 i;
-  const int r = range_of(G, i);
-  if (i >= G.n[r]) return;
-  if (r == 0) flag_a(A, i);
-  else if (r == 1) flag_b(A, i);
-  else cloud_dedupe(A, i);
-}
+#define JY_CLK(v) const u64 v = wall_clock64()
+#define JY_PROBE(...) probe(__VA_ARGS__)
+#else
+#define JY_CLK(v)
+#define JY_PROBE(...)
+#endif
 
-// ---- P4: compaction against the merged vv ------------------------------------------
-// union rank of x (column c, seq q) above v: state dots of c in (v, q) plus
-// de-duplicated delta dots of c in (v, q)
-__device__ __forceinline__ void compact_a(const UjArgs& A, u64 i) {
-  if (i == A.tc) {
-    A.keep_ca[i] = 0;
+constexpr u64 kLongSeg = 256;  // longer segments get their doc ids from the whole workgroup
+struct LongSeg {
+  u64 off, sz;
+  u32 k, sp;
+};
+
+// ---- U1: per delta doc (ticketed doc tiles first, for the look-back) and
+// per delta item (validation, dense delta vv) ---------------------------------
+__global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_el, u64 t_cl, u64 t_vv) {
+  __shared__ Shared S;
+  __shared__ u32 l_slot[kDocTile];
+  __shared__ LongSeg l_long[4 * kDocTile];
+  __shared__ u32 l_nlong;
+  if (blockIdx.x < ndt) {  // doc tiles: ticketed (the look-back walks tickets)
+    if (threadIdx.x == 0) l_nlong = 0;
+    const u32 t = jyscan::ticket(A.tick + T_U1, &S.tk);
+    const u64 k = (u64)t * kDocTile + threadIdx.x;
+    u64 asz = 0, csz = 0;
+    if (k < A.nd) {
+      const u32 s = A.slot[k];
+      l_slot[threadIdx.x] = s;
+      const UMeta m = A.meta[s];
+      A.abase[k] = m.ebase;
+      A.cbs[k] = m.cbase;
+      asz = m.elen;
+      csz = m.clen;
+      // claim the slot for this converge (one delta per doc per call): a
+      // later copy marks both bad and does not count its size
+      const u64 mine = ((u64)A.epoch << 32) | (u32)k;
+      u64 old = A.dptr[s];
+      for (;;) {
+        if ((u32)(old >> 32) == A.epoch) {
+          mark_bad(A, k);
+          mark_bad(A, (u32)old);
+          asz = csz = 0;
+          break;
+        }
+        const u64 seen = atomicCAS((unsigned long long*)(A.dptr + s), (unsigned long long)old,
+                                   (unsigned long long)mine);
+        if (seen == old) break;
+        old = seen;
+      }
+    }
+    u64 tot;
+    const u64 xa = jyscan::block_excl<kThreads, u64>(asz, S.red, tot);
+    const u64 pa = jyscan::lookback(A.st_ao, t, A.epoch, tot, &S.pre);
+    if (k < A.nd) A.ao[k] = pa + xa;
+    if (t == ndt - 1 && threadIdx.x == 0) {
+      A.ao[A.nd] = pa + tot;
+    }
+    const u64 xc = jyscan::block_excl<kThreads, u64>(csz, S.red, tot);
+    const u64 pc = jyscan::lookback(A.st_co, t, A.epoch, tot, &S.pre);
+    if (k < A.nd) {
+      A.co[k] = pc + xc;
+      // per-item doc ids: a doc writes its own short segments; long ones are
+      // queued for the whole workgroup
+      auto ids = [&](int sp, u32* sid, u64 off, u64 sz) {
+        if (sz <= kLongSeg) {
+          for (u64 j = 0; j < sz; j++) sid[off + j] = (u32)k;
+        } else {
+          const u32 q = atomicAdd(&l_nlong, 1u);
+          l_long[q] = LongSeg{off, sz, (u32)k, (u32)sp};
+        }
+      };
+      ids(0, A.sidA, pa + xa, asz);
+      ids(2, A.sidC, pc + xc, csz);
+      const u64 b0 = A.deoff[k], d0 = A.dcoff[k];
+      ids(1, A.sidB, b0, A.deoff[k + 1] - b0);
+      ids(3, A.sidD, d0, A.dcoff[k + 1] - d0);
+    }
+    if (t == ndt - 1 && threadIdx.x == 0) {
+      A.co[A.nd] = pc + tot;
+    }
+    __syncthreads();
+    for (u32 q = 0; q < l_nlong; q++) {
+      const LongSeg g = l_long[q];
+      u32* sid = g.sp == 0 ? A.sidA : g.sp == 1 ? A.sidB : g.sp == 2 ? A.sidC : A.sidD;
+      for (u64 j = threadIdx.x; j < g.sz; j += kThreads) sid[g.off + j] = g.k;
+    }
+    // the state vv rows (lanes on consecutive columns of a row), then the
+    // merged rows max(state, delta) from the docs' sparse delta vv entries
+    const u64 kt0 = (u64)t * kDocTile;
+    for (u64 j = threadIdx.x; j < kDocTile * A.R; j += kThreads) {
+      const u64 dk = j / A.R, c = j - dk * A.R;
+      if (kt0 + dk < A.nd) {
+        const u64 v = A.vv[(u64)l_slot[dk] * A.R + c], g = (kt0 + dk) * A.R + c;
+        A.vvs[g] = v;
+        A.vvm[g] = v;
+        A.vvn[g] = v;
+      }
+    }
+    const u64 kt1 = kt0 + kDocTile < A.nd ? kt0 + kDocTile : A.nd;
+    for (u64 j = threadIdx.x; j <= kt1 - kt0; j += kThreads) S.offs[j] = A.dvoff[kt0 + j];
+    __syncthreads();
+    for (u64 j = S.offs[0] + threadIdx.x; j < S.offs[kt1 - kt0]; j += kThreads) {
+      u32 lo = 0, hi = (u32)(kt1 - kt0 - 1);  // the doc of entry j
+      while (lo < hi) {
+        const u32 m = (lo + hi + 1) >> 1;
+        if (S.offs[m] <= j) lo = m;
+        else hi = m - 1;
+      }
+      const u64 x = A.dvv[j];
+      const u32 c = dcol(x);
+      if (c >= A.R) continue;  // a bad doc (U1 item tiles mark it)
+      const u64 g = (kt0 + lo) * A.R + c;
+      if (dseq(x) > A.vvm[g]) {  // one entry per (doc, column) unless the doc is bad
+        A.vvm[g] = dseq(x);
+        A.vvn[g] = dseq(x);
+      }
+    }
     return;
   }
-  const u32 k = A.acseg[i] & kSegMask;
-  if (A.bad[k]) {
-    A.keep_ca[i] = 0;
+  // delta items: strictly ascending dots per doc, col < R, seq >= 1; vv
+  // entries ascending by column
+  u64 tt = blockIdx.x - ndt;
+  const u64* offs;
+  u64 n;
+  int kind;
+  if (tt < t_el) {
+    kind = 0;
+    offs = A.deoff;
+    n = A.nb;
+  } else if ((tt -= t_el) < t_cl) {
+    kind = 1;
+    offs = A.dcoff;
+    n = A.cb;
+  } else if ((tt -= t_cl) < t_vv) {
+    kind = 2;
+    offs = A.dvoff;
+    n = A.nvv;
+  } else {
     return;
   }
-  const u64 lo0 = A.cbs[k];
-  const u64 pi = lo0 + (i - A.co[k]);
-  const u64 x = A.cloud[pi];
-  const u32 c = dcol(x);
-  const u64 q = dseq(x), v = A.vvm[(u64)k * A.R + c];
-  u32 keep = 0;
-  if (q > v) {
-    const u64 lo = mkdot(c, v + 1);
-    const u64 ra = pi - lower_bound(A.cloud, lo0, pi, lo);
-    const u64 blo = A.dcoff[k], bhi = A.dcoff[k + 1];
-    const u64 b0 = lower_bound(A.dcloud, blo, bhi, lo);
-    const u64 b1 = lower_bound(A.dcloud, b0, bhi, x);
-    const u64 rb = A.cscan_b[b1] - A.cscan_b[b0];
-    if (q == v + 1 + ra + rb) {
-      __hip_atomic_fetch_max(&A.vvn[(u64)k * A.R + c], q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const u64 i0 = tt * kTile1, i1 = i0 + kTile1 < n ? i0 + kTile1 : n;
+  const TileDocs T = tile_docs<kLdsDocs>(offs, A.nd, i0, i1, S.offs, S.sh);
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {
+    const u64 i = i0 + (u64)u * kThreads + threadIdx.x;
+    if (i >= i1) continue;
+    const u64 k = doc_of(T, offs, S.offs, i);
+    if (kind == 2) {
+      const u64 x = A.dvv[i];
+      const u32 c = dcol(x);
+      if (c >= A.R || (i > A.dvoff[k] && dcol(A.dvv[i - 1]) >= c)) {
+        mark_bad(A, k);
+        continue;
+      }
+      A.vvd[k * A.R + c] = dseq(x);
     } else {
-      keep = 1;
+      const u64* a = kind == 0 ? A.ddots : A.dcloud;
+      const u64 x = a[i];
+      if (dcol(x) >= A.R || dseq(x) < 1 || (i > offs[k] && a[i - 1] >= x)) mark_bad(A, k);
     }
   }
-  A.keep_ca[i] = keep;
 }
-__device__ __forceinline__ void compact_b(const UjArgs& A, u64 j) {
-  if (j == A.cb) {
-    A.keep_cb[j] = 0;
-    return;
+
+// ---- U2: keep flags + cross ranks ----------------------------------------------
+// kind 0: state elements (kept unless the delta saw them and lacks them);
+// kind 1: delta elements (added unless the state holds or saw them); kind 2:
+// delta cloud dots (dropped when the state cloud holds them).  The cross
+// rank of an item is its merge position on the other side (relative to that
+// side's segment of the doc); bit 31 of a state element's rank: U5 takes the
+// delta's element for it.
+__global__ __launch_bounds__(kItemThreads) void k_uj_flags(UjArgs A) {
+  __shared__ u64 red[kItemThreads / 64];
+  const u64 ta = A.ao[A.nd];
+  const u64 tA = cdiv(ta), tB = cdiv(A.nb), tC = cdiv(A.cb);
+  const u64 t = blockIdx.x;  // the grid is the host's bound: surplus workgroups exit
+  if (t >= tA + tB + tC) return;
+  JY_CLK(c0);
+  int kind;
+  u64 lt, n, gbase;
+  const u32* sid;
+  if (t < tA) {
+    kind = 0, lt = t, n = ta, gbase = 0, sid = A.sidA;
+  } else if (t < tA + tB) {
+    kind = 1, lt = t - tA, n = A.nb, gbase = ta, sid = A.sidB;
+  } else {
+    kind = 2, lt = t - tA - tB, n = A.cb, gbase = ta + A.nb, sid = A.sidD;
   }
-  u32 keep = 0;
-  if (A.cflag_b[j]) {  // (0 for malformed docs)
-    const u32 k = A.dcseg[j] & kSegMask;
-    const u64 x = A.dcloud[j];
-    const u32 c = dcol(x);
-    const u64 q = dseq(x), v = A.vvm[(u64)k * A.R + c];
-    if (q > v) {
-      const u64 lo = mkdot(c, v + 1);
-      const u64 alo = A.cbs[k], ahi = alo + A.csz[k];
-      const u64 a0 = lower_bound(A.cloud, alo, ahi, lo);
-      const u64 ra = lower_bound(A.cloud, a0, ahi, x) - a0;
-      const u64 b0 = lower_bound(A.dcloud, A.dcoff[k], j, lo);
-      const u64 rb = A.cscan_b[j] - A.cscan_b[b0];
-      if (q == v + 1 + ra + rb) {
-        __hip_atomic_fetch_max(&A.vvn[(u64)k * A.R + c], q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const u64 i = lt * kTile + threadIdx.x;
+  u64 f = 0;
+  if (i < n) {
+    const u64 k = sid[i];
+    if (!is_bad(A, k)) {
+      const u64 clo = A.cbs[k], chi = clo + (A.co[k + 1] - A.co[k]);
+      u32 xr;
+      if (kind == 0) {
+        const u64 d = A.rec[A.abase[k] + (i - A.ao[k])].dot;
+        const u64 lo = A.deoff[k], hi = A.deoff[k + 1];
+        const u64 p = lower_bound(A.ddots, lo, hi, d);
+        xr = (u32)(p - lo);
+        if (p < hi && A.ddots[p] == d) {
+          f = 1;
+          if (!in_state_ctx(A, k, d)) xr |= 1u << 31;
+        } else {
+          f = !(dseq(d) <= A.vvd[k * A.R + dcol(d)] || contains(A.dcloud, A.dcoff[k], A.dcoff[k + 1], d));
+        }
+      } else if (kind == 1) {
+        const u64 d = A.ddots[i];
+        const u64 lo = A.abase[k], hi = lo + (A.ao[k + 1] - A.ao[k]);
+        const u64 p = lb_g<true>(A.rec, lo, hi, d);
+        xr = (u32)(p - lo);
+        f = !(p < hi && A.rec[p].dot == d) && !(dseq(d) <= A.vvs[k * A.R + dcol(d)] || contains(A.cloud, clo, chi, d));
       } else {
-        keep = 1;
+        const u64 x = A.dcloud[i];
+        const u64 p = lower_bound(A.cloud, clo, chi, x);
+        xr = (u32)(p - clo);
+        f = !(p < chi && A.cloud[p] == x);
+      }
+      A.xr[gbase + i] = xr;
+    }
+  }
+  JY_CLK(c1);
+  u64 tot;
+  const u64 x = item_scan(f, red, tot);
+  JY_CLK(c2);
+  JY_PROBE(2, kind, (u32)t, c0, c1, c2);
+  if (i < n) A.sc[gbase + i] = (u32)x;
+  if (threadIdx.x == 0) A.tp[t] = tot;
+}
+
+// ---- U3: cloud compaction against the merged vv ---------------------------------
+// union rank of x (column c, seq q) above v: state dots of c in (v, q) plus
+// de-duplicated delta dots of c in (v, q) (U2's kind-2 flags); x folds into
+// the vv when the run from v + 1 reaches it unbroken
+__global__ __launch_bounds__(kItemThreads) void k_uj_compact(UjArgs A) {
+  __shared__ u64 red[kItemThreads / 64];
+  const u64 ta = A.ao[A.nd], tc = A.co[A.nd];
+  const ScanSp sp = sc_space(A);
+  const u64 cb0 = ta + A.nb;  // the delta cloud dedupe prefix: sp.at(cb0 + b)
+  const u64 tA = cdiv(tc), tB = cdiv(A.cb);
+  const u64 t = blockIdx.x;
+  if (t >= tA + tB) return;
+  JY_CLK(c0);
+  const bool sa = t < tA;  // state cloud items, else delta cloud items
+  const u64 lt = sa ? t : t - tA, n = sa ? tc : A.cb, gbase = sa ? 0 : tc;
+  const u64 i = lt * kTile + threadIdx.x;
+  u64 f = 0;
+  if (i < n) {
+    const u64 k = sa ? A.sidC[i] : A.sidD[i];
+    if (!is_bad(A, k)) {
+      const u64 alo = A.cbs[k], ahi = alo + (A.co[k + 1] - A.co[k]);
+      const u64 blo = A.dcoff[k], bhi = A.dcoff[k + 1];
+      if (sa) {
+        const u64 pi = alo + (i - A.co[k]);
+        const u64 x = A.cloud[pi];
+        const u32 c = dcol(x);
+        const u64 q = dseq(x), v = A.vvm[k * A.R + c];
+        if (q > v) {
+          const u64 lo = mkdot(c, v + 1);
+          const u64 ra = pi - lower_bound(A.cloud, alo, pi, lo);
+          const u64 b0 = lower_bound(A.dcloud, blo, bhi, lo);
+          const u64 b1 = lower_bound(A.dcloud, b0, bhi, x);
+          const u64 rb = sp.at(cb0 + b1) - sp.at(cb0 + b0);
+          if (q == v + 1 + ra + rb) {
+            __hip_atomic_fetch_max(&A.vvn[k * A.R + c], q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else {
+            f = 1;
+            A.kr[i] = (u32)(b1 - blo);
+          }
+        }
+      } else {
+        const u64 s0 = sp.at(cb0 + i);
+        if (sp.at(cb0 + i + 1) != s0) {  // not held by the state cloud
+          const u64 x = A.dcloud[i];
+          const u32 c = dcol(x);
+          const u64 q = dseq(x), v = A.vvm[k * A.R + c];
+          if (q > v) {
+            const u64 lo = mkdot(c, v + 1);
+            const u64 a0 = lower_bound(A.cloud, alo, ahi, lo);
+            const u64 a1 = lower_bound(A.cloud, a0, ahi, x);
+            const u64 b0 = lower_bound(A.dcloud, blo, i, lo);
+            const u64 rb = s0 - sp.at(cb0 + b0);
+            if (q == v + 1 + (a1 - a0) + rb) {
+              __hip_atomic_fetch_max(&A.vvn[k * A.R + c], q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+              f = 1;
+              A.kr[tc + i] = (u32)(a1 - alo);
+            }
+          }
+        }
       }
     }
   }
-  A.keep_cb[j] = keep;
-}
-__global__ __launch_bounds__(kThreads) void k_uj_compact(UjArgs A, Ranges G) {
-  u64 i;
-  const int r = range_of(G, i);
-  if (i >= G.n[r]) return;
-  if (r == 0) compact_a(A, i);
-  else compact_b(A, i);
+  JY_CLK(c1);
+  u64 tot;
+  const u64 x = item_scan(f, red, tot);
+  JY_CLK(c2);
+  JY_PROBE(3, sa ? 0 : 1, (u32)t, c0, c1, c2);
+  if (i < n) A.ksc[gbase + i] = (u32)x;
+  if (threadIdx.x == 0) A.ktp[t] = tot;
 }
 
-// ---- P5: per delta doc output sizes ------------------------------------------------
-__global__ __launch_bounds__(kThreads) void k_uj_sizes_out(UjArgs A, u64* __restrict__ ne, u64* __restrict__ nc) {
-  const u64 k = (u64)blockIdx.x * kThreads + threadIdx.x;
-  if (k > A.nd) return;
-  if (k == A.nd || A.bad[k]) {
-    ne[k] = 0;
-    nc[k] = 0;
+// ---- U4: output sizes per delta doc (scanned); the bump pointers move --------------
+__global__ __launch_bounds__(kThreads) void k_uj_sizes(UjArgs A, u64 ndt) {
+  __shared__ Shared S;
+  const u32 t = jyscan::ticket(A.tick + T_U4, &S.tk);
+  if (t >= ndt) return;
+  const u64 ta = A.ao[A.nd], tc = A.co[A.nd];
+  const ScanSp sp = sc_space(A), kp = ksc_space(A);
+  const u64 k = (u64)t * kDocTile + threadIdx.x;
+  JY_CLK(c0);
+  u64 ne = 0, nc = 0;
+  if (k < A.nd && is_bad(A, k) && A.dptr[A.slot[k]] == (((u64)A.epoch << 32) | (u32)k))
+    atomicAdd(A.skipped, 1ull);  // a bad doc counted once per slot
+  if (k < A.nd && !is_bad(A, k)) {
+    ne = (sp.at(A.ao[k + 1]) - sp.at(A.ao[k])) + (sp.at(ta + A.deoff[k + 1]) - sp.at(ta + A.deoff[k]));
+    nc = (kp.at(A.co[k + 1]) - kp.at(A.co[k])) + (kp.at(tc + A.dcoff[k + 1]) - kp.at(tc + A.dcoff[k]));
+  }
+  u64 tot;
+  const u64 xe = jyscan::block_excl<kThreads, u64>(ne, S.red, tot);
+  const u64 pe = jyscan::lookback(A.st_ne, t, A.epoch, tot, &S.pre);
+  const u64 te = pe + tot;
+  if (k < A.nd) A.neo[k] = pe + xe;
+  const u64 xc = jyscan::block_excl<kThreads, u64>(nc, S.red, tot);
+  const u64 pc = jyscan::lookback(A.st_nc, t, A.epoch, tot, &S.pre);
+  if (k < A.nd) A.nco[k] = pc + xc;
+  JY_CLK(c2);
+  JY_PROBE(4, 0, t, c0, c0, c2);
+  if (t == ndt - 1 && threadIdx.x == 0) {
+    const u64 tcl = pc + tot;
+    A.neo[A.nd] = te;
+    A.nco[A.nd] = tcl;
+    const u64 eb = A.ctr[0], cbb = A.ctr[1];
+    A.base[0] = eb;
+    A.base[1] = cbb;
+    A.ctr[0] = eb + te;
+    A.ctr[1] = cbb + tcl;
+    A.pin[0] = eb + te;  // mapped host memory: the host's exact pool use once the converge is done
+    A.pin[1] = cbb + tcl;
+  }
+}
+
+// ---- U5: scatter into the fresh runs; vv rows, metas; zero state for the next converge
+// (no scan: one item per thread; the grid is the host's bound, surplus
+// workgroups exit at once)
+__global__ __launch_bounds__(kItemThreads) void k_uj_scatter(UjArgs A) {
+  const u64 ta = A.ao[A.nd], tc = A.co[A.nd];
+  const ScanSp sp = sc_space(A), kp = ksc_space(A);
+  const u32* xrb = A.xr + ta;
+  const u32* krb = A.kr + tc;
+  const u64 nv = A.nd * A.R;
+  const u64 tl[6] = {cdiv(ta), cdiv(A.nb), cdiv(tc), cdiv(A.cb), cdiv(nv), cdiv(A.nd)};
+  const u64 t = blockIdx.x;
+  if (t == 0 && threadIdx.x == 0)
+    for (int c = T_U1; c <= T_U4; c++) A.tick[c] = 0;  // U1..U4 of this converge are done
+  int kind = 0;
+  u64 lt = t;
+  while (kind < 6 && lt >= tl[kind]) lt -= tl[kind++];
+  if (kind == 6) return;
+  const u64 i = lt * kTile + threadIdx.x;
+  const u64 eb0 = A.base[0], cb0 = A.base[1];
+  if (kind == 4) {  // vv rows back into the state; the dense delta vv back to zero
+    if (i >= nv) return;
+    const u64 k = i / A.R, c = i - k * A.R;
+    if (!is_bad(A, k)) A.vv[(u64)A.slot[k] * A.R + c] = A.vvn[i];
+    A.vvd[i] = 0;
     return;
   }
-  ne[k] = (A.scan_a[A.ao[k + 1]] - A.scan_a[A.ao[k]]) + (A.scan_b[A.deoff[k + 1]] - A.scan_b[A.deoff[k]]);
-  nc[k] = (A.kscan_a[A.co[k + 1]] - A.kscan_a[A.co[k]]) + (A.kscan_b[A.dcoff[k + 1]] - A.kscan_b[A.dcoff[k]]);
-}
-
-// ---- P6: scatter into fresh pool runs (merge-path positions) + vv / meta store -----
-struct Out {
-  const u64* neo;  // exclusive scans of the per-doc output sizes
-  const u64* nco;
-  URec* epool;
-  u64* cpool;
-  UMeta* meta;
-  u64 eb0, cb0;  // bump pointers: this converge's runs start here
-};
-
-__device__ __forceinline__ void scatter_a(const UjArgs& A, const Out& O, u64 i) {
-  if (!A.flag_a[i]) return;
-  const u32 k = A.aseg[i] & kSegMask;
-  const URec x = load_rec(A.rec + A.abase[k] + (i - A.ao[k]));
-  u64 e = x.elem;
-  u64 pos = O.neo[k] + (A.scan_a[i] - A.scan_a[A.ao[k]]);
-  const u64 lo = A.deoff[k], hi = A.deoff[k + 1];
-  const u64 p = lower_bound(A.ddots, lo, hi, x.dot);
-  pos += A.scan_b[p] - A.scan_b[lo];
-  if (p < hi && A.ddots[p] == x.dot && !in_state_ctx(A, k, x.dot)) e = A.delems[p];
-  store_rec(O.epool + O.eb0 + pos, x.dot, e);
-}
-__device__ __forceinline__ void scatter_b(const UjArgs& A, const Out& O, u64 j) {
-  if (!A.flag_b[j]) return;
-  const u32 k = A.dseg[j] & kSegMask;
-  const u64 d = A.ddots[j];
-  const u64 lo = A.abase[k];
-  const u64 pa = A.ao[k] + (lower_bound_rec(A.rec, lo, lo + A.asz[k], d) - lo);
-  const u64 pos = O.neo[k] + (A.scan_b[j] - A.scan_b[A.deoff[k]]) + (A.scan_a[pa] - A.scan_a[A.ao[k]]);
-  store_rec(O.epool + O.eb0 + pos, d, A.delems[j]);
-}
-__device__ __forceinline__ void cscatter_a(const UjArgs& A, const Out& O, u64 i) {
-  if (!A.keep_ca[i]) return;
-  const u32 k = A.acseg[i] & kSegMask;
-  const u64 x = A.cloud[A.cbs[k] + (i - A.co[k])];
-  const u64 lo = A.dcoff[k];
-  const u64 pos = O.nco[k] + (A.kscan_a[i] - A.kscan_a[A.co[k]]) +
-                  (A.kscan_b[lower_bound(A.dcloud, lo, A.dcoff[k + 1], x)] - A.kscan_b[lo]);
-  O.cpool[O.cb0 + pos] = x;
-}
-__device__ __forceinline__ void cscatter_b(const UjArgs& A, const Out& O, u64 j) {
-  if (!A.keep_cb[j]) return;
-  const u32 k = A.dcseg[j] & kSegMask;
-  const u64 x = A.dcloud[j];
-  const u64 lo = A.cbs[k];
-  const u64 pa = A.co[k] + (lower_bound(A.cloud, lo, lo + A.csz[k], x) - lo);
-  const u64 pos = O.nco[k] + (A.kscan_b[j] - A.kscan_b[A.dcoff[k]]) + (A.kscan_a[pa] - A.kscan_a[A.co[k]]);
-  O.cpool[O.cb0 + pos] = x;
-}
-// merged + compacted vv rows back into the state; column 0 repoints the doc
-__device__ __forceinline__ void vv_store(const UjArgs& A, const Out& O, u64 t) {
-  const u64 k = t / A.R;
-  const u32 c = (u32)(t - k * A.R);
-  if (A.bad[k]) return;
-  const u64 s = A.slot[k];
-  A.vv[s * A.R + c] = A.vvn[t];
-  if (c == 0) {
-    const u32 ne = (u32)(O.neo[k + 1] - O.neo[k]), nc = (u32)(O.nco[k + 1] - O.nco[k]);
-    O.meta[s] = UMeta{O.eb0 + O.neo[k], ne, ne, O.cb0 + O.nco[k], nc, nc};
+  if (kind == 5) {  // metas
+    if (i >= A.nd || is_bad(A, i)) return;
+    const u32 ne = (u32)(A.neo[i + 1] - A.neo[i]), nc = (u32)(A.nco[i + 1] - A.nco[i]);
+    A.meta[A.slot[i]] = UMeta{eb0 + A.neo[i], ne, ne, cb0 + A.nco[i], nc, nc};
+    return;
   }
-}
-__global__ __launch_bounds__(kThreads) void k_uj_scatter(UjArgs A, Out O, Ranges G) {
-  u64 i;
-  const int r = range_of(G, i);
-  if (i >= G.n[r]) return;
-  switch (r) {
-    case 0: vv_store(A, O, i); break;
-    case 1: scatter_a(A, O, i); break;
-    case 2: scatter_b(A, O, i); break;
-    case 3: cscatter_a(A, O, i); break;
-    default: cscatter_b(A, O, i); break;
-  }
-}
-
-__global__ void k_uj_bump(u64* __restrict__ ctr, const u64* __restrict__ neo, const u64* __restrict__ nco, u64 nd,
-                          u64 eb0, u64 cb0) {
-  ctr[0] = eb0 + neo[nd];
-  ctr[1] = cb0 + nco[nd];
-}
-
-// ---- segment ids of up to 5 CSRs over the same docs, one scan ----------------------
-// mark the first item of every non-empty segment with (range << 28 | doc);
-// an inclusive max-scan carries it on (each range starts with a mark, and
-// marks grow with the range)
-struct SegSrc {
-  const u64* o[5];
-  u64 base[5];  // first item of each range in the concatenation
-};
-__global__ __launch_bounds__(kThreads) void k_uj_seg_starts(SegSrc S, u64 nseg, u32* __restrict__ out) {
-  const u64 k = (u64)blockIdx.x * kThreads + threadIdx.x;
-  if (k >= nseg) return;
-#pragma unroll
-  for (u32 r = 0; r < 5; r++)
-    if (S.o[r][k] < S.o[r][k + 1]) out[S.base[r] + S.o[r][k]] = (r << kSegBits) | (u32)k;
-}
-
-// The max-scan that carries the marks on, one 4096-item tile per workgroup
-// with no inter-tile pass: a tile's carry-in is the segment of its first
-// item, found by one binary search over that range's offsets (the last
-// document whose segment starts at or before it), so every tile scans alone.
-constexpr int kFillPer = 16;
-constexpr u64 kFillTile = (u64)kThreads * kFillPer;
-__global__ __launch_bounds__(kThreads) void k_uj_seg_fill(SegSrc S, u64 nseg, u32* __restrict__ a, u64 n) {
-  typedef hipcub::BlockScan<u32, kThreads> Scan;
-  typedef hipcub::BlockLoad<u32, kThreads, kFillPer, hipcub::BLOCK_LOAD_WARP_TRANSPOSE> Load;
-  typedef hipcub::BlockStore<u32, kThreads, kFillPer, hipcub::BLOCK_STORE_WARP_TRANSPOSE> Store;
-  __shared__ union {
-    typename Scan::TempStorage scan;
-    typename Load::TempStorage load;
-    typename Store::TempStorage store;
-  } tmp;
-  __shared__ u32 carry;
-  const u64 t0 = (u64)blockIdx.x * kFillTile;
-  if (threadIdx.x < 64) {
-    // 64-ary search by the first wave: each round every lane tests one
-    // candidate and a ballot keeps the last one that passes (3 dependent
-    // loads for 2^18 documents instead of 18)
-    u32 r = 4;
-    while (r > 0 && S.base[r] > t0) r--;
-    const u64 local = t0 - S.base[r];
-    const u64* o = S.o[r];
-    const u32 lane = threadIdx.x;
-    u64 lo = 0, hi = nseg;  // the last doc k with o[k] <= local lies in [lo, hi]
-    while (lo < hi) {
-      const u64 step = (hi - lo + 63) / 64;
-      const u64 c = lo + (u64)(lane + 1) * step;
-      const u64 pass = __ballot(c <= hi && o[c] <= local);  // a prefix of the lanes
-      const u64 nlo = lo + (u64)__popcll(pass) * step;
-      hi = nlo + step - 1 < hi ? nlo + step - 1 : hi;
-      lo = nlo;
-    }
-    if (lane == 0) carry = (r << kSegBits) | (u32)lo;
-  }
-  // coalesced tile load, transposed through LDS into a blocked arrangement
-  u32 v[kFillPer];
-  const int valid = (int)(n - t0 < kFillTile ? n - t0 : kFillTile);
-  Load(tmp.load).Load(a + t0, v, valid, 0u);
-  __syncthreads();
-  Scan(tmp.scan).InclusiveScan(v, v, hipcub::Max());
-  __syncthreads();
-  const u32 c = carry;
-#pragma unroll
-  for (int u = 0; u < kFillPer; u++) v[u] = v[u] > c ? v[u] : c;
-  Store(tmp.store).Store(a + t0, v, valid);
-}
-
-// ---- exclusive scans by tiles (the per-document size pairs, the keep flags) ---------
-// reduce-then-scan: k_tile_sums sums each 4096-item tile of every array;
-// k_tile_scan adds up the sums of the tiles before its own (a few hundred at
-// most for these batches) and scans its tile.  Two launches for up to two
-// arrays, against two rocprim launches per array.
-template <typename T>
-struct ScanJob {
-  const T* in[2];
-  T* out[2];
-};
-template <typename T, int NA>
-__global__ __launch_bounds__(kThreads) void k_tile_sums(ScanJob<T> J, u64 n, T* __restrict__ sums) {
-  typedef hipcub::BlockReduce<T, kThreads> Red;
-  __shared__ typename Red::TempStorage tmp;
-  const u64 t0 = (u64)blockIdx.x * kFillTile;
-#pragma unroll
-  for (int x = 0; x < NA; x++) {
-    T acc = 0;
-#pragma unroll 4
-    for (u64 i = t0 + threadIdx.x; i < t0 + kFillTile && i < n; i += kThreads) acc += J.in[x][i];
-    acc = Red(tmp).Sum(acc);
-    if (threadIdx.x == 0) sums[(u64)NA * blockIdx.x + x] = acc;
-    __syncthreads();
-  }
-}
-template <typename T, int NA>
-__global__ __launch_bounds__(kThreads) void k_tile_scan(ScanJob<T> J, u64 n, const T* __restrict__ sums) {
-  typedef hipcub::BlockReduce<T, kThreads> Red;
-  typedef hipcub::BlockScan<T, kThreads> Scan;
-  typedef hipcub::BlockLoad<T, kThreads, kFillPer, hipcub::BLOCK_LOAD_WARP_TRANSPOSE> Load;
-  typedef hipcub::BlockStore<T, kThreads, kFillPer, hipcub::BLOCK_STORE_WARP_TRANSPOSE> Store;
-  __shared__ union {
-    typename Red::TempStorage red;
-    typename Scan::TempStorage scan;
-    typename Load::TempStorage load;
-    typename Store::TempStorage store;
-  } tmp;
-  __shared__ T carry;
-  const u64 t0 = (u64)blockIdx.x * kFillTile;
-  const int valid = (int)(n - t0 < kFillTile ? n - t0 : kFillTile);
-#pragma unroll
-  for (int x = 0; x < NA; x++) {
-    T c = 0;
-    for (u32 j = threadIdx.x; j < blockIdx.x; j += kThreads) c += sums[(u64)NA * j + x];
-    c = Red(tmp.red).Sum(c);
-    if (threadIdx.x == 0) carry = c;
-    __syncthreads();
-    c = carry;
-    T v[kFillPer];
-    Load(tmp.load).Load(J.in[x] + t0, v, valid, (T)0);
-    __syncthreads();
-    Scan(tmp.scan).ExclusiveSum(v, v);
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < kFillPer; u++) v[u] += c;
-    Store(tmp.store).Store(J.out[x] + t0, v, valid);
-    __syncthreads();
+  if (kind == 0) {  // state element
+    if (i >= ta) return;
+    const u64 si = sp.at(i);
+    if (sp.at(i + 1) == si) return;
+    const u64 k = A.sidA[i];
+    const URec x = load_rec(A.rec + A.abase[k] + (i - A.ao[k]));
+    const u32 xv = A.xr[i];
+    const u64 lo = A.deoff[k], p = lo + (xv & 0x7FFFFFFFu);
+    const u64 pos = A.neo[k] + (si - sp.at(A.ao[k])) + (sp.at(ta + p) - sp.at(ta + lo));
+    store_rec(A.epool_out + eb0 + pos, x.dot, (xv >> 31) ? A.delems[p] : x.elem);
+  } else if (kind == 1) {  // delta element
+    if (i >= A.nb) return;
+    const u64 si = sp.at(ta + i);
+    if (sp.at(ta + i + 1) == si) return;
+    const u64 k = A.sidB[i];
+    const u64 pa = A.ao[k] + xrb[i];
+    const u64 pos = A.neo[k] + (si - sp.at(ta + A.deoff[k])) + (sp.at(pa) - sp.at(A.ao[k]));
+    store_rec(A.epool_out + eb0 + pos, A.ddots[i], A.delems[i]);
+  } else if (kind == 2) {  // state cloud dot
+    if (i >= tc) return;
+    const u64 si = kp.at(i);
+    if (kp.at(i + 1) == si) return;
+    const u64 k = A.sidC[i];
+    const u64 x = A.cloud[A.cbs[k] + (i - A.co[k])];
+    const u64 lo = A.dcoff[k];
+    const u64 pos = A.nco[k] + (si - kp.at(A.co[k])) + (kp.at(tc + lo + A.kr[i]) - kp.at(tc + lo));
+    A.cpool_out[cb0 + pos] = x;
+  } else {  // delta cloud dot
+    if (i >= A.cb) return;
+    const u64 si = kp.at(tc + i);
+    if (kp.at(tc + i + 1) == si) return;
+    const u64 k = A.sidD[i];
+    const u64 pa = A.co[k] + krb[i];
+    const u64 pos = A.nco[k] + (si - kp.at(tc + A.dcoff[k])) + (kp.at(pa) - kp.at(A.co[k]));
+    A.cpool_out[cb0 + pos] = A.dcloud[i];
   }
 }
 
@@ -601,19 +743,16 @@ template <bool kElems, typename T>
 __global__ __launch_bounds__(kThreads) void k_uj_cmp_copy(const UMeta* __restrict__ meta, u64 nk,
                                                           const u64* __restrict__ off, const T* __restrict__ src,
                                                           T* __restrict__ dst) {
+  __shared__ Shared S;
   const u64 total = off[nk];
-  const u64 t0 = (u64)blockIdx.x * kTileOut;
+  const u64 t0 = (u64)blockIdx.x * kTileOut;  // the grid is the host's bound
   if (t0 >= total) return;
   const u64 t1 = t0 + kTileOut < total ? t0 + kTileOut : total;
+  const TileDocs D = tile_docs<kLdsDocs>(off, nk, t0, t1, S.offs, S.sh);
   for (u64 t = t0 + threadIdx.x; t < t1; t += kThreads) {
-    u64 lo = 0, hi = nk;  // last slot with off <= t
-    while (lo < hi) {
-      const u64 m = (lo + hi + 1) >> 1;
-      if (off[m] <= t) lo = m;
-      else hi = m - 1;
-    }
-    const UMeta m = meta[lo];
-    dst[t] = src[(kElems ? m.ebase : m.cbase) + (t - off[lo])];
+    const u64 k = doc_of(D, off, S.offs, t);
+    const UMeta m = meta[k];
+    dst[t] = src[(kElems ? m.ebase : m.cbase) + (t - off[k])];
   }
 }
 __global__ __launch_bounds__(kThreads) void k_uj_cmp_meta(UMeta* __restrict__ meta, u64 nk, const u64* __restrict__ eo,
@@ -629,7 +768,7 @@ __global__ __launch_bounds__(kThreads) void k_uj_cmp_meta(UMeta* __restrict__ me
 }
 
 // ---- reads ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kThreads) void k_uj_sizes(const UMeta* __restrict__ meta, const u32* __restrict__ slots,
+__global__ __launch_bounds__(kThreads) void k_uj_sizes_read(const UMeta* __restrict__ meta, const u32* __restrict__ slots,
                                                        u64 n, u64* __restrict__ ne, u64* __restrict__ nc) {
   const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
@@ -666,29 +805,28 @@ u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kThreads - 1) / kThrea
     JY_HIP(eng, hipGetLastError());                                                                \
   } while (0)
 
-// rewrite every document back to back into new pools with `room_e` / `room_c`
-// free entries after them; synchronises (the new sizes are read back)
-// exclusive scans of n items of one or two arrays (in -> out, not in place)
-template <typename T, int NA>
-static int32_t uj_tile_scan(jy_engine* eng, ScanJob<T> J, u64 n) {
-  if (n == 0) return JY_OK;
-  const u32 tiles = (u32)((n + kFillTile - 1) / kFillTile);
-  void* p;
-  JY_TRY(jy_scratch(eng, 19, (u64)tiles * NA * sizeof(T), &p));
-  T* sums = static_cast<T*>(p);
-  hipLaunchKernelGGL((k_tile_sums<T, NA>), dim3(tiles), dim3(kThreads), 0, eng->stream, J, n, sums);
-  hipLaunchKernelGGL((k_tile_scan<T, NA>), dim3(tiles), dim3(kThreads), 0, eng->stream, J, n, (const T*)sums);
-  JY_HIP(eng, hipGetLastError());
-  return JY_OK;
-}
-// a[0..n] -> oa and b[0..n] -> ob (oa[n], ob[n] = the totals)
-static int32_t uj_scan2(jy_engine* eng, const u64* a, u64* oa, const u64* b, u64* ob, u64 n) {
-  return uj_tile_scan<u64, 2>(eng, ScanJob<u64>{{a, b}, {oa, ob}}, n + 1);
+void ujson_absorb(UjsonState& u);
+
+// the compacted pools' bump pointers: on the device, and into the host's
+// mapped ring slot
+__global__ void k_uj_cmp_ctr(const u64* __restrict__ te, const u64* __restrict__ tc, u64* __restrict__ ctr,
+                             u64* __restrict__ pin) {
+  ctr[0] = pin[0] = *te;
+  ctr[1] = pin[1] = *tc;
 }
 
+// rewrite every document back to back into the spare pools, sized for the
+// host's bound of live entries plus `room_e` / `room_c` several times over,
+// then swap.  Asynchronous: the exact compacted sizes reach the host through
+// the converge ring like a converge's bump pointers (the spare pools are
+// reallocated -- a synchronising hipMalloc -- only when they are too small).
 int32_t ujson_compact(jy_engine* eng, u64 room_e, u64 room_c) {
   UjsonState& u = eng->ujson;
   const u64 nk = eng->nkeys[JY_UJSON];
+  if (u.seq - u.done == UjsonState::kRing) {  // its ring slot
+    JY_HIP(eng, hipEventSynchronize(u.ready[u.done % UjsonState::kRing]));
+    ujson_absorb(u);
+  }
   void* p;
   JY_TRY(jy_scratch(eng, 20, (nk + 1) * 32, &p));
   u64* se = static_cast<u64*>(p);
@@ -698,37 +836,97 @@ int32_t ujson_compact(jy_engine* eng, u64 room_e, u64 room_c) {
   LAUNCH(k_uj_cmp_size, nk + 1, u.meta, nk, se, sc);
   JY_TRY(jy_scan_u64(eng, se, eo, nk));
   JY_TRY(jy_scan_u64(eng, sc, co, nk));
-  JY_HIP(eng, hipMemcpyAsync(u.pin, eo + nk, 8, hipMemcpyDeviceToHost, eng->stream));
-  JY_HIP(eng, hipMemcpyAsync(u.pin + 1, co + nk, 8, hipMemcpyDeviceToHost, eng->stream));
-  JY_HIP(eng, hipStreamSynchronize(eng->stream));
-  const u64 te = u.pin[0], tc = u.pin[1];
-  // room for many merges like this one before the next compaction
-  const u64 ecap = std::max<u64>({te + 16 * room_e, 3 * te, eng->cfg.entry_capacity[JY_UJSON], 1024});
-  const u64 ccap = std::max<u64>({tc + 16 * room_c, 3 * tc, eng->cfg.entry_capacity[JY_UJSON], 1024});
-  JY_TRACE("ujson compact: %llu elements, %llu cloud dots -> pools %llu / %llu", (unsigned long long)te,
-           (unsigned long long)tc, (unsigned long long)ecap, (unsigned long long)ccap);
-  URec* ne = nullptr;
-  u64* nc = nullptr;
-  JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&ne), ecap * sizeof(URec), "ujson element pool"));
-  JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&nc), ccap * 8, "ujson cloud pool"));
-  if (te)
-    hipLaunchKernelGGL((k_uj_cmp_copy<true, URec>), dim3((u32)((te + kTileOut - 1) / kTileOut)), dim3(kThreads), 0,
-                       eng->stream, u.meta, nk, eo, u.epool, ne);
-  if (tc)
-    hipLaunchKernelGGL((k_uj_cmp_copy<false, u64>), dim3((u32)((tc + kTileOut - 1) / kTileOut)), dim3(kThreads), 0,
-                       eng->stream, u.meta, nk, co, u.cpool, nc);
+  const u64 be = u.live_e, bc = u.live_c;  // >= the compacted sizes
+  const u64 ecap = std::max<u64>({be + 8 * room_e, 3 * be, eng->cfg.entry_capacity[JY_UJSON], 1024});
+  const u64 ccap = std::max<u64>({bc + 8 * room_c, 3 * bc, eng->cfg.entry_capacity[JY_UJSON], 1024});
+  JY_TRACE("ujson compact: <= %llu elements, <= %llu cloud dots -> pools %llu / %llu", (unsigned long long)be,
+           (unsigned long long)bc, (unsigned long long)ecap, (unsigned long long)ccap);
+  if (u.spare_ecap < ecap) {
+    jy_dev_free(eng, u.spare_e);
+    u.spare_e = nullptr;
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.spare_e), ecap * sizeof(URec), "ujson element pool"));
+    u.spare_ecap = ecap;
+  }
+  if (u.spare_ccap < ccap) {
+    jy_dev_free(eng, u.spare_c);
+    u.spare_c = nullptr;
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.spare_c), ccap * 8, "ujson cloud pool"));
+    u.spare_ccap = ccap;
+  }
+  if (be)
+    hipLaunchKernelGGL((k_uj_cmp_copy<true, URec>), dim3((u32)((be + kTileOut - 1) / kTileOut)), dim3(kThreads), 0,
+                       eng->stream, u.meta, nk, eo, u.epool, u.spare_e);
+  if (bc)
+    hipLaunchKernelGGL((k_uj_cmp_copy<false, u64>), dim3((u32)((bc + kTileOut - 1) / kTileOut)), dim3(kThreads), 0,
+                       eng->stream, u.meta, nk, co, u.cpool, u.spare_c);
   JY_HIP(eng, hipGetLastError());
   if (nk) LAUNCH(k_uj_cmp_meta, nk, u.meta, nk, eo, co);
-  jy_dev_free(eng, u.epool);
-  jy_dev_free(eng, u.cpool);
-  u.epool = ne;
-  u.cpool = nc;
-  u.epcap = ecap;
-  u.cpcap = ccap;
-  u.pin[0] = te;
-  u.pin[1] = tc;
-  JY_HIP(eng, hipMemcpyAsync(u.ctr, u.pin, 16, hipMemcpyHostToDevice, eng->stream));
-  JY_HIP(eng, hipStreamSynchronize(eng->stream));  // pin is reused right away
+  const int r = (int)(u.seq % UjsonState::kRing);
+  hipLaunchKernelGGL(k_uj_cmp_ctr, dim3(1), dim3(1), 0, eng->stream, eo + nk, co + nk, u.ctr, u.pin_dev + 8 + 2 * r);
+  JY_HIP(eng, hipGetLastError());
+  std::swap(u.epool, u.spare_e);
+  std::swap(u.epcap, u.spare_ecap);
+  std::swap(u.cpool, u.spare_c);
+  std::swap(u.cpcap, u.spare_ccap);
+  // every earlier converge is compacted in; this one's sizes are bounded by be / bc
+  u.used_e = u.used_c = 0;
+  u.done = u.seq;
+  u.ring_e[r] = be;
+  u.ring_c[r] = bc;
+  JY_HIP(eng, hipEventRecord(u.ready[r], eng->stream));
+  u.seq++;
+  return JY_OK;
+}
+
+// Pool plan of one converge: the worst case (every live element touched,
+// every delta item kept) must fit after the bump pointers the host knows --
+// exact once the last converge's mapped readback has landed, an upper bound
+// before.  Only when it may not fit does the host wait for the GPU; only
+// when the pools are really short does it compact.
+// the newest finished converge's exact bump pointers (mapped readback)
+void ujson_absorb(UjsonState& u) {
+  for (u64 j = u.seq; j > u.done; j--) {
+    const int r = (int)((j - 1) % UjsonState::kRing);
+    if (hipEventQuery(u.ready[r]) == hipSuccess) {
+      u.used_e = u.pin[8 + 2 * r];
+      u.used_c = u.pin[9 + 2 * r];
+      u.done = j;
+      return;
+    }
+  }
+}
+int32_t ujson_plan(jy_engine* eng, u64 nel, u64 ncloud) {
+  UjsonState& u = eng->ujson;
+  ujson_absorb(u);
+  if (u.seq - u.done == UjsonState::kRing) {  // the ring slot is still in use: wait for its converge
+    JY_HIP(eng, hipEventSynchronize(u.ready[u.done % UjsonState::kRing]));
+    ujson_absorb(u);
+  }
+  const u64 we = u.live_e + nel, wc = u.live_c + ncloud;
+  auto fits = [&]() {
+    u64 be = u.used_e + we, bc = u.used_c + wc;
+    for (u64 j = u.done; j < u.seq; j++) {
+      be += u.ring_e[j % UjsonState::kRing];
+      bc += u.ring_c[j % UjsonState::kRing];
+    }
+    return be <= u.epcap && bc <= u.cpcap;
+  };
+  if (!fits()) {
+    if (u.seq > u.done) {
+      JY_HIP(eng, hipEventSynchronize(u.ready[(u.seq - 1) % UjsonState::kRing]));
+      ujson_absorb(u);
+    }
+    if (!fits()) JY_TRY(ujson_compact(eng, we, wc));
+  }
+  return JY_OK;
+}
+
+// a zeroed device buffer that only grows (contents kept when `keep`)
+int32_t grow_zero(jy_engine* eng, void** p, u64* cap_bytes, u64 need_bytes) {
+  if (need_bytes <= *cap_bytes && *p) return JY_OK;
+  const u64 nb = std::max<u64>(need_bytes, *cap_bytes * 2);
+  JY_TRY(jy_realloc(eng, p, *cap_bytes, nb, true));
+  *cap_bytes = nb;
   return JY_OK;
 }
 
@@ -740,7 +938,12 @@ int32_t jy_ujson_grow(jy_engine* eng, u64 need) {
   if (!u.ctr) {
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.ctr), 64, "ujson counters"));
     JY_HIP(eng, hipMemsetAsync(u.ctr, 0, 64, eng->stream));
-    JY_HIP(eng, hipHostMalloc(reinterpret_cast<void**>(&u.pin), 64, hipHostMallocDefault));
+    JY_HIP(eng, hipHostMalloc(reinterpret_cast<void**>(&u.pin), 128, hipHostMallocMapped));
+    std::memset(u.pin, 0, 128);
+    JY_HIP(eng, hipHostGetDevicePointer(reinterpret_cast<void**>(&u.pin_dev), u.pin, 0));
+    for (hipEvent_t& e : u.ready) JY_HIP(eng, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.tick), 64, "ujson tickets"));
+    JY_HIP(eng, hipMemsetAsync(u.tick, 0, 64, eng->stream));
     u.epcap = u.cpcap = std::max<u64>(eng->cfg.entry_capacity[JY_UJSON], 1024);
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.epool), u.epcap * sizeof(URec), "ujson element pool"));
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.cpool), u.cpcap * 8, "ujson cloud pool"));
@@ -754,6 +957,9 @@ int32_t jy_ujson_grow(jy_engine* eng, u64 need) {
   void* m = u.meta;
   JY_TRY(jy_realloc(eng, &m, u.kcap * sizeof(UMeta), nk * sizeof(UMeta), true));  // empty docs
   u.meta = static_cast<UMeta*>(m);
+  void* d = u.dptr;
+  JY_TRY(jy_realloc(eng, &d, u.kcap * 8, nk * 8, true));  // epoch 0: never claimed
+  u.dptr = static_cast<u64*>(d);
   u.kcap = nk;
   return JY_OK;
 }
@@ -768,12 +974,63 @@ int32_t jy_ujson_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* deoff
   UjsonState& u = eng->ujson;
   const u64 nk = eng->nkeys[JY_UJSON];
   if (nd == 0 || nk == 0) return JY_OK;
-  if (nd >= (1ull << kSegBits)) return eng->fail(JY_ERANGE, "ujson converge: more than 2^28 documents in one call");
+  if (nd >= 0xFFFFFFFFull) return eng->fail(JY_ERANGE, "ujson converge: more than 2^32 - 1 documents in one call");
   const u32 R = u.R;
+  const u64 live_e = u.live_e, live_c = u.live_c;  // bounds of the touched state, before this converge
+  JY_TRY(ujson_plan(eng, nel, ncloud));
+  const u64 le = std::min(u.live_e, live_e), lc = std::min(u.live_c, live_c);  // (a compaction makes them exact)
+  if (le + nel + ncloud + 2 >= (1ull << 32) || lc + ncloud + 2 >= (1ull << 32))
+    return eng->fail(JY_ERANGE, "ujson converge: more than 2^32 touched items");
+
+  // epoch: tags claims, bad marks and look-back words (no per-converge reset)
+  u.epoch++;
+  if ((u.epoch & ((1u << jyscan::kEpochBits) - 1)) == 0 || u.epoch == 0) {
+    // wrap: clear everything the tags protect
+    u.epoch = 1;
+    JY_HIP(eng, hipMemsetAsync(u.dptr, 0, u.kcap * 8, eng->stream));
+    if (u.bad) JY_HIP(eng, hipMemsetAsync(u.bad, 0, u.dcap * 4, eng->stream));
+    for (int i = 0; i < 6; i++)
+      if (u.st[i].p)
+        JY_HIP(eng, hipMemsetAsync(u.st[i].p, 0, u.st[i].bytes, eng->stream));
+  }
+  // persistent per-delta-doc state: bad marks and the dense delta vv (zero)
+  if (nd > u.dcap) {
+    u64 bcap = u.dcap * 4, vcap = u.dcap * R * 8;
+    void* b = u.bad;
+    void* v = u.vvd;
+    const u64 dcap = std::max<u64>(nd, 2 * u.dcap);
+    JY_TRY(grow_zero(eng, &b, &bcap, dcap * 4));
+    JY_TRY(grow_zero(eng, &v, &vcap, dcap * R * 8));
+    u.bad = static_cast<u32*>(b);
+    u.vvd = static_cast<u64*>(v);
+    u.dcap = dcap;
+  }
+  const u64 ndt = (nd + kDocTile - 1) / kDocTile;
+  const u64 tf = (le + kTile - 1) / kTile + (nel + kTile - 1) / kTile + (ncloud + kTile - 1) / kTile + 2;
+  const u64 tk = (lc + kTile - 1) / kTile + (ncloud + kTile - 1) / kTile + 2;
+  const u64 st_need[6] = {ndt, ndt, tf, tk, ndt, ndt};
+  u64* st[6];
+  for (int i = 0; i < 6; i++) {
+    JY_TRY(grow_zero(eng, &u.st[i].p, &u.st[i].bytes, st_need[i] * 8));
+    st[i] = static_cast<u64*>(u.st[i].p);
+  }
 
   UjArgs A{};
-  A.R = R;
+  A.meta = u.meta;
+  A.rec = u.epool;
+  A.cloud = u.cpool;
   A.vv = u.vv;
+  A.epool_out = u.epool;
+  A.cpool_out = u.cpool;
+  A.ctr = u.ctr;
+  const int slot_r = (int)(u.seq % UjsonState::kRing);
+  A.pin = u.pin_dev + 8 + 2 * slot_r;
+  A.R = R;
+  A.epoch = u.epoch;
+  A.dptr = u.dptr;
+  A.bad = u.bad;
+  A.skipped = reinterpret_cast<unsigned long long*>(eng->skipped_dev);
+  A.tick = u.tick;
   A.nd = nd;
   A.nb = nel;
   A.cb = ncloud;
@@ -786,129 +1043,84 @@ int32_t jy_ujson_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* deoff
   A.dvv = dvv;
   A.dcoff = dcoff;
   A.dcloud = dcloud;
-  A.skipped = reinterpret_cast<unsigned long long*>(eng->skipped_dev);
   void* p;
-  JY_TRY(jy_scratch(eng, 8, nk * 4, &p));
-  A.dptr = static_cast<u32*>(p);
-  JY_TRY(jy_scratch(eng, 9, nd * 4 + 16, &p));
-  A.bad = static_cast<u32*>(p);
-  JY_TRY(jy_scratch(eng, 10, nd * R * 32, &p));
-  A.vvm = static_cast<u64*>(p);
-  A.vvn = A.vvm + nd * R;
-  A.vvd = A.vvn + nd * R;
-  A.vvs = A.vvd + nd * R;
-  JY_TRY(jy_scratch(eng, 18, (nd + 1) * 48, &p));
+  JY_TRY(jy_scratch(eng, 18, (nd + 1) * 8 * 6 + 64, &p));
   u64* tb = static_cast<u64*>(p);
   A.abase = tb;
-  A.asz = tb + (nd + 1);
+  A.cbs = tb + (nd + 1);
   A.ao = tb + 2 * (nd + 1);
-  A.cbs = tb + 3 * (nd + 1);
-  A.csz = tb + 4 * (nd + 1);
-  A.co = tb + 5 * (nd + 1);
+  A.co = tb + 3 * (nd + 1);
+  A.neo = tb + 4 * (nd + 1);
+  A.nco = tb + 5 * (nd + 1);
+  A.base = tb + 6 * (nd + 1);
+  JY_TRY(jy_scratch(eng, 10, nd * R * 24 + 64, &p));
+  A.vvs = static_cast<u64*>(p);
+  A.vvm = A.vvs + nd * R;
+  A.vvn = A.vvm + nd * R;
+  A.vvd = u.vvd;
+  JY_TRY(jy_scratch(eng, 11, (le + nel + ncloud + 2) * 4, &p));
+  A.sc = static_cast<u32*>(p);
+  JY_TRY(jy_scratch(eng, 14, (lc + ncloud + 2) * 4, &p));
+  A.ksc = static_cast<u32*>(p);
+  JY_TRY(jy_scratch(eng, 12, (le + nel + ncloud + 2) * 4, &p));
+  A.xr = static_cast<u32*>(p);
+  JY_TRY(jy_scratch(eng, 13, (lc + ncloud + 2) * 4, &p));
+  A.kr = static_cast<u32*>(p);
+  JY_TRY(jy_scratch(eng, 19, (le + nel + lc + ncloud + 4) * 4, &p));
+  A.sidA = static_cast<u32*>(p);
+  A.sidB = A.sidA + le + 1;
+  A.sidC = A.sidB + nel + 1;
+  A.sidD = A.sidC + lc + 1;
+  JY_TRY(jy_scratch(eng, 17, (tf + tk + 2) * 8, &p));
+  A.tp = static_cast<u64*>(p);
+  A.ktp = A.tp + tf + 1;
+  A.st_ao = st[0];
+  A.st_co = st[1];
+  A.st_ne = st[4];
+  A.st_nc = st[5];
 
-  // touched-state sizes and the bump pointers: the one readback of a converge
-  u64 ta = 0, tc = 0, eb0 = 0, cb0 = 0;
-  for (int attempt = 0;; attempt++) {
-    A.meta = u.meta;
-    A.rec = u.epool;
-    A.cloud = u.cpool;
-    JY_HIP(eng, hipMemsetAsync(A.dptr, 0xFF, nk * 4, eng->stream));
-    JY_HIP(eng, hipMemsetAsync(A.bad, 0, nd * 4, eng->stream));
-    LAUNCH(k_uj_prep, nd * R, A);
-    JY_TRY(uj_scan2(eng, A.asz, A.ao, A.csz, A.co, nd));
-    JY_HIP(eng, hipMemcpyAsync(u.pin, A.ao + nd, 8, hipMemcpyDeviceToHost, eng->stream));
-    JY_HIP(eng, hipMemcpyAsync(u.pin + 1, A.co + nd, 8, hipMemcpyDeviceToHost, eng->stream));
-    JY_HIP(eng, hipMemcpyAsync(u.pin + 2, u.ctr, 16, hipMemcpyDeviceToHost, eng->stream));
-    JY_HIP(eng, hipStreamSynchronize(eng->stream));
-    ta = u.pin[0];
-    tc = u.pin[1];
-    eb0 = u.pin[2];
-    cb0 = u.pin[3];
-    if (eb0 + ta + nel <= u.epcap && cb0 + tc + ncloud <= u.cpcap) break;
-    if (attempt == 1) return eng->fail(JY_ENOMEM, "ujson pools: no room after compaction");
-    JY_TRY(ujson_compact(eng, ta + nel, tc + ncloud));  // moves every doc: plan again
-  }
-  if (ta + nel + 3 >= (1ull << 31) || tc + ncloud + 2 >= (1ull << 31))
-    return eng->fail(JY_ERANGE, "ujson converge: more than 2^31 touched elements");
-  A.ta = ta;
-  A.tc = tc;
-
-  const u64 nf = (ta + 1) + (nel + 1) + (ncloud + 1);
-  JY_TRY(jy_scratch(eng, 11, nf * 8, &p));
-  A.flag_a = static_cast<u32*>(p);
-  A.flag_b = A.flag_a + ta + 1;
-  A.cflag_b = A.flag_b + nel + 1;
-  A.scan_a = A.flag_a + nf;
-  A.scan_b = A.scan_a + ta + 1;
-  A.cscan_b = A.scan_b + nel + 1;
-  const u64 nkp = (tc + 1) + (ncloud + 1);
-  JY_TRY(jy_scratch(eng, 14, nkp * 8, &p));
-  A.keep_ca = static_cast<u32*>(p);
-  A.keep_cb = A.keep_ca + tc + 1;
-  A.kscan_a = A.keep_ca + nkp;
-  A.kscan_b = A.kscan_a + tc + 1;
-  JY_TRY(jy_scratch(eng, 16, (nd + 1) * 32, &p));
-  u64* ne = static_cast<u64*>(p);
-  u64* nc = ne + nd + 1;
-  u64* neo = nc + nd + 1;
-  u64* nco = neo + nd + 1;
-  // segment ids of delta elements, cloud dots, vv entries and the touched
-  // state's elements and cloud dots: one buffer, one scan
-  const u64 nsg = nel + ncloud + nvv + ta + tc;
-  JY_TRY(jy_scratch(eng, 17, std::max<u64>(nsg, 1) * 4, &p));
-  u32* sg = static_cast<u32*>(p);
-  A.dseg = sg;
-  A.dcseg = sg + nel;
-  A.vseg = sg + nel + ncloud;
-  A.aseg = sg + nel + ncloud + nvv;
-  A.acseg = sg + nel + ncloud + nvv + ta;
-
-  auto ranges = [](std::initializer_list<u64> ns) {
-    Ranges G{};
-    G.cnt = 0;
-    u32 b = 0;
-    for (u64 n : ns) {
-      G.n[G.cnt] = n;
-      G.b0[G.cnt] = b;
-      b += (u32)((n + kThreads - 1) / kThreads);
-      G.cnt++;
-    }
-    G.b0[G.cnt] = b;
-    return G;
-  };
-  auto launch_ranges = [&](auto kern, const Ranges& G, auto... args) -> int32_t {
-    if (G.b0[G.cnt] == 0) return JY_OK;
-    hipLaunchKernelGGL(kern, dim3(G.b0[G.cnt]), dim3(kThreads), 0, eng->stream, args..., G);
-    JY_HIP(eng, hipGetLastError());
-    return JY_OK;
-  };
-
-  if (nsg) {
-    SegSrc S{{deoff, dcoff, dvoff, A.ao, A.co}, {0, nel, nel + ncloud, nel + ncloud + nvv, nel + ncloud + nvv + ta}};
-    JY_HIP(eng, hipMemsetAsync(sg, 0, nsg * 4, eng->stream));
-    LAUNCH(k_uj_seg_starts, nd, S, nd, sg);
-    hipLaunchKernelGGL(k_uj_seg_fill, dim3((u32)((nsg + kFillTile - 1) / kFillTile)), dim3(kThreads), 0, eng->stream,
-                       S, nd, sg, nsg);
-    JY_HIP(eng, hipGetLastError());
-  }
-  JY_TRY(launch_ranges(k_uj_check, ranges({nvv, nel, ncloud}), A));
-  LAUNCH(k_uj_drop_bad, nd * R, A);
-  JY_TRY(launch_ranges(k_uj_flags, ranges({ta + 1, nel + 1, ncloud + 1}), A));
-  JY_TRY((uj_tile_scan<u32, 1>(eng, ScanJob<u32>{{A.flag_a, nullptr}, {A.flag_a + nf, nullptr}}, nf)));
-  JY_TRY(launch_ranges(k_uj_compact, ranges({tc + 1, ncloud + 1}), A));
-  JY_TRY((uj_tile_scan<u32, 1>(eng, ScanJob<u32>{{A.keep_ca, nullptr}, {A.keep_ca + nkp, nullptr}}, nkp)));
-  LAUNCH(k_uj_sizes_out, nd + 1, A, ne, nc);
-  JY_TRY(uj_scan2(eng, ne, neo, nc, nco, nd));
-  Out O{neo, nco, u.epool, u.cpool, u.meta, eb0, cb0};
-  JY_TRY(launch_ranges(k_uj_scatter, ranges({nd * R, ta, nel, tc, ncloud}), A, O));
-  hipLaunchKernelGGL(k_uj_bump, dim3(1), dim3(1), 0, eng->stream, u.ctr, neo, nco, nd, eb0, cb0);
+  const u64 g1 = ndt + (nel + kTile1 - 1) / kTile1 + (ncloud + kTile1 - 1) / kTile1 + (nvv + kTile1 - 1) / kTile1;
+  hipLaunchKernelGGL(k_uj_docs, dim3((u32)g1), dim3(kThreads), 0, eng->stream, A, ndt, (nel + kTile1 - 1) / kTile1,
+                     (ncloud + kTile1 - 1) / kTile1, (nvv + kTile1 - 1) / kTile1);
+  hipLaunchKernelGGL(k_uj_flags, dim3((u32)tf), dim3(kItemThreads), 0, eng->stream, A);
+  hipLaunchKernelGGL(k_uj_tscan, dim3(1), dim3(1024), 0, eng->stream, A, 0);
+  hipLaunchKernelGGL(k_uj_compact, dim3((u32)tk), dim3(kItemThreads), 0, eng->stream, A);
+  hipLaunchKernelGGL(k_uj_tscan, dim3(1), dim3(1024), 0, eng->stream, A, 1);
+  hipLaunchKernelGGL(k_uj_sizes, dim3((u32)ndt), dim3(kThreads), 0, eng->stream, A, ndt);
+  const u64 g5 = tf + tk + (nd * R + kTile - 1) / kTile + (nd + kTile - 1) / kTile + 2;
+  hipLaunchKernelGGL(k_uj_scatter, dim3((u32)g5), dim3(kItemThreads), 0, eng->stream, A);
   JY_HIP(eng, hipGetLastError());
+#ifdef JY_UJ_PROBE
+  if (const char* path = getenv("JY_UJ_PROBE_OUT")) {
+    static std::vector<u64> buf(kProbe * 6);
+    u32 n = 0;
+    JY_HIP(eng, hipStreamSynchronize(eng->stream));
+    JY_HIP(eng, hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_probe_n), 4));
+    n = std::min(n, kProbe);
+    JY_HIP(eng, hipMemcpyFromSymbol(buf.data(), HIP_SYMBOL(g_probe), (size_t)n * 48));
+    if (FILE* f = fopen(path, "ab")) {
+      const u64 hdr[4] = {~0ull, n, tf, tk};
+      fwrite(hdr, 8, 4, f);
+      fwrite(buf.data(), 48, n, f);
+      fclose(f);
+    }
+    const u32 zero = 0;
+    JY_HIP(eng, hipMemcpyToSymbol(HIP_SYMBOL(g_probe_n), &zero, 4));
+  }
+#endif
+  // the host's pool bounds: the worst case until the mapped readback lands
+  u.ring_e[slot_r] = le + nel;
+  u.ring_c[slot_r] = lc + ncloud;
+  u.live_e += nel;
+  u.live_c += ncloud;
+  JY_HIP(eng, hipEventRecord(u.ready[slot_r], eng->stream));
+  u.seq++;
   return JY_OK;
 }
 
 int32_t jy_ujson_sizes(jy_engine* eng, u64 n, const u32* slots, u64* ne, u64* nc) {
   UjsonState& u = eng->ujson;
-  LAUNCH(k_uj_sizes, n, u.meta, slots, n, ne, nc);
+  LAUNCH(k_uj_sizes_read, n, u.meta, slots, n, ne, nc);
   return JY_OK;
 }
 
