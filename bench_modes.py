@@ -15,7 +15,7 @@ import numpy as np
 HBM_PEAK_GBS = 8000.0
 
 
-def _timed(steps, warmup, step, dist, dev, eng=None):
+def _timed(steps, warmup, step, dist, dev, eng=None, before_timed=None):
     """warmup, then exactly `steps` steps bracketed by barrier + synchronize.
     Per-step device time: with `eng`, the engine's own HIP events around each
     merge call's device work (jy_timing_enable; host launch gaps excluded),
@@ -28,6 +28,8 @@ def _timed(steps, warmup, step, dist, dev, eng=None):
         dist.barrier()
     torch.cuda.synchronize(dev)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if before_timed is not None:
+        before_timed()
     if eng is not None:
         eng.timing(True)
     host = []
@@ -423,48 +425,38 @@ def bench_ujson(args, eng, dev, dist, rank, world):
         dev_batches.append((tuple(_to_dev(a, dev) for a in (slots, eo, dots, elems, vo, vv, co, cloud)),
                             len(slots), len(dots), len(cloud)))
     eng.sync()
-    # the documents each batch touches, with their sizes in the state the
-    # steps start from (sizes drift slowly over the steps)
-    s_all = np.arange(eng.nkeys(UJSON), dtype=np.uint32)
-    ne_all, nc_all = np.empty(len(s_all), np.uint64), np.empty(len(s_all), np.uint64)
-    eng._check(eng.lib.jy_ujson_read_sizes(eng.h, len(s_all), s_all.ctypes.data, ne_all.ctypes.data,
-                                           nc_all.ctypes.data))
-    touched = []
-    for b in dl:
-        sl = eng.lookup(UJSON, (b["key_bytes"], b["key_offs"])).astype(np.int64)
-        touched.append((float(ne_all[sl].sum()), float(nc_all[sl].sum())))
-
     def step(i):
         eng.ujson_converge(*dev_batches[i % nb][0])
 
-    elapsed, kt = _timed(args.steps, args.warmup, step, dist, dev, eng=eng)
+    marks = {}
+    elapsed, kt = _timed(args.steps, args.warmup, step, dist, dev, eng=eng,
+                         before_timed=lambda: marks.update(s0=eng.ujson_stats()))
+    s1 = eng.ujson_stats()
+    # what the timed converges really touched and wrote (the engine's own
+    # counters: the hot documents grow step by step)
+    d = {k: (s1[k] - marks["s0"][k]) / args.steps for k in s1}
     t = _max_over_ranks(elapsed, dist, dev)
     k = float(np.mean(kt))
-    used = [(args.warmup + i) % nb for i in range(args.steps)]
-    nd_docs = float(np.mean([dev_batches[i][1] for i in used]))
-    nd_el = float(np.mean([dev_batches[i][2] for i in used]))
-    nd_cl = float(np.mean([dev_batches[i][3] for i in used]))
-    st_el = float(np.mean([touched[i][0] for i in used]))
-    st_cl = float(np.mean([touched[i][1] for i in used]))
     R = 16
-    # 16 B per dot read + 16 B per dot written, 8R B of context
-    # read twice and written once per doc; the dots are those of the touched
-    # documents (state) and of the delta -- untouched documents are not read
-    bytes_conv = 32 * (st_el + nd_el) + 16 * (st_cl + nd_cl) + 24 * R * nd_docs
-    dots_examined = st_el + st_cl + nd_el + nd_cl
+    # 16 B per element read (touched state + delta) and written,
+    # 8 B per cloud dot read and written, 24R B of context per delta doc
+    bytes_conv = (16 * (d["touched_el"] + d["delta_el"] + d["out_el"]) +
+                  8 * (d["touched_cloud"] + d["delta_cloud"] + d["out_cloud"]) + 24 * R * d["delta_docs"])
+    dots_examined = d["touched_el"] + d["touched_cloud"] + d["delta_el"] + d["delta_cloud"]
     return {"workload": f"UJSON converge: {D} docs (~8 leaves, R=16), Zipf(1.1) delta docs per step "
-                        f"({int(nd_docs)} docs, {int(nd_el)} dots, {int(nd_cl)} cloud dots), "
-                        f"70/20/10 INS/RM/CLR (SURVEY 8d config 5)",
+                        f"({int(d['delta_docs'])} docs, {int(d['delta_el'])} dots, {int(d['delta_cloud'])} cloud dots; "
+                        f"{int(d['touched_el'])} touched state elements), 70/20/10 INS/RM/CLR (SURVEY 8d config 5)",
             "unit_of_work": "dot examined", "value": world * dots_examined * args.steps / t,
             "ms_per_step": t / args.steps * 1e3, "generate_s": gen_s,
-            "delta_docs_per_s": world * nd_docs * args.steps / t,
+            "delta_docs_per_s": world * d["delta_docs"] * args.steps / t,
+            "per_converge": d,
             "roofline": {"bound": "hbm", "achieved": bytes_conv / k / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": bytes_conv / k / 1e9 / HBM_PEAK_GBS,
                          "kernel": "UJSON converge (k_uj_*, all launches of one call)",
                          "converge_ms_avg": k * 1e3, "bytes_per_converge": bytes_conv,
-                         "bytes_note": "SURVEY 8d per dot examined (touched documents' state dots + delta dots): "
-                                       "16 B read + 16 B written per element, 8 + 8 B per cloud dot, 24R B "
-                                       "context per delta doc"}}
+                         "bytes_note": "SURVEY 8d, from jy_ujson_stats over the timed converges: 16 B per element "
+                                       "read (touched state + delta) and written, 8 B per cloud dot read and "
+                                       "written, 24R B context per delta doc; untouched documents are not read"}}
 
 
 MODES = {"gcount": bench_gcount, "treg": bench_treg, "tlog": bench_tlog, "ujson": bench_ujson}

@@ -186,6 +186,28 @@ int32_t jy_treg_flush(jy_engine* eng, uint64_t cap, uint32_t* slot_out, uint64_t
 int32_t jy_tlog_converge(jy_engine* eng, uint64_t nkeys, const uint32_t* slot, const uint64_t* cutoff,
                          const uint64_t* ent_offs, uint64_t nent, const uint64_t* ts,
                          const uint64_t* pre, const uint64_t* lr, int32_t mem);
+/* ---- TLOG write path: RepoTLOG.ins / trimat / trim / clr (repo_tlog.pony:85-111) ----
+ * n commands applied in order: op[i] is JY_TLOG_INS (value handle pre/lr from
+ * jy_values_pack at ts[i]), JY_TLOG_TRIMAT (ts[i]), JY_TLOG_TRIM (arg[i] =
+ * count) or JY_TLOG_CLR.  Each changes the state as TLog.write / raise_cutoff
+ * / trim / clear do, and where it changed the state the same change goes into
+ * the key's pending delta log; every command marks its key pending.  Host
+ * batches may repeat keys (applied in order); a device batch holds one
+ * command per key.  Unused columns may be null. */
+#define JY_TLOG_INS 0
+#define JY_TLOG_TRIMAT 1
+#define JY_TLOG_TRIM 2
+#define JY_TLOG_CLR 3
+int32_t jy_tlog_write(jy_engine* eng, uint64_t n, const uint8_t* op, const uint32_t* slot, const uint64_t* ts,
+                      const uint64_t* arg, const uint64_t* pre, const uint64_t* lr, int32_t mem);
+int32_t jy_tlog_deltas_size(jy_engine* eng, uint64_t* n_out);  /* deltas_size(); blocks */
+/* flush_deltas() (repo_tlog.pony:21-25): every pending key, ascending slot,
+ * with its delta log (cutoff, entries newest first as a CSR); then clears
+ * them.  With cap_keys / cap_ent too small nothing is written or cleared and
+ * *nkeys_out / *nent_out report the sizes needed (JY_OK). */
+int32_t jy_tlog_flush(jy_engine* eng, uint64_t cap_keys, uint64_t cap_ent, uint32_t* slot_out,
+                      uint64_t* cutoff_out, uint64_t* ent_offs_out, uint64_t* ts_out, uint64_t* pre_out,
+                      uint64_t* lr_out, uint64_t* nkeys_out, uint64_t* nent_out, int32_t mem);
 /* two-phase read: sizes (n entries per slot + cutoffs), then entries */
 int32_t jy_tlog_read_sizes(jy_engine* eng, uint64_t n, const uint32_t* slots, uint64_t* len_out,
                            uint64_t* cutoff_out);
@@ -210,6 +232,13 @@ int32_t jy_ujson_read_sizes(jy_engine* eng, uint64_t n, const uint32_t* slots, u
 int32_t jy_ujson_read(jy_engine* eng, uint64_t n, const uint32_t* slots, const uint64_t* el_offs,
                       uint64_t* dots_out, uint64_t* elems_out, uint64_t* vv_out,
                       const uint64_t* cloud_offs, uint64_t* cloud_out);
+
+/* cumulative converge counters since the engine was made (synchronising):
+ * [0] touched state elements, [1] touched state cloud dots, [2] elements
+ * written, [3] cloud dots written, [4] delta elements, [5] delta cloud dots,
+ * [6] delta documents, [7] converge calls.  Bench / telemetry only: the
+ * bytes a converge really moved. */
+int32_t jy_ujson_stats(jy_engine* eng, uint64_t* out8);
 
 /* ---- multi-GPU routing: the exchange step of a key-hash-sharded node ----
  * Replaces nothing in the reference (every node holds every key there); it is

@@ -16,6 +16,7 @@ GCOUNT, PNCOUNT, TREG, TLOG, UJSON = 0, 1, 2, 3, 4
 TYPE_NAMES = {"GCOUNT": GCOUNT, "PNCOUNT": PNCOUNT, "TREG": TREG, "TLOG": TLOG, "UJSON": UJSON}
 HOST, DEVICE = 0, 1
 CFG_TREG_WHOLE_LINES = 1
+TLOG_INS, TLOG_TRIMAT, TLOG_TRIM, TLOG_CLR = 0, 1, 2, 3
 
 
 class JyConfig(C.Structure):
@@ -80,6 +81,10 @@ SIGNATURES = {
     "jy_ujson_converge": (I32, [P, U64, P, P, U64, P, P, P, U64, P, P, U64, P, I32]),
     "jy_ujson_read_sizes": (I32, [P, U64, P, P, P]),
     "jy_ujson_read": (I32, [P, U64, P, P, P, P, P, P, P]),
+    "jy_ujson_stats": (I32, [P, P]),
+    "jy_tlog_write": (I32, [P, U64, P, P, P, P, P, P, I32]),
+    "jy_tlog_deltas_size": (I32, [P, P]),
+    "jy_tlog_flush": (I32, [P, U64, U64, P, P, P, P, P, P, P, P, I32]),
     "jy_keys_owner": (None, [U64, P, P, U32, P]),
     "jy_treg_route_part": (I32, [P, U64, P, P, P, P, P, U32, U64, U64, I32, P, P, P, P]),
     "jy_treg_converge_routed": (I32, [P, U32, U64, U64, P, P, P]),

@@ -113,6 +113,112 @@ int32_t jy_tlog_converge(jy_engine* eng, uint64_t n, const uint32_t* slot, const
                        (const u64*)dp, (const u64*)dl);
 }
 
+int32_t jy_tlog_write(jy_engine* eng, uint64_t n, const uint8_t* op, const uint32_t* slot, const uint64_t* ts,
+                      const uint64_t* arg, const uint64_t* pre, const uint64_t* lr, int32_t mem) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (n == 0) return JY_OK;
+  if (n >= 0xFFFFFFFFull) return eng->fail(JY_ERANGE, "more than 2^32 - 1 commands in one call");
+  JY_TRY(jy_slots_check(eng, JY_TLOG, n, slot, mem));
+  if (mem == JY_HOST) {
+    const u64 alen = eng->arena[JY_TLOG].len;
+    for (u64 i = 0; i < n; i++) {
+      if (op[i] > JY_TLOG_CLR) return eng->fail(JY_EINVAL, "unknown TLOG write op");
+      if (op[i] == JY_TLOG_INS && (!ts || !pre || !lr)) return eng->fail(JY_EINVAL, "INS needs ts, pre and lr");
+      if ((op[i] == JY_TLOG_TRIMAT && !ts) || (op[i] == JY_TLOG_TRIM && !arg))
+        return eng->fail(JY_EINVAL, "TRIMAT needs ts, TRIM needs arg");
+      if (op[i] == JY_TLOG_INS && (lr[i] & JY_LR_LEN_MASK) > 8 &&
+          (lr[i] >> JY_LR_LEN_BITS) + (lr[i] & JY_LR_LEN_MASK) > alen)
+        return eng->fail(JY_ERANGE, "value handle outside the arena");
+    }
+    std::vector<u32> occ;
+    const u32 rounds = rounds_of(n, slot, occ);
+    // full columns (zeros where a command does not use one)
+    std::vector<u64> cts(n, 0), carg(n, 0), cpre(n, 0), clr(n, 0);
+    for (u64 i = 0; i < n; i++) {
+      if (ts) cts[i] = ts[i];
+      if (arg) carg[i] = arg[i];
+      if (pre) cpre[i] = pre[i];
+      if (lr) clr[i] = lr[i];
+    }
+    for (u32 r = 0; r < rounds; r++) {
+      std::vector<uint8_t> o;
+      std::vector<u32> s;
+      std::vector<u64> a, b, c, d;
+      for (u64 i = 0; i < n; i++)
+        if (rounds == 1 || occ[i] == r) {
+          o.push_back(op[i]);
+          s.push_back(slot[i]);
+          a.push_back(cts[i]);
+          b.push_back(carg[i]);
+          c.push_back(cpre[i]);
+          d.push_back(clr[i]);
+        }
+      const u64 m = s.size();
+      const void *dop, *ds, *dt, *da, *dp, *dl;
+      JY_TRY(jy_stage_begin(eng));
+      JY_TRY(jy_stage(eng, 0, o.data(), m, JY_HOST, &dop));
+      JY_TRY(jy_stage(eng, 1, s.data(), m * 4, JY_HOST, &ds));
+      JY_TRY(jy_stage(eng, 2, a.data(), m * 8, JY_HOST, &dt));
+      JY_TRY(jy_stage(eng, 3, b.data(), m * 8, JY_HOST, &da));
+      JY_TRY(jy_stage(eng, 4, c.data(), m * 8, JY_HOST, &dp));
+      JY_TRY(jy_stage(eng, 5, d.data(), m * 8, JY_HOST, &dl));
+      JY_TRY(jy_stage_end(eng));
+      JY_TRY(jy_tlog_write_batch(eng, m, (const uint8_t*)dop, (const u32*)ds, (const u64*)dt, (const u64*)da,
+                                 (const u64*)dp, (const u64*)dl));
+    }
+    return JY_OK;
+  }
+  if (!op || !ts || !arg || !pre || !lr) return eng->fail(JY_EINVAL, "a device batch passes every column");
+  return jy_tlog_write_batch(eng, n, op, slot, ts, arg, pre, lr);
+}
+
+int32_t jy_tlog_deltas_size(jy_engine* eng, uint64_t* n_out) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  return jy_tlog_pending(eng, n_out);
+}
+
+int32_t jy_tlog_flush(jy_engine* eng, uint64_t cap_keys, uint64_t cap_ent, uint32_t* slot_out, uint64_t* cutoff_out,
+                      uint64_t* offs_out, uint64_t* ts_out, uint64_t* pre_out, uint64_t* lr_out, uint64_t* nkeys_out,
+                      uint64_t* nent_out, int32_t mem) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  u64 k = 0, m = 0;
+  // sizes first (nothing written or cleared)
+  JY_TRY(jy_tlog_flush_dev(eng, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, &k, &m));
+  *nkeys_out = k;
+  *nent_out = m;
+  if (k == 0 || cap_keys < k || cap_ent < m) return JY_OK;
+  u32* ds = slot_out;
+  u64 *dc = cutoff_out, *doff = offs_out, *dt = ts_out, *dp = pre_out, *dl = lr_out;
+  if (mem == JY_HOST) {
+    void* p;
+    JY_TRY(jy_scratch(eng, 0, k * 4 + 64, &p));
+    ds = static_cast<u32*>(p);
+    JY_TRY(jy_scratch(eng, 1, k * 8 + 64, &p));
+    dc = static_cast<u64*>(p);
+    JY_TRY(jy_scratch(eng, 2, (k + 1) * 8 + 64, &p));
+    doff = static_cast<u64*>(p);
+    JY_TRY(jy_scratch(eng, 3, m * 8 + 64, &p));
+    dt = static_cast<u64*>(p);
+    JY_TRY(jy_scratch(eng, 4, m * 8 + 64, &p));
+    dp = static_cast<u64*>(p);
+    JY_TRY(jy_scratch(eng, 5, m * 8 + 64, &p));
+    dl = static_cast<u64*>(p);
+  }
+  JY_TRY(jy_tlog_flush_dev(eng, k, m, ds, dc, doff, dt, dp, dl, &k, &m));
+  if (mem == JY_HOST) {
+    JY_HIP(eng, hipMemcpyAsync(slot_out, ds, k * 4, hipMemcpyDeviceToHost, eng->stream));
+    JY_HIP(eng, hipMemcpyAsync(cutoff_out, dc, k * 8, hipMemcpyDeviceToHost, eng->stream));
+    JY_HIP(eng, hipMemcpyAsync(offs_out, doff, (k + 1) * 8, hipMemcpyDeviceToHost, eng->stream));
+    if (m) {
+      JY_HIP(eng, hipMemcpyAsync(ts_out, dt, m * 8, hipMemcpyDeviceToHost, eng->stream));
+      JY_HIP(eng, hipMemcpyAsync(pre_out, dp, m * 8, hipMemcpyDeviceToHost, eng->stream));
+      JY_HIP(eng, hipMemcpyAsync(lr_out, dl, m * 8, hipMemcpyDeviceToHost, eng->stream));
+    }
+  }
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  return JY_OK;
+}
+
 int32_t jy_tlog_read_sizes(jy_engine* eng, uint64_t n, const uint32_t* slots, uint64_t* len, uint64_t* cut) {
   JY_HIP(eng, hipSetDevice(eng->device));
   if (n == 0) return JY_OK;

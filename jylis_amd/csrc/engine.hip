@@ -11,6 +11,7 @@
 #include <cstring>
 
 #include "jy_internal.hpp"
+#include "jy_scan.hpp"
 
 namespace {
 
@@ -52,6 +53,29 @@ int32_t jy_realloc(jy_engine* eng, void** p, u64 old_bytes, u64 new_bytes, bool 
     JY_HIP(eng, hipMemsetAsync(static_cast<uint8_t*>(np) + old_bytes, 0, new_bytes - old_bytes, eng->stream));
   jy_dev_free(eng, *p);
   *p = np;
+  return JY_OK;
+}
+
+int32_t jy_dscan_ctx(jy_engine* eng, u64 ntiles, u64** status, u32** tick, u32* epoch) {
+  if (!eng->dscan_tick) {
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&eng->dscan_tick), 64, "scan tickets"));
+    JY_HIP(eng, hipMemsetAsync(eng->dscan_tick, 0, 64, eng->stream));
+  }
+  DevArray& a = eng->dscan_st;
+  if (a.bytes < ntiles * 8) {
+    const u64 nb = std::max<u64>(round_up(2 * ntiles * 8, 256), 4096);
+    JY_TRY(jy_realloc(eng, &a.p, a.bytes, nb, true));
+    JY_HIP(eng, hipMemsetAsync(a.p, 0, nb, eng->stream));  // old words may carry any epoch
+    a.bytes = nb;
+  }
+  eng->dscan_epoch++;
+  if ((eng->dscan_epoch & ((1u << jyscan::kEpochBits) - 1)) == 0) {  // wrap: no stale word may match
+    eng->dscan_epoch = 1;
+    JY_HIP(eng, hipMemsetAsync(a.p, 0, a.bytes, eng->stream));
+  }
+  *status = static_cast<u64*>(a.p);
+  *tick = eng->dscan_tick;
+  *epoch = eng->dscan_epoch;
   return JY_OK;
 }
 
@@ -258,6 +282,13 @@ void jy_engine_destroy(jy_engine* eng) {
   F(eng->tlog.ctr);
   if (eng->tlog.pin) hipHostFree(eng->tlog.pin);
   if (eng->tlog.ready) hipEventDestroy(eng->tlog.ready);
+  F(eng->tlog_d.meta);
+  F(eng->tlog_d.pool);
+  F(eng->tlog_d.ctr);
+  if (eng->tlog_d.pin) hipHostFree(eng->tlog_d.pin);
+  if (eng->tlog_d.ready) hipEventDestroy(eng->tlog_d.ready);
+  F(eng->tl_dflag);
+  F(eng->tl_dcount);
   for (auto& k : eng->kdir) jy_keydir_free(eng, k);
   F(eng->ujson.vv);
   F(eng->ujson.meta);
@@ -271,6 +302,10 @@ void jy_engine_destroy(jy_engine* eng) {
   F(eng->ujson.vvd);
   F(eng->ujson.tick);
   for (auto& a : eng->ujson.st) F(a.p);
+  F(eng->ujson.tmap.p);
+  F(eng->dscan_st.p);
+  F(eng->dscan_tick);
+  F(eng->ujson.stats);
   if (eng->ujson.pin) hipHostFree(eng->ujson.pin);
   for (hipEvent_t e : eng->ujson.ready)
     if (e) hipEventDestroy(e);

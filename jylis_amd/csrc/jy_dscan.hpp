@@ -1,0 +1,213 @@
+// jy_dscan.hpp -- device-wide scans and selects for the engine (gfx950): one
+// launch each, a single pass with a decoupled look-back over ticketed tiles
+// (jy_scan.hpp).  Replaces the CUB-compatible DeviceScan / DeviceSelect of
+// round 1 on the product path (flush, key interning, log compaction, segment
+// ids).
+//
+// Status words are epoch-tagged (no reset between launches); the ticket
+// counter is reset by the workgroup that draws the launch's last ticket (every
+// other ticket is drawn by then).  Each launch takes a fresh epoch from the
+// engine (jy_dscan_ctx).
+#pragma once
+
+#include "jy_internal.hpp"
+#include "jy_scan.hpp"
+
+namespace jydscan {
+
+constexpr int kThreads = 256;
+constexpr int kPer = 8;
+constexpr u64 kTileItems = (u64)kThreads * kPer;  // 2048 items per tile
+
+struct Ctx {
+  u64* status;
+  u32* tick;
+  u32 epoch;
+};
+
+struct OpSum {
+  __device__ __forceinline__ u64 operator()(u64 a, u64 b) const { return a + b; }
+  static constexpr u64 kId = 0;
+};
+struct OpMax {
+  __device__ __forceinline__ u64 operator()(u64 a, u64 b) const { return a > b ? a : b; }
+  static constexpr u64 kId = 0;
+};
+
+template <class Op>
+__device__ __forceinline__ u64 wave_reduce(u64 x) {
+  Op op;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = op(x, __shfl_xor(x, o));
+  return x;
+}
+template <class Op>
+__device__ __forceinline__ u64 wave_incl(u64 x) {
+  Op op;
+  const int lane = __lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const u64 y = __shfl_up(x, o);
+    if (lane >= o) x = op(x, y);
+  }
+  return x;
+}
+// exclusive scan over the workgroup (identity for thread 0) and the total
+template <class Op>
+__device__ __forceinline__ u64 block_excl(u64 x, u64* lds, u64& total) {
+  Op op;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const u64 inc = wave_incl<Op>(x);
+  if (lane == 63) lds[w] = inc;
+  __syncthreads();
+  u64 off = Op::kId, tot = Op::kId;
+#pragma unroll
+  for (int i = 0; i < kThreads / 64; i++) {
+    const u64 v = lds[i];
+    if (i < w) off = op(off, v);
+    tot = op(tot, v);
+  }
+  __syncthreads();
+  total = tot;
+  const u64 ex = __shfl_up(inc, 1);
+  return op(off, lane == 0 ? Op::kId : ex);
+}
+
+// the look-back of jy_scan.hpp, generic over the operator (values < 2^40)
+template <class Op>
+__device__ __forceinline__ u64 lookback(const Ctx& c, u32 tile, u64 agg, u64* lds) {
+  using namespace jyscan;
+  Op op;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const u64 ep = (u64)(c.epoch & ((1u << kEpochBits) - 1));
+    if (lane == 0)
+      __hip_atomic_store(c.status + tile, lb_word(c.epoch, tile == 0 ? 2 : 1, agg), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    u64 excl = Op::kId;
+    if (tile > 0) {
+      long long top = (long long)tile - 1;
+      for (;;) {
+        const long long j = top - lane;
+        u64 w;
+        for (;;) {
+          w = j >= 0 ? __hip_atomic_load(c.status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                     : lb_word(c.epoch, 2, Op::kId);
+          if ((w >> 42) == ep && ((w >> 40) & 3u) != 0) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        const u64 incl = __ballot(((w >> 40) & 3u) == 2);
+        if (incl) {
+          const int L = __ffsll((unsigned long long)incl) - 1;
+          excl = op(excl, wave_reduce<Op>(lane <= L ? (w & kValMask) : Op::kId));
+          break;
+        }
+        excl = op(excl, wave_reduce<Op>(w & kValMask));
+        top -= 64;
+      }
+      if (lane == 0)
+        __hip_atomic_store(c.status + tile, lb_word(c.epoch, 2, op(excl, agg)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) *lds = excl;
+  }
+  __syncthreads();
+  const u64 r = *lds;
+  __syncthreads();
+  return r;
+}
+
+// out[i] = Op-prefix of ld(0..i-1) (exclusive) or of ld(0..i) (inclusive),
+// for i < n; items thread-consecutive within a tile
+template <class Op, bool kIncl, class Ld, class St>
+__global__ __launch_bounds__(kThreads) void k_scan(Ctx c, u64 n, u64 ntiles, Ld ld, St st) {
+  __shared__ u64 red[kThreads / 64];
+  __shared__ u64 pre;
+  __shared__ u32 tk;
+  Op op;
+  const u32 t = jyscan::ticket(c.tick, &tk);
+  if (t == ntiles - 1 && threadIdx.x == 0) *c.tick = 0;  // the launch's last ticket: all are drawn
+  const u64 i0 = (u64)t * kTileItems + (u64)threadIdx.x * kPer;
+  u64 v[kPer], acc = Op::kId;
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {
+    v[u] = i0 + u < n ? ld(i0 + u) : Op::kId;
+    acc = op(acc, v[u]);
+  }
+  u64 tot;
+  const u64 off = block_excl<Op>(acc, red, tot);
+  const u64 p = lookback<Op>(c, t, tot, &pre);
+  u64 run = op(p, off);
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {
+    const u64 i = i0 + u;
+    const u64 nx = op(run, v[u]);
+    if (i < n) st(i, kIncl ? nx : run);
+    run = nx;
+  }
+}
+
+// indices i < n with pred(i), in order, into out; the count into *count
+template <class Pred>
+__global__ __launch_bounds__(kThreads) void k_select(Ctx c, u64 n, u64 ntiles, Pred pred, u32* __restrict__ out,
+                                                     u32* __restrict__ count) {
+  __shared__ u64 red[kThreads / 64];
+  __shared__ u64 pre;
+  __shared__ u32 tk;
+  const u32 t = jyscan::ticket(c.tick, &tk);
+  if (t == ntiles - 1 && threadIdx.x == 0) *c.tick = 0;
+  const u64 i0 = (u64)t * kTileItems + (u64)threadIdx.x * kPer;
+  u32 f = 0;
+  u64 acc = 0;
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {
+    const bool s = i0 + u < n && pred(i0 + u);
+    f |= (u32)s << u;
+    acc += s;
+  }
+  u64 tot;
+  const u64 off = block_excl<OpSum>(acc, red, tot);
+  const u64 p = lookback<OpSum>(c, t, tot, &pre);
+  u64 pos = p + off;
+#pragma unroll
+  for (int u = 0; u < kPer; u++)
+    if (f >> u & 1) out[pos++] = (u32)(i0 + u);
+  if (t == ntiles - 1 && threadIdx.x == 0) *count = (u32)(p + tot);
+}
+
+inline u64 tiles_of(u64 n) { return n == 0 ? 1 : (n + kTileItems - 1) / kTileItems; }
+
+// a scan launch over n items: ld(i) -> u64, st(i, prefix)
+template <class Op, bool kIncl, class Ld, class St>
+int32_t scan(jy_engine* eng, u64 n, Ld ld, St st) {
+  if (n == 0) return JY_OK;
+  const u64 nt = tiles_of(n);
+  Ctx c;
+  JY_TRY(jy_dscan_ctx(eng, nt, &c.status, &c.tick, &c.epoch));
+  hipLaunchKernelGGL((k_scan<Op, kIncl, Ld, St>), dim3((u32)nt), dim3(kThreads), 0, eng->stream, c, n, nt, ld, st);
+  JY_HIP(eng, hipGetLastError());
+  return JY_OK;
+}
+template <class Pred>
+int32_t select(jy_engine* eng, u64 n, Pred pred, u32* out, u32* count) {
+  const u64 nt = tiles_of(n);
+  Ctx c;
+  JY_TRY(jy_dscan_ctx(eng, nt, &c.status, &c.tick, &c.epoch));
+  hipLaunchKernelGGL((k_select<Pred>), dim3((u32)nt), dim3(kThreads), 0, eng->stream, c, n, nt, pred, out, count);
+  JY_HIP(eng, hipGetLastError());
+  return JY_OK;
+}
+
+// loaders / storers
+template <class T>
+struct LdArr {
+  const T* a;
+  __device__ __forceinline__ u64 operator()(u64 i) const { return (u64)a[i]; }
+};
+template <class T>
+struct StArr {
+  T* a;
+  __device__ __forceinline__ void operator()(u64 i, u64 v) const { a[i] = (T)v; }
+};
+
+}  // namespace jydscan

@@ -307,6 +307,8 @@ struct UjsonState {  // per-document pool segments + dense vv
   u64 used_e = 0, used_c = 0;          // bump pointers after converge done - 1 (exact)
   u64 live_e = 0, live_c = 0;          // upper bounds of live elements / cloud dots
   DevArray st[6];                      // look-back status words of the scans (zeroed once)
+  DevArray tmap;                       // epoch-tagged tile -> doc maps of long segments (zeroed once)
+  u64* stats = nullptr;                // [8] cumulative converge counters (jy_ujson_stats)
 };
 
 struct Arena {
@@ -334,11 +336,22 @@ struct jy_engine {
   CounterState cnt[2];  // [0] GCOUNT, [1] PNCOUNT
   TregState treg;
   TlogState tlog;
+  // TLOG write path: the pending delta logs (repo_tlog.pony _deltas) are a
+  // second store of the same layout; tl_dflag marks the keys _delta_for
+  // touched since the last flush
+  TlogState tlog_d;
+  u32* tl_dflag = nullptr;
+  u64 tl_dkcap = 0;
+  u64* tl_dcount = nullptr;
   UjsonState ujson;
 
   // scratch (device) reused across calls, stream-ordered
   // 0-7 staged inputs, 8-14 and 16-23 merge temporaries, 15 scan temp storage
   DevArray scratch[24];
+  // device-wide scans / selects (jy_dscan.hpp): epoch-tagged look-back words
+  DevArray dscan_st;
+  u32* dscan_tick = nullptr;
+  u32 dscan_epoch = 0;
   // column lists of block merges, kept resident: a routed step cycles
   // through a few lists, and uploading one must not stall the stream
   struct ColList {
@@ -429,6 +442,8 @@ inline double jy_now_us() {
 
 // engine.hip helpers used by the kernel translation units
 int32_t jy_scratch(jy_engine* eng, int idx, u64 bytes, void** out);
+// look-back status words for `ntiles` tiles, the ticket counter and a fresh epoch
+int32_t jy_dscan_ctx(jy_engine* eng, u64 ntiles, u64** status, u32** tick, u32* epoch);
 // copy a borrowed input into device memory if it is on the host; returns a
 // device pointer valid in stream order (scratch slot `idx`)
 int32_t jy_stage(jy_engine* eng, int idx, const void* src, u64 bytes, int32_t mem, const void** dev_out);
@@ -471,6 +486,16 @@ int32_t jy_tlog_sizes(jy_engine* eng, u64 n, const u32* slots, u64* len, u64* cu
 int32_t jy_tlog_gather(jy_engine* eng, u64 n, const u32* slots, const u64* ooff, u64* ts, u64* pre, u64* lr);
 int32_t jy_tlog_merge(jy_engine* eng, u64 nkeys, const u32* slot, const u64* cutoff, const u64* offs, u64 nent,
                       const u64* ts, const u64* pre, const u64* lr);
+struct TlogState;
+int32_t jy_tlog_merge_into(jy_engine* eng, TlogState& t, u64 nd, const u32* slot, const u64* dcut, const u64* doff,
+                           u64 nent, const u64* dts, const u64* dpre, const u64* dlr);
+// TLOG write path (k_tlog.hip): one command per key (device arrays)
+int32_t jy_tlog_write_batch(jy_engine* eng, u64 n, const uint8_t* op, const u32* slot, const u64* ts, const u64* arg,
+                            const u64* pre, const u64* lr);
+int32_t jy_tlog_pending(jy_engine* eng, u64* count);
+// flush: pending slots, their delta logs; nkeys / nent: sizes (first call with caps 0 to size)
+int32_t jy_tlog_flush_dev(jy_engine* eng, u64 cap_keys, u64 cap_ent, u32* slots, u64* cut, u64* offs, u64* ts,
+                          u64* pre, u64* lr, u64* nkeys, u64* nent);
 
 int32_t jy_dev_alloc(jy_engine* eng, void** p, u64 bytes, const char* what);
 void jy_dev_free(jy_engine* eng, void* p);

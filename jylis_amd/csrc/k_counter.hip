@@ -17,8 +17,8 @@
 
 #include <algorithm>
 
-#include <hipcub/hipcub.hpp>
 
+#include "jy_dscan.hpp"
 #include "jy_internal.hpp"
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(kThreads) void k_cnt_record(const u64* __restrict__
 
 struct PendingPred {
   const u32* dflag;
-  __device__ bool operator()(u32 s) const { return dflag[s] != 0; }
+  __device__ bool operator()(u64 s) const { return dflag[s] != 0; }
 };
 
 // flush_deltas (repo_gcount.pony:18-23): emit every pending key, then clear it
@@ -289,14 +289,9 @@ int32_t jy_cnt_flush(jy_engine* eng, int which, u64 nkeys, u64 cap, u32* slots, 
   if (cnt == 0) return JY_OK;
   if (cnt > cap) return eng->fail(JY_ERANGE, "flush output capacity is smaller than the pending delta count");
   nkeys = std::min<u64>(nkeys, c.dkcap);
-  void *tmp = nullptr, *num = nullptr;
-  size_t tb = 0;
-  hipcub::CountingInputIterator<u32> it(0);
-  PendingPred pred{c.dflag};
-  JY_HIP(eng, hipcub::DeviceSelect::If(nullptr, tb, it, slots, (u32*)nullptr, (int)nkeys, pred, eng->stream));
-  JY_TRY(jy_scratch(eng, 15, tb, &tmp));
+  void* num = nullptr;
   JY_TRY(jy_scratch(eng, 14, 8, &num));
-  JY_HIP(eng, hipcub::DeviceSelect::If(tmp, tb, it, slots, static_cast<u32*>(num), (int)nkeys, pred, eng->stream));
+  JY_TRY(jydscan::select(eng, nkeys, PendingPred{c.dflag}, slots, static_cast<u32*>(num)));
   hipLaunchKernelGGL(k_cnt_flush, dim3((u32)((cnt + kThreads - 1) / kThreads)), dim3(kThreads), 0, eng->stream,
                      c.dflag, (const u64*)c.dval, (u32)(which + 1), (const u32*)slots, cnt, cap, vals, mask);
   JY_HIP(eng, hipGetLastError());

@@ -31,13 +31,13 @@
 // table probe chain (8 B entries), 4 B slot out; a new key adds its bytes +
 // 16 B written.
 
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
 
+#include "jy_dscan.hpp"
 #include "jy_internal.hpp"
 
 namespace {
@@ -354,14 +354,8 @@ int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, co
   LAUNCH(k_key_claim, n, I, D, res, th, owner, pos);
   LAUNCH(k_key_first, n, n, res, owner, first);
   LAUNCH(k_key_flags, n + 1, I, res, owner, first, flag, blen);
-  size_t tmp = 0;
-  JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, flag, rank, (int)(n + 1), eng->stream));
-  JY_TRY(jy_scratch(eng, 15, tmp, &p));
-  JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(p, tmp, flag, rank, (int)(n + 1), eng->stream));
-  tmp = 0;
-  JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, blen, boff, (int)(n + 1), eng->stream));
-  JY_TRY(jy_scratch(eng, 15, tmp, &p));
-  JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(p, tmp, blen, boff, (int)(n + 1), eng->stream));
+  JY_TRY((jydscan::scan<jydscan::OpSum, false>(eng, n + 1, jydscan::LdArr<u32>{flag}, jydscan::StArr<u32>{rank})));
+  JY_TRY((jydscan::scan<jydscan::OpSum, false>(eng, n + 1, jydscan::LdArr<u64>{blen}, jydscan::StArr<u64>{boff})));
   LAUNCH(k_key_commit, n, I, D, K.bytes, K.n, K.blen, res, th, owner, pos, first, rank, boff, slots);
   u32 nnew = 0;
   u64 nbytes = 0;

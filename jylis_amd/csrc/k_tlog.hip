@@ -44,10 +44,10 @@
 // and read back.  Rebuilt keys add 32 B read + 32 B written per surviving
 // entry.  See DESIGN.md "TLOG".
 
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 
+#include "jy_dscan.hpp"
 #include "jy_internal.hpp"
 
 namespace {
@@ -165,7 +165,6 @@ constexpr int kTile = 64;
 // code is general, 1 measured fastest: 2 and 4 raise VGPRs and cut waves in flight)
 constexpr int kU = 1;
 constexpr int kCU = 1;  // output entries per lane per pass of the rebuild (2: same time)
-typedef hipcub::BlockScan<u32, kTile> BlockScanU32;
 
 constexpr u32 kKept = 0x80000000u;  // eqx: kept flag | # kept entries of the key before this one
 
@@ -395,7 +394,6 @@ __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __
   __shared__ u64 l_woff[kTile + 1];
   __shared__ u64 l_src[kTile], l_dst[kTile], l_blo[kTile], l_bhi[kTile];
   __shared__ u32 l_drop[kTile], l_surv[kTile], l_M[kTile];
-  __shared__ typename BlockScanU32::TempStorage scan_tmp;
   const u32 tid = threadIdx.x;
   const u64 k0 = (u64)blockIdx.x * kTile;
   const u32 nt = (u32)(A.nd - k0 < kTile ? A.nd - k0 : kTile);
@@ -421,8 +419,8 @@ __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __
       w = (P.len - P.drop) + (u32)(bhi - blo);
     }
   }
-  u32 wo, wtot;
-  BlockScanU32(scan_tmp).ExclusiveSum(w, wo, wtot);
+  const u32 winc = jyscan::wave_incl<u32>(w);  // a key tile is one wave
+  const u32 wo = winc - w, wtot = __shfl(winc, 63);
   if (tid < nt) l_woff[tid] = wo;
   if (tid == 0) l_woff[nt] = wtot;
   __syncthreads();
@@ -585,6 +583,113 @@ __global__ __launch_bounds__(kThreads) void k_seg_starts(const u64* __restrict__
   if (k < nseg && offs[k] < offs[k + 1]) out[offs[k]] = (u32)k;
 }
 
+// ---- write path: RepoTLOG.ins / trimat / trim / clr (repo_tlog.pony:85-111) ----
+// Each command (one per key here) becomes a delta log for the state -- at
+// most one entry, and a cutoff -- judged against the state as it is:
+//   INS     the entry (ts, value); changes the state iff ts >= cutoff and the
+//           entry is new (TLog.write)
+//   TRIMAT  cutoff ts; changes iff ts > cutoff (raise_cutoff)
+//   TRIM n  cutoff = ts of the n-th newest entry (n == 0: CLR; past the end:
+//           nothing, as the reference's try swallows the bounds error)
+//   CLR     cutoff = newest ts + 1 (U64 wraps), nothing on an empty log
+// and, where the state changed, the same delta goes to the key's pending
+// delta log (d.write / d.raise_cutoff(l.cutoff) of the reference).  Every
+// command marks its key pending (_delta_for runs either way).
+struct WCmd {
+  const uint8_t* op;
+  const u32* slot;
+  const u64* ts;
+  const u64* arg;
+  const u64* pre;
+  const u64* lr;
+};
+__global__ __launch_bounds__(kThreads) void k_tlog_wprep(WCmd W, u64 n, const TMeta* __restrict__ meta,
+                                                         const TRec* __restrict__ pool,
+                                                         const uint8_t* __restrict__ arena, u64* __restrict__ scut,
+                                                         u64* __restrict__ sflag, u64* __restrict__ dcut,
+                                                         u64* __restrict__ dflag, u32* __restrict__ pend,
+                                                         u64* __restrict__ pcount) {
+  const u64 i = gid();
+  if (i >= n) return;
+  const u32 s = W.slot[i];
+  const TMeta m = meta[s];
+  u64 raise = 0;
+  bool ent = false, changed = false;
+  const uint8_t op = W.op[i];
+  if (op == JY_TLOG_INS) {
+    ent = true;
+    const Ent x{W.ts[i], W.pre[i], W.lr[i]};
+    if (x.t >= m.cut) {  // present? the log is ascending (ts, value) from base
+      u64 lo = m.base, hi = m.base + m.len;
+      while (lo < hi) {
+        const u64 mid = (lo + hi) >> 1;
+        if (cmp_at(pool, mid, x, arena) < 0) lo = mid + 1;
+        else hi = mid;
+      }
+      changed = !(lo < m.base + m.len && cmp_at(pool, lo, x, arena) == 0);
+    }
+  } else if (op == JY_TLOG_TRIMAT) {
+    raise = W.ts[i];
+    changed = raise > m.cut;
+  } else {
+    const u64 cnt = op == JY_TLOG_CLR ? 0 : W.arg[i];
+    if (cnt == 0) {
+      if (m.len) {
+        raise = m.newest + 1;
+        changed = raise > m.cut;
+      }
+    } else if (cnt - 1 < m.len) {
+      raise = pool[m.base + m.len - cnt].ts;
+      changed = raise > m.cut;
+    }
+    if (!changed) raise = 0;
+  }
+  scut[i] = raise;
+  sflag[i] = ent;
+  dcut[i] = changed ? raise : 0;
+  dflag[i] = ent && changed;
+  if (atomicExch(pend + s, 1u) == 0) atomicAdd((unsigned long long*)pcount, 1ull);
+}
+
+// the entries of the INS commands, packed for the state's delta (positions
+// from the scan of sflag) and for the pending deltas (scan of dflag)
+__global__ __launch_bounds__(kThreads) void k_tlog_wpack(WCmd W, u64 n, const u64* __restrict__ soff,
+                                                         const u64* __restrict__ doff, u64* __restrict__ sts,
+                                                         u64* __restrict__ spre, u64* __restrict__ slr,
+                                                         u64* __restrict__ dts, u64* __restrict__ dpre,
+                                                         u64* __restrict__ dlr) {
+  const u64 i = gid();
+  if (i >= n) return;
+  if (soff[i + 1] != soff[i]) {
+    const u64 o = soff[i];
+    sts[o] = W.ts[i];
+    spre[o] = W.pre[i];
+    slr[o] = W.lr[i];
+  }
+  if (doff[i + 1] != doff[i]) {
+    const u64 o = doff[i];
+    dts[o] = W.ts[i];
+    dpre[o] = W.pre[i];
+    dlr[o] = W.lr[i];
+  }
+}
+
+// flush: the pending keys' delta logs are emptied (their pool space is
+// released wholesale: every pending key is flushed at once)
+__global__ __launch_bounds__(kThreads) void k_tlog_wreset(TMeta* __restrict__ dmeta, u32* __restrict__ pend,
+                                                          const u32* __restrict__ slots, u64 n) {
+  const u64 i = gid();
+  if (i >= n) return;
+  const u32 s = slots[i];
+  dmeta[s] = TMeta{0, 0, 0, 0, 0};
+  pend[s] = 0;
+}
+
+struct PendPred {
+  const u32* pend;
+  __device__ bool operator()(u64 s) const { return pend[s] != 0; }
+};
+
 u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kThreads - 1) / kThreads); }
 
 #define LAUNCH(k, n, ...)                                                                          \
@@ -594,18 +699,12 @@ u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kThreads - 1) / kThrea
   } while (0)
 
 int32_t scan_excl_u64(jy_engine* eng, const u64* in, u64* out, u64 n_plus_1) {
-  size_t tmp = 0;
-  JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, in, out, (int)n_plus_1, eng->stream));
-  void* t;
-  JY_TRY(jy_scratch(eng, 15, tmp, &t));
-  JY_HIP(eng, hipcub::DeviceScan::ExclusiveSum(t, tmp, in, out, (int)n_plus_1, eng->stream));
-  return JY_OK;
+  return jydscan::scan<jydscan::OpSum, false>(eng, n_plus_1, jydscan::LdArr<u64>{in}, jydscan::StArr<u64>{out});
 }
 
 // rewrite every log back to back into a fresh pool with `room` free entries
 // after them; synchronises (the new size is read back)
-int32_t tlog_compact(jy_engine* eng, u64 room) {
-  TlogState& t = eng->tlog;
+int32_t tlog_compact(jy_engine* eng, TlogState& t, u64 room) {
   const u64 nk = eng->nkeys[JY_TLOG];
   const double t_enter = jy_tracing() ? jy_now_us() : 0;
   void* p;
@@ -657,16 +756,11 @@ int32_t jy_seg_ids(jy_engine* eng, const u64* offs, u64 nseg, u64 n, u32* out) {
   if (n == 0) return JY_OK;
   JY_HIP(eng, hipMemsetAsync(out, 0, n * 4, eng->stream));
   LAUNCH(k_seg_starts, nseg, offs, nseg, out);
-  size_t tmp = 0;
-  JY_HIP(eng, hipcub::DeviceScan::InclusiveScan(nullptr, tmp, out, out, hipcub::Max(), (int)n, eng->stream));
-  void* t;
-  JY_TRY(jy_scratch(eng, 15, tmp, &t));
-  JY_HIP(eng, hipcub::DeviceScan::InclusiveScan(t, tmp, out, out, hipcub::Max(), (int)n, eng->stream));
-  return JY_OK;
+  // in place: a tile loads its items before it stores them, and no other tile reads them
+  return jydscan::scan<jydscan::OpMax, true>(eng, n, jydscan::LdArr<u32>{out}, jydscan::StArr<u32>{out});
 }
 
-int32_t jy_tlog_grow(jy_engine* eng, u64 need) {
-  TlogState& t = eng->tlog;
+int32_t tlog_grow_store(jy_engine* eng, TlogState& t, u64 need) {
   if (!t.ctr) {
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.ctr), 64, "tlog counters"));
     JY_HIP(eng, hipMemsetAsync(t.ctr, 0, 64, eng->stream));
@@ -685,13 +779,24 @@ int32_t jy_tlog_grow(jy_engine* eng, u64 need) {
   return JY_OK;
 }
 
+int32_t jy_tlog_grow(jy_engine* eng, u64 need) {
+  JY_TRY(tlog_grow_store(eng, eng->tlog, need));
+  if (eng->tlog_d.ctr) JY_TRY(tlog_grow_store(eng, eng->tlog_d, eng->tlog.kcap));
+  return JY_OK;
+}
+
 // new slots start as empty logs: their meta is zeroed when it is allocated
 int32_t jy_tlog_extend(jy_engine*, u64, u64) { return JY_OK; }
 
 int32_t jy_tlog_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* dcut, const u64* doff, u64 nent,
                       const u64* dts, const u64* dpre, const u64* dlr) {
   JyTimed tm(eng);
-  TlogState& t = eng->tlog;
+  return jy_tlog_merge_into(eng, eng->tlog, nd, slot, dcut, doff, nent, dts, dpre, dlr);
+}
+
+// the merge into one store: the state, or the pending deltas of the write path
+int32_t jy_tlog_merge_into(jy_engine* eng, TlogState& t, u64 nd, const u32* slot, const u64* dcut, const u64* doff,
+                           u64 nent, const u64* dts, const u64* dpre, const u64* dlr) {
   const u64 nk = eng->nkeys[JY_TLOG];
   if (nd == 0 || nk == 0) return JY_OK;
   // worst case of fresh pool space this merge takes: every touched log
@@ -749,7 +854,7 @@ int32_t jy_tlog_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* dcut, 
     if (attempt == 2) return eng->fail(JY_ENOMEM, "tlog pool: no room after compaction");
     // room for this merge's rebuilds several times over; the last attempt
     // takes the worst case
-    JY_TRY(tlog_compact(eng, attempt == 0 ? 4 * (rebuilt + nent) : need));
+    JY_TRY(tlog_compact(eng, t, attempt == 0 ? 4 * (rebuilt + nent) : need));
   }
   t.live_bound += nent;
   hipLaunchKernelGGL(k_tlog_commit, dim3(tiles), dim3(kTile), 0, eng->stream, A, roff, t.ctr, t.pool, erank,
@@ -773,5 +878,106 @@ int32_t jy_tlog_sizes(jy_engine* eng, u64 n, const u32* slots, u64* len, u64* cu
 int32_t jy_tlog_gather(jy_engine* eng, u64 n, const u32* slots, const u64* ooff, u64* ts, u64* pre, u64* lr) {
   TlogState& t = eng->tlog;
   LAUNCH(k_tlog_gather, n, t.meta, t.pool, slots, ooff, n, ts, pre, lr);
+  return JY_OK;
+}
+
+// ---- TLOG write path --------------------------------------------------------
+namespace {
+int32_t tlog_pending_grow(jy_engine* eng) {
+  TlogState& d = eng->tlog_d;
+  JY_TRY(tlog_grow_store(eng, d, eng->tlog.kcap));
+  if (!eng->tl_dcount) {
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&eng->tl_dcount), 8, "tlog pending count"));
+    JY_HIP(eng, hipMemsetAsync(eng->tl_dcount, 0, 8, eng->stream));
+  }
+  if (eng->tl_dkcap < d.kcap || !eng->tl_dflag) {
+    void* f = eng->tl_dflag;
+    JY_TRY(jy_realloc(eng, &f, eng->tl_dkcap * 4, d.kcap * 4, true));
+    eng->tl_dflag = static_cast<u32*>(f);
+    eng->tl_dkcap = d.kcap;
+  }
+  return JY_OK;
+}
+}  // namespace
+
+int32_t jy_tlog_write_batch(jy_engine* eng, u64 n, const uint8_t* op, const u32* slot, const u64* ts, const u64* arg,
+                            const u64* pre, const u64* lr) {
+  if (n == 0) return JY_OK;
+  JY_TRY(tlog_pending_grow(eng));
+  void* p;
+  // (scratch 0..7 hold the staged commands; the merges use 8, 9, 12, 16)
+  JY_TRY(jy_scratch(eng, 10, (n + 1) * 8 * 8 + 64, &p));
+  u64* scut = static_cast<u64*>(p);
+  u64* sflag = scut + (n + 1);
+  u64* dcut = sflag + (n + 1);
+  u64* dflag = dcut + (n + 1);
+  u64* soff = dflag + (n + 1);
+  u64* doff = soff + (n + 1);
+  JY_TRY(jy_scratch(eng, 11, n * 8 * 6 + 64, &p));
+  u64* sts = static_cast<u64*>(p);
+  u64 *spre = sts + n, *slr = spre + n, *dts = slr + n, *dpre = dts + n, *dlr = dpre + n;
+  const WCmd W{op, slot, ts, arg, pre, lr};
+  TlogState& t = eng->tlog;
+  JY_HIP(eng, hipMemsetAsync(sflag + n, 0, 8, eng->stream));
+  JY_HIP(eng, hipMemsetAsync(dflag + n, 0, 8, eng->stream));
+  LAUNCH(k_tlog_wprep, n, W, n, t.meta, t.pool, eng->arena[JY_TLOG].p, scut, sflag, dcut, dflag, eng->tl_dflag,
+         eng->tl_dcount);
+  JY_TRY(scan_excl_u64(eng, sflag, soff, n + 1));
+  JY_TRY(scan_excl_u64(eng, dflag, doff, n + 1));
+  LAUNCH(k_tlog_wpack, n, W, n, soff, doff, sts, spre, slr, dts, dpre, dlr);
+  // n bounds the entry counts (the merges size from the device offsets)
+  JY_TRY(jy_tlog_merge_into(eng, t, n, slot, scut, soff, n, sts, spre, slr));
+  JY_TRY(jy_tlog_merge_into(eng, eng->tlog_d, n, slot, dcut, doff, n, dts, dpre, dlr));
+  return JY_OK;
+}
+
+int32_t jy_tlog_pending(jy_engine* eng, u64* count) {
+  *count = 0;
+  if (!eng->tl_dcount) return JY_OK;
+  JY_HIP(eng, hipMemcpyAsync(eng->pin_total, eng->tl_dcount, 8, hipMemcpyDeviceToHost, eng->stream));
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  *count = eng->pin_total[0];
+  return JY_OK;
+}
+
+// two calls: with caps too small (e.g. 0) it only reports the sizes; with
+// room for both it writes (device arrays) and clears the pending deltas
+int32_t jy_tlog_flush_dev(jy_engine* eng, u64 cap_keys, u64 cap_ent, u32* slots, u64* cut, u64* offs, u64* ts,
+                          u64* pre, u64* lr, u64* nkeys, u64* nent) {
+  u64 k = 0;
+  JY_TRY(jy_tlog_pending(eng, &k));
+  *nkeys = k;
+  *nent = 0;
+  if (k == 0) return JY_OK;
+  TlogState& d = eng->tlog_d;
+  void* p;
+  JY_TRY(jy_scratch(eng, 13, k * 4 + (k + 1) * 24 + 64, &p));
+  u32* sl = static_cast<u32*>(p);
+  u64* lens = reinterpret_cast<u64*>((reinterpret_cast<uintptr_t>(sl + k) + 15) & ~uintptr_t(15));
+  u64* cuts = lens + (k + 1);
+  u64* loff = cuts + (k + 1);
+  void* num;
+  JY_TRY(jy_scratch(eng, 14, 8, &num));
+  JY_TRY(jydscan::select(eng, std::min<u64>(eng->nkeys[JY_TLOG], eng->tl_dkcap), PendPred{eng->tl_dflag}, sl,
+                         static_cast<u32*>(num)));
+  JY_HIP(eng, hipMemsetAsync(lens + k, 0, 8, eng->stream));
+  LAUNCH(k_tlog_sizes, k, d.meta, sl, k, lens, cuts);
+  JY_TRY(scan_excl_u64(eng, lens, loff, k + 1));
+  JY_HIP(eng, hipMemcpyAsync(eng->pin_total, loff + k, 8, hipMemcpyDeviceToHost, eng->stream));
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  const u64 m = eng->pin_total[0];
+  *nent = m;
+  if (cap_keys < k || cap_ent < m) return JY_OK;  // sizes only
+  JY_HIP(eng, hipMemcpyAsync(slots, sl, k * 4, hipMemcpyDeviceToDevice, eng->stream));
+  JY_HIP(eng, hipMemcpyAsync(cut, cuts, k * 8, hipMemcpyDeviceToDevice, eng->stream));
+  JY_HIP(eng, hipMemcpyAsync(offs, loff, (k + 1) * 8, hipMemcpyDeviceToDevice, eng->stream));
+  if (m) LAUNCH(k_tlog_gather, k, d.meta, d.pool, sl, loff, k, ts, pre, lr);
+  LAUNCH(k_tlog_wreset, k, d.meta, eng->tl_dflag, sl, k);
+  JY_HIP(eng, hipMemsetAsync(eng->tl_dcount, 0, 8, eng->stream));
+  // every pending key was flushed: the delta pool is empty again
+  JY_HIP(eng, hipMemsetAsync(d.ctr, 0, 8, eng->stream));
+  d.used_bound = 0;
+  d.live_bound = 0;
+  d.known = false;
   return JY_OK;
 }

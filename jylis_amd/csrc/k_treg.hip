@@ -36,8 +36,8 @@
 
 #include <algorithm>
 
-#include <hipcub/hipcub.hpp>
 
+#include "jy_dscan.hpp"
 #include "jy_internal.hpp"
 
 namespace {
@@ -306,7 +306,7 @@ __global__ __launch_bounds__(kThreads) void k_treg_gather(const u64* __restrict_
 
 struct TregPendingPred {
   const u32* dflag;
-  __device__ bool operator()(u32 s) const { return dflag[s] != 0; }
+  __device__ bool operator()(u64 s) const { return dflag[s] != 0; }
 };
 
 // flush_deltas (repo_treg.pony:18-22): emit each pending key's delta TReg and
@@ -524,14 +524,9 @@ int32_t jy_treg_flush_dev(jy_engine* eng, u64 nkeys, u64 cap, u32* slots, u64* o
   if (cnt == 0) return JY_OK;
   if (cnt > cap) return eng->fail(JY_ERANGE, "flush output capacity is smaller than the pending delta count");
   nkeys = std::min<u64>(nkeys, t.dkcap);
-  void *tmp = nullptr, *num = nullptr;
-  size_t tb = 0;
-  hipcub::CountingInputIterator<u32> it(0);
-  TregPendingPred pred{t.dflag};
-  JY_HIP(eng, hipcub::DeviceSelect::If(nullptr, tb, it, slots, (u32*)nullptr, (int)nkeys, pred, eng->stream));
-  JY_TRY(jy_scratch(eng, 15, tb, &tmp));
+  void* num = nullptr;
   JY_TRY(jy_scratch(eng, 14, 8, &num));
-  JY_HIP(eng, hipcub::DeviceSelect::If(tmp, tb, it, slots, static_cast<u32*>(num), (int)nkeys, pred, eng->stream));
+  JY_TRY(jydscan::select(eng, nkeys, TregPendingPred{t.dflag}, slots, static_cast<u32*>(num)));
   hipLaunchKernelGGL(k_treg_flush, dim3(blocks(cnt, kThreads)), dim3(kThreads), 0, eng->stream, t.dflag, t.dts,
                      t.dval, (const u32*)slots, cnt, ots, opre, olr);
   JY_HIP(eng, hipGetLastError());

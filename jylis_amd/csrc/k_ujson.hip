@@ -175,6 +175,13 @@ struct UjArgs {
   u32* sidB;
   u32* sidC;
   u32* sidD;
+  // ... except inside long segments: there a tile lying wholly in one doc
+  // finds it in its space's tile map (epoch << 32 | doc)
+  u64* tmA;
+  u64* tmB;
+  u64* tmC;
+  u64* tmD;
+  u64* stats;
   u64* tp;   // [tiles + 1] sc tile aggregates -> exclusive tile prefixes (U2 -> k_uj_tscan)
   u64* ktp;  // ... of ksc
   u64* st_ne;
@@ -183,6 +190,10 @@ struct UjArgs {
 
 __device__ __forceinline__ bool is_bad(const UjArgs& A, u64 k) { return A.bad[k] == A.epoch; }
 __device__ __forceinline__ void mark_bad(const UjArgs& A, u64 k) { A.bad[k] = A.epoch; }  // same value from every writer
+__device__ __forceinline__ u64 doc_at(const UjArgs& A, const u64* tm, u64 tile, const u32* sid, u64 i) {
+  const u64 v = tm[tile];
+  return (u32)(v >> 32) == A.epoch ? (u32)v : sid[i];
+}
 
 // A scan space of up to three kinds laid back to back, each cut into kTile
 // tiles from its own start.  U2 / U3 write each item's exclusive prefix
@@ -326,10 +337,9 @@ __device__ __forceinline__ void probe(u32 kern, u32 kind, u32 t, u64 c0, u64 c1,
 #define JY_PROBE(...)
 #endif
 
-constexpr u64 kLongSeg = 256;  // longer segments get their doc ids from the whole workgroup
-struct LongSeg {
-  u64 off, sz;
-  u32 k, sp;
+constexpr u64 kLongSeg = 2 * kTile;  // longer segments use the tile maps
+struct LongRun {
+  u32 f0, f1, k, sp;  // whole tiles [f0, f1) of space sp lie in doc k
 };
 
 // ---- U1: per delta doc (ticketed doc tiles first, for the look-back) and
@@ -337,11 +347,12 @@ struct LongSeg {
 __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_el, u64 t_cl, u64 t_vv) {
   __shared__ Shared S;
   __shared__ u32 l_slot[kDocTile];
-  __shared__ LongSeg l_long[4 * kDocTile];
+  __shared__ LongRun l_long[4 * kDocTile];
   __shared__ u32 l_nlong;
   if (blockIdx.x < ndt) {  // doc tiles: ticketed (the look-back walks tickets)
     if (threadIdx.x == 0) l_nlong = 0;
     const u32 t = jyscan::ticket(A.tick + T_U1, &S.tk);
+    JY_CLK(c0);
     const u64 k = (u64)t * kDocTile + threadIdx.x;
     u64 asz = 0, csz = 0;
     if (k < A.nd) {
@@ -378,32 +389,36 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_e
     }
     const u64 xc = jyscan::block_excl<kThreads, u64>(csz, S.red, tot);
     const u64 pc = jyscan::lookback(A.st_co, t, A.epoch, tot, &S.pre);
+    JY_CLK(c1);
     if (k < A.nd) {
       A.co[k] = pc + xc;
-      // per-item doc ids: a doc writes its own short segments; long ones are
-      // queued for the whole workgroup
-      auto ids = [&](int sp, u32* sid, u64 off, u64 sz) {
-        if (sz <= kLongSeg) {
+      // per-item doc ids; a long segment names its doc once per whole tile
+      // in the tile map and writes ids only in its partial end tiles
+      auto ids = [&](u32* sid, u64* tm, u64 off, u64 sz) {
+        const u64 f0 = (off + kTile - 1) / kTile, f1 = (off + sz) / kTile;  // whole tiles [f0, f1)
+        if (sz <= kLongSeg || f0 >= f1) {
           for (u64 j = 0; j < sz; j++) sid[off + j] = (u32)k;
-        } else {
-          const u32 q = atomicAdd(&l_nlong, 1u);
-          l_long[q] = LongSeg{off, sz, (u32)k, (u32)sp};
+          return;
         }
+        for (u64 j = off; j < f0 * kTile; j++) sid[j] = (u32)k;
+        for (u64 j = f1 * kTile; j < off + sz; j++) sid[j] = (u32)k;
+        const u32 q = atomicAdd(&l_nlong, 1u);  // the workgroup fills its tile-map run
+        l_long[q] = LongRun{(u32)f0, (u32)f1, (u32)k, (u32)(tm == A.tmA ? 0 : tm == A.tmB ? 1 : tm == A.tmC ? 2 : 3)};
       };
-      ids(0, A.sidA, pa + xa, asz);
-      ids(2, A.sidC, pc + xc, csz);
+      ids(A.sidA, A.tmA, pa + xa, asz);
+      ids(A.sidC, A.tmC, pc + xc, csz);
       const u64 b0 = A.deoff[k], d0 = A.dcoff[k];
-      ids(1, A.sidB, b0, A.deoff[k + 1] - b0);
-      ids(3, A.sidD, d0, A.dcoff[k + 1] - d0);
+      ids(A.sidB, A.tmB, b0, A.deoff[k + 1] - b0);
+      ids(A.sidD, A.tmD, d0, A.dcoff[k + 1] - d0);
     }
     if (t == ndt - 1 && threadIdx.x == 0) {
       A.co[A.nd] = pc + tot;
     }
     __syncthreads();
     for (u32 q = 0; q < l_nlong; q++) {
-      const LongSeg g = l_long[q];
-      u32* sid = g.sp == 0 ? A.sidA : g.sp == 1 ? A.sidB : g.sp == 2 ? A.sidC : A.sidD;
-      for (u64 j = threadIdx.x; j < g.sz; j += kThreads) sid[g.off + j] = g.k;
+      const LongRun g = l_long[q];
+      u64* tm = g.sp == 0 ? A.tmA : g.sp == 1 ? A.tmB : g.sp == 2 ? A.tmC : A.tmD;
+      for (u64 m = g.f0 + threadIdx.x; m < g.f1; m += kThreads) tm[m] = ((u64)A.epoch << 32) | g.k;
     }
     // the state vv rows (lanes on consecutive columns of a row), then the
     // merged rows max(state, delta) from the docs' sparse delta vv entries
@@ -436,6 +451,8 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_e
         A.vvn[g] = dseq(x);
       }
     }
+    JY_CLK(c2);
+    JY_PROBE(1, 0, t, c0, c1, c2);
     return;
   }
   // delta items: strictly ascending dots per doc, col < R, seq >= 1; vv
@@ -499,17 +516,18 @@ __global__ __launch_bounds__(kItemThreads) void k_uj_flags(UjArgs A) {
   int kind;
   u64 lt, n, gbase;
   const u32* sid;
+  const u64* tm;
   if (t < tA) {
-    kind = 0, lt = t, n = ta, gbase = 0, sid = A.sidA;
+    kind = 0, lt = t, n = ta, gbase = 0, sid = A.sidA, tm = A.tmA;
   } else if (t < tA + tB) {
-    kind = 1, lt = t - tA, n = A.nb, gbase = ta, sid = A.sidB;
+    kind = 1, lt = t - tA, n = A.nb, gbase = ta, sid = A.sidB, tm = A.tmB;
   } else {
-    kind = 2, lt = t - tA - tB, n = A.cb, gbase = ta + A.nb, sid = A.sidD;
+    kind = 2, lt = t - tA - tB, n = A.cb, gbase = ta + A.nb, sid = A.sidD, tm = A.tmD;
   }
   const u64 i = lt * kTile + threadIdx.x;
   u64 f = 0;
   if (i < n) {
-    const u64 k = sid[i];
+    const u64 k = doc_at(A, tm, lt, sid, i);
     if (!is_bad(A, k)) {
       const u64 clo = A.cbs[k], chi = clo + (A.co[k + 1] - A.co[k]);
       u32 xr;
@@ -566,7 +584,7 @@ __global__ __launch_bounds__(kItemThreads) void k_uj_compact(UjArgs A) {
   const u64 i = lt * kTile + threadIdx.x;
   u64 f = 0;
   if (i < n) {
-    const u64 k = sa ? A.sidC[i] : A.sidD[i];
+    const u64 k = sa ? doc_at(A, A.tmC, lt, A.sidC, i) : doc_at(A, A.tmD, lt, A.sidD, i);
     if (!is_bad(A, k)) {
       const u64 alo = A.cbs[k], ahi = alo + (A.co[k + 1] - A.co[k]);
       const u64 blo = A.dcoff[k], bhi = A.dcoff[k + 1];
@@ -650,6 +668,15 @@ __global__ __launch_bounds__(kThreads) void k_uj_sizes(UjArgs A, u64 ndt) {
     const u64 tcl = pc + tot;
     A.neo[A.nd] = te;
     A.nco[A.nd] = tcl;
+    u64* st = A.stats;  // stream-ordered: one writer per converge
+    st[0] += A.ao[A.nd];
+    st[1] += A.co[A.nd];
+    st[2] += te;
+    st[3] += tcl;
+    st[4] += A.nb;
+    st[5] += A.cb;
+    st[6] += A.nd;
+    st[7] += 1;
     const u64 eb = A.ctr[0], cbb = A.ctr[1];
     A.base[0] = eb;
     A.base[1] = cbb;
@@ -696,7 +723,7 @@ __global__ __launch_bounds__(kItemThreads) void k_uj_scatter(UjArgs A) {
     if (i >= ta) return;
     const u64 si = sp.at(i);
     if (sp.at(i + 1) == si) return;
-    const u64 k = A.sidA[i];
+    const u64 k = doc_at(A, A.tmA, lt, A.sidA, i);
     const URec x = load_rec(A.rec + A.abase[k] + (i - A.ao[k]));
     const u32 xv = A.xr[i];
     const u64 lo = A.deoff[k], p = lo + (xv & 0x7FFFFFFFu);
@@ -706,7 +733,7 @@ __global__ __launch_bounds__(kItemThreads) void k_uj_scatter(UjArgs A) {
     if (i >= A.nb) return;
     const u64 si = sp.at(ta + i);
     if (sp.at(ta + i + 1) == si) return;
-    const u64 k = A.sidB[i];
+    const u64 k = doc_at(A, A.tmB, lt, A.sidB, i);
     const u64 pa = A.ao[k] + xrb[i];
     const u64 pos = A.neo[k] + (si - sp.at(ta + A.deoff[k])) + (sp.at(pa) - sp.at(A.ao[k]));
     store_rec(A.epool_out + eb0 + pos, A.ddots[i], A.delems[i]);
@@ -714,7 +741,7 @@ __global__ __launch_bounds__(kItemThreads) void k_uj_scatter(UjArgs A) {
     if (i >= tc) return;
     const u64 si = kp.at(i);
     if (kp.at(i + 1) == si) return;
-    const u64 k = A.sidC[i];
+    const u64 k = doc_at(A, A.tmC, lt, A.sidC, i);
     const u64 x = A.cloud[A.cbs[k] + (i - A.co[k])];
     const u64 lo = A.dcoff[k];
     const u64 pos = A.nco[k] + (si - kp.at(A.co[k])) + (kp.at(tc + lo + A.kr[i]) - kp.at(tc + lo));
@@ -723,7 +750,7 @@ __global__ __launch_bounds__(kItemThreads) void k_uj_scatter(UjArgs A) {
     if (i >= A.cb) return;
     const u64 si = kp.at(tc + i);
     if (kp.at(tc + i + 1) == si) return;
-    const u64 k = A.sidD[i];
+    const u64 k = doc_at(A, A.tmD, lt, A.sidD, i);
     const u64 pa = A.co[k] + krb[i];
     const u64 pos = A.nco[k] + (si - kp.at(tc + A.dcoff[k])) + (kp.at(pa) - kp.at(A.co[k]));
     A.cpool_out[cb0 + pos] = A.dcloud[i];
@@ -797,6 +824,7 @@ __global__ __launch_bounds__(kThreads) void k_uj_gather(const UMeta* __restrict_
   for (u32 c = 0; c < R; c++) ovv[i * R + c] = vv[s * R + c];
 }
 
+u64 cdiv_h(u64 a) { return (a + kTile - 1) / kTile; }
 u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kThreads - 1) / kThreads); }
 
 #define LAUNCH(k, n, ...)                                                                          \
@@ -944,6 +972,8 @@ int32_t jy_ujson_grow(jy_engine* eng, u64 need) {
     for (hipEvent_t& e : u.ready) JY_HIP(eng, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.tick), 64, "ujson tickets"));
     JY_HIP(eng, hipMemsetAsync(u.tick, 0, 64, eng->stream));
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.stats), 64, "ujson stats"));
+    JY_HIP(eng, hipMemsetAsync(u.stats, 0, 64, eng->stream));
     u.epcap = u.cpcap = std::max<u64>(eng->cfg.entry_capacity[JY_UJSON], 1024);
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.epool), u.epcap * sizeof(URec), "ujson element pool"));
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.cpool), u.cpcap * 8, "ujson cloud pool"));
@@ -992,6 +1022,7 @@ int32_t jy_ujson_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* deoff
     for (int i = 0; i < 6; i++)
       if (u.st[i].p)
         JY_HIP(eng, hipMemsetAsync(u.st[i].p, 0, u.st[i].bytes, eng->stream));
+    if (u.tmap.p) JY_HIP(eng, hipMemsetAsync(u.tmap.p, 0, u.tmap.bytes, eng->stream));
   }
   // persistent per-delta-doc state: bad marks and the dense delta vv (zero)
   if (nd > u.dcap) {
@@ -1071,6 +1102,15 @@ int32_t jy_ujson_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* deoff
   A.sidB = A.sidA + le + 1;
   A.sidC = A.sidB + nel + 1;
   A.sidD = A.sidC + lc + 1;
+  {
+    const u64 nA = cdiv_h(le) + 1, nB = cdiv_h(nel) + 1, nC = cdiv_h(lc) + 1, nD = cdiv_h(ncloud) + 1;
+    JY_TRY(grow_zero(eng, &u.tmap.p, &u.tmap.bytes, (nA + nB + nC + nD) * 8));
+    A.tmA = static_cast<u64*>(u.tmap.p);
+    A.tmB = A.tmA + nA;
+    A.tmC = A.tmB + nB;
+    A.tmD = A.tmC + nC;
+  }
+  A.stats = u.stats;
   JY_TRY(jy_scratch(eng, 17, (tf + tk + 2) * 8, &p));
   A.tp = static_cast<u64*>(p);
   A.ktp = A.tp + tf + 1;
@@ -1115,6 +1155,18 @@ int32_t jy_ujson_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* deoff
   u.live_c += ncloud;
   JY_HIP(eng, hipEventRecord(u.ready[slot_r], eng->stream));
   u.seq++;
+  return JY_OK;
+}
+
+int32_t jy_ujson_stats(jy_engine* eng, u64* out8) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  UjsonState& u = eng->ujson;
+  if (!u.stats) {
+    std::memset(out8, 0, 64);
+    return JY_OK;
+  }
+  JY_HIP(eng, hipMemcpyAsync(out8, u.stats, 64, hipMemcpyDeviceToHost, eng->stream));
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));
   return JY_OK;
 }
 

@@ -352,6 +352,40 @@ class Engine:
         mem = _same_mem(ma, mb, mc, md, me, mf)
         self._check(self.lib.jy_tlog_converge(self.h, len(a), pa, pb, pc, len(d), pd, pe, pf, mem))
 
+    def tlog_write(self, ops, slot, ts=None, arg=None, pre=None, lr=None):
+        """RepoTLOG.ins / trimat / trim / clr commands (jy_tlog_write), in order"""
+        n = len(slot)
+        cols = []
+        for x, t in ((ops, np.uint8), (slot, np.uint32), (ts, np.uint64), (arg, np.uint64), (pre, np.uint64),
+                     (lr, np.uint64)):
+            cols.append(_arg(np.zeros(n, t) if x is None else x, t))
+        mem = _same_mem(*[m for (_, _, m) in cols])
+        (o, po, _), (s, ps, _), (a, pa, _), (b, pb, _), (c, pc, _), (d, pd, _) = cols
+        self._check(self.lib.jy_tlog_write(self.h, n, po, ps, pa, pb, pc, pd, mem))
+
+    def tlog_deltas_size(self):
+        n = C.c_uint64()
+        self._check(self.lib.jy_tlog_deltas_size(self.h, C.byref(n)))
+        return n.value
+
+    def tlog_flush(self):
+        """flush_deltas -> (slots, cutoffs, offs, ts, pre, lr) of every pending key"""
+        k, m = C.c_uint64(), C.c_uint64()
+        z = np.zeros(1, np.uint64)
+        self._check(self.lib.jy_tlog_flush(self.h, 0, 0, None, None, None, None, None, None, C.byref(k), C.byref(m),
+                                           HOST))
+        nk, ne = k.value, m.value
+        slots = np.zeros(max(nk, 1), np.uint32)
+        cut = np.zeros(max(nk, 1), np.uint64)
+        offs = np.zeros(nk + 1, np.uint64)
+        ts, pre, lr = (np.zeros(max(ne, 1), np.uint64) for _ in range(3))
+        if nk:
+            self._check(self.lib.jy_tlog_flush(self.h, nk, ne, slots.ctypes.data, cut.ctypes.data, offs.ctypes.data,
+                                               ts.ctypes.data, pre.ctypes.data, lr.ctypes.data, C.byref(k),
+                                               C.byref(m), HOST))
+        del z
+        return slots[:nk].copy(), cut[:nk].copy(), offs, ts[:ne].copy(), pre[:ne].copy(), lr[:ne].copy()
+
     def tlog_read(self, slots):
         """-> (cutoff[n], offs[n+1], ts, pre, lr) for host slots"""
         s = np.ascontiguousarray(slots, np.uint32)
@@ -376,6 +410,13 @@ class Engine:
         (s, ps, _), (eo, peo, _), (d, pd, _), (e, pe, _), (vo, pvo, _), (v, pv, _), (co, pco, _), (c, pc, _) = args
         self._check(self.lib.jy_ujson_converge(self.h, len(s), ps, peo, len(d), pd, pe, pvo, len(v), pv,
                                                pco, len(c), pc, mem))
+
+    def ujson_stats(self):
+        """cumulative converge counters (jy_ujson_stats): dict of touched / written / delta sizes"""
+        out = np.zeros(8, np.uint64)
+        self._check(self.lib.jy_ujson_stats(self.h, out.ctypes.data))
+        keys = ("touched_el", "touched_cloud", "out_el", "out_cloud", "delta_el", "delta_cloud", "delta_docs", "calls")
+        return {k: int(v) for k, v in zip(keys, out)}
 
     def ujson_read(self, slots):
         """-> (el_offs, dots, elems, vv[n][R], cloud_offs, cloud)"""

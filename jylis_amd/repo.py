@@ -310,6 +310,57 @@ class RepoTLOG(_GpuRepo):
         return t
 
 
+    # -- local writes + flush_deltas (jy_tlog_write / _flush) --
+    def write(self, cmds):
+        """a batch of TLOG write commands, applied in order (keys may repeat):
+        ("INS", key, value, ts) | ("TRIMAT", key, ts) | ("TRIM", key, count) |
+        ("CLR", key)  -- repo_tlog.pony:85-111"""
+        if not cmds:
+            return
+        codes = {"INS": E._lib.TLOG_INS, "TRIMAT": E._lib.TLOG_TRIMAT, "TRIM": E._lib.TLOG_TRIM,
+                 "CLR": E._lib.TLOG_CLR}
+        kb, ko = E.encode_keys([c[1] for c in cmds])
+        slots = self._intern({"key_bytes": kb, "key_offs": ko})
+        n = len(cmds)
+        ops = np.array([codes[c[0]] for c in cmds], np.uint8)
+        ts = np.zeros(n, np.uint64)
+        arg = np.zeros(n, np.uint64)
+        vals = [b""] * n
+        for i, c in enumerate(cmds):
+            if c[0] == "INS":
+                vals[i] = c[2]
+                ts[i] = c[3]
+            elif c[0] == "TRIMAT":
+                ts[i] = c[2]
+            elif c[0] == "TRIM":
+                arg[i] = c[2]
+        pre, lr = self.eng.pack_values(TLOG, vals)
+        self.eng.tlog_write(ops, slots, ts, arg, pre, lr)
+
+    def ins(self, keys, values, ts):
+        self.write([("INS", k, v, int(t)) for k, v, t in zip(keys, values, ts)])
+
+    def trimat(self, keys, ts):
+        self.write([("TRIMAT", k, int(t)) for k, t in zip(keys, ts)])
+
+    def trim(self, keys, counts):
+        self.write([("TRIM", k, int(c)) for k, c in zip(keys, counts)])
+
+    def clr(self, keys):
+        self.write([("CLR", k) for k in keys])
+
+    def deltas_size(self):
+        return self.eng.tlog_deltas_size()
+
+    def flush_deltas(self):
+        """flush_deltas (repo_tlog.pony:21-25) -> oracle-format batch table"""
+        slots, cut, offs, ts, pre, lr = self.eng.tlog_flush()
+        t = self._keys_table(slots)
+        vb, vo = E.encode_keys([self.eng.value_bytes(TLOG, p, l) for p, l in zip(pre, lr)])
+        t.update({"cutoff": cut, "ent_offs": offs, "ts": ts, "val_bytes": vb, "val_offs": vo})
+        return t
+
+
 def _seg_ids(offs):
     offs = np.asarray(offs, np.int64)
     return np.repeat(np.arange(len(offs) - 1), np.diff(offs))
