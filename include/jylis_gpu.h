@@ -233,6 +233,30 @@ int32_t jy_ujson_read(jy_engine* eng, uint64_t n, const uint32_t* slots, const u
                       uint64_t* dots_out, uint64_t* elems_out, uint64_t* vv_out,
                       const uint64_t* cloud_offs, uint64_t* cloud_out);
 
+/* ---- UJSON write path: RepoUJSON.ins / rm / clr (repo_ujson.pony:74-110) ----
+ * Elements are opaque handles (the host interns (path, value) leaves; path-
+ * scoped CLR and SET are host compositions of RM / INS).  n commands applied
+ * in order: JY_UJSON_INS elem[i] under a fresh dot of replica column col
+ * (seq = the doc's vv[col] + 1); JY_UJSON_RM removes every element equal to
+ * elem[i] (observed remove); JY_UJSON_CLR removes every element of the doc.
+ * Each command's delta is converged into the state and into the doc's pending
+ * delta; every command marks its doc pending (issue RM / CLR only for docs
+ * that exist: repo_ujson.pony:86,108 create nothing).  Host batches may repeat
+ * docs (applied in order); a device batch holds one command per doc. */
+#define JY_UJSON_INS 0
+#define JY_UJSON_RM 1
+#define JY_UJSON_CLR 2
+int32_t jy_ujson_write(jy_engine* eng, uint64_t n, const uint8_t* op, const uint32_t* slot, const uint64_t* elem,
+                       uint32_t col, int32_t mem);
+int32_t jy_ujson_deltas_size(jy_engine* eng, uint64_t* n_out);  /* deltas_size(); blocks */
+/* flush_deltas() (repo_ujson.pony:22-26): every pending doc, ascending slot,
+ * with its delta document (elements CSR, dense vv [ndocs][ujson_columns],
+ * cloud CSR), then clears them.  Caps too small: sizes only (JY_OK). */
+int32_t jy_ujson_flush(jy_engine* eng, uint64_t cap_docs, uint64_t cap_el, uint64_t cap_cloud, uint32_t* slot_out,
+                       uint64_t* el_offs_out, uint64_t* dots_out, uint64_t* elems_out, uint64_t* vv_out,
+                       uint64_t* cloud_offs_out, uint64_t* cloud_out, uint64_t* ndocs_out, uint64_t* nel_out,
+                       uint64_t* ncloud_out, int32_t mem);
+
 /* cumulative converge counters since the engine was made (synchronising):
  * [0] touched state elements, [1] touched state cloud dots, [2] elements
  * written, [3] cloud dots written, [4] delta elements, [5] delta cloud dots,

@@ -17,6 +17,7 @@ TYPE_NAMES = {"GCOUNT": GCOUNT, "PNCOUNT": PNCOUNT, "TREG": TREG, "TLOG": TLOG, 
 HOST, DEVICE = 0, 1
 CFG_TREG_WHOLE_LINES = 1
 TLOG_INS, TLOG_TRIMAT, TLOG_TRIM, TLOG_CLR = 0, 1, 2, 3
+UJSON_INS, UJSON_RM, UJSON_CLR = 0, 1, 2
 
 
 class JyConfig(C.Structure):
@@ -83,6 +84,9 @@ SIGNATURES = {
     "jy_ujson_read": (I32, [P, U64, P, P, P, P, P, P, P]),
     "jy_ujson_stats": (I32, [P, P]),
     "jy_tlog_write": (I32, [P, U64, P, P, P, P, P, P, I32]),
+    "jy_ujson_write": (I32, [P, U64, P, P, P, U32, I32]),
+    "jy_ujson_deltas_size": (I32, [P, P]),
+    "jy_ujson_flush": (I32, [P, U64, U64, U64, P, P, P, P, P, P, P, P, P, P, I32]),
     "jy_tlog_deltas_size": (I32, [P, P]),
     "jy_tlog_flush": (I32, [P, U64, U64, P, P, P, P, P, P, P, P, I32]),
     "jy_keys_owner": (None, [U64, P, P, U32, P]),

@@ -305,6 +305,88 @@ int32_t jy_ujson_converge(jy_engine* eng, uint64_t n, const uint32_t* slot, cons
                         (const u64*)dv, nvv, (const u64*)dvv, (const u64*)dc, ncloud, (const u64*)dcl);
 }
 
+int32_t jy_ujson_write(jy_engine* eng, uint64_t n, const uint8_t* op, const uint32_t* slot, const uint64_t* elem,
+                       uint32_t col, int32_t mem) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (n == 0) return JY_OK;
+  if (n >= 0xFFFFFFFFull) return eng->fail(JY_ERANGE, "more than 2^32 - 1 commands in one call");
+  JY_TRY(jy_slots_check(eng, JY_UJSON, n, slot, mem));
+  if (mem != JY_HOST) return jy_ujson_write_batch(eng, n, op, slot, elem, col);
+  for (u64 i = 0; i < n; i++)
+    if (op[i] > JY_UJSON_CLR) return eng->fail(JY_EINVAL, "unknown UJSON write op");
+  std::vector<u32> occ;
+  const u32 rounds = rounds_of(n, slot, occ);
+  for (u32 r = 0; r < rounds; r++) {
+    std::vector<uint8_t> o;
+    std::vector<u32> s;
+    std::vector<u64> e;
+    for (u64 i = 0; i < n; i++)
+      if (rounds == 1 || occ[i] == r) {
+        o.push_back(op[i]);
+        s.push_back(slot[i]);
+        e.push_back(elem ? elem[i] : 0);
+      }
+    const u64 m = s.size();
+    const void *dop, *ds, *de;
+    JY_TRY(jy_stage_begin(eng));
+    JY_TRY(jy_stage(eng, 0, o.data(), m, JY_HOST, &dop));
+    JY_TRY(jy_stage(eng, 1, s.data(), m * 4, JY_HOST, &ds));
+    JY_TRY(jy_stage(eng, 2, e.data(), m * 8, JY_HOST, &de));
+    JY_TRY(jy_stage_end(eng));
+    JY_TRY(jy_ujson_write_batch(eng, m, (const uint8_t*)dop, (const u32*)ds, (const u64*)de, col));
+  }
+  return JY_OK;
+}
+
+int32_t jy_ujson_deltas_size(jy_engine* eng, uint64_t* n_out) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  return jy_ujson_pending(eng, n_out);
+}
+
+int32_t jy_ujson_flush(jy_engine* eng, uint64_t cap_docs, uint64_t cap_el, uint64_t cap_cl, uint32_t* slot_out,
+                       uint64_t* eoff_out, uint64_t* dots_out, uint64_t* elems_out, uint64_t* vv_out,
+                       uint64_t* coff_out, uint64_t* cloud_out, uint64_t* ndocs_out, uint64_t* nel_out,
+                       uint64_t* ncl_out, int32_t mem) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  u64 k = 0, me = 0, mc = 0;
+  JY_TRY(jy_ujson_flush_dev(eng, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, &k, &me,
+                            &mc));
+  *ndocs_out = k;
+  *nel_out = me;
+  *ncl_out = mc;
+  if (k == 0 || cap_docs < k || cap_el < me || cap_cl < mc) return JY_OK;
+  const u64 R = eng->ujson.R;
+  u32* ds = slot_out;
+  u64 *deo = eoff_out, *dd = dots_out, *de = elems_out, *dv = vv_out, *dco = coff_out, *dc = cloud_out;
+  if (mem == JY_HOST) {
+    void* p;
+    JY_TRY(jy_scratch(eng, 0, k * 4 + 64, &p));
+    ds = static_cast<u32*>(p);
+    JY_TRY(jy_scratch(eng, 1, (k + 1) * 8 * 2 + 64, &p));
+    deo = static_cast<u64*>(p);
+    dco = deo + (k + 1);
+    JY_TRY(jy_scratch(eng, 2, (2 * me + mc + k * R) * 8 + 64, &p));
+    dd = static_cast<u64*>(p);
+    de = dd + me;
+    dc = de + me;
+    dv = dc + mc;
+  }
+  JY_TRY(jy_ujson_flush_dev(eng, k, me, mc, ds, deo, dd, de, dv, dco, dc, &k, &me, &mc));
+  if (mem == JY_HOST) {
+    JY_HIP(eng, hipMemcpyAsync(slot_out, ds, k * 4, hipMemcpyDeviceToHost, eng->stream));
+    JY_HIP(eng, hipMemcpyAsync(eoff_out, deo, (k + 1) * 8, hipMemcpyDeviceToHost, eng->stream));
+    JY_HIP(eng, hipMemcpyAsync(coff_out, dco, (k + 1) * 8, hipMemcpyDeviceToHost, eng->stream));
+    if (me) {
+      JY_HIP(eng, hipMemcpyAsync(dots_out, dd, me * 8, hipMemcpyDeviceToHost, eng->stream));
+      JY_HIP(eng, hipMemcpyAsync(elems_out, de, me * 8, hipMemcpyDeviceToHost, eng->stream));
+    }
+    if (mc) JY_HIP(eng, hipMemcpyAsync(cloud_out, dc, mc * 8, hipMemcpyDeviceToHost, eng->stream));
+    JY_HIP(eng, hipMemcpyAsync(vv_out, dv, k * R * 8, hipMemcpyDeviceToHost, eng->stream));
+  }
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  return JY_OK;
+}
+
 int32_t jy_ujson_read_sizes(jy_engine* eng, uint64_t n, const uint32_t* slots, uint64_t* ne, uint64_t* nc) {
   JY_HIP(eng, hipSetDevice(eng->device));
   if (n == 0) return JY_OK;

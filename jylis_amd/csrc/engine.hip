@@ -290,25 +290,29 @@ void jy_engine_destroy(jy_engine* eng) {
   F(eng->tl_dflag);
   F(eng->tl_dcount);
   for (auto& k : eng->kdir) jy_keydir_free(eng, k);
-  F(eng->ujson.vv);
-  F(eng->ujson.meta);
-  F(eng->ujson.epool);
-  F(eng->ujson.cpool);
-  F(eng->ujson.spare_e);
-  F(eng->ujson.spare_c);
-  F(eng->ujson.ctr);
-  F(eng->ujson.dptr);
-  F(eng->ujson.bad);
-  F(eng->ujson.vvd);
-  F(eng->ujson.tick);
-  for (auto& a : eng->ujson.st) F(a.p);
-  F(eng->ujson.tmap.p);
+  for (UjsonState* u : {&eng->ujson, &eng->ujson_d}) {
+    F(u->vv);
+    F(u->meta);
+    F(u->epool);
+    F(u->cpool);
+    F(u->spare_e);
+    F(u->spare_c);
+    F(u->ctr);
+    F(u->dptr);
+    F(u->bad);
+    F(u->vvd);
+    F(u->tick);
+    for (auto& a : u->st) F(a.p);
+    F(u->tmap.p);
+    F(u->stats);
+    if (u->pin) hipHostFree(u->pin);
+    for (hipEvent_t e : u->ready)
+      if (e) hipEventDestroy(e);
+  }
+  F(eng->uj_dflag);
+  F(eng->uj_dcount);
   F(eng->dscan_st.p);
   F(eng->dscan_tick);
-  F(eng->ujson.stats);
-  if (eng->ujson.pin) hipHostFree(eng->ujson.pin);
-  for (hipEvent_t e : eng->ujson.ready)
-    if (e) hipEventDestroy(e);
   for (auto& a : eng->arena) F(a.p);
   for (auto& s : eng->scratch) F(s.p);
   if (eng->stream) hipStreamSynchronize(eng->stream);

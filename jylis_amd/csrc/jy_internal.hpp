@@ -340,6 +340,12 @@ struct jy_engine {
   // second store of the same layout; tl_dflag marks the keys _delta_for
   // touched since the last flush
   TlogState tlog_d;
+  // UJSON write path: pending delta documents (repo_ujson.pony _deltas), a
+  // second store of the same layout; uj_dflag marks the docs _delta_for touched
+  UjsonState ujson_d;
+  u32* uj_dflag = nullptr;
+  u64 uj_dkcap = 0;
+  u64* uj_dcount = nullptr;
   u32* tl_dflag = nullptr;
   u64 tl_dkcap = 0;
   u64* tl_dcount = nullptr;
@@ -511,6 +517,19 @@ int32_t jy_ujson_gather(jy_engine* eng, u64 n, const u32* slots, const u64* oeof
 int32_t jy_ujson_merge(jy_engine* eng, u64 ndocs, const u32* slot, const u64* eoffs, u64 nel, const u64* dots,
                        const u64* elems, const u64* vvoffs, u64 nvv, const u64* vv, const u64* coffs, u64 ncloud,
                        const u64* cloud);
+struct UjsonState;
+int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* slot, const u64* deoff, u64 nel,
+                            const u64* ddots, const u64* delems, const u64* dvoff, u64 nvv, const u64* dvv,
+                            const u64* dcoff, u64 ncloud, const u64* dcloud, bool keep_all = false);
+int32_t jy_ujson_sizes_of(jy_engine* eng, const UjsonState& u, u64 n, const u32* slots, u64* ne, u64* nc);
+int32_t jy_ujson_gather_of(jy_engine* eng, const UjsonState& u, u64 n, const u32* slots, const u64* oeoff,
+                           const u64* ocoff, u64* odots, u64* oelems, u64* ovv, u64* ocloud);
+int32_t ujson_grow_store(jy_engine* eng, UjsonState& u, u64 need, u64 init_cap);
+// UJSON write path (k_uj_write.hip): one command per doc (device arrays)
+int32_t jy_ujson_write_batch(jy_engine* eng, u64 n, const uint8_t* op, const u32* slot, const u64* elem, u32 col);
+int32_t jy_ujson_pending(jy_engine* eng, u64* count);
+int32_t jy_ujson_flush_dev(jy_engine* eng, u64 cap_docs, u64 cap_el, u64 cap_cl, u32* slots, u64* eoff, u64* dots,
+                           u64* elems, u64* vv, u64* coff, u64* cloud, u64* ndocs, u64* nel, u64* ncl);
 
 // device exclusive scan of n u64 counts into out[0..n] (out[n] = total)
 int32_t jy_scan_u64(jy_engine* eng, const u64* in, u64* out, u64 n);

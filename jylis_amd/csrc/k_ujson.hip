@@ -132,6 +132,7 @@ struct UjArgs {
   u64* pin;          // mapped pinned: [2..3] bump pointers after this converge
   u32 R;
   u32 epoch;
+  u32 keep_all;      // context-only join: every state element stays (the write path's pending deltas)
   u64* dptr;         // [kcap] epoch << 32 | first delta doc of the slot
   u32* bad;          // [nd] == epoch: skipped
   unsigned long long* skipped;
@@ -540,7 +541,8 @@ __global__ __launch_bounds__(kItemThreads) void k_uj_flags(UjArgs A) {
           f = 1;
           if (!in_state_ctx(A, k, d)) xr |= 1u << 31;
         } else {
-          f = !(dseq(d) <= A.vvd[k * A.R + dcol(d)] || contains(A.dcloud, A.dcoff[k], A.dcoff[k + 1], d));
+          f = A.keep_all ||
+              !(dseq(d) <= A.vvd[k * A.R + dcol(d)] || contains(A.dcloud, A.dcoff[k], A.dcoff[k + 1], d));
         }
       } else if (kind == 1) {
         const u64 d = A.ddots[i];
@@ -848,8 +850,7 @@ __global__ void k_uj_cmp_ctr(const u64* __restrict__ te, const u64* __restrict__
 // then swap.  Asynchronous: the exact compacted sizes reach the host through
 // the converge ring like a converge's bump pointers (the spare pools are
 // reallocated -- a synchronising hipMalloc -- only when they are too small).
-int32_t ujson_compact(jy_engine* eng, u64 room_e, u64 room_c) {
-  UjsonState& u = eng->ujson;
+int32_t ujson_compact(jy_engine* eng, UjsonState& u, u64 room_e, u64 room_c) {
   const u64 nk = eng->nkeys[JY_UJSON];
   if (u.seq - u.done == UjsonState::kRing) {  // its ring slot
     JY_HIP(eng, hipEventSynchronize(u.ready[u.done % UjsonState::kRing]));
@@ -923,8 +924,7 @@ void ujson_absorb(UjsonState& u) {
     }
   }
 }
-int32_t ujson_plan(jy_engine* eng, u64 nel, u64 ncloud) {
-  UjsonState& u = eng->ujson;
+int32_t ujson_plan(jy_engine* eng, UjsonState& u, u64 nel, u64 ncloud) {
   ujson_absorb(u);
   if (u.seq - u.done == UjsonState::kRing) {  // the ring slot is still in use: wait for its converge
     JY_HIP(eng, hipEventSynchronize(u.ready[u.done % UjsonState::kRing]));
@@ -944,7 +944,7 @@ int32_t ujson_plan(jy_engine* eng, u64 nel, u64 ncloud) {
       JY_HIP(eng, hipEventSynchronize(u.ready[(u.seq - 1) % UjsonState::kRing]));
       ujson_absorb(u);
     }
-    if (!fits()) JY_TRY(ujson_compact(eng, we, wc));
+    if (!fits()) JY_TRY(ujson_compact(eng, u, we, wc));
   }
   return JY_OK;
 }
@@ -960,8 +960,7 @@ int32_t grow_zero(jy_engine* eng, void** p, u64* cap_bytes, u64 need_bytes) {
 
 }  // namespace
 
-int32_t jy_ujson_grow(jy_engine* eng, u64 need) {
-  UjsonState& u = eng->ujson;
+int32_t ujson_grow_store(jy_engine* eng, UjsonState& u, u64 need, u64 init_cap) {
   if (u.R == 0) u.R = eng->cfg.ujson_columns;
   if (!u.ctr) {
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.ctr), 64, "ujson counters"));
@@ -974,7 +973,7 @@ int32_t jy_ujson_grow(jy_engine* eng, u64 need) {
     JY_HIP(eng, hipMemsetAsync(u.tick, 0, 64, eng->stream));
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.stats), 64, "ujson stats"));
     JY_HIP(eng, hipMemsetAsync(u.stats, 0, 64, eng->stream));
-    u.epcap = u.cpcap = std::max<u64>(eng->cfg.entry_capacity[JY_UJSON], 1024);
+    u.epcap = u.cpcap = std::max<u64>(init_cap, 1024);
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.epool), u.epcap * sizeof(URec), "ujson element pool"));
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.cpool), u.cpcap * 8, "ujson cloud pool"));
   }
@@ -994,6 +993,12 @@ int32_t jy_ujson_grow(jy_engine* eng, u64 need) {
   return JY_OK;
 }
 
+int32_t jy_ujson_grow(jy_engine* eng, u64 need) {
+  JY_TRY(ujson_grow_store(eng, eng->ujson, need, eng->cfg.entry_capacity[JY_UJSON]));
+  if (eng->ujson_d.ctr) JY_TRY(ujson_grow_store(eng, eng->ujson_d, eng->ujson.kcap, 0));
+  return JY_OK;
+}
+
 // new documents are empty: their meta is zeroed when it is allocated
 int32_t jy_ujson_extend(jy_engine*, u64, u64) { return JY_OK; }
 
@@ -1001,13 +1006,20 @@ int32_t jy_ujson_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* deoff
                        const u64* delems, const u64* dvoff, u64 nvv, const u64* dvv, const u64* dcoff, u64 ncloud,
                        const u64* dcloud) {
   JyTimed tm(eng);
-  UjsonState& u = eng->ujson;
+  return jy_ujson_merge_into(eng, eng->ujson, nd, slot, deoff, nel, ddots, delems, dvoff, nvv, dvv, dcoff, ncloud,
+                             dcloud);
+}
+
+// the converge into one store: the state, or the pending deltas of the write path
+int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* slot, const u64* deoff, u64 nel,
+                            const u64* ddots, const u64* delems, const u64* dvoff, u64 nvv, const u64* dvv,
+                            const u64* dcoff, u64 ncloud, const u64* dcloud, bool keep_all) {
   const u64 nk = eng->nkeys[JY_UJSON];
   if (nd == 0 || nk == 0) return JY_OK;
   if (nd >= 0xFFFFFFFFull) return eng->fail(JY_ERANGE, "ujson converge: more than 2^32 - 1 documents in one call");
   const u32 R = u.R;
   const u64 live_e = u.live_e, live_c = u.live_c;  // bounds of the touched state, before this converge
-  JY_TRY(ujson_plan(eng, nel, ncloud));
+  JY_TRY(ujson_plan(eng, u, nel, ncloud));
   const u64 le = std::min(u.live_e, live_e), lc = std::min(u.live_c, live_c);  // (a compaction makes them exact)
   if (le + nel + ncloud + 2 >= (1ull << 32) || lc + ncloud + 2 >= (1ull << 32))
     return eng->fail(JY_ERANGE, "ujson converge: more than 2^32 touched items");
@@ -1058,6 +1070,7 @@ int32_t jy_ujson_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* deoff
   A.pin = u.pin_dev + 8 + 2 * slot_r;
   A.R = R;
   A.epoch = u.epoch;
+  A.keep_all = keep_all;
   A.dptr = u.dptr;
   A.bad = u.bad;
   A.skipped = reinterpret_cast<unsigned long long*>(eng->skipped_dev);
@@ -1171,14 +1184,19 @@ int32_t jy_ujson_stats(jy_engine* eng, u64* out8) {
 }
 
 int32_t jy_ujson_sizes(jy_engine* eng, u64 n, const u32* slots, u64* ne, u64* nc) {
-  UjsonState& u = eng->ujson;
+  return jy_ujson_sizes_of(eng, eng->ujson, n, slots, ne, nc);
+}
+int32_t jy_ujson_sizes_of(jy_engine* eng, const UjsonState& u, u64 n, const u32* slots, u64* ne, u64* nc) {
   LAUNCH(k_uj_sizes_read, n, u.meta, slots, n, ne, nc);
   return JY_OK;
 }
 
 int32_t jy_ujson_gather(jy_engine* eng, u64 n, const u32* slots, const u64* oeoff, const u64* ocoff, u64* odots,
                         u64* oelems, u64* ovv, u64* ocloud) {
-  UjsonState& u = eng->ujson;
+  return jy_ujson_gather_of(eng, eng->ujson, n, slots, oeoff, ocoff, odots, oelems, ovv, ocloud);
+}
+int32_t jy_ujson_gather_of(jy_engine* eng, const UjsonState& u, u64 n, const u32* slots, const u64* oeoff,
+                           const u64* ocoff, u64* odots, u64* oelems, u64* ovv, u64* ocloud) {
   LAUNCH(k_uj_gather, n, u.meta, u.epool, u.cpool, u.vv, u.R, slots, n, oeoff, ocoff, odots, oelems, ovv, ocloud);
   return JY_OK;
 }

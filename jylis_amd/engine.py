@@ -411,6 +411,38 @@ class Engine:
         self._check(self.lib.jy_ujson_converge(self.h, len(s), ps, peo, len(d), pd, pe, pvo, len(v), pv,
                                                pco, len(c), pc, mem))
 
+    def ujson_write(self, ops, slot, elem, col):
+        """RepoUJSON.ins / rm / clr on opaque element handles (jy_ujson_write), in order"""
+        n = len(slot)
+        o, po, mo = _arg(ops, np.uint8)
+        s, ps, ms = _arg(slot, np.uint32)
+        e, pe, me = _arg(np.zeros(n, np.uint64) if elem is None else elem, np.uint64)
+        self._check(self.lib.jy_ujson_write(self.h, n, po, ps, pe, int(col), _same_mem(mo, ms, me)))
+
+    def ujson_deltas_size(self):
+        n = C.c_uint64()
+        self._check(self.lib.jy_ujson_deltas_size(self.h, C.byref(n)))
+        return n.value
+
+    def ujson_flush(self):
+        """flush_deltas -> (slots, el_offs, dots, elems, vv[n][R], cloud_offs, cloud) of every pending doc"""
+        k, me, mc = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        self._check(self.lib.jy_ujson_flush(self.h, 0, 0, 0, None, None, None, None, None, None, None,
+                                            C.byref(k), C.byref(me), C.byref(mc), HOST))
+        nk, ne, nc = k.value, me.value, mc.value
+        R = self.ujson_columns
+        slots = np.zeros(max(nk, 1), np.uint32)
+        eo = np.zeros(nk + 1, np.uint64)
+        co = np.zeros(nk + 1, np.uint64)
+        dots, elems = np.zeros(max(ne, 1), np.uint64), np.zeros(max(ne, 1), np.uint64)
+        cloud = np.zeros(max(nc, 1), np.uint64)
+        vv = np.zeros((max(nk, 1), R), np.uint64)
+        if nk:
+            self._check(self.lib.jy_ujson_flush(self.h, nk, ne, nc, slots.ctypes.data, eo.ctypes.data,
+                                                dots.ctypes.data, elems.ctypes.data, vv.ctypes.data, co.ctypes.data,
+                                                cloud.ctypes.data, C.byref(k), C.byref(me), C.byref(mc), HOST))
+        return slots[:nk].copy(), eo, dots[:ne].copy(), elems[:ne].copy(), vv[:nk].copy(), co, cloud[:nc].copy()
+
     def ujson_stats(self):
         """cumulative converge counters (jy_ujson_stats): dict of touched / written / delta sizes"""
         out = np.zeros(8, np.uint64)

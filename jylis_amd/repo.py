@@ -396,6 +396,38 @@ class RepoUJSON(_GpuRepo):
         (cloud,) = self._sort_segments(co, self._pack(batch["cloud_ids"], batch["cloud_seqs"]))
         self.eng.ujson_converge(slots, eo, dots, elems, vo, vv, co, cloud)
 
+    # -- local writes on opaque elements + flush_deltas (jy_ujson_write / _flush) --
+    def write(self, cmds, identity):
+        """("INS", key, elem) | ("RM", key, elem) | ("CLR", key), applied in order;
+        RM / CLR of a key that does not exist do nothing (repo_ujson.pony:86,108)"""
+        codes = {"INS": E._lib.UJSON_INS, "RM": E._lib.UJSON_RM, "CLR": E._lib.UJSON_CLR}
+        live = []
+        for c in cmds:
+            if c[0] == "INS":
+                live.append(c)
+            else:
+                s = int(self.slots_of([c[1]])[0])
+                if s != E._lib.JY_NO_SLOT:
+                    live.append(c)
+                elif any(d[0] == "INS" and d[1] == c[1] for d in live):
+                    live.append(c)  # created earlier in this batch
+        if not live:
+            return
+        kb, ko = E.encode_keys([c[1] for c in live])
+        slots = self._intern({"key_bytes": kb, "key_offs": ko})
+        ops = np.array([codes[c[0]] for c in live], np.uint8)
+        elems = np.array([c[2] if c[0] != "CLR" else 0 for c in live], np.uint64)
+        col = int(self.eng.replica_cols([identity])[0])
+        self.eng.ujson_write(ops, slots, elems, col)
+
+    def deltas_size(self):
+        return self.eng.ujson_deltas_size()
+
+    def flush_deltas(self):
+        """flush_deltas (repo_ujson.pony:22-26) -> oracle-format batch table"""
+        slots, eo, dots, elems, vv, co, cloud = self.eng.ujson_flush()
+        return self._docs_table(slots, eo, dots, elems, vv, co, cloud)
+
     def elements(self, key):
         """the observable element set of a doc (what GET renders, repo_ujson.pony:68-72)"""
         s = int(self.slots_of([key])[0])
@@ -405,12 +437,18 @@ class RepoUJSON(_GpuRepo):
 
     def state(self):
         slots = self._sorted_slots()
+        if len(slots) == 0:
+            return self._docs_table(slots, None, None, None, None, None, None)
+        eo, dots, elems, vv, co, cloud = self.eng.ujson_read(slots)
+        return self._docs_table(slots, eo, dots, elems, vv, co, cloud)
+
+    def _docs_table(self, slots, eo, dots, elems, vv, co, cloud):
+        """device doc rows -> oracle-format table (replica ids, sorted segments)"""
         t = self._keys_table(slots)
         n = len(slots)
         out = {k: [] for k in ("dot_ids", "dot_seqs", "elems", "vv_ids", "vv_seqs", "cloud_ids", "cloud_seqs")}
         eoffs, voffs, coffs = [0], [0], [0]
         if n:
-            eo, dots, elems, vv, co, cloud = self.eng.ujson_read(slots)
             R = vv.shape[1]
             ids = np.array([self.eng.replica_id(c) for c in range(self.eng.replica_count())] or [0], np.uint64)
             for i in range(n):
