@@ -398,25 +398,29 @@ class RepoUJSON(_GpuRepo):
 
     # -- local writes on opaque elements + flush_deltas (jy_ujson_write / _flush) --
     def write(self, cmds, identity):
-        """("INS", key, elem) | ("RM", key, elem) | ("CLR", key), applied in order;
-        RM / CLR of a key that does not exist do nothing (repo_ujson.pony:86,108)"""
-        codes = {"INS": E._lib.UJSON_INS, "RM": E._lib.UJSON_RM, "CLR": E._lib.UJSON_CLR}
+        """("INS", key, elem) | ("RM", key, elem) | ("CLR", key) | ("TOUCH", key),
+        applied in order; RM / CLR of a key that does not exist do nothing
+        (repo_ujson.pony:86,108); TOUCH creates the key and its delta and
+        changes nothing (SET of an empty node, a path-scoped CLR that matches
+        nothing): an RM of handle 0, which no element holds"""
+        codes = {"INS": E._lib.UJSON_INS, "RM": E._lib.UJSON_RM, "CLR": E._lib.UJSON_CLR,
+                 "TOUCH": E._lib.UJSON_RM}
         live = []
         for c in cmds:
-            if c[0] == "INS":
+            if c[0] in ("INS", "TOUCH"):
                 live.append(c)
             else:
                 s = int(self.slots_of([c[1]])[0])
                 if s != E._lib.JY_NO_SLOT:
                     live.append(c)
-                elif any(d[0] == "INS" and d[1] == c[1] for d in live):
+                elif any(d[0] in ("INS", "TOUCH") and d[1] == c[1] for d in live):
                     live.append(c)  # created earlier in this batch
         if not live:
             return
         kb, ko = E.encode_keys([c[1] for c in live])
         slots = self._intern({"key_bytes": kb, "key_offs": ko})
         ops = np.array([codes[c[0]] for c in live], np.uint8)
-        elems = np.array([c[2] if c[0] != "CLR" else 0 for c in live], np.uint64)
+        elems = np.array([c[2] if c[0] in ("INS", "RM") else 0 for c in live], np.uint64)
         col = int(self.eng.replica_cols([identity])[0])
         self.eng.ujson_write(ops, slots, elems, col)
 

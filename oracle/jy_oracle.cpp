@@ -890,5 +890,13 @@ void or_ujson_clr(void* rp, const char* k, u64 n) {  // repo_ujson.pony:85-88 (n
   auto it = r->uj.find(K(k, n));
   if (it != r->uj.end()) it->second.clear(r->uj_d[it->first]);
 }
+// _data_for(key) + _delta_for(key) with no change: SET of an empty node
+// (repo_ujson.pony:80-81), a path-scoped CLR that matches nothing (:86)
+void or_ujson_touch(void* rp, const char* k, u64 n) {
+  Repo* r = static_cast<Repo*>(rp);
+  std::string key = K(k, n);
+  r->uj[key];
+  r->uj_d[key];
+}
 
 }  // extern "C"

@@ -61,6 +61,7 @@ def load():
         "or_ujson_ins": (None, [P, C.c_char_p, U64, U64]),
         "or_ujson_rm": (None, [P, C.c_char_p, U64, U64]),
         "or_ujson_clr": (None, [P, C.c_char_p, U64]),
+        "or_ujson_touch": (None, [P, C.c_char_p, U64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -225,6 +226,10 @@ class Repo:
     def ujson_clr(self, k):
         k = _b(k)
         self.lib.or_ujson_clr(self.h, k, len(k))
+
+    def ujson_touch(self, k):
+        k = _b(k)
+        self.lib.or_ujson_touch(self.h, k, len(k))
 
 
 def split_keys(table):
