@@ -12,7 +12,8 @@ handles; this module owns the mapping.
   INS key [path...] value   add the leaf (path, value)
   RM  key [path...] value   remove the leaf (path, value) (no key creation)
 
-Handles are a 64-bit hash of the canonical (path, value) encoding, so every
+Handles are a 64-bit hash (FNV-1a) of the canonical (path, value) encoding
+(each path segment length-prefixed, then 0xFFFFFFFF, then the value), so every
 replica derives the same handle for the same leaf (the CRDT compares elements
 by handle); `LeafTable` keeps handle -> leaf for rendering and refuses a hash
 collision.  Rendering follows the primer: maps render as objects, several
@@ -21,7 +22,6 @@ merged map inside a set, nothing for empty collections.  Set and map order is
 not specified by the reference (pony Map iteration); this module renders keys
 and set members in sorted order, and tests compare renders canonically
 (`canonical`)."""
-import hashlib
 import json
 
 import numpy as np
@@ -63,6 +63,13 @@ def flatten(text, prefix=()):
     return out
 
 
+def _fnv1a64(b):
+    h = 0xCBF29CE484222325
+    for x in b:
+        h = ((h ^ x) * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
 def _encode(path, value):
     b = bytearray()
     for p in path:
@@ -80,8 +87,9 @@ class LeafTable:
 
     def handle(self, path, value):
         path = tuple(path)
+        # FNV-1a 64 of the encoding (the Pony glue computes the same handle);
         # handle 0 is reserved: "no element" (the engine's key-touching RM)
-        h = int.from_bytes(hashlib.blake2b(_encode(path, value), digest_size=8).digest(), "little") or 1
+        h = _fnv1a64(_encode(path, value)) or 1
         old = self._leaf.setdefault(h, (path, value))
         if old != (path, value):
             raise RuntimeError(f"64-bit leaf handle collision: {old} vs {(path, value)}")

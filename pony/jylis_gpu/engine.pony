@@ -1,0 +1,109 @@
+"""
+The engine handle and the marshalling every GPU repo shares (package jylis).
+UNBUILT here (no ponyc); see INTEGRATION.md.
+
+A GPU repo holds `(_Engine | None)`: `RepoAny.create` (repo_manager.pony:6)
+is not partial, so a missing GPU is reported per call (`_Fail`), not at
+construction.
+"""
+use "collections"
+use "resp"
+
+class _Engine
+  """One engine per Database and type (one GPU, one key shard); owned by the
+  RepoManager actor that owns the repo, so calls are never concurrent."""
+  let ptr: Pointer[None] tag
+  let _names: Array[String] = _names.create()    // slot -> key (slots are dense)
+  let _col: U32                                   // this replica's column
+
+  new create(identity: U64, device: I32 = 0) ? =>
+    let cfg = JyConfig
+    @jy_config_default(cfg)
+    cfg.device = device
+    var p = Pointer[None]
+    if @jy_engine_create(cfg, addressof p) != 0 then error end
+    ptr = p
+    var c: U32 = 0
+    if @jy_replica_col(ptr, identity, addressof c) != 0 then error end
+    _col = c
+
+  fun col(): U32 => _col
+
+  fun check(rc: I32) ? => if rc != 0 then error end
+
+  fun ref intern(ty: I32, keys: Array[String] box): Array[U32] ? =>
+    """slots of `keys`, creating missing ones (Repo._data_for)"""
+    let m = _Strs(keys)
+    let slots = Array[U32].init(0, keys.size())
+    check(@jy_keys_intern(ptr, ty, keys.size().u64(), m.bytes.cpointer(), m.offs.cpointer(),
+      slots.cpointer()))?
+    for (i, s) in slots.pairs() do
+      while _names.size() <= s.usize() do _names.push("") end
+      _names(s.usize())? = keys(i)?
+    end
+    slots
+
+  fun lookup(ty: I32, key: String): U32 =>
+    """slot of `key`, or JyNoSlot (Repo._data(key)? failing)"""
+    let m = _Strs([key])
+    var s: U32 = JyNoSlot()
+    @jy_keys_lookup(ptr, ty, 1, m.bytes.cpointer(), m.offs.cpointer(), addressof s)
+    s
+
+  fun name(slot: U32): String => try _names(slot.usize())? else "" end
+
+  fun replica(col': U32): U64 =>
+    var id: U64 = 0
+    @jy_replica_id(ptr, col', addressof id)
+    id
+
+  fun ref replica_col(id: U64): U16 ? =>
+    var c: U32 = 0
+    check(@jy_replica_col(ptr, id, addressof c))?
+    c.u16()
+
+  fun ref pack(ty: I32, values: Array[String] box): (Array[U64], Array[U64]) ? =>
+    """value strings -> (pre, lr) handles (long values into the arena)"""
+    let m = _Strs(values)
+    let pre = Array[U64].init(0, values.size())
+    let lr = Array[U64].init(0, values.size())
+    check(@jy_values_pack(ptr, ty, values.size().u64(), m.bytes.cpointer(), m.offs.cpointer(),
+      pre.cpointer(), lr.cpointer()))?
+    (pre, lr)
+
+  fun unpack(ty: I32, pre: U64, lr: U64): String =>
+    """(pre, lr) -> the value string: <= 8 bytes live in pre (big-endian),
+    longer ones in the arena at lr >> 24"""
+    let len = (lr and 0xFFFFFF).usize()
+    let out = recover String(len) end
+    if len <= 8 then
+      var i: USize = 0
+      while i < len do
+        out.push(((pre >> (56 - (8 * i.u64()))) and 0xFF).u8())
+        i = i + 1
+      end
+    else
+      let buf = Array[U8].init(0, len)
+      @jy_arena_read(ptr, ty, lr >> 24, len.u64(), buf.cpointer())
+      for b in buf.values() do out.push(b) end
+    end
+    consume out
+
+  fun _final() => @jy_engine_destroy(ptr)
+
+class _Strs
+  """strings marshalled as bytes + offsets (the C-ABI's key / value columns)"""
+  let bytes: Array[U8] = bytes.create()
+  let offs: Array[U64] = offs.create()
+
+  new create(strs: Array[String] box) =>
+    offs.push(0)
+    for k in strs.values() do
+      bytes.append(k)
+      offs.push(bytes.size().u64())
+    end
+
+primitive _Fail
+  fun apply(resp: Respond): Bool =>
+    resp.err("GPU engine unavailable")
+    false

@@ -1,0 +1,285 @@
+"""
+GPU-backed RepoTREG / RepoTLOG: drop-in replacements for jylis/repo_treg.pony
+and jylis/repo_tlog.pony behind RepoAny (jylis/repo_manager.pony:5-10).
+UNBUILT here (no ponyc); INTEGRATION.md.
+
+converge queues the pair and the next entry point merges the whole queue in
+one engine call (see repo_counters_gpu.pony).  Writes and flush_deltas run on
+the engine (jy_treg_set / _flush, jy_tlog_write / _flush); flush rebuilds the
+pony-crdt deltas from the engine's pending registers / logs.  Values travel
+as (pre, lr) handles (jy_values_pack); reads turn them back into Strings.
+"""
+use "collections"
+use "crdt"
+use "resp"
+
+class RepoTREGGpu
+  let _eng: (_Engine | None)
+  embed _in: Array[(String, Any box)] = _in.create()
+
+  new create(identity': U64) =>
+    _eng = try _Engine(identity')? else None end
+
+  fun ref deltas_size(): USize =>
+    match _eng
+    | let e: _Engine =>
+      var n: U64 = 0
+      @jy_treg_deltas_size(e.ptr, addressof n)
+      n.usize()
+    else 0
+    end
+
+  fun ref flush_deltas(): Array[(String, Any box)] box =>
+    """repo_treg.pony:18-22: every pending key with its delta register"""
+    let out = Array[(String, Any box)]
+    match _eng
+    | let e: _Engine =>
+      try
+        var n: U64 = 0
+        e.check(@jy_treg_deltas_size(e.ptr, addressof n))?
+        let cap = n.usize().max(1)
+        let slots = Array[U32].init(0, cap)
+        let ts = Array[U64].init(0, cap)
+        let pre = Array[U64].init(0, cap)
+        let lr = Array[U64].init(0, cap)
+        var got: U64 = 0
+        e.check(@jy_treg_flush(e.ptr, cap.u64(), slots.cpointer(), ts.cpointer(), pre.cpointer(),
+          lr.cpointer(), addressof got, JyHost()))?
+        for i in Range(0, got.usize()) do
+          let d = TRegString
+          d.update(e.unpack(JyTREG(), pre(i)?, lr(i)?), ts(i)?)
+          out.push((e.name(slots(i)?), d))
+        end
+      end
+    end
+    out
+
+  fun ref converge(key: String, delta': Any box) =>
+    _in.push((key, delta'))
+
+  fun ref _drain() =>
+    if _in.size() == 0 then return end
+    match _eng
+    | let e: _Engine =>
+      try
+        let keys = Array[String]
+        let vals = Array[String]
+        let ts = Array[U64]
+        for (k, d') in _in.values() do
+          match d'
+          | let d: TRegString box => keys.push(k); vals.push(d.value()); ts.push(d.timestamp())
+          end
+        end
+        if keys.size() > 0 then
+          let slots = e.intern(JyTREG(), keys)?
+          (let pre, let lr) = e.pack(JyTREG(), vals)?
+          e.check(@jy_treg_converge(e.ptr, slots.size().u64(), slots.cpointer(), ts.cpointer(),
+            pre.cpointer(), lr.cpointer(), JyHost()))?
+        end
+      end
+    end
+    _in.clear()
+
+  fun ref apply(r: Respond, cmd: Iterator[String]): Bool? =>
+    match cmd.next()?
+    | "GET" => get(r, cmd.next()?)
+    | "SET" => set(r, cmd.next()?, cmd.next()?, cmd.next()?.u64()?)
+    else error
+    end
+
+  fun ref get(resp: Respond, key: String): Bool =>
+    """repo_treg.pony:54-63: [value, timestamp], or null for a missing key"""
+    _drain()
+    match _eng
+    | let e: _Engine =>
+      var slot = e.lookup(JyTREG(), key)
+      if slot == JyNoSlot() then resp.null(); return false end
+      var ts: U64 = 0
+      var pre: U64 = 0
+      var lr: U64 = 0
+      @jy_treg_read(e.ptr, 1, addressof slot, addressof ts, addressof pre, addressof lr)
+      resp.array_start(2)
+      resp.string(e.unpack(JyTREG(), pre, lr))
+      resp.u64(ts)
+      false
+    else _Fail(resp)
+    end
+
+  fun ref set(resp: Respond, key: String, value: String, timestamp: U64): Bool =>
+    """repo_treg.pony:65-68"""
+    _drain()
+    match _eng
+    | let e: _Engine =>
+      try
+        let slots = e.intern(JyTREG(), [key])?
+        (let pre, let lr) = e.pack(JyTREG(), [value])?
+        var ts = timestamp
+        e.check(@jy_treg_set(e.ptr, 1, slots.cpointer(), addressof ts, pre.cpointer(), lr.cpointer(),
+          JyHost()))?
+        resp.ok()
+        true
+      else _Fail(resp)
+      end
+    else _Fail(resp)
+    end
+
+primitive _TlogOp
+  fun ins(): U8 => 0
+  fun trimat(): U8 => 1
+  fun trim(): U8 => 2
+  fun clr(): U8 => 3
+
+class RepoTLOGGpu
+  let _eng: (_Engine | None)
+  embed _in: Array[(String, Any box)] = _in.create()
+
+  new create(identity': U64) =>
+    _eng = try _Engine(identity')? else None end
+
+  fun ref deltas_size(): USize =>
+    match _eng
+    | let e: _Engine =>
+      var n: U64 = 0
+      @jy_tlog_deltas_size(e.ptr, addressof n)
+      n.usize()
+    else 0
+    end
+
+  fun ref flush_deltas(): Array[(String, Any box)] box =>
+    """repo_tlog.pony:21-25: every pending key with its delta log"""
+    let out = Array[(String, Any box)]
+    match _eng
+    | let e: _Engine =>
+      try
+        var nk: U64 = 0
+        var ne: U64 = 0
+        e.check(@jy_tlog_flush(e.ptr, 0, 0, Pointer[U32], Pointer[U64], Pointer[U64], Pointer[U64],
+          Pointer[U64], Pointer[U64], addressof nk, addressof ne, JyHost()))?
+        if nk == 0 then return out end
+        let slots = Array[U32].init(0, nk.usize())
+        let cut = Array[U64].init(0, nk.usize())
+        let offs = Array[U64].init(0, nk.usize() + 1)
+        let ts = Array[U64].init(0, ne.usize().max(1))
+        let pre = Array[U64].init(0, ne.usize().max(1))
+        let lr = Array[U64].init(0, ne.usize().max(1))
+        e.check(@jy_tlog_flush(e.ptr, nk, ne, slots.cpointer(), cut.cpointer(), offs.cpointer(),
+          ts.cpointer(), pre.cpointer(), lr.cpointer(), addressof nk, addressof ne, JyHost()))?
+        for i in Range(0, nk.usize()) do
+          let d = TLog[String]
+          d.raise_cutoff(cut(i)?)
+          for j in Range(offs(i)?.usize(), offs(i + 1)?.usize()) do
+            d.write(e.unpack(JyTLOG(), pre(j)?, lr(j)?), ts(j)?)
+          end
+          out.push((e.name(slots(i)?), d))
+        end
+      end
+    end
+    out
+
+  fun ref converge(key: String, delta': Any box) =>
+    _in.push((key, delta'))
+
+  fun ref _drain() =>
+    """every queued TLog delta in one jy_tlog_converge (CSR of entries)"""
+    if _in.size() == 0 then return end
+    match _eng
+    | let e: _Engine =>
+      try
+        let keys = Array[String]
+        let cut = Array[U64]
+        let offs: Array[U64] = [0]
+        let vals = Array[String]
+        let ts = Array[U64]
+        for (k, d') in _in.values() do
+          match d'
+          | let d: TLog[String] box =>
+            keys.push(k)
+            cut.push(d.cutoff())
+            for (v, t) in d.entries() do vals.push(v); ts.push(t) end   // newest first
+            offs.push(vals.size().u64())
+          end
+        end
+        if keys.size() > 0 then
+          let slots = e.intern(JyTLOG(), keys)?
+          (let pre, let lr) = e.pack(JyTLOG(), vals)?
+          e.check(@jy_tlog_converge(e.ptr, slots.size().u64(), slots.cpointer(), cut.cpointer(),
+            offs.cpointer(), vals.size().u64(), ts.cpointer(), pre.cpointer(), lr.cpointer(), JyHost()))?
+        end
+      end
+    end
+    _in.clear()
+
+  fun ref apply(r: Respond, cmd: Iterator[String]): Bool? =>
+    match cmd.next()?
+    | "GET"    => get(r, cmd.next()?, try cmd.next()?.usize()? else USize.max_value() end)
+    | "INS"    =>
+      let k = cmd.next()?
+      let v = cmd.next()?
+      write(r, k, _TlogOp.ins(), v, cmd.next()?.u64()?, 0)?
+    | "SIZE"   => size(r, cmd.next()?, false)
+    | "CUTOFF" => size(r, cmd.next()?, true)
+    | "TRIMAT" => write(r, cmd.next()?, _TlogOp.trimat(), "", cmd.next()?.u64()?, 0)?
+    | "TRIM"   => write(r, cmd.next()?, _TlogOp.trim(), "", 0, cmd.next()?.u64()?)?
+    | "CLR"    => write(r, cmd.next()?, _TlogOp.clr(), "", 0, 0)?
+    else error
+    end
+
+  fun ref write(resp: Respond, key: String, op: U8, value: String, ts': U64, count: U64): Bool ? =>
+    """INS key value ts / TRIMAT key ts / TRIM key count / CLR key
+    (repo_tlog.pony:85-111): one jy_tlog_write command"""
+    var ts = ts'
+    _drain()
+    match _eng
+    | let e: _Engine =>
+      let slots = e.intern(JyTLOG(), [key])?
+      (let pre, let lr) = e.pack(JyTLOG(), [value])?
+      var o = op
+      var c = count
+      e.check(@jy_tlog_write(e.ptr, 1, addressof o, slots.cpointer(), addressof ts, addressof c,
+        pre.cpointer(), lr.cpointer(), JyHost()))?
+      resp.ok()
+      true
+    else _Fail(resp)
+    end
+
+  fun ref get(resp: Respond, key: String, count: USize): Bool =>
+    """repo_tlog.pony:69-83: at most `count` entries, newest first"""
+    _drain()
+    match _eng
+    | let e: _Engine =>
+      var slot = e.lookup(JyTLOG(), key)
+      if slot == JyNoSlot() then resp.array_start(0); return false end
+      var len: U64 = 0
+      var cut: U64 = 0
+      @jy_tlog_read_sizes(e.ptr, 1, addressof slot, addressof len, addressof cut)
+      let offs: Array[U64] = [0; len]
+      let ts = Array[U64].init(0, len.usize().max(1))
+      let pre = Array[U64].init(0, len.usize().max(1))
+      let lr = Array[U64].init(0, len.usize().max(1))
+      @jy_tlog_read(e.ptr, 1, addressof slot, offs.cpointer(), ts.cpointer(), pre.cpointer(), lr.cpointer())
+      let total = len.usize().min(count)
+      resp.array_start(total)
+      for i in Range(0, total) do
+        resp.array_start(2)
+        resp.string(try e.unpack(JyTLOG(), pre(i)?, lr(i)?) else "" end)
+        resp.u64(try ts(i)? else 0 end)
+      end
+      false
+    else _Fail(resp)
+    end
+
+  fun ref size(resp: Respond, key: String, cutoff: Bool): Bool =>
+    """SIZE / CUTOFF (repo_tlog.pony:90-96): 0 for a missing key"""
+    _drain()
+    match _eng
+    | let e: _Engine =>
+      var slot = e.lookup(JyTLOG(), key)
+      var len: U64 = 0
+      var cut: U64 = 0
+      if slot != JyNoSlot() then
+        @jy_tlog_read_sizes(e.ptr, 1, addressof slot, addressof len, addressof cut)
+      end
+      resp.u64(if cutoff then cut else len end)
+      false
+    else _Fail(resp)
+    end
