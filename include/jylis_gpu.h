@@ -108,9 +108,20 @@ uint32_t jy_key_owner(const uint8_t* key, uint64_t len, uint32_t nshards);
 /* ---- string arena of TREG / TLOG values (value bytes beyond the 8-byte prefix) ----
  * A value is held as (prefix u64 = first 8 bytes big-endian, zero padded;
  * lr u64 = arena_offset << 24 | length).  Values of <= 8 bytes never touch
- * the arena.  jy_values_pack appends long values and fills pre/lr. */
+ * the arena.  jy_values_pack appends long values (each on an 8-byte
+ * boundary) and fills pre/lr. */
 int32_t jy_values_pack(jy_engine* eng, int32_t type, uint64_t n, const uint8_t* bytes,
                        const uint64_t* offs, uint64_t* pre_out, uint64_t* lr_out);
+
+/* arena bytes in use / reserved (host counters, no GPU work) */
+int32_t jy_arena_usage(jy_engine* eng, int32_t type, uint64_t* len_out, uint64_t* cap_out);
+/* Reclaim the arena (TREG, TLOG): copy the values every live register, log
+ * entry and pending delta still references back to back into a fresh arena
+ * and rewrite their handles; *live_out = the bytes kept.  Handles packed by
+ * jy_values_pack but not yet merged become INVALID: call between converge /
+ * write calls (the reference frees a replaced value, repo_treg.pony:51-52).
+ * Blocks. */
+int32_t jy_arena_collect(jy_engine* eng, int32_t type, uint64_t* live_out);
 
 /* ---- GCOUNT: GCounter.converge (repo_gcount.pony:50-51) / value (:53-55) ----
  * COO form: n cells (slot, col, value): s[slot][col] = max(s, value). */

@@ -83,6 +83,8 @@ SIGNATURES = {
     "jy_ujson_read_sizes": (I32, [P, U64, P, P, P]),
     "jy_ujson_read": (I32, [P, U64, P, P, P, P, P, P, P]),
     "jy_ujson_stats": (I32, [P, P]),
+    "jy_arena_usage": (I32, [P, I32, P, P]),
+    "jy_arena_collect": (I32, [P, I32, P]),
     "jy_tlog_write": (I32, [P, U64, P, P, P, P, P, P, I32]),
     "jy_ujson_write": (I32, [P, U64, P, P, P, U32, I32]),
     "jy_ujson_deltas_size": (I32, [P, P]),

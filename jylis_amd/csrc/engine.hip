@@ -528,11 +528,13 @@ int32_t jy_values_pack(jy_engine* eng, int32_t type, uint64_t n, const uint8_t* 
   JY_TRY(check_type(eng, type));
   JY_HIP(eng, hipSetDevice(eng->device));
   Arena& a = eng->arena[type];
-  u64 add = 0;
+  // long values start on kArenaAlign granules (jy_arena_collect relies on it)
+  const u64 base = round_up(a.len, kArenaAlign);
+  u64 add = base - a.len;
   for (u64 i = 0; i < n; i++) {
     u64 len = offs[i + 1] - offs[i];
     if (len > JY_MAX_VALUE_LEN) return eng->fail(JY_ERANGE, "value longer than 16 MiB");
-    if (len > 8) add += len;
+    if (len > 8) add += round_up(len, kArenaAlign);
   }
   if (a.len + add > a.cap) {
     u64 nc = std::max<u64>(std::max<u64>(a.cap * 2, a.len + add), 1 << 16);
@@ -542,9 +544,9 @@ int32_t jy_values_pack(jy_engine* eng, int32_t type, uint64_t n, const uint8_t* 
     a.cap = nc;
   }
   if ((a.len + add) >> (64 - JY_LR_LEN_BITS)) return eng->fail(JY_ERANGE, "arena offset overflow");
-  std::vector<uint8_t> tail;
+  std::vector<uint8_t> tail(base - a.len, 0);
   tail.reserve(add);
-  u64 at = a.len;
+  u64 at = base;
   for (u64 i = 0; i < n; i++) {
     const uint8_t* v = bytes + offs[i];
     u64 len = offs[i + 1] - offs[i];
@@ -554,7 +556,8 @@ int32_t jy_values_pack(jy_engine* eng, int32_t type, uint64_t n, const uint8_t* 
     if (len > 8) {
       lr[i] = (at << JY_LR_LEN_BITS) | len;
       tail.insert(tail.end(), v, v + len);
-      at += len;
+      tail.resize(tail.size() + (round_up(len, kArenaAlign) - len), 0);
+      at += round_up(len, kArenaAlign);
     } else {
       lr[i] = len;
     }

@@ -448,6 +448,9 @@ inline double jy_now_us() {
 
 // engine.hip helpers used by the kernel translation units
 int32_t jy_scratch(jy_engine* eng, int idx, u64 bytes, void** out);
+int32_t jy_treg_fold(jy_engine* eng);
+// long values start on 8-byte granules (an arena collection maps granules)
+constexpr u64 kArenaAlign = 8;
 // look-back status words for `ntiles` tiles, the ticket counter and a fresh epoch
 int32_t jy_dscan_ctx(jy_engine* eng, u64 ntiles, u64** status, u32** tick, u32* epoch);
 // copy a borrowed input into device memory if it is on the host; returns a

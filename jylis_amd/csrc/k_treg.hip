@@ -386,6 +386,9 @@ int32_t claim_begin(jy_engine* eng, u64 n, u32 nblocks, TregK& K) {
 
 }  // namespace
 
+// pending duplicates folded in (before an arena collection moves values)
+int32_t jy_treg_fold(jy_engine* eng) { return fold_now(eng); }
+
 int32_t jy_treg_grow(jy_engine* eng, u64 need) {
   TregState& t = eng->treg;
   if (need <= t.kcap && t.ts) return JY_OK;

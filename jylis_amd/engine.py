@@ -196,6 +196,17 @@ class Engine:
                                             pre.ctypes.data, lr.ctypes.data))
         return pre, lr
 
+    def arena_usage(self, ctype):
+        n, c = C.c_uint64(), C.c_uint64()
+        self._check(self.lib.jy_arena_usage(self.h, ctype, C.byref(n), C.byref(c)))
+        return n.value, c.value
+
+    def arena_collect(self, ctype):
+        """reclaim dead value bytes (jy_arena_collect); unmerged packed handles become invalid"""
+        live = C.c_uint64()
+        self._check(self.lib.jy_arena_collect(self.h, ctype, C.byref(live)))
+        return live.value
+
     def arena_read(self, ctype, off, n):
         buf = np.empty(max(n, 1), np.uint8)
         self._check(self.lib.jy_arena_read(self.h, ctype, off, n, buf.ctypes.data))

@@ -214,7 +214,18 @@ def _counter_table(eng, ctype, slots, prefix, sign):
             prefix + "vals": np.concatenate(vals) if vals else np.zeros(0, np.uint64)}
 
 
-class RepoTREG(_GpuRepo):
+class _ArenaGC:
+    """collect the value arena when dead bytes outnumber live ones (after a
+    call that consumed every handle it packed)"""
+    _arena_live = 0
+
+    def _maybe_collect(self):
+        n, _ = self.eng.arena_usage(self.ctype)
+        if n > 2 * self._arena_live + (1 << 20):
+            self._arena_live = self.eng.arena_collect(self.ctype)
+
+
+class RepoTREG(_ArenaGC, _GpuRepo):
     """repo_treg.pony: TRegString per key, LWW by (timestamp, value)."""
     ctype = TREG
 
@@ -226,6 +237,7 @@ class RepoTREG(_GpuRepo):
             return
         pre, lr = self.eng.pack_values(TREG, (batch["val_bytes"], batch["val_offs"]))
         self.eng.treg_converge(slots, np.asarray(batch["ts"], np.uint64), pre, lr)
+        self._maybe_collect()
 
     def get(self, key):
         """TREG GET (repo_treg.pony:54-63): (value, ts), or None if never touched"""
@@ -251,6 +263,7 @@ class RepoTREG(_GpuRepo):
         slots = self._intern({"key_bytes": kb, "key_offs": ko})
         pre, lr = self.eng.pack_values(TREG, list(values))
         self.eng.treg_set(slots, np.asarray(ts, np.uint64), pre, lr)
+        self._maybe_collect()
 
     def deltas_size(self):
         return self.eng.treg_deltas_size()
@@ -264,7 +277,7 @@ class RepoTREG(_GpuRepo):
         return t
 
 
-class RepoTLOG(_GpuRepo):
+class RepoTLOG(_ArenaGC, _GpuRepo):
     """repo_tlog.pony: TLog[String] per key (sorted log with grow-only cutoff)."""
     ctype = TLOG
 
@@ -277,6 +290,7 @@ class RepoTLOG(_GpuRepo):
         pre, lr = self.eng.pack_values(TLOG, (batch["val_bytes"], batch["val_offs"]))
         self.eng.tlog_converge(slots, np.asarray(batch["cutoff"], np.uint64), np.asarray(batch["ent_offs"], np.uint64),
                                np.asarray(batch["ts"], np.uint64), pre, lr)
+        self._maybe_collect()
 
     def get(self, key, count=None):
         """TLOG GET key [count] (repo_tlog.pony:69-83): [(value, ts)], newest first"""
@@ -336,6 +350,7 @@ class RepoTLOG(_GpuRepo):
                 arg[i] = c[2]
         pre, lr = self.eng.pack_values(TLOG, vals)
         self.eng.tlog_write(ops, slots, ts, arg, pre, lr)
+        self._maybe_collect()
 
     def ins(self, keys, values, ts):
         self.write([("INS", k, v, int(t)) for k, v, t in zip(keys, values, ts)])
