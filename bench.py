@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--cpu-keys-per-thread", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=None, help="per-launch HBM bytes from a PMC run (json)")
-    ap.add_argument("--type", default="pncount", choices=["pncount", "gcount", "treg", "tlog", "ujson"],
+    ap.add_argument("--type", default="pncount", choices=["pncount", "gcount", "treg", "tlog", "ujson", "e2e", "read"],
                     help="pncount = the BASELINE metric line; the others measure SURVEY 8d configs 1,3,4,5")
     ap.add_argument("--route", action="store_true", help="treg: run the routing exchange even on 1 GPU")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -80,7 +80,8 @@ def other_mode(args, rank, world, local, dist):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = bench_modes.cpu_baseline(args.type)
     if rank == 0:
-        line = {"metric": f"{args.type.upper()} delta converge throughput (SURVEY 8d)", "value": res.pop("value"),
+        line = {"metric": res.pop("metric", f"{args.type.upper()} delta converge throughput (SURVEY 8d)"),
+                "value": res.pop("value"),
                 "unit": res.pop("unit_of_work") + "s/s", "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": res.pop("ms_per_step"), "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic (jylis_amd/synth.py)",

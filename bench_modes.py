@@ -459,4 +459,124 @@ def bench_ujson(args, eng, dev, dist, rank, world):
                                        "written, 24R B context per delta doc; untouched documents are not read"}}
 
 
-MODES = {"gcount": bench_gcount, "treg": bench_treg, "tlog": bench_tlog, "ujson": bench_ujson}
+# ---- end-to-end ingest: the ABI path the Pony glue calls (host batches) -----------
+
+def bench_e2e(args, eng, dev, dist, rank, world):
+    """One step = what RepoGCOUNTGpu._drain does with one decoded peer batch:
+    B key strings from host memory interned on the GPU (jy_keys_intern, the
+    reference's per-key _data_for probe, repo_gcount.pony:36-41), then the
+    (slot, replica column, value) cells merged from host memory through the
+    pinned staging ring (jy_gcount_converge COO, JY_HOST).  Wall-clock per
+    step, host included; the merge kernel is priced on its own too."""
+    import torch
+    from jylis_amd import synth as S
+    K, R = args.keys or (1 << 24), 16
+    B = 1 << 20
+    seed = S.BASE_SEED + 11
+    kb, ko = S.counter_keys(K, prefix=f"s{rank}:e".encode(), width=8)
+    eng.reserve(0, K + K // 8)
+    t0 = time.perf_counter()
+    eng.intern(0, (kb, ko))
+    setup_intern_s = time.perf_counter() - t0
+    cols = eng.replica_cols(S.replica_ids(R, seed).tolist())
+    rng = np.random.default_rng(seed + rank)
+    nb = max(2, args.batches)
+    batches = []
+    L = int(ko[1] - ko[0])
+    for j in range(nb):
+        pick = rng.integers(0, K, B)
+        # 1 in 16 keys is new to this replica (interned on the fly)
+        new = rng.random(B) < 1 / 16
+        rows = kb.reshape(K, L)[pick].copy()
+        rows[new, 0] = ord("n")
+        bkb = np.ascontiguousarray(rows).reshape(-1)
+        bko = np.arange(B + 1, dtype=np.uint64) * np.uint64(L)
+        col = cols[rng.integers(0, R, B)].astype(np.uint16)
+        val = rng.integers(1, 1 << 62, B, dtype=np.uint64)
+        batches.append((bkb, bko, col, val))
+    times = {"intern": [], "converge": []}
+
+    def step(i):
+        bkb, bko, col, val = batches[i % nb]
+        a = time.perf_counter()
+        slots = eng.intern(0, (bkb, bko))
+        b = time.perf_counter()
+        eng.gcount_converge(slots, col, val)
+        c = time.perf_counter()
+        times["intern"].append(b - a)
+        times["converge"].append(c - b)
+
+    elapsed, kt = _timed(args.steps, args.warmup, step, dist, dev, eng=eng)
+    t = _max_over_ranks(elapsed, dist, dev)
+    k = float(np.mean(kt))
+    h2d = B * (L + 8 + 4 + 2 + 8)  # key bytes + offsets, slots, cols, values
+    tail = slice(args.warmup, None)
+    return {"metric": "GCOUNT end-to-end ingest throughput (host batches through the C-ABI)",
+            "workload": f"GCOUNT end-to-end ingest: {B} host cells per step (one decoded peer batch; "
+                        f"1/16 new keys) into {K} keys x {R} replicas: jy_keys_intern (host key strings) + "
+                        f"jy_gcount_converge COO from host memory (pinned staging)",
+            "unit_of_work": "cell ingested", "value": world * B * args.steps / t,
+            "ms_per_step": t / args.steps * 1e3,
+            "host_intern_ms": float(np.mean(times["intern"][tail])) * 1e3,
+            "host_converge_call_ms": float(np.mean(times["converge"][tail])) * 1e3,
+            "h2d_bytes_per_step": h2d, "h2d_GBps_effective": h2d / (t / args.steps) / 1e9,
+            "setup_intern_s": setup_intern_s,
+            "roofline": {"bound": "hbm", "achieved": 24 * B / k / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": 24 * B / k / 1e9 / HBM_PEAK_GBS, "kernel": "k_coo_max (merge only)",
+                         "kernel_ms_avg": k * 1e3, "bytes_per_unit": 24,
+                         "note": "random 8-B cells: each touches a whole 64-B line; the step is interning- "
+                                 "and PCIe-bound, the merge is a small part"}}
+
+
+# ---- batched read path at scale -------------------------------------------------
+
+def bench_read(args, eng, dev, dist, rank, world):
+    """PNCOUNT GET over every key of a 16M-key x 64-replica shard in one call
+    (jy_pncount_get, device slots -> device i64: the reference's
+    repo_pncount.pony:55-57 value() per key), plus the RESP-sized host
+    readback of the same answers."""
+    import torch
+    from jylis_amd import synth as S
+    K, R = args.keys or (1 << 24), 64
+    seed = S.BASE_SEED + 12
+    kb, ko = S.counter_keys(K, prefix=f"s{rank}:r".encode(), width=8)
+    eng.reserve(1, K)
+    eng.intern(1, (kb, ko))
+    cols = eng.replica_cols(S.replica_ids(R, seed).tolist())
+    st = torch.empty((2, R, K), dtype=torch.int64, device=dev)
+    S.counter_rows_torch(st, seed, wrap_frac=False)
+    eng.pncount_converge_block(cols, 0, st[0], st[1])
+    del st
+    slots = torch.arange(K, dtype=torch.int32, device=dev)
+    out = {}
+
+    def step(i):
+        out["v"] = eng.pncount_get(slots)
+
+    elapsed, kt = _timed(args.steps, args.warmup, step, dist, dev)
+    t = _max_over_ranks(elapsed, dist, dev)
+    k = float(np.mean(kt))
+    bytes_per_key = 2 * R * 8 + 4 + 8  # both slabs' columns + slot + answer
+    # verification: a sampled key's sum recomputed from an export of its columns
+    v = out["v"].cpu().numpy()
+    sample = np.random.default_rng(1).integers(0, K, 64)
+    ok = True
+    for s in sample.tolist():
+        ex = eng.counter_export(1, R, int(s), 1).reshape(2, R)
+        d = (sum(int(x) for x in ex[0]) - sum(int(x) for x in ex[1])) % (1 << 64)  # wrapping, as GCounter
+        ok = ok and int(v[s]) == (d - (1 << 64) if d >= 1 << 63 else d)
+    t1 = time.perf_counter()
+    host = out["v"].cpu().numpy()
+    d2h_s = time.perf_counter() - t1
+    return {"metric": "PNCOUNT GET throughput (batched read path, SURVEY 8f rank 4)",
+            "workload": f"PNCOUNT GET of every key: {K} keys x {R} replicas x {{P,N}} per GPU in one "
+                        f"jy_pncount_get (device slots -> device answers)",
+            "unit_of_work": "key read", "value": world * K * args.steps / t, "ms_per_step": t / args.steps * 1e3,
+            "verified_sampled_keys": bool(ok), "d2h_all_answers_ms": d2h_s * 1e3, "answers": int(len(host)),
+            "roofline": {"bound": "hbm", "achieved": bytes_per_key * K / k / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": bytes_per_key * K / k / 1e9 / HBM_PEAK_GBS,
+                         "kernel": "k_sum (pncount)", "kernel_ms_avg": k * 1e3, "bytes_per_unit": bytes_per_key}}
+
+
+MODES = {"gcount": bench_gcount, "treg": bench_treg, "tlog": bench_tlog, "ujson": bench_ujson, "e2e": bench_e2e,
+         "read": bench_read}
