@@ -163,6 +163,13 @@ def _to_dev(a, dev, dtype=None):
 
 # ---- GCOUNT (config 1: 1M keys x 16 replicas) --------------------------------
 
+def _u64max(a, b):
+    """elementwise max of int64 tensors holding u64 bit patterns"""
+    import torch
+    flip = torch.tensor(-(1 << 63), dtype=torch.int64, device=a.device)
+    return torch.maximum(a ^ flip, b ^ flip) ^ flip
+
+
 def bench_gcount(args, eng, dev, dist, rank, world):
     import torch
     from jylis_amd import synth as S
@@ -184,11 +191,19 @@ def bench_gcount(args, eng, dev, dist, rank, world):
     elapsed, kt = _timed(args.steps, args.warmup, lambda i: eng.gcount_converge_block(cols, 0, ds[i % nb][0]),
                          dist, dev, eng=eng)
     t = _max_over_ranks(elapsed, dist, dev)
+    # verification: sampled keys recomputed as the max over every batch applied
+    sample = torch.from_numpy(np.random.default_rng(5).integers(0, K, 64)).to(dev)
+    exp = st[0][:, sample].clone()
+    for i in range(args.warmup + args.steps):
+        exp = _u64max(exp, ds[i % nb][0][:, sample])
+    exp = exp.cpu().numpy().view(np.uint64)
+    verified = all(np.array_equal(eng.counter_export(0, R, int(k), 1).reshape(R), exp[:, j])
+                   for j, k in enumerate(sample.tolist()))
     cells = R * K
     k = float(np.mean(kt))
     return {"workload": f"GCOUNT converge: {K} keys x {R} replicas per GPU, one full delta batch "
                         f"({R} peer batches) per step (SURVEY 8d config 1)",
-            "unit_of_work": "cell merge", "units_per_step_per_gpu": cells,
+            "unit_of_work": "cell merge", "units_per_step_per_gpu": cells, "verified_sampled_keys": bool(verified),
             "value": world * cells * args.steps / t, "ms_per_step": t / args.steps * 1e3,
             "roofline": {"bound": "hbm", "achieved": 24 * cells / k / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": 24 * cells / k / 1e9 / HBM_PEAK_GBS, "kernel": "k_block_max<true>",
@@ -280,6 +295,23 @@ def bench_treg(args, eng, dev, dist, rank, world):
     t = _max_over_ranks(elapsed, dist, dev)
     k = float(np.mean(kt))
     wf = float(np.mean(win)) if win else 0.5
+    verified = None
+    if not routed:
+        # sampled keys: LWW over every applied batch, (ts, value) with the
+        # value order of Pony's String (bytewise, shorter first on a prefix)
+        idx = np.random.default_rng(6).integers(0, n, 128)
+        applied = [batches[0]] + [batches[1 + i % nb] for i in range(args.warmup + args.steps)]
+        best = {}
+        for b in applied:
+            ts_h = b[2][idx].cpu().numpy().view(np.uint64)
+            pre_h, lr_h = b[3][idx].cpu().numpy().view(np.uint64), b[4][idx].cpu().numpy().view(np.uint64)
+            for j in range(len(idx)):
+                cand = (int(ts_h[j]), eng.value_bytes(TREG, pre_h[j], lr_h[j]))
+                if j not in best or cand > best[j]:
+                    best[j] = cand
+        s_h = batches[0][1][idx].cpu().numpy().view(np.uint32)
+        gts, gpre, glr = eng.treg_read(s_h)
+        verified = all((int(gts[j]), eng.value_bytes(TREG, gpre[j], glr[j])) == best[j] for j in range(len(idx)))
     # SURVEY 8d prices a key LWW select at 48 B (16 delta + 16 state read +
     # 16 state write, the write counted unconditionally); what the kernel
     # actually moves in this layout is reported beside it
@@ -290,7 +322,7 @@ def bench_treg(args, eng, dev, dist, rank, world):
                        f"per step{' routed by owner (all-to-all)' if routed else ''} (SURVEY 8d config 3)",
            "unit_of_work": "key LWW select", "units_per_step_per_gpu": n,
            "value": world * n * args.steps / t, "ms_per_step": t / args.steps * 1e3, "setup_s": setup_s,
-           "winner_fraction": wf}
+           "winner_fraction": wf, "verified_sampled_keys": verified}
     if not routed:
         out["roofline"] = {"bound": "hbm", "achieved": bytes_per_key * n / k / 1e9, "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": bytes_per_key * n / k / 1e9 / HBM_PEAK_GBS,
@@ -371,13 +403,32 @@ def bench_tlog(args, eng, dev, dist, rank, world):
             ins.append(prev + nd)
         prev = now
     e2.close()
+    # verification: sampled logs recomputed from the applied tables
+    # (union of entries, largest cutoff, newest first, value order bytewise)
+    samp = np.random.default_rng(7).integers(0, K, 128)
+    applied = [st] + [dl[i % nb] for i in range(args.warmup + args.steps)]
+    want = {int(k): (0, set()) for k in samp}
+    for b in applied:
+        eo_, vo_ = np.asarray(b["ent_offs"], np.int64), np.asarray(b["val_offs"], np.int64)
+        for k in want:
+            cut, ents = want[k]
+            cut = max(cut, int(b["cutoff"][k]))
+            for j in range(eo_[k], eo_[k + 1]):
+                ents.add((int(b["ts"][j]), bytes(b["val_bytes"][vo_[j]:vo_[j + 1]])))
+            want[k] = (cut, ents)
+    cut_g, offs_g, ts_g, pre_g, lr_g = eng.tlog_read(np.array(list(want), np.uint32))
+    verified = True
+    for i, (k, (cut, ents)) in enumerate(want.items()):
+        exp = sorted((e for e in ents if e[0] >= cut), reverse=True)
+        got = [(int(ts_g[j]), eng.value_bytes(TLOG, pre_g[j], lr_g[j])) for j in range(offs_g[i], offs_g[i + 1])]
+        verified = verified and int(cut_g[i]) == cut and got == exp
     k = float(np.mean(kt))
     avg_b = float(np.mean(byts))
     units = float(np.mean(ins))
     return {"workload": f"TLOG converge: {K} logs, state ~Geom(8, cap 64) entries, delta ~Geom(2) per key "
                         f"per step, dups/ties/cutoffs (SURVEY 8d config 4); {n_state0} initial entries",
             "unit_of_work": "log entry (input)", "value": world * units * args.steps / t,
-            "ms_per_step": t / args.steps * 1e3,
+            "ms_per_step": t / args.steps * 1e3, "verified_sampled_keys": bool(verified),
             "roofline": {"bound": "hbm", "achieved": avg_b / k / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": avg_b / k / 1e9 / HBM_PEAK_GBS,
                          "kernel": "TLOG converge (k_tlog_*, all launches of one call)",
@@ -385,6 +436,7 @@ def bench_tlog(args, eng, dev, dist, rank, world):
                          "bytes_note": "SURVEY 8d: 16 B read per input entry (state + delta) + 16 B written per "
                                        "output entry + 24 B per key (a whole-state rewrite)",
                          "min_bytes_moved_per_converge": float(np.mean(moved)),
+                         "frac_moved": float(np.mean(moved)) / k / 1e9 / HBM_PEAK_GBS,
                          "min_bytes_moved_note": "append layout lower bound: 24 B per delta entry read + 32 B per "
                                                  "net new entry written + 64 B meta per delta key"}}
 
@@ -432,6 +484,7 @@ def bench_ujson(args, eng, dev, dist, rank, world):
     elapsed, kt = _timed(args.steps, args.warmup, step, dist, dev, eng=eng,
                          before_timed=lambda: marks.update(s0=eng.ujson_stats()))
     s1 = eng.ujson_stats()
+    verified = _verify_ujson(eng, repo, st, [dl[i % nb] for i in range(args.warmup + args.steps)], D)
     # what the timed converges really touched and wrote (the engine's own
     # counters: the hot documents grow step by step)
     d = {k: (s1[k] - marks["s0"][k]) / args.steps for k in s1}
@@ -448,7 +501,7 @@ def bench_ujson(args, eng, dev, dist, rank, world):
                         f"{int(d['touched_el'])} touched state elements), 70/20/10 INS/RM/CLR (SURVEY 8d config 5)",
             "unit_of_work": "dot examined", "value": world * dots_examined * args.steps / t,
             "ms_per_step": t / args.steps * 1e3, "generate_s": gen_s,
-            "delta_docs_per_s": world * d["delta_docs"] * args.steps / t,
+            "delta_docs_per_s": world * d["delta_docs"] * args.steps / t, "verified_sampled_docs": verified,
             "per_converge": d,
             "roofline": {"bound": "hbm", "achieved": bytes_conv / k / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": bytes_conv / k / 1e9 / HBM_PEAK_GBS,
@@ -576,6 +629,74 @@ def bench_read(args, eng, dev, dist, rank, world):
             "roofline": {"bound": "hbm", "achieved": bytes_per_key * K / k / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": bytes_per_key * K / k / 1e9 / HBM_PEAK_GBS,
                          "kernel": "k_sum (pncount)", "kernel_ms_avg": k * 1e3, "bytes_per_unit": bytes_per_key}}
+
+
+def _uj_doc(t, i):
+    """row i of a UJSON table -> ({(id, seq): elem}, {id: n}, {(id, seq)})"""
+    eo, vo, co = (np.asarray(t[k], np.int64) for k in ("el_offs", "vv_offs", "cloud_offs"))
+    m = {(int(t["dot_ids"][j]), int(t["dot_seqs"][j])): int(t["elems"][j]) for j in range(eo[i], eo[i + 1])}
+    vv = {int(t["vv_ids"][j]): int(t["vv_seqs"][j]) for j in range(vo[i], vo[i + 1])}
+    cl = {(int(t["cloud_ids"][j]), int(t["cloud_seqs"][j])) for j in range(co[i], co[i + 1])}
+    return m, vv, cl
+
+
+def _uj_join(a, b):
+    """the dot-kernel join restated independently (ujson.md:176-182): keep a's
+    dots b's context has not seen or b also holds; add b's dots a has not
+    seen; contexts united and compacted"""
+    (am, avv, acl), (bm, bvv, bcl) = a, b
+
+    def seen(vv, cl, d):
+        return d[1] <= vv.get(d[0], 0) or d in cl
+    m = {d: e for d, e in am.items() if d in bm or not seen(bvv, bcl, d)}
+    for d, e in bm.items():
+        if not seen(avv, acl, d):
+            m[d] = e
+    vv = dict(avv)
+    for r, n in bvv.items():
+        vv[r] = max(vv.get(r, 0), n)
+    cl = acl | bcl
+    for r in {d[0] for d in cl}:
+        while (r, vv.get(r, 0) + 1) in cl:
+            vv[r] = vv.get(r, 0) + 1
+    cl = {d for d in cl if d[1] > vv.get(d[0], 0)}
+    return m, vv, cl
+
+
+def _verify_ujson(eng, repo, st, applied, D, nsample=96):
+    """sampled docs (the hottest delta docs and random ones) recomputed from
+    the tables with _uj_join and compared with the engine's documents"""
+    width = len(st["key_offs"]) and int(st["key_offs"][1] - st["key_offs"][0])
+
+    def docs_of(t):
+        kb, ko = np.asarray(t["key_bytes"], np.uint8), np.asarray(t["key_offs"], np.int64)
+        return [int(bytes(kb[ko[i]:ko[i + 1]])[width - 8:]) for i in range(len(ko) - 1)]
+    rows = [dict((d, i) for i, d in enumerate(docs_of(t))) for t in applied]
+    hot = {}
+    for t, r in zip(applied, rows):
+        eo = np.diff(np.asarray(t["el_offs"], np.int64))
+        for d, i in r.items():
+            hot[d] = hot.get(d, 0) + int(eo[i])
+    pick = sorted(hot, key=hot.get, reverse=True)[:nsample // 2]
+    pick += np.random.default_rng(9).integers(0, D, nsample - len(pick)).tolist()
+    slots = eng.lookup(4, [bytes(np.asarray(st["key_bytes"], np.uint8)[
+        int(st["key_offs"][d]):int(st["key_offs"][d + 1])]) for d in pick])
+    eo, dots, elems, vv, co, cloud = eng.ujson_read(np.asarray(slots, np.uint32))
+    ids = [eng.replica_id(c) for c in range(eng.replica_count())]
+    from jylis_amd import engine as E
+    for i, d in enumerate(pick):
+        want = _uj_doc(st, d)
+        for t, r in zip(applied, rows):
+            if d in r:
+                want = _uj_join(want, _uj_doc(t, r[d]))
+        c, q = E.unpack_dot(dots[eo[i]:eo[i + 1]])
+        gm = {(ids[int(x)], int(y)): int(e) for x, y, e in zip(c, q, elems[eo[i]:eo[i + 1]])}
+        gvv = {ids[j]: int(n) for j, n in enumerate(vv[i]) if n}
+        c, q = E.unpack_dot(cloud[co[i]:co[i + 1]])
+        gcl = {(ids[int(x)], int(y)) for x, y in zip(c, q)}
+        if (gm, gvv, gcl) != want:
+            return False
+    return True
 
 
 MODES = {"gcount": bench_gcount, "treg": bench_treg, "tlog": bench_tlog, "ujson": bench_ujson, "e2e": bench_e2e,
