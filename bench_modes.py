@@ -236,7 +236,7 @@ def bench_treg(args, eng, dev, dist, rank, world):
     import torch
     from jylis_amd import synth as S
     from jylis_amd._lib import TREG
-    from jylis_amd.route import ShardRouter, TregRouter
+    from jylis_amd.route import ShardRouter, TregRouter, long_bytes
     Kper = args.keys or (8 << 20)
     G = Kper * world
     rng = np.random.default_rng(S.BASE_SEED + 3 + 1000 * rank)
@@ -268,8 +268,7 @@ def bench_treg(args, eng, dev, dist, rank, world):
         # fresh writes: batch j's timestamps sit 2^18 above batch j-1's in a
         # 2^20 window, so ~70% of keys take the delta and ties are dense
         ts = (rng.integers(0, 1 << 20, n) + (j << 18)).astype(np.uint64)
-        lens = lr & np.uint64((1 << 24) - 1)
-        batches.append(tuple(_to_dev(a, dev) for a in (own, slot, ts, pre, lr)) + (int(lens[lens > 8].sum()),))
+        batches.append(tuple(_to_dev(a, dev) for a in (own, slot, ts, pre, lr)) + (long_bytes(lr),))
     win = []
 
     def step_of(b):

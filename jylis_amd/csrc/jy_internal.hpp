@@ -353,7 +353,7 @@ struct jy_engine {
 
   // scratch (device) reused across calls, stream-ordered
   // 0-7 staged inputs, 8-14 and 16-23 merge temporaries, 15 scan temp storage
-  DevArray scratch[24];
+  DevArray scratch[28];
   // device-wide scans / selects (jy_dscan.hpp): epoch-tagged look-back words
   DevArray dscan_st;
   u32* dscan_tick = nullptr;
@@ -451,6 +451,7 @@ int32_t jy_scratch(jy_engine* eng, int idx, u64 bytes, void** out);
 int32_t jy_treg_fold(jy_engine* eng);
 // long values start on 8-byte granules (an arena collection maps granules)
 constexpr u64 kArenaAlign = 8;
+int32_t jy_arena_append_dev(jy_engine* eng, int32_t type, const uint8_t* src, u64 bytes, u64* rebase_out);
 // look-back status words for `ntiles` tiles, the ticket counter and a fresh epoch
 int32_t jy_dscan_ctx(jy_engine* eng, u64 ntiles, u64** status, u32** tick, u32* epoch);
 // copy a borrowed input into device memory if it is on the host; returns a

@@ -97,6 +97,26 @@ struct LdPad {
 
 }  // namespace
 
+// device bytes appended to a type's arena on its 8-byte granule; *rebase_out
+// receives their arena offset (routed runs: k_route.hip, k_route_csr.hip)
+int32_t jy_arena_append_dev(jy_engine* eng, int32_t type, const uint8_t* src, u64 bytes, u64* rebase_out) {
+  Arena& a = eng->arena[type];
+  const u64 at = (a.len + kArenaAlign - 1) / kArenaAlign * kArenaAlign;
+  *rebase_out = at;
+  if (bytes == 0) return JY_OK;
+  if ((at + bytes) >> (64 - JY_LR_LEN_BITS)) return eng->fail(JY_ERANGE, "arena offset overflow");
+  if (at + bytes > a.cap) {
+    const u64 nc = std::max<u64>(std::max<u64>(a.cap * 2, at + bytes), 1 << 16);
+    void* p = a.p;
+    JY_TRY(jy_realloc(eng, &p, a.len, nc, false));
+    a.p = static_cast<uint8_t*>(p);
+    a.cap = nc;
+  }
+  JY_HIP(eng, hipMemcpyAsync(a.p + at, src, bytes, hipMemcpyDeviceToDevice, eng->stream));
+  a.len = at + bytes;
+  return JY_OK;
+}
+
 extern "C" int32_t jy_arena_usage(jy_engine* eng, int32_t type, uint64_t* len_out, uint64_t* cap_out) {
   if (type < 0 || type >= JY_NTYPES) return eng->fail(JY_EINVAL, "bad type");
   *len_out = eng->arena[type].len;

@@ -28,6 +28,7 @@ constexpr int kPer = 8;  // entries per lane: one tile of 2048 entries per workg
 constexpr u64 kTile = (u64)kThreads * kPer;
 constexpr u32 kMaxShards = 64;
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u64 round_up8(u64 x) { return (x + kArenaAlign - 1) & ~(kArenaAlign - 1); }
 
 // Per-owner counts without same-address atomics per lane: a wave walks the
 // distinct owners among its lanes (one ballot each), and its leader adds the
@@ -107,7 +108,9 @@ __global__ __launch_bounds__(kThreads) void k_route_part_treg(
   for (int u = 0; u < kPer; u++) {
     const u64 len = l[u] & JY_LR_LEN_MASK;
     rk[u] = brk[u] = 0;
-    wave_aggregate<true>(base + (u64)u * kThreads < n, o[u], len > 8 ? (u32)len : 0u, lrec, lbyte, &rk[u], &brk[u]);
+    // long values keep the arena's 8-byte granules (jy_arena_collect)
+    wave_aggregate<true>(base + (u64)u * kThreads < n, o[u], len > 8 ? (u32)round_up8(len) : 0u, lrec, lbyte, &rk[u],
+                         &brk[u]);
   }
   __syncthreads();
   for (u32 d = threadIdx.x; d < S; d += kThreads) {
@@ -123,7 +126,7 @@ __global__ __launch_bounds__(kThreads) void k_route_part_treg(
     const u64 len = l[u] & JY_LR_LEN_MASK;
     const u64 bpos = gbyte[o[u]] + brk[u];
     const bool long_v = len > 8;
-    const bool fits = pos < cap && (!long_v || bpos + len <= cap_byte);
+    const bool fits = pos < cap && (!long_v || bpos + round_up8(len) <= cap_byte);
     u64x2* r = reinterpret_cast<u64x2*>(recs + ((u64)o[u] * cap + pos) * 4);  // 32-B records, two 16-B stores
     if (!fits) {
       ovf[1 + atomicAdd(ovf, 1u)] = (u32)i;
@@ -161,6 +164,7 @@ int32_t jy_treg_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, co
   if (n == 0) return JY_OK;
   if (n >= 0xFFFFFFFFull) return eng->fail(JY_ERANGE, "more than 2^32 - 1 entries in one call");
   if (reinterpret_cast<uintptr_t>(recs_dev) % 16) return eng->fail(JY_EINVAL, "recs_dev must be 16-B aligned");
+  if (cap_byte % kArenaAlign) return eng->fail(JY_EINVAL, "cap_byte must be a multiple of 8");
   if (mem == JY_HOST)
     for (u64 i = 0; i < n; i++)
       if (owner[i] >= nshards) return eng->fail(JY_ERANGE, "owner outside [0, nshards)");
@@ -184,23 +188,11 @@ int32_t jy_treg_converge_routed(jy_engine* eng, uint32_t nsrc, uint64_t cap, uin
                                 const uint64_t* recs_dev, const uint8_t* bytes_dev, const uint64_t* hdr_dev) {
   JY_HIP(eng, hipSetDevice(eng->device));
   if (nsrc == 0 || cap == 0) return JY_OK;
+  if (cap_byte % kArenaAlign) return eng->fail(JY_EINVAL, "cap_byte must be a multiple of 8");
   // the sources' byte runs go to the arena whole (nsrc x cap_byte); the
   // records address them relative to their run
-  const u64 total_bytes = (u64)nsrc * cap_byte;
-  Arena& a = eng->arena[JY_TREG];
-  if ((a.len + total_bytes) >> (64 - JY_LR_LEN_BITS)) return eng->fail(JY_ERANGE, "arena offset overflow");
-  const u64 rebase = a.len;
-  if (total_bytes) {
-    if (a.len + total_bytes > a.cap) {
-      u64 nc = std::max<u64>(std::max<u64>(a.cap * 2, a.len + total_bytes), 1 << 16);
-      void* p = a.p;
-      JY_TRY(jy_realloc(eng, &p, a.len, nc, false));
-      a.p = static_cast<uint8_t*>(p);
-      a.cap = nc;
-    }
-    JY_HIP(eng, hipMemcpyAsync(a.p + a.len, bytes_dev, total_bytes, hipMemcpyDeviceToDevice, eng->stream));
-    a.len += total_bytes;
-  }
+  u64 rebase;
+  JY_TRY(jy_arena_append_dev(eng, JY_TREG, bytes_dev, (u64)nsrc * cap_byte, &rebase));
   return jy_treg_merge_routed(eng, nsrc, cap, cap_byte, recs_dev, hdr_dev, rebase);
 }
 

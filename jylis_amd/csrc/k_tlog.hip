@@ -133,7 +133,9 @@ struct TlogArgs {
 __global__ __launch_bounds__(kThreads) void k_tlog_prep(TlogArgs A) {
   const u64 k = gid();
   if (k >= A.nd) return;
-  const u32 prev = atomicCAS(A.dptr + A.slot[k], kNone, (u32)k);
+  const u32 s = A.slot[k];
+  if (s == JY_NO_SLOT) return;  // a hole of a routed run (k_route_csr.hip)
+  const u32 prev = atomicCAS(A.dptr + s, kNone, (u32)k);
   if (prev != kNone) {
     A.bad[k] = 1;
     A.bad[prev] = 1;
@@ -196,7 +198,9 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
   // 1. keys
   if (tid < nt) {
     const u64 k = k0 + tid;
-    const TMeta m = A.meta[A.slot[k]];
+    const u32 s = A.slot[k];
+    const bool hole = s == JY_NO_SLOT;  // a routed run's unused record: skipped, not counted
+    const TMeta m = hole ? TMeta{0, 0, 0, 0, 0} : A.meta[s];
     const u64 cd = A.dcut[k];
     const u64 cut = m.cut > cd ? m.cut : cd;
     u32 drop = 0;
@@ -216,7 +220,7 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
     l_len[tid] = m.len;
     l_cap[tid] = m.cap;
     l_drop[tid] = drop;
-    l_bad[tid] = A.bad[k];
+    l_bad[tid] = hole ? 4u : A.bad[k];
     l_M[tid] = 0;
     l_minrank[tid] = 0xFFFFFFFFu;
     l_tn[tid] = 0;
@@ -402,7 +406,7 @@ __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __
     const u64 k = k0 + tid;
     const PInfo P = A.pinfo[k];
     if (P.mode == kSkip) {
-      if (A.dptr[P.s] == (u32)k) atomicAdd(skipped, 1ull);  // once per slot
+      if (P.s != JY_NO_SLOT && A.dptr[P.s] == (u32)k) atomicAdd(skipped, 1ull);  // once per slot
     } else if (P.mode == kAppend) {
       A.meta[P.s] = TMeta{P.src + P.drop, P.newlen, P.cap - P.drop, P.cut, P.newest};
     } else {

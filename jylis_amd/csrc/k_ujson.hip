@@ -349,7 +349,7 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_e
   __shared__ Shared S;
   __shared__ u32 l_slot[kDocTile];
   __shared__ LongRun l_long[4 * kDocTile];
-  __shared__ u32 l_nlong;
+  __shared__ u32 l_nlong, l_nreal;
   if (blockIdx.x < ndt) {  // doc tiles: ticketed (the look-back walks tickets)
     if (threadIdx.x == 0) l_nlong = 0;
     const u32 t = jyscan::ticket(A.tick + T_U1, &S.tk);
@@ -359,7 +359,8 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_e
     if (k < A.nd) {
       const u32 s = A.slot[k];
       l_slot[threadIdx.x] = s;
-      const UMeta m = A.meta[s];
+      const bool hole = s == JY_NO_SLOT;  // a routed run's unused record (k_route_csr.hip)
+      const UMeta m = hole ? UMeta{} : A.meta[s];
       A.abase[k] = m.ebase;
       A.cbs[k] = m.cbase;
       asz = m.elen;
@@ -367,8 +368,9 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_e
       // claim the slot for this converge (one delta per doc per call): a
       // later copy marks both bad and does not count its size
       const u64 mine = ((u64)A.epoch << 32) | (u32)k;
-      u64 old = A.dptr[s];
-      for (;;) {
+      u64 old = hole ? 0 : A.dptr[s];
+      if (hole) mark_bad(A, k);
+      for (; !hole;) {
         if ((u32)(old >> 32) == A.epoch) {
           mark_bad(A, k);
           mark_bad(A, (u32)old);
@@ -427,7 +429,7 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_e
     for (u64 j = threadIdx.x; j < kDocTile * A.R; j += kThreads) {
       const u64 dk = j / A.R, c = j - dk * A.R;
       if (kt0 + dk < A.nd) {
-        const u64 v = A.vv[(u64)l_slot[dk] * A.R + c], g = (kt0 + dk) * A.R + c;
+        const u64 v = l_slot[dk] == JY_NO_SLOT ? 0 : A.vv[(u64)l_slot[dk] * A.R + c], g = (kt0 + dk) * A.R + c;
         A.vvs[g] = v;
         A.vvm[g] = v;
         A.vvn[g] = v;
@@ -435,8 +437,13 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_e
     }
     const u64 kt1 = kt0 + kDocTile < A.nd ? kt0 + kDocTile : A.nd;
     for (u64 j = threadIdx.x; j <= kt1 - kt0; j += kThreads) S.offs[j] = A.dvoff[kt0 + j];
+    // a routed run ends in holes whose last one spans the run's unused
+    // capacity: the walk stops after the tile's last real doc
+    if (threadIdx.x == 0) l_nreal = 0;
     __syncthreads();
-    for (u64 j = S.offs[0] + threadIdx.x; j < S.offs[kt1 - kt0]; j += kThreads) {
+    if (kt0 + threadIdx.x < kt1 && l_slot[threadIdx.x] != JY_NO_SLOT) atomicMax(&l_nreal, threadIdx.x + 1);
+    __syncthreads();
+    for (u64 j = S.offs[0] + threadIdx.x; j < S.offs[l_nreal]; j += kThreads) {
       u32 lo = 0, hi = (u32)(kt1 - kt0 - 1);  // the doc of entry j
       while (lo < hi) {
         const u32 m = (lo + hi + 1) >> 1;
@@ -650,7 +657,7 @@ __global__ __launch_bounds__(kThreads) void k_uj_sizes(UjArgs A, u64 ndt) {
   const u64 k = (u64)t * kDocTile + threadIdx.x;
   JY_CLK(c0);
   u64 ne = 0, nc = 0;
-  if (k < A.nd && is_bad(A, k) && A.dptr[A.slot[k]] == (((u64)A.epoch << 32) | (u32)k))
+  if (k < A.nd && is_bad(A, k) && A.slot[k] != JY_NO_SLOT && A.dptr[A.slot[k]] == (((u64)A.epoch << 32) | (u32)k))
     atomicAdd(A.skipped, 1ull);  // a bad doc counted once per slot
   if (k < A.nd && !is_bad(A, k)) {
     ne = (sp.at(A.ao[k + 1]) - sp.at(A.ao[k])) + (sp.at(ta + A.deoff[k + 1]) - sp.at(ta + A.deoff[k]));

@@ -50,10 +50,10 @@ def run_caps(n_max, bytes_max, world):
     """(records, value bytes) per destination run for batches of at most
     n_max entries / bytes_max long-value bytes per rank"""
     if world == 1:
-        return max(n_max, 1), max(bytes_max, 1)
+        return max(n_max, 1), round8(max(bytes_max, 1))
     cap = min(max(n_max, 1), int(np.ceil(n_max / world * CAP_SLACK)) + CAP_MARGIN)
     capb = min(max(bytes_max, 1), int(np.ceil(bytes_max / world * BYTE_SLACK)) + BYTE_MARGIN)
-    return cap, capb
+    return cap, round8(capb)
 
 
 # ---- fabrics ------------------------------------------------------------------
@@ -163,18 +163,43 @@ def _check_streams(engines):
                                "switching streams")
 
 
-# ---- TREG ---------------------------------------------------------------------
+# ---- fixed-capacity runs (TREG records, TLOG logs, UJSON documents) ------------
 
-class TregRouter:
-    """Routes TREG delta batches between the shards of one node.
+def round8(x):
+    return (int(x) + 7) // 8 * 8
 
-    `step(batches)`: batches[i] = (owner, slot, ts, pre, lr, long_bytes) for
-    local rank i (CUDA tensors; owner/slot int32, the rest int64 bits;
-    long_bytes = total bytes of its values longer than 8 bytes, a host int).
-    Partition -> header + records + bytes all-to-all -> one merge of every
-    received run.  Entries that overflowed a run are sent by a drain round
-    at the next step (or `drain()`), decided from a global maximum read back
-    without stalling the GPU."""
+
+def long_bytes(lr):
+    """padded bytes of the values longer than 8 bytes among value handles
+    `lr` (numpy uint64 or CUDA int64 tensor): what their runs' byte sections take"""
+    if isinstance(lr, np.ndarray):
+        lens = (lr & np.uint64((1 << 24) - 1)).astype(np.int64)
+        return int(((lens[lens > 8] + 7) // 8 * 8).sum())
+    import torch
+    lens = lr & ((1 << 24) - 1)
+    pad = (lens + 7) // 8 * 8
+    return int(torch.where(lens > 8, pad, torch.zeros_like(pad)).sum())
+
+
+def _csr_pick(offs, idx, cols):
+    """sub-batch of the keys `idx` of a CSR on the device: (offsets, columns)"""
+    import torch
+    lo, hi = offs[idx], offs[idx + 1]
+    cnt = hi - lo
+    noffs = torch.zeros(len(idx) + 1, dtype=torch.int64, device=offs.device)
+    noffs[1:] = torch.cumsum(cnt, 0)
+    total = int(noffs[-1])
+    ent = (torch.repeat_interleave(lo - noffs[:-1], cnt, output_size=total)
+           + torch.arange(total, dtype=torch.int64, device=offs.device))
+    return noffs, [c.index_select(0, ent) for c in cols]
+
+
+class _RunRouter:
+    """Common driver of the routers: partition into fixed-capacity runs,
+    exchange (one equal-split all-to-all per buffer), merge every received
+    run; overflow goes out in a drain round decided one step later from an
+    asynchronously read global maximum.  Subclasses give the batch sizes,
+    capacities, partition, merge and the overflow sub-batch."""
 
     def __init__(self, engines, fabric):
         self.engs = list(engines)
@@ -201,42 +226,25 @@ class TregRouter:
         while self.pending is not None:
             self._settle(wait=True)
 
-    # one exchange round over the given per-rank batches
     def _round(self, batches, caps=None):
         import torch
         S, fab = self.S, self.fabric
         if caps is None:
-            nb = [np.array([int(b[0].numel()), int(b[5])], np.int64) for b in batches]
-            m = fab.host_max(nb)[0]
-            caps = run_caps(int(m[0]), int(m[1]), S)
-        cap, capb = caps
+            m = fab.host_max([np.array(self._sizes(b), np.int64) for b in batches])[0]
+            caps = self._caps([int(x) for x in m])
         sends, ovfs = [], []
         for eng, b in zip(self.engs, batches):
-            own, slot, ts, pre, lr = b[:5]
-            n = int(own.numel())
-            dev = torch.device("cuda", eng.device)
-            recs = torch.empty((S * cap, 4), dtype=torch.int64, device=dev)
-            byts = torch.empty(S * capb, dtype=torch.uint8, device=dev)
-            hdr = torch.zeros((S, 2), dtype=torch.int64, device=dev)
-            ovf = torch.zeros(n + 1, dtype=torch.int32, device=dev)
-            if n:
-                for t in (own, slot, ts, pre, lr):
-                    assert t.is_cuda and t.is_contiguous() and t.numel() == n
-                eng._check(eng.lib.jy_treg_route_part(
-                    eng.h, n, own.data_ptr(), slot.data_ptr(), ts.data_ptr(), pre.data_ptr(), lr.data_ptr(), S, cap,
-                    capb, _lib.DEVICE, C.c_void_p(recs.data_ptr()), C.c_void_p(byts.data_ptr()),
-                    C.c_void_p(hdr.data_ptr()), C.c_void_p(ovf.data_ptr())))
-            sends.append((recs, byts, hdr))
+            snd, ovf = self._part(eng, b, caps)
+            sends.append(snd)
             ovfs.append(ovf)
         if S == 1:
             recvs = sends
         else:
             recvs = [tuple(torch.empty_like(x) for x in snd) for snd in sends]
-            for k in (2, 0, 1):  # header, records, bytes
+            for k in range(len(sends[0])):
                 fab.a2a([r[k] for r in recvs], [s[k] for s in sends])
-        for eng, (recs, byts, hdr) in zip(self.engs, recvs):
-            eng._check(eng.lib.jy_treg_converge_routed(eng.h, S, cap, capb, C.c_void_p(recs.data_ptr()),
-                                                       C.c_void_p(byts.data_ptr()), C.c_void_p(hdr.data_ptr())))
+        for eng, rcv in zip(self.engs, recvs):
+            self._merge(eng, rcv, caps)
         self.routed += 1
         return ovfs
 
@@ -246,7 +254,7 @@ class TregRouter:
         gm = [o[:1].clone() for o in ovfs]
         self.fabric.max_all(gm)
         pins = []
-        for eng, g, o in zip(self.engs, gm, ovfs):
+        for g, o in zip(gm, ovfs):
             p = torch.empty(2, dtype=torch.int32, pin_memory=True)
             p[0:1].copy_(g, non_blocking=True)
             p[1:2].copy_(o[:1], non_blocking=True)
@@ -264,24 +272,182 @@ class TregRouter:
             return
         ev.synchronize()
         self.pending = None
-        gmax = int(pins[0][0])
-        if gmax == 0:
+        if int(pins[0][0]) == 0:
             return
-        import torch
-        sub = []
-        for b, o, p in zip(batches, ovfs, pins):
-            k = int(p[1])
-            idx = o[1:1 + k].long()
-            own, slot, ts, pre, lr = (t.index_select(0, idx) for t in b[:5])
-            lens = lr & ((1 << 24) - 1)
-            nbytes = int(torch.where(lens > 8, lens, torch.zeros_like(lens)).sum())
-            sub.append((own.contiguous(), slot.contiguous(), ts.contiguous(), pre.contiguous(), lr.contiguous(),
-                        nbytes))
-        m = self.fabric.host_max([np.array([int(s[0].numel()), int(s[5])], np.int64) for s in sub])[0]
+        sub = [self._subset(b, o[1:1 + int(p[1])].long()) for b, o, p in zip(batches, ovfs, pins)]
+        m = self.fabric.host_max([np.array(self._sizes(s), np.int64) for s in sub])[0]
         # capacity = the whole overflow of the largest sender: nothing can overflow again
-        ovfs2 = self._round(sub, caps=(max(int(m[0]), 1), max(int(m[1]), 1)))
+        ovfs2 = self._round(sub, caps=self._drain_caps([int(x) for x in m]))
         self.drains += 1
         self._publish(sub, ovfs2)
+
+    @staticmethod
+    def _ptr(t):
+        return C.c_void_p(t.data_ptr())
+
+
+# ---- TREG ---------------------------------------------------------------------
+
+class TregRouter(_RunRouter):
+    """Routes TREG delta batches between the shards of one node.
+
+    `step(batches)`: batches[i] = (owner, slot, ts, pre, lr, long_bytes) for
+    local rank i (CUDA tensors; owner/slot int32, the rest int64 bits;
+    long_bytes = `long_bytes(lr)`, a host int).  Partition -> header +
+    records + bytes all-to-all -> one merge of every received run."""
+
+    def _sizes(self, b):
+        return (int(b[0].numel()), int(b[5]))
+
+    def _caps(self, m):
+        return run_caps(m[0], m[1], self.S)
+
+    def _drain_caps(self, m):
+        return (max(m[0], 1), round8(max(m[1], 8)))
+
+    def _part(self, eng, b, caps):
+        import torch
+        S = self.S
+        cap, capb = caps
+        own, slot, ts, pre, lr = b[:5]
+        n = int(own.numel())
+        dev = torch.device("cuda", eng.device)
+        recs = torch.empty((S * cap, 4), dtype=torch.int64, device=dev)
+        byts = torch.empty(S * capb, dtype=torch.uint8, device=dev)
+        hdr = torch.zeros((S, 2), dtype=torch.int64, device=dev)
+        ovf = torch.zeros(n + 1, dtype=torch.int32, device=dev)
+        if n:
+            for t in (own, slot, ts, pre, lr):
+                assert t.is_cuda and t.is_contiguous() and t.numel() == n
+            eng._check(eng.lib.jy_treg_route_part(
+                eng.h, n, own.data_ptr(), slot.data_ptr(), ts.data_ptr(), pre.data_ptr(), lr.data_ptr(), S, cap,
+                capb, _lib.DEVICE, self._ptr(recs), self._ptr(byts), self._ptr(hdr), self._ptr(ovf)))
+        return (hdr, recs, byts), ovf
+
+    def _merge(self, eng, rcv, caps):
+        hdr, recs, byts = rcv
+        eng._check(eng.lib.jy_treg_converge_routed(eng.h, self.S, caps[0], caps[1], self._ptr(recs), self._ptr(byts),
+                                                   self._ptr(hdr)))
+
+    def _subset(self, b, idx):
+        own, slot, ts, pre, lr = (t.index_select(0, idx).contiguous() for t in b[:5])
+        return (own, slot, ts, pre, lr, long_bytes(lr))
+
+
+# ---- TLOG / UJSON (CSR runs, k_route_csr.hip) ------------------------------------
+
+ENT_SLACK = 1.25
+ENT_MARGIN = 1024
+
+
+def _cap_of(m, world, slack, margin):
+    if world == 1:
+        return max(m, 1)
+    return min(max(m, 1), int(np.ceil(m / world * slack)) + margin)
+
+
+class TlogRouter(_RunRouter):
+    """Routes TLOG delta batches (a key with its whole log) between shards.
+
+    batches[i] = (owner, slot, cutoff, ent_offs, ts, pre, lr, long_bytes):
+    per key owner / owner-side slot (int32), cutoff (int64 bits) and CSR
+    offsets (int64, n + 1); per entry ts, value handle pre / lr (int64 bits,
+    packed on the sending engine); long_bytes = `long_bytes(lr)`.  Each
+    owner merges the received runs one source at a time."""
+
+    def _sizes(self, b):
+        return (int(b[0].numel()), int(b[4].numel()), int(b[7]))
+
+    def _caps(self, m):
+        S = self.S
+        return (_cap_of(m[0], S, CAP_SLACK, CAP_MARGIN), _cap_of(m[1], S, ENT_SLACK, ENT_MARGIN),
+                round8(_cap_of(m[2], S, BYTE_SLACK, BYTE_MARGIN)))
+
+    def _drain_caps(self, m):
+        return (max(m[0], 1), max(m[1], 1), round8(max(m[2], 8)))
+
+    def _part(self, eng, b, caps):
+        import torch
+        S = self.S
+        cap_k, cap_e, capb = caps
+        own, slot, cut, offs, ts, pre, lr = b[:7]
+        n, nent = int(own.numel()), int(ts.numel())
+        assert int(offs.numel()) == n + 1
+        W = int(eng.lib.jy_route_words(_lib.TLOG, cap_k, (C.c_uint64 * 1)(cap_e)))
+        dev = torch.device("cuda", eng.device)
+        runs = torch.empty(S * W, dtype=torch.int64, device=dev)
+        byts = torch.empty(S * capb, dtype=torch.uint8, device=dev)
+        hdr = torch.empty(S * 8, dtype=torch.int64, device=dev)
+        ovf = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        eng._check(eng.lib.jy_tlog_route_part(
+            eng.h, n, own.data_ptr(), slot.data_ptr(), cut.data_ptr(), offs.data_ptr(), nent, ts.data_ptr(),
+            pre.data_ptr(), lr.data_ptr(), S, cap_k, cap_e, capb, _lib.DEVICE, self._ptr(runs), self._ptr(byts),
+            self._ptr(hdr), self._ptr(ovf)))
+        self.last_hdr = hdr
+        return (runs, byts), ovf
+
+    def _merge(self, eng, rcv, caps):
+        runs, byts = rcv
+        eng._check(eng.lib.jy_tlog_converge_routed(eng.h, self.S, caps[0], caps[1], caps[2], self._ptr(runs),
+                                                   self._ptr(byts)))
+
+    def _subset(self, b, idx):
+        own, slot, cut, offs, ts, pre, lr = b[:7]
+        noffs, (ts2, pre2, lr2) = _csr_pick(offs, idx, [ts, pre, lr])
+        return (own.index_select(0, idx), slot.index_select(0, idx), cut.index_select(0, idx), noffs, ts2, pre2,
+                lr2, long_bytes(lr2))
+
+
+class UjsonRouter(_RunRouter):
+    """Routes UJSON delta batches (a document with its elements, vv entries
+    and cloud dots) between shards.
+
+    batches[i] = (owner, slot, el_offs, dots, elems, vv_offs, vv, cloud_offs,
+    cloud): int32 per-doc owner / owner-side slot, int64 CSR offsets and
+    packed dots (column << 48 | seq).  Dots carry engine columns, so every
+    shard must register the cluster's replica ids in one order
+    (`Engine.replica_cols` with the same list on every shard)."""
+
+    def _sizes(self, b):
+        return (int(b[0].numel()), int(b[3].numel()), int(b[6].numel()), int(b[8].numel()))
+
+    def _caps(self, m):
+        S = self.S
+        return (_cap_of(m[0], S, CAP_SLACK, CAP_MARGIN) + 1, _cap_of(m[1], S, ENT_SLACK, ENT_MARGIN),
+                _cap_of(m[2], S, ENT_SLACK, ENT_MARGIN), _cap_of(m[3], S, ENT_SLACK, ENT_MARGIN))
+
+    def _drain_caps(self, m):
+        return (max(m[0], 1) + 1, max(m[1], 1), max(m[2], 1), max(m[3], 1))
+
+    def _part(self, eng, b, caps):
+        import torch
+        S = self.S
+        cap_k, cap_e, cap_v, cap_c = caps
+        own, slot, eo, dots, elems, vo, vv, co, cloud = b[:9]
+        n = int(own.numel())
+        W = int(eng.lib.jy_route_words(_lib.UJSON, cap_k, (C.c_uint64 * 3)(cap_e, cap_v, cap_c)))
+        dev = torch.device("cuda", eng.device)
+        runs = torch.empty(S * W, dtype=torch.int64, device=dev)
+        hdr = torch.empty(S * 8, dtype=torch.int64, device=dev)
+        ovf = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        eng._check(eng.lib.jy_ujson_route_part(
+            eng.h, n, own.data_ptr(), slot.data_ptr(), eo.data_ptr(), int(dots.numel()), dots.data_ptr(),
+            elems.data_ptr(), vo.data_ptr(), int(vv.numel()), vv.data_ptr(), co.data_ptr(), int(cloud.numel()),
+            cloud.data_ptr(), S, cap_k, cap_e, cap_v, cap_c, _lib.DEVICE, self._ptr(runs), self._ptr(hdr),
+            self._ptr(ovf)))
+        self.last_hdr = hdr
+        return (runs,), ovf
+
+    def _merge(self, eng, rcv, caps):
+        (runs,) = rcv
+        eng._check(eng.lib.jy_ujson_converge_routed(eng.h, self.S, *caps, self._ptr(runs)))
+
+    def _subset(self, b, idx):
+        own, slot, eo, dots, elems, vo, vv, co, cloud = b[:9]
+        eo2, (dots2, elems2) = _csr_pick(eo, idx, [dots, elems])
+        vo2, (vv2,) = _csr_pick(vo, idx, [vv])
+        co2, (cloud2,) = _csr_pick(co, idx, [cloud])
+        return (own.index_select(0, idx), slot.index_select(0, idx), eo2, dots2, elems2, vo2, vv2, co2, cloud2)
 
 
 # ---- counters (dense column blocks) --------------------------------------------

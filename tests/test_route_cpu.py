@@ -30,10 +30,10 @@ def test_owner_hash_matches_single_key_form():
 
 def test_run_caps():
     from jylis_amd.route import run_caps
-    assert run_caps(1000, 50, 1) == (1000, 50)
+    assert run_caps(1000, 50, 1) == (1000, 56)  # bytes: 8-byte granules
     cap, capb = run_caps(1 << 20, 1 << 22, 8)
     assert (1 << 17) < cap < (1 << 20) and (1 << 19) < capb < (1 << 22)
-    assert run_caps(10, 0, 4) == (10, 1)  # never above the whole batch
+    assert run_caps(10, 0, 4) == (10, 8)  # never above the whole batch
 
 
 def test_local_fabric_semantics():

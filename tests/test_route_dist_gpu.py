@@ -22,6 +22,27 @@ def _free_port():
     return p
 
 
+def _tlog_table(rank, rnd):
+    """rank's TLOG batch of round rnd: a random 60% of a shared key space"""
+    from jylis_amd.synth import tlog_tables
+    from test_route_csr_gpu import TLOG_CSRS, pick_rows
+    st, ds = tlog_tables(1500, 1000 + 10 * rnd + rank, rounds=1)
+    t = st if rnd == 0 else ds[0]
+    idx = np.random.default_rng(50 + 10 * rnd + rank).permutation(1500)[:900]
+    return pick_rows(t, idx, TLOG_CSRS, per_key=("cutoff",))
+
+
+def _ujson_table(rank, rnd):
+    """rank's UJSON batch of round rnd: a random 70% of one document history"""
+    from jylis_amd.synth import ujson_tables
+    from test_route_csr_gpu import UJSON_CSRS, pick_rows
+    st, ds = ujson_tables(1200, 7, rounds=rnd + 1)
+    t = st if rnd == 0 else ds[rnd - 1]
+    nk = len(t["key_offs"]) - 1
+    idx = np.random.default_rng(70 + 10 * rnd + rank).permutation(nk)[:int(nk * 0.7)]
+    return pick_rows(t, idx, UJSON_CSRS)
+
+
 def _worker(rank, world, port, q, seed):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -33,11 +54,11 @@ def _worker(rank, world, port, q, seed):
         from jylis_amd._lib import PNCOUNT, TREG
         from jylis_amd.engine import Engine, encode_keys
         from jylis_amd.repo import RepoTREG
-        from jylis_amd.route import CounterRouter, DistFabric, ShardRouter, TregRouter
+        from jylis_amd.route import CounterRouter, DistFabric, ShardRouter, TregRouter, long_bytes
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
         torch.cuda.set_device(0)
-        eng = Engine(device=0, counter_columns=8)
+        eng = Engine(device=0, counter_columns=8, ujson_columns=32)
         repo = RepoTREG(eng)
         fab = DistFabric(dist)
         ctl = ShardRouter(rank, world, lambda tab: repo._intern({"key_bytes": tab[0], "key_offs": tab[1]}),
@@ -56,8 +77,7 @@ def _worker(rank, world, port, q, seed):
             kb, ko = encode_keys(keys)
             own, slot = ctl.resolve(kb, ko)
             pre, lr = eng.pack_values(TREG, vals)
-            lens = lr & np.uint64((1 << 24) - 1)
-            router.step([(dev(own), dev(slot), dev(ts), dev(pre), dev(lr), int(lens[lens > 8].sum()))])
+            router.step([(dev(own), dev(slot), dev(ts), dev(pre), dev(lr), long_bytes(lr))])
             q.put(("batch", rank, rnd, keys, [v.decode() for v in vals], ts.tolist()))
         router.drain()
         st = repo.state()
@@ -77,6 +97,27 @@ def _worker(rank, world, port, q, seed):
             crt.step([torch.from_numpy(v.view(np.int64)).to("cuda:0")], peer)
         eng.sync()
         q.put(("pn", rank, eng.counter_export(PNCOUNT, world * Cn, 0, K).tolist()))
+        # ---- TLOG logs and UJSON documents, routed with their entries
+        from jylis_amd.repo import RepoTLOG, RepoUJSON
+        from jylis_amd.route import TlogRouter, UjsonRouter
+        from jylis_amd.synth import replica_ids
+        from test_route_csr_gpu import table_rows, tlog_device_batch, ujson_device_batch
+        tl, uj = RepoTLOG(eng), RepoUJSON(eng)
+        eng.replica_cols(replica_ids(16, 7).tolist())  # one registration order on every shard
+        ctl_t = ShardRouter(rank, world, lambda tab: tl._intern({"key_bytes": tab[0], "key_offs": tab[1]}), dist=dist)
+        ctl_u = ShardRouter(rank, world, lambda tab: uj._intern({"key_bytes": tab[0], "key_offs": tab[1]}), dist=dist)
+        trt, urt = TlogRouter([eng], fab), UjsonRouter([eng], fab)
+        for rnd in range(3):
+            t = _tlog_table(rank, rnd)
+            own, slot = ctl_t.resolve(t["key_bytes"], t["key_offs"])
+            trt.step([tlog_device_batch(eng, own, slot, t)])
+            u = _ujson_table(rank, rnd)
+            own, slot = ctl_u.resolve(u["key_bytes"], u["key_offs"])
+            urt.step([ujson_device_batch(uj, own, slot, u)])
+        trt.drain()
+        urt.drain()
+        q.put(("tlog", rank, table_rows(tl.ctype, tl.state())))
+        q.put(("ujson", rank, table_rows(uj.ctype, uj.state())))
         eng.close()
         dist.destroy_process_group()
     except Exception:
@@ -98,7 +139,7 @@ def test_two_process_routing(oracle_mod):
     for p in procs:
         p.start()
     from helpers import collect
-    msgs = collect(procs, q, world * 5)
+    msgs = collect(procs, q, world * 7)
     ref = O.Repo(O.TREG)
     for _, rank, rnd, keys, vals, ts in sorted(m for m in msgs if m[0] == "batch"):
         kb, ko = encode_keys(keys)
@@ -125,3 +166,18 @@ def test_two_process_routing(oracle_mod):
                 for c in range(Cn):
                     np.maximum(exp[:, r * Cn + c], v[:, c, d], out=exp[:, r * Cn + c])
         np.testing.assert_array_equal(dump, exp)
+    # TLOG / UJSON: the union of the two shards = one oracle repo over every batch
+    from test_route_csr_gpu import table_rows
+    for ctype, mk in ((O.TLOG, _tlog_table), (O.UJSON, _ujson_table)):
+        ref = O.Repo(ctype)
+        for rnd in range(3):
+            for r in range(world):
+                ref.converge(mk(r, rnd))
+        want = table_rows(ctype, ref.state())
+        name = "tlog" if ctype == O.TLOG else "ujson"
+        got = {}
+        for m in msgs:
+            if m[0] == name:
+                assert not set(got) & set(m[2]), "a key on two shards"
+                got.update(m[2])
+        assert got == want, name

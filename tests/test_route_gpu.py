@@ -60,9 +60,9 @@ class _Node:
                 from jylis_amd.route import _pick_keys
                 kb, ko = _pick_keys(np.asarray(b["key_bytes"], np.uint8), np.asarray(b["key_offs"], np.uint64), idx)
                 slot[idx] = self.repos[d]._intern({"key_bytes": kb, "key_offs": ko})
+        from jylis_amd.route import long_bytes
         pre, lr = self.engs[rank].pack_values(TREG, (b["val_bytes"], b["val_offs"]))
-        lens = lr & np.uint64((1 << 24) - 1)
-        nbytes = int(lens[lens > 8].sum())
+        nbytes = long_bytes(lr)
         return (_dev(own, np.uint32), _dev(slot, np.uint32), _dev(b["ts"], np.uint64), _dev(pre, np.uint64),
                 _dev(lr, np.uint64), nbytes)
 
