@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--traffic-file", default=None, help="per-launch HBM bytes from a PMC run (json)")
     ap.add_argument("--type", default="pncount", choices=["pncount", "gcount", "treg", "tlog", "ujson", "e2e", "read"],
                     help="pncount = the BASELINE metric line; the others measure SURVEY 8d configs 1,3,4,5")
-    ap.add_argument("--route", action="store_true", help="treg: run the routing exchange even on 1 GPU")
+    ap.add_argument("--route", action="store_true", help="treg / tlog / ujson: run the routing path even on 1 GPU")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1 collectives: nccl (RCCL over xGMI); gloo only rehearses the routed path "
                          "with several ranks on one GPU")

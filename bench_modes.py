@@ -353,6 +353,8 @@ def _key_strings(idx, prefix):
 # ---- TLOG (config 4: 4M keys) --------------------------------------------------
 
 def bench_tlog(args, eng, dev, dist, rank, world):
+    if world > 1 or args.route:
+        return _bench_csr_routed(args, eng, dev, dist, rank, world, "tlog")
     import torch
     from jylis_amd import synth as S
     from jylis_amd._lib import TLOG
@@ -402,25 +404,7 @@ def bench_tlog(args, eng, dev, dist, rank, world):
             ins.append(prev + nd)
         prev = now
     e2.close()
-    # verification: sampled logs recomputed from the applied tables
-    # (union of entries, largest cutoff, newest first, value order bytewise)
-    samp = np.random.default_rng(7).integers(0, K, 128)
-    applied = [st] + [dl[i % nb] for i in range(args.warmup + args.steps)]
-    want = {int(k): (0, set()) for k in samp}
-    for b in applied:
-        eo_, vo_ = np.asarray(b["ent_offs"], np.int64), np.asarray(b["val_offs"], np.int64)
-        for k in want:
-            cut, ents = want[k]
-            cut = max(cut, int(b["cutoff"][k]))
-            for j in range(eo_[k], eo_[k + 1]):
-                ents.add((int(b["ts"][j]), bytes(b["val_bytes"][vo_[j]:vo_[j + 1]])))
-            want[k] = (cut, ents)
-    cut_g, offs_g, ts_g, pre_g, lr_g = eng.tlog_read(np.array(list(want), np.uint32))
-    verified = True
-    for i, (k, (cut, ents)) in enumerate(want.items()):
-        exp = sorted((e for e in ents if e[0] >= cut), reverse=True)
-        got = [(int(ts_g[j]), eng.value_bytes(TLOG, pre_g[j], lr_g[j])) for j in range(offs_g[i], offs_g[i + 1])]
-        verified = verified and int(cut_g[i]) == cut and got == exp
+    verified = _verify_tlog(eng, st, [st] + [dl[i % nb] for i in range(args.warmup + args.steps)], K)
     k = float(np.mean(kt))
     avg_b = float(np.mean(byts))
     units = float(np.mean(ins))
@@ -440,6 +424,120 @@ def bench_tlog(args, eng, dev, dist, rank, world):
                                                  "net new entry written + 64 B meta per delta key"}}
 
 
+def _verify_tlog(eng, st, applied, K, nsample=128):
+    """sampled logs (slot = key index) recomputed from the applied tables
+    (union of entries, largest cutoff, newest first, value order bytewise)"""
+    from jylis_amd._lib import TLOG
+    samp = np.random.default_rng(7).integers(0, K, nsample)
+    want = {int(k): (0, set()) for k in samp}
+    for b in applied:
+        eo_, vo_ = np.asarray(b["ent_offs"], np.int64), np.asarray(b["val_offs"], np.int64)
+        for k in want:
+            cut, ents = want[k]
+            cut = max(cut, int(b["cutoff"][k]))
+            for j in range(eo_[k], eo_[k + 1]):
+                ents.add((int(b["ts"][j]), bytes(b["val_bytes"][vo_[j]:vo_[j + 1]])))
+            want[k] = (cut, ents)
+    cut_g, offs_g, ts_g, pre_g, lr_g = eng.tlog_read(np.array(list(want), np.uint32))
+    verified = True
+    for i, (k, (cut, ents)) in enumerate(want.items()):
+        exp = sorted((e for e in ents if e[0] >= cut), reverse=True)
+        got = [(int(ts_g[j]), eng.value_bytes(TLOG, pre_g[j], lr_g[j])) for j in range(offs_g[i], offs_g[i + 1])]
+        verified = verified and int(cut_g[i]) == cut and got == exp
+    return bool(verified)
+
+
+def _doc_index(t):
+    """the index of every key of a synth table (fixed-width keys ending in 8 digits)"""
+    kb, ko = np.asarray(t["key_bytes"], np.uint8), np.asarray(t["key_offs"], np.int64)
+    n = len(ko) - 1
+    if n == 0:
+        return np.zeros(0, np.int64)
+    rows = kb.reshape(n, int(ko[1] - ko[0]))[:, -8:].astype(np.int64) - ord("0")
+    return rows @ (10 ** np.arange(7, -1, -1, dtype=np.int64))
+
+
+def _bench_csr_routed(args, eng, dev, dist, rank, world, kind):
+    """Routed TLOG / UJSON converge: every rank ingests its own
+    peer batches (a key space of its own, keys hash-owned by all ranks) and
+    TlogRouter / UjsonRouter partition them into fixed-capacity runs, move
+    them with RCCL all-to-alls in key-range chunks (chunk c + 1 in flight
+    while chunk c merges) and the owners merge them.  At world 1 (--route)
+    the same kernels run against one shard, without an exchange."""
+    import torch
+    from jylis_amd import synth as S
+    from jylis_amd._lib import TLOG, UJSON
+    from jylis_amd.repo import RepoUJSON
+    from jylis_amd.route import DistFabric, LocalFabric, ShardRouter, TlogRouter, UjsonRouter, long_bytes
+    nb = max(1, args.batches, args.warmup + args.steps)
+    ctype = TLOG if kind == "tlog" else UJSON
+    K = args.keys or ((4 << 20) if kind == "tlog" else (1 << 20))
+    t0 = time.perf_counter()
+    if kind == "tlog":
+        st, dl = S.tlog_tables(K, seed=S.BASE_SEED + 4 + 1000 * rank, rounds=nb, key_prefix=b"l%d:" % rank)
+    else:
+        # one cluster of 16 replicas: every shard registers the ids in one order
+        st, dl = S.ujson_tables(K, seed=S.BASE_SEED + 5 + 1000 * rank, rounds=nb, R=16, key_prefix=b"u%d:" % rank,
+                                id_seed=S.BASE_SEED + 5)
+        eng.replica_cols(S.replica_ids(16, S.BASE_SEED + 5).tolist())
+    gen_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    import torch.distributed as tdist
+    cpu_group = tdist.new_group(backend="gloo") if world > 1 else None
+    ctl = ShardRouter(rank, world, lambda tab: eng.intern(ctype, tab), dist=tdist if world > 1 else None,
+                      group=cpu_group)
+    own, slot = ctl.resolve(st["key_bytes"], st["key_offs"])
+    fabric = DistFabric(tdist, cpu_group=cpu_group) if world > 1 else LocalFabric(1)
+    router = (TlogRouter if kind == "tlog" else UjsonRouter)([eng], fabric)
+    batches, units = [], []
+    repo = RepoUJSON(eng) if kind == "ujson" else None
+    for b in [st] + dl:
+        di = _doc_index(b)
+        o, s_ = own[di], slot[di]
+        if kind == "tlog":
+            pre, lr = eng.pack_values(TLOG, (b["val_bytes"], b["val_offs"]))
+            batches.append(tuple(_to_dev(a, dev) for a in (o, s_, b["cutoff"], b["ent_offs"], b["ts"], pre, lr))
+                           + (long_bytes(lr),))
+            units.append(len(b["ts"]))
+        else:
+            eo, vo, co = (np.asarray(b[k], np.uint64) for k in ("el_offs", "vv_offs", "cloud_offs"))
+            dots, elems = repo._sort_segments(eo, repo._pack(b["dot_ids"], b["dot_seqs"]), np.asarray(b["elems"]))
+            (vv,) = repo._sort_segments(vo, repo._pack(b["vv_ids"], b["vv_seqs"]))
+            (cloud,) = repo._sort_segments(co, repo._pack(b["cloud_ids"], b["cloud_seqs"]))
+            batches.append(tuple(_to_dev(a, dev) for a in (o, s_, eo, dots, elems, vo, vv, co, cloud)))
+            units.append(len(dots) + len(cloud))
+    router.step([batches[0]])
+    router.drain()
+    setup_s = time.perf_counter() - t0
+    last = args.warmup + args.steps - 1
+
+    def step(i):
+        router.step([batches[1 + i % nb]])
+        if i == last:
+            router.drain()  # the last step's overflow is part of the timed work
+
+    elapsed, kt = _timed(args.steps, args.warmup, step, dist, dev)
+    t = _max_over_ranks(elapsed, dist, dev)
+    applied = [st] + [dl[i % nb] for i in range(args.warmup + args.steps)]
+    verified = None
+    if world == 1:
+        verified = (_verify_tlog(eng, st, applied, K) if kind == "tlog"
+                    else _verify_ujson(eng, repo, st, applied, K))
+    per_step = float(np.mean([units[1 + i % nb] for i in range(args.warmup, args.warmup + args.steps)]))
+    tot = torch.tensor([per_step], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(tot)
+    name = ("TLOG converge: {K} logs per rank" if kind == "tlog" else "UJSON converge: {K} docs per rank").format(K=K)
+    return {"workload": f"{name}, peer batches routed to their key owners over {world} GPU(s) "
+                        f"(fixed-capacity runs, chunked all-to-all overlapped with the merge; SURVEY 8d config "
+                        f"{4 if kind == 'tlog' else 5}, 8e)",
+            "unit_of_work": "log entry (input)" if kind == "tlog" else "delta dot (input)",
+            "value": float(tot[0]) * args.steps / t, "ms_per_step": t / args.steps * 1e3,
+            "step_ms_avg_events": float(np.mean(kt)) * 1e3, "generate_s": gen_s, "setup_s": setup_s,
+            "routed": True, "chunks": router.chunks if world > 1 else 1, "drain_rounds": router.drains,
+            "verified_sampled_keys": verified}
+
+
 def _tlog_total(eng):
     """live TLOG entries (sum of all slot lengths)"""
     n = eng.nkeys(3)
@@ -455,6 +553,8 @@ def _tlog_total(eng):
 # ---- UJSON (config 5: 1M docs, Zipf) --------------------------------------------
 
 def bench_ujson(args, eng, dev, dist, rank, world):
+    if world > 1 or args.route:
+        return _bench_csr_routed(args, eng, dev, dist, rank, world, "ujson")
     import torch
     from jylis_amd import synth as S
     from jylis_amd._lib import UJSON

@@ -312,10 +312,13 @@ int32_t jy_treg_converge_routed(jy_engine* eng, uint32_t nsrc, uint64_t cap, uin
  * entries, cloud dots); runs_dev is u64[nshards][words], 16-B aligned.
  * Keys keep their input order in a run; the first key of a destination that
  * does not fit (records, entries or long-value bytes) and every later one go
- * to ovf_dev (u32[1 + n]: count, then input indices); unused records are
- * holes the receiver skips.  hdr_dev u64[nshards][8] receives per run the
- * keys, the entries per CSR and (TLOG) the value bytes placed; hdr and the
- * overflow count are zeroed by the call.  TLOG value bytes go to bytes_dev
+ * to ovf_dev (u32[1 + n]: [0] the count, ZERO before the first call; calls
+ * append key_base + their input index, so the chunks of one batch -- key
+ * ranges passed as offset pointers with the full entry arrays -- share one
+ * list); unused records are holes the receiver skips.  hdr_dev
+ * u64[nshards][8] receives per run the keys, the entries per CSR and (TLOG)
+ * the value bytes placed (zeroed by the call).  Offsets are absolute: a
+ * chunk's ent_offs[0] may be > 0 and nent bounds the entries it names.  TLOG value bytes go to bytes_dev
  * (u8[nshards][cap_byte], cap_byte a multiple of 8); UJSON runs need
  * cap_k >= 2 (the last record is a hole spanning the unused capacity).
  * Receiver: nsrc received runs, source-major; each source's run is merged
@@ -327,16 +330,16 @@ uint64_t jy_route_words(int32_t type, uint64_t cap_k, const uint64_t* caps);
 int32_t jy_tlog_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, const uint32_t* slot,
                            const uint64_t* cutoff, const uint64_t* ent_offs, uint64_t nent, const uint64_t* ts,
                            const uint64_t* pre, const uint64_t* lr, uint32_t nshards, uint64_t cap_k, uint64_t cap_e,
-                           uint64_t cap_byte, int32_t mem, uint64_t* runs_dev, uint8_t* bytes_dev, uint64_t* hdr_dev,
-                           uint32_t* ovf_dev);
+                           uint64_t cap_byte, uint64_t key_base, int32_t mem, uint64_t* runs_dev, uint8_t* bytes_dev,
+                           uint64_t* hdr_dev, uint32_t* ovf_dev);
 int32_t jy_tlog_converge_routed(jy_engine* eng, uint32_t nsrc, uint64_t cap_k, uint64_t cap_e, uint64_t cap_byte,
                                 uint64_t* runs_dev, const uint8_t* bytes_dev);
 int32_t jy_ujson_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, const uint32_t* slot,
                             const uint64_t* el_offs, uint64_t nel, const uint64_t* dots, const uint64_t* elems,
                             const uint64_t* vv_offs, uint64_t nvv, const uint64_t* vv, const uint64_t* cloud_offs,
                             uint64_t ncloud, const uint64_t* cloud, uint32_t nshards, uint64_t cap_k, uint64_t cap_e,
-                            uint64_t cap_v, uint64_t cap_c, int32_t mem, uint64_t* runs_dev, uint64_t* hdr_dev,
-                            uint32_t* ovf_dev);
+                            uint64_t cap_v, uint64_t cap_c, uint64_t key_base, int32_t mem, uint64_t* runs_dev,
+                            uint64_t* hdr_dev, uint32_t* ovf_dev);
 int32_t jy_ujson_converge_routed(jy_engine* eng, uint32_t nsrc, uint64_t cap_k, uint64_t cap_e, uint64_t cap_v,
                                  uint64_t cap_c, const uint64_t* runs_dev);
 

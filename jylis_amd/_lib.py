@@ -95,10 +95,10 @@ SIGNATURES = {
     "jy_treg_route_part": (I32, [P, U64, P, P, P, P, P, U32, U64, U64, I32, P, P, P, P]),
     "jy_treg_converge_routed": (I32, [P, U32, U64, U64, P, P, P]),
     "jy_route_words": (U64, [I32, U64, P]),
-    "jy_tlog_route_part": (I32, [P, U64, P, P, P, P, U64, P, P, P, U32, U64, U64, U64, I32, P, P, P, P]),
+    "jy_tlog_route_part": (I32, [P, U64, P, P, P, P, U64, P, P, P, U32, U64, U64, U64, U64, I32, P, P, P, P]),
     "jy_tlog_converge_routed": (I32, [P, U32, U64, U64, U64, P, P]),
-    "jy_ujson_route_part": (I32, [P, U64, P, P, P, U64, P, P, P, U64, P, P, U64, P, U32, U64, U64, U64, U64, I32,
-                                  P, P, P]),
+    "jy_ujson_route_part": (I32, [P, U64, P, P, P, U64, P, P, P, U64, P, P, U64, P, U32, U64, U64, U64, U64, U64,
+                                  I32, P, P, P]),
     "jy_ujson_converge_routed": (I32, [P, U32, U64, U64, U64, U64, P]),
 }
 

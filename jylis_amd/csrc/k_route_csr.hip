@@ -60,6 +60,7 @@ struct Csr {
 template <int kC>
 struct RouteArgs {
   u64 n;
+  u64 kbase;  // input index of key 0 (overflow lists name keys of the whole batch)
   u32 S;
   u64 cap_k;  // records per run
   u64 kfit;   // records that may hold a key (cap_k, or cap_k - 1 with a slack hole)
@@ -228,7 +229,7 @@ __global__ __launch_bounds__(kThreads) void k_rc_place(RouteArgs<kC> A) {
     if (kLR) fits = fits && at[1 + kC] + v[1 + kC] <= A.cap_b;
     if (!fits) {
       A.kdst[k] = kNone;
-      A.ovf[1 + atomicAdd(A.ovf, 1u)] = (u32)k;
+      A.ovf[1 + atomicAdd(A.ovf, 1u)] = (u32)(A.kbase + k);
     } else {
       u64* R = A.out + (u64)o * A.W;
       reinterpret_cast<u32*>(R + A.o_slot)[at[0]] = A.slot[k];
@@ -265,7 +266,9 @@ __global__ __launch_bounds__(kThreads) void k_rc_place(RouteArgs<kC> A) {
 }
 
 // R4: entry columns; a tile of entries of one CSR finds its keys with two
-// wave searches and per-thread bisection between them
+// wave searches and per-thread bisection between them.  The offsets are
+// absolute (a chunk of a batch starts at offs[0] > 0); the grid is the
+// host's bound, surplus tiles exit
 template <int kC, bool kLR>
 __global__ __launch_bounds__(kThreads) void k_rc_copy(RouteArgs<kC> A, u64 t1, u64 t2) {
   __shared__ u64 sh[2];
@@ -276,7 +279,7 @@ __global__ __launch_bounds__(kThreads) void k_rc_copy(RouteArgs<kC> A, u64 t1, u
   const Csr C = c == 0 ? A.c[0] : c == 1 ? A.c[kC > 1 ? 1 : 0] : A.c[kC > 2 ? 2 : 0];  // uniform: no indexed kernarg
   const u32 ncol = c == 0 ? A.ncol[0] : c == 1 ? A.ncol[kC > 1 ? 1 : 0] : A.ncol[kC > 2 ? 2 : 0];
   const u64 nent = C.offs[A.n];
-  const u64 j0 = t * kThreads;
+  const u64 j0 = C.offs[0] + t * kThreads;
   if (j0 >= nent) return;
   const u64 j1 = j0 + kThreads < nent ? j0 + kThreads : nent;
   if (threadIdx.x < 128) {
@@ -354,7 +357,6 @@ int32_t route_part(jy_engine* eng, RouteArgs<kC>& A) {
   constexpr int kQ = 1 + kC + (kLR ? 1 : 0);
   A.skipped = reinterpret_cast<unsigned long long*>(eng->skipped_dev);
   JY_HIP(eng, hipMemsetAsync(A.hdr, 0, (u64)A.S * 8 * 8, eng->stream));
-  JY_HIP(eng, hipMemsetAsync(A.ovf, 0, 4, eng->stream));
   if (n) {
     const u64 ntiles = (n + kThreads - 1) / kThreads;
     void* p;
@@ -421,8 +423,8 @@ uint64_t jy_route_words(int32_t type, uint64_t cap_k, const uint64_t* caps) {
 int32_t jy_tlog_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, const uint32_t* slot,
                            const uint64_t* cutoff, const uint64_t* ent_offs, uint64_t nent, const uint64_t* ts,
                            const uint64_t* pre, const uint64_t* lr, uint32_t nshards, uint64_t cap_k, uint64_t cap_e,
-                           uint64_t cap_byte, int32_t mem, uint64_t* runs_dev, uint8_t* bytes_dev, uint64_t* hdr_dev,
-                           uint32_t* ovf_dev) {
+                           uint64_t cap_byte, uint64_t key_base, int32_t mem, uint64_t* runs_dev, uint8_t* bytes_dev,
+                           uint64_t* hdr_dev, uint32_t* ovf_dev) {
   JY_HIP(eng, hipSetDevice(eng->device));
   JY_TRY(check_part(eng, n, nshards, cap_k, runs_dev, mem, owner));
   if (cap_byte % kArenaAlign) return eng->fail(JY_EINVAL, "cap_byte must be a multiple of 8");
@@ -430,6 +432,7 @@ int32_t jy_tlog_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, co
     return eng->fail(JY_EINVAL, "entry offsets are not a CSR of nent entries");
   RouteArgs<1> A{};
   A.n = n;
+  A.kbase = key_base;
   A.S = nshards;
   A.cap_k = cap_k;
   A.kfit = cap_k;
@@ -493,8 +496,8 @@ int32_t jy_ujson_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, c
                             const uint64_t* el_offs, uint64_t nel, const uint64_t* dots, const uint64_t* elems,
                             const uint64_t* vv_offs, uint64_t nvv, const uint64_t* vv, const uint64_t* cloud_offs,
                             uint64_t ncloud, const uint64_t* cloud, uint32_t nshards, uint64_t cap_k, uint64_t cap_e,
-                            uint64_t cap_v, uint64_t cap_c, int32_t mem, uint64_t* runs_dev, uint64_t* hdr_dev,
-                            uint32_t* ovf_dev) {
+                            uint64_t cap_v, uint64_t cap_c, uint64_t key_base, int32_t mem, uint64_t* runs_dev,
+                            uint64_t* hdr_dev, uint32_t* ovf_dev) {
   JY_HIP(eng, hipSetDevice(eng->device));
   JY_TRY(check_part(eng, n, nshards, cap_k, runs_dev, mem, owner));
   if (cap_k < 2) return eng->fail(JY_EINVAL, "cap_k must be at least 2 (the last record is a hole)");
@@ -502,6 +505,7 @@ int32_t jy_ujson_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, c
     return eng->fail(JY_EINVAL, "element / vv / cloud offsets are not CSRs of their totals");
   RouteArgs<3> A{};
   A.n = n;
+  A.kbase = key_base;
   A.S = nshards;
   A.cap_k = cap_k;
   A.kfit = cap_k - 1;

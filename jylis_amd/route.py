@@ -226,25 +226,48 @@ class _RunRouter:
         while self.pending is not None:
             self._settle(wait=True)
 
+    chunks = 1  # key-range chunks per round (CSR routers pipeline the exchange over them)
+
     def _round(self, batches, caps=None):
+        """one exchange round.  The batches are cut into `chunks` key ranges;
+        chunk c + 1's all-to-alls are in flight while the owners merge chunk c
+        (RCCL runs on its own stream; the engine's merge kernels on the
+        compute stream).  Drain rounds (caps given) go in one chunk."""
         import torch
         S, fab = self.S, self.fabric
+        nch = self.chunks if (caps is None and S > 1) else 1
         if caps is None:
             m = fab.host_max([np.array(self._sizes(b), np.int64) for b in batches])[0]
-            caps = self._caps([int(x) for x in m])
-        sends, ovfs = [], []
-        for eng, b in zip(self.engs, batches):
-            snd, ovf = self._part(eng, b, caps)
-            sends.append(snd)
-            ovfs.append(ovf)
+            caps = self._caps([int(x) for x in m], nch)
+        ovfs = [torch.zeros(int(b[0].numel()) + 1, dtype=torch.int32, device=torch.device("cuda", e.device))
+                for e, b in zip(self.engs, batches)]
+        sends = []  # [chunk][local rank]
+        for c in range(nch):
+            per = []
+            for eng, b, ovf in zip(self.engs, batches, ovfs):
+                n = int(b[0].numel())
+                per.append(self._part(eng, b, caps, c * n // nch, (c + 1) * n // nch, ovf))
+            sends.append(per)
         if S == 1:
-            recvs = sends
+            for per in sends:
+                for eng, snd in zip(self.engs, per):
+                    self._merge(eng, snd, caps)
         else:
-            recvs = [tuple(torch.empty_like(x) for x in snd) for snd in sends]
-            for k in range(len(sends[0])):
-                fab.a2a([r[k] for r in recvs], [s[k] for s in sends])
-        for eng, rcv in zip(self.engs, recvs):
-            self._merge(eng, rcv, caps)
+            def issue(c):
+                recv = [tuple(torch.empty_like(x) for x in snd) for snd in sends[c]]
+                works = [fab.a2a([r[k] for r in recv], [s_[k] for s_ in sends[c]], async_op=True)
+                         for k in range(len(sends[c][0]))]
+                return recv, works
+
+            cur = issue(0)
+            for c in range(nch):
+                recv, works = cur
+                for w in works:
+                    w.wait()
+                if c + 1 < nch:
+                    cur = issue(c + 1)
+                for eng, rcv in zip(self.engs, recv):
+                    self._merge(eng, rcv, caps)
         self.routed += 1
         return ovfs
 
@@ -299,30 +322,30 @@ class TregRouter(_RunRouter):
     def _sizes(self, b):
         return (int(b[0].numel()), int(b[5]))
 
-    def _caps(self, m):
+    def _caps(self, m, nch):
         return run_caps(m[0], m[1], self.S)
 
     def _drain_caps(self, m):
         return (max(m[0], 1), round8(max(m[1], 8)))
 
-    def _part(self, eng, b, caps):
+    def _part(self, eng, b, caps, a, e, ovf):
         import torch
         S = self.S
         cap, capb = caps
         own, slot, ts, pre, lr = b[:5]
         n = int(own.numel())
+        assert (a, e) == (0, n), "TREG rounds are not chunked"
         dev = torch.device("cuda", eng.device)
         recs = torch.empty((S * cap, 4), dtype=torch.int64, device=dev)
         byts = torch.empty(S * capb, dtype=torch.uint8, device=dev)
         hdr = torch.zeros((S, 2), dtype=torch.int64, device=dev)
-        ovf = torch.zeros(n + 1, dtype=torch.int32, device=dev)
         if n:
             for t in (own, slot, ts, pre, lr):
                 assert t.is_cuda and t.is_contiguous() and t.numel() == n
             eng._check(eng.lib.jy_treg_route_part(
                 eng.h, n, own.data_ptr(), slot.data_ptr(), ts.data_ptr(), pre.data_ptr(), lr.data_ptr(), S, cap,
                 capb, _lib.DEVICE, self._ptr(recs), self._ptr(byts), self._ptr(hdr), self._ptr(ovf)))
-        return (hdr, recs, byts), ovf
+        return (hdr, recs, byts)
 
     def _merge(self, eng, rcv, caps):
         hdr, recs, byts = rcv
@@ -358,15 +381,18 @@ class TlogRouter(_RunRouter):
     def _sizes(self, b):
         return (int(b[0].numel()), int(b[4].numel()), int(b[7]))
 
-    def _caps(self, m):
+    chunks = 4
+
+    def _caps(self, m, nch):
         S = self.S
+        m = [-(-x // nch) for x in m]
         return (_cap_of(m[0], S, CAP_SLACK, CAP_MARGIN), _cap_of(m[1], S, ENT_SLACK, ENT_MARGIN),
                 round8(_cap_of(m[2], S, BYTE_SLACK, BYTE_MARGIN)))
 
     def _drain_caps(self, m):
         return (max(m[0], 1), max(m[1], 1), round8(max(m[2], 8)))
 
-    def _part(self, eng, b, caps):
+    def _part(self, eng, b, caps, a, e, ovf):
         import torch
         S = self.S
         cap_k, cap_e, capb = caps
@@ -378,13 +404,12 @@ class TlogRouter(_RunRouter):
         runs = torch.empty(S * W, dtype=torch.int64, device=dev)
         byts = torch.empty(S * capb, dtype=torch.uint8, device=dev)
         hdr = torch.empty(S * 8, dtype=torch.int64, device=dev)
-        ovf = torch.empty(n + 1, dtype=torch.int32, device=dev)
         eng._check(eng.lib.jy_tlog_route_part(
-            eng.h, n, own.data_ptr(), slot.data_ptr(), cut.data_ptr(), offs.data_ptr(), nent, ts.data_ptr(),
-            pre.data_ptr(), lr.data_ptr(), S, cap_k, cap_e, capb, _lib.DEVICE, self._ptr(runs), self._ptr(byts),
-            self._ptr(hdr), self._ptr(ovf)))
+            eng.h, e - a, own[a:].data_ptr(), slot[a:].data_ptr(), cut[a:].data_ptr(), offs[a:].data_ptr(), nent,
+            ts.data_ptr(), pre.data_ptr(), lr.data_ptr(), S, cap_k, cap_e, capb, a, _lib.DEVICE, self._ptr(runs),
+            self._ptr(byts), self._ptr(hdr), self._ptr(ovf)))
         self.last_hdr = hdr
-        return (runs, byts), ovf
+        return (runs, byts)
 
     def _merge(self, eng, rcv, caps):
         runs, byts = rcv
@@ -411,32 +436,33 @@ class UjsonRouter(_RunRouter):
     def _sizes(self, b):
         return (int(b[0].numel()), int(b[3].numel()), int(b[6].numel()), int(b[8].numel()))
 
-    def _caps(self, m):
+    chunks = 4
+
+    def _caps(self, m, nch):
         S = self.S
+        m = [-(-x // nch) for x in m]
         return (_cap_of(m[0], S, CAP_SLACK, CAP_MARGIN) + 1, _cap_of(m[1], S, ENT_SLACK, ENT_MARGIN),
                 _cap_of(m[2], S, ENT_SLACK, ENT_MARGIN), _cap_of(m[3], S, ENT_SLACK, ENT_MARGIN))
 
     def _drain_caps(self, m):
         return (max(m[0], 1) + 1, max(m[1], 1), max(m[2], 1), max(m[3], 1))
 
-    def _part(self, eng, b, caps):
+    def _part(self, eng, b, caps, a, e, ovf):
         import torch
         S = self.S
         cap_k, cap_e, cap_v, cap_c = caps
         own, slot, eo, dots, elems, vo, vv, co, cloud = b[:9]
-        n = int(own.numel())
         W = int(eng.lib.jy_route_words(_lib.UJSON, cap_k, (C.c_uint64 * 3)(cap_e, cap_v, cap_c)))
         dev = torch.device("cuda", eng.device)
         runs = torch.empty(S * W, dtype=torch.int64, device=dev)
         hdr = torch.empty(S * 8, dtype=torch.int64, device=dev)
-        ovf = torch.empty(n + 1, dtype=torch.int32, device=dev)
         eng._check(eng.lib.jy_ujson_route_part(
-            eng.h, n, own.data_ptr(), slot.data_ptr(), eo.data_ptr(), int(dots.numel()), dots.data_ptr(),
-            elems.data_ptr(), vo.data_ptr(), int(vv.numel()), vv.data_ptr(), co.data_ptr(), int(cloud.numel()),
-            cloud.data_ptr(), S, cap_k, cap_e, cap_v, cap_c, _lib.DEVICE, self._ptr(runs), self._ptr(hdr),
-            self._ptr(ovf)))
+            eng.h, e - a, own[a:].data_ptr(), slot[a:].data_ptr(), eo[a:].data_ptr(), int(dots.numel()),
+            dots.data_ptr(), elems.data_ptr(), vo[a:].data_ptr(), int(vv.numel()), vv.data_ptr(), co[a:].data_ptr(),
+            int(cloud.numel()), cloud.data_ptr(), S, cap_k, cap_e, cap_v, cap_c, a, _lib.DEVICE, self._ptr(runs),
+            self._ptr(hdr), self._ptr(ovf)))
         self.last_hdr = hdr
-        return (runs,), ovf
+        return (runs,)
 
     def _merge(self, eng, rcv, caps):
         (runs,) = rcv

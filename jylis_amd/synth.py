@@ -252,13 +252,14 @@ def tlog_tables(K, seed, rounds=1, mean_state=8, cap=64, mean_delta=2, key_prefi
     return state, deltas
 
 
-def ujson_tables(D, seed, rounds=1, R=16, leaves=8, zipf=1.1, ops_per_round=None, key_prefix=b"u"):
+def ujson_tables(D, seed, rounds=1, R=16, leaves=8, zipf=1.1, ops_per_round=None, key_prefix=b"u", id_seed=None):
     """Config-5 stream: D docs with ~`leaves` elements over R
     replicas, then `rounds` delta batches whose ops (70% INS, 20% RM, 10% CLR)
     hit docs with Zipf(zipf) popularity; ops on one doc fold into one delta.
-    Tables use replica ids (oracle layout).  Returns (state, [deltas])."""
+    Tables use replica ids (oracle layout; `id_seed` picks the id set, so
+    shards can share one cluster of replicas).  Returns (state, [deltas])."""
     rng = np.random.default_rng(seed)
-    ids = replica_ids(R, seed)
+    ids = replica_ids(R, seed if id_seed is None else id_seed)
     kb, ko = counter_keys(D, prefix=key_prefix)
     # ---- state, vectorised: vv, elements under seen dots, gapped cloud dots
     vv = rng.integers(0, 24, (D, R)).astype(np.int64)

@@ -328,7 +328,7 @@ def test_run_layout_holes():
         ovf = torch.zeros(7, dtype=torch.int32, device="cuda:0")
         d = [_dev(x) for x in (own, slot, cut, offs, ts, pre, lr)]
         eng._check(eng.lib.jy_tlog_route_part(eng.h, 6, *[x.data_ptr() for x in d[:4]], 8,
-                                              *[x.data_ptr() for x in d[4:]], S, cap_k, cap_e, 8, _lib.DEVICE,
+                                              *[x.data_ptr() for x in d[4:]], S, cap_k, cap_e, 8, 0, _lib.DEVICE,
                                               C.c_void_p(runs.data_ptr()), C.c_void_p(byts.data_ptr()),
                                               C.c_void_p(hdr.data_ptr()), C.c_void_p(ovf.data_ptr())))
         torch.cuda.synchronize()
