@@ -93,19 +93,19 @@ __device__ __forceinline__ TRec load_rec(const TRec* __restrict__ p) {
   return r;
 }
 
-enum : u32 { kSkip = 0, kAppend = 1, kRebuild = 2 };
+enum : u32 { kSkip = 0, kAppend = 1, kRebuild = 2, kFast = 3 };
 
-// per delta key: what k_tlog_tile decided (k_tlog_commit publishes it)
+// per REBUILT key (a worklist entry): what k_tlog_tile decided; the log's
+// current base is read from its meta at commit (a compaction may move it)
 struct alignas(16) PInfo {
-  u64 src;      // old base of the log
-  u64 newest;   // newest ts after the merge
-  u64 cut;      // merged cutoff
-  u32 len;      // old length
-  u32 drop;     // state entries dropped by the cutoff (a prefix)
-  u32 newlen;   // entries after the merge
-  u32 cap;      // append: old cap; rebuild: the new segment's capacity
-  u32 mode;
-  u32 s;
+  u64 newest;  // newest ts after the merge
+  u64 cut;     // merged cutoff
+  u32 k;       // delta key
+  u32 s;       // slot
+  u32 len;     // old length
+  u32 drop;    // state entries dropped by the cutoff (a prefix)
+  u32 newlen;  // entries after the merge
+  u32 cap;     // the new segment's capacity
 };
 
 struct TlogArgs {
@@ -121,10 +121,11 @@ struct TlogArgs {
   const u64* dpre;
   const u64* dlr;
   // temporaries
-  u32* dptr;     // [nkeys] delta key merging into each slot
-  u32* bad;      // [nd] repeated slot in the batch
-  PInfo* pinfo;  // [nd]
-  u64* relsz;    // [nd + 1] pool entries a rebuilt key takes (0 otherwise)
+  u32* dptr;      // [nkeys] delta key merging into each slot
+  u32* bad;       // [nd] repeated slot in the batch
+  PInfo* pinfo;   // [nd] written for rebuilt keys only
+  u32* rz;        // [nd + 1] pool entries a rebuilt key takes (0 otherwise)
+  unsigned long long* skipped;
 };
 
 // A slot named twice in one device batch breaks the one-delta-per-key
@@ -142,9 +143,70 @@ __global__ __launch_bounds__(kThreads) void k_tlog_prep(TlogArgs A) {
   }
 }
 
-// capacity of a rebuilt segment: room to double by appends, power of two
+// first position in [lo, hi) of the log at pool[base..] whose timestamp is
+// >= x (the log ascends): 16-ary probes, every probe of a round loaded at
+// once -- one round trip for a log of <= 16 entries, two up to 256
+constexpr u32 kProbe = 16;
+__device__ __forceinline__ u32 ts_lower(const TRec* __restrict__ pool, u64 base, u32 lo, u32 hi, u64 x) {
+  while (hi > lo) {
+    const u32 n = hi - lo;
+    const u32 step = (n + kProbe - 1) / kProbe;  // probe i looks at lo + i * step + step - 1
+    u32 c = 0;
+#pragma unroll
+    for (u32 i = 0; i < kProbe; i++) {
+      const u32 at = lo + i * step + step - 1;
+      if (at < hi) c += pool[base + at].ts < x;
+    }
+    // c whole blocks of `step` lie below x; the answer is inside block c
+    const u32 nlo = lo + c * step;
+    if (step == 1) return nlo;
+    hi = nlo + step - 1 < hi ? nlo + step - 1 : hi;  // the block's last entry was probed >= x (or is hi)
+    lo = nlo;
+  }
+  return lo;
+}
+
+// first position in [lo, hi) of a log whose timestamps ascend from `tlo`
+// (at lo) to `thi` (at hi - 1) with timestamp >= x.  Timestamps follow wall
+// time, so an interpolated guess and one window of kWin entries around it
+// (loaded at once: one round trip, ~2 cache lines) usually settle it; else
+// a binary search of the side the window ruled out
+constexpr u32 kWin = 8;
+__device__ __forceinline__ u32 ts_interp(const TRec* __restrict__ pool, u64 base, u32 lo, u32 hi, u64 tlo, u64 thi,
+                                         u64 x) {
+  if (hi - lo > kWin && x > tlo && x <= thi && thi > tlo) {
+    const double f = (double)(x - tlo) / (double)(thi - tlo);
+    u32 g = lo + (u32)(f * (double)(hi - 1 - lo));
+    g = g >= lo + kWin / 2 ? g - kWin / 2 : lo;
+    if (g > hi - kWin) g = hi - kWin;
+    u64 w[kWin];
+#pragma unroll
+    for (u32 i = 0; i < kWin; i++) w[i] = pool[base + g + i].ts;
+    u32 c = 0;
+#pragma unroll
+    for (u32 i = 0; i < kWin; i++) c += w[i] < x;
+    if (c == 0) {
+      if (g == lo) return lo;
+      hi = g;  // the answer is at or before g
+    } else if (c == kWin) {
+      lo = g + kWin;  // after the window
+    } else {
+      return g + c;
+    }
+  }
+  while (lo < hi) {
+    const u32 m = (lo + hi) >> 1;
+    if (pool[base + m].ts < x) lo = m + 1;
+    else hi = m;
+  }
+  return lo;
+}
+
+// capacity of a rebuilt segment: room to grow 4x by appends, power of two
+// (HBM is plentiful; every rebuild copies the whole log, so they should be rare)
+constexpr u64 kGrow = 4;
 __device__ __forceinline__ u32 pow2_cap(u32 n) {
-  const u64 want = 2 * (u64)n + 2;
+  const u64 want = kGrow * (u64)n + kGrow;
   u64 c = 4;
   while (c < want) c <<= 1;
   return c > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)c;
@@ -163,185 +225,201 @@ __device__ __forceinline__ u32 lds_last_le(const u64* a, u32 n, u64 x) {
 
 // key tiles are one wave: no cross-wave barriers, many tiles in flight per CU
 constexpr int kTile = 64;
-// delta entries per lane per pass of k_tlog_tile (rows of kTile entries; the
-// code is general, 1 measured fastest: 2 and 4 raise VGPRs and cut waves in flight)
-constexpr int kU = 1;
-constexpr int kCU = 1;  // output entries per lane per pass of the rebuild (2: same time)
+constexpr int kFastEnt = 4;  // delta entries a key may have for the lane-per-key fast path
+constexpr int kCache = 2;    // passes of slow entries kept in registers for the append stores
+constexpr int kCU = 1;       // output entries per lane per pass of the rebuild (2: same time)
 
 constexpr u32 kKept = 0x80000000u;  // eqx: kept flag | # kept entries of the key before this one
 
-// KEY TILES: a workgroup (one wave) owns kTile consecutive delta keys and all their
-// delta entries (contiguous in the batch).  Keys are staged in LDS, entries
-// are walked in coalesced chunks of kTile with lanes on consecutive
-// entries, and per-key facts are gathered with LDS atomics and a block scan:
-//   1. per key (lane = key): log meta, merged cutoff, dropped prefix
-//   2. per entry: order check against the previous entry; kept flag and
-//      rank (# state entries older than it: len for the usual entry, newer
-//      than the log; else a binary search of the log, duplicates dropped);
-//      q = kept entries of the key before it (block scan with carry)
-//   3. per key: append (every kept entry has rank len, room left) or rebuild
-//   4. per entry: kept entries of append keys go to the tail, oldest first
-// rank/q of every entry go to HBM for the rebuild in k_tlog_commit.
+// KEY TILES: a workgroup (one wave) owns kTile consecutive delta keys.
+//   1. per key (lane = key): meta, merged cutoff; the FAST PATH -- a delta of
+//      at most kFastEnt entries, strictly newest first, every kept entry
+//      newer than the log, room in the segment, no cutoff raise -- is
+//      appended and its meta published right here, its entries loaded by
+//      the key's own lane together with the meta (one round trip)
+//   2. the other keys' entries, flattened (LDS prefix of their counts), lanes
+//      on consecutive entries: order check against the previous entry; kept
+//      flag and rank (# state entries older than it: len for an entry newer
+//      than the log, else a binary search, duplicates dropped); q = kept
+//      entries of the key before it (ballot with carry)
+//   3. per key: append (every kept entry has rank len, room left) -> meta
+//      published; rebuild -> its plan and size for k_tlog_commit; skip
+//   4. appends: kept entries to the tail, oldest first (the first kCache
+//      passes from registers)
+// rank / q of the slow entries go to HBM for the rebuild in k_tlog_commit.
 #ifndef JY_TLOG_TILE_ATTR
-// 80 VGPRs: 6 waves per SIMD (81 gave 5; measured 7% faster converges)
-#define JY_TLOG_TILE_ATTR __attribute__((amdgpu_waves_per_eu(6)))
+#define JY_TLOG_TILE_ATTR
 #endif
-__global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs A, TRec* __restrict__ pool, u32* __restrict__ erank,
-                                                        u32* __restrict__ eqx) {
-  __shared__ u64 l_eoff[kTile + 1];
+__global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs A, TRec* __restrict__ pool,
+                                                                        u32* __restrict__ erank,
+                                                                        u32* __restrict__ eqx) {
+  __shared__ u64 l_soff[kTile + 1];  // flattened offsets of the slow keys' entries
+  __shared__ u64 l_gb[kTile];        // first delta entry of each key
+  __shared__ u32 l_slot[kTile];
+  __shared__ u64 l_oldest[kTile];  // oldest surviving timestamp of a slow key's log
   __shared__ u64 l_base[kTile], l_newest[kTile], l_cut[kTile], l_tn[kTile];
-  __shared__ u32 l_len[kTile], l_cap[kTile], l_drop[kTile], l_M[kTile], l_minrank[kTile],
-      l_bad[kTile], l_gstart[kTile], l_mode[kTile];
+  __shared__ u32 l_len[kTile], l_cap[kTile], l_drop[kTile], l_M[kTile], l_minrank[kTile], l_bad[kTile],
+      l_gstart[kTile], l_mode[kTile];
   const u32 tid = threadIdx.x;
+  const u64 lanelt = (1ull << tid) - 1;
   const u64 k0 = (u64)blockIdx.x * kTile;
   const u32 nt = (u32)(A.nd - k0 < kTile ? A.nd - k0 : kTile);
   // 1. keys
+  u64 sc = 0;  // slow entries of this lane's key
   if (tid < nt) {
     const u64 k = k0 + tid;
     const u32 s = A.slot[k];
+    const u64 b0 = A.doff[k], b1 = A.doff[k + 1];
+    const u64 ne = b1 - b0;
+    u64 ft[kFastEnt], fp[kFastEnt], fl[kFastEnt];
+#pragma unroll
+    for (int u = 0; u < kFastEnt; u++) {  // issued with the meta load
+      ft[u] = fp[u] = fl[u] = 0;
+      if ((u64)u < ne) {
+        ft[u] = A.dts[b0 + u];
+        fp[u] = A.dpre[b0 + u];
+        fl[u] = A.dlr[b0 + u];
+      }
+    }
     const bool hole = s == JY_NO_SLOT;  // a routed run's unused record: skipped, not counted
     const TMeta m = hole ? TMeta{0, 0, 0, 0, 0} : A.meta[s];
     const u64 cd = A.dcut[k];
+    const u32 bad = hole ? 4u : A.bad[k];
     const u64 cut = m.cut > cd ? m.cut : cd;
-    u32 drop = 0;
-    if (cd > m.cut && m.len > 0 && A.pool[m.base].ts < cut) {
-      u32 l = 0, h = m.len;  // oldest first: the cutoff drops a prefix
-      while (l < h) {
-        const u32 mid = (l + h) >> 1;
-        if (A.pool[m.base + mid].ts < cut) l = mid + 1;
-        else h = mid;
+    bool fast = !bad && ne <= kFastEnt && cd <= m.cut;
+    u32 M = 0;  // kept entries newer than the log: a prefix (strictly newest first)
+#pragma unroll
+    for (int u = 0; u < kFastEnt; u++) {
+      if ((u64)u >= ne) continue;
+      if (u > 0) fast = fast && ft[u - 1] > ft[u];  // equal timestamps need the value order
+      if (ft[u] >= cut) {
+        if (m.len == 0 || ft[u] > m.newest) M++;
+        else fast = false;  // not newer than the log: a search (stage 2)
       }
-      drop = l;
     }
-    l_eoff[tid] = A.doff[k];
-    l_base[tid] = m.base;
-    l_newest[tid] = m.newest;
-    l_cut[tid] = cut;
-    l_len[tid] = m.len;
-    l_cap[tid] = m.cap;
-    l_drop[tid] = drop;
-    l_bad[tid] = hole ? 4u : A.bad[k];
-    l_M[tid] = 0;
-    l_minrank[tid] = 0xFFFFFFFFu;
-    l_tn[tid] = 0;
+    fast = fast && m.len + M <= m.cap;
+    if (fast) {
+#pragma unroll
+      for (int u = 0; u < kFastEnt; u++)
+        if ((u32)u < M) store_rec(pool + m.base + m.len + (M - 1 - u), ft[u], fp[u], fl[u]);
+      if (M) A.meta[s] = TMeta{m.base, m.len + M, m.cap, m.cut, (m.len == 0 || ft[0] > m.newest) ? ft[0] : m.newest};
+    } else {
+      u32 drop = 0;
+      if (cd > m.cut && m.len > 0) drop = ts_lower(A.pool, m.base, 0, m.len, cut);  // oldest first: a prefix
+      l_oldest[tid] = m.len > drop ? A.pool[m.base + drop].ts : 0;  // for the interpolated searches
+      sc = ne;
+      l_base[tid] = m.base;
+      l_newest[tid] = m.newest;
+      l_cut[tid] = cut;
+      l_len[tid] = m.len;
+      l_cap[tid] = m.cap;
+      l_drop[tid] = drop;
+      l_bad[tid] = bad;
+      l_M[tid] = 0;
+      l_minrank[tid] = 0xFFFFFFFFu;
+      l_tn[tid] = 0;
+    }
+    l_gb[tid] = b0;
+    l_slot[tid] = s;
+    l_mode[tid] = fast ? kFast : kSkip;
   }
-  if (tid == 0) l_eoff[nt] = A.doff[k0 + nt];
-  if (blockIdx.x == 0 && tid == 0) A.relsz[A.nd] = 0;
+  {
+    const u64 inc = jyscan::wave_incl<u64>(sc);
+    const u64 tot = __shfl(inc, 63);  // every lane: a shuffle reads only active lanes
+    if (tid < nt) l_soff[tid] = inc - sc;
+    if (tid == 0) l_soff[nt] = tot;
+  }
   __syncthreads();
-  const u64 E0 = l_eoff[0], E1 = l_eoff[nt];
-  // 2. entries, kU per lane per pass (row u = lanes on consecutive entries):
-  // every load of a pass is issued before any decision, and the binary
-  // searches of the pass advance level by level together
+#ifdef JY_TLOG_AB_NOSLOW  // A/B only: the cost of stage 1 alone (WRONG results)
+  const u64 F = 0;
+#else
+  const u64 F = l_soff[nt];
+#endif
+  // 2. slow entries, one per lane per pass
   u32 carry = 0;
-  const u64 lanelt = (1ull << tid) - 1;
-  for (u64 c0 = E0; c0 < E1; c0 += (u64)kTile * kU) {
-    u32 idx[kU], flag[kU], rank[kU], lo[kU], hi[kU];
-    u64 t[kU], pp[kU], ll[kU], pt[kU];
+  u64 c_t[kCache], c_p[kCache], c_l[kCache];
+  u32 c_q[kCache], c_i[kCache];
 #pragma unroll
-    for (int u = 0; u < kU; u++) {
-      const u64 j = c0 + (u64)u * kTile + tid;
-      flag[u] = rank[u] = 0;
-      lo[u] = hi[u] = 0;
-      idx[u] = 0;
-      if (j < E1) {
-        idx[u] = lds_last_le(l_eoff, nt - 1, j);
-        t[u] = A.dts[j];
-        pp[u] = A.dpre[j];
-        ll[u] = A.dlr[j];
-        pt[u] = j > l_eoff[idx[u]] ? A.dts[j - 1] : ~0ull;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-      const u64 j = c0 + (u64)u * kTile + tid;
-      const u32 i = idx[u];
-      u32 f = 0, r = 0, l = 0, h = 0;
-      if (j < E1) {
-        // strictly newest first; the previous value is read only on a ts tie
-        if (j > l_eoff[i] && (pt[u] < t[u] || (pt[u] == t[u] && jy_value_cmp(A.dpre[j - 1], A.dlr[j - 1], pp[u],
-                                                                             ll[u], A.arena) <= 0)))
-          atomicOr(&l_bad[i], 2u);
-        const u32 len = l_len[i], drop = l_drop[i];
-        if (t[u] >= l_cut[i]) {
-          if (len == drop || t[u] > l_newest[i]) {
-            f = 1;
-            r = len;
-          } else {
-            l = drop;  // search: first entry of the log not older than x
-            h = len;
-            f = 2;     // pending
-          }
+  for (int c = 0; c < kCache; c++) c_q[c] = c_i[c] = 0, c_t[c] = c_p[c] = c_l[c] = 0;
+  int pass = 0;
+  for (u64 c0 = 0; c0 < F; c0 += kTile, pass++) {
+    const u64 f = c0 + tid;
+    u32 idx = 0, flag = 0, rank = 0, lo = 0, hi = 0;
+    u64 t = 0, pp = 0, ll = 0, j = 0;
+    if (f < F) {
+      idx = lds_last_le(l_soff, nt - 1, f);
+      j = l_gb[idx] + (f - l_soff[idx]);
+      t = A.dts[j];
+      pp = A.dpre[j];
+      ll = A.dlr[j];
+      const u64 pt = f > l_soff[idx] ? A.dts[j - 1] : ~0ull;
+      // strictly newest first; the previous value is read only on a ts tie
+      if (f > l_soff[idx] && (pt < t || (pt == t && jy_value_cmp(A.dpre[j - 1], A.dlr[j - 1], pp, ll, A.arena) <= 0)))
+        atomicOr(&l_bad[idx], 2u);
+      const u32 len = l_len[idx], drop = l_drop[idx];
+      if (t >= l_cut[idx]) {
+        if (len == drop || t > l_newest[idx]) {
+          flag = 1;
+          rank = len;
+        } else {
+          lo = drop;  // search: first entry of the log not older than x
+          hi = len;
+          flag = 2;   // pending
         }
       }
-      flag[u] = f;
-      rank[u] = r;
-      lo[u] = l;
-      hi[u] = h;
     }
-    // interleaved binary searches: one level of every pending search per round
-    for (;;) {
-      bool any = false;
-      u64 mt[kU];
-#pragma unroll
-      for (int u = 0; u < kU; u++)
-        if (flag[u] == 2 && lo[u] < hi[u]) {
-          mt[u] = A.pool[l_base[idx[u]] + ((lo[u] + hi[u]) >> 1)].ts;
-          any = true;
-        }
-      if (!any) break;
-#pragma unroll
-      for (int u = 0; u < kU; u++)
-        if (flag[u] == 2 && lo[u] < hi[u]) {
-          const u32 m = (lo[u] + hi[u]) >> 1;
-          const Ent x{t[u], pp[u], ll[u]};
-          const int c = mt[u] != x.t ? (mt[u] > x.t ? 1 : -1) : cmp_at(A.pool, l_base[idx[u]] + m, x, A.arena);
-          if (c < 0) lo[u] = m + 1;
-          else hi[u] = m;
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < kU; u++)
-      if (flag[u] == 2) {
-        const Ent x{t[u], pp[u], ll[u]};
-        rank[u] = lo[u];
-        flag[u] = !(lo[u] < l_len[idx[u]] && cmp_at(A.pool, l_base[idx[u]] + lo[u], x, A.arena) == 0);
+    if (flag == 2) {
+      // the first log entry not older than x: a binary search of the
+      // timestamps (16-ary probes read ~2x the lines: measured slower), then
+      // the values of the (usually 0 or 1) entries with x's timestamp
+      const u64 base = l_base[idx];
+      const u32 r = ts_interp(A.pool, base, lo, hi, l_oldest[idx], l_newest[idx], t);
+      int c = 1;
+      u32 e = r;
+      for (; e < hi; e++) {
+        const TRec y = A.pool[base + e];
+        if (y.ts != t) break;
+        c = jy_value_cmp(y.pre, y.lr, pp, ll, A.arena);
+        if (c >= 0) break;
       }
-    // kept ranks in entry order: rows in turn (a wave ballot per row)
-    u32 g[kU];
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-      const u64 mask = __ballot(flag[u] != 0);
-      g[u] = carry + (u32)__popcll(mask & lanelt);
-      carry += (u32)__popcll(mask);
-      const u64 j = c0 + (u64)u * kTile + tid;
-      if (j < E1 && j == l_eoff[idx[u]]) l_gstart[idx[u]] = g[u];
+      rank = e;
+      flag = c != 0;  // c == 0: a duplicate of entry e
     }
+    // kept ranks in entry order (a wave ballot per pass)
+    const u64 mask = __ballot(flag != 0);
+    const u32 g = carry + (u32)__popcll(mask & lanelt);
+    carry += (u32)__popcll(mask);
+    if (f < F && f == l_soff[idx]) l_gstart[idx] = g;
     __syncthreads();
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-      const u64 j = c0 + (u64)u * kTile + tid;
-      if (j >= E1) continue;
-      const u32 i = idx[u];
-      const u32 q = g[u] - l_gstart[i];
-      erank[j] = rank[u];
-      eqx[j] = q | (flag[u] ? kKept : 0u);
-      if (flag[u]) {
-        atomicAdd(&l_M[i], 1u);
-        atomicMin(&l_minrank[i], rank[u]);
-        atomicMax((unsigned long long*)&l_tn[i], (unsigned long long)t[u]);  // newest kept
+    u32 qx = 0;
+    if (f < F) {
+      qx = (g - l_gstart[idx]) | (flag ? kKept : 0u);
+      erank[j] = rank;
+      eqx[j] = qx;
+      if (flag) {
+        atomicAdd(&l_M[idx], 1u);
+        atomicMin(&l_minrank[idx], rank);
+        atomicMax((unsigned long long*)&l_tn[idx], (unsigned long long)t);  // newest kept
       }
     }
+#pragma unroll
+    for (int c = 0; c < kCache; c++)
+      if (c == pass) {
+        c_t[c] = t, c_p[c] = pp, c_l[c] = ll, c_q[c] = qx, c_i[c] = idx;
+      }
     __syncthreads();  // l_gstart reuse
   }
-  (void)lanelt;
-  // 3. per key decision
-  if (tid < nt) {
+  // 3. per slow key: append (meta published here), rebuild (planned) or skip
+  u32 mode = kFast;
+  PInfo P{};
+  if (blockIdx.x == 0 && tid == 0) A.rz[A.nd] = 0;
+  if (tid < nt && l_mode[tid] != kFast) {
     const u64 k = k0 + tid;
-    PInfo P;
-    P.s = A.slot[k];
+    P.k = (u32)k;
+    P.s = l_slot[tid];
     if (l_bad[tid]) {
-      P.mode = kSkip;
-      A.relsz[k] = 0;
+      mode = kSkip;
+      if (P.s != JY_NO_SLOT && A.dptr[P.s] == (u32)k) atomicAdd(A.skipped, 1ull);  // once per slot
     } else {
       const u32 len = l_len[tid], drop = l_drop[tid], M = l_M[tid];
       const u32 surv = len - drop;
@@ -351,77 +429,85 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
         const u64 tn = l_tn[tid];
         nn = (surv == 0 || tn > newest) ? tn : newest;
       }
-      P.src = l_base[tid];
       P.len = len;
       P.drop = drop;
       P.newlen = surv + M;
       P.cut = l_cut[tid];
       P.newest = nn;
       if ((M == 0 || l_minrank[tid] == len) && (u64)len + M <= l_cap[tid]) {
-        P.mode = kAppend;
-        P.cap = l_cap[tid];
-        A.relsz[k] = 0;
+        mode = kAppend;
+        A.meta[P.s] = TMeta{l_base[tid] + drop, P.newlen, l_cap[tid] - drop, P.cut, nn};
       } else {
-        P.mode = kRebuild;
+        mode = kRebuild;
         P.cap = pow2_cap(surv + M);
-        A.relsz[k] = P.cap;
+        A.pinfo[k] = P;
       }
     }
-    l_mode[tid] = P.mode;
-    A.pinfo[k] = P;
+    l_mode[tid] = mode;
   }
+  if (tid < nt) A.rz[k0 + tid] = mode == kRebuild ? P.cap : 0u;
   __syncthreads();
   // 4. appends: kept entries of append keys go to the tail, oldest first
-  for (u64 c0 = E0; c0 < E1; c0 += kTile) {
-    const u64 j = c0 + tid;
-    if (j >= E1) continue;
-    const u32 idx = lds_last_le(l_eoff, nt - 1, j);
-    const u32 qx = eqx[j];
-    if (l_mode[idx] != kAppend || !(qx & kKept)) continue;
+  pass = 0;
+  for (u64 c0 = 0; c0 < F; c0 += kTile, pass++) {
+    const u64 f = c0 + tid;
+    if (f >= F) continue;
+    u32 idx, qx;
+    u64 t, pp, ll;
+    if (pass < kCache) {
+      idx = c_i[0], qx = c_q[0], t = c_t[0], pp = c_p[0], ll = c_l[0];
+#pragma unroll
+      for (int c = 1; c < kCache; c++)
+        if (c == pass) idx = c_i[c], qx = c_q[c], t = c_t[c], pp = c_p[c], ll = c_l[c];
+      if (l_mode[idx] != kAppend || !(qx & kKept)) continue;
+    } else {
+      idx = lds_last_le(l_soff, nt - 1, f);
+      if (l_mode[idx] != kAppend) continue;
+      const u64 j = l_gb[idx] + (f - l_soff[idx]);
+      qx = eqx[j];
+      if (!(qx & kKept)) continue;
+      t = A.dts[j], pp = A.dpre[j], ll = A.dlr[j];
+    }
     const u64 tail = l_base[idx] + l_len[idx] + l_M[idx] - 1;
-    store_rec(pool + tail - (qx & ~kKept), A.dts[j], A.dpre[j], A.dlr[j]);
+    store_rec(pool + tail - (qx & ~kKept), t, pp, ll);
   }
 }
 
-// KEY TILES again, after the scan of rebuilt sizes: publish every key's meta
-// and rebuild the rebuilt keys into their fresh space, one lane per output
-// (state survivors and delta entries of the tile's rebuilt keys, flattened
-// by a block scan):
+// KEY TILES again, after the scan of rebuilt sizes: the rebuilt keys'
+// segments are written into their fresh space (tiles without one exit after
+// one load), one lane per output (state survivors and delta entries of the
+// tile's rebuilt keys, flattened by a wave scan):
 //   state entry i (i >= drop): (i - drop) + #kept deltas with rank <= i;
 //     ranks fall along the newest-first delta segment, so that is M - q of
 //     the first entry with rank <= i (binary search)
 //   kept delta entry j: (rank_j - drop) + (M - 1 - q_j)
 __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __restrict__ roff,
-                                                          const u64* __restrict__ ctr, TRec* __restrict__ pool,
-                                                          const u32* __restrict__ erank, const u32* __restrict__ eqx,
-                                                          unsigned long long* __restrict__ skipped) {
+                                                       const u64* __restrict__ ctr, TRec* __restrict__ pool,
+                                                       const u32* __restrict__ erank, const u32* __restrict__ eqx) {
   __shared__ u64 l_woff[kTile + 1];
   __shared__ u64 l_src[kTile], l_dst[kTile], l_blo[kTile], l_bhi[kTile];
   __shared__ u32 l_drop[kTile], l_surv[kTile], l_M[kTile];
   const u32 tid = threadIdx.x;
   const u64 k0 = (u64)blockIdx.x * kTile;
   const u32 nt = (u32)(A.nd - k0 < kTile ? A.nd - k0 : kTile);
+  const u32 cap = tid < nt ? A.rz[k0 + tid] : 0u;
+  if (__ballot(cap != 0) == 0) return;
   u32 w = 0;
-  if (tid < nt) {
+  if (cap) {
     const u64 k = k0 + tid;
     const PInfo P = A.pinfo[k];
-    if (P.mode == kSkip) {
-      if (P.s != JY_NO_SLOT && A.dptr[P.s] == (u32)k) atomicAdd(skipped, 1ull);  // once per slot
-    } else if (P.mode == kAppend) {
-      A.meta[P.s] = TMeta{P.src + P.drop, P.newlen, P.cap - P.drop, P.cut, P.newest};
-    } else {
-      const u64 dst = ctr[0] + roff[k];
-      A.meta[P.s] = TMeta{dst, P.newlen, P.cap, P.cut, P.newest};
-      const u64 blo = A.doff[k], bhi = A.doff[k + 1];
-      l_src[tid] = P.src;
-      l_dst[tid] = dst;
-      l_blo[tid] = blo;
-      l_bhi[tid] = bhi;
-      l_drop[tid] = P.drop;
-      l_surv[tid] = P.len - P.drop;
-      l_M[tid] = P.newlen - (P.len - P.drop);
-      w = (P.len - P.drop) + (u32)(bhi - blo);
-    }
+    const u64 src = A.meta[P.s].base;  // current (a compaction may have moved the log)
+    const u64 dst = ctr[0] + roff[k];
+    A.meta[P.s] = TMeta{dst, P.newlen, P.cap, P.cut, P.newest};
+    const u64 blo = A.doff[k], bhi = A.doff[k + 1];
+    l_src[tid] = src;
+    l_dst[tid] = dst;
+    l_blo[tid] = blo;
+    l_bhi[tid] = bhi;
+    l_drop[tid] = P.drop;
+    l_surv[tid] = P.len - P.drop;
+    l_M[tid] = P.newlen - (P.len - P.drop);
+    w = (P.len - P.drop) + (u32)(bhi - blo);
   }
   const u32 winc = jyscan::wave_incl<u32>(w);  // a key tile is one wave
   const u32 wo = winc - w, wtot = __shfl(winc, 63);
@@ -521,28 +607,63 @@ __global__ __launch_bounds__(kThreads) void k_cmp_size(const TMeta* __restrict__
     return;
   }
   const u32 n = meta[s].len;
-  sz[s] = n ? (u64)n + (n / 2 > 2 ? n / 2 : 2) : 0;  // headroom for appends
+  sz[s] = n ? (u64)n + (n > 4 ? n : 4) : 0;  // headroom for appends: as long again
   lens[s] = n;
 }
 
+// a tile of kTileOut output entries: its first and last logs found by two
+// wave searches, their offsets and segments staged in LDS (per-entry search
+// there), then the live entries copied (coalesced stores)
+constexpr u32 kCmpLds = 1024;
 __global__ __launch_bounds__(kThreads) void k_cmp_copy(const TMeta* __restrict__ meta, u64 nk,
                                                        const u64* __restrict__ roff, const TRec* __restrict__ src,
                                                        TRec* __restrict__ dst) {
+  __shared__ u64 l_off[kCmpLds + 1], l_base[kCmpLds];
+  __shared__ u32 l_len[kCmpLds];
+  __shared__ u64 sh[2];
   const u64 total = roff[nk];
   const u64 t0 = (u64)blockIdx.x * kTileOut;
   if (t0 >= total) return;
   const u64 t1 = t0 + kTileOut < total ? t0 + kTileOut : total;
-  for (u64 t = t0 + threadIdx.x; t < t1; t += kThreads) {
-    u64 lo = 0, hi = nk;
-    while (lo < hi) {
-      const u64 m = (lo + hi + 1) >> 1;
-      if (roff[m] <= t) lo = m;
-      else hi = m - 1;
+  if (threadIdx.x < 128) {
+    const u64 k = jyscan::wave_last_le(roff, nk, threadIdx.x < 64 ? t0 : t1 - 1);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = k;
+  }
+  __syncthreads();
+  const u64 k0 = sh[0], cnt = sh[1] - sh[0] + 1;
+  const bool lds = cnt <= kCmpLds;
+  if (lds) {
+    for (u64 j = threadIdx.x; j < cnt; j += kThreads) {
+      const TMeta m = meta[k0 + j];
+      l_off[j] = roff[k0 + j];
+      l_base[j] = m.base;
+      l_len[j] = m.len;
     }
-    const u64 r = t - roff[lo];
-    const TMeta m = meta[lo];
-    if (r >= m.len) continue;
-    const TRec x = load_rec(src + m.base + r);
+  }
+  __syncthreads();
+  for (u64 t = t0 + threadIdx.x; t < t1; t += kThreads) {
+    u64 base, r;
+    u32 len;
+    if (lds) {
+      u32 lo = 0, hi = (u32)cnt - 1;
+      while (lo < hi) {
+        const u32 m = (lo + hi + 1) >> 1;
+        if (l_off[m] <= t) lo = m;
+        else hi = m - 1;
+      }
+      base = l_base[lo], len = l_len[lo], r = t - l_off[lo];
+    } else {
+      u64 lo = k0, hi = k0 + cnt - 1;
+      while (lo < hi) {
+        const u64 m = (lo + hi + 1) >> 1;
+        if (roff[m] <= t) lo = m;
+        else hi = m - 1;
+      }
+      const TMeta m = meta[lo];
+      base = m.base, len = m.len, r = t - roff[lo];
+    }
+    if (r >= len) continue;  // headroom
+    const TRec x = load_rec(src + base + r);
     store_rec(dst + t, x.ts, x.pre, x.lr);
   }
 }
@@ -712,7 +833,7 @@ int32_t tlog_compact(jy_engine* eng, TlogState& t, u64 room) {
   const u64 nk = eng->nkeys[JY_TLOG];
   const double t_enter = jy_tracing() ? jy_now_us() : 0;
   void* p;
-  JY_TRY(jy_scratch(eng, 16, (nk + 1) * 32, &p));
+  JY_TRY(jy_scratch(eng, 17, (nk + 1) * 32, &p));
   u64* sz = static_cast<u64*>(p);
   u64* roff = sz + nk + 1;
   u64* lens = roff + nk + 1;
@@ -725,7 +846,7 @@ int32_t tlog_compact(jy_engine* eng, TlogState& t, u64 room) {
   JY_HIP(eng, hipStreamSynchronize(eng->stream));
   const u64 total = t.pin[0], live = t.pin[1];
   // the next merges' worst case fits several times over before the next sync
-  const u64 ncap = std::max<u64>({total + room, 2 * total, eng->cfg.entry_capacity[JY_TLOG], 1024});
+  const u64 ncap = std::max<u64>({total + room, 3 * total, eng->cfg.entry_capacity[JY_TLOG], 1024});
   TRec* np = nullptr;
   JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&np), ncap * sizeof(TRec), "tlog pool"));
   if (total) {
@@ -804,8 +925,8 @@ int32_t jy_tlog_merge_into(jy_engine* eng, TlogState& t, u64 nd, const u32* slot
   const u64 nk = eng->nkeys[JY_TLOG];
   if (nd == 0 || nk == 0) return JY_OK;
   // worst case of fresh pool space this merge takes: every touched log
-  // rebuilt into pow2_cap(new length) <= 4 * length + 8 entries
-  const u64 need = 4 * (t.live_bound + nent) + 8 * nd + 64;
+  // rebuilt into pow2_cap(new length) <= 2 * kGrow * (length + 1) entries
+  const u64 need = 2 * kGrow * (t.live_bound + nent + nd) + 64;
   if (t.known && hipEventQuery(t.ready) == hipSuccess) t.used_bound = *t.pin;
 
   TlogArgs A{};
@@ -817,52 +938,50 @@ int32_t jy_tlog_merge_into(jy_engine* eng, TlogState& t, u64 nd, const u32* slot
   A.dts = dts;
   A.dpre = dpre;
   A.dlr = dlr;
+  A.skipped = reinterpret_cast<unsigned long long*>(eng->skipped_dev);
   void* p;
   JY_TRY(jy_scratch(eng, 8, nk * 4, &p));
   A.dptr = static_cast<u32*>(p);
-  JY_TRY(jy_scratch(eng, 9, nd * (sizeof(PInfo) + 4) + 64, &p));
+  JY_TRY(jy_scratch(eng, 9, nd * (sizeof(PInfo) + 8) + 64, &p));
   A.pinfo = static_cast<PInfo*>(p);
   A.bad = reinterpret_cast<u32*>(A.pinfo + nd);
+  A.rz = A.bad + nd;
+  JY_TRY(jy_scratch(eng, 16, (nd + 1) * 8, &p));
+  u64* roff = static_cast<u64*>(p);
   JY_TRY(jy_scratch(eng, 12, std::max<u64>(nent, 1) * 8, &p));
   u32* erank = static_cast<u32*>(p);
   u32* eqx = erank + std::max<u64>(nent, 1);
   const u32 tiles = (u32)((nd + kTile - 1) / kTile);
-  u64* roff = nullptr;
   JY_HIP(eng, hipMemsetAsync(A.dptr, 0xFF, nk * 4, eng->stream));
   JY_HIP(eng, hipMemsetAsync(A.bad, 0, nd * 4, eng->stream));
   LAUNCH(k_tlog_prep, nd, A);
-  for (int attempt = 0;; attempt++) {
-    A.meta = t.meta;
-    A.pool = t.pool;
-    JY_TRY(jy_scratch(eng, 16, (nd + 1) * 16, &p));
-    A.relsz = static_cast<u64*>(p);
-    roff = A.relsz + nd + 1;
-    hipLaunchKernelGGL(k_tlog_tile, dim3(tiles), dim3(kTile), 0, eng->stream, A, t.pool, erank, eqx);
-    JY_HIP(eng, hipGetLastError());
-    JY_TRY(scan_excl_u64(eng, A.relsz, roff, nd + 1));
-    if (t.used_bound + need <= t.pcap) {
-      t.used_bound += need;
-      break;
-    }
-    // the worst case may not fit: wait for the exact rebuild size (nothing
-    // is published yet, so a compaction can still move every log)
+  A.meta = t.meta;
+  A.pool = t.pool;
+  hipLaunchKernelGGL(k_tlog_tile, dim3(tiles), dim3(kTile), 0, eng->stream, A, t.pool, erank, eqx);
+  JY_HIP(eng, hipGetLastError());
+  JY_TRY((jydscan::scan<jydscan::OpSum, false>(eng, nd + 1, jydscan::LdArr<u32>{A.rz}, jydscan::StArr<u64>{roff})));
+  if (t.used_bound + need <= t.pcap) {
+    t.used_bound += need;
+  } else {
+    // the worst case may not fit: wait for the exact rebuild size.  Appends
+    // are published already; the rebuilt keys' logs are still in place, and
+    // k_tlog_commit reads their bases after any compaction (which uses
+    // scratch 17 and up, not this merge's).
     JY_HIP(eng, hipMemcpyAsync(t.pin + 2, roff + nd, 8, hipMemcpyDeviceToHost, eng->stream));
     JY_HIP(eng, hipMemcpyAsync(t.pin, t.ctr, 8, hipMemcpyDeviceToHost, eng->stream));
     JY_HIP(eng, hipStreamSynchronize(eng->stream));
-    t.used_bound = t.pin[0];
     const u64 rebuilt = t.pin[2];
-    if (t.used_bound + rebuilt <= t.pcap) {
-      t.used_bound += rebuilt;
-      break;
+    t.used_bound = t.pin[0];
+    if (t.used_bound + rebuilt > t.pcap) {
+      // room for this merge's rebuilds several times over
+      JY_TRY(tlog_compact(eng, t, 4 * (rebuilt + nent)));
+      if (t.used_bound + rebuilt > t.pcap) return eng->fail(JY_ENOMEM, "tlog pool: no room after compaction");
+      A.pool = t.pool;
     }
-    if (attempt == 2) return eng->fail(JY_ENOMEM, "tlog pool: no room after compaction");
-    // room for this merge's rebuilds several times over; the last attempt
-    // takes the worst case
-    JY_TRY(tlog_compact(eng, t, attempt == 0 ? 4 * (rebuilt + nent) : need));
+    t.used_bound += rebuilt;
   }
   t.live_bound += nent;
-  hipLaunchKernelGGL(k_tlog_commit, dim3(tiles), dim3(kTile), 0, eng->stream, A, roff, t.ctr, t.pool, erank,
-                     eqx, reinterpret_cast<unsigned long long*>(eng->skipped_dev));
+  hipLaunchKernelGGL(k_tlog_commit, dim3(tiles), dim3(kTile), 0, eng->stream, A, roff, t.ctr, t.pool, erank, eqx);
   JY_HIP(eng, hipGetLastError());
   hipLaunchKernelGGL(k_tlog_bump, dim3(1), dim3(1), 0, eng->stream, t.ctr, roff, nd);
   JY_HIP(eng, hipGetLastError());
