@@ -285,10 +285,11 @@ int32_t jy_ujson_stats(jy_engine* eng, uint64_t* out8);
  * Sender: jy_treg_route_part partitions n ingested TREG entries (owner
  * shard, slot on the owner, ts, pre, lr) into nshards runs:
  *   recs_dev  u64[nshards][cap][4] {slot, ts, pre, lr'}, 16-B aligned; lr' of a
- *             value > 8 bytes addresses the run's own bytes
- *   bytes_dev u8[nshards][cap_byte]
- *   hdr_dev   u64[nshards][2]: records / value bytes reserved per destination
- *             (ZERO on entry; may end above the capacities)
+ *             value > 8 bytes addresses the run's own bytes (8-byte granules)
+ *   bytes_dev u8[nshards][cap_byte], cap_byte a multiple of 8
+ *   hdr_dev   u64[nshards][2]: records / value bytes placed per destination
+ *             (written by the call); entries keep their input order in a run
+ *             and the placed ones are a prefix of each destination's sequence
  *   ovf_dev   u32[1 + n]: [0] = entries that did not fit (ZERO on entry), then
  *             their input indices -- the caller sends those in a later round.
  * Receiver: jy_treg_converge_routed merges nsrc received runs (the same

@@ -20,132 +20,152 @@
 #include <algorithm>
 
 #include "jy_internal.hpp"
+#include "jy_scan.hpp"
 
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kPer = 8;  // entries per lane: one tile of 2048 entries per workgroup
-constexpr u64 kTile = (u64)kThreads * kPer;
 constexpr u32 kMaxShards = 64;
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u64 round_up8(u64 x) { return (x + kArenaAlign - 1) & ~(kArenaAlign - 1); }
 
-// Per-owner counts without same-address atomics per lane: a wave walks the
-// distinct owners among its lanes (one ballot each), and its leader adds the
-// wave's count and long-value bytes to the workgroup's LDS counters once.
-// `rank`/`brank` (scatter only) receive each lane's position inside the
-// workgroup's run for its owner.  All lanes of the wave call this together.
-template <bool kRanks>
-__device__ __forceinline__ void wave_aggregate(bool valid, u32 o, u32 blen, unsigned long long* lrec,
-                                               unsigned long long* lbyte, u64* rank, u64* brank) {
-  const int lane = __lane_id();
+// Three passes, no same-address global atomics (one reservation atomic per
+// workgroup and owner serialised ~4k workgroups on one header word):
+//   k_rt_count  per tile of 256 entries: records and long-value bytes per owner
+//   k_rt_tscan  per (owner, quantity): exclusive scan over the tiles; the
+//               grand totals go to the header
+//   k_rt_place  per entry: its place in its owner's run = tile base + the
+//               waves before it + its rank among its wave's entries for the
+//               same owner (one ballot per distinct owner, masked scans);
+//               an entry that fits is written, else listed in ovf -- and the
+//               first entry of an owner that does not fit writes the header
+//               (the placed entries are the prefix before it: the ends grow
+//               along an owner's sequence)
+constexpr int kT = 256;  // entries per tile, one per thread
+
+__global__ __launch_bounds__(kT) void k_rt_count(const u32* __restrict__ owner, const u64* __restrict__ lr, u64 n,
+                                                 u32 S, u64* __restrict__ tcnt) {
+  __shared__ unsigned long long lc[kMaxShards * 2];
+  for (u32 j = threadIdx.x; j < S * 2; j += kT) lc[j] = 0;
+  __syncthreads();
+  const u64 i = (u64)blockIdx.x * kT + threadIdx.x;
+  if (i < n) {
+    const u32 o = owner[i];
+    if (o < S) {
+      const u64 len = lr[i] & JY_LR_LEN_MASK;
+      atomicAdd(&lc[o * 2], 1ull);
+      if (len > 8) atomicAdd(&lc[o * 2 + 1], (unsigned long long)round_up8(len));
+    }
+  }
+  __syncthreads();
+  u64* row = tcnt + (u64)blockIdx.x * S * 2;
+  for (u32 j = threadIdx.x; j < S * 2; j += kT) row[j] = lc[j];
+}
+
+constexpr int kScanT = 1024, kScanPer = 4;  // a tile-count column per workgroup: 4096 tiles per round
+__global__ __launch_bounds__(kScanT) void k_rt_tscan(u64* __restrict__ tcnt, u64 ntiles,
+                                                     unsigned long long* __restrict__ hdr) {
+  __shared__ u64 red[kScanT / 64];
+  const u32 col = blockIdx.x, width = gridDim.x;
+  u64 carry = 0;
+  for (u64 t0 = 0; t0 < ntiles; t0 += kScanT * kScanPer) {
+    u64 v[kScanPer], sum = 0;
+#pragma unroll
+    for (int u = 0; u < kScanPer; u++) {
+      const u64 t = t0 + (u64)threadIdx.x * kScanPer + u;
+      v[u] = t < ntiles ? tcnt[t * width + col] : 0;
+      sum += v[u];
+    }
+    u64 tot;
+    u64 x = jyscan::block_excl<kScanT, u64>(sum, red, tot) + carry;
+#pragma unroll
+    for (int u = 0; u < kScanPer; u++) {
+      const u64 t = t0 + (u64)threadIdx.x * kScanPer + u;
+      if (t < ntiles) tcnt[t * width + col] = x;
+      x += v[u];
+    }
+    carry += tot;
+  }
+  if (threadIdx.x == 0) hdr[col] = carry;  // hdr[2d] records, hdr[2d + 1] bytes
+}
+
+__global__ __launch_bounds__(kT) void k_rt_place(const u32* __restrict__ owner, const u32* __restrict__ slot,
+                                                 const u64* __restrict__ ts, const u64* __restrict__ pre,
+                                                 const u64* __restrict__ lr, const uint8_t* __restrict__ arena, u64 n,
+                                                 u32 S, u64 cap, u64 cap_byte, const u64* __restrict__ tcnt,
+                                                 unsigned long long* __restrict__ hdr, u64* __restrict__ recs,
+                                                 uint8_t* __restrict__ bytes, u32* __restrict__ ovf,
+                                                 unsigned long long* __restrict__ skipped) {
+  constexpr int kW = kT / 64;
+  __shared__ u64 wt[kW][kMaxShards * 2];
+  for (u32 j = threadIdx.x; j < S * 2; j += kT) {
+#pragma unroll
+    for (int w = 0; w < kW; w++) wt[w][j] = 0;
+  }
+  __syncthreads();
+  const u64 i = (u64)blockIdx.x * kT + threadIdx.x;
+  const int lane = __lane_id(), wv = threadIdx.x >> 6;
   const u64 lt = (1ull << lane) - 1;
+  u32 o = 0xFFFFFFFFu, sl = 0;
+  u64 t = 0, p = 0, l = 0, b = 0;
+  if (i < n) {
+    o = owner[i];
+    sl = slot[i];
+    t = ts[i];
+    p = pre[i];
+    l = lr[i];
+    const u64 len = l & JY_LR_LEN_MASK;
+    b = len > 8 ? round_up8(len) : 0;
+  }
+  const bool valid = i < n && o < S;
+  if (i < n && !valid) atomicAdd(skipped, 1ull);  // an owner outside [0, S): dropped, counted
+  u64 rk = 0, bk = 0;
   u64 pending = __ballot(valid);
   while (pending) {
     const int leader = __ffsll((unsigned long long)pending) - 1;
     const u32 d = __shfl(o, leader);
     const bool mine = valid && o == d;
     const u64 m = __ballot(mine);
-    // inclusive scan of the long-value bytes of this owner's lanes (a value
-    // is < 2^24 bytes, so a wave's sum fits 32 bits); skipped when none is long
-    u32 x = mine ? blen : 0;
-    u32 bsum = 0;
-    if (__ballot(x != 0)) {
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const u32 y = __shfl_up(x, off);
-        if (lane >= off) x += y;
-      }
-      bsum = __shfl(x, 63);
+    const u64 x = mine ? b : 0;
+    const u64 inc = jyscan::wave_incl<u64>(x);
+    if (mine) {
+      rk = __popcll(m & lt);
+      bk = inc - x;
     }
-    unsigned long long rb = 0, bb = 0;
+    const u64 tot = __shfl(inc, 63);
     if (lane == leader) {
-      rb = atomicAdd(&lrec[d], (unsigned long long)__popcll(m));
-      if (bsum) bb = atomicAdd(&lbyte[d], (unsigned long long)bsum);
-    }
-    if (kRanks) {
-      rb = __shfl(rb, leader);
-      bb = __shfl(bb, leader);
-      if (mine) {
-        *rank = rb + __popcll(m & lt);
-        *brank = bb + x - blen;
-      }
+      wt[wv][d * 2] = __popcll(m);
+      wt[wv][d * 2 + 1] = tot;
     }
     pending &= ~m;
   }
-}
-
-// One pass: per-owner ranks inside the workgroup (wave_aggregate), one
-// global reservation per (workgroup, owner) on the header cursors, then
-// every entry that fits its owner's run is written there.  An entry past
-// the run's record capacity, or whose long value would pass the run's byte
-// capacity, is listed in ovf (input index) -- a record slot it took is left
-// as a hole (slot ~0) the receiver skips.  hdr[2d] / hdr[2d + 1] end as the
-// records / bytes reserved for owner d, which may pass the capacities; the
-// receiver clamps.
-__global__ __launch_bounds__(kThreads) void k_route_part_treg(
-    const u32* __restrict__ owner, const u32* __restrict__ slot, const u64* __restrict__ ts,
-    const u64* __restrict__ pre, const u64* __restrict__ lr, const uint8_t* __restrict__ arena, u64 n, u32 S, u64 cap,
-    u64 cap_byte, unsigned long long* __restrict__ hdr, u64* __restrict__ recs, uint8_t* __restrict__ bytes,
-    u32* __restrict__ ovf) {
-  __shared__ unsigned long long lrec[kMaxShards], lbyte[kMaxShards], grec[kMaxShards], gbyte[kMaxShards];
-  for (u32 d = threadIdx.x; d < S; d += kThreads) lrec[d] = lbyte[d] = 0;
   __syncthreads();
-  const u64 base = (u64)blockIdx.x * kTile + threadIdx.x;
-  u32 o[kPer], sl[kPer];
-  u64 l[kPer], t[kPer], p[kPer], rk[kPer], brk[kPer];
-#pragma unroll
-  for (int u = 0; u < kPer; u++) {  // every load in flight before the first ballot
-    const u64 i = base + (u64)u * kThreads;
-    const bool valid = i < n;
-    o[u] = valid ? owner[i] : 0;
-    l[u] = valid ? lr[i] : 0;
-    sl[u] = valid ? slot[i] : 0;
-    t[u] = valid ? ts[i] : 0;
-    p[u] = valid ? pre[i] : 0;
+  if (!valid) return;
+  const u64* tb = tcnt + (u64)blockIdx.x * S * 2 + o * 2;
+  u64 pos = tb[0] + rk, bpos = tb[1] + bk;
+  for (int w = 0; w < wv; w++) {
+    pos += wt[w][o * 2];
+    bpos += wt[w][o * 2 + 1];
   }
-#pragma unroll
-  for (int u = 0; u < kPer; u++) {
-    const u64 len = l[u] & JY_LR_LEN_MASK;
-    rk[u] = brk[u] = 0;
-    // long values keep the arena's 8-byte granules (jy_arena_collect)
-    wave_aggregate<true>(base + (u64)u * kThreads < n, o[u], len > 8 ? (u32)round_up8(len) : 0u, lrec, lbyte, &rk[u],
-                         &brk[u]);
-  }
-  __syncthreads();
-  for (u32 d = threadIdx.x; d < S; d += kThreads) {
-    grec[d] = lrec[d] ? atomicAdd(&hdr[2 * d], lrec[d]) : 0;
-    gbyte[d] = lbyte[d] ? atomicAdd(&hdr[2 * d + 1], lbyte[d]) : 0;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int u = 0; u < kPer; u++) {
-    const u64 i = base + (u64)u * kThreads;
-    if (i >= n) continue;
-    const u64 pos = grec[o[u]] + rk[u];
-    const u64 len = l[u] & JY_LR_LEN_MASK;
-    const u64 bpos = gbyte[o[u]] + brk[u];
-    const bool long_v = len > 8;
-    const bool fits = pos < cap && (!long_v || bpos + round_up8(len) <= cap_byte);
-    u64x2* r = reinterpret_cast<u64x2*>(recs + ((u64)o[u] * cap + pos) * 4);  // 32-B records, two 16-B stores
-    if (!fits) {
-      ovf[1 + atomicAdd(ovf, 1u)] = (u32)i;
-      if (pos < cap) r[0] = u64x2{~0ull, 0};  // hole
-      continue;
+  const bool fits = pos < cap && bpos + b <= cap_byte;
+  if (!fits) {
+    ovf[1 + atomicAdd(ovf, 1u)] = (u32)i;
+    if (pos == 0 || (pos - 1 < cap && bpos <= cap_byte)) {  // the first of its owner that does not fit
+      hdr[2 * o] = pos;
+      hdr[2 * o + 1] = bpos;
     }
-    u64 out_lr = l[u];
-    if (long_v) {
-      uint8_t* dst = bytes + (u64)o[u] * cap_byte + bpos;
-      const uint8_t* src = arena + (l[u] >> JY_LR_LEN_BITS);
-      for (u64 j = 0; j < len; j++) dst[j] = src[j];
-      out_lr = (bpos << JY_LR_LEN_BITS) | len;
-    }
-    r[0] = u64x2{(u64)sl[u], t[u]};
-    r[1] = u64x2{p[u], out_lr};
+    return;
   }
+  u64 out_lr = l;
+  if (b) {  // the value's 8-B granules into the run's byte section
+    const u64* src = reinterpret_cast<const u64*>(arena + (l >> JY_LR_LEN_BITS));
+    u64* dst = reinterpret_cast<u64*>(bytes + (u64)o * cap_byte + bpos);
+    for (u64 w = 0; w < b / 8; w++) dst[w] = src[w];
+    out_lr = (bpos << JY_LR_LEN_BITS) | (l & JY_LR_LEN_MASK);
+  }
+  u64x2* r = reinterpret_cast<u64x2*>(recs + ((u64)o * cap + pos) * 4);  // 32-B records, two 16-B stores
+  r[0] = u64x2{(u64)sl, t};
+  r[1] = u64x2{p, out_lr};
 }
-
-u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kTile - 1) / kTile); }
 
 }  // namespace
 
@@ -161,7 +181,10 @@ int32_t jy_treg_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, co
                            uint32_t* ovf_dev) {
   JY_HIP(eng, hipSetDevice(eng->device));
   if (nshards == 0 || nshards > kMaxShards) return eng->fail(JY_ERANGE, "nshards must be in [1, 64]");
-  if (n == 0) return JY_OK;
+  if (n == 0) {
+    JY_HIP(eng, hipMemsetAsync(hdr_dev, 0, (u64)nshards * 16, eng->stream));
+    return JY_OK;
+  }
   if (n >= 0xFFFFFFFFull) return eng->fail(JY_ERANGE, "more than 2^32 - 1 entries in one call");
   if (reinterpret_cast<uintptr_t>(recs_dev) % 16) return eng->fail(JY_EINVAL, "recs_dev must be 16-B aligned");
   if (cap_byte % kArenaAlign) return eng->fail(JY_EINVAL, "cap_byte must be a multiple of 8");
@@ -176,10 +199,21 @@ int32_t jy_treg_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, co
   JY_TRY(jy_stage(eng, 3, pre, n * 8, mem, &dpre));
   JY_TRY(jy_stage(eng, 4, lr, n * 8, mem, &dlr));
   JY_TRY(jy_stage_end(eng));
-  hipLaunchKernelGGL(k_route_part_treg, dim3(blocks_for(n)), dim3(kThreads), 0, eng->stream,
-                     static_cast<const u32*>(dow), static_cast<const u32*>(dsl), static_cast<const u64*>(dts),
-                     static_cast<const u64*>(dpre), static_cast<const u64*>(dlr), eng->arena[JY_TREG].p, n, nshards,
-                     cap, cap_byte, reinterpret_cast<unsigned long long*>(hdr_dev), recs_dev, bytes_dev, ovf_dev);
+  const u64 ntiles = (n + kT - 1) / kT;
+  void* p;
+  JY_TRY(jy_scratch(eng, 24, ntiles * nshards * 2 * 8 + 64, &p));
+  u64* tcnt = static_cast<u64*>(p);
+  const u32* own = static_cast<const u32*>(dow);
+  const u64* l = static_cast<const u64*>(dlr);
+  hipLaunchKernelGGL(k_rt_count, dim3((u32)ntiles), dim3(kT), 0, eng->stream, own, l, n, nshards, tcnt);
+  JY_HIP(eng, hipGetLastError());
+  hipLaunchKernelGGL(k_rt_tscan, dim3(nshards * 2), dim3(kScanT), 0, eng->stream, tcnt, ntiles,
+                     reinterpret_cast<unsigned long long*>(hdr_dev));
+  JY_HIP(eng, hipGetLastError());
+  hipLaunchKernelGGL(k_rt_place, dim3((u32)ntiles), dim3(kT), 0, eng->stream, own, static_cast<const u32*>(dsl),
+                     static_cast<const u64*>(dts), static_cast<const u64*>(dpre), l, eng->arena[JY_TREG].p, n, nshards,
+                     cap, cap_byte, tcnt, reinterpret_cast<unsigned long long*>(hdr_dev), recs_dev, bytes_dev, ovf_dev,
+                     reinterpret_cast<unsigned long long*>(eng->skipped_dev));
   JY_HIP(eng, hipGetLastError());
   return JY_OK;
 }

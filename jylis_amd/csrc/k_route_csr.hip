@@ -21,8 +21,9 @@
 //                   CSR, long-value bytes)
 //   R2 k_rc_tscan   per (destination, quantity): exclusive scan over tiles
 //   R3 k_rc_place   per key: its place in its destination's run (tile base
-//                   + wave ranks), fit test, key records, long-value bytes
-//   R4 k_rc_copy    per entry: the entry columns into the key's run range
+//                   + wave ranks), fit test, key records
+//   R4 k_rc_copy    per entry: the entry columns into the key's run range,
+//                   long values' bytes into the run's byte section
 //   R5 k_rc_finish  holes after each run's placed keys
 // Receiver: TLOG value handles are rebased onto the arena (k_rc_rebase) and
 // each source's run is merged by the type's own converge kernels, one source
@@ -81,8 +82,9 @@ struct RouteArgs {
   unsigned long long* skipped;
   u64* tcnt;  // [ntiles][S][kQ]
   u64* kb;    // [n] long-value bytes of the key (padded)
+  u32* eb;    // [entries of CSR 0] a long value's byte offset inside its key's bytes
   u32* kdst;  // [n] destination, or kNone
-  u64* keo;   // [n][kC] first entry of the key in its run
+  u64* keo;   // [n][kC (+1)] first entry of the key in its run per CSR (+ its first value byte)
 };
 
 // layout of one run in u64 words: slots (u32, packed), [per-key scalars],
@@ -132,7 +134,10 @@ __global__ __launch_bounds__(kThreads) void k_rc_count(RouteArgs<kC> A) {
       u64 b = 0;
       for (u64 j = A.c[0].offs[k]; j < A.c[0].offs[k + 1]; j++) {
         const u64 len = lr[j] & JY_LR_LEN_MASK;
-        if (len > 8) b += round8(len);
+        if (len > 8) {
+          A.eb[j] = (u32)b;
+          b += round8(len);
+        }
       }
       A.kb[k] = b;
     }
@@ -149,19 +154,34 @@ __global__ __launch_bounds__(kThreads) void k_rc_count(RouteArgs<kC> A) {
   for (u32 j = threadIdx.x; j < A.S * kQ; j += kThreads) row[j] = lc[j];
 }
 
-// R2: one workgroup per (destination, quantity): exclusive scan over tiles
-__global__ __launch_bounds__(kThreads) void k_rc_tscan(u64* __restrict__ tcnt, u64 ntiles, u32 width) {
-  __shared__ u64 red[kThreads / 64];
-  const u32 col = blockIdx.x;
+// R2: one workgroup per (destination, quantity): exclusive scan over tiles;
+// the grand total goes to the header (every key placed, unless R3's first
+// key that does not fit overwrites it with the placed prefix)
+constexpr int kScanT = 1024, kScanPer = 4;  // a tile-count column per workgroup: 4096 tiles per round
+__global__ __launch_bounds__(kScanT) void k_rc_tscan(u64* __restrict__ tcnt, u64 ntiles, u32 kq,
+                                                     unsigned long long* __restrict__ hdr) {
+  __shared__ u64 red[kScanT / 64];
+  const u32 col = blockIdx.x, width = gridDim.x;
   u64 carry = 0;
-  for (u64 t0 = 0; t0 < ntiles; t0 += kThreads) {
-    const u64 t = t0 + threadIdx.x;
-    const u64 v = t < ntiles ? tcnt[t * width + col] : 0;
+  for (u64 t0 = 0; t0 < ntiles; t0 += kScanT * kScanPer) {
+    u64 v[kScanPer], sum = 0;
+#pragma unroll
+    for (int u = 0; u < kScanPer; u++) {
+      const u64 t = t0 + (u64)threadIdx.x * kScanPer + u;
+      v[u] = t < ntiles ? tcnt[t * width + col] : 0;
+      sum += v[u];
+    }
     u64 tot;
-    const u64 x = jyscan::block_excl<kThreads, u64>(v, red, tot);
-    if (t < ntiles) tcnt[t * width + col] = carry + x;
+    u64 x = jyscan::block_excl<kScanT, u64>(sum, red, tot) + carry;
+#pragma unroll
+    for (int u = 0; u < kScanPer; u++) {
+      const u64 t = t0 + (u64)threadIdx.x * kScanPer + u;
+      if (t < ntiles) tcnt[t * width + col] = x;
+      x += v[u];
+    }
     carry += tot;
   }
+  if (threadIdx.x == 0) hdr[(col / kq) * 8 + col % kq] = carry;
 }
 
 // R3: the key's place in its run: tile base (R2) + the waves before it + its
@@ -172,9 +192,7 @@ __global__ __launch_bounds__(kThreads) void k_rc_place(RouteArgs<kC> A) {
   constexpr int kQ = 1 + kC + (kLR ? 1 : 0);
   constexpr int kW = kThreads / 64;
   __shared__ u64 wt[kW][kMaxShards * kQ];
-  __shared__ unsigned long long tmax[kMaxShards * kQ];
   for (u32 j = threadIdx.x; j < A.S * kQ; j += kThreads) {
-    tmax[j] = 0;
 #pragma unroll
     for (int w = 0; w < kW; w++) wt[w][j] = 0;
   }
@@ -230,39 +248,31 @@ __global__ __launch_bounds__(kThreads) void k_rc_place(RouteArgs<kC> A) {
     if (!fits) {
       A.kdst[k] = kNone;
       A.ovf[1 + atomicAdd(A.ovf, 1u)] = (u32)(A.kbase + k);
+      // the first key of its destination that does not fit (the one before
+      // it, whose ends are this key's starts, fits) writes the run's header:
+      // the placed keys are exactly the prefix before it (no atomics)
+      bool prev = at[0] > 0 && at[0] - 1 < A.kfit;
+#pragma unroll
+      for (int c = 0; c < kC; c++) prev = prev && at[1 + c] <= A.c[c].cap;
+      if (kLR) prev = prev && at[1 + kC] <= A.cap_b;
+      if (at[0] == 0 || prev) {
+#pragma unroll
+        for (int q = 0; q < kQ; q++) A.hdr[o * 8 + q] = at[q];
+      }
     } else {
       u64* R = A.out + (u64)o * A.W;
       reinterpret_cast<u32*>(R + A.o_slot)[at[0]] = A.slot[k];
       if (A.kx) R[A.o_kx + at[0]] = A.kx[k];
+      constexpr int kE = kC + (kLR ? 1 : 0);
 #pragma unroll
       for (int c = 0; c < kC; c++) {
         R[A.c[c].o_offs + at[0] + 1] = at[1 + c] + v[1 + c];
-        A.keo[k * kC + c] = at[1 + c];
+        A.keo[k * kE + c] = at[1 + c];
       }
+      if (kLR) A.keo[k * kE + kC] = at[1 + kC];  // the key's values start here in the byte section
       A.kdst[k] = o;
-      if (kLR && v[1 + kC]) {  // long values: bytes into the run's byte section, handles rewritten
-        const u64* lr = A.c[0].col[A.lr];
-        u64* lro = R + A.c[0].o_col[A.lr];
-        uint8_t* B = A.bytes + (u64)o * A.cap_b;
-        u64 b = at[1 + kC];
-        const u64 j0 = A.c[0].offs[k];
-        for (u64 j = j0; j < A.c[0].offs[k + 1]; j++) {
-          const u64 h = lr[j], len = h & JY_LR_LEN_MASK;
-          if (len <= 8) continue;
-          const u64* src = reinterpret_cast<const u64*>(A.arena + (h >> JY_LR_LEN_BITS));  // 8-B granules
-          u64* dst = reinterpret_cast<u64*>(B + b);
-          for (u64 w = 0; w < round8(len) / 8; w++) dst[w] = src[w];
-          lro[at[1] + (j - j0)] = (b << JY_LR_LEN_BITS) | len;
-          b += round8(len);
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < kQ; q++) atomicMax(&tmax[o * kQ + q], (unsigned long long)(at[q] + v[q]));
     }
   }
-  __syncthreads();
-  for (u32 j = threadIdx.x; j < A.S * kQ; j += kThreads)
-    if (tmax[j]) atomicMax(&A.hdr[(j / kQ) * 8 + (j % kQ)], tmax[j]);
 }
 
 // R4: entry columns; a tile of entries of one CSR finds its keys with two
@@ -271,7 +281,11 @@ __global__ __launch_bounds__(kThreads) void k_rc_place(RouteArgs<kC> A) {
 // host's bound, surplus tiles exit
 template <int kC, bool kLR>
 __global__ __launch_bounds__(kThreads) void k_rc_copy(RouteArgs<kC> A, u64 t1, u64 t2) {
+  constexpr u32 kLds = kThreads;  // keys a tile stages (a tile of entries spans at most 256 non-empty keys)
+  constexpr int kE = kC + (kLR ? 1 : 0);
   __shared__ u64 sh[2];
+  __shared__ u64 l_off[kLds + 1], l_at[kLds], l_bb[kLds];
+  __shared__ u32 l_d[kLds];
   u64 t = blockIdx.x;
   const int c = t < t1 ? 0 : t < t2 ? 1 : 2;
   if (c >= kC) return;
@@ -287,23 +301,56 @@ __global__ __launch_bounds__(kThreads) void k_rc_copy(RouteArgs<kC> A, u64 t1, u
     if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = kk;
   }
   __syncthreads();
+  const u64 k0 = sh[0], cnt = sh[1] - sh[0] + 1;
+  const bool lds = cnt <= kLds;  // empty keys between them can make it more
+  if (lds && threadIdx.x < cnt) {  // the tile's keys: offsets, destination, first entry in the run
+    const u64 k = k0 + threadIdx.x;
+    l_off[threadIdx.x] = C.offs[k];
+    l_d[threadIdx.x] = A.kdst[k];
+    l_at[threadIdx.x] = A.keo[k * kE + c];
+    if (kLR && c == 0) l_bb[threadIdx.x] = A.keo[k * kE + kC];
+  }
+  __syncthreads();
   const u64 j = j0 + threadIdx.x;
   if (j >= j1) return;
-  u64 lo = sh[0], hi = sh[1];
-  while (lo < hi) {
-    const u64 m = (lo + hi + 1) >> 1;
-    if (C.offs[m] <= j) lo = m;
-    else hi = m - 1;
+  u64 lo, off;
+  u32 d;
+  u64 at0, bb = 0;
+  if (lds) {
+    u32 a = 0, h = (u32)cnt - 1;
+    while (a < h) {
+      const u32 m = (a + h + 1) >> 1;
+      if (l_off[m] <= j) a = m;
+      else h = m - 1;
+    }
+    off = l_off[a], d = l_d[a], at0 = l_at[a];
+    if (kLR && c == 0) bb = l_bb[a];
+  } else {
+    lo = k0;
+    u64 hi = sh[1];
+    while (lo < hi) {
+      const u64 m = (lo + hi + 1) >> 1;
+      if (C.offs[m] <= j) lo = m;
+      else hi = m - 1;
+    }
+    off = C.offs[lo], d = A.kdst[lo], at0 = d == kNone ? 0 : A.keo[lo * kE + c];
+    if (kLR && c == 0 && d != kNone) bb = A.keo[lo * kE + kC];
   }
-  const u32 d = A.kdst[lo];
   if (d == kNone) return;
   u64* R = A.out + (u64)d * A.W;
-  const u64 at = A.keo[lo * kC + c] + (j - C.offs[lo]);
+  const u64 at = at0 + (j - off);
 #pragma unroll
   for (u32 q = 0; q < 3; q++) {
     if (q >= ncol) break;
-    const u64 x = C.col[q][j];
-    if (kLR && c == 0 && (int)q == A.lr && (x & JY_LR_LEN_MASK) > 8) continue;  // written by R3
+    u64 x = C.col[q][j];
+    if (kLR && c == 0 && (int)q == A.lr && (x & JY_LR_LEN_MASK) > 8) {
+      // a long value: its 8-B granules into the run's byte section, the handle rewritten
+      const u64 len = x & JY_LR_LEN_MASK, b = bb + A.eb[j];
+      const u64* src = reinterpret_cast<const u64*>(A.arena + (x >> JY_LR_LEN_BITS));
+      u64* dst = reinterpret_cast<u64*>(A.bytes + (u64)d * A.cap_b + b);
+      for (u64 w = 0; w < round8(len) / 8; w++) dst[w] = src[w];
+      x = (b << JY_LR_LEN_BITS) | len;
+    }
     R[C.o_col[q] + at] = x;
   }
 }
@@ -362,15 +409,16 @@ int32_t route_part(jy_engine* eng, RouteArgs<kC>& A) {
     void* p;
     JY_TRY(jy_scratch(eng, 24, ntiles * A.S * kQ * 8 + 64, &p));
     A.tcnt = static_cast<u64*>(p);
-    JY_TRY(jy_scratch(eng, 25, n * 8 + 64, &p));
+    JY_TRY(jy_scratch(eng, 25, n * 8 + (kLR ? A.c[0].nent_host * 4 : 0) + 64, &p));
     A.kb = static_cast<u64*>(p);
+    A.eb = reinterpret_cast<u32*>(A.kb + n);
     JY_TRY(jy_scratch(eng, 26, n * 4 + 64, &p));
     A.kdst = static_cast<u32*>(p);
-    JY_TRY(jy_scratch(eng, 27, n * kC * 8 + 64, &p));
+    JY_TRY(jy_scratch(eng, 27, n * (kC + (kLR ? 1 : 0)) * 8 + 64, &p));
     A.keo = static_cast<u64*>(p);
     hipLaunchKernelGGL((k_rc_count<kC, kLR>), dim3((u32)ntiles), dim3(kThreads), 0, eng->stream, A);
     JY_HIP(eng, hipGetLastError());
-    hipLaunchKernelGGL(k_rc_tscan, dim3(A.S * kQ), dim3(kThreads), 0, eng->stream, A.tcnt, ntiles, A.S * kQ);
+    hipLaunchKernelGGL(k_rc_tscan, dim3(A.S * kQ), dim3(kScanT), 0, eng->stream, A.tcnt, ntiles, (u32)kQ, A.hdr);
     JY_HIP(eng, hipGetLastError());
     hipLaunchKernelGGL((k_rc_place<kC, kLR>), dim3((u32)ntiles), dim3(kThreads), 0, eng->stream, A);
     JY_HIP(eng, hipGetLastError());

@@ -239,8 +239,10 @@ class _RunRouter:
         if caps is None:
             m = fab.host_max([np.array(self._sizes(b), np.int64) for b in batches])[0]
             caps = self._caps([int(x) for x in m], nch)
-        ovfs = [torch.zeros(int(b[0].numel()) + 1, dtype=torch.int32, device=torch.device("cuda", e.device))
+        ovfs = [torch.empty(int(b[0].numel()) + 1, dtype=torch.int32, device=torch.device("cuda", e.device))
                 for e, b in zip(self.engs, batches)]
+        for o in ovfs:
+            o[:1].zero_()  # the count; the list is written as it grows
         sends = []  # [chunk][local rank]
         for c in range(nch):
             per = []
@@ -338,13 +340,15 @@ class TregRouter(_RunRouter):
         dev = torch.device("cuda", eng.device)
         recs = torch.empty((S * cap, 4), dtype=torch.int64, device=dev)
         byts = torch.empty(S * capb, dtype=torch.uint8, device=dev)
-        hdr = torch.zeros((S, 2), dtype=torch.int64, device=dev)
+        hdr = torch.empty((S, 2), dtype=torch.int64, device=dev)
         if n:
             for t in (own, slot, ts, pre, lr):
                 assert t.is_cuda and t.is_contiguous() and t.numel() == n
             eng._check(eng.lib.jy_treg_route_part(
                 eng.h, n, own.data_ptr(), slot.data_ptr(), ts.data_ptr(), pre.data_ptr(), lr.data_ptr(), S, cap,
                 capb, _lib.DEVICE, self._ptr(recs), self._ptr(byts), self._ptr(hdr), self._ptr(ovf)))
+        else:
+            hdr.zero_()
         return (hdr, recs, byts)
 
     def _merge(self, eng, rcv, caps):
