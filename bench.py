@@ -78,7 +78,9 @@ def other_mode(args, rank, world, local, dist):
         args.keys = 0  # per-mode default size
     res = bench_modes.MODES[args.type](args, eng, dev, dist, rank, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = bench_modes.cpu_baseline(args.type)
+        cb = bench_modes.cpu_baseline(args.type)
+        if cb is not None:
+            res["cpu_baseline"] = cb
     if rank == 0:
         line = {"metric": res.pop("metric", f"{args.type.upper()} delta converge throughput (SURVEY 8d)"),
                 "value": res.pop("value"),

@@ -75,7 +75,9 @@ def cpu_baseline(mode, rounds=2):
     import oracle as O
     from jylis_amd import synth as S
     t_conv, units, sample = 0.0, 0, ""
-    if mode == "gcount":
+    if mode == "read":
+        return None  # no C-level GET loop in the oracle; a Python loop over it would time ctypes
+    if mode in ("gcount", "e2e"):  # e2e: the oracle's converge probes its Map by key string, as e2e interns
         K, R = 262144, 16
         seed = S.BASE_SEED + 1
         kb, ko = S.counter_keys(K, prefix=b"g", width=7)

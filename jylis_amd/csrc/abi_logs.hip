@@ -422,7 +422,7 @@ int32_t jy_ujson_read(jy_engine* eng, uint64_t n, const uint32_t* slots, const u
   JY_TRY(jy_scratch(eng, 11, std::max<u64>(words, 1) * 8, &o));
   u64* d = static_cast<u64*>(o);
   u64 *odots = d, *oelems = d + me, *ocloud = d + 2 * me, *ovv = d + 2 * me + mc;
-  JY_TRY(jy_ujson_gather(eng, n, (const u32*)ds, (const u64*)de, (const u64*)dc, odots, oelems, ovv, ocloud));
+  JY_TRY(jy_ujson_gather(eng, n, (const u32*)ds, (const u64*)de, (const u64*)dc, me, mc, odots, oelems, ovv, ocloud));
   if (me) {
     JY_HIP(eng, hipMemcpyAsync(dots, odots, me * 8, hipMemcpyDeviceToHost, eng->stream));
     JY_HIP(eng, hipMemcpyAsync(elems, oelems, me * 8, hipMemcpyDeviceToHost, eng->stream));

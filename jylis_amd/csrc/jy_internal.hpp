@@ -516,8 +516,8 @@ int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, co
 int32_t jy_ujson_grow(jy_engine* eng, u64 need_slots);
 int32_t jy_ujson_extend(jy_engine* eng, u64 from, u64 to);
 int32_t jy_ujson_sizes(jy_engine* eng, u64 n, const u32* slots, u64* ne, u64* nc);
-int32_t jy_ujson_gather(jy_engine* eng, u64 n, const u32* slots, const u64* oeoff, const u64* ocoff, u64* odots,
-                        u64* oelems, u64* ovv, u64* ocloud);
+int32_t jy_ujson_gather(jy_engine* eng, u64 n, const u32* slots, const u64* oeoff, const u64* ocoff, u64 nel, u64 ncl,
+                        u64* odots, u64* oelems, u64* ovv, u64* ocloud);
 int32_t jy_ujson_merge(jy_engine* eng, u64 ndocs, const u32* slot, const u64* eoffs, u64 nel, const u64* dots,
                        const u64* elems, const u64* vvoffs, u64 nvv, const u64* vv, const u64* coffs, u64 ncloud,
                        const u64* cloud);
@@ -527,7 +527,7 @@ int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* sl
                             const u64* dcoff, u64 ncloud, const u64* dcloud, bool keep_all = false);
 int32_t jy_ujson_sizes_of(jy_engine* eng, const UjsonState& u, u64 n, const u32* slots, u64* ne, u64* nc);
 int32_t jy_ujson_gather_of(jy_engine* eng, const UjsonState& u, u64 n, const u32* slots, const u64* oeoff,
-                           const u64* ocoff, u64* odots, u64* oelems, u64* ovv, u64* ocloud);
+                           const u64* ocoff, u64 nel, u64 ncl, u64* odots, u64* oelems, u64* ovv, u64* ocloud);
 int32_t ujson_grow_store(jy_engine* eng, UjsonState& u, u64 need, u64 init_cap);
 // UJSON write path (k_uj_write.hip): one command per doc (device arrays)
 int32_t jy_ujson_write_batch(jy_engine* eng, u64 n, const uint8_t* op, const u32* slot, const u64* elem, u32 col);

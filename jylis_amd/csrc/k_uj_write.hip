@@ -218,7 +218,7 @@ int32_t jy_ujson_flush_dev(jy_engine* eng, u64 cap_docs, u64 cap_el, u64 cap_cl,
   JY_HIP(eng, hipMemcpyAsync(slots, sl, k * 4, hipMemcpyDeviceToDevice, eng->stream));
   JY_HIP(eng, hipMemcpyAsync(eoff, eo, (k + 1) * 8, hipMemcpyDeviceToDevice, eng->stream));
   JY_HIP(eng, hipMemcpyAsync(coff, co, (k + 1) * 8, hipMemcpyDeviceToDevice, eng->stream));
-  JY_TRY(jy_ujson_gather_of(eng, d, k, sl, eo, co, dots, elems, vv, cloud));
+  JY_TRY(jy_ujson_gather_of(eng, d, k, sl, eo, co, me, mc, dots, elems, vv, cloud));
   LAUNCH(k_ujw_reset, k, d.meta, d.vv, d.R, eng->uj_dflag, sl, k);
   JY_HIP(eng, hipMemsetAsync(eng->uj_dcount, 0, 8, eng->stream));
   // every pending doc was flushed: the delta pools are empty again (in-flight

@@ -813,24 +813,51 @@ __global__ __launch_bounds__(kThreads) void k_uj_sizes_read(const UMeta* __restr
   nc[i] = m.clen;
 }
 
-__global__ __launch_bounds__(kThreads) void k_uj_gather(const UMeta* __restrict__ meta, const URec* __restrict__ rec,
-                                                        const u64* __restrict__ cloud, const u64* __restrict__ vv,
-                                                        u32 R, const u32* __restrict__ slots, u64 n,
-                                                        const u64* __restrict__ oeoff, const u64* __restrict__ ocoff,
-                                                        u64* __restrict__ odots, u64* __restrict__ oelems,
-                                                        u64* __restrict__ ovv, u64* __restrict__ ocloud) {
-  const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= n) return;
-  const u64 s = slots[i];
-  const UMeta m = meta[s];
-  u64 o = oeoff[i];
-  for (u64 j = 0; j < m.elen; j++, o++) {
-    odots[o] = rec[m.ebase + j].dot;
-    oelems[o] = rec[m.ebase + j].elem;
+// reads, flattened over the output: a tile of kThreads output items finds
+// its documents with two wave searches of the output offsets (a hot document
+// of 10^5 elements is spread over many tiles instead of one thread's loop)
+template <bool kEl>
+__global__ __launch_bounds__(kThreads) void k_uj_gather_items(const UMeta* __restrict__ meta,
+                                                              const URec* __restrict__ rec,
+                                                              const u64* __restrict__ cloud,
+                                                              const u32* __restrict__ slots, u64 n,
+                                                              const u64* __restrict__ ooff, u64 total,
+                                                              u64* __restrict__ oa, u64* __restrict__ ob) {
+  __shared__ u64 sh[2];
+  const u64 t0 = (u64)blockIdx.x * kThreads;
+  if (t0 >= total) return;
+  const u64 t1 = t0 + kThreads < total ? t0 + kThreads : total;
+  if (threadIdx.x < 128) {
+    const u64 k = jyscan::wave_last_le(ooff, n, threadIdx.x < 64 ? t0 : t1 - 1);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = k;
   }
-  o = ocoff[i];
-  for (u64 j = 0; j < m.clen; j++, o++) ocloud[o] = cloud[m.cbase + j];
-  for (u32 c = 0; c < R; c++) ovv[i * R + c] = vv[s * R + c];
+  __syncthreads();
+  const u64 t = t0 + threadIdx.x;
+  if (t >= t1) return;
+  u64 lo = sh[0], hi = sh[1];
+  while (lo < hi) {
+    const u64 m = (lo + hi + 1) >> 1;
+    if (ooff[m] <= t) lo = m;
+    else hi = m - 1;
+  }
+  const UMeta m = meta[slots[lo]];
+  const u64 j = t - ooff[lo];
+  if (kEl) {
+    const URec r = rec[m.ebase + j];
+    oa[t] = r.dot;
+    ob[t] = r.elem;
+  } else {
+    oa[t] = cloud[m.cbase + j];
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_uj_gather_vv(const u64* __restrict__ vv, u32 R,
+                                                           const u32* __restrict__ slots, u64 n,
+                                                           u64* __restrict__ ovv) {
+  const u64 g = (u64)blockIdx.x * kThreads + threadIdx.x;
+  if (g >= n * R) return;
+  const u64 i = g / R, c = g - i * R;
+  ovv[g] = vv[(u64)slots[i] * R + c];
 }
 
 u64 cdiv_h(u64 a) { return (a + kTile - 1) / kTile; }
@@ -1198,12 +1225,14 @@ int32_t jy_ujson_sizes_of(jy_engine* eng, const UjsonState& u, u64 n, const u32*
   return JY_OK;
 }
 
-int32_t jy_ujson_gather(jy_engine* eng, u64 n, const u32* slots, const u64* oeoff, const u64* ocoff, u64* odots,
-                        u64* oelems, u64* ovv, u64* ocloud) {
-  return jy_ujson_gather_of(eng, eng->ujson, n, slots, oeoff, ocoff, odots, oelems, ovv, ocloud);
+int32_t jy_ujson_gather(jy_engine* eng, u64 n, const u32* slots, const u64* oeoff, const u64* ocoff, u64 nel, u64 ncl,
+                        u64* odots, u64* oelems, u64* ovv, u64* ocloud) {
+  return jy_ujson_gather_of(eng, eng->ujson, n, slots, oeoff, ocoff, nel, ncl, odots, oelems, ovv, ocloud);
 }
 int32_t jy_ujson_gather_of(jy_engine* eng, const UjsonState& u, u64 n, const u32* slots, const u64* oeoff,
-                           const u64* ocoff, u64* odots, u64* oelems, u64* ovv, u64* ocloud) {
-  LAUNCH(k_uj_gather, n, u.meta, u.epool, u.cpool, u.vv, u.R, slots, n, oeoff, ocoff, odots, oelems, ovv, ocloud);
+                           const u64* ocoff, u64 nel, u64 ncl, u64* odots, u64* oelems, u64* ovv, u64* ocloud) {
+  if (nel) LAUNCH(k_uj_gather_items<true>, nel, u.meta, u.epool, u.cpool, slots, n, oeoff, nel, odots, oelems);
+  if (ncl) LAUNCH(k_uj_gather_items<false>, ncl, u.meta, u.epool, u.cpool, slots, n, ocoff, ncl, ocloud, ocloud);
+  LAUNCH(k_uj_gather_vv, n * u.R, u.vv, u.R, slots, n, ovv);
   return JY_OK;
 }
