@@ -846,7 +846,9 @@ int32_t tlog_compact(jy_engine* eng, TlogState& t, u64 room) {
   JY_HIP(eng, hipStreamSynchronize(eng->stream));
   const u64 total = t.pin[0], live = t.pin[1];
   // the next merges' worst case fits several times over before the next sync
-  const u64 ncap = std::max<u64>({total + room, 3 * total, eng->cfg.entry_capacity[JY_TLOG], 1024});
+  // 6x the live entries: a compaction costs a copy of the pool, so they
+  // should be rare (HBM is plentiful: 4M logs of ~15 entries -> ~12 GB)
+  const u64 ncap = std::max<u64>({total + room, 6 * total, eng->cfg.entry_capacity[JY_TLOG], 1024});
   TRec* np = nullptr;
   JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&np), ncap * sizeof(TRec), "tlog pool"));
   if (total) {
