@@ -137,3 +137,61 @@ def test_many_rounds_pool_reuse(oracle_mod):
         assert_state_equal(O.UJSON, want.state(), got.state())
     finally:
         eng.close()
+
+
+def test_hot_document_long_segments(oracle_mod):
+    """one document of 24,000 elements next to small ones: long segments go
+    through U1's tile maps, and the read gathers a document over many tiles
+    (jy_ujson_read is flattened over the output); deltas insert and remove
+    thousands of its dots"""
+    from jylis_amd import synth as S
+    from jylis_amd.engine import Engine
+    from jylis_amd.repo import RepoUJSON
+    O = oracle_mod
+    R = 8
+    ids = S.replica_ids(R, 77)
+    rng = np.random.default_rng(12)
+    keys = [b"hot"] + [b"cold%d" % i for i in range(40)]
+
+    def table(docs):
+        """docs: list of (key, {(col, seq): elem}, {col: n}, {(col, seq)})"""
+        from jylis_amd.engine import encode_keys
+        t = {k: [] for k in ("dot_ids", "dot_seqs", "elems", "vv_ids", "vv_seqs", "cloud_ids", "cloud_seqs")}
+        eo, vo, co = [0], [0], [0]
+        for _, els, vv, cl in docs:
+            for (c, q), e in sorted(els.items()):
+                t["dot_ids"].append(ids[c]), t["dot_seqs"].append(q), t["elems"].append(e)
+            for c, n in sorted(vv.items()):
+                t["vv_ids"].append(ids[c]), t["vv_seqs"].append(n)
+            for c, q in sorted(cl):
+                t["cloud_ids"].append(ids[c]), t["cloud_seqs"].append(q)
+            eo.append(len(t["elems"])), vo.append(len(t["vv_ids"])), co.append(len(t["cloud_ids"]))
+        out = {k: np.array(v, np.uint64) for k, v in t.items()}
+        out["key_bytes"], out["key_offs"] = encode_keys([d[0] for d in docs])
+        out["el_offs"], out["vv_offs"], out["cloud_offs"] = (np.array(x, np.uint64) for x in (eo, vo, co))
+        return out
+
+    hot = {(c, q): int(rng.integers(1, 1 << 40)) for c in range(R) for q in range(1, 3001)}
+    state = [(b"hot", hot, {c: 3000 for c in range(R)}, set())]
+    for k in keys[1:]:
+        els = {(int(c), q): int(rng.integers(1, 99)) for c in rng.integers(0, R, 3) for q in (1, 2)}
+        state.append((k, els, {c: 2 for c in range(R)}, set()))
+    batches = [table(state)]
+    for rnd in range(3):
+        # the hot doc: 2000 fresh dots, 2500 of its dots removed (context only)
+        new = {(int(c), 3000 + 1000 * rnd + int(q)): int(rng.integers(1, 1 << 40))
+               for c, q in zip(rng.integers(0, R, 2000), rng.integers(1, 900, 2000))}
+        rm = {(int(c), int(q)) for c, q in zip(rng.integers(0, R, 2500), rng.integers(1, 3001, 2500))}
+        docs = [(b"hot", new, {}, set(new) | rm)]
+        docs.append((keys[1 + rnd], {(0, 10 + rnd): 5}, {}, {(0, 10 + rnd), (1, 1)}))
+        batches.append(table(docs))
+    eng = Engine(device=0, ujson_columns=R)
+    try:
+        want = O.Repo(O.UJSON, 1)
+        got = RepoUJSON(eng)
+        for b in batches:
+            want.converge(b)
+            got.converge_deltas(b)
+            assert_state_equal(O.UJSON, want.state(), got.state())
+    finally:
+        eng.close()
