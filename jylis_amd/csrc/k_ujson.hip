@@ -536,6 +536,10 @@ __global__ __launch_bounds__(kItemThreads) void k_uj_flags(UjArgs A) {
   u64 f = 0;
   if (i < n) {
     const u64 k = doc_at(A, tm, lt, sid, i);
+#ifdef JY_UJ_AB_NOLONG  // A/B only: items of long documents skip their searches (WRONG results)
+    if ((u32)(tm[lt] >> 32) == A.epoch) {
+    } else
+#endif
     if (!is_bad(A, k)) {
       const u64 clo = A.cbs[k], chi = clo + (A.co[k + 1] - A.co[k]);
       u32 xr;
