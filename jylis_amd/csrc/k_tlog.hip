@@ -226,7 +226,10 @@ __device__ __forceinline__ u32 lds_last_le(const u64* a, u32 n, u64 x) {
 // key tiles are one wave: no cross-wave barriers, many tiles in flight per CU
 constexpr int kTile = 64;
 constexpr int kFastEnt = 4;  // delta entries a key may have for the lane-per-key fast path
-constexpr int kCache = 2;    // passes of slow entries kept in registers for the append stores
+#ifndef JY_TLOG_KCACHE
+#define JY_TLOG_KCACHE 1
+#endif
+constexpr int kCache = JY_TLOG_KCACHE;  // passes of slow entries kept in registers for the append stores
 constexpr int kCU = 1;       // output entries per lane per pass of the rebuild (2: same time)
 
 constexpr u32 kKept = 0x80000000u;  // eqx: kept flag | # kept entries of the key before this one
@@ -248,7 +251,8 @@ constexpr u32 kKept = 0x80000000u;  // eqx: kept flag | # kept entries of the ke
 //      passes from registers)
 // rank / q of the slow entries go to HBM for the rebuild in k_tlog_commit.
 #ifndef JY_TLOG_TILE_ATTR
-#define JY_TLOG_TILE_ATTR
+// 80 VGPRs: 6 waves per SIMD (one cached pass; 2 cached passes took 90 VGPRs / 5 waves)
+#define JY_TLOG_TILE_ATTR __attribute__((amdgpu_waves_per_eu(6)))
 #endif
 __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs A, TRec* __restrict__ pool,
                                                                         u32* __restrict__ erank,
