@@ -93,7 +93,7 @@ __device__ __forceinline__ TRec load_rec(const TRec* __restrict__ p) {
   return r;
 }
 
-enum : u32 { kSkip = 0, kAppend = 1, kRebuild = 2, kFast = 3 };
+enum : u32 { kSkip = 0, kAppend = 1, kRebuild = 2, kFast = 3, kInsert = 4 };
 
 // per REBUILT key (a worklist entry): what k_tlog_tile decided; the log's
 // current base is read from its meta at commit (a compaction may move it)
@@ -105,7 +105,9 @@ struct alignas(16) PInfo {
   u32 len;     // old length
   u32 drop;    // state entries dropped by the cutoff (a prefix)
   u32 newlen;  // entries after the merge
-  u32 cap;     // the new segment's capacity
+  u32 cap;     // the new segment's capacity (rebuild) or the old one (insert)
+  u32 minrank; // insert: the first log position that moves
+  u32 ins;     // 1: inserted in place (the segment has room), 0: rebuilt
 };
 
 struct TlogArgs {
@@ -123,8 +125,9 @@ struct TlogArgs {
   // temporaries
   u32* dptr;      // [nkeys] delta key merging into each slot
   u32* bad;       // [nd] repeated slot in the batch
-  PInfo* pinfo;   // [nd] written for rebuilt keys only
+  PInfo* pinfo;   // [nd] written for rebuilt and inserted keys only
   u32* rz;        // [nd + 1] pool entries a rebuilt key takes (0 otherwise)
+  u32* ins;       // [nd] 1: the key's delta interleaves with its log and fits its segment
   unsigned long long* skipped;
 };
 
@@ -230,7 +233,6 @@ constexpr int kFastEnt = 4;  // delta entries a key may have for the lane-per-ke
 #define JY_TLOG_KCACHE 1
 #endif
 constexpr int kCache = JY_TLOG_KCACHE;  // passes of slow entries kept in registers for the append stores
-constexpr int kCU = 1;       // output entries per lane per pass of the rebuild (2: same time)
 
 constexpr u32 kKept = 0x80000000u;  // eqx: kept flag | # kept entries of the key before this one
 
@@ -441,15 +443,27 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
       if ((M == 0 || l_minrank[tid] == len) && (u64)len + M <= l_cap[tid]) {
         mode = kAppend;
         A.meta[P.s] = TMeta{l_base[tid] + drop, P.newlen, l_cap[tid] - drop, P.cut, nn};
+      } else if ((u64)len + M <= l_cap[tid]) {
+        // interleaves, but the segment has room: k_tlog_commit shifts the
+        // log's suffix from minrank up in place (no fresh space)
+        mode = kInsert;
+        P.cap = l_cap[tid];
+        P.minrank = l_minrank[tid];
+        P.ins = 1;
+        A.pinfo[k] = P;
       } else {
         mode = kRebuild;
         P.cap = pow2_cap(surv + M);
+        P.ins = 0;
         A.pinfo[k] = P;
       }
     }
     l_mode[tid] = mode;
   }
-  if (tid < nt) A.rz[k0 + tid] = mode == kRebuild ? P.cap : 0u;
+  if (tid < nt) {
+    A.rz[k0 + tid] = mode == kRebuild ? P.cap : 0u;
+    A.ins[k0 + tid] = mode == kInsert;
+  }
   __syncthreads();
   // 4. appends: kept entries of append keys go to the tail, oldest first
   pass = 0;
@@ -477,122 +491,116 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
   }
 }
 
-// KEY TILES again, after the scan of rebuilt sizes: the rebuilt keys'
-// segments are written into their fresh space (tiles without one exit after
-// one load), one lane per output (state survivors and delta entries of the
-// tile's rebuilt keys, flattened by a wave scan):
-//   state entry i (i >= drop): (i - drop) + #kept deltas with rank <= i;
-//     ranks fall along the newest-first delta segment, so that is M - q of
-//     the first entry with rank <= i (binary search)
+// KEY TILES again, after the scan of rebuilt sizes (tiles without a rebuilt
+// or inserted key exit after one load), one lane per output entry (state
+// entries and delta entries of the tile's keys, flattened by a wave scan):
+//   state entry i: (i - drop) + #kept deltas with rank <= i; ranks fall along
+//     the newest-first delta segment, so that is M - q of the first entry
+//     with rank <= i (binary search)
 //   kept delta entry j: (rank_j - drop) + (M - 1 - q_j)
+// relative to the log's new base.  REBUILT keys write every survivor into
+// fresh space.  INSERTED keys (the delta interleaves, the segment has room)
+// stay in place: only the suffix from minrank moves up.  Their items go
+// delta entries first, and the passes run from the last item down, so every
+// state entry is read (in its own pass, or an earlier one) before anything
+// is written over it: a pass's loads all return before its stores (one wave),
+// and a state entry only moves up.
 __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __restrict__ roff,
                                                        const u64* __restrict__ ctr, TRec* __restrict__ pool,
                                                        const u32* __restrict__ erank, const u32* __restrict__ eqx) {
   __shared__ u64 l_woff[kTile + 1];
   __shared__ u64 l_src[kTile], l_dst[kTile], l_blo[kTile], l_bhi[kTile];
-  __shared__ u32 l_drop[kTile], l_surv[kTile], l_M[kTile];
+  __shared__ u32 l_drop[kTile], l_s0[kTile], l_ns[kTile], l_M[kTile], l_dfirst[kTile];
   const u32 tid = threadIdx.x;
   const u64 k0 = (u64)blockIdx.x * kTile;
   const u32 nt = (u32)(A.nd - k0 < kTile ? A.nd - k0 : kTile);
   const u32 cap = tid < nt ? A.rz[k0 + tid] : 0u;
-  if (__ballot(cap != 0) == 0) return;
+  const u32 ins = tid < nt ? A.ins[k0 + tid] : 0u;
+  if (__ballot(cap != 0 || ins != 0) == 0) return;
   u32 w = 0;
-  if (cap) {
+  if (cap || ins) {
     const u64 k = k0 + tid;
     const PInfo P = A.pinfo[k];
     const u64 src = A.meta[P.s].base;  // current (a compaction may have moved the log)
-    const u64 dst = ctr[0] + roff[k];
-    A.meta[P.s] = TMeta{dst, P.newlen, P.cap, P.cut, P.newest};
+    const u64 dst = ins ? src + P.drop : ctr[0] + roff[k];
+    A.meta[P.s] = TMeta{dst, P.newlen, ins ? P.cap - P.drop : P.cap, P.cut, P.newest};
     const u64 blo = A.doff[k], bhi = A.doff[k + 1];
     l_src[tid] = src;
     l_dst[tid] = dst;
     l_blo[tid] = blo;
     l_bhi[tid] = bhi;
     l_drop[tid] = P.drop;
-    l_surv[tid] = P.len - P.drop;
+    l_s0[tid] = ins ? P.minrank : P.drop;
+    l_ns[tid] = P.len - (ins ? P.minrank : P.drop);
     l_M[tid] = P.newlen - (P.len - P.drop);
-    w = (P.len - P.drop) + (u32)(bhi - blo);
+    l_dfirst[tid] = ins;
+    w = l_ns[tid] + (u32)(bhi - blo);
   }
   const u32 winc = jyscan::wave_incl<u32>(w);  // a key tile is one wave
   const u32 wo = winc - w, wtot = __shfl(winc, 63);
   if (tid < nt) l_woff[tid] = wo;
   if (tid == 0) l_woff[nt] = wtot;
   __syncthreads();
-  for (u32 c0 = 0; c0 < wtot; c0 += kTile * kCU) {
-    u32 idx[kCU], r[kCU];
-    u64 lo[kCU], hi[kCU];
-    bool st[kCU], live[kCU];
-#pragma unroll
-    for (int u = 0; u < kCU; u++) {
-      const u32 item = c0 + u * kTile + tid;
-      live[u] = item < wtot;
-      st[u] = false;
-      idx[u] = 0;
-      r[u] = 0;
-      lo[u] = hi[u] = 0;
-      if (!live[u]) continue;
-      u32 a = 0, h = nt - 1;  // last idx with woff <= item (a key with items)
+  if (wtot == 0) return;
+  for (long long c0 = (long long)((wtot - 1) / kTile) * kTile; c0 >= 0; c0 -= kTile) {
+    const u32 item = (u32)c0 + tid;
+    const bool live = item < wtot;
+    u32 a = 0;
+    bool st = false;
+    u64 i = 0, j = 0, lo = 0, hi = 0;
+    if (live) {
+      u32 h = nt - 1;  // last idx with woff <= item (a key with items)
       while (a < h) {
         const u32 m = (a + h + 1) >> 1;
         if (l_woff[m] <= item) a = m;
         else h = m - 1;
       }
-      idx[u] = a;
-      r[u] = item - (u32)l_woff[a];
-      st[u] = r[u] < l_surv[a];
-      if (st[u]) {  // first delta entry with rank <= i
-        lo[u] = l_blo[a];
-        hi[u] = l_bhi[a];
-      }
-    }
-    for (;;) {
-      bool any = false;
-      u32 mr[kCU];
-#pragma unroll
-      for (int u = 0; u < kCU; u++)
-        if (st[u] && lo[u] < hi[u]) {
-          mr[u] = erank[(lo[u] + hi[u]) >> 1];
-          any = true;
-        }
-      if (!any) break;
-#pragma unroll
-      for (int u = 0; u < kCU; u++)
-        if (st[u] && lo[u] < hi[u]) {
-          const u64 m = (lo[u] + hi[u]) >> 1;
-          if (mr[u] <= l_drop[idx[u]] + r[u]) hi[u] = m;
-          else lo[u] = m + 1;
-        }
-    }
-    u32 qx[kCU];
-    TRec x[kCU];
-#pragma unroll
-    for (int u = 0; u < kCU; u++) {
-      if (!live[u]) continue;
-      const u32 a = idx[u];
-      if (st[u]) {
-        qx[u] = lo[u] < l_bhi[a] ? eqx[lo[u]] : 0u;
-        x[u] = load_rec(A.pool + l_src[a] + l_drop[a] + r[u]);
+      const u32 r = item - (u32)l_woff[a];
+      const u32 nd = (u32)(l_bhi[a] - l_blo[a]);
+      if (l_dfirst[a]) {
+        st = r >= nd;
+        i = l_s0[a] + (r - nd);
+        j = l_blo[a] + r;
       } else {
-        const u64 j = l_blo[a] + (r[u] - l_surv[a]);
-        qx[u] = eqx[j];
-        x[u].ts = A.dts[j];
-        x[u].pre = A.dpre[j];
-        x[u].lr = A.dlr[j];
-        x[u].pad = erank[j];
+        st = r < l_ns[a];
+        i = l_s0[a] + r;
+        j = l_blo[a] + (r - l_ns[a]);
+      }
+      if (st) {  // first delta entry with rank <= i
+        lo = l_blo[a];
+        hi = l_bhi[a];
+        while (lo < hi) {
+          const u64 m = (lo + hi) >> 1;
+          if (erank[m] <= i) hi = m;
+          else lo = m + 1;
+        }
       }
     }
-#pragma unroll
-    for (int u = 0; u < kCU; u++) {
-      if (!live[u]) continue;
-      const u32 a = idx[u], M = l_M[a];
+    u32 qx = 0;
+    TRec x{};
+    if (live) {
+      if (st) {
+        qx = lo < l_bhi[a] ? eqx[lo] : 0u;
+        x = load_rec(A.pool + l_src[a] + i);
+      } else {
+        qx = eqx[j];
+        x.ts = A.dts[j];
+        x.pre = A.dpre[j];
+        x.lr = A.dlr[j];
+        x.pad = erank[j];
+      }
+    }
+    if (live) {
+      const u32 M = l_M[a];
       u64 pos;
-      if (st[u]) {
-        pos = r[u] + (lo[u] < l_bhi[a] ? M - (qx[u] & ~kKept) : 0u);
+      bool write = true;
+      if (st) {
+        pos = (i - l_drop[a]) + (lo < l_bhi[a] ? M - (qx & ~kKept) : 0u);
       } else {
-        if (!(qx[u] & kKept)) continue;
-        pos = (u64)((u32)x[u].pad - l_drop[a]) + (M - 1 - (qx[u] & ~kKept));
+        write = (qx & kKept) != 0;
+        pos = (u64)((u32)x.pad - l_drop[a]) + (M - 1 - (qx & ~kKept));
       }
-      store_rec(pool + l_dst[a] + pos, x[u].ts, x[u].pre, x[u].lr);
+      if (write) store_rec(pool + l_dst[a] + pos, x.ts, x.pre, x.lr);
     }
   }
 }
@@ -610,8 +618,13 @@ __global__ __launch_bounds__(kThreads) void k_cmp_size(const TMeta* __restrict__
     sz[s] = lens[s] = 0;
     return;
   }
-  const u32 n = meta[s].len;
-  sz[s] = n ? (u64)n + (n > 4 ? n : 4) : 0;  // headroom for appends: as long again
+  const TMeta m = meta[s];
+  const u32 n = m.len;
+  // headroom for appends: as long again, and never less than the segment had
+  // (a merge between its tile and commit pass may have planned an in-place
+  // insert against that capacity)
+  const u64 want = (u64)n + (n > 4 ? n : 4);
+  sz[s] = n ? (want > m.cap ? want : m.cap) : 0;
   lens[s] = n;
 }
 
@@ -948,10 +961,11 @@ int32_t jy_tlog_merge_into(jy_engine* eng, TlogState& t, u64 nd, const u32* slot
   void* p;
   JY_TRY(jy_scratch(eng, 8, nk * 4, &p));
   A.dptr = static_cast<u32*>(p);
-  JY_TRY(jy_scratch(eng, 9, nd * (sizeof(PInfo) + 8) + 64, &p));
+  JY_TRY(jy_scratch(eng, 9, nd * (sizeof(PInfo) + 12) + 64, &p));
   A.pinfo = static_cast<PInfo*>(p);
   A.bad = reinterpret_cast<u32*>(A.pinfo + nd);
   A.rz = A.bad + nd;
+  A.ins = A.rz + nd + 1;
   JY_TRY(jy_scratch(eng, 16, (nd + 1) * 8, &p));
   u64* roff = static_cast<u64*>(p);
   JY_TRY(jy_scratch(eng, 12, std::max<u64>(nent, 1) * 8, &p));
