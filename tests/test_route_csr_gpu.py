@@ -348,3 +348,83 @@ def test_run_layout_holes():
             assert r[dd, 26:26 + len(ents)].tolist() == lr[ents].tolist()
     finally:
         eng.close()
+
+
+def test_route_part_host_inputs_match_device():
+    """jy_tlog_route_part / jy_ujson_route_part with host inputs (staged through
+    pinned memory) build the same runs, headers and overflow as with device
+    inputs; a key owned by a shard >= nshards is rejected on the host path"""
+    import ctypes as C
+
+    import torch
+
+    from jylis_amd import _lib
+    from jylis_amd.engine import Engine
+    from jylis_amd.synth import tlog_tables, ujson_tables
+    eng = Engine(device=0, ujson_columns=16)
+    try:
+        S, rng = 3, np.random.default_rng(4)
+        st, _ = tlog_tables(700, 9, rounds=1)
+        n, nent = len(st["ent_offs"]) - 1, len(st["ts"])
+        own = rng.integers(0, S, n).astype(np.uint32)
+        slot = np.arange(n, dtype=np.uint32)
+        pre, lr = eng.pack_values(_lib.TLOG, (st["val_bytes"], st["val_offs"]))
+        cols = [own, slot, np.asarray(st["cutoff"], np.uint64), np.asarray(st["ent_offs"], np.uint64)]
+        ents = [np.asarray(st["ts"], np.uint64), pre, lr]
+        cap_k, cap_e, cap_b = 200, 1200, 4096
+        W = int(eng.lib.jy_route_words(_lib.TLOG, cap_k, (C.c_uint64 * 1)(cap_e)))
+        outs = []
+        for mem in (_lib.HOST, _lib.DEVICE):
+            runs = torch.zeros(S * W, dtype=torch.int64, device="cuda:0")
+            byts = torch.zeros(S * cap_b, dtype=torch.uint8, device="cuda:0")
+            hdr = torch.zeros(S * 8, dtype=torch.int64, device="cuda:0")
+            ovf = torch.zeros(n + 1, dtype=torch.int32, device="cuda:0")
+            if mem == _lib.HOST:
+                ptr = [a.ctypes.data for a in cols], [a.ctypes.data for a in ents]
+            else:
+                dv = [_dev(a) for a in cols], [_dev(a) for a in ents]
+                ptr = [t.data_ptr() for t in dv[0]], [t.data_ptr() for t in dv[1]]
+            eng._check(eng.lib.jy_tlog_route_part(eng.h, n, *ptr[0], nent, *ptr[1], S, cap_k, cap_e, cap_b, 0, mem,
+                                                  C.c_void_p(runs.data_ptr()), C.c_void_p(byts.data_ptr()),
+                                                  C.c_void_p(hdr.data_ptr()), C.c_void_p(ovf.data_ptr())))
+            torch.cuda.synchronize()
+            o = ovf.cpu().numpy()
+            outs.append((runs.cpu().numpy(), byts.cpu().numpy(), hdr.cpu().numpy(), sorted(o[1:1 + o[0]].tolist())))
+        h, d = outs
+        for a, b in zip(h, d):
+            np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
+        assert len(h[3]) > 0  # capacities below a balanced share: some keys overflow
+        bad = own.copy()
+        bad[5] = S
+        rc = eng.lib.jy_tlog_route_part(eng.h, n, bad.ctypes.data, *[a.ctypes.data for a in cols[1:]], nent,
+                                        *[a.ctypes.data for a in ents], S, cap_k, cap_e, cap_b, 0, _lib.HOST,
+                                        C.c_void_p(runs.data_ptr()), C.c_void_p(byts.data_ptr()),
+                                        C.c_void_p(hdr.data_ptr()), C.c_void_p(ovf.data_ptr()))
+        assert rc == _lib.JY_ERANGE
+        # UJSON: host and device inputs agree as well
+        ust, _ = ujson_tables(500, 3, rounds=1, R=16)
+        from jylis_amd.repo import RepoUJSON
+        repo = RepoUJSON(eng)
+        nd = len(ust["el_offs"]) - 1
+        uown = rng.integers(0, S, nd).astype(np.uint32)
+        b = ujson_device_batch(repo, uown, np.arange(nd, dtype=np.uint32), ust)
+        hb = [t.cpu().numpy() for t in b]
+        hb = [x.view(np.uint32) if x.dtype == np.int32 else x.view(np.uint64) for x in hb]
+        caps = (120, 900, 500, 500)
+        Wu = int(eng.lib.jy_route_words(_lib.UJSON, caps[0], (C.c_uint64 * 3)(*caps[1:])))
+        res = []
+        for mem, src in ((_lib.HOST, [x.ctypes.data for x in hb]), (_lib.DEVICE, [t.data_ptr() for t in b])):
+            runs = torch.zeros(S * Wu, dtype=torch.int64, device="cuda:0")
+            hdr = torch.zeros(S * 8, dtype=torch.int64, device="cuda:0")
+            ovf = torch.zeros(nd + 1, dtype=torch.int32, device="cuda:0")
+            own_p, slot_p, eo, dots, elems, vo, vv, co, cloud = src
+            eng._check(eng.lib.jy_ujson_route_part(
+                eng.h, nd, own_p, slot_p, eo, len(hb[3]), dots, elems, vo, len(hb[6]), vv, co, len(hb[8]), cloud, S,
+                *caps, 0, mem, C.c_void_p(runs.data_ptr()), C.c_void_p(hdr.data_ptr()), C.c_void_p(ovf.data_ptr())))
+            torch.cuda.synchronize()
+            o = ovf.cpu().numpy()
+            res.append((runs.cpu().numpy(), hdr.cpu().numpy(), sorted(o[1:1 + o[0]].tolist())))
+        for a, b2 in zip(*res):
+            np.testing.assert_array_equal(np.asarray(a), np.asarray(b2))
+    finally:
+        eng.close()
