@@ -426,13 +426,32 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_e
     // the state vv rows (lanes on consecutive columns of a row), then the
     // merged rows max(state, delta) from the docs' sparse delta vv entries
     const u64 kt0 = (u64)t * kDocTile;
-    for (u64 j = threadIdx.x; j < kDocTile * A.R; j += kThreads) {
-      const u64 dk = j / A.R, c = j - dk * A.R;
-      if (kt0 + dk < A.nd) {
-        const u64 v = l_slot[dk] == JY_NO_SLOT ? 0 : A.vv[(u64)l_slot[dk] * A.R + c], g = (kt0 + dk) * A.R + c;
-        A.vvs[g] = v;
-        A.vvm[g] = v;
-        A.vvn[g] = v;
+    {
+      // kVvBatch rows' loads in flight before their stores (the arrays may
+      // alias as far as the compiler knows: without the batching every
+      // iteration waited for its own load, ~16 round trips at R = 16)
+      constexpr int kVvBatch = 8;
+      const u64 tot = kDocTile * A.R;
+      for (u64 j0 = threadIdx.x; j0 < tot; j0 += (u64)kThreads * kVvBatch) {
+        u64 v[kVvBatch];
+#pragma unroll
+        for (int u = 0; u < kVvBatch; u++) {
+          const u64 j = j0 + (u64)u * kThreads;
+          const u64 dk = j / A.R, c = j - dk * A.R;
+          v[u] = 0;
+          if (j < tot && kt0 + dk < A.nd && l_slot[dk] != JY_NO_SLOT) v[u] = A.vv[(u64)l_slot[dk] * A.R + c];
+        }
+#pragma unroll
+        for (int u = 0; u < kVvBatch; u++) {
+          const u64 j = j0 + (u64)u * kThreads;
+          const u64 dk = j / A.R;
+          if (j < tot && kt0 + dk < A.nd) {
+            const u64 g = kt0 * A.R + j;
+            A.vvs[g] = v[u];
+            A.vvm[g] = v[u];
+            A.vvn[g] = v[u];
+          }
+        }
       }
     }
     const u64 kt1 = kt0 + kDocTile < A.nd ? kt0 + kDocTile : A.nd;
