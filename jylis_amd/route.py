@@ -207,6 +207,7 @@ class _RunRouter:
         self.S = fabric.world
         assert len(self.engs) == len(fabric.ranks)
         self.pending = None  # (batches, ovf tensors, pinned global max, event)
+        self._pins = None
         self.routed = 0
         self.drains = 0
         self.bind()
@@ -278,12 +279,13 @@ class _RunRouter:
         import torch
         gm = [o[:1].clone() for o in ovfs]
         self.fabric.max_all(gm)
-        pins = []
-        for g, o in zip(gm, ovfs):
-            p = torch.empty(2, dtype=torch.int32, pin_memory=True)
+        if self._pins is None:
+            # one pinned pair per engine, reused: _settle reads it before the next _publish
+            self._pins = [torch.empty(2, dtype=torch.int32, pin_memory=True) for _ in ovfs]
+        pins = self._pins
+        for g, o, p in zip(gm, ovfs, pins):
             p[0:1].copy_(g, non_blocking=True)
             p[1:2].copy_(o[:1], non_blocking=True)
-            pins.append(p)
         ev = torch.cuda.Event()
         ev.record()
         self.pending = (batches, ovfs, pins, ev)
@@ -299,7 +301,8 @@ class _RunRouter:
         self.pending = None
         if int(pins[0][0]) == 0:
             return
-        sub = [self._subset(b, o[1:1 + int(p[1])].long()) for b, o, p in zip(batches, ovfs, pins)]
+        counts = [int(p[1]) for p in pins]  # read before the drain round reuses the pinned pairs
+        sub = [self._subset(b, o[1:1 + k].long()) for b, o, k in zip(batches, ovfs, counts)]
         m = self.fabric.host_max([np.array(self._sizes(s), np.int64) for s in sub])[0]
         # capacity = the whole overflow of the largest sender: nothing can overflow again
         ovfs2 = self._round(sub, caps=self._drain_caps([int(x) for x in m]))
