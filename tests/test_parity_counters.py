@@ -41,14 +41,14 @@ def test_test_cluster_on_gpu(oracle_mod, engine):
     assert int(gpu.get(["foo"])[0]) == 9
 
 
-@pytest.mark.parametrize("ctype", [0, 1])
-def test_synthetic_block_and_coo(oracle_mod, engine, ctype):
+@pytest.mark.parametrize("ctype,K,R", [(0, 6000, 8), (1, 6000, 8), (0, 1500, 64), (1, 1500, 64)])
+def test_synthetic_block_and_coo(oracle_mod, engine, ctype, K, R):
     """config-1/2 shaped stream (every peer batch = one replica column over all
-    keys) at K=6000, R=8: dense block path for half the rounds, COO for the rest"""
+    keys): dense block path for half the rounds, COO for the rest.  R=64 is
+    config 2's replica count (the headline's k_block_max launch shape)"""
     from jylis_amd import synth as S
     from jylis_amd.repo import REPOS
     O = oracle_mod
-    K, R = 6000, 8
     nsigns = 1 if ctype == 0 else 2
     seed = S.BASE_SEED + 1 + ctype
     kb, ko = S.counter_keys(K, prefix=b"g" if ctype == 0 else b"p")
