@@ -312,6 +312,7 @@ void jy_engine_destroy(jy_engine* eng) {
   F(eng->uj_dflag);
   F(eng->uj_dcount);
   F(eng->dscan_st.p);
+  F(eng->tl_claim.p);
   F(eng->dscan_tick);
   for (auto& a : eng->arena) F(a.p);
   for (auto& s : eng->scratch) F(s.p);

@@ -354,6 +354,9 @@ struct jy_engine {
   // scratch (device) reused across calls, stream-ordered
   // 0-7 staged inputs, 8-14 and 16-23 merge temporaries, 15 scan temp storage
   DevArray scratch[28];
+  // TLOG merge: the delta key claiming each slot (kNone between merges; a
+  // merge resets only its batch's slots, so no per-merge memset over all keys)
+  DevArray tl_claim;
   // device-wide scans / selects (jy_dscan.hpp): epoch-tagged look-back words
   DevArray dscan_st;
   u32* dscan_tick = nullptr;

@@ -133,7 +133,8 @@ struct TlogArgs {
 
 // A slot named twice in one device batch breaks the one-delta-per-key
 // contract: both deltas are skipped (counted once), the key is left untouched.
-// dptr[] and bad[] are cleared before this launch.
+// dptr[] is all kNone on entry (k_tlog_unclaim restores that after the
+// merge's last reader); bad[] is cleared before this launch.
 __global__ __launch_bounds__(kThreads) void k_tlog_prep(TlogArgs A) {
   const u64 k = gid();
   if (k >= A.nd) return;
@@ -144,6 +145,14 @@ __global__ __launch_bounds__(kThreads) void k_tlog_prep(TlogArgs A) {
     A.bad[k] = 1;
     A.bad[prev] = 1;
   }
+}
+
+// after k_tlog_tile (dptr's last reader): the batch's slots back to kNone
+__global__ __launch_bounds__(kThreads) void k_tlog_unclaim(const u32* __restrict__ slot, u64 nd, u32* __restrict__ dptr) {
+  const u64 k = gid();
+  if (k >= nd) return;
+  const u32 s = slot[k];
+  if (s != JY_NO_SLOT) dptr[s] = kNone;  // every copy of a repeated slot writes the same value
 }
 
 // first position in [lo, hi) of the log at pool[base..] whose timestamp is
@@ -959,8 +968,19 @@ int32_t jy_tlog_merge_into(jy_engine* eng, TlogState& t, u64 nd, const u32* slot
   A.dlr = dlr;
   A.skipped = reinterpret_cast<unsigned long long*>(eng->skipped_dev);
   void* p;
-  JY_TRY(jy_scratch(eng, 8, nk * 4, &p));
-  A.dptr = static_cast<u32*>(p);
+  {
+    DevArray& c = eng->tl_claim;
+    if (c.bytes < nk * 4) {  // grows rarely: the whole array (re)set to kNone once
+      const u64 nb = std::max<u64>(nk * 4, c.bytes * 2);
+      jy_dev_free(eng, c.p);
+      c.p = nullptr;
+      c.bytes = 0;
+      JY_TRY(jy_dev_alloc(eng, &c.p, nb, "tlog slot claims"));
+      c.bytes = nb;
+      JY_HIP(eng, hipMemsetAsync(c.p, 0xFF, nb, eng->stream));
+    }
+    A.dptr = static_cast<u32*>(c.p);
+  }
   JY_TRY(jy_scratch(eng, 9, nd * (sizeof(PInfo) + 12) + 64, &p));
   A.pinfo = static_cast<PInfo*>(p);
   A.bad = reinterpret_cast<u32*>(A.pinfo + nd);
@@ -972,13 +992,13 @@ int32_t jy_tlog_merge_into(jy_engine* eng, TlogState& t, u64 nd, const u32* slot
   u32* erank = static_cast<u32*>(p);
   u32* eqx = erank + std::max<u64>(nent, 1);
   const u32 tiles = (u32)((nd + kTile - 1) / kTile);
-  JY_HIP(eng, hipMemsetAsync(A.dptr, 0xFF, nk * 4, eng->stream));
   JY_HIP(eng, hipMemsetAsync(A.bad, 0, nd * 4, eng->stream));
   LAUNCH(k_tlog_prep, nd, A);
   A.meta = t.meta;
   A.pool = t.pool;
   hipLaunchKernelGGL(k_tlog_tile, dim3(tiles), dim3(kTile), 0, eng->stream, A, t.pool, erank, eqx);
   JY_HIP(eng, hipGetLastError());
+  LAUNCH(k_tlog_unclaim, nd, slot, nd, A.dptr);
   JY_TRY((jydscan::scan<jydscan::OpSum, false>(eng, nd + 1, jydscan::LdArr<u32>{A.rz}, jydscan::StArr<u64>{roff})));
   if (t.used_bound + need <= t.pcap) {
     t.used_bound += need;

@@ -95,7 +95,7 @@ def test_malformed_delta_is_skipped(engine):
     assert vv[1].sum() == 0
 
 
-@pytest.mark.parametrize("R", [16, 4])
+@pytest.mark.parametrize("R", [16, 4, 40])  # R = 40: vv rows wider than a doc tile row batch
 def test_synthetic_zipf(oracle_mod, R):
     """config-5 shaped stream at 3000 docs: Zipf(1.1) popularity, INS/RM/CLR mix"""
     from jylis_amd import synth as S
