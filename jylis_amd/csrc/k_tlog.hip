@@ -128,6 +128,7 @@ struct TlogArgs {
   PInfo* pinfo;   // [nd] written for rebuilt and inserted keys only
   u32* rz;        // [nd + 1] pool entries a rebuilt key takes (0 otherwise)
   u32* ins;       // [nd] 1: the key's delta interleaves with its log and fits its segment
+  u64* rsum;      // [tiles + 1] rebuilt pool entries per key tile (scanned in place before k_tlog_commit)
   unsigned long long* skipped;
 };
 
@@ -473,6 +474,10 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
     A.rz[k0 + tid] = mode == kRebuild ? P.cap : 0u;
     A.ins[k0 + tid] = mode == kInsert;
   }
+  {  // the tile's rebuilt space: k_tlog_commit offsets its keys from the scan of these
+    const u64 r = jyscan::wave_sum<u64>(tid < nt && mode == kRebuild ? (u64)P.cap : 0ull);
+    if (tid == 0) A.rsum[blockIdx.x] = r;
+  }
   __syncthreads();
   // 4. appends: kept entries of append keys go to the tail, oldest first
   pass = 0;
@@ -514,7 +519,7 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
 // state entry is read (in its own pass, or an earlier one) before anything
 // is written over it: a pass's loads all return before its stores (one wave),
 // and a state entry only moves up.
-__global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __restrict__ roff,
+__global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __restrict__ rtile,
                                                        const u64* __restrict__ ctr, TRec* __restrict__ pool,
                                                        const u32* __restrict__ erank, const u32* __restrict__ eqx) {
   __shared__ u64 l_woff[kTile + 1];
@@ -526,12 +531,13 @@ __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __
   const u32 cap = tid < nt ? A.rz[k0 + tid] : 0u;
   const u32 ins = tid < nt ? A.ins[k0 + tid] : 0u;
   if (__ballot(cap != 0 || ins != 0) == 0) return;
+  const u64 roff_k = rtile[blockIdx.x] + jyscan::wave_incl<u64>(cap) - cap;  // the key's rebuilt space
   u32 w = 0;
   if (cap || ins) {
     const u64 k = k0 + tid;
     const PInfo P = A.pinfo[k];
     const u64 src = A.meta[P.s].base;  // current (a compaction may have moved the log)
-    const u64 dst = ins ? src + P.drop : ctr[0] + roff[k];
+    const u64 dst = ins ? src + P.drop : ctr[0] + roff_k;
     A.meta[P.s] = TMeta{dst, P.newlen, ins ? P.cap - P.drop : P.cap, P.cut, P.newest};
     const u64 blo = A.doff[k], bhi = A.doff[k + 1];
     l_src[tid] = src;
@@ -986,20 +992,24 @@ int32_t jy_tlog_merge_into(jy_engine* eng, TlogState& t, u64 nd, const u32* slot
   A.bad = reinterpret_cast<u32*>(A.pinfo + nd);
   A.rz = A.bad + nd;
   A.ins = A.rz + nd + 1;
-  JY_TRY(jy_scratch(eng, 16, (nd + 1) * 8, &p));
-  u64* roff = static_cast<u64*>(p);
+  const u32 tiles = (u32)((nd + kTile - 1) / kTile);
+  JY_TRY(jy_scratch(eng, 16, ((u64)tiles + 1) * 8, &p));
+  A.rsum = static_cast<u64*>(p);  // per key tile, then (scanned in place) each tile's offset; [tiles] = total
   JY_TRY(jy_scratch(eng, 12, std::max<u64>(nent, 1) * 8, &p));
   u32* erank = static_cast<u32*>(p);
   u32* eqx = erank + std::max<u64>(nent, 1);
-  const u32 tiles = (u32)((nd + kTile - 1) / kTile);
   JY_HIP(eng, hipMemsetAsync(A.bad, 0, nd * 4, eng->stream));
+  JY_HIP(eng, hipMemsetAsync(A.rsum + tiles, 0, 8, eng->stream));
   LAUNCH(k_tlog_prep, nd, A);
   A.meta = t.meta;
   A.pool = t.pool;
   hipLaunchKernelGGL(k_tlog_tile, dim3(tiles), dim3(kTile), 0, eng->stream, A, t.pool, erank, eqx);
   JY_HIP(eng, hipGetLastError());
   LAUNCH(k_tlog_unclaim, nd, slot, nd, A.dptr);
-  JY_TRY((jydscan::scan<jydscan::OpSum, false>(eng, nd + 1, jydscan::LdArr<u32>{A.rz}, jydscan::StArr<u64>{roff})));
+  // one offset per 64-key tile (a key's own offset is a wave prefix in k_tlog_commit): 64x fewer
+  // items than a scan over every key (61 -> a few us at 4M keys)
+  JY_TRY((jydscan::scan<jydscan::OpSum, false>(eng, (u64)tiles + 1, jydscan::LdArr<u64>{A.rsum},
+                                                jydscan::StArr<u64>{A.rsum})));
   if (t.used_bound + need <= t.pcap) {
     t.used_bound += need;
   } else {
@@ -1007,7 +1017,7 @@ int32_t jy_tlog_merge_into(jy_engine* eng, TlogState& t, u64 nd, const u32* slot
     // are published already; the rebuilt keys' logs are still in place, and
     // k_tlog_commit reads their bases after any compaction (which uses
     // scratch 17 and up, not this merge's).
-    JY_HIP(eng, hipMemcpyAsync(t.pin + 2, roff + nd, 8, hipMemcpyDeviceToHost, eng->stream));
+    JY_HIP(eng, hipMemcpyAsync(t.pin + 2, A.rsum + tiles, 8, hipMemcpyDeviceToHost, eng->stream));
     JY_HIP(eng, hipMemcpyAsync(t.pin, t.ctr, 8, hipMemcpyDeviceToHost, eng->stream));
     JY_HIP(eng, hipStreamSynchronize(eng->stream));
     const u64 rebuilt = t.pin[2];
@@ -1021,9 +1031,9 @@ int32_t jy_tlog_merge_into(jy_engine* eng, TlogState& t, u64 nd, const u32* slot
     t.used_bound += rebuilt;
   }
   t.live_bound += nent;
-  hipLaunchKernelGGL(k_tlog_commit, dim3(tiles), dim3(kTile), 0, eng->stream, A, roff, t.ctr, t.pool, erank, eqx);
+  hipLaunchKernelGGL(k_tlog_commit, dim3(tiles), dim3(kTile), 0, eng->stream, A, A.rsum, t.ctr, t.pool, erank, eqx);
   JY_HIP(eng, hipGetLastError());
-  hipLaunchKernelGGL(k_tlog_bump, dim3(1), dim3(1), 0, eng->stream, t.ctr, roff, nd);
+  hipLaunchKernelGGL(k_tlog_bump, dim3(1), dim3(1), 0, eng->stream, t.ctr, A.rsum, (u64)tiles);
   JY_HIP(eng, hipGetLastError());
   // publish the bump pointer for the next call (read back asynchronously)
   JY_HIP(eng, hipMemcpyAsync(t.pin, t.ctr, 8, hipMemcpyDeviceToHost, eng->stream));
