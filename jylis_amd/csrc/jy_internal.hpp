@@ -303,6 +303,10 @@ struct UjsonState {  // per-document pool segments + dense vv
   static constexpr int kRing = 4;
   hipEvent_t ready[kRing] = {};
   u64 ring_e[kRing] = {}, ring_c[kRing] = {};
+  // touched state elements / cloud dots of the newest finished converge (pin[2j ..]):
+  // sizes the item launches' grids (they stride over any excess)
+  u64 pred_ta = 0, pred_tc = 0;
+  bool has_pred = false;
   u64 seq = 0, done = 0;               // converges issued / absorbed
   u64 used_e = 0, used_c = 0;          // bump pointers after converge done - 1 (exact)
   u64 live_e = 0, live_c = 0;          // upper bounds of live elements / cloud dots

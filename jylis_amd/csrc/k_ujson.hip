@@ -129,7 +129,8 @@ struct UjArgs {
   URec* epool_out;
   u64* cpool_out;
   u64* ctr;          // bump pointers (device)
-  u64* pin;          // mapped pinned: [2..3] bump pointers after this converge
+  u64* pin;          // mapped pinned: bump pointers after this converge
+  u64* pin_t;        // mapped pinned: this converge's touched state elements / cloud dots
   u32 R;
   u32 epoch;
   u32 keep_all;      // context-only join: every state element stays (the write path's pending deltas)
@@ -533,12 +534,9 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_e
 // rank of an item is its merge position on the other side (relative to that
 // side's segment of the doc); bit 31 of a state element's rank: U5 takes the
 // delta's element for it.
-__global__ __launch_bounds__(kItemThreads) void k_uj_flags(UjArgs A) {
-  __shared__ u64 red[kItemThreads / 64];
+__device__ __forceinline__ void uj_flags_tile(const UjArgs& A, const u64 t, u64* red) {
   const u64 ta = A.ao[A.nd];
-  const u64 tA = cdiv(ta), tB = cdiv(A.nb), tC = cdiv(A.cb);
-  const u64 t = blockIdx.x;  // the grid is the host's bound: surplus workgroups exit
-  if (t >= tA + tB + tC) return;
+  const u64 tA = cdiv(ta), tB = cdiv(A.nb);
   JY_CLK(c0);
   int kind;
   u64 lt, n, gbase;
@@ -598,18 +596,26 @@ __global__ __launch_bounds__(kItemThreads) void k_uj_flags(UjArgs A) {
   if (threadIdx.x == 0) A.tp[t] = tot;
 }
 
+// item launches: the grid comes from the newest finished converge's touched
+// sizes (a prediction, not a bound); the workgroups stride over the tiles this
+// converge really has (read on the device), so a short grid stays exact.  The
+// host's safe bound (the live-element count) launched ~4x the real tiles,
+// and every surplus workgroup paid a dispatch and a dependent load to exit.
+__global__ __launch_bounds__(kItemThreads) void k_uj_flags(UjArgs A) {
+  __shared__ u64 red[kItemThreads / 64];
+  const u64 T = cdiv(A.ao[A.nd]) + cdiv(A.nb) + cdiv(A.cb);
+  for (u64 t = blockIdx.x; t < T; t += gridDim.x) uj_flags_tile(A, t, red);
+}
+
 // ---- U3: cloud compaction against the merged vv ---------------------------------
 // union rank of x (column c, seq q) above v: state dots of c in (v, q) plus
 // de-duplicated delta dots of c in (v, q) (U2's kind-2 flags); x folds into
 // the vv when the run from v + 1 reaches it unbroken
-__global__ __launch_bounds__(kItemThreads) void k_uj_compact(UjArgs A) {
-  __shared__ u64 red[kItemThreads / 64];
+__device__ __forceinline__ void uj_compact_tile(const UjArgs& A, const u64 t, u64* red) {
   const u64 ta = A.ao[A.nd], tc = A.co[A.nd];
   const ScanSp sp = sc_space(A);
   const u64 cb0 = ta + A.nb;  // the delta cloud dedupe prefix: sp.at(cb0 + b)
-  const u64 tA = cdiv(tc), tB = cdiv(A.cb);
-  const u64 t = blockIdx.x;
-  if (t >= tA + tB) return;
+  const u64 tA = cdiv(tc);
   JY_CLK(c0);
   const bool sa = t < tA;  // state cloud items, else delta cloud items
   const u64 lt = sa ? t : t - tA, n = sa ? tc : A.cb, gbase = sa ? 0 : tc;
@@ -670,6 +676,12 @@ __global__ __launch_bounds__(kItemThreads) void k_uj_compact(UjArgs A) {
   if (threadIdx.x == 0) A.ktp[t] = tot;
 }
 
+__global__ __launch_bounds__(kItemThreads) void k_uj_compact(UjArgs A) {
+  __shared__ u64 red[kItemThreads / 64];
+  const u64 T = cdiv(A.co[A.nd]) + cdiv(A.cb);
+  for (u64 t = blockIdx.x; t < T; t += gridDim.x) uj_compact_tile(A, t, red);
+}
+
 // ---- U4: output sizes per delta doc (scanned); the bump pointers move --------------
 __global__ __launch_bounds__(kThreads) void k_uj_sizes(UjArgs A, u64 ndt) {
   __shared__ Shared S;
@@ -716,22 +728,21 @@ __global__ __launch_bounds__(kThreads) void k_uj_sizes(UjArgs A, u64 ndt) {
     A.ctr[1] = cbb + tcl;
     A.pin[0] = eb + te;  // mapped host memory: the host's exact pool use once the converge is done
     A.pin[1] = cbb + tcl;
+    A.pin_t[0] = A.ao[A.nd];
+    A.pin_t[1] = A.co[A.nd];
   }
 }
 
 // ---- U5: scatter into the fresh runs; vv rows, metas; zero state for the next converge
 // (no scan: one item per thread; the grid is the host's bound, surplus
 // workgroups exit at once)
-__global__ __launch_bounds__(kItemThreads) void k_uj_scatter(UjArgs A) {
+__device__ __forceinline__ void uj_scatter_tile(const UjArgs& A, const u64 t) {
   const u64 ta = A.ao[A.nd], tc = A.co[A.nd];
   const ScanSp sp = sc_space(A), kp = ksc_space(A);
   const u32* xrb = A.xr + ta;
   const u32* krb = A.kr + tc;
   const u64 nv = A.nd * A.R;
   const u64 tl[6] = {cdiv(ta), cdiv(A.nb), cdiv(tc), cdiv(A.cb), cdiv(nv), cdiv(A.nd)};
-  const u64 t = blockIdx.x;
-  if (t == 0 && threadIdx.x == 0)
-    for (int c = T_U1; c <= T_U4; c++) A.tick[c] = 0;  // U1..U4 of this converge are done
   int kind = 0;
   u64 lt = t;
   while (kind < 6 && lt >= tl[kind]) lt -= tl[kind++];
@@ -787,6 +798,13 @@ __global__ __launch_bounds__(kItemThreads) void k_uj_scatter(UjArgs A) {
     const u64 pos = A.nco[k] + (si - kp.at(tc + A.dcoff[k])) + (kp.at(pa) - kp.at(A.co[k]));
     A.cpool_out[cb0 + pos] = A.dcloud[i];
   }
+}
+
+__global__ __launch_bounds__(kItemThreads) void k_uj_scatter(UjArgs A) {
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    for (int c = T_U1; c <= T_U4; c++) A.tick[c] = 0;  // U1..U4 of this converge are done
+  const u64 T = cdiv(A.ao[A.nd]) + cdiv(A.nb) + cdiv(A.co[A.nd]) + cdiv(A.cb) + cdiv(A.nd * A.R) + cdiv(A.nd);
+  for (u64 t = blockIdx.x; t < T; t += gridDim.x) uj_scatter_tile(A, t);
 }
 
 // ---- compaction: every document rewritten back to back into fresh pools ------------
@@ -976,6 +994,9 @@ void ujson_absorb(UjsonState& u) {
     if (hipEventQuery(u.ready[r]) == hipSuccess) {
       u.used_e = u.pin[8 + 2 * r];
       u.used_c = u.pin[9 + 2 * r];
+      u.pred_ta = u.pin[2 * r];
+      u.pred_tc = u.pin[1 + 2 * r];
+      u.has_pred = true;
       u.done = j;
       return;
     }
@@ -1125,6 +1146,7 @@ int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* sl
   A.ctr = u.ctr;
   const int slot_r = (int)(u.seq % UjsonState::kRing);
   A.pin = u.pin_dev + 8 + 2 * slot_r;
+  A.pin_t = u.pin_dev + 2 * slot_r;
   A.R = R;
   A.epoch = u.epoch;
   A.keep_all = keep_all;
@@ -1192,12 +1214,18 @@ int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* sl
   const u64 g1 = ndt + (nel + kTile1 - 1) / kTile1 + (ncloud + kTile1 - 1) / kTile1 + (nvv + kTile1 - 1) / kTile1;
   hipLaunchKernelGGL(k_uj_docs, dim3((u32)g1), dim3(kThreads), 0, eng->stream, A, ndt, (nel + kTile1 - 1) / kTile1,
                      (ncloud + kTile1 - 1) / kTile1, (nvv + kTile1 - 1) / kTile1);
-  hipLaunchKernelGGL(k_uj_flags, dim3((u32)tf), dim3(kItemThreads), 0, eng->stream, A);
+  // grids from the newest finished converge's touched sizes (+25 %), never above the safe bound
+  static const bool safe_grid = getenv("JY_UJ_SAFE_GRID") != nullptr;  // A/B: the bound's grid
+  const u64 pa = u.has_pred && !safe_grid ? std::min(le, u.pred_ta + u.pred_ta / 4 + 4096) : le;
+  const u64 pc = u.has_pred && !safe_grid ? std::min(lc, u.pred_tc + u.pred_tc / 4 + 4096) : lc;
+  const u64 gf = cdiv_h(pa) + cdiv_h(nel) + cdiv_h(ncloud) + 2;
+  const u64 gk = cdiv_h(pc) + cdiv_h(ncloud) + 2;
+  hipLaunchKernelGGL(k_uj_flags, dim3((u32)gf), dim3(kItemThreads), 0, eng->stream, A);
   hipLaunchKernelGGL(k_uj_tscan, dim3(1), dim3(1024), 0, eng->stream, A, 0);
-  hipLaunchKernelGGL(k_uj_compact, dim3((u32)tk), dim3(kItemThreads), 0, eng->stream, A);
+  hipLaunchKernelGGL(k_uj_compact, dim3((u32)gk), dim3(kItemThreads), 0, eng->stream, A);
   hipLaunchKernelGGL(k_uj_tscan, dim3(1), dim3(1024), 0, eng->stream, A, 1);
   hipLaunchKernelGGL(k_uj_sizes, dim3((u32)ndt), dim3(kThreads), 0, eng->stream, A, ndt);
-  const u64 g5 = tf + tk + (nd * R + kTile - 1) / kTile + (nd + kTile - 1) / kTile + 2;
+  const u64 g5 = gf + gk + (nd * R + kTile - 1) / kTile + (nd + kTile - 1) / kTile + 2;
   hipLaunchKernelGGL(k_uj_scatter, dim3((u32)g5), dim3(kItemThreads), 0, eng->stream, A);
   JY_HIP(eng, hipGetLastError());
 #ifdef JY_UJ_PROBE
