@@ -42,26 +42,49 @@ __device__ __forceinline__ u64 round_up8(u64 x) { return (x + kArenaAlign - 1) &
 //               along an owner's sequence)
 constexpr int kT = 256;  // entries per tile, one per thread
 
+// lanes with the same owner add their quantities with one LDS atomic per
+// owner and quantity (per-lane atomics serialise on one word when a wave's
+// entries share an owner: every lane at S = 1)
+template <int kQ>
+__device__ __forceinline__ void wave_add_by_owner(u32 o, bool valid, const u64 (&v)[kQ],
+                                                  unsigned long long* __restrict__ lc) {
+  u64 pending = __ballot(valid);
+  while (pending) {
+    const int leader = __ffsll((unsigned long long)pending) - 1;
+    const u32 lo = __shfl(o, leader);
+    const bool mine = valid && o == lo;
+    pending &= ~__ballot(mine);
+#pragma unroll
+    for (int q = 0; q < kQ; q++) {
+      const u64 sum = jyscan::wave_sum<u64>(mine ? v[q] : 0ull);
+      if (__lane_id() == (u32)leader && sum) atomicAdd(&lc[lo * kQ + q], (unsigned long long)sum);
+    }
+  }
+}
+
 __global__ __launch_bounds__(kT) void k_rt_count(const u32* __restrict__ owner, const u64* __restrict__ lr, u64 n,
                                                  u32 S, u64* __restrict__ tcnt) {
   __shared__ unsigned long long lc[kMaxShards * 2];
   for (u32 j = threadIdx.x; j < S * 2; j += kT) lc[j] = 0;
   __syncthreads();
   const u64 i = (u64)blockIdx.x * kT + threadIdx.x;
+  u32 o = S;
+  u64 v[2] = {0, 0};
   if (i < n) {
-    const u32 o = owner[i];
-    if (o < S) {
-      const u64 len = lr[i] & JY_LR_LEN_MASK;
-      atomicAdd(&lc[o * 2], 1ull);
-      if (len > 8) atomicAdd(&lc[o * 2 + 1], (unsigned long long)round_up8(len));
-    }
+    o = owner[i];
+    const u64 len = lr[i] & JY_LR_LEN_MASK;
+    v[0] = 1;
+    v[1] = len > 8 ? round_up8(len) : 0;
   }
+  wave_add_by_owner<2>(o, o < S, v, lc);  // one LDS atomic per (wave, owner, quantity)
   __syncthreads();
   u64* row = tcnt + (u64)blockIdx.x * S * 2;
   for (u32 j = threadIdx.x; j < S * 2; j += kT) row[j] = lc[j];
 }
 
-constexpr int kScanT = 1024, kScanPer = 4;  // a tile-count column per workgroup: 4096 tiles per round
+// a tile-count column per workgroup: 4096 tiles per round (8 per lane: 41 us
+// instead of 35 at 8M entries, measured and dropped)
+constexpr int kScanT = 1024, kScanPer = 4;
 __global__ __launch_bounds__(kScanT) void k_rt_tscan(u64* __restrict__ tcnt, u64 ntiles,
                                                      unsigned long long* __restrict__ hdr) {
   __shared__ u64 red[kScanT / 64];

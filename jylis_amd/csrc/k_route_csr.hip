@@ -120,6 +120,25 @@ __device__ __forceinline__ void key_quantities(const RouteArgs<kC>& A, u64 k, u6
 }
 
 // R1: per tile of keys, per destination totals; the key's long-value bytes
+// lanes with the same destination add their quantities with one LDS atomic
+// per destination and quantity
+template <int kQ>
+__device__ __forceinline__ void wave_add_by_owner(u32 o, bool valid, const u64 (&v)[kQ],
+                                                  unsigned long long* __restrict__ lc) {
+  u64 pending = __ballot(valid);
+  while (pending) {
+    const int leader = __ffsll((unsigned long long)pending) - 1;
+    const u32 lo = __shfl(o, leader);
+    const bool mine = valid && o == lo;
+    pending &= ~__ballot(mine);
+#pragma unroll
+    for (int q = 0; q < kQ; q++) {
+      const u64 sum = jyscan::wave_sum<u64>(mine ? v[q] : 0ull);
+      if (__lane_id() == (u32)leader && sum) atomicAdd(&lc[lo * kQ + q], (unsigned long long)sum);
+    }
+  }
+}
+
 template <int kC, bool kLR>
 __global__ __launch_bounds__(kThreads) void k_rc_count(RouteArgs<kC> A) {
   constexpr int kQ = 1 + kC + (kLR ? 1 : 0);
@@ -128,7 +147,6 @@ __global__ __launch_bounds__(kThreads) void k_rc_count(RouteArgs<kC> A) {
   __syncthreads();
   const u64 k = (u64)blockIdx.x * kThreads + threadIdx.x;
   if (k < A.n) {
-    const u32 o = A.owner[k];
     if (kLR) {
       const u64* lr = A.c[0].col[A.lr];
       u64 b = 0;
@@ -141,13 +159,15 @@ __global__ __launch_bounds__(kThreads) void k_rc_count(RouteArgs<kC> A) {
       }
       A.kb[k] = b;
     }
-    if (o < A.S) {
-      u64 v[kQ];
-      key_quantities<kC, kLR>(A, k, v);
-#pragma unroll
-      for (int q = 0; q < kQ; q++)
-        if (v[q]) atomicAdd(&lc[o * kQ + q], (unsigned long long)v[q]);
+  }
+  {
+    u32 o = A.S;
+    u64 v[kQ] = {};
+    if (k < A.n) {
+      o = A.owner[k];
+      if (o < A.S) key_quantities<kC, kLR>(A, k, v);
     }
+    wave_add_by_owner<kQ>(o, o < A.S, v, lc);  // one LDS atomic per (wave, owner, quantity)
   }
   __syncthreads();
   u64* row = A.tcnt + (u64)blockIdx.x * A.S * kQ;

@@ -201,13 +201,22 @@ class _RunRouter:
     asynchronously read global maximum.  Subclasses give the batch sizes,
     capacities, partition, merge and the overflow sub-batch."""
 
+    # rounds in flight before the host reads the oldest one's overflow: with
+    # 2, step i + 1 is enqueued while step i still runs (with 1 the host waited
+    # for every step before enqueuing the next, and the GPU idled through the
+    # host's enqueue).  A drain round merges after a later step's runs, which
+    # is exact: every join is commutative, associative and idempotent.  The
+    # caller keeps a step's batches alive until `depth` steps later (or drain()).
+    depth = 2
+
     def __init__(self, engines, fabric):
+        import collections
         self.engs = list(engines)
         self.fabric = fabric
         self.S = fabric.world
         assert len(self.engs) == len(fabric.ranks)
-        self.pending = None  # (batches, ovf tensors, pinned global max, event)
-        self._pins = None
+        self.pending = collections.deque()  # (batches, ovf tensors, pinned pairs, event), oldest first
+        self._pin_pool = []  # pinned (global max, own count) pairs per engine, reused
         self.routed = 0
         self.drains = 0
         self.bind()
@@ -217,15 +226,16 @@ class _RunRouter:
 
     def step(self, batches):
         _check_streams(self.engs)
-        self._settle(wait=True)
+        while len(self.pending) >= self.depth:
+            self._settle()
         ovfs = self._round(batches)
         self._publish(batches, ovfs)
 
     def drain(self):
         """route everything still pending (a collective: every rank calls it)"""
         _check_streams(self.engs)
-        while self.pending is not None:
-            self._settle(wait=True)
+        while self.pending:
+            self._settle()
 
     chunks = 1  # key-range chunks per round (CSR routers pipeline the exchange over them)
 
@@ -279,29 +289,27 @@ class _RunRouter:
         import torch
         gm = [o[:1].clone() for o in ovfs]
         self.fabric.max_all(gm)
-        if self._pins is None:
-            # one pinned pair per engine, reused: _settle reads it before the next _publish
-            self._pins = [torch.empty(2, dtype=torch.int32, pin_memory=True) for _ in ovfs]
-        pins = self._pins
+        # a pinned pair per engine for this round, back in the pool once settled
+        pins = self._pin_pool.pop() if self._pin_pool else [torch.empty(2, dtype=torch.int32, pin_memory=True)
+                                                            for _ in ovfs]
         for g, o, p in zip(gm, ovfs, pins):
             p[0:1].copy_(g, non_blocking=True)
             p[1:2].copy_(o[:1], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        self.pending = (batches, ovfs, pins, ev)
+        self.pending.append((batches, ovfs, pins, ev))
 
-    def _settle(self, wait):
-        """check the last round's overflow; run a drain round if any rank overflowed"""
-        if self.pending is None:
+    def _settle(self):
+        """check the oldest pending round's overflow; run a drain round if any rank overflowed"""
+        if not self.pending:
             return
-        batches, ovfs, pins, ev = self.pending
-        if not wait and not ev.query():
-            return
+        batches, ovfs, pins, ev = self.pending.popleft()
         ev.synchronize()
-        self.pending = None
-        if int(pins[0][0]) == 0:
+        gmax = int(pins[0][0])
+        counts = [int(p[1]) for p in pins]
+        self._pin_pool.append(pins)
+        if gmax == 0:
             return
-        counts = [int(p[1]) for p in pins]  # read before the drain round reuses the pinned pairs
         sub = [self._subset(b, o[1:1 + k].long()) for b, o, k in zip(batches, ovfs, counts)]
         m = self.fabric.host_max([np.array(self._sizes(s), np.int64) for s in sub])[0]
         # capacity = the whole overflow of the largest sender: nothing can overflow again
