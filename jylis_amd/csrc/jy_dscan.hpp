@@ -210,4 +210,29 @@ struct StArr {
   __device__ __forceinline__ void operator()(u64 i, u64 v) const { a[i] = (T)v; }
 };
 
+// a row-major [rows][W] matrix scanned column after column (column c's rows
+// are contiguous in the scan order); scan index rows * W is one extra word
+// after the matrix (the grand total of an exclusive scan)
+struct LdColMajor {
+  const u64* a;
+  u64 rows, W;
+  __device__ __forceinline__ u64 operator()(u64 f) const {
+    if (f >= rows * W) return 0;
+    const u64 c = f / rows;
+    return a[(f - c * rows) * W + c];
+  }
+};
+struct StColMajor {
+  u64* a;
+  u64 rows, W;
+  __device__ __forceinline__ void operator()(u64 f, u64 v) const {
+    if (f >= rows * W) {
+      a[rows * W] = v;
+      return;
+    }
+    const u64 c = f / rows;
+    a[(f - c * rows) * W + c] = v;
+  }
+};
+
 }  // namespace jydscan

@@ -20,6 +20,7 @@
 #include <algorithm>
 
 #include "jy_internal.hpp"
+#include "jy_dscan.hpp"
 #include "jy_scan.hpp"
 
 namespace {
@@ -31,8 +32,9 @@ __device__ __forceinline__ u64 round_up8(u64 x) { return (x + kArenaAlign - 1) &
 // Three passes, no same-address global atomics (one reservation atomic per
 // workgroup and owner serialised ~4k workgroups on one header word):
 //   k_rt_count  per tile of 256 entries: records and long-value bytes per owner
-//   k_rt_tscan  per (owner, quantity): exclusive scan over the tiles; the
-//               grand totals go to the header
+//   scan        every (owner, quantity) column of tile counts in one
+//               device-wide scan taken column after column (jy_dscan.hpp);
+//               k_rt_hdr takes the grand totals to the header
 //   k_rt_place  per entry: its place in its owner's run = tile base + the
 //               waves before it + its rank among its wave's entries for the
 //               same owner (one ballot per distinct owner, masked scans);
@@ -82,33 +84,14 @@ __global__ __launch_bounds__(kT) void k_rt_count(const u32* __restrict__ owner, 
   for (u32 j = threadIdx.x; j < S * 2; j += kT) row[j] = lc[j];
 }
 
-// a tile-count column per workgroup: 4096 tiles per round (8 per lane: 41 us
-// instead of 35 at 8M entries, measured and dropped)
-constexpr int kScanT = 1024, kScanPer = 4;
-__global__ __launch_bounds__(kScanT) void k_rt_tscan(u64* __restrict__ tcnt, u64 ntiles,
-                                                     unsigned long long* __restrict__ hdr) {
-  __shared__ u64 red[kScanT / 64];
-  const u32 col = blockIdx.x, width = gridDim.x;
-  u64 carry = 0;
-  for (u64 t0 = 0; t0 < ntiles; t0 += kScanT * kScanPer) {
-    u64 v[kScanPer], sum = 0;
-#pragma unroll
-    for (int u = 0; u < kScanPer; u++) {
-      const u64 t = t0 + (u64)threadIdx.x * kScanPer + u;
-      v[u] = t < ntiles ? tcnt[t * width + col] : 0;
-      sum += v[u];
-    }
-    u64 tot;
-    u64 x = jyscan::block_excl<kScanT, u64>(sum, red, tot) + carry;
-#pragma unroll
-    for (int u = 0; u < kScanPer; u++) {
-      const u64 t = t0 + (u64)threadIdx.x * kScanPer + u;
-      if (t < ntiles) tcnt[t * width + col] = x;
-      x += v[u];
-    }
-    carry += tot;
-  }
-  if (threadIdx.x == 0) hdr[col] = carry;  // hdr[2d] records, hdr[2d + 1] bytes
+
+// after the column-major device scan of tcnt (every column's prefix offset by
+// the columns before it): the header's totals per (owner, quantity)
+__global__ void k_rt_hdr(const u64* __restrict__ tcnt, u64 ntiles, u32 W, unsigned long long* __restrict__ hdr) {
+  const u32 c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= W) return;
+  const u64 hi = c + 1 < W ? tcnt[c + 1] : tcnt[ntiles * W];
+  hdr[c] = hi - tcnt[c];
 }
 
 __global__ __launch_bounds__(kT) void k_rt_place(const u32* __restrict__ owner, const u32* __restrict__ slot,
@@ -163,8 +146,8 @@ __global__ __launch_bounds__(kT) void k_rt_place(const u32* __restrict__ owner, 
   }
   __syncthreads();
   if (!valid) return;
-  const u64* tb = tcnt + (u64)blockIdx.x * S * 2 + o * 2;
-  u64 pos = tb[0] + rk, bpos = tb[1] + bk;
+  const u64* tb = tcnt + (u64)blockIdx.x * S * 2 + o * 2;  // less the column's base (row 0)
+  u64 pos = tb[0] - tcnt[o * 2] + rk, bpos = tb[1] - tcnt[o * 2 + 1] + bk;
   for (int w = 0; w < wv; w++) {
     pos += wt[w][o * 2];
     bpos += wt[w][o * 2 + 1];
@@ -230,9 +213,17 @@ int32_t jy_treg_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, co
   const u64* l = static_cast<const u64*>(dlr);
   hipLaunchKernelGGL(k_rt_count, dim3((u32)ntiles), dim3(kT), 0, eng->stream, own, l, n, nshards, tcnt);
   JY_HIP(eng, hipGetLastError());
-  hipLaunchKernelGGL(k_rt_tscan, dim3(nshards * 2), dim3(kScanT), 0, eng->stream, tcnt, ntiles,
-                     reinterpret_cast<unsigned long long*>(hdr_dev));
-  JY_HIP(eng, hipGetLastError());
+  {
+    // the tile counts of every (owner, quantity) column in ONE device-wide
+    // scan taken column after column (a workgroup per column walking its
+    // tiles took 35 us at 8M entries); each column's base is its row-0 entry
+    const u64 W = (u64)nshards * 2;
+    JY_TRY((jydscan::scan<jydscan::OpSum, false>(eng, ntiles * W + 1, jydscan::LdColMajor{tcnt, ntiles, W},
+                                                  jydscan::StColMajor{tcnt, ntiles, W})));
+    hipLaunchKernelGGL(k_rt_hdr, dim3(1), dim3(128), 0, eng->stream, tcnt, ntiles, (u32)W,
+                       reinterpret_cast<unsigned long long*>(hdr_dev));
+    JY_HIP(eng, hipGetLastError());
+  }
   hipLaunchKernelGGL(k_rt_place, dim3((u32)ntiles), dim3(kT), 0, eng->stream, own, static_cast<const u32*>(dsl),
                      static_cast<const u64*>(dts), static_cast<const u64*>(dpre), l, eng->arena[JY_TREG].p, n, nshards,
                      cap, cap_byte, tcnt, reinterpret_cast<unsigned long long*>(hdr_dev), recs_dev, bytes_dev, ovf_dev,

@@ -19,7 +19,8 @@
 // is always a hole that spans the run's unused entry capacity.
 //   R1 k_rc_count   per key tile: per destination totals (keys, entries per
 //                   CSR, long-value bytes)
-//   R2 k_rc_tscan   per (destination, quantity): exclusive scan over tiles
+//   R2 scan         every (destination, quantity) column of tile counts in
+//                   one device-wide scan, column after column; k_rc_hdr
 //   R3 k_rc_place   per key: its place in its destination's run (tile base
 //                   + wave ranks), fit test, key records
 //   R4 k_rc_copy    per entry: the entry columns into the key's run range,
@@ -39,6 +40,7 @@
 #include <algorithm>
 
 #include "jy_internal.hpp"
+#include "jy_dscan.hpp"
 #include "jy_scan.hpp"
 
 namespace {
@@ -174,35 +176,15 @@ __global__ __launch_bounds__(kThreads) void k_rc_count(RouteArgs<kC> A) {
   for (u32 j = threadIdx.x; j < A.S * kQ; j += kThreads) row[j] = lc[j];
 }
 
-// R2: one workgroup per (destination, quantity): exclusive scan over tiles;
-// the grand total goes to the header (every key placed, unless R3's first
-// key that does not fit overwrites it with the placed prefix)
-constexpr int kScanT = 1024, kScanPer = 4;  // a tile-count column per workgroup: 4096 tiles per round
-__global__ __launch_bounds__(kScanT) void k_rc_tscan(u64* __restrict__ tcnt, u64 ntiles, u32 kq,
-                                                     unsigned long long* __restrict__ hdr) {
-  __shared__ u64 red[kScanT / 64];
-  const u32 col = blockIdx.x, width = gridDim.x;
-  u64 carry = 0;
-  for (u64 t0 = 0; t0 < ntiles; t0 += kScanT * kScanPer) {
-    u64 v[kScanPer], sum = 0;
-#pragma unroll
-    for (int u = 0; u < kScanPer; u++) {
-      const u64 t = t0 + (u64)threadIdx.x * kScanPer + u;
-      v[u] = t < ntiles ? tcnt[t * width + col] : 0;
-      sum += v[u];
-    }
-    u64 tot;
-    u64 x = jyscan::block_excl<kScanT, u64>(sum, red, tot) + carry;
-#pragma unroll
-    for (int u = 0; u < kScanPer; u++) {
-      const u64 t = t0 + (u64)threadIdx.x * kScanPer + u;
-      if (t < ntiles) tcnt[t * width + col] = x;
-      x += v[u];
-    }
-    carry += tot;
-  }
-  if (threadIdx.x == 0) hdr[(col / kq) * 8 + col % kq] = carry;
+// R2 (as launched): one device-wide scan of the tile counts column after
+// column, then the header's totals from the column bases
+__global__ void k_rc_hdr(const u64* __restrict__ tcnt, u64 ntiles, u32 W, u32 kq, unsigned long long* __restrict__ hdr) {
+  const u32 c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= W) return;
+  const u64 hi = c + 1 < W ? tcnt[c + 1] : tcnt[ntiles * W];
+  hdr[(c / kq) * 8 + c % kq] = hi - tcnt[c];
 }
+
 
 // R3: the key's place in its run: tile base (R2) + the waves before it + its
 // rank among its wave's keys of the same destination (one ballot per
@@ -257,7 +239,7 @@ __global__ __launch_bounds__(kThreads) void k_rc_place(RouteArgs<kC> A) {
     u64 at[kQ];
 #pragma unroll
     for (int q = 0; q < kQ; q++) {
-      u64 x = tb[q] + pre[q];
+      u64 x = tb[q] - A.tcnt[o * kQ + q] + pre[q];  // less the column's base (row 0)
       for (int w = 0; w < wv; w++) x += wt[w][o * kQ + q];
       at[q] = x;
     }
@@ -438,8 +420,16 @@ int32_t route_part(jy_engine* eng, RouteArgs<kC>& A) {
     A.keo = static_cast<u64*>(p);
     hipLaunchKernelGGL((k_rc_count<kC, kLR>), dim3((u32)ntiles), dim3(kThreads), 0, eng->stream, A);
     JY_HIP(eng, hipGetLastError());
-    hipLaunchKernelGGL(k_rc_tscan, dim3(A.S * kQ), dim3(kScanT), 0, eng->stream, A.tcnt, ntiles, (u32)kQ, A.hdr);
-    JY_HIP(eng, hipGetLastError());
+    {
+      // every (destination, quantity) column in ONE device-wide scan taken
+      // column after column; each column's base is its row-0 entry
+      const u64 W = (u64)A.S * kQ;
+      JY_TRY((jydscan::scan<jydscan::OpSum, false>(eng, ntiles * W + 1, jydscan::LdColMajor{A.tcnt, ntiles, W},
+                                                    jydscan::StColMajor{A.tcnt, ntiles, W})));
+      hipLaunchKernelGGL(k_rc_hdr, dim3((u32)((W + 255) / 256)), dim3(256), 0, eng->stream, A.tcnt, ntiles, (u32)W,
+                         (u32)kQ, A.hdr);
+      JY_HIP(eng, hipGetLastError());
+    }
     hipLaunchKernelGGL((k_rc_place<kC, kLR>), dim3((u32)ntiles), dim3(kThreads), 0, eng->stream, A);
     JY_HIP(eng, hipGetLastError());
     // entry tiles per CSR: bounded by the host's totals
