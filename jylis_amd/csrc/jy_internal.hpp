@@ -250,7 +250,9 @@ struct TlogState {  // per-slot segments of one entry pool
   TRec* pool = nullptr;   // [pcap]
   u64 pcap = 0;
   u64* ctr = nullptr;     // device: [0] pool entries handed out (bump pointer)
-  u64* pin = nullptr;     // pinned readback of ctr[0]
+  u64* pin = nullptr;     // pinned readback of ctr[0] (mapped: [4..6] written by k_tlog_pub)
+  u64* pin_dev = nullptr; // device view of pin
+  u64 pub_seq = 0;        // k_tlog_pub's sequence number (pin[6])
   hipEvent_t ready = nullptr;
   bool known = false;     // pin holds the bump pointer after the last merge
   u64 used_bound = 0;     // host upper bound of ctr[0]

@@ -46,6 +46,7 @@
 
 
 #include <algorithm>
+#include <cstring>
 
 #include "jy_dscan.hpp"
 #include "jy_internal.hpp"
@@ -146,6 +147,15 @@ __global__ __launch_bounds__(kThreads) void k_tlog_prep(TlogArgs A) {
     A.bad[k] = 1;
     A.bad[prev] = 1;
   }
+}
+
+// the exact rebuild total and the bump pointer into mapped host memory, then
+// the sequence word the host waits on (system-scope release: the two words
+// are visible before it)
+__global__ void k_tlog_pub(const u64* __restrict__ total, const u64* __restrict__ ctr, u64* __restrict__ pin, u64 seq) {
+  pin[4] = *ctr;
+  pin[5] = *total;
+  __hip_atomic_store(pin + 6, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // after k_tlog_tile (dptr's last reader): the batch's slots back to kNone
@@ -923,7 +933,9 @@ int32_t tlog_grow_store(jy_engine* eng, TlogState& t, u64 need) {
   if (!t.ctr) {
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.ctr), 64, "tlog counters"));
     JY_HIP(eng, hipMemsetAsync(t.ctr, 0, 64, eng->stream));
-    JY_HIP(eng, hipHostMalloc(reinterpret_cast<void**>(&t.pin), 64, hipHostMallocDefault));
+    JY_HIP(eng, hipHostMalloc(reinterpret_cast<void**>(&t.pin), 64, hipHostMallocMapped));
+    std::memset(t.pin, 0, 64);
+    JY_HIP(eng, hipHostGetDevicePointer(reinterpret_cast<void**>(&t.pin_dev), t.pin, 0));
     JY_HIP(eng, hipEventCreateWithFlags(&t.ready, hipEventDisableTiming));
     t.pcap = std::max<u64>(eng->cfg.entry_capacity[JY_TLOG], 1024);
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.pool), t.pcap * sizeof(TRec), "tlog pool"));
@@ -1017,11 +1029,21 @@ int32_t jy_tlog_merge_into(jy_engine* eng, TlogState& t, u64 nd, const u32* slot
     // are published already; the rebuilt keys' logs are still in place, and
     // k_tlog_commit reads their bases after any compaction (which uses
     // scratch 17 and up, not this merge's).
-    JY_HIP(eng, hipMemcpyAsync(t.pin + 2, A.rsum + tiles, 8, hipMemcpyDeviceToHost, eng->stream));
-    JY_HIP(eng, hipMemcpyAsync(t.pin, t.ctr, 8, hipMemcpyDeviceToHost, eng->stream));
-    JY_HIP(eng, hipStreamSynchronize(eng->stream));
-    const u64 rebuilt = t.pin[2];
-    t.used_bound = t.pin[0];
+    // k_tlog_pub writes both words and then a sequence number into mapped
+    // host memory; the host spins on that word (a stream synchronize woke
+    // ~40 us after the scan ended: the GPU idled that long before the commit)
+    const u64 seq = ++t.pub_seq;
+    hipLaunchKernelGGL(k_tlog_pub, dim3(1), dim3(1), 0, eng->stream, A.rsum + tiles, t.ctr, t.pin_dev, seq);
+    JY_HIP(eng, hipGetLastError());
+    for (u64 spin = 0; __atomic_load_n(t.pin + 6, __ATOMIC_ACQUIRE) != seq; spin++) {
+      if ((spin & 1023) == 1023 && hipStreamQuery(eng->stream) != hipErrorNotReady) {  // done, or failed
+        if (__atomic_load_n(t.pin + 6, __ATOMIC_ACQUIRE) == seq) break;
+        JY_HIP(eng, hipStreamSynchronize(eng->stream));  // reports the stream's error
+        return eng->fail(JY_EINVAL, "tlog: the pool readback never arrived");
+      }
+    }
+    const u64 rebuilt = t.pin[5];
+    t.used_bound = t.pin[4];
     if (t.used_bound + rebuilt > t.pcap) {
       // room for this merge's rebuilds several times over
       JY_TRY(tlog_compact(eng, t, 4 * (rebuilt + nent)));
