@@ -359,7 +359,7 @@ struct jy_engine {
 
   // scratch (device) reused across calls, stream-ordered
   // 0-7 staged inputs, 8-14 and 16-23 merge temporaries, 15 scan temp storage
-  DevArray scratch[28];
+  DevArray scratch[32];
   // TLOG merge: the delta key claiming each slot (kNone between merges; a
   // merge resets only its batch's slots, so no per-merge memset over all keys)
   DevArray tl_claim;
