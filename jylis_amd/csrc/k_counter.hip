@@ -123,7 +123,7 @@ __global__ __launch_bounds__(kThreads) void k_cnt_add(u64* __restrict__ cell0, u
   if (i >= n) return;
   const u32 s = slot[i];
   atomicAdd(cell0 + s, val[i]);
-  if (atomicOr(dflag + s, bit) == 0u) atomicAdd(dcount, 1ull);
+  jy_wave_count(atomicOr(dflag + s, bit) == 0u, reinterpret_cast<unsigned long long*>(dcount));
 }
 
 // the delta records the post-write total (GCounter.increment writes

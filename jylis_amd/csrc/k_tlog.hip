@@ -815,7 +815,7 @@ __global__ __launch_bounds__(kThreads) void k_tlog_wprep(WCmd W, u64 n, const TM
   sflag[i] = ent;
   dcut[i] = changed ? raise : 0;
   dflag[i] = ent && changed;
-  if (atomicExch(pend + s, 1u) == 0) atomicAdd((unsigned long long*)pcount, 1ull);
+  jy_wave_count(atomicExch(pend + s, 1u) == 0, (unsigned long long*)pcount);
 }
 
 // the entries of the INS commands, packed for the state's delta (positions

@@ -89,7 +89,7 @@ struct TregK {
 // state; the delta key exists either way (oracle/jy_oracle.cpp or_treg_set)
 template <bool kCoh = false>
 __device__ __forceinline__ void set_one(const TregK& K, u32 s, u64 t, u64 p, u64 l) {
-  if (atomicOr(K.pflag + s, 1u) == 0u) atomicAdd(K.pcount, 1ull);
+  jy_wave_count(atomicOr(K.pflag + s, 1u) == 0u, reinterpret_cast<unsigned long long*>(K.pcount));
   const u64 t0 = ld64<kCoh>(K.ts + s);
   if (t < t0 || !lww_wins<kCoh>(t, t0, p, l, K.val, s, K.arena)) return;
   K.ts[s] = t;

@@ -63,7 +63,7 @@ __global__ __launch_bounds__(kThreads) void k_ujw_count(WArgs W, u64* __restrict
   }
   ne[i] = e;
   nc[i] = c;
-  if (atomicExch(pend + s, 1u) == 0) atomicAdd((unsigned long long*)pcount, 1ull);
+  jy_wave_count(atomicExch(pend + s, 1u) == 0, (unsigned long long*)pcount);
 }
 
 // the delta documents: elements, cloud (ascending: the state's elements are
