@@ -135,8 +135,8 @@ struct TlogArgs {
 
 // A slot named twice in one device batch breaks the one-delta-per-key
 // contract: both deltas are skipped (counted once), the key is left untouched.
-// dptr[] is all kNone on entry (k_tlog_unclaim restores that after the
-// merge's last reader); bad[] is cleared before this launch.
+// dptr[] is all kNone on entry (k_tlog_commit restores that after the
+// merge's last reader, k_tlog_tile); bad[] is cleared before this launch.
 __global__ __launch_bounds__(kThreads) void k_tlog_prep(TlogArgs A) {
   const u64 k = gid();
   if (k >= A.nd) return;
@@ -158,13 +158,6 @@ __global__ void k_tlog_pub(const u64* __restrict__ total, const u64* __restrict_
   __hip_atomic_store(pin + 6, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// after k_tlog_tile (dptr's last reader): the batch's slots back to kNone
-__global__ __launch_bounds__(kThreads) void k_tlog_unclaim(const u32* __restrict__ slot, u64 nd, u32* __restrict__ dptr) {
-  const u64 k = gid();
-  if (k >= nd) return;
-  const u32 s = slot[k];
-  if (s != JY_NO_SLOT) dptr[s] = kNone;  // every copy of a repeated slot writes the same value
-}
 
 // first position in [lo, hi) of the log at pool[base..] whose timestamp is
 // >= x (the log ascends): 16-ary probes, every probe of a round loaded at
@@ -540,6 +533,10 @@ __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __
   const u32 nt = (u32)(A.nd - k0 < kTile ? A.nd - k0 : kTile);
   const u32 cap = tid < nt ? A.rz[k0 + tid] : 0u;
   const u32 ins = tid < nt ? A.ins[k0 + tid] : 0u;
+  if (tid < nt) {  // the batch's slot claims back to kNone (k_tlog_tile, their last reader, is done)
+    const u32 s = A.slot[k0 + tid];
+    if (s != JY_NO_SLOT) A.dptr[s] = kNone;  // every copy of a repeated slot writes the same value
+  }
   if (__ballot(cap != 0 || ins != 0) == 0) return;
   const u64 roff_k = rtile[blockIdx.x] + jyscan::wave_incl<u64>(cap) - cap;  // the key's rebuilt space
   u32 w = 0;
@@ -1017,7 +1014,6 @@ int32_t jy_tlog_merge_into(jy_engine* eng, TlogState& t, u64 nd, const u32* slot
   A.pool = t.pool;
   hipLaunchKernelGGL(k_tlog_tile, dim3(tiles), dim3(kTile), 0, eng->stream, A, t.pool, erank, eqx);
   JY_HIP(eng, hipGetLastError());
-  LAUNCH(k_tlog_unclaim, nd, slot, nd, A.dptr);
   // one offset per 64-key tile (a key's own offset is a wave prefix in k_tlog_commit): 64x fewer
   // items than a scan over every key (61 -> a few us at 4M keys)
   JY_TRY((jydscan::scan<jydscan::OpSum, false>(eng, (u64)tiles + 1, jydscan::LdArr<u64>{A.rsum},
@@ -1046,8 +1042,12 @@ int32_t jy_tlog_merge_into(jy_engine* eng, TlogState& t, u64 nd, const u32* slot
     t.used_bound = t.pin[4];
     if (t.used_bound + rebuilt > t.pcap) {
       // room for this merge's rebuilds several times over
-      JY_TRY(tlog_compact(eng, t, 4 * (rebuilt + nent)));
-      if (t.used_bound + rebuilt > t.pcap) return eng->fail(JY_ENOMEM, "tlog pool: no room after compaction");
+      // a failure here skips k_tlog_commit, which would release the batch's slot claims
+      const int32_t rc = tlog_compact(eng, t, 4 * (rebuilt + nent));
+      if (rc != JY_OK || t.used_bound + rebuilt > t.pcap) {
+        hipMemsetAsync(A.dptr, 0xFF, nk * 4, eng->stream);
+        return rc != JY_OK ? rc : eng->fail(JY_ENOMEM, "tlog pool: no room after compaction");
+      }
       A.pool = t.pool;
     }
     t.used_bound += rebuilt;
