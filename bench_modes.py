@@ -297,7 +297,9 @@ def bench_treg(args, eng, dev, dist, rank, world):
     k = float(np.mean(kt))
     wf = float(np.mean(win)) if win else 0.5
     verified = None
-    if not routed:
+    if world == 1:  # (routed at world 1 too: its runs are merged against this shard)
+        if routed:
+            tr.drain()
         # sampled keys: LWW over every applied batch, (ts, value) with the
         # value order of Pony's String (bytewise, shorter first on a prefix)
         idx = np.random.default_rng(6).integers(0, n, 128)
