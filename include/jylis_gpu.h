@@ -219,6 +219,17 @@ int32_t jy_tlog_deltas_size(jy_engine* eng, uint64_t* n_out);  /* deltas_size();
 int32_t jy_tlog_flush(jy_engine* eng, uint64_t cap_keys, uint64_t cap_ent, uint32_t* slot_out,
                       uint64_t* cutoff_out, uint64_t* ent_offs_out, uint64_t* ts_out, uint64_t* pre_out,
                       uint64_t* lr_out, uint64_t* nkeys_out, uint64_t* nent_out, int32_t mem);
+/* Threading: a TLOG converge only enqueues.  Where a merge's rebuilt logs do
+ * not fit the entry pool, the device leaves those keys as they were and keeps
+ * their deltas; they are re-merged after a pool compaction by the next call
+ * that finds the merge finished, or by any call that reads TLOG state (reads,
+ * write commands, flush, jy_arena_collect, jy_sync), which waits for it.  A
+ * call that fails midway may have applied part of its batch; retrying it is
+ * safe (the join is idempotent). */
+/* telemetry of the state store (not on the reference's surface): [0] merges
+ * issued, [1] merges whose rebuilt logs were spilled and re-merged, [2] pool
+ * compactions, [3] pool capacity in entries */
+int32_t jy_tlog_stats(jy_engine* eng, uint64_t* out4);
 /* two-phase read: sizes (n entries per slot + cutoffs), then entries */
 int32_t jy_tlog_read_sizes(jy_engine* eng, uint64_t n, const uint32_t* slots, uint64_t* len_out,
                            uint64_t* cutoff_out);

@@ -83,6 +83,7 @@ SIGNATURES = {
     "jy_ujson_read_sizes": (I32, [P, U64, P, P, P]),
     "jy_ujson_read": (I32, [P, U64, P, P, P, P, P, P, P]),
     "jy_ujson_stats": (I32, [P, P]),
+    "jy_tlog_stats": (I32, [P, P]),
     "jy_arena_usage": (I32, [P, I32, P, P]),
     "jy_arena_collect": (I32, [P, I32, P]),
     "jy_tlog_write": (I32, [P, U64, P, P, P, P, P, P, I32]),

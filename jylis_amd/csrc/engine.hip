@@ -277,16 +277,16 @@ void jy_engine_destroy(jy_engine* eng) {
   F(eng->treg.seen[1]);
   F(eng->treg.dupn);
   F(eng->treg.dups);
-  F(eng->tlog.meta);
-  F(eng->tlog.pool);
-  F(eng->tlog.ctr);
-  if (eng->tlog.pin) hipHostFree(eng->tlog.pin);
-  if (eng->tlog.ready) hipEventDestroy(eng->tlog.ready);
-  F(eng->tlog_d.meta);
-  F(eng->tlog_d.pool);
-  F(eng->tlog_d.ctr);
-  if (eng->tlog_d.pin) hipHostFree(eng->tlog_d.pin);
-  if (eng->tlog_d.ready) hipEventDestroy(eng->tlog_d.ready);
+  for (TlogState* t : {&eng->tlog, &eng->tlog_d}) {
+    F(t->meta);
+    F(t->pool);
+    F(t->ctr);
+    if (t->pin) hipHostFree(t->pin);
+    for (auto& sp : t->spill) {
+      F(sp.buf.p);
+      if (sp.done) hipEventDestroy(sp.done);
+    }
+  }
   F(eng->tl_dflag);
   F(eng->tl_dcount);
   for (auto& k : eng->kdir) jy_keydir_free(eng, k);
@@ -360,6 +360,7 @@ void* jy_get_stream(jy_engine* eng) { return eng->stream; }
 
 int32_t jy_sync(jy_engine* eng) {
   JY_HIP(eng, hipSetDevice(eng->device));
+  JY_TRY(jy_tlog_settle(eng));  // spilled TLOG rebuilds re-merged: every converge has landed
   JY_HIP(eng, hipStreamSynchronize(eng->stream));
   return JY_OK;
 }

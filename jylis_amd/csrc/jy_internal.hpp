@@ -257,14 +257,30 @@ struct TlogState {  // per-slot segments of one entry pool
   TRec* pool = nullptr;   // [pcap]
   u64 pcap = 0;
   u64* ctr = nullptr;     // device: [0] pool entries handed out (bump pointer)
-  u64* pin = nullptr;     // pinned readback of ctr[0] (mapped: [4..6] written by k_tlog_pub)
+  u64* pin = nullptr;     // pinned, mapped: [0..7] compaction readback, [8 + 4 i ..] merge ring slot i
   u64* pin_dev = nullptr; // device view of pin
-  u64 pub_seq = 0;        // k_tlog_pub's sequence number (pin[6])
-  hipEvent_t ready = nullptr;
-  bool known = false;     // pin holds the bump pointer after the last merge
-  u64 used_bound = 0;     // host upper bound of ctr[0]
-  u64 live_bound = 0;     // host upper bound of live entries
   u64 kcap = 0;
+  // Merges never wait for the host: k_tlog_commit checks ON THE DEVICE that
+  // the merge's rebuilt logs fit the pool.  If they do not, it leaves those
+  // keys untouched and copies their deltas into the merge's spill buffer;
+  // the host re-merges the spill after a compaction once it sees the flag
+  // (the next merge call that finds the merge finished, or any call that
+  // reads the store, which waits for it).  A spill buffer per merge in
+  // flight; [kSpill] serves the re-merges, which settle synchronously.
+  static constexpr int kSpill = 2;
+  struct Spill {
+    DevArray buf;           // slot u32[nd] | cutoff, offsets u64[nd], [nd + 1] | ts, pre, lr u64[nent]
+    u64 nd = 0, nent = 0;   // the merge's batch shape
+    u64 seq = 0;            // merge number
+    bool busy = false;      // issued, not yet settled
+    hipEvent_t done = nullptr;
+  };
+  Spill spill[kSpill + 1];
+  u64 seq = 0;          // merges issued
+  u64 compact_seq = 0;  // merges issued before the newest compaction (their readback is stale)
+  u64 used = 0;         // bump pointer after the newest settled merge
+  u64 spills = 0;       // merges whose rebuilt keys were spilled and re-merged (telemetry)
+  u64 compactions = 0;
 };
 
 // one UJSON element: (dot, element handle), moved with one 16-B access
@@ -515,6 +531,9 @@ int32_t jy_tlog_merge(jy_engine* eng, u64 nkeys, const u32* slot, const u64* cut
 struct TlogState;
 int32_t jy_tlog_merge_into(jy_engine* eng, TlogState& t, u64 nd, const u32* slot, const u64* dcut, const u64* doff,
                            u64 nent, const u64* dts, const u64* dpre, const u64* dlr);
+// wait for every TLOG merge in flight (state and pending stores) and re-merge
+// any spilled rebuilds: every call that reads a TLOG store goes through this
+int32_t jy_tlog_settle(jy_engine* eng);
 // TLOG write path (k_tlog.hip): one command per key (device arrays)
 int32_t jy_tlog_write_batch(jy_engine* eng, u64 n, const uint8_t* op, const u32* slot, const u64* ts, const u64* arg,
                             const u64* pre, const u64* lr);

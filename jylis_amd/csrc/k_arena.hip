@@ -127,6 +127,7 @@ extern "C" int32_t jy_arena_usage(jy_engine* eng, int32_t type, uint64_t* len_ou
 extern "C" int32_t jy_arena_collect(jy_engine* eng, int32_t type, uint64_t* live_out) {
   JY_HIP(eng, hipSetDevice(eng->device));
   if (type != JY_TREG && type != JY_TLOG) return eng->fail(JY_EINVAL, "only TREG and TLOG hold an arena");
+  if (type == JY_TLOG) JY_TRY(jy_tlog_settle(eng));  // a spilled merge's handles are live too
   Arena& a = eng->arena[type];
   *live_out = 0;
   if (a.len == 0) return JY_OK;

@@ -34,10 +34,16 @@
 //   k_tlog_commit  publish the new meta; rebuilt keys are written into the
 //                  fresh space the scan of their sizes gave them, one lane
 //                  per output entry (merge-path positions from the ranks)
-// Pool space for rebuilt keys is only known on the device after that scan.
-// The host keeps an upper bound of the bump pointer; when the worst case may
-// not fit, it waits for the scan, reads the exact total and, if the pool is
-// really short, compacts and re-plans (nothing is published before commit).
+// Pool space for rebuilt keys is only known on the device after that scan,
+// so the host never waits for it: k_tlog_commit checks on the device that the
+// rebuilt logs fit the pool.  If they do not, those keys are left untouched
+// and their deltas are copied into the merge's spill buffer; the host sees
+// the flag once the merge has finished (the next merge call, or any call
+// that reads the store), compacts the pool and re-merges the spill -- exact,
+// since the join is commutative, associative and idempotent.  Appends and
+// in-place inserts are published by the tile / commit passes themselves, so
+// a call that fails midway may have applied part of its batch (retrying it
+// is safe for the same reason).
 //
 // Roofline: HBM.  An append-path delta entry costs 24 B read + 32 B written;
 // per delta key 32 B meta read + 32 B written + a 48-B plan record written
@@ -131,6 +137,12 @@ struct TlogArgs {
   u32* ins;       // [nd] 1: the key's delta interleaves with its log and fits its segment
   u64* rsum;      // [tiles + 1] rebuilt pool entries per key tile (scanned in place before k_tlog_commit)
   unsigned long long* skipped;
+  // the device-side pool check: when the rebuilt logs do not fit pcap, the
+  // rebuilt keys' deltas go to the spill (the batch's shape: slot JY_NO_SLOT
+  // for every other key, the same offsets, only the rebuilt keys' entries)
+  u64 pcap;
+  u32* sp_slot;
+  u64 *sp_cut, *sp_off, *sp_ts, *sp_pre, *sp_lr;
 };
 
 // A slot named twice in one device batch breaks the one-delta-per-key
@@ -148,16 +160,6 @@ __global__ __launch_bounds__(kThreads) void k_tlog_prep(TlogArgs A) {
     A.bad[prev] = 1;
   }
 }
-
-// the exact rebuild total and the bump pointer into mapped host memory, then
-// the sequence word the host waits on (system-scope release: the two words
-// are visible before it)
-__global__ void k_tlog_pub(const u64* __restrict__ total, const u64* __restrict__ ctr, u64* __restrict__ pin, u64 seq) {
-  pin[4] = *ctr;
-  pin[5] = *total;
-  __hip_atomic_store(pin + 6, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 
 // first position in [lo, hi) of the log at pool[base..] whose timestamp is
 // >= x (the log ascends): 16-ary probes, every probe of a round loaded at
@@ -326,7 +328,7 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
       u32 drop = 0;
       if (cd > m.cut && m.len > 0) drop = ts_lower(A.pool, m.base, 0, m.len, cut);  // oldest first: a prefix
       l_oldest[tid] = m.len > drop ? A.pool[m.base + drop].ts : 0;  // for the interpolated searches
-      sc = ne;
+      sc = hole ? 0 : ne;  // a hole's entries (a spill's unspilled keys) are never walked
       l_base[tid] = m.base;
       l_newest[tid] = m.newest;
       l_cut[tid] = cut;
@@ -531,11 +533,32 @@ __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __
   const u32 tid = threadIdx.x;
   const u64 k0 = (u64)blockIdx.x * kTile;
   const u32 nt = (u32)(A.nd - k0 < kTile ? A.nd - k0 : kTile);
-  const u32 cap = tid < nt ? A.rz[k0 + tid] : 0u;
+  u32 cap = tid < nt ? A.rz[k0 + tid] : 0u;
   const u32 ins = tid < nt ? A.ins[k0 + tid] : 0u;
+  u32 s = JY_NO_SLOT;
   if (tid < nt) {  // the batch's slot claims back to kNone (k_tlog_tile, their last reader, is done)
-    const u32 s = A.slot[k0 + tid];
+    s = A.slot[k0 + tid];
     if (s != JY_NO_SLOT) A.dptr[s] = kNone;  // every copy of a repeated slot writes the same value
+  }
+  // the pool check (uniform: k_tlog_bump moves ctr only after every tile)
+  if (ctr[0] + rtile[gridDim.x] > A.pcap) {
+    // no room for this merge's rebuilt logs: they stay as they are and their
+    // deltas go to the spill, which the host re-merges after a compaction
+    if (tid < nt) {
+      const u64 k = k0 + tid;
+      const u64 b0 = A.doff[k], b1 = A.doff[k + 1];
+      A.sp_slot[k] = cap ? s : JY_NO_SLOT;
+      A.sp_cut[k] = A.dcut[k];
+      A.sp_off[k] = b0;
+      if (k + 1 == A.nd) A.sp_off[A.nd] = b1;
+      if (cap)
+        for (u64 j = b0; j < b1; j++) {
+          A.sp_ts[j] = A.dts[j];
+          A.sp_pre[j] = A.dpre[j];
+          A.sp_lr[j] = A.dlr[j];
+        }
+    }
+    cap = 0;  // in-place inserts still go ahead
   }
   if (__ballot(cap != 0 || ins != 0) == 0) return;
   const u64 roff_k = rtile[blockIdx.x] + jyscan::wave_incl<u64>(cap) - cap;  // the key's rebuilt space
@@ -627,7 +650,18 @@ __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __
   }
 }
 
-__global__ void k_tlog_bump(u64* __restrict__ ctr, const u64* __restrict__ roff, u64 nd) { ctr[0] += roff[nd]; }
+// the bump pointer moves only if the rebuilt logs were written (the same
+// check as k_tlog_commit's); the outcome goes to the merge's words of mapped
+// host memory: bump pointer after it, rebuilt entries, 1 if spilled
+__global__ void k_tlog_bump(u64* __restrict__ ctr, const u64* __restrict__ roff, u64 tiles, u64 pcap,
+                            u64* __restrict__ pin) {
+  const u64 total = roff[tiles];
+  const bool over = ctr[0] + total > pcap;
+  if (!over) ctr[0] += total;
+  __hip_atomic_store(pin, ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(pin + 1, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(pin + 2, (u64)over, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 constexpr u32 kTileOut = 2048;
 
@@ -902,9 +936,10 @@ int32_t tlog_compact(jy_engine* eng, TlogState& t, u64 room) {
   *t.pin = total;
   JY_HIP(eng, hipMemcpyAsync(t.ctr, t.pin, 8, hipMemcpyHostToDevice, eng->stream));
   JY_HIP(eng, hipStreamSynchronize(eng->stream));  // pin is reused right away
-  t.used_bound = total;
-  t.live_bound = live;
-  t.known = false;
+  t.used = total;
+  t.compact_seq = t.seq;
+  t.compactions++;
+  (void)live;
   JY_TRACE("tlog compact: %llu entries, pool %llu, %.1f us", (unsigned long long)total, (unsigned long long)ncap,
            jy_now_us() - t_enter);
   return JY_OK;
@@ -930,10 +965,11 @@ int32_t tlog_grow_store(jy_engine* eng, TlogState& t, u64 need) {
   if (!t.ctr) {
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.ctr), 64, "tlog counters"));
     JY_HIP(eng, hipMemsetAsync(t.ctr, 0, 64, eng->stream));
-    JY_HIP(eng, hipHostMalloc(reinterpret_cast<void**>(&t.pin), 64, hipHostMallocMapped));
-    std::memset(t.pin, 0, 64);
+    JY_HIP(eng, hipHostMalloc(reinterpret_cast<void**>(&t.pin), 8 * (8 + 4 * (TlogState::kSpill + 1)),
+                              hipHostMallocMapped));
+    std::memset(t.pin, 0, 8 * (8 + 4 * (TlogState::kSpill + 1)));
     JY_HIP(eng, hipHostGetDevicePointer(reinterpret_cast<void**>(&t.pin_dev), t.pin, 0));
-    JY_HIP(eng, hipEventCreateWithFlags(&t.ready, hipEventDisableTiming));
+    for (auto& sp : t.spill) JY_HIP(eng, hipEventCreateWithFlags(&sp.done, hipEventDisableTiming));
     t.pcap = std::max<u64>(eng->cfg.entry_capacity[JY_TLOG], 1024);
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.pool), t.pcap * sizeof(TRec), "tlog pool"));
   }
@@ -962,16 +998,60 @@ int32_t jy_tlog_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* dcut, 
   return jy_tlog_merge_into(eng, eng->tlog, nd, slot, dcut, doff, nent, dts, dpre, dlr);
 }
 
-// the merge into one store: the state, or the pending deltas of the write path
-int32_t jy_tlog_merge_into(jy_engine* eng, TlogState& t, u64 nd, const u32* slot, const u64* dcut, const u64* doff,
-                           u64 nent, const u64* dts, const u64* dpre, const u64* dlr) {
-  const u64 nk = eng->nkeys[JY_TLOG];
-  if (nd == 0 || nk == 0) return JY_OK;
-  // worst case of fresh pool space this merge takes: every touched log
-  // rebuilt into pow2_cap(new length) <= 2 * kGrow * (length + 1) entries
-  const u64 need = 2 * kGrow * (t.live_bound + nent + nd) + 64;
-  if (t.known && hipEventQuery(t.ready) == hipSuccess) t.used_bound = *t.pin;
+namespace {
 
+// the slot claims a merge takes in k_tlog_prep are released by k_tlog_commit;
+// an error exit between the two releases them here (every later merge would
+// otherwise find those slots claimed and skip them)
+struct ClaimGuard {
+  jy_engine* eng;
+  u32* dptr;
+  u64 nk;
+  bool armed = true;
+  ~ClaimGuard() {
+    if (armed) (void)hipMemsetAsync(dptr, 0xFF, nk * 4, eng->stream);
+  }
+};
+
+// spill buffer views of ring slot r sized for (nd, nent)
+int32_t spill_reserve(jy_engine* eng, TlogState::Spill& sp, u64 nd, u64 nent) {
+  const u64 bytes = ((nd * 4 + 15) & ~15ull) + (2 * nd + 1) * 8 + 3 * std::max<u64>(nent, 1) * 8 + 64;
+  if (sp.buf.bytes < bytes) {
+    jy_dev_free(eng, sp.buf.p);
+    sp.buf.p = nullptr;
+    sp.buf.bytes = 0;
+    const u64 nb = std::max<u64>(bytes, sp.buf.bytes * 2);
+    JY_TRY(jy_dev_alloc(eng, &sp.buf.p, nb, "tlog spill"));
+    sp.buf.bytes = nb;
+  }
+  sp.nd = nd;
+  sp.nent = nent;
+  return JY_OK;
+}
+
+struct SpillView {
+  u32* slot;
+  u64 *cut, *off, *ts, *pre, *lr;
+};
+SpillView spill_view(const TlogState::Spill& sp) {
+  SpillView v;
+  v.slot = static_cast<u32*>(sp.buf.p);
+  v.cut = reinterpret_cast<u64*>(static_cast<char*>(sp.buf.p) + ((sp.nd * 4 + 15) & ~15ull));
+  v.off = v.cut + sp.nd;
+  v.ts = v.off + sp.nd + 1;
+  v.pre = v.ts + std::max<u64>(sp.nent, 1);
+  v.lr = v.pre + std::max<u64>(sp.nent, 1);
+  return v;
+}
+
+// enqueue one merge of a device batch into store t; spill ring slot r
+// receives its rebuilt keys if they do not fit the pool.  Never waits.
+int32_t tlog_launch(jy_engine* eng, TlogState& t, int r, u64 nd, const u32* slot, const u64* dcut, const u64* doff,
+                    u64 nent, const u64* dts, const u64* dpre, const u64* dlr) {
+  const u64 nk = eng->nkeys[JY_TLOG];
+  TlogState::Spill& sp = t.spill[r];
+  JY_TRY(spill_reserve(eng, sp, nd, nent));
+  const SpillView v = spill_view(sp);
   TlogArgs A{};
   A.arena = eng->arena[JY_TLOG].p;
   A.nd = nd;
@@ -982,6 +1062,13 @@ int32_t jy_tlog_merge_into(jy_engine* eng, TlogState& t, u64 nd, const u32* slot
   A.dpre = dpre;
   A.dlr = dlr;
   A.skipped = reinterpret_cast<unsigned long long*>(eng->skipped_dev);
+  A.pcap = t.pcap;
+  A.sp_slot = v.slot;
+  A.sp_cut = v.cut;
+  A.sp_off = v.off;
+  A.sp_ts = v.ts;
+  A.sp_pre = v.pre;
+  A.sp_lr = v.lr;
   void* p;
   {
     DevArray& c = eng->tl_claim;
@@ -1010,6 +1097,7 @@ int32_t jy_tlog_merge_into(jy_engine* eng, TlogState& t, u64 nd, const u32* slot
   JY_HIP(eng, hipMemsetAsync(A.bad, 0, nd * 4, eng->stream));
   JY_HIP(eng, hipMemsetAsync(A.rsum + tiles, 0, 8, eng->stream));
   LAUNCH(k_tlog_prep, nd, A);
+  ClaimGuard guard{eng, A.dptr, nk};
   A.meta = t.meta;
   A.pool = t.pool;
   hipLaunchKernelGGL(k_tlog_tile, dim3(tiles), dim3(kTile), 0, eng->stream, A, t.pool, erank, eqx);
@@ -1018,59 +1106,103 @@ int32_t jy_tlog_merge_into(jy_engine* eng, TlogState& t, u64 nd, const u32* slot
   // items than a scan over every key (61 -> a few us at 4M keys)
   JY_TRY((jydscan::scan<jydscan::OpSum, false>(eng, (u64)tiles + 1, jydscan::LdArr<u64>{A.rsum},
                                                 jydscan::StArr<u64>{A.rsum})));
-  if (t.used_bound + need <= t.pcap) {
-    t.used_bound += need;
-  } else {
-    // the worst case may not fit: wait for the exact rebuild size.  Appends
-    // are published already; the rebuilt keys' logs are still in place, and
-    // k_tlog_commit reads their bases after any compaction (which uses
-    // scratch 17 and up, not this merge's).
-    // k_tlog_pub writes both words and then a sequence number into mapped
-    // host memory; the host spins on that word (a stream synchronize woke
-    // ~40 us after the scan ended: the GPU idled that long before the commit)
-    const u64 seq = ++t.pub_seq;
-    hipLaunchKernelGGL(k_tlog_pub, dim3(1), dim3(1), 0, eng->stream, A.rsum + tiles, t.ctr, t.pin_dev, seq);
-    JY_HIP(eng, hipGetLastError());
-    for (u64 spin = 0; __atomic_load_n(t.pin + 6, __ATOMIC_ACQUIRE) != seq; spin++) {
-      if ((spin & 1023) == 1023 && hipStreamQuery(eng->stream) != hipErrorNotReady) {  // done, or failed
-        if (__atomic_load_n(t.pin + 6, __ATOMIC_ACQUIRE) == seq) break;
-        JY_HIP(eng, hipStreamSynchronize(eng->stream));  // reports the stream's error
-        return eng->fail(JY_EINVAL, "tlog: the pool readback never arrived");
-      }
-    }
-    const u64 rebuilt = t.pin[5];
-    t.used_bound = t.pin[4];
-    if (t.used_bound + rebuilt > t.pcap) {
-      // room for this merge's rebuilds several times over
-      // a failure here skips k_tlog_commit, which would release the batch's slot claims
-      const int32_t rc = tlog_compact(eng, t, 4 * (rebuilt + nent));
-      if (rc != JY_OK || t.used_bound + rebuilt > t.pcap) {
-        hipMemsetAsync(A.dptr, 0xFF, nk * 4, eng->stream);
-        return rc != JY_OK ? rc : eng->fail(JY_ENOMEM, "tlog pool: no room after compaction");
-      }
-      A.pool = t.pool;
-    }
-    t.used_bound += rebuilt;
-  }
-  t.live_bound += nent;
   hipLaunchKernelGGL(k_tlog_commit, dim3(tiles), dim3(kTile), 0, eng->stream, A, A.rsum, t.ctr, t.pool, erank, eqx);
   JY_HIP(eng, hipGetLastError());
-  hipLaunchKernelGGL(k_tlog_bump, dim3(1), dim3(1), 0, eng->stream, t.ctr, A.rsum, (u64)tiles);
+  guard.armed = false;  // k_tlog_commit released the claims
+  hipLaunchKernelGGL(k_tlog_bump, dim3(1), dim3(1), 0, eng->stream, t.ctr, A.rsum, (u64)tiles, t.pcap,
+                     t.pin_dev + 8 + 4 * r);
   JY_HIP(eng, hipGetLastError());
-  // publish the bump pointer for the next call (read back asynchronously)
-  JY_HIP(eng, hipMemcpyAsync(t.pin, t.ctr, 8, hipMemcpyDeviceToHost, eng->stream));
-  JY_HIP(eng, hipEventRecord(t.ready, eng->stream));
-  t.known = true;
+  JY_HIP(eng, hipEventRecord(sp.done, eng->stream));
+  sp.seq = ++t.seq;
+  sp.busy = true;
   return JY_OK;
 }
 
+// absorb the outcome of ring slot r's merge (waits for it); a spilled merge
+// is re-merged after a compaction sized for it
+int32_t tlog_absorb(jy_engine* eng, TlogState& t, int r) {
+  TlogState::Spill& sp = t.spill[r];
+  JY_HIP(eng, hipEventSynchronize(sp.done));
+  sp.busy = false;
+  const u64* w = t.pin + 8 + 4 * r;
+  const u64 used = __atomic_load_n(w, __ATOMIC_ACQUIRE), rebuilt = w[1], over = w[2];
+  if (sp.seq > t.compact_seq) t.used = used;
+  if (!over) return JY_OK;
+  // room for the spilled rebuilds several times over
+  t.spills++;
+  JY_TRACE("tlog: merge %llu spilled %llu rebuilt entries (pool %llu of %llu used)", (unsigned long long)sp.seq,
+           (unsigned long long)rebuilt, (unsigned long long)used, (unsigned long long)t.pcap);
+  JY_TRY(tlog_compact(eng, t, 4 * (rebuilt + sp.nent) + 1024));
+  const SpillView v = spill_view(sp);
+  constexpr int R = TlogState::kSpill;
+  JY_TRY(tlog_launch(eng, t, R, sp.nd, v.slot, v.cut, v.off, sp.nent, v.ts, v.pre, v.lr));
+  JY_HIP(eng, hipEventSynchronize(t.spill[R].done));
+  t.spill[R].busy = false;
+  const u64* w2 = t.pin + 8 + 4 * R;
+  if (w2[2]) return eng->fail(JY_ENOMEM, "tlog pool: no room for a spilled merge after compaction");
+  t.used = w2[0];
+  return JY_OK;
+}
+
+// absorb finished merges, oldest first; with `block`, every merge in flight
+int32_t tlog_reap(jy_engine* eng, TlogState& t, bool block) {
+  for (;;) {
+    int r = -1;
+    for (int i = 0; i < TlogState::kSpill; i++)
+      if (t.spill[i].busy && (r < 0 || t.spill[i].seq < t.spill[r].seq)) r = i;
+    if (r < 0) return JY_OK;
+    if (!block && hipEventQuery(t.spill[r].done) == hipErrorNotReady) return JY_OK;
+    JY_TRY(tlog_absorb(eng, t, r));
+  }
+}
+
+}  // namespace
+
+extern "C" int32_t jy_tlog_stats(jy_engine* eng, uint64_t* out4) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  const TlogState& t = eng->tlog;
+  out4[0] = t.seq;
+  out4[1] = t.spills;
+  out4[2] = t.compactions;
+  out4[3] = t.pcap;
+  return JY_OK;
+}
+
+int32_t jy_tlog_settle(jy_engine* eng) {
+  if (eng->tlog.ctr) JY_TRY(tlog_reap(eng, eng->tlog, true));
+  if (eng->tlog_d.ctr) JY_TRY(tlog_reap(eng, eng->tlog_d, true));
+  return JY_OK;
+}
+
+// the merge into one store: the state, or the pending deltas of the write path.
+// Only enqueues: no host wait unless every spill buffer is still in flight
+// (kSpill merges ahead of the GPU), when it waits for the oldest.
+int32_t jy_tlog_merge_into(jy_engine* eng, TlogState& t, u64 nd, const u32* slot, const u64* dcut, const u64* doff,
+                           u64 nent, const u64* dts, const u64* dpre, const u64* dlr) {
+  const u64 nk = eng->nkeys[JY_TLOG];
+  if (nd == 0 || nk == 0) return JY_OK;
+  JY_TRY(tlog_reap(eng, t, false));
+  int r = -1;
+  for (int i = 0; i < TlogState::kSpill && r < 0; i++)
+    if (!t.spill[i].busy) r = i;
+  if (r < 0) {  // every ring slot in flight: settle the oldest
+    r = 0;
+    for (int i = 1; i < TlogState::kSpill; i++)
+      if (t.spill[i].seq < t.spill[r].seq) r = i;
+    JY_TRY(tlog_absorb(eng, t, r));
+  }
+  return tlog_launch(eng, t, r, nd, slot, dcut, doff, nent, dts, dpre, dlr);
+}
+
 int32_t jy_tlog_sizes(jy_engine* eng, u64 n, const u32* slots, u64* len, u64* cut) {
+  JY_TRY(jy_tlog_settle(eng));
   TlogState& t = eng->tlog;
   LAUNCH(k_tlog_sizes, n, t.meta, slots, n, len, cut);
   return JY_OK;
 }
 
 int32_t jy_tlog_gather(jy_engine* eng, u64 n, const u32* slots, const u64* ooff, u64* ts, u64* pre, u64* lr) {
+  JY_TRY(jy_tlog_settle(eng));
   TlogState& t = eng->tlog;
   LAUNCH(k_tlog_gather, n, t.meta, t.pool, slots, ooff, n, ts, pre, lr);
   return JY_OK;
@@ -1099,6 +1231,8 @@ int32_t jy_tlog_write_batch(jy_engine* eng, u64 n, const uint8_t* op, const u32*
                             const u64* pre, const u64* lr) {
   if (n == 0) return JY_OK;
   JY_TRY(tlog_pending_grow(eng));
+  // every command is judged against the state as it is: no merge may still be pending
+  JY_TRY(jy_tlog_settle(eng));
   void* p;
   // (scratch 0..7 hold the staged commands; the merges use 8, 9, 12, 16)
   JY_TRY(jy_scratch(eng, 10, (n + 1) * 8 * 8 + 64, &p));
@@ -1140,6 +1274,7 @@ int32_t jy_tlog_pending(jy_engine* eng, u64* count) {
 int32_t jy_tlog_flush_dev(jy_engine* eng, u64 cap_keys, u64 cap_ent, u32* slots, u64* cut, u64* offs, u64* ts,
                           u64* pre, u64* lr, u64* nkeys, u64* nent) {
   u64 k = 0;
+  JY_TRY(jy_tlog_settle(eng));
   JY_TRY(jy_tlog_pending(eng, &k));
   *nkeys = k;
   *nent = 0;
@@ -1171,8 +1306,7 @@ int32_t jy_tlog_flush_dev(jy_engine* eng, u64 cap_keys, u64 cap_ent, u32* slots,
   JY_HIP(eng, hipMemsetAsync(eng->tl_dcount, 0, 8, eng->stream));
   // every pending key was flushed: the delta pool is empty again
   JY_HIP(eng, hipMemsetAsync(d.ctr, 0, 8, eng->stream));
-  d.used_bound = 0;
-  d.live_bound = 0;
-  d.known = false;
+  d.used = 0;
+  d.compact_seq = d.seq;
   return JY_OK;
 }

@@ -397,6 +397,12 @@ class Engine:
         del z
         return slots[:nk].copy(), cut[:nk].copy(), offs, ts[:ne].copy(), pre[:ne].copy(), lr[:ne].copy()
 
+    def tlog_stats(self):
+        """jy_tlog_stats: merges issued, spilled (re-merged after a compaction), compactions, pool capacity"""
+        out = np.zeros(4, np.uint64)
+        self._check(self.lib.jy_tlog_stats(self.h, out.ctypes.data))
+        return dict(zip(("merges", "spills", "compactions", "pool_entries"), (int(x) for x in out)))
+
     def tlog_read(self, slots):
         """-> (cutoff[n], offs[n+1], ts, pre, lr) for host slots"""
         s = np.ascontiguousarray(slots, np.uint32)

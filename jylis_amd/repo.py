@@ -7,9 +7,11 @@ surface as RepoAny (jylis/repo_manager.pony:5-10):
   converge(key, delta)        one (key, delta) pair   (repo_*.pony `converge`)
   converge_deltas(batch)      a whole decoded batch   (repo_manager.pony:92-93)
 
-but the batch form marshals the whole Array[(String, Any box)] into
-structure-of-arrays and makes ONE engine call, which is the change
-INTEGRATION.md describes for the Pony host.  Batches use the table layout of
+converge() queues the pair; the queue is marshalled into structure-of-arrays
+and merged in ONE engine call (converge_deltas) by the repo's next entry
+point -- deltas_size() on the heartbeat, flush_deltas(), reads, writes -- or
+at DRAIN_BOUND pairs.  That is the change INTEGRATION.md describes for the
+Pony host (pony/jylis_gpu/*.pony `_drain`).  Batches use the table layout of
 oracle/oracle.py (key_bytes/key_offs + per-type CSR columns), the decoded
 form of a MsgPushDeltas payload (jylis/msg.pony:20-24).
 
@@ -27,14 +29,44 @@ def _keys_of(table):
     return np.ascontiguousarray(table["key_bytes"], np.uint8), np.ascontiguousarray(table["key_offs"], np.uint64)
 
 
+# Queued (key, delta) pairs that force a drain without waiting for the next
+# entry point: bounds the host memory a read-idle replica holds between
+# heartbeats and the work one drain call does.
+DRAIN_BOUND = 1 << 16
+
+
+def concat_rows(pairs):
+    """[(key bytes, one-key delta table without key columns)] -> one batch
+    table: the marshalling of an Array[(String, Any box)] into SoA.  Every
+    `*offs` column is an offsets array (CSR, possibly nested: TLOG val_offs
+    counts bytes per entry) and is rebased; every other column concatenates."""
+    keys = [k for k, _ in pairs]
+    out = {"key_bytes": np.frombuffer(b"".join(keys), np.uint8).copy(),
+           "key_offs": np.concatenate([[0], np.cumsum([len(k) for k in keys])]).astype(np.uint64)}
+    for name in pairs[0][1]:
+        parts = [np.asarray(r[name]) for _, r in pairs]
+        if name.endswith("offs"):
+            res, base = [np.zeros(1, np.uint64)], 0
+            for p in parts:
+                p = p.astype(np.uint64)
+                res.append(p[1:] - p[0] + np.uint64(base))
+                base += int(p[-1] - p[0])
+            out[name] = np.concatenate(res)
+        else:
+            out[name] = np.concatenate(parts)
+    return out
+
+
 class _GpuRepo:
     ctype = None
 
-    def __init__(self, eng):
+    def __init__(self, eng, identity=None):
         self.eng = eng
+        self.identity = identity  # RepoXXX.create(identity') (repo_manager.pony:6)
         # slot -> key bytes (the engine interns; the host keeps names for reads),
         # one list per engine and type: every repo over the engine shares its slots
         self.names = eng.__dict__.setdefault("_slot_names", {}).setdefault(self.ctype, [])
+        self._in = []  # queued (key, delta) pairs of RepoAny.converge
 
     def _intern(self, table):
         kb, ko = _keys_of(table)
@@ -53,17 +85,33 @@ class _GpuRepo:
         return slots
 
     def slots_of(self, keys):
+        self._drain()
         return self.eng.lookup(self.ctype, keys)
 
-    def converge(self, key, delta_table_row):
-        """RepoXXX.converge(key, delta') for one pair (delta given as a 1-key table)."""
-        t = dict(delta_table_row)
+    def converge(self, key, delta_row):
+        """RepoAny.converge(key, delta') (repo_manager.pony:10), which
+        RepoManagerCore.converge_deltas calls once per pair (:92-93).  The pair
+        (delta = a one-key table without key columns) is queued; every queued
+        pair is merged in ONE engine call (converge_deltas) by the next entry
+        point -- reads, writes, deltas_size (the heartbeat's call,
+        repo_manager.pony:86-90), flush_deltas -- or once DRAIN_BOUND pairs
+        wait, so a replica that only receives still applies them every tick."""
         kb = key.encode() if isinstance(key, str) else bytes(key)
-        t["key_bytes"] = np.frombuffer(kb, np.uint8)
-        t["key_offs"] = np.array([0, len(kb)], np.uint64)
-        self.converge_deltas(t)
+        self._in.append((kb, delta_row))
+        if len(self._in) >= DRAIN_BOUND:
+            self._drain()
+
+    def _drain(self):
+        if self._in:
+            pairs, self._in = self._in, []
+            self.converge_deltas(concat_rows(pairs))
+
+    def pending_pairs(self):
+        """queued converge pairs not yet handed to the engine"""
+        return len(self._in)
 
     def _sorted_slots(self):
+        self._drain()
         order = sorted(range(len(self.names)), key=lambda s: self.names[s])
         return np.array(order, dtype=np.uint32)
 
@@ -112,9 +160,10 @@ class RepoGCOUNT(_GpuRepo):
         _counter_write(self, keys, vals, identity, 0)
 
     def deltas_size(self):
+        self._drain()
         return self.eng.counter_deltas_size(self.ctype)
 
-    def flush_deltas(self, identity):
+    def flush_deltas(self, identity=None):
         """flush_deltas (repo_gcount.pony:18-23) -> oracle-format batch table"""
         return _counter_flush(self, identity, ("",))
 
@@ -164,13 +213,15 @@ class RepoPNCOUNT(_GpuRepo):
         _counter_write(self, keys, vals, identity, 1)
 
     def deltas_size(self):
+        self._drain()
         return self.eng.counter_deltas_size(self.ctype)
 
-    def flush_deltas(self, identity):
+    def flush_deltas(self, identity=None):
         return _counter_flush(self, identity, ("p_", "n_"))
 
 
 def _counter_write(repo, keys, vals, identity, sign):
+    repo._drain()
     kb, ko = E.encode_keys(keys)
     slots = repo._intern({"key_bytes": kb, "key_offs": ko})
     v = np.asarray(vals)
@@ -179,6 +230,8 @@ def _counter_write(repo, keys, vals, identity, sign):
 
 
 def _counter_flush(repo, identity, prefixes):
+    repo._drain()
+    identity = repo.identity if identity is None else identity
     slots, vals, mask = repo.eng.counter_flush(repo.ctype)
     t = repo._keys_table(slots)
     rid = np.uint64(int(identity) & (2**64 - 1))
@@ -259,6 +312,7 @@ class RepoTREG(_ArenaGC, _GpuRepo):
     # -- local writes + flush_deltas (jy_treg_set / _flush) --
     def set(self, keys, values, ts):
         """TREG SET for a batch (repo_treg.pony:65-68); keys may repeat (in order)"""
+        self._drain()
         kb, ko = E.encode_keys(keys)
         slots = self._intern({"key_bytes": kb, "key_offs": ko})
         pre, lr = self.eng.pack_values(TREG, list(values))
@@ -266,10 +320,12 @@ class RepoTREG(_ArenaGC, _GpuRepo):
         self._maybe_collect()
 
     def deltas_size(self):
+        self._drain()
         return self.eng.treg_deltas_size()
 
     def flush_deltas(self):
         """flush_deltas (repo_treg.pony:18-22) -> oracle-format batch table"""
+        self._drain()
         slots, ts, pre, lr = self.eng.treg_flush()
         t = self._keys_table(slots)
         vb, vo = E.encode_keys([self.eng.value_bytes(TREG, p, l) for p, l in zip(pre, lr)])
@@ -329,6 +385,7 @@ class RepoTLOG(_ArenaGC, _GpuRepo):
         """a batch of TLOG write commands, applied in order (keys may repeat):
         ("INS", key, value, ts) | ("TRIMAT", key, ts) | ("TRIM", key, count) |
         ("CLR", key)  -- repo_tlog.pony:85-111"""
+        self._drain()
         if not cmds:
             return
         codes = {"INS": E._lib.TLOG_INS, "TRIMAT": E._lib.TLOG_TRIMAT, "TRIM": E._lib.TLOG_TRIM,
@@ -365,10 +422,12 @@ class RepoTLOG(_ArenaGC, _GpuRepo):
         self.write([("CLR", k) for k in keys])
 
     def deltas_size(self):
+        self._drain()
         return self.eng.tlog_deltas_size()
 
     def flush_deltas(self):
         """flush_deltas (repo_tlog.pony:21-25) -> oracle-format batch table"""
+        self._drain()
         slots, cut, offs, ts, pre, lr = self.eng.tlog_flush()
         t = self._keys_table(slots)
         vb, vo = E.encode_keys([self.eng.value_bytes(TLOG, p, l) for p, l in zip(pre, lr)])
@@ -418,6 +477,7 @@ class RepoUJSON(_GpuRepo):
         (repo_ujson.pony:86,108); TOUCH creates the key and its delta and
         changes nothing (SET of an empty node, a path-scoped CLR that matches
         nothing): an RM of handle 0, which no element holds"""
+        self._drain()
         codes = {"INS": E._lib.UJSON_INS, "RM": E._lib.UJSON_RM, "CLR": E._lib.UJSON_CLR,
                  "TOUCH": E._lib.UJSON_RM}
         live = []
@@ -440,10 +500,12 @@ class RepoUJSON(_GpuRepo):
         self.eng.ujson_write(ops, slots, elems, col)
 
     def deltas_size(self):
+        self._drain()
         return self.eng.ujson_deltas_size()
 
     def flush_deltas(self):
         """flush_deltas (repo_ujson.pony:22-26) -> oracle-format batch table"""
+        self._drain()
         slots, eo, dots, elems, vv, co, cloud = self.eng.ujson_flush()
         return self._docs_table(slots, eo, dots, elems, vv, co, cloud)
 

@@ -1,6 +1,6 @@
 """
 The engine handle and the marshalling every GPU repo shares (package jylis).
-UNBUILT here (no ponyc); see INTEGRATION.md.
+NOT COMPILE-CHECKED: unbuilt here (no ponyc); see INTEGRATION.md.
 
 A GPU repo holds `(_Engine | None)`: `RepoAny.create` (repo_manager.pony:6)
 is not partial, so a missing GPU is reported per call (`_Fail`), not at
@@ -15,6 +15,7 @@ class _Engine
   let ptr: Pointer[None] tag
   let _names: Array[String] = _names.create()    // slot -> key (slots are dense)
   let _col: U32                                   // this replica's column
+  var _arena_live: Array[U64] = Array[U64].init(0, 5)  // bytes kept by the last collect, per type
 
   new create(identity: U64, device: I32 = 0) ? =>
     let cfg = JyConfig
@@ -88,6 +89,22 @@ class _Engine
       for b in buf.values() do out.push(b) end
     end
     consume out
+
+  fun ref maybe_collect(ty: I32) =>
+    """Reclaim the TREG / TLOG value arena once dead bytes pass twice the
+    live ones (the policy of jylis_amd/repo.py _ArenaGC).  Call only after a
+    converge / SET / INS that consumed every handle it packed: collection
+    rewrites live handles and invalidates packed-but-unmerged ones."""
+    var n: U64 = 0
+    var cap: U64 = 0
+    if @jy_arena_usage(ptr, ty, addressof n, addressof cap) != 0 then return end
+    let live = try _arena_live(ty.usize())? else 0 end
+    if n > ((2 * live) + (1 << 20)) then
+      var kept: U64 = 0
+      if @jy_arena_collect(ptr, ty, addressof kept) == 0 then
+        try _arena_live(ty.usize())? = kept end
+      end
+    end
 
   fun _final() => @jy_engine_destroy(ptr)
 

@@ -1,6 +1,6 @@
 """
 FFI declarations of the MI355X engine (include/jylis_gpu.h), for package
-jylis.  UNBUILT in this repository: the image has no ponyc and jemc/pony-crdt
+jylis.  NOT COMPILE-CHECKED: UNBUILT in this repository: the image has no ponyc and jemc/pony-crdt
 is not vendored (DESIGN.md "Oracle").  Every @-call returns an I32 status
 (0 ok, negative JY_E*); pointers are borrowed for the duration of the call
 (JyHost memory: the engine stages host buffers itself).
@@ -26,6 +26,8 @@ use @jy_keys_lookup[I32](eng: Pointer[None] tag, ty: I32, n: U64,
 use @jy_values_pack[I32](eng: Pointer[None] tag, ty: I32, n: U64,
   bytes: Pointer[U8] tag, offs: Pointer[U64] tag, pre: Pointer[U64] tag, lr: Pointer[U64] tag)
 use @jy_arena_read[I32](eng: Pointer[None] tag, ty: I32, off: U64, len: U64, dst: Pointer[U8] tag)
+use @jy_arena_usage[I32](eng: Pointer[None] tag, ty: I32, len_out: Pointer[U64] tag, cap_out: Pointer[U64] tag)
+use @jy_arena_collect[I32](eng: Pointer[None] tag, ty: I32, live_out: Pointer[U64] tag)
 
 // ---- GCOUNT / PNCOUNT ---------------------------------------------------------
 use @jy_gcount_converge[I32](eng: Pointer[None] tag, n: U64, slot: Pointer[U32] tag,
@@ -102,6 +104,8 @@ primitive JyTLOG fun apply(): I32 => 3
 primitive JyUJSON fun apply(): I32 => 4
 primitive JyNoSlot fun apply(): U32 => U32.max_value()
 primitive JyDotSeqBits fun apply(): U64 => 48
+// queued converge pairs that force a drain before the next entry point
+primitive _DrainBound fun apply(): USize => 65536
 
 // struct jy_config (include/jylis_gpu.h): field order and widths match
 struct JyConfig

@@ -1,7 +1,7 @@
 """
 GPU-backed RepoGCOUNT / RepoPNCOUNT: drop-in replacements for
 jylis/repo_gcount.pony and jylis/repo_pncount.pony behind RepoAny
-(jylis/repo_manager.pony:5-10).  UNBUILT here (no ponyc); INTEGRATION.md.
+(jylis/repo_manager.pony:5-10).  NOT COMPILE-CHECKED: unbuilt here (no ponyc); INTEGRATION.md.
 
 * converge (repo_gcount.pony:50-51) queues the pair; the next entry point
   merges every queued pair in ONE engine call (RepoManagerCore.converge_deltas
@@ -31,6 +31,10 @@ class RepoGCOUNTGpu
     _eng = try _Engine(identity')? else None end
 
   fun ref deltas_size(): USize =>
+    """the heartbeat's call (repo_manager.pony:86-90): applies every queued
+    peer pair first, so a replica with no local commands still converges
+    each tick"""
+    _drain()
     match _eng
     | let e: _Engine =>
       var n: U64 = 0
@@ -41,6 +45,7 @@ class RepoGCOUNTGpu
 
   fun ref flush_deltas(): Array[(String, Any box)] box =>
     """repo_gcount.pony:18-23: every pending key with its post-write total"""
+    _drain()
     let out = Array[(String, Any box)]
     match _eng
     | let e: _Engine =>
@@ -56,7 +61,10 @@ class RepoGCOUNTGpu
     out
 
   fun ref converge(key: String, delta': Any box) =>
+    """RepoAny.converge, once per pair (repo_manager.pony:92-93): queue it;
+    a full queue is merged at once (bounded memory between heartbeats)"""
     _in.push((key, delta'))
+    if _in.size() >= _DrainBound() then _drain() end
 
   fun ref _drain() =>
     if _in.size() == 0 then return end
@@ -112,6 +120,10 @@ class RepoPNCOUNTGpu
     _eng = try _Engine(identity')? else None end
 
   fun ref deltas_size(): USize =>
+    """the heartbeat's call (repo_manager.pony:86-90): applies every queued
+    peer pair first, so a replica with no local commands still converges
+    each tick"""
+    _drain()
     match _eng
     | let e: _Engine =>
       var n: U64 = 0
@@ -122,6 +134,7 @@ class RepoPNCOUNTGpu
 
   fun ref flush_deltas(): Array[(String, Any box)] box =>
     """repo_pncount.pony:19-24"""
+    _drain()
     let out = Array[(String, Any box)]
     match _eng
     | let e: _Engine =>
@@ -139,7 +152,10 @@ class RepoPNCOUNTGpu
     out
 
   fun ref converge(key: String, delta': Any box) =>
+    """RepoAny.converge, once per pair (repo_manager.pony:92-93): queue it;
+    a full queue is merged at once (bounded memory between heartbeats)"""
     _in.push((key, delta'))
+    if _in.size() >= _DrainBound() then _drain() end
 
   fun ref _drain() =>
     if _in.size() == 0 then return end

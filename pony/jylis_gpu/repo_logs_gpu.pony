@@ -1,7 +1,7 @@
 """
 GPU-backed RepoTREG / RepoTLOG: drop-in replacements for jylis/repo_treg.pony
 and jylis/repo_tlog.pony behind RepoAny (jylis/repo_manager.pony:5-10).
-UNBUILT here (no ponyc); INTEGRATION.md.
+NOT COMPILE-CHECKED: unbuilt here (no ponyc); INTEGRATION.md.
 
 converge queues the pair and the next entry point merges the whole queue in
 one engine call (see repo_counters_gpu.pony).  Writes and flush_deltas run on
@@ -21,6 +21,10 @@ class RepoTREGGpu
     _eng = try _Engine(identity')? else None end
 
   fun ref deltas_size(): USize =>
+    """the heartbeat's call (repo_manager.pony:86-90): applies every queued
+    peer pair first, so a replica with no local commands still converges
+    each tick"""
+    _drain()
     match _eng
     | let e: _Engine =>
       var n: U64 = 0
@@ -31,6 +35,7 @@ class RepoTREGGpu
 
   fun ref flush_deltas(): Array[(String, Any box)] box =>
     """repo_treg.pony:18-22: every pending key with its delta register"""
+    _drain()
     let out = Array[(String, Any box)]
     match _eng
     | let e: _Engine =>
@@ -55,7 +60,10 @@ class RepoTREGGpu
     out
 
   fun ref converge(key: String, delta': Any box) =>
+    """RepoAny.converge, once per pair (repo_manager.pony:92-93): queue it;
+    a full queue is merged at once (bounded memory between heartbeats)"""
     _in.push((key, delta'))
+    if _in.size() >= _DrainBound() then _drain() end
 
   fun ref _drain() =>
     if _in.size() == 0 then return end
@@ -77,6 +85,7 @@ class RepoTREGGpu
             pre.cpointer(), lr.cpointer(), JyHost()))?
         end
       end
+      e.maybe_collect(JyTREG())
     end
     _in.clear()
 
@@ -116,6 +125,7 @@ class RepoTREGGpu
         var ts = timestamp
         e.check(@jy_treg_set(e.ptr, 1, slots.cpointer(), addressof ts, pre.cpointer(), lr.cpointer(),
           JyHost()))?
+        e.maybe_collect(JyTREG())
         resp.ok()
         true
       else _Fail(resp)
@@ -137,6 +147,10 @@ class RepoTLOGGpu
     _eng = try _Engine(identity')? else None end
 
   fun ref deltas_size(): USize =>
+    """the heartbeat's call (repo_manager.pony:86-90): applies every queued
+    peer pair first, so a replica with no local commands still converges
+    each tick"""
+    _drain()
     match _eng
     | let e: _Engine =>
       var n: U64 = 0
@@ -147,6 +161,7 @@ class RepoTLOGGpu
 
   fun ref flush_deltas(): Array[(String, Any box)] box =>
     """repo_tlog.pony:21-25: every pending key with its delta log"""
+    _drain()
     let out = Array[(String, Any box)]
     match _eng
     | let e: _Engine =>
@@ -177,7 +192,10 @@ class RepoTLOGGpu
     out
 
   fun ref converge(key: String, delta': Any box) =>
+    """RepoAny.converge, once per pair (repo_manager.pony:92-93): queue it;
+    a full queue is merged at once (bounded memory between heartbeats)"""
     _in.push((key, delta'))
+    if _in.size() >= _DrainBound() then _drain() end
 
   fun ref _drain() =>
     """every queued TLog delta in one jy_tlog_converge (CSR of entries)"""
@@ -206,6 +224,7 @@ class RepoTLOGGpu
             offs.cpointer(), vals.size().u64(), ts.cpointer(), pre.cpointer(), lr.cpointer(), JyHost()))?
         end
       end
+      e.maybe_collect(JyTLOG())
     end
     _in.clear()
 
@@ -237,6 +256,7 @@ class RepoTLOGGpu
       var c = count
       e.check(@jy_tlog_write(e.ptr, 1, addressof o, slots.cpointer(), addressof ts, addressof c,
         pre.cpointer(), lr.cpointer(), JyHost()))?
+      e.maybe_collect(JyTLOG())
       resp.ok()
       true
     else _Fail(resp)
@@ -252,7 +272,8 @@ class RepoTLOGGpu
       var len: U64 = 0
       var cut: U64 = 0
       @jy_tlog_read_sizes(e.ptr, 1, addressof slot, addressof len, addressof cut)
-      let offs: Array[U64] = [0; len]
+      let offs = Array[U64].init(0, 2)   // the one slot's CSR: [0, len]
+      try offs(1)? = len end
       let ts = Array[U64].init(0, len.usize().max(1))
       let pre = Array[U64].init(0, len.usize().max(1))
       let lr = Array[U64].init(0, len.usize().max(1))

@@ -1,6 +1,6 @@
 """
 GPU-backed RepoUJSON: drop-in replacement for jylis/repo_ujson.pony behind
-RepoAny (jylis/repo_manager.pony:5-10).  UNBUILT here (no ponyc);
+RepoAny (jylis/repo_manager.pony:5-10).  NOT COMPILE-CHECKED: unbuilt here (no ponyc);
 INTEGRATION.md.  The same layer in Python is jylis_amd/ujson_doc.py (tested).
 
 The engine keeps each document's observed-remove dot kernel over opaque u64
@@ -64,6 +64,10 @@ class RepoUJSONGpu
     h
 
   fun ref deltas_size(): USize =>
+    """the heartbeat's call (repo_manager.pony:86-90): applies every queued
+    peer pair first, so a replica with no local commands still converges
+    each tick"""
+    _drain()
     match _eng
     | let e: _Engine =>
       var n: U64 = 0
@@ -74,6 +78,7 @@ class RepoUJSONGpu
 
   fun ref flush_deltas(): Array[(String, Any box)] box =>
     """repo_ujson.pony:22-26: every pending doc with its delta document"""
+    _drain()
     let out = Array[(String, Any box)]
     match _eng
     | let e: _Engine =>
@@ -99,7 +104,7 @@ class RepoUJSONGpu
           let d = UJSON(0)
           for j in Range(eo(i)?.usize(), eo(i + 1)?.usize()) do
             (let p, let v) = _leaves(elems(j)?)?
-            d.from_dot(e.replica(dots(j)? >> JyDotSeqBits()), dots(j)? and 0xFFFFFFFFFFFF, p, v)
+            d.from_dot(e.replica((dots(j)? >> JyDotSeqBits()).u32()), dots(j)? and 0xFFFFFFFFFFFF, p, v)
           end
           for c in Range(0, r) do
             let n = vv((i * r) + c)?
@@ -115,7 +120,10 @@ class RepoUJSONGpu
     out
 
   fun ref converge(key: String, delta': Any box) =>
+    """RepoAny.converge, once per pair (repo_manager.pony:92-93): queue it;
+    a full queue is merged at once (bounded memory between heartbeats)"""
     _in.push((key, delta'))
+    if _in.size() >= _DrainBound() then _drain() end
 
   fun ref _drain() =>
     """every queued UJSON delta in one jy_ujson_converge"""
@@ -135,13 +143,17 @@ class RepoUJSONGpu
           match d'
           | let d: UJSON box =>
             keys.push(k)
-            // sorted per doc by (column, seq): the engine's segment order
-            let ds = Array[(U64, U64)]
+            // sorted per doc by packed dot (column, seq): the engine's segment
+            // order; a doc's dots are unique, so sort the dots and map back
+            let ds = Array[U64]
+            let hs = Map[U64, U64]
             for (id, seq, path, value) in d.dots() do
-              ds.push(((e.replica_col(id)?.u64() << JyDotSeqBits()) or seq, _handle(path, value)?))
+              let dot = (e.replica_col(id)?.u64() << JyDotSeqBits()) or seq
+              ds.push(dot)
+              hs(dot) = _handle(path, value)?
             end
-            for (dot, h) in Sort[Array[(U64, U64)], (U64, U64)](ds).values() do
-              dots.push(dot); elems.push(h)
+            for dot in Sort[Array[U64], U64](ds).values() do
+              dots.push(dot); elems.push(hs(dot)?)
             end
             eo.push(dots.size().u64())
             let vs = Array[U64]
@@ -190,8 +202,9 @@ class RepoUJSONGpu
     var ne: U64 = 0
     var nc: U64 = 0
     @jy_ujson_read_sizes(e.ptr, 1, addressof slot, addressof ne, addressof nc)
-    let eo: Array[U64] = [0; ne]
-    let co: Array[U64] = [0; nc]
+    let eo = Array[U64].init(0, 2)   // the one doc's CSRs: [0, ne], [0, nc]
+    let co = Array[U64].init(0, 2)
+    try eo(1)? = ne; co(1)? = nc end
     let dots = Array[U64].init(0, ne.usize().max(1))
     let elems = Array[U64].init(0, ne.usize().max(1))
     let vv = Array[U64].init(0, 16)

@@ -42,39 +42,10 @@ def random_history(O, ctype, seed, nrep=4, nops=300, nkeys=12, val_len=14, gossi
     keys = [f"k{i}" for i in range(nkeys)]
     batches = []
 
-    def rstr():
-        n = int(rng.integers(0, val_len))
-        # small alphabet -> many shared prefixes / ties
-        return bytes(rng.choice(np.frombuffer(b"aab\x00\xff", np.uint8), size=n))
-
     for _ in range(nops):
         r = reps[rng.integers(nrep)]
         k = keys[rng.integers(nkeys)]
-        if ctype == O.GCOUNT:
-            r.gcount_inc(k, int(rng.integers(0, 1 << 62)))
-        elif ctype == O.PNCOUNT:
-            v = int(rng.integers(-(1 << 62), 1 << 62))
-            (r.pncount_inc if rng.random() < 0.5 else r.pncount_dec)(k, v)
-        elif ctype == O.TREG:
-            r.treg_set(k, rstr(), int(rng.integers(0, 6)))
-        elif ctype == O.TLOG:
-            x = rng.random()
-            if x < 0.8:
-                r.tlog_ins(k, rstr(), int(rng.integers(0, 40)))
-            elif x < 0.9:
-                r.tlog_trimat(k, int(rng.integers(0, 30)))
-            elif x < 0.97:
-                r.tlog_trim(k, int(rng.integers(0, 8)))
-            else:
-                r.tlog_clr(k)
-        elif ctype == O.UJSON:
-            x = rng.random()
-            if x < 0.65:
-                r.ujson_ins(k, int(rng.integers(1, 8)))
-            elif x < 0.9:
-                r.ujson_rm(k, int(rng.integers(1, 8)))
-            else:
-                r.ujson_clr(k)
+        random_write(O, ctype, r, k, rng, val_len)
         if rng.random() < gossip:
             b = r.flush().table()
             batches.append(b)
@@ -85,6 +56,77 @@ def random_history(O, ctype, seed, nrep=4, nops=300, nkeys=12, val_len=14, gossi
         batches.append(r.flush().table())
         batches.append(r.state())  # full-state deltas too
     return batches
+
+
+def random_write(O, ctype, r, k, rng, val_len=14):
+    """one random local write command of `ctype` on oracle replica r"""
+    def rstr():
+        n = int(rng.integers(0, val_len))
+        # small alphabet -> many shared prefixes / ties
+        return bytes(rng.choice(np.frombuffer(b"aab\x00\xff", np.uint8), size=n))
+
+    if ctype == O.GCOUNT:
+        r.gcount_inc(k, int(rng.integers(0, 1 << 62)))
+    elif ctype == O.PNCOUNT:
+        v = int(rng.integers(-(1 << 62), 1 << 62))
+        (r.pncount_inc if rng.random() < 0.5 else r.pncount_dec)(k, v)
+    elif ctype == O.TREG:
+        r.treg_set(k, rstr(), int(rng.integers(0, 6)))
+    elif ctype == O.TLOG:
+        x = rng.random()
+        if x < 0.8:
+            r.tlog_ins(k, rstr(), int(rng.integers(0, 40)))
+        elif x < 0.9:
+            r.tlog_trimat(k, int(rng.integers(0, 30)))
+        elif x < 0.97:
+            r.tlog_trim(k, int(rng.integers(0, 8)))
+        else:
+            r.tlog_clr(k)
+    elif ctype == O.UJSON:
+        x = rng.random()
+        if x < 0.65:
+            r.ujson_ins(k, int(rng.integers(1, 8)))
+        elif x < 0.9:
+            r.ujson_rm(k, int(rng.integers(1, 8)))
+        else:
+            r.ujson_clr(k)
+
+
+# per-type batch layout: per-key columns, and CSR groups (offsets column,
+# data columns, optional nested CSR over the group's items)
+ROW_SCHEMA = {
+    0: ([], [("offs", ("ids", "vals"), None)]),
+    1: ([], [("p_offs", ("p_ids", "p_vals"), None), ("n_offs", ("n_ids", "n_vals"), None)]),
+    2: (["ts"], [("val_offs", ("val_bytes",), None)]),
+    3: (["cutoff"], [("ent_offs", ("ts",), ("val_offs", ("val_bytes",)))]),
+    4: ([], [("el_offs", ("dot_ids", "dot_seqs", "elems"), None), ("vv_offs", ("vv_ids", "vv_seqs"), None),
+             ("cloud_offs", ("cloud_ids", "cloud_seqs"), None)]),
+}
+
+
+def split_rows(ctype, table):
+    """a batch table -> [(key bytes, one-key delta table)]: the decoded
+    Array[(String, Any box)] that RepoManagerCore.converge_deltas walks pair
+    by pair (repo_manager.pony:92-93)"""
+    per_key, groups = ROW_SCHEMA[ctype]
+    kb, ko = np.asarray(table["key_bytes"], np.uint8), np.asarray(table["key_offs"], np.int64)
+    rows = []
+    for i in range(len(ko) - 1):
+        row = {c: np.asarray(table[c])[i:i + 1] for c in per_key}
+        for offs, cols, nested in groups:
+            o = np.asarray(table[offs], np.int64)
+            lo, hi = int(o[i]), int(o[i + 1])
+            row[offs] = np.array([0, hi - lo], np.uint64)
+            for c in cols:
+                row[c] = np.asarray(table[c])[lo:hi]
+            if nested:
+                noffs, ncols = nested
+                no = np.asarray(table[noffs], np.int64)
+                row[noffs] = (no[lo:hi + 1] - no[lo]).astype(np.uint64)
+                for c in ncols:
+                    row[c] = np.asarray(table[c])[no[lo]:no[hi]]
+        rows.append((bytes(kb[ko[i]:ko[i + 1]]), row))
+    return rows
 
 
 def collect(procs, q, n, deadline_s=150.0):

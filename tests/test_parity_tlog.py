@@ -161,3 +161,29 @@ def test_many_rounds_pool_reuse(oracle_mod):
         assert_state_equal(O.TLOG, want.state(), got.state())
     finally:
         eng.close()
+
+
+def test_spilled_merges_in_flight(oracle_mod):
+    """merges enqueued back to back, nothing read between them, on a pool too
+    small for their rebuilt logs: the device-side check leaves those keys
+    alone and spills their deltas, later merges run before the host sees it,
+    and the re-merge after a compaction (at the next call that finds the
+    merge done, or at the read) still gives the exact join"""
+    from jylis_amd import synth as S
+    from jylis_amd.engine import Engine
+    from jylis_amd.repo import RepoTLOG
+    O = oracle_mod
+    eng = Engine(device=0, entry_capacity=1024)
+    try:
+        st, dl = S.tlog_tables(4000, seed=S.BASE_SEED + 41, rounds=6, mean_state=4, mean_delta=3)
+        want = O.Repo(O.TLOG)
+        got = RepoTLOG(eng)
+        for b in [st] + dl:
+            want.converge(b)
+            got.converge_deltas(b)
+        assert_state_equal(O.TLOG, want.state(), got.state())
+        stats = eng.tlog_stats()
+        assert stats["spills"] >= 1 and stats["compactions"] >= 1, stats
+        assert stats["merges"] >= len(dl) + 1
+    finally:
+        eng.close()
