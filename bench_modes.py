@@ -64,6 +64,37 @@ def _max_over_ranks(x, dist, dev):
     return float(t[0])
 
 
+def _ask_owners(dist, cpu_group, rank, world, reqs, answer):
+    """answers for sampled keys wherever they live: reqs = [(owner rank,
+    owner-side slot)], answer(slots) -> one answer per slot, run by each owner
+    on its own engine.  At N > 1 the requests and answers travel over the CPU
+    (gloo) group, so every routed line verifies at any world size."""
+    if world == 1 or dist is None:
+        return list(answer(np.array([s for _, s in reqs], np.uint32))) if reqs else []
+    every = [None] * world
+    dist.all_gather_object(every, reqs, group=cpu_group)
+    mine = [(src, i, s) for src, rq in enumerate(every) for i, (o, s) in enumerate(rq) if o == rank]
+    ans = list(answer(np.array([s for _, _, s in mine], np.uint32))) if mine else []
+    back = [None] * world
+    dist.all_gather_object(back, [(src, i, a) for (src, i, _), a in zip(mine, ans)], group=cpu_group)
+    res = [None] * len(reqs)
+    for lst in back:
+        for src, i, a in lst:
+            if src == rank:
+                res[i] = a
+    return res
+
+
+def _all_true(ok, dist, dev):
+    """every rank verified (min over ranks)"""
+    if not dist:
+        return bool(ok)
+    import torch
+    t = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0]) == 0.0
+
+
 def cpu_baseline(mode, rounds=2):
     """The oracle (oracle/jy_oracle.cpp: the reference's Map[String, CRDT] +
     per-key converge loop, repo_manager.pony:92-93) timed single-threaded on a
@@ -260,6 +291,7 @@ def bench_treg(args, eng, dev, dist, rank, world):
     else:
         slot = eng.intern(TREG, (kb, ko))
         own = np.zeros(len(slot), np.uint32)
+        cpu_group = None
     setup_s = time.perf_counter() - t0
     n = len(slot)
     batches = []
@@ -296,25 +328,30 @@ def bench_treg(args, eng, dev, dist, rank, world):
     t = _max_over_ranks(elapsed, dist, dev)
     k = float(np.mean(kt))
     wf = float(np.mean(win)) if win else 0.5
-    verified = None
-    if world == 1:  # (routed at world 1 too: its runs are merged against this shard)
-        if routed:
-            tr.drain()
-        # sampled keys: LWW over every applied batch, (ts, value) with the
-        # value order of Pony's String (bytewise, shorter first on a prefix)
-        idx = np.random.default_rng(6).integers(0, n, 128)
-        applied = [batches[0]] + [batches[1 + i % nb] for i in range(args.warmup + args.steps)]
-        best = {}
-        for b in applied:
-            ts_h = b[2][idx].cpu().numpy().view(np.uint64)
-            pre_h, lr_h = b[3][idx].cpu().numpy().view(np.uint64), b[4][idx].cpu().numpy().view(np.uint64)
-            for j in range(len(idx)):
-                cand = (int(ts_h[j]), eng.value_bytes(TREG, pre_h[j], lr_h[j]))
-                if j not in best or cand > best[j]:
-                    best[j] = cand
-        s_h = batches[0][1][idx].cpu().numpy().view(np.uint32)
-        gts, gpre, glr = eng.treg_read(s_h)
-        verified = all((int(gts[j]), eng.value_bytes(TREG, gpre[j], glr[j])) == best[j] for j in range(len(idx)))
+    # sampled keys of this rank's ingest: LWW over every applied batch, (ts,
+    # value) with the value order of Pony's String (bytewise, shorter first on
+    # a prefix), against the OWNER's register (asked over the CPU group at N > 1)
+    if routed:
+        tr.drain()
+    idx = np.random.default_rng(6 + rank).integers(0, n, 128)
+    applied = [batches[0]] + [batches[1 + i % nb] for i in range(args.warmup + args.steps)]
+    best = {}
+    for b in applied:
+        ts_h = b[2][idx].cpu().numpy().view(np.uint64)
+        pre_h, lr_h = b[3][idx].cpu().numpy().view(np.uint64), b[4][idx].cpu().numpy().view(np.uint64)
+        for j in range(len(idx)):
+            cand = (int(ts_h[j]), eng.value_bytes(TREG, pre_h[j], lr_h[j]))
+            if j not in best or cand > best[j]:
+                best[j] = cand
+    o_h = batches[0][0][idx].cpu().numpy().view(np.uint32)
+    s_h = batches[0][1][idx].cpu().numpy().view(np.uint32)
+
+    def answer(slots):
+        gts, gpre, glr = eng.treg_read(slots)
+        return [(int(a), eng.value_bytes(TREG, p, q)) for a, p, q in zip(gts, gpre, glr)]
+    got = _ask_owners(dist, cpu_group if routed else None, rank, world,
+                      [(int(o), int(x)) for o, x in zip(o_h, s_h)], answer)
+    verified = _all_true(all(got[j] == best[j] for j in range(len(idx))), dist, dev)
     # SURVEY 8d prices a key LWW select at 48 B (16 delta + 16 state read +
     # 16 state write, the write counted unconditionally); what the kernel
     # actually moves in this layout is reported beside it
@@ -428,9 +465,11 @@ def bench_tlog(args, eng, dev, dist, rank, world):
                                                  "net new entry written + 64 B meta per delta key"}}
 
 
-def _verify_tlog(eng, st, applied, K, nsample=128):
-    """sampled logs (slot = key index) recomputed from the applied tables
-    (union of entries, largest cutoff, newest first, value order bytewise)"""
+def _verify_tlog(eng, st, applied, K, nsample=128, locate=None, ask=None):
+    """sampled logs recomputed from the applied tables (union of entries,
+    largest cutoff, newest first, value order bytewise) against the owner's
+    log: locate(k) -> (owner, slot), ask(reqs, answer) -> answers (bench runs
+    at N > 1); by default slot = key index on this engine"""
     from jylis_amd._lib import TLOG
     samp = np.random.default_rng(7).integers(0, K, nsample)
     want = {int(k): (0, set()) for k in samp}
@@ -442,12 +481,20 @@ def _verify_tlog(eng, st, applied, K, nsample=128):
             for j in range(eo_[k], eo_[k + 1]):
                 ents.add((int(b["ts"][j]), bytes(b["val_bytes"][vo_[j]:vo_[j + 1]])))
             want[k] = (cut, ents)
-    cut_g, offs_g, ts_g, pre_g, lr_g = eng.tlog_read(np.array(list(want), np.uint32))
+
+    def answer(slots):
+        cut_g, offs_g, ts_g, pre_g, lr_g = eng.tlog_read(slots)
+        return [(int(cut_g[i]), [(int(ts_g[j]), eng.value_bytes(TLOG, pre_g[j], lr_g[j]))
+                                 for j in range(offs_g[i], offs_g[i + 1])]) for i in range(len(slots))]
+    keys = list(want)
+    if locate is None:
+        got = answer(np.array(keys, np.uint32))
+    else:
+        got = ask([locate(k) for k in keys], answer)
     verified = True
-    for i, (k, (cut, ents)) in enumerate(want.items()):
+    for (k, (cut, ents)), (gcut, gents) in zip(want.items(), got):
         exp = sorted((e for e in ents if e[0] >= cut), reverse=True)
-        got = [(int(ts_g[j]), eng.value_bytes(TLOG, pre_g[j], lr_g[j])) for j in range(offs_g[i], offs_g[i + 1])]
-        verified = verified and int(cut_g[i]) == cut and got == exp
+        verified = verified and gcut == cut and gents == exp
     return bool(verified)
 
 
@@ -523,10 +570,16 @@ def _bench_csr_routed(args, eng, dev, dist, rank, world, kind):
     elapsed, kt = _timed(args.steps, args.warmup, step, dist, dev)
     t = _max_over_ranks(elapsed, dist, dev)
     applied = [st] + [dl[i % nb] for i in range(args.warmup + args.steps)]
-    verified = None
-    if world == 1:
-        verified = (_verify_tlog(eng, st, applied, K) if kind == "tlog"
-                    else _verify_ujson(eng, repo, st, applied, K))
+    # sampled keys of this rank's ingest against their OWNERS' state (the
+    # requests and answers cross the CPU group at N > 1)
+    def locate(k):
+        return int(own[k]), int(slot[k])
+
+    def ask(reqs, answer):
+        return _ask_owners(tdist if world > 1 else None, cpu_group, rank, world, reqs, answer)
+    ok = (_verify_tlog(eng, st, applied, K, locate=locate, ask=ask) if kind == "tlog"
+          else _verify_ujson(eng, repo, st, applied, K, locate=locate, ask=ask))
+    verified = _all_true(ok, dist, dev)
     per_step = float(np.mean([units[1 + i % nb] for i in range(args.warmup, args.warmup + args.steps)]))
     tot = torch.tensor([per_step], dtype=torch.float64, device=dev)
     if dist:
@@ -766,9 +819,10 @@ def _uj_join(a, b):
     return m, vv, cl
 
 
-def _verify_ujson(eng, repo, st, applied, D, nsample=96):
+def _verify_ujson(eng, repo, st, applied, D, nsample=96, locate=None, ask=None):
     """sampled docs (the hottest delta docs and random ones) recomputed from
-    the tables with _uj_join and compared with the engine's documents"""
+    the tables with _uj_join and compared with the owner's documents
+    (locate / ask as in _verify_tlog; by default a lookup on this engine)"""
     width = len(st["key_offs"]) and int(st["key_offs"][1] - st["key_offs"][0])
 
     def docs_of(t):
@@ -782,22 +836,31 @@ def _verify_ujson(eng, repo, st, applied, D, nsample=96):
             hot[d] = hot.get(d, 0) + int(eo[i])
     pick = sorted(hot, key=hot.get, reverse=True)[:nsample // 2]
     pick += np.random.default_rng(9).integers(0, D, nsample - len(pick)).tolist()
-    slots = eng.lookup(4, [bytes(np.asarray(st["key_bytes"], np.uint8)[
-        int(st["key_offs"][d]):int(st["key_offs"][d + 1])]) for d in pick])
-    eo, dots, elems, vv, co, cloud = eng.ujson_read(np.asarray(slots, np.uint32))
-    ids = [eng.replica_id(c) for c in range(eng.replica_count())]
     from jylis_amd import engine as E
-    for i, d in enumerate(pick):
+
+    def answer(slots):
+        eo, dots, elems, vv, co, cloud = eng.ujson_read(np.asarray(slots, np.uint32))
+        ids = [eng.replica_id(c) for c in range(eng.replica_count())]
+        out = []
+        for i in range(len(slots)):
+            c, q = E.unpack_dot(dots[eo[i]:eo[i + 1]])
+            gm = {(ids[int(x)], int(y)): int(e) for x, y, e in zip(c, q, elems[eo[i]:eo[i + 1]])}
+            gvv = {ids[j]: int(n) for j, n in enumerate(vv[i]) if n}
+            c, q = E.unpack_dot(cloud[co[i]:co[i + 1]])
+            out.append((gm, gvv, {(ids[int(x)], int(y)) for x, y in zip(c, q)}))
+        return out
+    if locate is None:
+        slots = eng.lookup(4, [bytes(np.asarray(st["key_bytes"], np.uint8)[
+            int(st["key_offs"][d]):int(st["key_offs"][d + 1])]) for d in pick])
+        got = answer(slots)
+    else:
+        got = ask([locate(d) for d in pick], answer)
+    for d, g in zip(pick, got):
         want = _uj_doc(st, d)
         for t, r in zip(applied, rows):
             if d in r:
                 want = _uj_join(want, _uj_doc(t, r[d]))
-        c, q = E.unpack_dot(dots[eo[i]:eo[i + 1]])
-        gm = {(ids[int(x)], int(y)): int(e) for x, y, e in zip(c, q, elems[eo[i]:eo[i + 1]])}
-        gvv = {ids[j]: int(n) for j, n in enumerate(vv[i]) if n}
-        c, q = E.unpack_dot(cloud[co[i]:co[i + 1]])
-        gcl = {(ids[int(x)], int(y)) for x, y in zip(c, q)}
-        if (gm, gvv, gcl) != want:
+        if g != want:
             return False
     return True
 

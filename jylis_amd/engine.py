@@ -202,7 +202,13 @@ class Engine:
         return n.value, c.value
 
     def arena_collect(self, ctype):
-        """reclaim dead value bytes (jy_arena_collect); unmerged packed handles become invalid"""
+        """reclaim dead value bytes (jy_arena_collect); unmerged packed handles become invalid.
+        Refused while a router holds rounds of this engine's batches in flight: their
+        handles would be read again by a drain round (route.py _RunRouter)."""
+        holds = getattr(self, "_route_holds", None)
+        if holds:
+            raise RuntimeError("arena_collect while a router has rounds in flight on this engine: "
+                               "call router.drain() first")
         live = C.c_uint64()
         self._check(self.lib.jy_arena_collect(self.h, ctype, C.byref(live)))
         return live.value

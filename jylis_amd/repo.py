@@ -273,6 +273,8 @@ class _ArenaGC:
     _arena_live = 0
 
     def _maybe_collect(self):
+        if getattr(self.eng, "_route_holds", None):
+            return  # a router's rounds in flight still read handles of this arena (route.py)
         n, _ = self.eng.arena_usage(self.ctype)
         if n > 2 * self._arena_live + (1 << 20):
             self._arena_live = self.eng.arena_collect(self.ctype)

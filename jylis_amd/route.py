@@ -63,15 +63,35 @@ class _Done:
         pass
 
 
+class _Pending:
+    """an in-flight transfer: wait() orders the current stream after it
+    (what RCCL's Work.wait() does for an async collective)"""
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        import torch
+        torch.cuda.current_stream().wait_event(self.ev)
+
+
 class LocalFabric:
     """S shards hosted by one process (tests on one GPU): the all-to-all is a
-    set of device copies on the current stream."""
+    set of device copies.  With `async_copies`, an async all-to-all runs its
+    copies on a side stream (after the current stream's work, optionally
+    behind a spin delay) and returns pending work whose wait() orders the
+    current stream after them -- the ordering contract of an async RCCL
+    collective, so the routers' works / wait() / chunk pipelining is exercised
+    with transfers genuinely in flight."""
 
-    def __init__(self, world):
+    def __init__(self, world, async_copies=False, delay_cycles=0):
         self.world = world
         self.ranks = list(range(world))
+        self.async_copies = async_copies
+        self.delay_cycles = delay_cycles
+        self._side = None
 
-    def a2a(self, outs, ins, async_op=False):
+    def _copies(self, outs, ins):
         S = self.world
         for r in range(S):
             cr = outs[r].numel() // S
@@ -79,7 +99,25 @@ class LocalFabric:
                 cs = ins[s].numel() // S
                 assert cs == cr, "equal-split all-to-all: every rank sends the same chunk size"
                 outs[r].view(-1)[s * cr:(s + 1) * cr].copy_(ins[s].view(-1)[r * cs:(r + 1) * cs])
-        return _Done()
+
+    def a2a(self, outs, ins, async_op=False):
+        if not (async_op and self.async_copies):
+            self._copies(outs, ins)
+            return _Done()
+        import torch
+        cur = torch.cuda.current_stream()
+        if self._side is None:
+            self._side = torch.cuda.Stream(cur.device)
+        self._side.wait_stream(cur)
+        with torch.cuda.stream(self._side):
+            if self.delay_cycles:
+                torch.cuda._sleep(self.delay_cycles)  # a slow link: a missing wait() reads stale runs
+            self._copies(outs, ins)
+            for t in list(outs) + list(ins):
+                t.record_stream(self._side)
+            ev = torch.cuda.Event()
+            ev.record(self._side)
+        return _Pending(ev)
 
     def max_all(self, ts):
         """in place: every tensor becomes the max over ranks"""
@@ -231,11 +269,28 @@ class _RunRouter:
         ovfs = self._round(batches)
         self._publish(batches, ovfs)
 
-    def drain(self):
-        """route everything still pending (a collective: every rank calls it)"""
+    arena_type = None  # the value arena the sending batches' handles point into (TREG / TLOG)
+
+    def drain(self, collect=False):
+        """route everything still pending (a collective: every rank calls it).
+        With `collect`, then reclaim the engines' value arenas when dead bytes
+        pass twice the live ones: the receivers append every run's byte
+        section, and collection is refused while rounds are in flight (the
+        pending batches' handles are read again by a drain round)."""
         _check_streams(self.engs)
         while self.pending:
             self._settle()
+        if collect and self.arena_type is not None:
+            for e in self.engs:
+                n, _ = e.arena_usage(self.arena_type)
+                live = getattr(e, "_arena_live", {}).get(self.arena_type, 0)
+                if n > 2 * live + (1 << 20):
+                    e.__dict__.setdefault("_arena_live", {})[self.arena_type] = e.arena_collect(self.arena_type)
+
+    def _hold(self, on):
+        for e in self.engs:
+            holds = e.__dict__.setdefault("_route_holds", set())
+            (holds.add if on else holds.discard)(id(self))
 
     chunks = 1  # key-range chunks per round (CSR routers pipeline the exchange over them)
 
@@ -298,12 +353,15 @@ class _RunRouter:
         ev = torch.cuda.Event()
         ev.record()
         self.pending.append((batches, ovfs, pins, ev))
+        self._hold(True)
 
     def _settle(self):
         """check the oldest pending round's overflow; run a drain round if any rank overflowed"""
         if not self.pending:
             return
         batches, ovfs, pins, ev = self.pending.popleft()
+        if not self.pending:
+            self._hold(False)  # a drain round below holds them again
         ev.synchronize()
         gmax = int(pins[0][0])
         counts = [int(p[1]) for p in pins]
@@ -331,6 +389,7 @@ class TregRouter(_RunRouter):
     local rank i (CUDA tensors; owner/slot int32, the rest int64 bits;
     long_bytes = `long_bytes(lr)`, a host int).  Partition -> header +
     records + bytes all-to-all -> one merge of every received run."""
+    arena_type = _lib.TREG
 
     def _sizes(self, b):
         return (int(b[0].numel()), int(b[5]))
@@ -392,6 +451,7 @@ class TlogRouter(_RunRouter):
     offsets (int64, n + 1); per entry ts, value handle pre / lr (int64 bits,
     packed on the sending engine); long_bytes = `long_bytes(lr)`.  Each
     owner merges the received runs one source at a time."""
+    arena_type = _lib.TLOG
 
     def _sizes(self, b):
         return (int(b[0].numel()), int(b[4].numel()), int(b[7]))

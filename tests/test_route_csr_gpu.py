@@ -12,6 +12,10 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
+# "async": every async all-to-all runs on a side stream behind a spin delay
+# (RCCL's ordering contract: the runs are valid only after wait())
+FABRIC = {"sync": {}, "async": {"async_copies": True, "delay_cycles": 400000}}
+
 TLOG_CSRS = [("ent_offs", ["ts"], True)]
 UJSON_CSRS = [("el_offs", ["dot_ids", "dot_seqs", "elems"], False), ("vv_offs", ["vv_ids", "vv_seqs"], False),
               ("cloud_offs", ["cloud_ids", "cloud_seqs"], False)]
@@ -169,14 +173,15 @@ def _tlog_stream(rng, S, rounds, K=3000):
     return out
 
 
+@pytest.mark.parametrize("fab", sorted(FABRIC))
 @pytest.mark.parametrize("S", [1, 2, 3])
-def test_tlog_routed_local_fabric(oracle_mod, S):
+def test_tlog_routed_local_fabric(oracle_mod, S, fab):
     from jylis_amd._lib import TLOG
     from jylis_amd.route import LocalFabric, TlogRouter
     rng = np.random.default_rng(60 + S)
     node = CsrNode(S, TLOG)
     try:
-        router = TlogRouter(node.engs, LocalFabric(S))
+        router = TlogRouter(node.engs, LocalFabric(S, **FABRIC[fab]))
         seen = []
         for per in _tlog_stream(rng, S, 3):
             seen += per
@@ -250,15 +255,16 @@ def _ujson_stream(rng, S, rounds, D=1500):
     return out, replica_ids(16, 7)
 
 
+@pytest.mark.parametrize("fab", sorted(FABRIC))
 @pytest.mark.parametrize("S", [1, 2, 3])
-def test_ujson_routed_local_fabric(oracle_mod, S):
+def test_ujson_routed_local_fabric(oracle_mod, S, fab):
     from jylis_amd._lib import UJSON
     from jylis_amd.route import LocalFabric, UjsonRouter
     rng = np.random.default_rng(80 + S)
     stream, rids = _ujson_stream(rng, S, 3)
     node = CsrNode(S, UJSON, rids)
     try:
-        router = UjsonRouter(node.engs, LocalFabric(S))
+        router = UjsonRouter(node.engs, LocalFabric(S, **FABRIC[fab]))
         seen = []
         for per in stream:
             seen += per

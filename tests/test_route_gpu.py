@@ -12,6 +12,11 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
+# LocalFabric modes: "async" runs every async all-to-all on a side stream
+# behind a spin delay, so a router that read its runs before wait() would see
+# stale buffers (the ordering contract of RCCL's async collectives)
+FABRIC = {"sync": {}, "async": {"async_copies": True, "delay_cycles": 400000}}
+
 
 def _treg_batch(rng, n, keyspace, ts_hi=4):
     from jylis_amd.engine import encode_keys
@@ -89,15 +94,16 @@ def _oracle_dict(O, batches):
             for i, (k, t) in enumerate(zip(O.split_keys(st), st["ts"]))}
 
 
+@pytest.mark.parametrize("fab", sorted(FABRIC))
 @pytest.mark.parametrize("S", [1, 2, 3])
-def test_treg_routed_local_fabric(oracle_mod, S):
+def test_treg_routed_local_fabric(oracle_mod, S, fab):
     """every rank ingests its own batch over a shared key space; keys that
     several ranks ingest in the same step meet in one merge launch"""
     from jylis_amd.route import LocalFabric, TregRouter
     rng = np.random.default_rng(40 + S)
     node = _Node(S)
     try:
-        router = TregRouter(node.engs, LocalFabric(S))
+        router = TregRouter(node.engs, LocalFabric(S, **FABRIC[fab]))
         seen = []
         for _ in range(4):
             bs = [_treg_batch(rng, 2500, 4000) for _ in range(S)]
@@ -139,6 +145,48 @@ def test_treg_routed_overflow_drains(oracle_mod):
             router.step([node.ingest(r, b) for r, b in enumerate(bs)])
         router.drain()
         assert router.drains >= 1
+        assert node.union_state() == _oracle_dict(oracle_mod, seen)
+    finally:
+        node.close()
+
+
+def test_treg_arena_collect_waits_for_drain(oracle_mod):
+    """a drain round re-reads the long-value bytes of a pending
+    batch through its handles, so collecting the sending engine's arena
+    between step() and drain() would route the wrong bytes.  Collection is
+    refused while rounds are in flight; after drain() it runs, and the state
+    (long values included) stays exact"""
+    from jylis_amd._lib import TREG
+    from jylis_amd.engine import encode_keys
+    from jylis_amd.route import LocalFabric, TregRouter, owners
+    S = 2
+    rng = np.random.default_rng(11)
+    cand = [f"ac{i}" for i in range(20000)]
+    kb, ko = encode_keys(cand)
+    hot = [k for k, o in zip(cand, owners(kb, ko, S)) if o == 0][:5000]
+    node = _Node(S)
+    try:
+        router = TregRouter(node.engs, LocalFabric(S))
+        seen = []
+        for rnd in range(3):
+            bs = []
+            for r in range(S):
+                keys = [hot[int(i)] for i in rng.choice(len(hot), 4000, replace=False)]
+                vals = [b"long-value-%d-%d-" % (rnd, r) + bytes(rng.integers(97, 123, 12).astype(np.uint8))
+                        for _ in keys]
+                kb2, ko2 = encode_keys(keys)
+                vb, vo = encode_keys(vals)
+                bs.append({"key_bytes": kb2, "key_offs": ko2, "ts": np.full(4000, rnd, np.uint64),
+                           "val_bytes": vb, "val_offs": vo})
+            seen += bs
+            router.step([node.ingest(r, b) for r, b in enumerate(bs)])
+            for e in node.engs:
+                with pytest.raises(RuntimeError):
+                    e.arena_collect(TREG)
+        router.drain(collect=True)
+        assert router.drains >= 1
+        for e in node.engs:
+            e.arena_collect(TREG)  # no rounds in flight: allowed
         assert node.union_state() == _oracle_dict(oracle_mod, seen)
     finally:
         node.close()
@@ -248,8 +296,9 @@ def test_treg_set_repeated_keys_device(oracle_mod):
         eng.close()
 
 
+@pytest.mark.parametrize("fab", sorted(FABRIC))
 @pytest.mark.parametrize("S", [2, 3])
-def test_pncount_routed_local_fabric(S):
+def test_pncount_routed_local_fabric(S, fab):
     """dense PNCOUNT peer batches grouped by owner, exchanged column by
     column (double-buffered) and block-merged on the owners; checked against
     a numpy max over everything ingested"""
@@ -270,7 +319,7 @@ def test_pncount_routed_local_fabric(S):
             cols.append(e.replica_cols(rids.tolist()))
         assert all((c == cols[0]).all() for c in cols)  # one registration order on every shard
         peer_cols = [[int(cols[0][r * Cn + c]) for c in range(Cn)] for r in range(S)]
-        router = CounterRouter(engs, LocalFabric(S), PNCOUNT)
+        router = CounterRouter(engs, LocalFabric(S, **FABRIC[fab]), PNCOUNT)
         rng = np.random.default_rng(S)
         want = [np.zeros((2, S * Cn, K), np.uint64) for _ in range(S)]
         for rnd in range(3):
