@@ -57,6 +57,13 @@ def parse():
     ap.add_argument("--type", default="pncount", choices=["pncount", "gcount", "treg", "tlog", "ujson", "e2e", "read"],
                     help="pncount = the BASELINE metric line; the others measure SURVEY 8d configs 1,3,4,5")
     ap.add_argument("--route", action="store_true", help="treg / tlog / ujson: run the routing path even on 1 GPU")
+    ap.add_argument("--overlap", type=float, default=None,
+                    help="treg --route: S local shards on one GPU whose sources share this fraction of their keys "
+                         "in every step (timed beside the same run with no overlap)")
+    ap.add_argument("--shards", type=int, default=2, help="--overlap: local shards (engines) on the GPU")
+    ap.add_argument("--resolve", action="store_true",
+                    help="treg --route: every timed step first resolves its batch's key strings on the GPU "
+                         "(route.KeyResolver), 1/16 of them new to the node")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1 collectives: nccl (RCCL over xGMI); gloo only rehearses the routed path "
                          "with several ranks on one GPU")

@@ -261,11 +261,110 @@ def _treg_values(rng, n):
     return vb, vo
 
 
+def bench_treg_overlap(args, eng, dev, dist, rank, world):
+    """Routed TREG with keys that several peers flushed in the same step
+    (VERDICT r2 #5): S shards (engines) on one GPU exchange through a
+    LocalFabric; source r ingests n = G / S records per step, its own share of
+    the G keys except that a fraction `overlap` of them are keys of source
+    r + 1's share, so those keys reach their owner from two sources in one
+    step.  The same run with no overlap is timed first; both per-step times
+    are reported (same records per step)."""
+    import torch
+    from jylis_amd import synth as S_
+    from jylis_amd._lib import TREG
+    from jylis_amd.engine import Engine
+    from jylis_amd.route import LocalFabric, TregRouter, long_bytes, owners
+    S = max(2, args.shards)
+    G = args.keys or (8 << 20)
+    n = G // S
+    engs = [eng] + [Engine(device=eng.device, counter_columns=16) for _ in range(S - 1)]
+    for e in engs[1:]:
+        e.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    gidx = np.arange(G, dtype=np.uint64)
+    kb, ko = _key_strings(gidx, b"t")
+    own = owners(kb, ko, S)
+    slot = np.zeros(G, np.uint32)
+    for d in range(S):
+        ix = np.nonzero(own == d)[0]
+        width = int(ko[1] - ko[0])
+        sub = np.ascontiguousarray(kb.reshape(G, width)[ix]).reshape(-1)
+        slot[ix] = engs[d].intern(TREG, (sub, np.arange(len(ix) + 1, dtype=np.uint64) * np.uint64(width)))
+    rng = np.random.default_rng(S_.BASE_SEED + 31)
+    nb = max(1, args.batches, args.warmup + args.steps)
+
+    def keys_of(r, f):
+        mine = np.arange(r, G, S, dtype=np.int64)[:n]
+        m = int(round(f * n))
+        if m:  # the head of source r + 1's share, which source r + 1 ingests too (f <= 1/2)
+            other = np.arange((r + 1) % S, G, S, dtype=np.int64)[:n]
+            mine = np.concatenate([mine[:n - m], other[:m]])
+        return mine
+
+    def batches_for(f, tbase):
+        out = []
+        for j in range(nb + 1):
+            per = []
+            for r in range(S):
+                k = keys_of(r, f)
+                vb, vo = _treg_values(rng, n)
+                pre, lr = engs[r].pack_values(TREG, (vb, vo))
+                ts = (rng.integers(0, 1 << 20, n) + (j << 18) + tbase).astype(np.uint64)
+                per.append((k, tuple(_to_dev(a, dev) for a in (own[k], slot[k], ts, pre, lr)) + (long_bytes(lr),)))
+            out.append(per)
+        return out
+
+    res = {}
+    for run, f in enumerate((0.0, float(args.overlap))):
+        # the second run's timestamps lie above every one of the first run's:
+        # the state the first run left never wins a key the second run writes
+        bs = batches_for(f, run * ((nb + 8) << 18))
+        router = TregRouter(engs, LocalFabric(S))
+        router.step([b for _, b in bs[0]])
+        elapsed, _ = _timed(args.steps, args.warmup, lambda i: router.step([b for _, b in bs[1 + i % nb]]), dist, dev)
+        router.drain()
+        # verification: sampled keys of source 0's batches, LWW over every
+        # source's applied batches that hold them, against the owner's register
+        applied = [bs[0]] + [bs[1 + i % nb] for i in range(args.warmup + args.steps)]
+        samp = np.random.default_rng(3).choice(keys_of(0, f), 64, replace=False)
+        best = {}
+        for per in applied:
+            for r, (k, b) in enumerate(per):
+                pos = {int(x): i for i, x in enumerate(k)}
+                hit = [(int(g), pos[int(g)]) for g in samp if int(g) in pos]
+                if not hit:
+                    continue
+                ii = torch.tensor([i for _, i in hit], device=dev)
+                ts_h = b[2][ii].cpu().numpy().view(np.uint64)
+                pre_h, lr_h = b[3][ii].cpu().numpy().view(np.uint64), b[4][ii].cpu().numpy().view(np.uint64)
+                for (g, _), t_, p_, l_ in zip(hit, ts_h, pre_h, lr_h):
+                    cand = (int(t_), engs[r].value_bytes(TREG, p_, l_))
+                    if g not in best or cand > best[g]:
+                        best[g] = cand
+        ok = True
+        for g in samp:
+            e = engs[int(own[g])]
+            gts, gpre, glr = e.treg_read(np.array([slot[g]], np.uint32))
+            ok = ok and (int(gts[0]), e.value_bytes(TREG, gpre[0], glr[0])) == best[int(g)]
+        res[f] = (elapsed / args.steps, ok)
+        del bs, router
+    for e in engs[1:]:
+        e.close()
+    (t0, ok0), (t1, ok1) = res[0.0], res[float(args.overlap)]
+    return {"workload": f"TREG routed LWW converge: {G} keys over {S} shards on one GPU (LocalFabric), {n} records "
+                        f"per source per step; {args.overlap:.0%} of each source's keys shared with another source "
+                        f"in the same step (SURVEY 8d config 3, 8e)",
+            "unit_of_work": "routed record", "value": S * n / t1, "ms_per_step": t1 * 1e3,
+            "no_overlap_ms_per_step": t0 * 1e3, "overlap_vs_no_overlap": t1 / t0, "overlap": args.overlap,
+            "verified_sampled_keys": bool(ok0 and ok1)}
+
+
 def bench_treg(args, eng, dev, dist, rank, world):
     """Routed TREG converge: every rank ingests 1/world of the global key space
     per step and routes records + long value bytes to their owners (RCCL
     all-to-all), which LWW-merge them.  At world 1 the exchange is skipped
     unless --route (then it runs the same kernels against itself)."""
+    if args.overlap is not None:
+        return bench_treg_overlap(args, eng, dev, dist, rank, world)
     import torch
     from jylis_amd import synth as S
     from jylis_amd._lib import TREG
@@ -278,15 +377,18 @@ def bench_treg(args, eng, dev, dist, rank, world):
     kb, ko = _key_strings(idx, b"t")
     routed = world > 1 or args.route
     t0 = time.perf_counter()
+    if args.resolve and not routed:
+        raise SystemExit("--resolve needs the routed path (--route or --gpus > 1)")
     if routed:
         import torch.distributed as tdist
 
-        from jylis_amd.route import DistFabric, LocalFabric
+        from jylis_amd.route import DistFabric, KeyResolver, LocalFabric
         cpu_group = tdist.new_group(backend="gloo") if world > 1 else None
-        router = ShardRouter(rank, world, lambda tab: eng.intern(TREG, tab), dist=tdist if world > 1 else None,
-                             group=cpu_group)
-        own, slot = router.resolve(kb, ko)
         fabric = DistFabric(tdist, cpu_group=cpu_group) if world > 1 else LocalFabric(1)
+        # owner slots resolved on the GPU (k_keyroute.hip): key strings in HBM
+        kr = KeyResolver([eng], fabric, TREG)
+        ((own_d, slot_d),) = kr.resolve([(_to_dev(kb, dev), _to_dev(ko, dev))])
+        own, slot = own_d.cpu().numpy().view(np.uint32), slot_d.cpu().numpy().view(np.uint32)
         tr = TregRouter([eng], fabric)
     else:
         slot = eng.intern(TREG, (kb, ko))
@@ -294,29 +396,45 @@ def bench_treg(args, eng, dev, dist, rank, world):
         cpu_group = None
     setup_s = time.perf_counter() - t0
     n = len(slot)
-    batches = []
+    m = n // 16 if args.resolve else 0  # --resolve: keys new to the node in every step
+    batches, keysets = [], []
     # batch 0 = initial state; a distinct batch for every step (no replays)
     for j in range(max(1, args.batches, args.warmup + args.steps) + 1):
-        vb, vo = _treg_values(rng, n)
+        vb, vo = _treg_values(rng, n + m)
         pre, lr = eng.pack_values(TREG, (vb, vo))
         # fresh writes: batch j's timestamps sit 2^18 above batch j-1's in a
         # 2^20 window, so ~70% of keys take the delta and ties are dense
-        ts = (rng.integers(0, 1 << 20, n) + (j << 18)).astype(np.uint64)
-        batches.append(tuple(_to_dev(a, dev) for a in (own, slot, ts, pre, lr)) + (long_bytes(lr),))
+        ts = (rng.integers(0, 1 << 20, n + m) + (j << 18)).astype(np.uint64)
+        if args.resolve:
+            # the batch as key strings in HBM: this rank's keys + m new ones
+            nkb, nko = _key_strings(np.arange(m, dtype=np.uint64) + np.uint64(m * j), b"n%d:" % rank)
+            w = int(ko[1] - ko[0])
+            keysets.append((_to_dev(np.concatenate([kb, nkb]), dev),
+                            _to_dev(np.concatenate([ko, nko[1:] + np.uint64(len(kb))]), dev)))
+            batches.append((None, None) + tuple(_to_dev(a, dev) for a in (ts, pre, lr)) + (long_bytes(lr),))
+        else:
+            batches.append(tuple(_to_dev(a, dev) for a in (own, slot, ts, pre, lr)) + (long_bytes(lr),))
     win = []
+    resolve_s = []
 
-    def step_of(b):
+    def step_of(b, j=None):
+        if args.resolve:
+            # the step resolves its key strings on the GPU, then routes the entries
+            h0 = time.perf_counter()
+            ((o, s_),) = kr.resolve([keysets[j]])
+            resolve_s.append(time.perf_counter() - h0)
+            b = (o, s_) + b[2:]
         o, s, ts, pre, lr, nbytes = b
         if routed:
             tr.step([b])
         else:
             eng.treg_converge(s, ts, pre, lr)
 
-    step_of(batches[0])
+    step_of(batches[0], 0)
     # winners per step from timestamps (ties need the value compare: rare)
     cur = batches[0][2].clone() if not routed else None
     nb = len(batches) - 1
-    elapsed, kt = _timed(args.steps, args.warmup, lambda i: step_of(batches[1 + i % nb]), dist, dev,
+    elapsed, kt = _timed(args.steps, args.warmup, lambda i: step_of(batches[1 + i % nb], 1 + i % nb), dist, dev,
                          eng=None if routed else eng)
     if cur is not None:
         for i in range(args.warmup + args.steps):
@@ -343,8 +461,7 @@ def bench_treg(args, eng, dev, dist, rank, world):
             cand = (int(ts_h[j]), eng.value_bytes(TREG, pre_h[j], lr_h[j]))
             if j not in best or cand > best[j]:
                 best[j] = cand
-    o_h = batches[0][0][idx].cpu().numpy().view(np.uint32)
-    s_h = batches[0][1][idx].cpu().numpy().view(np.uint32)
+    o_h, s_h = own[idx], slot[idx]
 
     def answer(slots):
         gts, gpre, glr = eng.treg_read(slots)
@@ -359,10 +476,17 @@ def bench_treg(args, eng, dev, dist, rank, world):
     whole = n * 24 > (256 << 20)  # k_treg_lww<true>: state over the Infinity Cache
     moved = 4 + 24 + 8 + 8 + (16 if whole else 16 * wf) + (16 * (1 - wf) if whole else 0)
     out = {"workload": f"TREG LWW converge: {G} keys over {world} GPU(s) ({Kper} per GPU), one delta per key "
-                       f"per step{' routed by owner (all-to-all)' if routed else ''} (SURVEY 8d config 3)",
-           "unit_of_work": "key LWW select", "units_per_step_per_gpu": n,
-           "value": world * n * args.steps / t, "ms_per_step": t / args.steps * 1e3, "setup_s": setup_s,
+                       f"per step{' routed by owner (all-to-all)' if routed else ''}"
+                       + (f"; every step first resolves its {n + m} key strings ({m} new to the node) on the GPU "
+                          f"(KeyResolver: regroup by owner, exchange, intern on the owner, slots back)"
+                          if args.resolve else "") + " (SURVEY 8d config 3)",
+           "unit_of_work": "key LWW select", "units_per_step_per_gpu": n + m,
+           "value": world * (n + m) * args.steps / t, "ms_per_step": t / args.steps * 1e3, "setup_s": setup_s,
            "winner_fraction": wf, "verified_sampled_keys": verified}
+    if args.resolve:
+        out["metric"] = "TREG end-to-end routed ingest (key strings resolved on the GPU + routed LWW)"
+        out["resolve_host_ms_avg"] = float(np.mean(resolve_s[-args.steps:])) * 1e3
+        out["keys_interned_after"] = int(eng.nkeys(TREG))
     if not routed:
         out["roofline"] = {"bound": "hbm", "achieved": bytes_per_key * n / k / 1e9, "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": bytes_per_key * n / k / 1e9 / HBM_PEAK_GBS,

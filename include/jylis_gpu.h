@@ -101,6 +101,12 @@ int32_t jy_keys_intern_mem(jy_engine* eng, int32_t type, uint64_t n, const uint8
 int32_t jy_keys_lookup_mem(jy_engine* eng, int32_t type, uint64_t n, const uint8_t* key_bytes,
                            const uint64_t* key_offs, uint32_t* slots_out, int32_t mem);
 uint64_t jy_keys_count(const jy_engine* eng, int32_t type);
+/* the key strings of slots [slot0, slot0 + n) (host out): offs_out u64[n + 1];
+ * bytes_out is written when cap_bytes >= offs_out[n] (else sizes only).
+ * Keys interned on the device (jy_keys_intern_mem, jy_keys_intern_lens) get
+ * their names back this way.  Blocks. */
+int32_t jy_keys_export(jy_engine* eng, int32_t type, uint64_t slot0, uint64_t n, uint64_t* offs_out,
+                       uint8_t* bytes_out, uint64_t cap_bytes);
 int32_t jy_keys_reserve(jy_engine* eng, int32_t type, uint64_t key_capacity);
 /* owner shard of a key when keys are hash-sharded over `nshards` engines */
 uint32_t jy_key_owner(const uint8_t* key, uint64_t len, uint32_t nshards);
@@ -315,6 +321,27 @@ int32_t jy_treg_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, co
                            uint64_t* hdr_dev, uint32_t* ovf_dev);
 int32_t jy_treg_converge_routed(jy_engine* eng, uint32_t nsrc, uint64_t cap, uint64_t cap_byte,
                                 const uint64_t* recs_dev, const uint8_t* bytes_dev, const uint64_t* hdr_dev);
+
+/* ---- cross-shard key resolution (k_keyroute.hip): `_data_for(key)`
+ * (repo_treg.pony:37-42, every repo_*.pony) when the key's slot lives on
+ * another GPU.  All pointers are device memory; the calls only enqueue.
+ * Sender: jy_keys_route_part computes every key's owner (jy_key_owner, on the
+ * device) and regroups the keys by owner for a variable all-to-all:
+ *   owner_out u32[n], pos_out u32[n] (each key's index in owner order),
+ *   send_lens u64[n] and send_bytes u8[total key bytes] in owner order,
+ *   counts_out u64[2 * nshards]: keys per owner, then bytes per owner.
+ * Owner: jy_keys_intern_lens interns the n received keys (lengths + bytes)
+ *   in its directory -- create on miss, like jy_keys_intern_mem -- and
+ *   writes their slots (it synchronises, as interning does).
+ * Sender, once the slots came back in its owner order:
+ *   jy_keys_route_back writes slots_out[i] = answers[pos[i]]. */
+int32_t jy_keys_route_part(jy_engine* eng, uint64_t n, const uint8_t* key_bytes, const uint64_t* key_offs,
+                           uint32_t nshards, uint32_t* owner_out, uint32_t* pos_out, uint64_t* send_lens,
+                           uint8_t* send_bytes, uint64_t* counts_out);
+int32_t jy_keys_intern_lens(jy_engine* eng, int32_t type, uint64_t n, const uint8_t* bytes, const uint64_t* lens,
+                            uint32_t* slots_out);
+int32_t jy_keys_route_back(jy_engine* eng, uint64_t n, const uint32_t* pos, const uint32_t* answers,
+                           uint32_t* slots_out);
 
 /* ---- routing TLOG logs and UJSON documents (k_route_csr.hip) ----
  * The CSR counterpart of the TREG pair above: a key travels with its whole

@@ -58,6 +58,7 @@ SIGNATURES = {
     "jy_keys_lookup_mem": (I32, [P, I32, U64, P, P, P, I32]),
     "jy_keys_count": (U64, [P, I32]),
     "jy_keys_reserve": (I32, [P, I32, U64]),
+    "jy_keys_export": (I32, [P, I32, U64, U64, P, P, U64]),
     "jy_key_owner": (U32, [P, U64, U32]),
     "jy_values_pack": (I32, [P, I32, U64, P, P, P, P]),
     "jy_gcount_converge": (I32, [P, U64, P, P, P, I32]),
@@ -93,6 +94,9 @@ SIGNATURES = {
     "jy_tlog_deltas_size": (I32, [P, P]),
     "jy_tlog_flush": (I32, [P, U64, U64, P, P, P, P, P, P, P, P, I32]),
     "jy_keys_owner": (None, [U64, P, P, U32, P]),
+    "jy_keys_route_part": (I32, [P, U64, P, P, U32, P, P, P, P, P]),
+    "jy_keys_intern_lens": (I32, [P, I32, U64, P, P, P]),
+    "jy_keys_route_back": (I32, [P, U64, P, P, P]),
     "jy_treg_route_part": (I32, [P, U64, P, P, P, P, P, U32, U64, U64, I32, P, P, P, P]),
     "jy_treg_converge_routed": (I32, [P, U32, U64, U64, P, P, P]),
     "jy_route_words": (U64, [I32, U64, P]),

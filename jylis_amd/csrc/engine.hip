@@ -277,6 +277,8 @@ void jy_engine_destroy(jy_engine* eng) {
   F(eng->treg.seen[1]);
   F(eng->treg.dupn);
   F(eng->treg.dups);
+  F(eng->treg.dupn_alt);
+  F(eng->treg.dups_alt);
   for (TlogState* t : {&eng->tlog, &eng->tlog_d}) {
     F(t->meta);
     F(t->pool);

@@ -230,6 +230,8 @@ struct TregState {  // per slot: ts u64 (read by every merge) + TVal (written by
   int parity = 0;
   u32* dupn = nullptr;
   u64* dups = nullptr;
+  u32* dupn_alt = nullptr;  // the other list of a parallel fold round (k_treg_fold_round)
+  u64* dups_alt = nullptr;
   u64 dup_cap = 0;
   u64 dup_bound = 0;
 };

@@ -404,3 +404,30 @@ int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, co
   *created = nnew;
   return JY_OK;
 }
+
+// the key strings of slots [slot0, slot0 + n): the directory keeps them in
+// slot order, so this is two device-to-host copies (the handles, then one
+// byte range).  Blocks.
+extern "C" int32_t jy_keys_export(jy_engine* eng, int32_t type, uint64_t slot0, uint64_t n, uint64_t* offs_out,
+                                  uint8_t* bytes_out, uint64_t cap_bytes) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (type < 0 || type >= JY_NTYPES) return eng->fail(JY_ETYPE, "unknown CRDT type");
+  KeyDir& K = eng->kdir[type];
+  if (slot0 + n > K.n) return eng->fail(JY_ERANGE, "slots beyond the interned keys");
+  offs_out[0] = 0;
+  if (n == 0) return JY_OK;
+  std::vector<u64> ref(n);
+  JY_HIP(eng, hipMemcpyAsync(ref.data(), K.kref + slot0, n * 8, hipMemcpyDeviceToHost, eng->stream));
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  const u64 b0 = ref[0] >> 24;
+  for (u64 i = 0; i < n; i++) {
+    if ((ref[i] >> 24) != b0 + offs_out[i]) return eng->fail(JY_EINVAL, "key directory bytes out of slot order");
+    offs_out[i + 1] = offs_out[i] + (ref[i] & JY_LR_LEN_MASK);
+  }
+  if (!bytes_out || cap_bytes < offs_out[n]) return JY_OK;  // sizes only
+  if (offs_out[n]) {
+    JY_HIP(eng, hipMemcpyAsync(bytes_out, K.bytes + b0, offs_out[n], hipMemcpyDeviceToHost, eng->stream));
+    JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  }
+  return JY_OK;
+}

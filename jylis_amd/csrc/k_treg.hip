@@ -19,12 +19,18 @@
 // one-delta-per-key contract, or routed runs of two sources touching one
 // key) is resolved EXACTLY: the first entry of each slot (jy_claim_rows, one
 // bit per slot) is merged by the wide kernel; the others are copied into a
-// duplicate list that one wave folds in later -- before the next read or
-// SET of the register file, since LWW is a join and the fold's timing and
-// order do not change the result.  A dense batch in slot order costs the
-// claim one atomic instruction per wave.  Two claim bitmaps alternate: each
-// launch clears the other one, slice by slice, so no launch is spent on
-// resetting them.
+// duplicate list that is folded in later -- before the next read or SET of
+// the register file, since LWW is a join and the fold's timing and order do
+// not change the result.  The fold runs in parallel ROUNDS over the whole
+// GPU (k_treg_fold_round: each round merges the first record of every slot
+// in the list and moves the rest to the next round's list), so a key that
+// arrives many times costs one round per extra occurrence, not a serial walk;
+// one wave folds whatever a few rounds leave (unbounded repeats only).
+// Routed runs are merged one source per launch: keys that several peers
+// flushed in the same step never become duplicates.  A dense batch in slot
+// order costs the claim one atomic instruction per wave.  Two claim bitmaps
+// alternate: each launch clears the other one, slice by slice, so no launch
+// is spent on resetting them.
 //
 // Roofline: HBM.  SURVEY 8d prices a key at 48 B (16 delta + 16 state read
 // + 16 state write).  What this kernel moves per delta entry: 28 B delta
@@ -292,6 +298,58 @@ __global__ __launch_bounds__(64) void k_treg_fold(TregK K) {
   if (lane == 0) *K.dupn = 0;
 }
 
+// One round of the parallel fold, grid-stride over the list's count: the
+// first record of each slot (this launch's claim bitmap) is merged, the
+// others are pushed to K's list (the next round's input).  Every lane of a
+// wave runs the same iterations (jy_claim_rows is wave-collective).
+template <bool kSet>
+__global__ __launch_bounds__(kThreads) void k_treg_fold_round(TregK K, const u32* __restrict__ in_n,
+                                                              const u64* __restrict__ in) {
+  constexpr int U = 2;
+  clear_slice(K);
+  const u64 n = *in_n;
+  for (u64 b0 = (u64)blockIdx.x * (kThreads * U); b0 < n; b0 += (u64)gridDim.x * (kThreads * U)) {
+    const u64 base = b0 + (threadIdx.x >> 6) * (64 * U) + (threadIdx.x & 63);
+    u32 s[U];
+    u64 t[U], p[U], l[U], t0[U];
+    bool valid[U], first[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const u64 i = base + (u64)u * 64;
+      valid[u] = i < n;
+      s[u] = 0;
+      if (valid[u]) {
+        const u64x2 a = reinterpret_cast<const u64x2*>(in + i * 4)[0];
+        const u64x2 b = reinterpret_cast<const u64x2*>(in + i * 4)[1];
+        s[u] = (u32)a.x;
+        t[u] = a.y;
+        p[u] = b.x;
+        l[u] = b.y;
+      }
+    }
+    if (!kSet) {
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (valid[u]) t0[u] = K.ts[s[u]];
+    }
+    jy_claim_rows<U>(valid, s, K.seen, first);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (!valid[u]) continue;
+      if (!first[u]) {
+        push_dup(K, s[u], t[u], p[u], l[u]);
+        continue;
+      }
+      if (kSet) {
+        set_one(K, s[u], t[u], p[u], l[u]);
+      } else if (t[u] >= t0[u] && lww_wins(t[u], t0[u], p[u], l[u], K.val, s[u], K.arena)) {
+        K.ts[s[u]] = t[u];
+        K.val[s[u]] = TVal{p[u], l[u]};
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void k_treg_gather(const u64* __restrict__ ts, const TVal* __restrict__ val,
                                                           const u32* __restrict__ slots, u64 n, u64* __restrict__ ots,
                                                           u64* __restrict__ opre, u64* __restrict__ olr) {
@@ -340,11 +398,67 @@ TregK state_of(jy_engine* eng) {
   return K;
 }
 
+// the claim bitmaps of one launch: this launch's (clean) and the other one,
+// which the launch clears (or a memset, for a grid too small to clear it)
+int32_t claim_bits(jy_engine* eng, u32 nblocks, TregK& K) {
+  TregState& t = eng->treg;
+  K.seen = t.seen[t.parity];
+  const u64 bytes = ((t.seen_words * 4 + 15) & ~15ull);
+  if (bytes > (u64)nblocks * 4096) {
+    JY_HIP(eng, hipMemsetAsync(t.seen[t.parity ^ 1], 0, bytes, eng->stream));
+    K.clear = nullptr;
+    K.clear_bytes = 0;
+  } else {
+    K.clear = t.seen[t.parity ^ 1];
+    K.clear_bytes = bytes;
+  }
+  t.parity ^= 1;
+  return JY_OK;
+}
+
+// parallel fold rounds over the pending duplicate list (k_treg_fold_round):
+// after `rounds` rounds no slot is left that appeared at most `rounds` + 1
+// times in the list
+int32_t fold_rounds(jy_engine* eng, int rounds, bool set) {
+  TregState& t = eng->treg;
+  if (!t.dups_alt) {
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.dups_alt), std::max<u64>(t.dup_cap, 1) * 32,
+                        "treg duplicate list"));
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.dupn_alt), 64, "treg duplicate count"));
+  }
+  const u32 grid = (u32)std::min<u64>(blocks(std::max<u64>(t.dup_bound, 1), kThreads * 2), 1024);
+  for (int r = 0; r < rounds; r++) {
+    TregK K = state_of(eng);
+    K.dupn = t.dupn_alt;
+    K.dups = t.dups_alt;
+    if (set) {
+      K.pts = t.dts;
+      K.pval = t.dval;
+      K.pflag = t.dflag;
+      K.pcount = t.dcount;
+    }
+    JY_TRY(claim_bits(eng, grid, K));
+    JY_HIP(eng, hipMemsetAsync(t.dupn_alt, 0, 4, eng->stream));
+    if (set)
+      hipLaunchKernelGGL((k_treg_fold_round<true>), dim3(grid), dim3(kThreads), 0, eng->stream, K, t.dupn, t.dups);
+    else
+      hipLaunchKernelGGL((k_treg_fold_round<false>), dim3(grid), dim3(kThreads), 0, eng->stream, K, t.dupn, t.dups);
+    JY_HIP(eng, hipGetLastError());
+    std::swap(t.dupn, t.dupn_alt);
+    std::swap(t.dups, t.dups_alt);
+  }
+  return JY_OK;
+}
+
 // fold the pending duplicates (converge paths) now: before a read, a SET
-// batch (whose pending-delta test must see them) or an arena move
+// batch (whose pending-delta test must see them) or an arena move.  Parallel
+// rounds first; one wave then folds what is left (a slot repeated more often
+// than the rounds cover) and resets the list.
+constexpr int kFoldRounds = 3;
 int32_t fold_now(jy_engine* eng) {
   TregState& t = eng->treg;
   if (t.dup_bound == 0) return JY_OK;
+  JY_TRY(fold_rounds(eng, kFoldRounds, false));
   hipLaunchKernelGGL((k_treg_fold<false>), dim3(1), dim3(64), 0, eng->stream, state_of(eng));
   JY_HIP(eng, hipGetLastError());
   t.dup_bound = 0;
@@ -361,25 +475,17 @@ int32_t claim_begin(jy_engine* eng, u64 n, u32 nblocks, TregK& K) {
     if (n > t.dup_cap) {
       const u64 cap = std::max<u64>(4 * n, 1 << 16);
       jy_dev_free(eng, t.dups);
-      t.dups = nullptr;
+      jy_dev_free(eng, t.dups_alt);
+      t.dups = t.dups_alt = nullptr;
       t.dup_cap = 0;
       JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.dups), cap * 32, "treg duplicate list"));
+      JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.dups_alt), cap * 32, "treg duplicate list"));
+      if (!t.dupn_alt) JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.dupn_alt), 64, "treg duplicate count"));
       t.dup_cap = cap;
     }
   }
   K = state_of(eng);
-  K.seen = t.seen[t.parity];
-  const u64 bytes = ((t.seen_words * 4 + 15) & ~15ull);
-  // a grid too small to clear the other bitmap cheaply leaves it to a memset
-  if (bytes > (u64)nblocks * 4096) {
-    JY_HIP(eng, hipMemsetAsync(t.seen[t.parity ^ 1], 0, bytes, eng->stream));
-    K.clear = nullptr;
-    K.clear_bytes = 0;
-  } else {
-    K.clear = t.seen[t.parity ^ 1];
-    K.clear_bytes = bytes;
-  }
-  t.parity ^= 1;
+  JY_TRY(claim_bits(eng, nblocks, K));
   t.dup_bound += n;
   return JY_OK;
 }
@@ -441,16 +547,19 @@ int32_t jy_treg_merge(jy_engine* eng, u64 n, const u32* slot, const u64* ts, con
 
 int32_t jy_treg_merge_routed(jy_engine* eng, u32 S, u64 cap, u64 cap_byte, const u64* recs, const u64* hdr,
                              u64 rebase) {
-  const u64 n = (u64)S * cap;
-  if (n == 0) return JY_OK;
+  if ((u64)S * cap == 0) return JY_OK;
   JyTimed tm(eng);
-  const u32 grid = blocks(n, kThreads * 2);
-  TregK K{};
-  JY_TRY(claim_begin(eng, n, grid, K));
-  RoutedIn R{recs, hdr, S, cap, cap_byte, rebase, eng->nkeys[JY_TREG],
-             reinterpret_cast<unsigned long long*>(eng->skipped_dev)};
-  hipLaunchKernelGGL(k_treg_lww_routed, dim3(grid), dim3(kThreads), 0, eng->stream, K, R);
-  JY_HIP(eng, hipGetLastError());
+  // one source's run per launch: a key that several peers flushed in the same
+  // step is merged launch after launch (stream order), never a duplicate
+  const u32 grid = blocks(cap, kThreads * 2);
+  for (u32 src = 0; src < S; src++) {
+    TregK K{};
+    JY_TRY(claim_begin(eng, cap, grid, K));
+    RoutedIn R{recs + (u64)src * cap * 4, hdr + 2 * (u64)src, 1, cap, cap_byte, rebase + (u64)src * cap_byte,
+               eng->nkeys[JY_TREG], reinterpret_cast<unsigned long long*>(eng->skipped_dev)};
+    hipLaunchKernelGGL(k_treg_lww_routed, dim3(grid), dim3(kThreads), 0, eng->stream, K, R);
+    JY_HIP(eng, hipGetLastError());
+  }
   return JY_OK;
 }
 
@@ -503,6 +612,13 @@ int32_t jy_treg_set_batch(jy_engine* eng, u64 n, const u32* slot, const u64* ts,
   K.pflag = t.dflag;
   K.pcount = t.dcount;
   hipLaunchKernelGGL((k_treg_lww<false, true>), dim3(grid), dim3(kThreads), 0, eng->stream, K, slot, ts, pre, lr, n);
+  JY_HIP(eng, hipGetLastError());
+  JY_TRY(fold_rounds(eng, kFoldRounds, true));
+  K = state_of(eng);
+  K.pts = t.dts;
+  K.pval = t.dval;
+  K.pflag = t.dflag;
+  K.pcount = t.dcount;
   hipLaunchKernelGGL((k_treg_fold<true>), dim3(1), dim3(64), 0, eng->stream, K);
   JY_HIP(eng, hipGetLastError());
   t.dup_bound = 0;

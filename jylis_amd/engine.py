@@ -178,6 +178,53 @@ class Engine:
         self._check(fn(self.h, ctype, n, key_bytes.data_ptr(), key_offs.data_ptr(), out.data_ptr(), DEVICE))
         return out[:n]
 
+    def key_names(self, ctype, slot0, n):
+        """key strings of slots [slot0, slot0 + n) from the device directory (jy_keys_export)"""
+        offs = np.zeros(n + 1, np.uint64)
+        if n == 0:
+            return []
+        self._check(self.lib.jy_keys_export(self.h, ctype, slot0, n, offs.ctypes.data, None, 0))
+        buf = np.empty(max(int(offs[-1]), 1), np.uint8)
+        self._check(self.lib.jy_keys_export(self.h, ctype, slot0, n, offs.ctypes.data, buf.ctypes.data, len(buf)))
+        raw = buf.tobytes()
+        return [raw[int(offs[i]):int(offs[i + 1])] for i in range(n)]
+
+    def keys_route_part(self, key_bytes, key_offs, nshards):
+        """cross-shard key resolution, sender side (jy_keys_route_part): CUDA
+        uint8 key bytes + int64 offsets -> (owner i32[n], pos i32[n], lens
+        i64[n], bytes u8, counts i64[2 * nshards]) with the keys in owner order"""
+        import torch
+        n = int(key_offs.numel()) - 1
+        dev = key_offs.device
+        own = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        pos = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        lens = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        byts = torch.empty(max(int(key_bytes.numel()), 1), dtype=torch.uint8, device=dev)
+        cnt = torch.empty(2 * nshards, dtype=torch.int64, device=dev)
+        self._check(self.lib.jy_keys_route_part(self.h, n, key_bytes.data_ptr(), key_offs.data_ptr(), nshards,
+                                                own.data_ptr(), pos.data_ptr(), lens.data_ptr(), byts.data_ptr(),
+                                                cnt.data_ptr()))
+        return own[:n], pos[:n], lens[:n], byts, cnt
+
+    def keys_intern_lens(self, ctype, key_bytes, lens):
+        """intern received keys given as (bytes, lengths) CUDA tensors -> int32 slots (jy_keys_intern_lens)"""
+        import torch
+        n = int(lens.numel())
+        out = torch.empty(max(n, 1), dtype=torch.int32, device=lens.device)
+        if n:
+            self._check(self.lib.jy_keys_intern_lens(self.h, ctype, n, key_bytes.data_ptr(), lens.data_ptr(),
+                                                     out.data_ptr()))
+        return out[:n]
+
+    def keys_route_back(self, pos, answers):
+        """slots in input order: out[i] = answers[pos[i]] (jy_keys_route_back)"""
+        import torch
+        n = int(pos.numel())
+        out = torch.empty(max(n, 1), dtype=torch.int32, device=pos.device)
+        if n:
+            self._check(self.lib.jy_keys_route_back(self.h, n, pos.data_ptr(), answers.data_ptr(), out.data_ptr()))
+        return out[:n]
+
     def nkeys(self, ctype):
         return int(self.lib.jy_keys_count(self.h, ctype))
 

@@ -70,6 +70,7 @@ class _GpuRepo:
 
     def _intern(self, table):
         kb, ko = _keys_of(table)
+        self._sync_names()
         before = self.eng.nkeys(self.ctype)
         slots = self.eng.intern(self.ctype, (kb, ko))
         after = self.eng.nkeys(self.ctype)
@@ -83,6 +84,13 @@ class _GpuRepo:
                     seen.add(s)
                     self.names.append(bytes(kb[ko[i]:ko[i + 1]]))
         return slots
+
+    def _sync_names(self):
+        """names of keys interned on the device (route.KeyResolver, Engine.intern_device)
+        fetched from the directory (jy_keys_export)"""
+        n = self.eng.nkeys(self.ctype)
+        if len(self.names) < n:
+            self.names.extend(self.eng.key_names(self.ctype, len(self.names), n - len(self.names)))
 
     def slots_of(self, keys):
         self._drain()
@@ -112,10 +120,12 @@ class _GpuRepo:
 
     def _sorted_slots(self):
         self._drain()
+        self._sync_names()
         order = sorted(range(len(self.names)), key=lambda s: self.names[s])
         return np.array(order, dtype=np.uint32)
 
     def _keys_table(self, slots):
+        self._sync_names()
         names = [self.names[s] for s in slots]
         kb, ko = E.encode_keys(names)
         return {"key_bytes": kb, "key_offs": ko}

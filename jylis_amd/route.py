@@ -131,6 +131,25 @@ class LocalFabric:
         m = np.max(np.asarray(vals, np.int64), axis=0)
         return [m.copy() for _ in vals]
 
+    def host_a2a(self, vals):
+        """vals[s][r]: what rank s sends rank r (host ints) -> out[r][s]"""
+        v = np.asarray(vals, np.int64)
+        return [v[:, r].copy() for r in range(self.world)]
+
+    def a2a_v(self, outs, ins, out_splits, in_splits):
+        """variable all-to-all: rank s's segment r (in_splits[s][r] items) lands
+        as rank r's segment s (out_splits[r][s])"""
+        S = self.world
+        ioff = [np.concatenate([[0], np.cumsum(np.asarray(x, np.int64))]) for x in in_splits]
+        ooff = [np.concatenate([[0], np.cumsum(np.asarray(x, np.int64))]) for x in out_splits]
+        for r in range(S):
+            for s_ in range(S):
+                k = int(in_splits[s_][r])
+                assert k == int(out_splits[r][s_])
+                if k:
+                    outs[r].view(-1)[int(ooff[r][s_]):int(ooff[r][s_]) + k].copy_(
+                        ins[s_].view(-1)[int(ioff[s_][r]):int(ioff[s_][r]) + k])
+
 
 class DistFabric:
     """One rank per process over torch.distributed.  With the nccl backend
@@ -173,6 +192,26 @@ class DistFabric:
         t = torch.tensor(np.asarray(v, np.int64))
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.cpu_group)
         return [t.numpy()]
+
+    def host_a2a(self, vals):
+        """this rank's host ints per destination -> what every rank sends this one"""
+        import torch
+        (v,) = vals
+        t = torch.tensor(np.asarray(v, np.int64))
+        out = torch.empty_like(t)
+        self.dist.all_to_all_single(out, t, group=self.cpu_group)
+        return [out.numpy()]
+
+    def a2a_v(self, outs, ins, out_splits, in_splits):
+        """variable all-to-all (RCCL for CUDA tensors; gloo through host memory)"""
+        (out,), (inp,), (osp,), (isp,) = outs, ins, out_splits, in_splits
+        osp, isp = [int(x) for x in osp], [int(x) for x in isp]
+        if self.staged:
+            o = out.view(-1).cpu()
+            self.dist.all_to_all_single(o, inp.view(-1).cpu(), osp, isp, group=self.group)
+            out.view(-1).copy_(o)
+            return
+        self.dist.all_to_all_single(out.view(-1), inp.view(-1), osp, isp, group=self.group)
 
 
 def _bind_streams(engines):
@@ -613,6 +652,54 @@ class CounterRouter:
         return lambda cols, v: eng.gcount_converge_block(cols, 0, v[0])
 
 
+# ---- cross-shard key resolution on the GPU ----------------------------------------
+
+class KeyResolver:
+    """Owner and owner-side slot of every key of ingested batches, on the GPU
+    (k_keyroute.hip): the reference's `_data_for(key)` (repo_treg.pony:37-42,
+    every repo_*.pony) when the key's slot lives on another shard.
+
+    `resolve(keysets)`: keysets[i] = (key bytes uint8, key offsets int64) CUDA
+    tensors of local rank i -> [(owner int32, slot int32)] CUDA tensors.
+    Per call: the senders regroup their keys by owner (jy_keys_route_part),
+    the per-owner counts cross the host (one small readback + a host
+    all-to-all), the key lengths and bytes go to their owners (variable
+    all-to-alls: RCCL over xGMI with nccl), every owner interns what it
+    received in its device directory (jy_keys_intern_lens, create on miss),
+    and the slots come back the same way (jy_keys_route_back puts them in
+    input order).  Keys are never walked by the host."""
+
+    def __init__(self, engines, fabric, ctype):
+        self.engs = list(engines)
+        self.fabric = fabric
+        self.S = fabric.world
+        self.ctype = ctype
+        assert len(self.engs) == len(fabric.ranks)
+        _bind_streams(self.engs)
+
+    def resolve(self, keysets):
+        import torch
+        _check_streams(self.engs)
+        S, fab = self.S, self.fabric
+        parts = [e.keys_route_part(kb, ko, S) for e, (kb, ko) in zip(self.engs, keysets)]
+        cnt = [p[4].cpu().numpy() for p in parts]  # [keys per owner, bytes per owner]
+        send_k = [c[:S] for c in cnt]
+        send_b = [c[S:] for c in cnt]
+        recv_k = fab.host_a2a(send_k)
+        recv_b = fab.host_a2a(send_b)
+        dev = [torch.device("cuda", e.device) for e in self.engs]
+        lens = [torch.empty(max(int(k.sum()), 1), dtype=torch.int64, device=d) for k, d in zip(recv_k, dev)]
+        byts = [torch.empty(max(int(b.sum()), 1), dtype=torch.uint8, device=d) for b, d in zip(recv_b, dev)]
+        fab.a2a_v(lens, [p[2] for p in parts], recv_k, send_k)
+        fab.a2a_v(byts, [p[3] for p in parts], recv_b, send_b)
+        answers = [e.keys_intern_lens(self.ctype, b, l[:int(k.sum())])
+                   for e, b, l, k in zip(self.engs, byts, lens, recv_k)]
+        back = [torch.empty(max(int(p[0].numel()), 1), dtype=torch.int32, device=d) for p, d in zip(parts, dev)]
+        fab.a2a_v(back, [a if a.numel() else torch.empty(1, dtype=torch.int32, device=a.device) for a in answers],
+                  send_k, recv_k)
+        return [(p[0], e.keys_route_back(p[1], b)) for e, p, b in zip(self.engs, parts, back)]
+
+
 # ---- control plane ----------------------------------------------------------------
 
 def _a2a_host(dist, group, send, send_counts):
@@ -629,7 +716,9 @@ def _a2a_host(dist, group, send, send_counts):
 
 
 class ShardRouter:
-    """Owner-slot directory of one rank.
+    """Owner-slot directory of one rank, on the host: the reference the GPU
+    path (KeyResolver) is checked against, and the resolver of the CPU-only
+    gloo tests (an oracle stand-in interns there).
 
     `intern_local(keys_table) -> slots` interns keys on this rank's engine
     (or, in CPU tests, on an oracle stand-in)."""

@@ -51,6 +51,19 @@ def test_local_fabric_semantics():
     f.max_all(ts)
     assert [int(t) for t in ts] == [9, 9, 9]
     assert [m.tolist() for m in f.host_max([np.array([1, 5]), np.array([4, 2]), np.array([0, 0])])] == [[4, 5]] * 3
+    # variable all-to-all (key resolution): rank s sends splits[s][r] items to rank r
+    splits = np.array([[1, 0, 2], [0, 3, 1], [2, 2, 0]])
+    recv = f.host_a2a(splits)
+    assert [r.tolist() for r in recv] == [splits[:, r].tolist() for r in range(S)]
+    ins = [torch.arange(int(splits[s].sum()), dtype=torch.int64) + 100 * s for s in range(S)]
+    outs = [torch.empty(int(recv[r].sum()), dtype=torch.int64) for r in range(S)]
+    f.a2a_v(outs, ins, recv, splits)
+    for r in range(S):
+        want = []
+        for s in range(S):
+            a = int(splits[s][:r].sum())
+            want += (ins[s][a:a + int(splits[s][r])]).tolist()
+        assert outs[r].tolist() == want
 
 
 def _free_port():
@@ -81,7 +94,13 @@ def _worker(rank, world, port, q):
         m = torch.tensor([rank * 7 + 1], dtype=torch.int32)
         fab.max_all([m])
         hm = fab.host_max([np.array([rank, 10 - rank], np.int64)])[0]
-        q.put(("fabric", rank, out.tolist(), int(m), hm.tolist()))
+        # variable all-to-all: rank r sends r + 1 + d items to rank d
+        sp = np.array([rank + 1 + d for d in range(world)], np.int64)
+        rv = fab.host_a2a([sp])[0]
+        vin = torch.arange(int(sp.sum()), dtype=torch.int64) + 1000 * rank
+        vout = torch.empty(int(rv.sum()), dtype=torch.int64)
+        fab.a2a_v([vout], [vin], [rv], [sp])
+        q.put(("fabric", rank, out.tolist(), int(m), hm.tolist(), rv.tolist(), vout.tolist()))
         # ---- control plane: owner-side slots through the directory exchange
         names, index = [], {}
 
@@ -123,10 +142,16 @@ def test_two_rank_fabric_and_directory():
         p.start()
     from helpers import collect
     msgs = collect(procs, q, world * (1 + 3 + 1))
-    for _, rank, out, m, hm in (m for m in msgs if m[0] == "fabric"):
+    for _, rank, out, m, hm, rv, vout in (m for m in msgs if m[0] == "fabric"):
         assert out == [s * 1000 + rank * 3 + j for s in range(world) for j in range(3)]
         assert m == (world - 1) * 7 + 1
         assert hm == [world - 1, 10]
+        assert rv == [s + 1 + rank for s in range(world)]
+        want = []
+        for s in range(world):
+            a = sum(s + 1 + d for d in range(rank))
+            want += [1000 * s + a + j for j in range(s + 1 + rank)]
+        assert vout == want
     names = {m[1]: m[2] for m in msgs if m[0] == "names"}
     for _, rank, keys, own, slot in (m for m in msgs if m[0] == "resolved"):
         for k, o, s in zip(keys, own, slot):

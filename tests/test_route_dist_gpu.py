@@ -1,7 +1,9 @@
 """World-size-2 routing with the real data plane: two processes on cuda:0,
 each with its own engine (shard), torch.distributed over gloo (the
 collectives go through host memory; on an 8-GPU node the same DistFabric
-uses RCCL over xGMI).  The control plane resolves owner-side slots, the
+uses RCCL over xGMI).  The key resolution runs on the GPU (route.KeyResolver:
+keys regrouped by owner on the device, variable all-to-alls, interned by
+the owner's device directory, slots sent back), the
 HIP partition kernels build fixed-capacity runs, the runs cross the fabric
 and each owner merges what it received; the union of the two shards must
 equal one oracle repo that converged every ingested batch."""
@@ -54,15 +56,24 @@ def _worker(rank, world, port, q, seed):
         from jylis_amd._lib import PNCOUNT, TREG
         from jylis_amd.engine import Engine, encode_keys
         from jylis_amd.repo import RepoTREG
-        from jylis_amd.route import CounterRouter, DistFabric, ShardRouter, TregRouter, long_bytes
+        from jylis_amd.route import CounterRouter, DistFabric, KeyResolver, TregRouter, long_bytes
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
         torch.cuda.set_device(0)
         eng = Engine(device=0, counter_columns=8, ujson_columns=32)
         repo = RepoTREG(eng)
         fab = DistFabric(dist)
-        ctl = ShardRouter(rank, world, lambda tab: repo._intern({"key_bytes": tab[0], "key_offs": tab[1]}),
-                          dist=dist)
+
+        def resolver(ctype):
+            kr = KeyResolver([eng], fab, ctype)
+
+            def resolve(kb, ko):
+                kbt = torch.from_numpy(np.ascontiguousarray(kb, np.uint8)).to("cuda:0")
+                kot = torch.from_numpy(np.asarray(ko, np.uint64).view(np.int64)).to("cuda:0")
+                ((own, slot),) = kr.resolve([(kbt, kot)])
+                return own.cpu().numpy().view(np.uint32), slot.cpu().numpy().view(np.uint32)
+            return resolve
+        resolve_treg = resolver(TREG)
         router = TregRouter([eng], fab)
         rng = np.random.default_rng(seed + rank)
 
@@ -75,7 +86,7 @@ def _worker(rank, world, port, q, seed):
             vals = [bytes(rng.integers(97, 100, int(rng.integers(0, 20))).astype(np.uint8)) for _ in keys]
             ts = rng.integers(0, 4, len(keys)).astype(np.uint64)
             kb, ko = encode_keys(keys)
-            own, slot = ctl.resolve(kb, ko)
+            own, slot = resolve_treg(kb, ko)
             pre, lr = eng.pack_values(TREG, vals)
             router.step([(dev(own), dev(slot), dev(ts), dev(pre), dev(lr), long_bytes(lr))])
             q.put(("batch", rank, rnd, keys, [v.decode() for v in vals], ts.tolist()))
@@ -104,15 +115,15 @@ def _worker(rank, world, port, q, seed):
         from test_route_csr_gpu import table_rows, tlog_device_batch, ujson_device_batch
         tl, uj = RepoTLOG(eng), RepoUJSON(eng)
         eng.replica_cols(replica_ids(16, 7).tolist())  # one registration order on every shard
-        ctl_t = ShardRouter(rank, world, lambda tab: tl._intern({"key_bytes": tab[0], "key_offs": tab[1]}), dist=dist)
-        ctl_u = ShardRouter(rank, world, lambda tab: uj._intern({"key_bytes": tab[0], "key_offs": tab[1]}), dist=dist)
+        from jylis_amd._lib import TLOG, UJSON
+        resolve_tlog, resolve_ujson = resolver(TLOG), resolver(UJSON)
         trt, urt = TlogRouter([eng], fab), UjsonRouter([eng], fab)
         for rnd in range(3):
             t = _tlog_table(rank, rnd)
-            own, slot = ctl_t.resolve(t["key_bytes"], t["key_offs"])
+            own, slot = resolve_tlog(t["key_bytes"], t["key_offs"])
             trt.step([tlog_device_batch(eng, own, slot, t)])
             u = _ujson_table(rank, rnd)
-            own, slot = ctl_u.resolve(u["key_bytes"], u["key_offs"])
+            own, slot = resolve_ujson(u["key_bytes"], u["key_offs"])
             urt.step([ujson_device_batch(uj, own, slot, u)])
         trt.drain()
         urt.drain()

@@ -150,6 +150,142 @@ def test_treg_routed_overflow_drains(oracle_mod):
         node.close()
 
 
+@pytest.mark.parametrize("fab", sorted(FABRIC))
+def test_treg_routed_full_overlap(oracle_mod, fab):
+    """every key arrives from ALL S sources in one routed step
+    (every peer flushed the same hot keys): the owners merge the sources'
+    runs one launch per source, so the overlapping keys are exact and never
+    pile up in the duplicate fold"""
+    from jylis_amd.route import LocalFabric, TregRouter
+    S = 3
+    rng = np.random.default_rng(123)
+    node = _Node(S)
+    try:
+        router = TregRouter(node.engs, LocalFabric(S, **FABRIC[fab]))
+        seen = []
+        keys = rng.choice(6000, 3000, replace=False)
+        for rnd in range(3):
+            bs = []
+            for r in range(S):
+                b = _treg_batch(np.random.default_rng(1000 * rnd + r), 3000, 6000, ts_hi=3)
+                # the same key set on every source (values and timestamps differ)
+                from jylis_amd.engine import encode_keys
+                kb, ko = encode_keys([f"rk{int(x)}" for x in keys])
+                b["key_bytes"], b["key_offs"] = kb, ko
+                bs.append(b)
+            seen += bs
+            router.step([node.ingest(r, b) for r, b in enumerate(bs)])
+        router.drain()
+        assert node.union_state() == _oracle_dict(oracle_mod, seen)
+    finally:
+        node.close()
+
+
+def test_treg_device_batch_many_repeats(oracle_mod):
+    """a device batch naming each of its keys up to 12 times: the parallel
+    fold rounds take the first few occurrences, the one-wave fold the rest"""
+    from jylis_amd._lib import TREG
+    from jylis_amd.engine import Engine, encode_keys
+    from jylis_amd.repo import RepoTREG
+    rng = np.random.default_rng(5)
+    eng = Engine(device=0)
+    try:
+        repo = RepoTREG(eng)
+        names = [f"m{i}" for i in range(2000)]
+        kb, ko = encode_keys(names)
+        slots = repo._intern({"key_bytes": kb, "key_offs": ko})
+        reps = rng.integers(1, 13, len(names))
+        idx = rng.permutation(np.repeat(np.arange(len(names)), reps))
+        vals = [bytes(rng.integers(97, 100, int(rng.integers(0, 14))).astype(np.uint8)) for _ in idx]
+        ts = rng.integers(0, 4, len(idx)).astype(np.uint64)
+        pre, lr = eng.pack_values(TREG, vals)
+        eng.treg_converge(_dev(slots[idx], np.uint32), _dev(ts, np.uint64), _dev(pre, np.uint64),
+                          _dev(lr, np.uint64))
+        want = O_dict = {}
+        for i, v, t in zip(idx, vals, ts):
+            k = names[i].encode()
+            cand = (int(t), v)
+            if k not in want or cand > want[k]:
+                want[k] = cand
+        st = repo.state()
+        got = {k: (int(t), bytes(st["val_bytes"][st["val_offs"][i]:st["val_offs"][i + 1]]))
+               for i, (k, t) in enumerate(zip(oracle_mod.split_keys(st), st["ts"]))}
+        assert got == O_dict
+    finally:
+        eng.close()
+
+
+def _keys_dev(keys):
+    import torch
+    from jylis_amd.engine import encode_keys
+    kb, ko = encode_keys(keys)
+    return (torch.from_numpy(np.ascontiguousarray(kb, np.uint8)).to("cuda:0"),
+            torch.from_numpy(np.asarray(ko, np.uint64).view(np.int64)).to("cuda:0"))
+
+
+@pytest.mark.parametrize("S", [1, 2, 3])
+def test_key_resolver_on_device(oracle_mod, S):
+    """cross-shard key resolution on the GPU (k_keyroute.hip,
+    route.KeyResolver): owners hashed on the device equal jy_key_owner; every
+    key's slot names that key in its owner's directory; a key gets one slot
+    whichever rank ingests it, and repeated within a batch; an empty batch,
+    the empty key and keys past 8 bytes ride along; the TREG data plane routed
+    with those slots equals one oracle repo"""
+    from jylis_amd._lib import TREG
+    from jylis_amd.engine import encode_keys
+    from jylis_amd.route import KeyResolver, LocalFabric, TregRouter, long_bytes, owners
+    rng = np.random.default_rng(70 + S)
+    node = _Node(S)
+    try:
+        fab = LocalFabric(S)
+        kr = KeyResolver(node.engs, fab, TREG)
+        router = TregRouter(node.engs, fab)
+        slot_of = {}
+        seen = []
+        for rnd in range(3):
+            keysets, per = [], []
+            for r in range(S):
+                n = 0 if (rnd == 1 and r == S - 1) else 1500
+                keys = [f"rk{int(x)}" + ("-long-key-suffix" if int(x) % 7 == 0 else "")
+                        for x in rng.integers(0, 4000, n)]  # repeats inside the batch
+                if n and rnd == 2:
+                    keys[0] = ""
+                per.append(keys)
+                keysets.append(_keys_dev(keys))
+            res = kr.resolve(keysets)
+            batches = []
+            for r, (keys, (own, slot)) in enumerate(zip(per, res)):
+                own_h = own.cpu().numpy().view(np.uint32)
+                slot_h = slot.cpu().numpy().view(np.uint32)
+                kb, ko = encode_keys(keys)
+                assert (own_h == owners(kb, ko, S)).all()
+                for k, o, sl in zip(keys, own_h, slot_h):
+                    assert slot_of.setdefault(k, (int(o), int(sl))) == (int(o), int(sl))
+                # one delta per key per batch (the contract of a flushed batch)
+                first = {}
+                for i, k in enumerate(keys):
+                    first.setdefault(k, i)
+                idx = np.array(sorted(first.values()), np.int64)
+                ks = [keys[i] for i in idx]
+                vals = [bytes(rng.integers(97, 100, int(rng.integers(0, 20))).astype(np.uint8)) for _ in ks]
+                ts = rng.integers(0, 4, len(ks)).astype(np.uint64)
+                kb2, ko2 = encode_keys(ks)
+                vb, vo = encode_keys(vals)
+                seen.append({"key_bytes": kb2, "key_offs": ko2, "ts": ts, "val_bytes": vb, "val_offs": vo})
+                pre, lr = node.engs[r].pack_values(TREG, vals)
+                batches.append((_dev(own_h[idx], np.uint32), _dev(slot_h[idx], np.uint32), _dev(ts, np.uint64),
+                                _dev(pre, np.uint64), _dev(lr, np.uint64), long_bytes(lr)))
+            router.step(batches)
+        router.drain()
+        for d, repo in enumerate(node.repos):
+            repo._sync_names()
+        for k, (o, sl) in slot_of.items():
+            assert node.repos[o].names[sl] == k.encode()
+        assert node.union_state() == _oracle_dict(oracle_mod, seen)
+    finally:
+        node.close()
+
+
 def test_treg_arena_collect_waits_for_drain(oracle_mod):
     """a drain round re-reads the long-value bytes of a pending
     batch through its handles, so collecting the sending engine's arena
