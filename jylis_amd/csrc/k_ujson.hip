@@ -109,6 +109,87 @@ __device__ __forceinline__ bool contains(const u64* __restrict__ a, u64 lo, u64 
   return i < hi && a[i] == x;
 }
 
+// ---- wave-cooperative lower bounds (every lane of a wave calls with the
+// same searches): 64-ary probes per round, so a segment of n sorted dots
+// costs ceil(log64 n) dependent round trips instead of ~log2 n; the N
+// searches advance together (each round issues all their probes at once).
+// A wave whose 64 items lie in ONE long document bounds every item's search
+// this way (the other side's range between its first and last dot), and the
+// items then search only those few entries.
+struct WSearch {
+  const u64* a;  // dots at a[i * stride]
+  u32 stride;
+  u64 lo, hi, x;  // in: range and key; out: lo = hi = first index with a >= x
+};
+template <int N>
+__device__ __forceinline__ void wave_lbs(WSearch (&s)[N]) {
+  const u64 lane = __lane_id();
+  for (;;) {  // wave-uniform: lo / hi come from ballots
+    bool more = false;
+    u64 v[N], step[N];
+#pragma unroll
+    for (int q = 0; q < N; q++) {
+      step[q] = s[q].hi > s[q].lo ? (s[q].hi - s[q].lo + 63) / 64 : 0;
+      const u64 at = s[q].lo + (lane + 1) * step[q] - 1;
+      v[q] = step[q] && at < s[q].hi ? s[q].a[at * s[q].stride] : ~0ull;
+    }
+#pragma unroll
+    for (int q = 0; q < N; q++) {
+      if (!step[q]) continue;
+      const u64 at = s[q].lo + (lane + 1) * step[q] - 1;
+      const u64 c = __popcll(__ballot(at < s[q].hi && v[q] < s[q].x));  // blocks wholly below x (a prefix)
+      const u64 nlo = s[q].lo + c * step[q];
+      s[q].lo = nlo;
+      if (step[q] == 1) {
+        s[q].hi = nlo;
+      } else {
+        // block c's last entry is >= x (or past hi): the bound is at or before it
+        s[q].hi = nlo + step[q] - 1 < s[q].hi ? nlo + step[q] - 1 : s[q].hi;
+        more = true;
+      }
+    }
+    if (!more) return;
+  }
+}
+
+// A short segment's lower bound + membership with the final window's loads
+// issued up front (win_load) and consumed later (win_rank): an item issues
+// the windows of all its lookups at once -- one round trip for the short
+// segments of a small document -- instead of one search after another.
+// Segments of W or more are first bisected down to W - 1 (dependent loads).
+template <int W>
+struct Win {
+  u64 lo, hi;
+  u64 v[W];
+};
+// The lower bound lies in [lo, hi] after bisecting, so the window spans
+// [lo, lo + W) clipped to the segment's end (w.hi), which includes position
+// hi itself: an equal dot found there is a member.
+template <bool kRec, int W>
+__device__ __forceinline__ void win_load(Win<W>& w, const void* src, u64 lo, u64 hi, u64 x) {
+  const u64 end = hi;
+  while (hi - lo >= W) {
+    const u64 m = (lo + hi) >> 1;
+    if (dot_at<kRec>(src, m) < x) lo = m + 1;
+    else hi = m;
+  }
+  w.lo = lo;
+  w.hi = end;
+#pragma unroll
+  for (int j = 0; j < W; j++) w.v[j] = lo + j < end ? dot_at<kRec>(src, lo + j) : ~0ull;
+}
+template <int W>
+__device__ __forceinline__ u64 win_rank(const Win<W>& w, u64 x, bool& eq) {
+  u32 c = 0;
+  eq = false;
+#pragma unroll
+  for (int j = 0; j < W; j++) {
+    c += w.v[j] < x;
+    eq = eq || (w.v[j] == x && w.lo + j < w.hi);
+  }
+  return w.lo + c;
+}
+
 __device__ __forceinline__ URec load_rec(const URec* p) {
   const u64x2 v = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(p));
   return URec{v.x, v.y};
@@ -156,10 +237,9 @@ struct UjArgs {
   u64* neo;    // [nd + 1] output offsets (elements)
   u64* nco;    // [nd + 1] output offsets (cloud)
   u64* base;   // [2] this converge's pool bases
-  u64* vvs;    // [nd][R] state vv rows as they were
   u64* vvd;    // [nd][R] the delta's vv, dense (zero between converges)
-  u64* vvm;    // [nd][R] max(vvs, vvd)
-  u64* vvn;    // [nd][R] after compaction
+  u64* vvm;    // [nd][R] max(state row, vvd): the ONE working row per delta doc;
+               // the state rows are read in place and raised by U3's folds
   // scans: sc over [state elements | delta elements | delta cloud], ksc over
   // [state cloud | delta cloud]; tile-local exclusive prefixes (see ScanSp)
   u32* sc;
@@ -225,10 +305,10 @@ __device__ __forceinline__ ScanSp ksc_space(const UjArgs& A) {
   return ScanSp{A.ksc, A.ktp, tc, tc + A.cb, tc + A.cb, t1, tn, tn};
 }
 
-__device__ __forceinline__ bool in_state_ctx(const UjArgs& A, u64 k, u64 d) {
-  if (dseq(d) <= A.vvs[k * A.R + dcol(d)]) return true;
-  return contains(A.cloud, A.cbs[k], A.cbs[k] + (A.co[k + 1] - A.co[k]), d);
-}
+// the state's vv entry of delta doc k: the state rows are read in place
+// (only U5 writes them, after U3's folds raised them with atomics)
+__device__ __forceinline__ u64 state_vv(const UjArgs& A, u64 k, u32 c) { return A.vv[(u64)A.slot[k] * A.R + c]; }
+
 
 // ---- tiles: the documents of an item range [i0, i1) of a CSR offs[0..nd],
 // staged in LDS (first wave searches; everyone loads); doc_of() per item
@@ -448,9 +528,7 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_e
           const u64 dk = j / A.R;
           if (j < tot && kt0 + dk < A.nd) {
             const u64 g = kt0 * A.R + j;
-            A.vvs[g] = v[u];
             A.vvm[g] = v[u];
-            A.vvn[g] = v[u];
           }
         }
       }
@@ -476,7 +554,6 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_e
       const u64 g = (kt0 + lo) * A.R + c;
       if (dseq(x) > A.vvm[g]) {  // one entry per (doc, column) unless the doc is bad
         A.vvm[g] = dseq(x);
-        A.vvn[g] = dseq(x);
       }
     }
     JY_CLK(c2);
@@ -534,6 +611,61 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_e
 // rank of an item is its merge position on the other side (relative to that
 // side's segment of the doc); bit 31 of a state element's rank: U5 takes the
 // delta's element for it.
+// U2 for a wave of items inside long document k (wave-uniform): the keep
+// flag and cross rank of item i (as uj_flags_tile), every search bounded by
+// the wave's cooperative searches of the other side(s)
+__device__ __forceinline__ void uj_flags_long(const UjArgs& A, int kind, u64 k, u64 i, u64 n, u64 gbase, u64& f) {
+  const bool live = i < n;
+  const u64 lm = __ballot(live);
+  if (lm == 0) return;  // a wave past the space's end
+  const u64 lastl = (u64)__popcll(lm) - 1;  // the wave's items are a prefix of its lanes
+  const u64 clo = A.cbs[k], chi = clo + (A.co[k + 1] - A.co[k]);
+  u64 d = 0;
+  if (kind == 0) {
+    if (live) d = A.rec[A.abase[k] + (i - A.ao[k])].dot;
+  } else if (kind == 1) {
+    if (live) d = A.ddots[i];
+  } else {
+    if (live) d = A.dcloud[i];
+  }
+  const u64 d0 = __shfl(d, 0), d1 = __shfl(d, (int)lastl) + 1;  // the wave's dots lie in [d0, d1)
+  if (kind == 0) {
+    // the delta's elements, the delta's cloud and the state cloud over [d0, d1)
+    const u64 lo = A.deoff[k], hi = A.deoff[k + 1], blo = A.dcoff[k], bhi = A.dcoff[k + 1];
+    WSearch s[6] = {{A.ddots, 1, lo, hi, d0},  {A.ddots, 1, lo, hi, d1},  {A.dcloud, 1, blo, bhi, d0},
+                    {A.dcloud, 1, blo, bhi, d1}, {A.cloud, 1, clo, chi, d0}, {A.cloud, 1, clo, chi, d1}};
+    wave_lbs<6>(s);
+    if (!live) return;
+    const u64 p = lower_bound(A.ddots, s[0].lo, s[1].lo, d);
+    u32 xr = (u32)(p - lo);
+    if (p < hi && A.ddots[p] == d) {
+      f = 1;
+      if (!(dseq(d) <= state_vv(A, k, dcol(d)) || contains(A.cloud, s[4].lo, s[5].lo, d))) xr |= 1u << 31;
+    } else {
+      f = A.keep_all || !(dseq(d) <= A.vvd[k * A.R + dcol(d)] || contains(A.dcloud, s[2].lo, s[3].lo, d));
+    }
+    A.xr[gbase + i] = xr;
+  } else if (kind == 1) {
+    // the state's elements and cloud over [d0, d1)
+    const u64 lo = A.abase[k], hi = lo + (A.ao[k + 1] - A.ao[k]);
+    WSearch s[4] = {{&A.rec[0].dot, 2, lo, hi, d0}, {&A.rec[0].dot, 2, lo, hi, d1}, {A.cloud, 1, clo, chi, d0},
+                    {A.cloud, 1, clo, chi, d1}};
+    wave_lbs<4>(s);
+    if (!live) return;
+    const u64 p = lb_g<true>(A.rec, s[0].lo, s[1].lo, d);
+    f = !(p < hi && A.rec[p].dot == d) &&
+        !(dseq(d) <= state_vv(A, k, dcol(d)) || contains(A.cloud, s[2].lo, s[3].lo, d));
+    A.xr[gbase + i] = (u32)(p - lo);
+  } else {
+    WSearch s[2] = {{A.cloud, 1, clo, chi, d0}, {A.cloud, 1, clo, chi, d1}};
+    wave_lbs<2>(s);
+    if (!live) return;
+    const u64 p = lower_bound(A.cloud, s[0].lo, s[1].lo, d);
+    f = !(p < chi && A.cloud[p] == d);
+    A.xr[gbase + i] = (u32)(p - clo);
+  }
+}
+
 __device__ __forceinline__ void uj_flags_tile(const UjArgs& A, const u64 t, u64* red) {
   const u64 ta = A.ao[A.nd];
   const u64 tA = cdiv(ta), tB = cdiv(A.nb);
@@ -551,38 +683,62 @@ __device__ __forceinline__ void uj_flags_tile(const UjArgs& A, const u64 t, u64*
   }
   const u64 i = lt * kTile + threadIdx.x;
   u64 f = 0;
-  if (i < n) {
-    const u64 k = doc_at(A, tm, lt, sid, i);
-#ifdef JY_UJ_AB_NOLONG  // A/B only: items of long documents skip their searches (WRONG results)
-    if ((u32)(tm[lt] >> 32) == A.epoch) {
-    } else
-#endif
-    if (!is_bad(A, k)) {
-      const u64 clo = A.cbs[k], chi = clo + (A.co[k + 1] - A.co[k]);
+  // a tile wholly inside one long document: its waves bound every item's
+  // search with wave-cooperative searches between their first and last dot
+  const u64 tmv = tm[lt];
+  if ((u32)(tmv >> 32) == A.epoch) {
+    const u64 k = (u32)tmv;
+    if (!is_bad(A, k)) uj_flags_long(A, kind, k, i, n, gbase, f);
+  } else if (i < n) {
+    // small documents: every lookup of the item issued at once (the doc's
+    // words, then the item's dot, then all its windows): ~4 round trips
+    const u64 k = (u32)(tmv >> 32) == A.epoch ? (u32)tmv : sid[i];
+    const bool bad = is_bad(A, k);
+    const u64 clo = A.cbs[k], chi = clo + (A.co[k + 1] - A.co[k]);
+    const u32 sl = A.slot[k];
+    if (!bad) {
       u32 xr;
       if (kind == 0) {
+        const u64 lo = A.deoff[k], hi = A.deoff[k + 1], blo = A.dcoff[k], bhi = A.dcoff[k + 1];
         const u64 d = A.rec[A.abase[k] + (i - A.ao[k])].dot;
-        const u64 lo = A.deoff[k], hi = A.deoff[k + 1];
-        const u64 p = lower_bound(A.ddots, lo, hi, d);
+        Win<8> wb;
+        Win<4> wdc, wsc;
+        win_load<false>(wb, A.ddots, lo, hi, d);
+        win_load<false>(wdc, A.dcloud, blo, bhi, d);
+        win_load<false>(wsc, A.cloud, clo, chi, d);
+        const u64 vd = A.vvd[k * A.R + dcol(d)], vs = A.vv[(u64)sl * A.R + dcol(d)];
+        bool eqb, indc, insc;
+        const u64 p = win_rank(wb, d, eqb);
+        win_rank(wdc, d, indc);
+        win_rank(wsc, d, insc);
         xr = (u32)(p - lo);
-        if (p < hi && A.ddots[p] == d) {
+        if (eqb) {
           f = 1;
-          if (!in_state_ctx(A, k, d)) xr |= 1u << 31;
+          if (!(dseq(d) <= vs || insc)) xr |= 1u << 31;
         } else {
-          f = A.keep_all ||
-              !(dseq(d) <= A.vvd[k * A.R + dcol(d)] || contains(A.dcloud, A.dcoff[k], A.dcoff[k + 1], d));
+          f = A.keep_all || !(dseq(d) <= vd || indc);
         }
       } else if (kind == 1) {
-        const u64 d = A.ddots[i];
         const u64 lo = A.abase[k], hi = lo + (A.ao[k + 1] - A.ao[k]);
-        const u64 p = lb_g<true>(A.rec, lo, hi, d);
+        const u64 d = A.ddots[i];
+        Win<8> wa;
+        Win<4> wsc;
+        win_load<true>(wa, A.rec, lo, hi, d);
+        win_load<false>(wsc, A.cloud, clo, chi, d);
+        const u64 vs = A.vv[(u64)sl * A.R + dcol(d)];
+        bool eqa, insc;
+        const u64 p = win_rank(wa, d, eqa);
+        win_rank(wsc, d, insc);
         xr = (u32)(p - lo);
-        f = !(p < hi && A.rec[p].dot == d) && !(dseq(d) <= A.vvs[k * A.R + dcol(d)] || contains(A.cloud, clo, chi, d));
+        f = !eqa && !(dseq(d) <= vs || insc);
       } else {
         const u64 x = A.dcloud[i];
-        const u64 p = lower_bound(A.cloud, clo, chi, x);
+        Win<8> wsc;
+        win_load<false>(wsc, A.cloud, clo, chi, x);
+        bool insc;
+        const u64 p = win_rank(wsc, x, insc);
         xr = (u32)(p - clo);
-        f = !(p < chi && A.cloud[p] == x);
+        f = !insc;
       }
       A.xr[gbase + i] = xr;
     }
@@ -611,6 +767,63 @@ __global__ __launch_bounds__(kItemThreads) void k_uj_flags(UjArgs A) {
 // union rank of x (column c, seq q) above v: state dots of c in (v, q) plus
 // de-duplicated delta dots of c in (v, q) (U2's kind-2 flags); x folds into
 // the vv when the run from v + 1 reaches it unbroken
+// U3 for a wave of cloud items inside long document k (wave-uniform; sa:
+// state cloud, else delta cloud): as uj_compact_tile, with the run starts of
+// the wave's first and last column and the bounds of its dot range found by
+// wave-cooperative searches (a wave of a long cloud spans one or two columns)
+__device__ __forceinline__ void uj_compact_long(const UjArgs& A, bool sa, u64 k, u64 i, u64 n, u64& f) {
+  const bool live = i < n;
+  const u64 lm = __ballot(live);
+  if (lm == 0) return;
+  const int lastl = __popcll(lm) - 1;
+  const u64 ta = A.ao[A.nd], tc = A.co[A.nd];
+  const ScanSp sp = sc_space(A);
+  const u64 cb0 = ta + A.nb;
+  const u64 alo = A.cbs[k], ahi = alo + (A.co[k + 1] - A.co[k]);
+  const u64 blo = A.dcoff[k], bhi = A.dcoff[k + 1];
+  const u64 pi = alo + (i - A.co[k]);
+  u64 x = 0;
+  if (live) x = sa ? A.cloud[pi] : A.dcloud[i];
+  const u64 x0 = __shfl(x, 0), x1 = __shfl(x, lastl) + 1;
+  const u32 cf = dcol(x0), cl = dcol(x1 - 1);
+  const u64 lof = mkdot(cf, A.vvm[k * A.R + cf] + 1), lol = mkdot(cl, A.vvm[k * A.R + cl] + 1);
+  // [0, 1]: run starts on the state side, [2, 3]: on the delta side, [4, 5]:
+  // the other side's bounds of the wave's dots
+  WSearch s[6] = {{A.cloud, 1, alo, ahi, lof},  {A.cloud, 1, alo, ahi, lol}, {A.dcloud, 1, blo, bhi, lof},
+                  {A.dcloud, 1, blo, bhi, lol}, {sa ? A.dcloud : A.cloud, 1, sa ? blo : alo, sa ? bhi : ahi, x0},
+                  {sa ? A.dcloud : A.cloud, 1, sa ? blo : alo, sa ? bhi : ahi, x1}};
+  wave_lbs<6>(s);
+  if (!live) return;
+  const u32 c = dcol(x);
+  const u64 q = dseq(x), v = A.vvm[k * A.R + c];
+  if (q <= v) return;
+  const u64 lo = mkdot(c, v + 1);
+  const u64 ra0 = c == cf ? s[0].lo : c == cl ? s[1].lo : lower_bound(A.cloud, alo, ahi, lo);
+  const u64 b0 = c == cf ? s[2].lo : c == cl ? s[3].lo : lower_bound(A.dcloud, blo, bhi, lo);
+  if (sa) {
+    const u64 ra = pi - ra0;
+    const u64 b1 = lower_bound(A.dcloud, s[4].lo, s[5].lo, x);
+    const u64 rb = sp.at(cb0 + b1) - sp.at(cb0 + b0);
+    if (q == v + 1 + ra + rb) {
+      __hip_atomic_fetch_max(&A.vv[(u64)A.slot[k] * A.R + c], q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      f = 1;
+      A.kr[i] = (u32)(b1 - blo);
+    }
+  } else {
+    const u64 s0 = sp.at(cb0 + i);
+    if (sp.at(cb0 + i + 1) == s0) return;  // held by the state cloud
+    const u64 a1 = lower_bound(A.cloud, s[4].lo, s[5].lo, x);
+    const u64 rb = s0 - sp.at(cb0 + b0);
+    if (q == v + 1 + (a1 - ra0) + rb) {
+      __hip_atomic_fetch_max(&A.vv[(u64)A.slot[k] * A.R + c], q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      f = 1;
+      A.kr[tc + i] = (u32)(a1 - alo);
+    }
+  }
+}
+
 __device__ __forceinline__ void uj_compact_tile(const UjArgs& A, const u64 t, u64* red) {
   const u64 ta = A.ao[A.nd], tc = A.co[A.nd];
   const ScanSp sp = sc_space(A);
@@ -621,47 +834,67 @@ __device__ __forceinline__ void uj_compact_tile(const UjArgs& A, const u64 t, u6
   const u64 lt = sa ? t : t - tA, n = sa ? tc : A.cb, gbase = sa ? 0 : tc;
   const u64 i = lt * kTile + threadIdx.x;
   u64 f = 0;
-  if (i < n) {
-    const u64 k = sa ? doc_at(A, A.tmC, lt, A.sidC, i) : doc_at(A, A.tmD, lt, A.sidD, i);
-    if (!is_bad(A, k)) {
-      const u64 alo = A.cbs[k], ahi = alo + (A.co[k + 1] - A.co[k]);
-      const u64 blo = A.dcoff[k], bhi = A.dcoff[k + 1];
-      if (sa) {
-        const u64 pi = alo + (i - A.co[k]);
-        const u64 x = A.cloud[pi];
-        const u32 c = dcol(x);
-        const u64 q = dseq(x), v = A.vvm[k * A.R + c];
+  const u64 tmv = sa ? A.tmC[lt] : A.tmD[lt];
+  if ((u32)(tmv >> 32) == A.epoch) {  // a tile inside one long document
+    const u64 k = (u32)tmv;
+    if (!is_bad(A, k)) uj_compact_long(A, sa, k, i, n, f);
+  } else if (i < n) {
+    // small documents: the item's independent lookups issued together
+    const u64 k = (u32)(tmv >> 32) == A.epoch ? (u32)tmv : (sa ? A.sidC[i] : A.sidD[i]);
+    const bool bad = is_bad(A, k);
+    const u64 alo = A.cbs[k], co0 = A.co[k], ahi = alo + (A.co[k + 1] - co0);
+    const u64 blo = A.dcoff[k], bhi = A.dcoff[k + 1];
+    const u32 sl = A.slot[k];
+    if (sa) {
+      const u64 pi = alo + (i - co0);
+      const u64 x = bad ? 0 : A.cloud[pi];
+      const u32 c = dcol(x);
+      const u64 q = dseq(x);
+      Win<4> w1;
+      if (!bad) win_load<false>(w1, A.dcloud, blo, bhi, x);  // b1 needs only x
+      const u64 v = bad ? ~0ull : A.vvm[k * A.R + c];
+      if (q > v) {
+        const u64 lo = mkdot(c, v + 1);
+        Win<4> wa, w0;
+        win_load<false>(wa, A.cloud, alo, pi, lo);
+        win_load<false>(w0, A.dcloud, blo, bhi, lo);
+        bool e;
+        const u64 b1 = win_rank(w1, x, e);
+        const u64 ra = pi - win_rank(wa, lo, e);
+        const u64 b0 = win_rank(w0, lo, e);
+        const u64 rb = sp.at(cb0 + b1) - sp.at(cb0 + b0);
+        if (q == v + 1 + ra + rb) {
+          __hip_atomic_fetch_max(&A.vv[(u64)sl * A.R + c], q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          f = 1;
+          A.kr[i] = (u32)(b1 - blo);
+        }
+      }
+    } else {
+      // the dedupe prefix and the dot need no document
+      const u64 s0 = sp.at(cb0 + i), s1 = sp.at(cb0 + i + 1);
+      const u64 x = A.dcloud[i];
+      const u32 c = dcol(x);
+      const u64 q = dseq(x);
+      if (!bad && s1 != s0) {  // not held by the state cloud
+        Win<4> w1;
+        win_load<false>(w1, A.cloud, alo, ahi, x);  // a1 needs only x
+        const u64 v = A.vvm[k * A.R + c];
         if (q > v) {
           const u64 lo = mkdot(c, v + 1);
-          const u64 ra = pi - lower_bound(A.cloud, alo, pi, lo);
-          const u64 b0 = lower_bound(A.dcloud, blo, bhi, lo);
-          const u64 b1 = lower_bound(A.dcloud, b0, bhi, x);
-          const u64 rb = sp.at(cb0 + b1) - sp.at(cb0 + b0);
-          if (q == v + 1 + ra + rb) {
-            __hip_atomic_fetch_max(&A.vvn[k * A.R + c], q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          Win<4> wa, wb;
+          win_load<false>(wa, A.cloud, alo, ahi, lo);
+          win_load<false>(wb, A.dcloud, blo, i, lo);
+          bool e;
+          const u64 a1 = win_rank(w1, x, e);
+          const u64 a0 = win_rank(wa, lo, e);
+          const u64 b0 = win_rank(wb, lo, e);
+          const u64 rb = s0 - sp.at(cb0 + b0);
+          if (q == v + 1 + (a1 - a0) + rb) {
+            __hip_atomic_fetch_max(&A.vv[(u64)sl * A.R + c], q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           } else {
             f = 1;
-            A.kr[i] = (u32)(b1 - blo);
-          }
-        }
-      } else {
-        const u64 s0 = sp.at(cb0 + i);
-        if (sp.at(cb0 + i + 1) != s0) {  // not held by the state cloud
-          const u64 x = A.dcloud[i];
-          const u32 c = dcol(x);
-          const u64 q = dseq(x), v = A.vvm[k * A.R + c];
-          if (q > v) {
-            const u64 lo = mkdot(c, v + 1);
-            const u64 a0 = lower_bound(A.cloud, alo, ahi, lo);
-            const u64 a1 = lower_bound(A.cloud, a0, ahi, x);
-            const u64 b0 = lower_bound(A.dcloud, blo, i, lo);
-            const u64 rb = s0 - sp.at(cb0 + b0);
-            if (q == v + 1 + (a1 - a0) + rb) {
-              __hip_atomic_fetch_max(&A.vvn[k * A.R + c], q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-              f = 1;
-              A.kr[tc + i] = (u32)(a1 - alo);
-            }
+            A.kr[tc + i] = (u32)(a1 - alo);
           }
         }
       }
@@ -752,8 +985,12 @@ __device__ __forceinline__ void uj_scatter_tile(const UjArgs& A, const u64 t) {
   if (kind == 4) {  // vv rows back into the state; the dense delta vv back to zero
     if (i >= nv) return;
     const u64 k = i / A.R, c = i - k * A.R;
-    if (!is_bad(A, k)) A.vv[(u64)A.slot[k] * A.R + c] = A.vvn[i];
-    A.vvd[i] = 0;
+    if (!is_bad(A, k)) {  // max(state row as U3's folds left it, merged row)
+      u64* r = A.vv + (u64)A.slot[k] * A.R + c;
+      const u64 m = A.vvm[i];
+      if (m > *r) *r = m;
+    }
+    if (A.vvd[i]) A.vvd[i] = 0;  // only the delta's sparse entries were set
     return;
   }
   if (kind == 5) {  // metas
@@ -1176,10 +1413,8 @@ int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* sl
   A.neo = tb + 4 * (nd + 1);
   A.nco = tb + 5 * (nd + 1);
   A.base = tb + 6 * (nd + 1);
-  JY_TRY(jy_scratch(eng, 10, nd * R * 24 + 64, &p));
-  A.vvs = static_cast<u64*>(p);
-  A.vvm = A.vvs + nd * R;
-  A.vvn = A.vvm + nd * R;
+  JY_TRY(jy_scratch(eng, 10, nd * R * 8 + 64, &p));
+  A.vvm = static_cast<u64*>(p);
   A.vvd = u.vvd;
   JY_TRY(jy_scratch(eng, 11, (le + nel + ncloud + 2) * 4, &p));
   A.sc = static_cast<u32*>(p);

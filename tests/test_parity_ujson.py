@@ -195,3 +195,60 @@ def test_hot_document_long_segments(oracle_mod):
             assert_state_equal(O.UJSON, want.state(), got.state())
     finally:
         eng.close()
+
+
+def test_hot_document_long_cloud(oracle_mod):
+    """a document whose causal context holds thousands of gapped cloud dots
+    over every column, then deltas that fill some gaps (the runs fold into the
+    vv) and leave others: long cloud segments take the wave-cooperative
+    searches of U2 / U3 on both the state and the delta side, and the waves
+    straddle column boundaries"""
+    from jylis_amd import synth as S
+    from jylis_amd.engine import Engine, encode_keys
+    from jylis_amd.repo import RepoUJSON
+    O = oracle_mod
+    R = 6
+    ids = S.replica_ids(R, 91)
+    rng = np.random.default_rng(21)
+
+    def table(docs):
+        t = {k: [] for k in ("dot_ids", "dot_seqs", "elems", "vv_ids", "vv_seqs", "cloud_ids", "cloud_seqs")}
+        eo, vo, co = [0], [0], [0]
+        for _, els, vv, cl in docs:
+            for (c, q), e in sorted(els.items()):
+                t["dot_ids"].append(ids[c]), t["dot_seqs"].append(q), t["elems"].append(e)
+            for c, n in sorted(vv.items()):
+                t["vv_ids"].append(ids[c]), t["vv_seqs"].append(n)
+            for c, q in sorted(cl):
+                t["cloud_ids"].append(ids[c]), t["cloud_seqs"].append(q)
+            eo.append(len(t["elems"])), vo.append(len(t["vv_ids"])), co.append(len(t["cloud_ids"]))
+        out = {k: np.array(v, np.uint64) for k, v in t.items()}
+        out["key_bytes"], out["key_offs"] = encode_keys([d[0] for d in docs])
+        out["el_offs"], out["vv_offs"], out["cloud_offs"] = (np.array(x, np.uint64) for x in (eo, vo, co))
+        return out
+
+    # state: vv = 1 per column, the odd seqs 3, 5, ... up to ~2 * 700 in the
+    # cloud, an element under every fourth cloud dot
+    cl = {(c, q) for c in range(R) for q in range(3, 3 + 2 * int(rng.integers(500, 900)), 2)}
+    els = {d: int(rng.integers(1, 1 << 30)) for d in sorted(cl)[::4]}
+    batches = [table([(b"hot", els, {c: 1 for c in range(R)}, cl), (b"cold", {(0, 1): 3}, {0: 1}, set())])]
+    for rnd in range(3):
+        # fill the gaps 2, 4, ... of some columns up to a random point (a
+        # contiguous run folds), plus scattered even dots further up
+        dcl = set()
+        for c in range(R):
+            top = int(rng.integers(0, 1200))
+            dcl |= {(c, q) for q in range(2, top, 2)}
+            dcl |= {(c, int(q)) for q in rng.integers(top, 2000, 40) if q % 2 == 0}
+        dels = {d: int(rng.integers(1, 1 << 30)) for d in sorted(dcl)[::7]}
+        batches.append(table([(b"hot", dels, {}, dcl)]))
+    eng = Engine(device=0, ujson_columns=R)
+    try:
+        want = O.Repo(O.UJSON, 1)
+        got = RepoUJSON(eng)
+        for b in batches:
+            want.converge(b)
+            got.converge_deltas(b)
+            assert_state_equal(O.UJSON, want.state(), got.state())
+    finally:
+        eng.close()
