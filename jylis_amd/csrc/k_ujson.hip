@@ -30,21 +30,26 @@
 // above the merged vv v folds into the vv iff seq(x) == v + 1 + |union dots
 // of c in (v, seq(x))|.
 //
-// FIVE launches per converge and no host round trip:
-//   U1 k_uj_docs     per delta doc: slot claim, meta, state vv rows, scans of
-//                    the touched-state sizes; per delta item: validation and
+// FIVE item launches (+ two one-workgroup tile scans) per converge and no
+// host round trip:
+//   U1 k_uj_docs     per delta doc: slot claim, meta, scans of the touched-
+//                    state sizes, the doc of every item (ids, or a tile map
+//                    inside long segments); per delta item: validation and
 //                    the dense delta vv
-//   U2 k_uj_flags    keep flags of state / delta elements and delta cloud
-//                    dedupe, scanned; merged vv
-//   U3 k_uj_compact  cloud compaction against the merged vv, scanned
+//   U2 k_uj_flags    keep flags and cross ranks of state / delta elements and
+//                    delta cloud dedupe, tile-scanned
+//   U3 k_uj_compact  cloud compaction against the merged vv (the state rows,
+//                    raised in place by the folds, max the delta vv),
+//                    tile-scanned
 //   U4 k_uj_sizes    per-document output sizes, scanned; the pools' bump
 //                    pointers move on the device
-//   U5 k_uj_scatter  every kept item to its merge-path position; vv rows and
-//                    metas; the next converge's zero state
-// Scans are single-pass (jy_scan.hpp: tickets + decoupled look-back), item
-// launches are persistent grids that read their sizes from device memory,
-// and each tile finds the documents of its items with one search over the
-// CSR offsets staged in LDS -- no segment-id arrays.  Claims (a slot named
+//   U5 k_uj_scatter  every kept item to its merge-path position; the delta's
+//                    sparse vv entries into the state rows; metas; the dense
+//                    delta vv back to zero
+// No [docs][R] working rows: the state rows are read in place and only the
+// delta's sparse vv entries are written back.  Doc scans are single-pass
+// (jy_scan.hpp: tickets + decoupled look-back); item launches are persistent
+// grids that read their sizes from device memory.  Claims (a slot named
 // twice in one batch: both copies skipped) and bad marks carry the
 // converge's epoch, so nothing is reset with a memset.  The host reads pool
 // use back only through a mapped pinned word written by U4 and checks it
@@ -52,7 +57,7 @@
 //
 // Roofline: HBM.  Per touched element: 16 B read + 16 B written (+ 4 B
 // scan value, written and read); per touched cloud dot 8 B read + 8 B
-// written (+ 4 B); vv rows and metas of delta docs.
+// written (+ 4 B); the delta's vv entries and the metas of delta docs.
 
 #include <algorithm>
 #include <cstring>
@@ -103,10 +108,6 @@ __device__ __forceinline__ u64 lb_g(const void* src, u64 lo, u64 hi, u64 x) {
 }
 __device__ __forceinline__ u64 lower_bound(const u64* __restrict__ a, u64 lo, u64 hi, u64 x) {
   return lb_g<false>(a, lo, hi, x);
-}
-__device__ __forceinline__ bool contains(const u64* __restrict__ a, u64 lo, u64 hi, u64 x) {
-  const u64 i = lower_bound(a, lo, hi, x);
-  return i < hi && a[i] == x;
 }
 
 // ---- wave-cooperative lower bounds (every lane of a wave calls with the
@@ -238,8 +239,7 @@ struct UjArgs {
   u64* nco;    // [nd + 1] output offsets (cloud)
   u64* base;   // [2] this converge's pool bases
   u64* vvd;    // [nd][R] the delta's vv, dense (zero between converges)
-  u64* vvm;    // [nd][R] max(state row, vvd): the ONE working row per delta doc;
-               // the state rows are read in place and raised by U3's folds
+  u32* sidV;   // [nvv] the doc of every sparse delta vv entry (U1 -> U5)
   // scans: sc over [state elements | delta elements | delta cloud], ksc over
   // [state cloud | delta cloud]; tile-local exclusive prefixes (see ScanSp)
   u32* sc;
@@ -308,6 +308,15 @@ __device__ __forceinline__ ScanSp ksc_space(const UjArgs& A) {
 // the state's vv entry of delta doc k: the state rows are read in place
 // (only U5 writes them, after U3's folds raised them with atomics)
 __device__ __forceinline__ u64 state_vv(const UjArgs& A, u64 k, u32 c) { return A.vv[(u64)A.slot[k] * A.R + c]; }
+// the merged vv entry max(state, delta) of delta doc k for U3.  U3's folds
+// raise the state rows in place while other items read them: any value read
+// is the merged entry raised by a run of folded dots that starts at it, and
+// "seq(x) == v + 1 + |union dots in (v, seq(x))|" decides the same for every
+// such v (a value at or past seq(x) means x itself is folded: dropped)
+__device__ __forceinline__ u64 merged_vv(const UjArgs& A, u64 k, u32 c) {
+  const u64 s = state_vv(A, k, c), d = A.vvd[k * A.R + c];
+  return s > d ? s : d;
+}
 
 
 // ---- tiles: the documents of an item range [i0, i1) of a CSR offs[0..nd],
@@ -397,7 +406,7 @@ __global__ __launch_bounds__(1024) void k_uj_tscan(UjArgs A, int which) {
 }
 
 #ifdef JY_UJ_PROBE  // A/B only: per-tile clocks of U2..U4 (wall clock, 100 MHz)
-constexpr u32 kProbe = 32768;
+constexpr u32 kProbe = 65536;
 __device__ u64 g_probe[kProbe][6];
 __device__ u32 g_probe_n;
 __device__ __forceinline__ void probe(u32 kern, u32 kind, u32 t, u64 c0, u64 c1, u64 c2, u64 ca = 0, u64 cb = 0) {
@@ -428,9 +437,8 @@ struct LongRun {
 // per delta item (validation, dense delta vv) ---------------------------------
 __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_el, u64 t_cl, u64 t_vv) {
   __shared__ Shared S;
-  __shared__ u32 l_slot[kDocTile];
   __shared__ LongRun l_long[4 * kDocTile];
-  __shared__ u32 l_nlong, l_nreal;
+  __shared__ u32 l_nlong;
   if (blockIdx.x < ndt) {  // doc tiles: ticketed (the look-back walks tickets)
     if (threadIdx.x == 0) l_nlong = 0;
     const u32 t = jyscan::ticket(A.tick + T_U1, &S.tk);
@@ -439,7 +447,6 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_e
     u64 asz = 0, csz = 0;
     if (k < A.nd) {
       const u32 s = A.slot[k];
-      l_slot[threadIdx.x] = s;
       const bool hole = s == JY_NO_SLOT;  // a routed run's unused record (k_route_csr.hip)
       const UMeta m = hole ? UMeta{} : A.meta[s];
       A.abase[k] = m.ebase;
@@ -504,58 +511,6 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_e
       u64* tm = g.sp == 0 ? A.tmA : g.sp == 1 ? A.tmB : g.sp == 2 ? A.tmC : A.tmD;
       for (u64 m = g.f0 + threadIdx.x; m < g.f1; m += kThreads) tm[m] = ((u64)A.epoch << 32) | g.k;
     }
-    // the state vv rows (lanes on consecutive columns of a row), then the
-    // merged rows max(state, delta) from the docs' sparse delta vv entries
-    const u64 kt0 = (u64)t * kDocTile;
-    {
-      // kVvBatch rows' loads in flight before their stores (the arrays may
-      // alias as far as the compiler knows: without the batching every
-      // iteration waited for its own load, ~16 round trips at R = 16)
-      constexpr int kVvBatch = 8;
-      const u64 tot = kDocTile * A.R;
-      for (u64 j0 = threadIdx.x; j0 < tot; j0 += (u64)kThreads * kVvBatch) {
-        u64 v[kVvBatch];
-#pragma unroll
-        for (int u = 0; u < kVvBatch; u++) {
-          const u64 j = j0 + (u64)u * kThreads;
-          const u64 dk = j / A.R, c = j - dk * A.R;
-          v[u] = 0;
-          if (j < tot && kt0 + dk < A.nd && l_slot[dk] != JY_NO_SLOT) v[u] = A.vv[(u64)l_slot[dk] * A.R + c];
-        }
-#pragma unroll
-        for (int u = 0; u < kVvBatch; u++) {
-          const u64 j = j0 + (u64)u * kThreads;
-          const u64 dk = j / A.R;
-          if (j < tot && kt0 + dk < A.nd) {
-            const u64 g = kt0 * A.R + j;
-            A.vvm[g] = v[u];
-          }
-        }
-      }
-    }
-    const u64 kt1 = kt0 + kDocTile < A.nd ? kt0 + kDocTile : A.nd;
-    for (u64 j = threadIdx.x; j <= kt1 - kt0; j += kThreads) S.offs[j] = A.dvoff[kt0 + j];
-    // a routed run ends in holes whose last one spans the run's unused
-    // capacity: the walk stops after the tile's last real doc
-    if (threadIdx.x == 0) l_nreal = 0;
-    __syncthreads();
-    if (kt0 + threadIdx.x < kt1 && l_slot[threadIdx.x] != JY_NO_SLOT) atomicMax(&l_nreal, threadIdx.x + 1);
-    __syncthreads();
-    for (u64 j = S.offs[0] + threadIdx.x; j < S.offs[l_nreal]; j += kThreads) {
-      u32 lo = 0, hi = (u32)(kt1 - kt0 - 1);  // the doc of entry j
-      while (lo < hi) {
-        const u32 m = (lo + hi + 1) >> 1;
-        if (S.offs[m] <= j) lo = m;
-        else hi = m - 1;
-      }
-      const u64 x = A.dvv[j];
-      const u32 c = dcol(x);
-      if (c >= A.R) continue;  // a bad doc (U1 item tiles mark it)
-      const u64 g = (kt0 + lo) * A.R + c;
-      if (dseq(x) > A.vvm[g]) {  // one entry per (doc, column) unless the doc is bad
-        A.vvm[g] = dseq(x);
-      }
-    }
     JY_CLK(c2);
     JY_PROBE(1, 0, t, c0, c1, c2);
     return;
@@ -581,6 +536,7 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_e
   } else {
     return;
   }
+  JY_CLK(c0);
   const u64 i0 = tt * kTile1, i1 = i0 + kTile1 < n ? i0 + kTile1 : n;
   const TileDocs T = tile_docs<kLdsDocs>(offs, A.nd, i0, i1, S.offs, S.sh);
 #pragma unroll
@@ -591,6 +547,7 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_e
     if (kind == 2) {
       const u64 x = A.dvv[i];
       const u32 c = dcol(x);
+      A.sidV[i] = (u32)k;
       if (c >= A.R || (i > A.dvoff[k] && dcol(A.dvv[i - 1]) >= c)) {
         mark_bad(A, k);
         continue;
@@ -602,6 +559,8 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_e
       if (dcol(x) >= A.R || dseq(x) < 1 || (i > offs[k] && a[i - 1] >= x)) mark_bad(A, k);
     }
   }
+  JY_CLK(c2);
+  JY_PROBE(1, 1 + kind, (u32)tt, c0, c2, c2);
 }
 
 // ---- U2: keep flags + cross ranks ----------------------------------------------
@@ -636,13 +595,25 @@ __device__ __forceinline__ void uj_flags_long(const UjArgs& A, int kind, u64 k, 
                     {A.dcloud, 1, blo, bhi, d1}, {A.cloud, 1, clo, chi, d0}, {A.cloud, 1, clo, chi, d1}};
     wave_lbs<6>(s);
     if (!live) return;
-    const u64 p = lower_bound(A.ddots, s[0].lo, s[1].lo, d);
+    // the item's three lookups inside the wave's bounds, issued together
+    // with its vv entries (the bounds hold every dot of [d0, d1), so a dot
+    // equal to d lies inside them)
+    Win<8> wb;
+    Win<4> wdc, wsc;
+    win_load<false>(wb, A.ddots, s[0].lo, s[1].lo, d);
+    win_load<false>(wdc, A.dcloud, s[2].lo, s[3].lo, d);
+    win_load<false>(wsc, A.cloud, s[4].lo, s[5].lo, d);
+    const u64 vd = A.vvd[k * A.R + dcol(d)], vs = state_vv(A, k, dcol(d));
+    bool eqb, indc, insc;
+    const u64 p = win_rank(wb, d, eqb);
+    win_rank(wdc, d, indc);
+    win_rank(wsc, d, insc);
     u32 xr = (u32)(p - lo);
-    if (p < hi && A.ddots[p] == d) {
+    if (eqb) {
       f = 1;
-      if (!(dseq(d) <= state_vv(A, k, dcol(d)) || contains(A.cloud, s[4].lo, s[5].lo, d))) xr |= 1u << 31;
+      if (!(dseq(d) <= vs || insc)) xr |= 1u << 31;
     } else {
-      f = A.keep_all || !(dseq(d) <= A.vvd[k * A.R + dcol(d)] || contains(A.dcloud, s[2].lo, s[3].lo, d));
+      f = A.keep_all || !(dseq(d) <= vd || indc);
     }
     A.xr[gbase + i] = xr;
   } else if (kind == 1) {
@@ -652,16 +623,25 @@ __device__ __forceinline__ void uj_flags_long(const UjArgs& A, int kind, u64 k, 
                     {A.cloud, 1, clo, chi, d1}};
     wave_lbs<4>(s);
     if (!live) return;
-    const u64 p = lb_g<true>(A.rec, s[0].lo, s[1].lo, d);
-    f = !(p < hi && A.rec[p].dot == d) &&
-        !(dseq(d) <= state_vv(A, k, dcol(d)) || contains(A.cloud, s[2].lo, s[3].lo, d));
+    Win<8> wa;
+    Win<4> wsc;
+    win_load<true>(wa, A.rec, s[0].lo, s[1].lo, d);
+    win_load<false>(wsc, A.cloud, s[2].lo, s[3].lo, d);
+    const u64 vs = state_vv(A, k, dcol(d));
+    bool eqa, insc;
+    const u64 p = win_rank(wa, d, eqa);
+    win_rank(wsc, d, insc);
+    f = !eqa && !(dseq(d) <= vs || insc);
     A.xr[gbase + i] = (u32)(p - lo);
   } else {
     WSearch s[2] = {{A.cloud, 1, clo, chi, d0}, {A.cloud, 1, clo, chi, d1}};
     wave_lbs<2>(s);
     if (!live) return;
-    const u64 p = lower_bound(A.cloud, s[0].lo, s[1].lo, d);
-    f = !(p < chi && A.cloud[p] == d);
+    Win<8> wsc;
+    win_load<false>(wsc, A.cloud, s[0].lo, s[1].lo, d);
+    bool insc;
+    const u64 p = win_rank(wsc, d, insc);
+    f = !insc;
     A.xr[gbase + i] = (u32)(p - clo);
   }
 }
@@ -747,7 +727,7 @@ __device__ __forceinline__ void uj_flags_tile(const UjArgs& A, const u64 t, u64*
   u64 tot;
   const u64 x = item_scan(f, red, tot);
   JY_CLK(c2);
-  JY_PROBE(2, kind, (u32)t, c0, c1, c2);
+  JY_PROBE(2, kind + ((u32)(tmv >> 32) == A.epoch ? 8 : 0), (u32)t, c0, c1, c2);
   if (i < n) A.sc[gbase + i] = (u32)x;
   if (threadIdx.x == 0) A.tp[t] = tot;
 }
@@ -786,7 +766,7 @@ __device__ __forceinline__ void uj_compact_long(const UjArgs& A, bool sa, u64 k,
   if (live) x = sa ? A.cloud[pi] : A.dcloud[i];
   const u64 x0 = __shfl(x, 0), x1 = __shfl(x, lastl) + 1;
   const u32 cf = dcol(x0), cl = dcol(x1 - 1);
-  const u64 lof = mkdot(cf, A.vvm[k * A.R + cf] + 1), lol = mkdot(cl, A.vvm[k * A.R + cl] + 1);
+  const u64 lof = mkdot(cf, merged_vv(A, k, cf) + 1), lol = mkdot(cl, merged_vv(A, k, cl) + 1);
   // [0, 1]: run starts on the state side, [2, 3]: on the delta side, [4, 5]:
   // the other side's bounds of the wave's dots
   WSearch s[6] = {{A.cloud, 1, alo, ahi, lof},  {A.cloud, 1, alo, ahi, lol}, {A.dcloud, 1, blo, bhi, lof},
@@ -795,7 +775,7 @@ __device__ __forceinline__ void uj_compact_long(const UjArgs& A, bool sa, u64 k,
   wave_lbs<6>(s);
   if (!live) return;
   const u32 c = dcol(x);
-  const u64 q = dseq(x), v = A.vvm[k * A.R + c];
+  const u64 q = dseq(x), v = merged_vv(A, k, c);
   if (q <= v) return;
   const u64 lo = mkdot(c, v + 1);
   const u64 ra0 = c == cf ? s[0].lo : c == cl ? s[1].lo : lower_bound(A.cloud, alo, ahi, lo);
@@ -852,7 +832,7 @@ __device__ __forceinline__ void uj_compact_tile(const UjArgs& A, const u64 t, u6
       const u64 q = dseq(x);
       Win<4> w1;
       if (!bad) win_load<false>(w1, A.dcloud, blo, bhi, x);  // b1 needs only x
-      const u64 v = bad ? ~0ull : A.vvm[k * A.R + c];
+      const u64 v = bad ? ~0ull : merged_vv(A, k, c);
       if (q > v) {
         const u64 lo = mkdot(c, v + 1);
         Win<4> wa, w0;
@@ -879,7 +859,7 @@ __device__ __forceinline__ void uj_compact_tile(const UjArgs& A, const u64 t, u6
       if (!bad && s1 != s0) {  // not held by the state cloud
         Win<4> w1;
         win_load<false>(w1, A.cloud, alo, ahi, x);  // a1 needs only x
-        const u64 v = A.vvm[k * A.R + c];
+        const u64 v = merged_vv(A, k, c);
         if (q > v) {
           const u64 lo = mkdot(c, v + 1);
           Win<4> wa, wb;
@@ -904,7 +884,7 @@ __device__ __forceinline__ void uj_compact_tile(const UjArgs& A, const u64 t, u6
   u64 tot;
   const u64 x = item_scan(f, red, tot);
   JY_CLK(c2);
-  JY_PROBE(3, sa ? 0 : 1, (u32)t, c0, c1, c2);
+  JY_PROBE(3, (sa ? 0 : 1) + ((u32)(tmv >> 32) == A.epoch ? 8 : 0), (u32)t, c0, c1, c2);
   if (i < n) A.ksc[gbase + i] = (u32)x;
   if (threadIdx.x == 0) A.ktp[t] = tot;
 }
@@ -969,28 +949,46 @@ __global__ __launch_bounds__(kThreads) void k_uj_sizes(UjArgs A, u64 ndt) {
 // ---- U5: scatter into the fresh runs; vv rows, metas; zero state for the next converge
 // (no scan: one item per thread; the grid is the host's bound, surplus
 // workgroups exit at once)
+__device__ __forceinline__ void uj_scatter_kind(const UjArgs& A, int kind, u64 lt, u64 ta, u64 tc, const ScanSp& sp,
+                                                const ScanSp& kp, const u32* xrb, const u32* krb, u64 nv);
 __device__ __forceinline__ void uj_scatter_tile(const UjArgs& A, const u64 t) {
   const u64 ta = A.ao[A.nd], tc = A.co[A.nd];
   const ScanSp sp = sc_space(A), kp = ksc_space(A);
   const u32* xrb = A.xr + ta;
   const u32* krb = A.kr + tc;
-  const u64 nv = A.nd * A.R;
+  const u64 nv = A.nvv;
   const u64 tl[6] = {cdiv(ta), cdiv(A.nb), cdiv(tc), cdiv(A.cb), cdiv(nv), cdiv(A.nd)};
   int kind = 0;
   u64 lt = t;
   while (kind < 6 && lt >= tl[kind]) lt -= tl[kind++];
   if (kind == 6) return;
+  JY_CLK(c0);
+  uj_scatter_kind(A, kind, lt, ta, tc, sp, kp, xrb, krb, nv);
+  JY_CLK(c2);
+#ifdef JY_UJ_PROBE
+  const u64* tmk = kind == 0 ? A.tmA : kind == 1 ? A.tmB : kind == 2 ? A.tmC : A.tmD;
+  const bool lng = kind < 4 && (u32)(tmk[lt] >> 32) == A.epoch;
+#endif
+  JY_PROBE(5, kind + (lng ? 8 : 0), (u32)lt, c0, c2, c2);
+}
+__device__ __forceinline__ void uj_scatter_kind(const UjArgs& A, int kind, u64 lt, u64 ta, u64 tc, const ScanSp& sp,
+                                                const ScanSp& kp, const u32* xrb, const u32* krb, u64 nv) {
   const u64 i = lt * kTile + threadIdx.x;
   const u64 eb0 = A.base[0], cb0 = A.base[1];
-  if (kind == 4) {  // vv rows back into the state; the dense delta vv back to zero
+  if (kind == 4) {  // the delta's sparse vv entries into the state rows; the dense delta vv back to zero
     if (i >= nv) return;
-    const u64 k = i / A.R, c = i - k * A.R;
-    if (!is_bad(A, k)) {  // max(state row as U3's folds left it, merged row)
+    const u64 x = A.dvv[i];
+    const u32 c = dcol(x);
+    if (c >= A.R) return;  // never written (the doc is bad)
+    const u64 k = A.sidV[i];
+    // the state rows already hold U3's folds; elsewhere max(state, delta) is
+    // the state (one entry per (doc, column) unless the doc is bad)
+    if (!is_bad(A, k)) {
       u64* r = A.vv + (u64)A.slot[k] * A.R + c;
-      const u64 m = A.vvm[i];
-      if (m > *r) *r = m;
+      const u64 q = dseq(x);
+      if (q > *r) *r = q;
     }
-    if (A.vvd[i]) A.vvd[i] = 0;  // only the delta's sparse entries were set
+    A.vvd[k * A.R + c] = 0;
     return;
   }
   if (kind == 5) {  // metas
@@ -1040,7 +1038,7 @@ __device__ __forceinline__ void uj_scatter_tile(const UjArgs& A, const u64 t) {
 __global__ __launch_bounds__(kItemThreads) void k_uj_scatter(UjArgs A) {
   if (blockIdx.x == 0 && threadIdx.x == 0)
     for (int c = T_U1; c <= T_U4; c++) A.tick[c] = 0;  // U1..U4 of this converge are done
-  const u64 T = cdiv(A.ao[A.nd]) + cdiv(A.nb) + cdiv(A.co[A.nd]) + cdiv(A.cb) + cdiv(A.nd * A.R) + cdiv(A.nd);
+  const u64 T = cdiv(A.ao[A.nd]) + cdiv(A.nb) + cdiv(A.co[A.nd]) + cdiv(A.cb) + cdiv(A.nvv) + cdiv(A.nd);
   for (u64 t = blockIdx.x; t < T; t += gridDim.x) uj_scatter_tile(A, t);
 }
 
@@ -1413,8 +1411,8 @@ int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* sl
   A.neo = tb + 4 * (nd + 1);
   A.nco = tb + 5 * (nd + 1);
   A.base = tb + 6 * (nd + 1);
-  JY_TRY(jy_scratch(eng, 10, nd * R * 8 + 64, &p));
-  A.vvm = static_cast<u64*>(p);
+  JY_TRY(jy_scratch(eng, 10, nvv * 4 + 64, &p));
+  A.sidV = static_cast<u32*>(p);
   A.vvd = u.vvd;
   JY_TRY(jy_scratch(eng, 11, (le + nel + ncloud + 2) * 4, &p));
   A.sc = static_cast<u32*>(p);
@@ -1460,7 +1458,7 @@ int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* sl
   hipLaunchKernelGGL(k_uj_compact, dim3((u32)gk), dim3(kItemThreads), 0, eng->stream, A);
   hipLaunchKernelGGL(k_uj_tscan, dim3(1), dim3(1024), 0, eng->stream, A, 1);
   hipLaunchKernelGGL(k_uj_sizes, dim3((u32)ndt), dim3(kThreads), 0, eng->stream, A, ndt);
-  const u64 g5 = gf + gk + (nd * R + kTile - 1) / kTile + (nd + kTile - 1) / kTile + 2;
+  const u64 g5 = gf + gk + (nvv + kTile - 1) / kTile + (nd + kTile - 1) / kTile + 2;
   hipLaunchKernelGGL(k_uj_scatter, dim3((u32)g5), dim3(kItemThreads), 0, eng->stream, A);
   JY_HIP(eng, hipGetLastError());
 #ifdef JY_UJ_PROBE

@@ -10,7 +10,7 @@ while i < len(a):
 for r in calls[-1:]:
     kern = (r[:, 0] >> 56) & 0xff; kind = (r[:, 0] >> 48) & 0xff; t = r[:, 0] & 0xffffffff
     t0 = r[:, 1].min()
-    for K in (1, 2, 3, 4):
+    for K in (1, 2, 3, 4, 5):
         m = kern == K
         if not m.any():
             continue
