@@ -437,7 +437,11 @@ struct LongRun {
 // per delta item (validation, dense delta vv) ---------------------------------
 __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_el, u64 t_cl, u64 t_vv) {
   __shared__ Shared S;
-  __shared__ LongRun l_long[4 * kDocTile];
+  // 64 runs staged (1 KB): U1's LDS stays small enough for every tile of a
+  // converge to be resident at once; a tile with more long runs has the
+  // owning threads fill the rest themselves
+  constexpr u32 kLongCap = 64;
+  __shared__ LongRun l_long[kLongCap];
   __shared__ u32 l_nlong;
   if (blockIdx.x < ndt) {  // doc tiles: ticketed (the look-back walks tickets)
     if (threadIdx.x == 0) l_nlong = 0;
@@ -494,7 +498,11 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_e
         for (u64 j = off; j < f0 * kTile; j++) sid[j] = (u32)k;
         for (u64 j = f1 * kTile; j < off + sz; j++) sid[j] = (u32)k;
         const u32 q = atomicAdd(&l_nlong, 1u);  // the workgroup fills its tile-map run
-        l_long[q] = LongRun{(u32)f0, (u32)f1, (u32)k, (u32)(tm == A.tmA ? 0 : tm == A.tmB ? 1 : tm == A.tmC ? 2 : 3)};
+        if (q < kLongCap) {
+          l_long[q] = LongRun{(u32)f0, (u32)f1, (u32)k, (u32)(tm == A.tmA ? 0 : tm == A.tmB ? 1 : tm == A.tmC ? 2 : 3)};
+        } else {
+          for (u64 m = f0; m < f1; m++) tm[m] = ((u64)A.epoch << 32) | k;
+        }
       };
       ids(A.sidA, A.tmA, pa + xa, asz);
       ids(A.sidC, A.tmC, pc + xc, csz);
@@ -506,7 +514,7 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_e
       A.co[A.nd] = pc + tot;
     }
     __syncthreads();
-    for (u32 q = 0; q < l_nlong; q++) {
+    for (u32 q = 0; q < min(l_nlong, kLongCap); q++) {
       const LongRun g = l_long[q];
       u64* tm = g.sp == 0 ? A.tmA : g.sp == 1 ? A.tmB : g.sp == 2 ? A.tmC : A.tmD;
       for (u64 m = g.f0 + threadIdx.x; m < g.f1; m += kThreads) tm[m] = ((u64)A.epoch << 32) | g.k;
