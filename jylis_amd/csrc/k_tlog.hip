@@ -358,8 +358,9 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
 #endif
   // 2. slow entries, one per lane per pass
   u32 carry = 0;
-  u64 c_t[kCache], c_p[kCache], c_l[kCache];
-  u32 c_q[kCache], c_i[kCache];
+  constexpr int kCacheN = kCache > 0 ? kCache : 1;
+  u64 c_t[kCacheN], c_p[kCacheN], c_l[kCacheN];
+  u32 c_q[kCacheN], c_i[kCacheN];
 #pragma unroll
   for (int c = 0; c < kCache; c++) c_q[c] = c_i[c] = 0, c_t[c] = c_p[c] = c_l[c] = 0;
   int pass = 0;
