@@ -540,8 +540,11 @@ def bench_tlog(args, eng, dev, dist, rank, world):
     def step(i):
         eng.tlog_converge(*dev_batches[1 + i % nb])
 
+    st0 = eng.tlog_stats()
     elapsed, kt = _timed(args.steps, args.warmup, step, dist, dev, eng=eng)
     t = _max_over_ranks(elapsed, dist, dev)
+    eng.sync()  # settles the last merge: its spill (if any) is counted
+    st1 = eng.tlog_stats()
     # replay the same sequence on a fresh engine pass to get exact in/out
     # entry counts per step: state entries are the running total (the engine
     # keeps it), so re-run step by step outside the timed region
@@ -577,6 +580,9 @@ def bench_tlog(args, eng, dev, dist, rank, world):
                         f"per step, dups/ties/cutoffs (SURVEY 8d config 4); {n_state0} initial entries",
             "unit_of_work": "log entry (input)", "value": world * units * args.steps / t,
             "ms_per_step": t / args.steps * 1e3, "verified_sampled_keys": bool(verified),
+            # merges of warmup + timed steps that spilled (re-merged after a
+            # compaction, host never waited) and the compactions they caused
+            "spills_compactions": [st1["spills"] - st0["spills"], st1["compactions"] - st0["compactions"]],
             "roofline": {"bound": "hbm", "achieved": avg_b / k / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": avg_b / k / 1e9 / HBM_PEAK_GBS,
                          "kernel": "TLOG converge (k_tlog_*, all launches of one call)",
