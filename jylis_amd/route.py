@@ -122,6 +122,8 @@ class LocalFabric:
     def max_all(self, ts):
         """in place: every tensor becomes the max over ranks"""
         import torch
+        if len(ts) == 1:
+            return _Done()  # the max over one rank is its own value
         m = torch.stack([t.view(-1) for t in ts]).max(0).values
         for t in ts:
             t.view(-1).copy_(m)
@@ -381,14 +383,18 @@ class _RunRouter:
     def _publish(self, batches, ovfs):
         """global max of the overflow counts, copied to pinned memory behind an event"""
         import torch
-        gm = [o[:1].clone() for o in ovfs]
-        self.fabric.max_all(gm)
         # a pinned pair per engine for this round, back in the pool once settled
         pins = self._pin_pool.pop() if self._pin_pool else [torch.empty(2, dtype=torch.int32, pin_memory=True)
                                                             for _ in ovfs]
-        for g, o, p in zip(gm, ovfs, pins):
-            p[0:1].copy_(g, non_blocking=True)
-            p[1:2].copy_(o[:1], non_blocking=True)
+        if self.S == 1 and len(ovfs) == 1:
+            # one rank: the global max is the own count (one copy, no reduction)
+            pins[0][0:1].copy_(ovfs[0][:1], non_blocking=True)
+        else:
+            gm = [o[:1].clone() for o in ovfs]
+            self.fabric.max_all(gm)
+            for g, o, p in zip(gm, ovfs, pins):
+                p[0:1].copy_(g, non_blocking=True)
+                p[1:2].copy_(o[:1], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         self.pending.append((batches, ovfs, pins, ev))
@@ -403,7 +409,7 @@ class _RunRouter:
             self._hold(False)  # a drain round below holds them again
         ev.synchronize()
         gmax = int(pins[0][0])
-        counts = [int(p[1]) for p in pins]
+        counts = [gmax] if (self.S == 1 and len(pins) == 1) else [int(p[1]) for p in pins]
         self._pin_pool.append(pins)
         if gmax == 0:
             return
