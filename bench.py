@@ -6,16 +6,20 @@ Workload (BASELINE.json configs[1]): PNCOUNT,
 delta batch: 64 flushed peer batches (one per replica column, each covering
 every key, both signs) = 2^31 cell merges per shard, HBM-resident input.
 
-Keys are hash-sharded over the N GPUs (weak scaling: 16M keys per GPU).  At
-N = 1 a step is ONE engine call (jy_pncount_converge_block) over the 64
-columns.  At N > 1 the peer batches are ROUTED (north_star): rank
-r ingests the 64/N peer columns c with c % N == r, each covering the keys of
-every owner (grouped by owner, as a peer running the same sharding flushes
-them), and route.CounterRouter moves them to their owners with equal-split
-RCCL all-to-alls over xGMI, one column per rank at a time, double-buffered so
-chunk c+1 is in flight while the owners merge chunk c.  `value` counts the
-cells merged on all ranks per wall second including the exchange; the
-roofline line prices the merge kernel alone.
+Keys are hash-sharded over the N GPUs (weak scaling: 16M keys per GPU).  A
+step is ONE engine call per shard (jy_pncount_converge_block) over the 64
+peer columns of that shard's keys: peers that run the same key sharding
+flush shard by shard, so each shard's part of a peer batch arrives at its
+owner and no collective sits on the data path (`value`, `roofline`).
+
+At N > 1 the line also carries `routed`: the same converge with the peer
+batches arriving MIXED (north_star) -- rank r ingests the 64/N
+peer columns c with c % N == r for the keys of every owner and
+route.CounterRouter moves each owner's part to it with equal-split RCCL
+all-to-alls over xGMI, double-buffered so chunk c+1 is in flight while the
+owners merge chunk c.  (N - 1)/N of every batch then crosses xGMI, as many
+bytes as the merge reads from HBM, so that step is bound by the links; it
+reports its exchange GB/s against the links it uses.
 
 Inputs: seeded splitmix64 streams generated in HBM (jylis_amd/synth.py); the
 state starts from a synthetic full state and `--batches` distinct delta
@@ -207,7 +211,6 @@ def main():
     from jylis_amd import synth as S
     from jylis_amd._lib import PNCOUNT
     from jylis_amd.engine import Engine
-    from jylis_amd.route import CounterRouter, DistFabric, LocalFabric
     K, R = args.keys, args.replicas
     assert R % world == 0, "the replica columns are split evenly over the ranks"
     Cn = R // world  # peer columns ingested per rank
@@ -235,26 +238,38 @@ def main():
     S.counter_rows_torch(tmp, seed_me)
     eng.pncount_converge_block(cols, 0, tmp[0], tmp[1])
     del tmp
-    # the delta chain this rank ingests: [sign][c][owner][K] per batch
     nb = max(1, args.batches)
-    ingests = [torch.empty((2, Cn, world, K), dtype=torch.int64, device=dev) for _ in range(nb)]
-    for d in range(world):
-        seed_d = _owner_seed(seed, d)
-        for c in range(Cn):
-            g = peer[rank][c]
-            prev = torch.empty((2, 1, K), dtype=torch.int64, device=dev)
-            S.counter_rows_torch(prev, seed_d, col_offset=g, col_total=R)
-            for j in range(nb):
-                cur = torch.empty_like(prev)
-                S.counter_rows_torch(cur, seed_d, rnd=j, prev=prev, col_offset=g, col_total=R)
-                ingests[j][:, c, d].copy_(cur[:, 0])
-                prev = cur
+
+    def chain_into(seed_d, g, outs):
+        """column g of owner d's delta chain: outs[j][sign][K] <- round j"""
+        prev = torch.empty((2, 1, K), dtype=torch.int64, device=dev)
+        S.counter_rows_torch(prev, seed_d, col_offset=g, col_total=R)
+        for j, o in enumerate(outs):
+            cur = torch.empty_like(prev)
+            S.counter_rows_torch(cur, seed_d, rnd=j, prev=prev, col_offset=g, col_total=R)
+            o.copy_(cur[:, 0])
+            prev = cur
+
+    # sharded ingest: every peer batch of this rank's keys, [sign][R][K] per
+    # round -- peers that run the same key sharding flush shard by shard, so
+    # each shard's part of a peer batch arrives at its owner
+    shard = [torch.empty((2, R, K), dtype=torch.int64, device=dev) for _ in range(nb)]
+    for g in range(R):
+        chain_into(seed_me, g, [shard[j][:, g] for j in range(nb)])
+    all_cols = np.arange(R, dtype=np.uint16)
+    # routed ingest (N > 1): rank r holds the Cn peer columns c % N == r for
+    # the keys of EVERY owner, [sign][c][owner][K] per round, and routes them
+    nbr = min(nb, 2)
+    routed = []
+    if world > 1:
+        routed = [torch.empty((2, Cn, world, K), dtype=torch.int64, device=dev) for _ in range(nbr)]
+        for d in range(world):
+            for c in range(Cn):
+                chain_into(_owner_seed(seed, d), peer[rank][c], [routed[j][:, c, d] for j in range(nbr)])
     torch.cuda.synchronize(dev)
-    fabric = DistFabric(dist, cpu_group=cpu_group) if world > 1 else LocalFabric(1)
-    router = CounterRouter([eng], fabric, PNCOUNT)
 
     def step(i):
-        router.step([ingests[i % nb]], peer)
+        eng.pncount_converge_block(all_cols, 0, shard[i % nb][0], shard[i % nb][1])
 
     changed = None
     for i in range(args.warmup):
@@ -280,31 +295,37 @@ def main():
     eng.timing(False)
     merge_ms_per_step = float(np.sum(calls)) / args.steps
 
-    # correctness spot-check on sampled cells of this shard: state == max(initial, applied batches)
-    applied = sorted({(args.warmup + i) % nb for i in range(args.steps)} | {i % nb for i in range(args.warmup)})
+    # correctness spot-check on sampled cells of this shard: state == max(initial, applied rounds)
     rng = np.random.default_rng(rank)
     s0 = int(rng.integers(0, K - 64))
     cells = (np.arange(2)[:, None, None] * R * K + np.arange(R)[None, :, None] * K
              + (s0 + np.arange(64))[None, None, :]).astype(np.uint64)
-    exp = S.counter_state_np(K, R, 2, seed_me, cells=cells)
-    chain = exp.copy()
-    best = exp.copy()
-    for j in range(nb):
-        chain = S.counter_delta_np(chain, j, seed_me, cells=cells)
-        if j in applied:
-            best = np.maximum(best, chain)
-    got = eng.counter_export(PNCOUNT, R, s0, 64)
-    ok = bool((got == best).all())
-    sums = eng.pncount_get(np.arange(s0, s0 + 64, dtype=np.uint32))
-    exp_sum = (best[0].sum(axis=0, dtype=np.uint64) - best[1].sum(axis=0, dtype=np.uint64)).view(np.int64)
-    ok = ok and bool((sums == exp_sum).all())
+
+    def verify(applied):
+        exp = S.counter_state_np(K, R, 2, seed_me, cells=cells)
+        chain, best = exp.copy(), exp.copy()
+        for j in range(max(applied) + 1):
+            chain = S.counter_delta_np(chain, j, seed_me, cells=cells)
+            if j in applied:
+                best = np.maximum(best, chain)
+        ok = bool((eng.counter_export(PNCOUNT, R, s0, 64) == best).all())
+        sums = eng.pncount_get(np.arange(s0, s0 + 64, dtype=np.uint32))
+        exp_sum = (best[0].sum(axis=0, dtype=np.uint64) - best[1].sum(axis=0, dtype=np.uint64)).view(np.int64)
+        ok = ok and bool((sums == exp_sum).all())
+        if dist:
+            t = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ok = float(t[0]) == 0.0
+        return ok
+
+    applied = {i % nb for i in range(args.warmup + args.steps)}
+    ok = verify(applied)
 
     t_max = elapsed
     if dist:
-        tt = torch.tensor([elapsed, 0.0 if ok else 1.0, merge_ms_per_step], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed, merge_ms_per_step], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_max, bad, merge_ms_per_step = float(tt[0]), float(tt[1]), float(tt[2])
-        ok = bad == 0.0
+        t_max, merge_ms_per_step = float(tt[0]), float(tt[1])
     cells_per_step = 2 * R * K
     value = world * cells_per_step * args.steps / t_max
     avg_kern_s = merge_ms_per_step / 1e3
@@ -326,43 +347,107 @@ def main():
         cpu = cpu_baseline(args, seed)
         cpu_par = cpu_baseline_parallel(args, seed) if args.cpu_threads > 1 else None
 
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "merges/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": t_max / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (seeded splitmix64 in HBM; SURVEY.md 8d config 2)",
+        "config": {"workload": f"PNCOUNT converge: {K // (1 << 20)}M keys x {R} replicas x {{P,N}} per GPU shard, "
+                               f"one full delta batch ({R} peer batches) per step, each shard's part of every peer "
+                               f"batch converged on its owner",
+                   "keys_per_gpu": K, "replicas": R, "signs": 2, "cells_per_step_per_gpu": cells_per_step,
+                   "parallelism": f"key-sharded x{world}", "distinct_batches": nb},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "k_block_max<true>", "kernel_ms_avg": avg_kern_s * 1e3,
+                     "merge_launches_per_step": len(calls) // max(args.steps, 1),
+                     "bytes_per_cell": BYTES_PER_CELL},
+        "cpu_baseline": cpu,
+        "cpu_baseline_parallel": cpu_par,
+        "first_cycle_changes": {"cells_changed": changed, "cells_sampled": 2 * R * min(K, 1 << 16)},
+        "verified": ok,
+    }
+    if world > 1:
+        line["routed"] = routed_phase(args, eng, dev, dist, rank, world, routed, peer, fabric_of(dist, cpu_group),
+                                      cells_per_step, line, verify, applied)
     if rank == 0:
-        xbytes = 2 * Cn * (world - 1) * K * 8  # sent (= received) per rank per step
-        line = {
-            "metric": METRIC,
-            "value": value,
-            "unit": "merges/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": t_max / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u64",
-            "data": "synthetic (seeded splitmix64 in HBM; SURVEY.md 8d config 2)",
-            "config": {"workload": f"PNCOUNT converge: {K // (1 << 20)}M keys x {R} replicas x {{P,N}} per GPU shard, "
-                                   f"one full delta batch ({R} peer batches) per step"
-                                   + (", peer batches routed to owners (RCCL all-to-all)" if world > 1 else ""),
-                       "keys_per_gpu": K, "replicas": R, "signs": 2, "cells_per_step_per_gpu": cells_per_step,
-                       "parallelism": f"key-sharded x{world}", "distinct_batches": nb,
-                       "routed": world > 1, "exchange_bytes_per_gpu_per_step": xbytes},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_block_max<true>", "kernel_ms_avg": avg_kern_s * 1e3,
-                         "merge_launches_per_step": len(calls) // max(args.steps, 1),
-                         "bytes_per_cell": BYTES_PER_CELL},
-            "cpu_baseline": cpu,
-            "cpu_baseline_parallel": cpu_par,
-            "first_cycle_changes": {"cells_changed": changed, "cells_sampled": 2 * R * min(K, 1 << 16)},
-            "verified": ok,
-        }
-        if world > 1:
-            line["exchange_GBps_per_gpu"] = xbytes / (t_max / args.steps) / 1e9
         print(json.dumps(line), flush=True)
     eng.close()
     if dist:
         dist.destroy_process_group()
+
+
+XGMI_LINK_GBPS = 153.0  # per xGMI link and direction, nominal (MI355X: 7 links per GPU)
+
+
+def fabric_of(dist, cpu_group):
+    from jylis_amd.route import DistFabric
+    return DistFabric(dist, cpu_group=cpu_group)
+
+
+def routed_phase(args, eng, dev, dist, rank, world, routed, peer, fabric, cells_per_step, line, verify, applied):
+    """The same converge with the peer batches arriving MIXED: rank r holds
+    whole peer columns (the keys of every owner) and route.CounterRouter moves
+    each owner's part to it with equal-split RCCL all-to-alls over xGMI,
+    double-buffered against the owner's merge.  Every cell a
+    shard merges then crosses xGMI once unless the ingesting rank owns it:
+    (N - 1) / N of the batch, as many bytes as the merge reads, so the step
+    is bound by the links, not by HBM.  Timed apart from `value` with its own
+    few steps; a watchdog prints the line without it if a collective hangs."""
+    import threading
+
+    import torch
+    from jylis_amd._lib import PNCOUNT
+    from jylis_amd.route import CounterRouter
+    limit = float(os.environ.get("JY_ROUTED_LIMIT_S", "240"))
+
+    def fire():
+        if rank == 0:
+            line["routed"] = {"error": f"routed phase did not finish within {limit:.0f} s"}
+            print(json.dumps(line), flush=True)
+        os._exit(0)
+
+    dog = threading.Timer(limit, fire)
+    dog.daemon = True
+    dog.start()
+    router = CounterRouter([eng], fabric, PNCOUNT)
+    nbr = len(routed)
+    warm, steps = 1, max(1, min(args.steps, 4))
+    for i in range(warm):
+        router.step([routed[i % nbr]], peer)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        router.step([routed[(warm + i) % nbr]], peer)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    tt = torch.tensor([el], dtype=torch.float64, device=dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    t = float(tt[0])
+    ok = verify(applied | {i % nbr for i in range(warm + steps)})
+    dog.cancel()
+    _, Cn, _, K = routed[0].shape
+    xbytes = 2 * Cn * (world - 1) * K * 8  # sent (= received) per rank per step
+    ms = t / steps * 1e3
+    return {"value": world * cells_per_step * steps / t, "unit": "merges/s", "steps": steps, "warmup": warm,
+            "ms_per_step": ms, "verified": ok,
+            "exchange_bytes_per_gpu_per_step": xbytes, "exchange_GBps_per_gpu": xbytes / (ms / 1e3) / 1e9,
+            "xgmi_links_used": world - 1, "xgmi_link_GBps_nominal": XGMI_LINK_GBPS,
+            "exchange_frac_of_links": xbytes / (ms / 1e3) / 1e9 / ((world - 1) * XGMI_LINK_GBPS),
+            "note": "peer batches ingested mixed: rank r holds peer columns c % N == r for every owner and routes "
+                    "them (route.CounterRouter, RCCL all-to-all, double-buffered against the merge)"}
 
 
 if __name__ == "__main__":
