@@ -139,6 +139,21 @@ int32_t jy_gcount_converge_block(jy_engine* eng, uint32_t ncols, const uint16_t*
                                  uint32_t slot0, uint32_t nslots, const uint64_t* vals, int32_t mem);
 int32_t jy_gcount_get(jy_engine* eng, uint64_t n, const uint32_t* slots, uint64_t* out, int32_t mem);
 
+/* ---- GCOUNT / PNCOUNT: one decoded peer batch WITH its key strings ----
+ * RepoManagerCore.converge_deltas (repo_manager.pony:92-93) of a counter
+ * batch including each key's _data_for (repo_gcount.pony:36-41,
+ * repo_pncount.pony:38-43: create on miss) in ONE call: the nkeys key strings
+ * (key_bytes / key_offs, as jy_keys_intern) are interned on the device and
+ * the ncells cells merged with their device slots -- no slot crosses to the
+ * host (jy_keys_intern + jy_gcount_converge move every slot down and up).
+ * Cell i belongs to key cell_key[i] (NULL: cell i is key i, ncells == nkeys)
+ * and, for PNCOUNT, to sign[i] (0 = P, 1 = N; NULL: all P); GCOUNT takes
+ * sign NULL.  s[slot][col] = max(s, val).  mem applies to every array (with
+ * JY_DEVICE the key bytes / offsets are in HBM too). */
+int32_t jy_counter_converge_keys(jy_engine* eng, int32_t type, uint64_t nkeys, const uint8_t* key_bytes,
+                                 const uint64_t* key_offs, uint64_t ncells, const uint32_t* cell_key,
+                                 const uint8_t* sign, const uint16_t* col, const uint64_t* val, int32_t mem);
+
 /* ---- PNCOUNT: two GCounters (repo_pncount.pony:52-57); GET = (sum P - sum N) as i64 ---- */
 int32_t jy_pncount_converge(jy_engine* eng, uint64_t np, const uint32_t* pslot, const uint16_t* pcol,
                             const uint64_t* pval, uint64_t nn, const uint32_t* nslot,

@@ -67,6 +67,7 @@ SIGNATURES = {
     "jy_pncount_converge": (I32, [P, U64, P, P, P, U64, P, P, P, I32]),
     "jy_pncount_converge_block": (I32, [P, U32, P, U32, U32, P, P, I32]),
     "jy_pncount_get": (I32, [P, U64, P, P, I32]),
+    "jy_counter_converge_keys": (I32, [P, I32, U64, P, P, U64, P, P, P, P, I32]),
     "jy_counter_export": (I32, [P, I32, U32, U32, U32, P]),
     "jy_counter_write": (I32, [P, I32, I32, U32, U64, P, P, I32]),
     "jy_counter_deltas_size": (I32, [P, I32, P]),
@@ -142,7 +143,11 @@ def load(path=LIB_PATH):
         pass
     lib = C.CDLL(path)
     for name, (res, args) in list(SIGNATURES.items()) + list(HOST_SIGNATURES.items()):
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if path == os.path.join(_HERE, "libjylis_gpu.so"):
+                raise RuntimeError(f"{path} does not export {name}: rebuild it (make -C jylis_amd)")
+            continue  # an older A/B build (JY_LIB) without a newer entry point
         fn.restype = res
         fn.argtypes = args
     _lib = lib

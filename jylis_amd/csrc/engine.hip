@@ -143,10 +143,31 @@ int32_t jy_stage(jy_engine* eng, int idx, const void* src, u64 bytes, int32_t me
     ps.bytes = nb;
   }
   u64 at = round_up(eng->pin_cursor, 256);
-  std::memcpy(static_cast<uint8_t*>(ps.p) + at, src, bytes);
-  JY_HIP(eng, hipMemcpyAsync(d, static_cast<uint8_t*>(ps.p) + at, bytes, hipMemcpyHostToDevice, eng->stream));
+  // chunked: large copies run on the copy pool, each chunk's DMA issued as it lands
+  JY_TRY(jy_copy_h2d_staged(eng, d, static_cast<uint8_t*>(ps.p) + at, src, bytes));
   eng->pin_cursor = at + bytes;
   *dev_out = d;
+  return JY_OK;
+}
+
+int32_t jy_readback(jy_engine* eng, void* dst, const void* dev, u64 bytes) {
+  if (bytes < (1ull << 20)) {
+    JY_HIP(eng, hipMemcpyAsync(dst, dev, bytes, hipMemcpyDeviceToHost, eng->stream));
+    JY_HIP(eng, hipStreamSynchronize(eng->stream));
+    return JY_OK;
+  }
+  if (eng->pin_rb_bytes < bytes) {
+    JY_HIP(eng, hipStreamSynchronize(eng->stream));
+    if (eng->pin_rb) JY_HIP(eng, hipHostFree(eng->pin_rb));
+    eng->pin_rb = nullptr;
+    eng->pin_rb_bytes = 0;
+    const u64 nb = std::max<u64>(bytes + bytes / 2, 4ull << 20);
+    JY_HIP(eng, hipHostMalloc(&eng->pin_rb, nb, hipHostMallocDefault));
+    eng->pin_rb_bytes = nb;
+  }
+  JY_HIP(eng, hipMemcpyAsync(eng->pin_rb, dev, bytes, hipMemcpyDeviceToHost, eng->stream));
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  jy_copy_host(dst, eng->pin_rb, bytes);
   return JY_OK;
 }
 
@@ -329,6 +350,7 @@ void jy_engine_destroy(jy_engine* eng) {
     if (ps.ready) hipEventDestroy(ps.ready);
   }
   if (eng->pin_total) hipHostFree(eng->pin_total);
+  if (eng->pin_rb) hipHostFree(eng->pin_rb);
   for (auto& ev : eng->tm_ev) {
     hipEventDestroy(ev.first);
     hipEventDestroy(ev.second);
@@ -447,8 +469,7 @@ static int32_t keys_host(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb,
     u64 created = 0;
     JY_TRY(jy_keydir_run(eng, type, n, static_cast<const uint8_t*>(db), static_cast<const u64*>(dofs),
                          static_cast<u32*>(ds), create, &created));
-    JY_HIP(eng, hipMemcpyAsync(slots, ds, n * 4, hipMemcpyDeviceToHost, eng->stream));
-    JY_HIP(eng, hipStreamSynchronize(eng->stream));
+    JY_TRY(jy_readback(eng, slots, ds, n * 4));
     return keys_created(eng, type, created);
   }
   std::vector<u64> miss;
@@ -643,6 +664,52 @@ int32_t jy_gcount_converge(jy_engine* eng, uint64_t n, const uint32_t* slot, con
   return jy_counter_coo(eng, 0, 0, n, (const u32*)ds, (const u16*)dc, (const u64*)dv);
 }
 
+// one decoded peer batch with its key strings: device interning (_data_for,
+// create on miss) feeding the COO merge directly -- the slots never cross to
+// the host.  Everything is staged in one pinned region first (one run of
+// DMAs), then the directory runs, then the cells merge.
+int32_t jy_counter_converge_keys(jy_engine* eng, int32_t type, uint64_t nkeys, const uint8_t* kb, const uint64_t* ko,
+                                 uint64_t ncells, const uint32_t* cell_key, const uint8_t* sign, const uint16_t* col,
+                                 const uint64_t* val, int32_t mem) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (type != JY_GCOUNT && type != JY_PNCOUNT) return eng->fail(JY_EINVAL, "type must be JY_GCOUNT or JY_PNCOUNT");
+  if (mem != JY_HOST && mem != JY_DEVICE) return eng->fail(JY_EINVAL, "mem must be JY_HOST or JY_DEVICE");
+  if (!cell_key && ncells != nkeys) return eng->fail(JY_EINVAL, "without cell_key, cell i is key i: ncells == nkeys");
+  if (type == JY_GCOUNT && sign) return eng->fail(JY_EINVAL, "GCOUNT cells have no sign");
+  if (nkeys == 0 || ncells == 0) return JY_OK;
+  const int which = type == JY_GCOUNT ? 0 : 1;
+  if (mem == JY_HOST) {
+    if (cell_key)
+      for (u64 i = 0; i < ncells; i++)
+        if (cell_key[i] >= nkeys) return eng->fail(JY_ERANGE, "cell_key names no key of the batch");
+    if (sign)
+      for (u64 i = 0; i < ncells; i++)
+        if (sign[i] > 1) return eng->fail(JY_ERANGE, "sign must be 0 (P) or 1 (N)");
+  }
+  JY_TRY(counter_cols_check(eng, which, ncells, col, mem));
+  const double t0 = jy_tracing() ? jy_now_us() : 0;
+  const void *db, *dofs, *dk = nullptr, *dsg = nullptr, *dc, *dv;
+  JY_TRY(stage_begin(eng));
+  JY_TRY(jy_stage(eng, 0, kb, mem == JY_HOST ? ko[nkeys] : 0, mem, &db));  // device: used in place
+  JY_TRY(jy_stage(eng, 1, ko, (nkeys + 1) * 8, mem, &dofs));
+  if (cell_key) JY_TRY(jy_stage(eng, 3, cell_key, ncells * 4, mem, &dk));
+  if (sign) JY_TRY(jy_stage(eng, 4, sign, ncells, mem, &dsg));
+  JY_TRY(jy_stage(eng, 5, col, ncells * 2, mem, &dc));
+  JY_TRY(jy_stage(eng, 6, val, ncells * 8, mem, &dv));
+  JY_TRY(stage_end(eng));
+  void* ds;
+  JY_TRY(jy_scratch(eng, 2, nkeys * 4, &ds));
+  u64 created = 0;
+  JY_TRY(jy_keydir_run(eng, type, nkeys, static_cast<const uint8_t*>(db), static_cast<const u64*>(dofs),
+                       static_cast<u32*>(ds), true, &created));
+  JY_TRY(keys_created(eng, type, created));  // grows the slabs before the merge is enqueued
+  JY_TRACE("converge_keys: %llu keys, %llu cells: %.1f us after the host checks", (unsigned long long)nkeys,
+           (unsigned long long)ncells, jy_now_us() - t0);
+  return jy_counter_coo_keyed(eng, which, ncells, static_cast<const u32*>(ds), static_cast<const u32*>(dk),
+                              static_cast<const uint8_t*>(dsg), static_cast<const u16*>(dc),
+                              static_cast<const u64*>(dv));
+}
+
 int32_t jy_gcount_converge_block(jy_engine* eng, uint32_t ncols, const uint16_t* cols, uint32_t slot0,
                                  uint32_t nslots, const uint64_t* vals, int32_t mem) {
   JY_HIP(eng, hipSetDevice(eng->device));
@@ -674,8 +741,7 @@ static int32_t counter_get(jy_engine* eng, int which, int32_t type, uint64_t n, 
   }
   JY_TRY(jy_counter_sum(eng, which, n, (const u32*)ds, dout));
   if (mem == JY_HOST) {
-    JY_HIP(eng, hipMemcpyAsync(out, dout, n * 8, hipMemcpyDeviceToHost, eng->stream));
-    JY_HIP(eng, hipStreamSynchronize(eng->stream));
+    JY_TRY(jy_readback(eng, out, dout, n * 8));
   }
   (void)type;
   return JY_OK;

@@ -412,6 +412,10 @@ struct jy_engine {
   u64 pin_cursor = 0;
   bool pin_used = false;
   u64* pin_total = nullptr;        // pinned u64[4] for async totals
+  // pinned landing area of large device -> host results (slots of a host key
+  // batch): DMA here, then a parallel host copy out (host_copy.hip)
+  void* pin_rb = nullptr;
+  u64 pin_rb_bytes = 0;
   hipEvent_t total_ready = nullptr;
 
   // jy_timing_enable: event pairs around the device work of merge calls
@@ -501,6 +505,8 @@ int32_t jy_realloc(jy_engine* eng, void** p, u64 old_bytes, u64 new_bytes, bool 
 // kernel-side entry points (k_*.hip)
 int32_t jy_counter_grow(jy_engine* eng, int which, u32 need_cols, u64 need_slots);
 int32_t jy_counter_coo(jy_engine* eng, int which, int sign, u64 n, const u32* slot, const u16* col, const u64* val);
+int32_t jy_counter_coo_keyed(jy_engine* eng, int which, u64 n, const u32* kslot, const u32* cell_key,
+                             const uint8_t* sign, const u16* col, const u64* val);
 int32_t jy_counter_block(jy_engine* eng, int which, u32 ncols, const u16* cols_dev, u32 slot0, u32 nslots,
                          const u64* vals_p, const u64* vals_n);
 int32_t jy_counter_sum(jy_engine* eng, int which, u64 n, const u32* slots_dev, u64* out_dev);
@@ -576,3 +582,9 @@ int32_t jy_ujson_flush_dev(jy_engine* eng, u64 cap_docs, u64 cap_el, u64 cap_cl,
 int32_t jy_scan_u64(jy_engine* eng, const u64* in, u64* out, u64 n);
 // segment id (u32) of each of the n items of a CSR offs[0..nseg]
 int32_t jy_seg_ids(jy_engine* eng, const u64* offs, u64 nseg, u64 n, u32* out);
+
+// host_copy.hip: chunked parallel host copies of the staging paths
+int32_t jy_copy_h2d_staged(jy_engine* eng, void* dev, uint8_t* pinned, const void* src, u64 bytes);
+void jy_copy_host(void* dst, const void* src, u64 bytes);
+// device -> pageable host through the pinned landing area (synchronises the stream)
+int32_t jy_readback(jy_engine* eng, void* dst, const void* dev, u64 bytes);

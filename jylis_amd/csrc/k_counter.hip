@@ -92,6 +92,23 @@ __global__ __launch_bounds__(kThreads) void k_coo_max(u64* __restrict__ slab, u6
   if (v > *p) __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// COO cells whose slots come from a device key interning of the same call
+// (jy_counter_converge_keys): cell i belongs to key cell_key[i] (identity
+// when null) and to slab `sign[i]` (P when null)
+__global__ __launch_bounds__(kThreads) void k_coo_max_keyed(u64* __restrict__ slab, u64 row_pitch, u64 sign_pitch,
+                                                            const u32* __restrict__ kslot,
+                                                            const u32* __restrict__ cell_key,
+                                                            const uint8_t* __restrict__ sign,
+                                                            const u16* __restrict__ col,
+                                                            const u64* __restrict__ val, u64 n) {
+  const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const u32 s = kslot[cell_key ? cell_key[i] : i];
+  u64* p = slab + (sign && sign[i] ? sign_pitch : 0) + (u64)col[i] * row_pitch + s;
+  const u64 v = val[i];
+  if (v > *p) __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // value(): wrapping sum over the used replica columns; PNCOUNT subtracts N.
 __global__ __launch_bounds__(kThreads) void k_sum(const u64* __restrict__ slab, u64 row_pitch, u64 sign_pitch,
                                                   u32 ncols, u32 nsigns, const u32* __restrict__ slots, u64 n,
@@ -194,6 +211,18 @@ int32_t jy_counter_coo(jy_engine* eng, int which, int sign, u64 n, const u32* sl
   u64* base = c.slab + (u64)sign * c.ccap * c.kcap;
   const u64 blocks = (n + kThreads - 1) / kThreads;
   hipLaunchKernelGGL(k_coo_max, dim3((u32)blocks), dim3(kThreads), 0, eng->stream, base, c.kcap, slot, col, val, n);
+  JY_HIP(eng, hipGetLastError());
+  return JY_OK;
+}
+
+int32_t jy_counter_coo_keyed(jy_engine* eng, int which, u64 n, const u32* kslot, const u32* cell_key,
+                             const uint8_t* sign, const u16* col, const u64* val) {
+  if (n == 0) return JY_OK;
+  JyTimed tm(eng);
+  CounterState& c = eng->cnt[which];
+  const u64 blocks = (n + kThreads - 1) / kThreads;
+  hipLaunchKernelGGL(k_coo_max_keyed, dim3((u32)blocks), dim3(kThreads), 0, eng->stream, c.slab, c.kcap,
+                     c.ccap * c.kcap, kslot, cell_key, sign, col, val, n);
   JY_HIP(eng, hipGetLastError());
   return JY_OK;
 }

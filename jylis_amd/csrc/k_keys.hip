@@ -364,8 +364,10 @@ int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, co
   hipLaunchKernelGGL(k_key_sum, dim3(1), dim3(kThreads), 0, eng->stream, parts, nb, counts);
   JY_HIP(eng, hipGetLastError());
   u64 hc[3];
+  const double t0 = jy_tracing() ? jy_now_us() : 0;
   JY_HIP(eng, hipMemcpyAsync(hc, counts, 24, hipMemcpyDeviceToHost, eng->stream));
   JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  JY_TRACE("keydir %llu keys: probe counts after %.1f us of waiting", (unsigned long long)n, jy_now_us() - t0);
   const u64 m = hc[0], mbytes = hc[1];
   if (!create || m == 0) {
     LAUNCH(k_key_copy_res, n, n, res, slots);

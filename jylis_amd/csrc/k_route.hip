@@ -35,53 +35,73 @@ __device__ __forceinline__ u64 round_up8(u64 x) { return (x + kArenaAlign - 1) &
 //   scan        every (owner, quantity) column of tile counts in one
 //               device-wide scan taken column after column (jy_dscan.hpp);
 //               k_rt_hdr takes the grand totals to the header
-//   k_rt_place  per entry: its place in its owner's run = tile base + the
-//               waves before it + its rank among its wave's entries for the
-//               same owner (one ballot per distinct owner, masked scans);
-//               an entry that fits is written, else listed in ovf -- and the
-//               first entry of an owner that does not fit writes the header
-//               (the placed entries are the prefix before it: the ends grow
-//               along an owner's sequence)
-constexpr int kT = 256;  // entries per tile, one per thread
+//   k_rt_place  per entry: its place in its owner's run = tile base + its
+//               rank among the tile's earlier entries for the same owner
+//               (one ballot per distinct owner and 64-entry slice); an entry
+//               that fits is written, else listed in ovf -- and the first
+//               entry of an owner that does not fit writes the header (the
+//               placed entries are the prefix before it: the ends grow along
+//               an owner's sequence)
+// A tile is ONE WAVE (4 entries per lane, slice u = entries u*64 + lane, so
+// the slices run in input order).  Owner d's running counts live in lane d's
+// registers (S <= 64): no LDS, no barrier, and the tile's bases are loaded
+// together with the entries, so placing an entry needs one round trip.
+// (Round 2's form, a 256-thread workgroup per tile with LDS counts per wave,
+// took 45 us (count) + 134 us (place) at 8M entries.)
+#ifndef JY_RT_PLACE_WG
+#define JY_RT_PLACE_WG 0
+#endif
+#ifndef JY_RT_SLICES
+#define JY_RT_SLICES 4
+#endif
+constexpr int kSlices = JY_RT_SLICES;  // 64-entry slices per tile (one wave)
+constexpr int kT = 64 * kSlices;       // entries per tile
+constexpr int kWG = 256;      // threads per workgroup = 4 tiles
 
-// lanes with the same owner add their quantities with one LDS atomic per
-// owner and quantity (per-lane atomics serialise on one word when a wave's
-// entries share an owner: every lane at S = 1)
-template <int kQ>
-__device__ __forceinline__ void wave_add_by_owner(u32 o, bool valid, const u64 (&v)[kQ],
-                                                  unsigned long long* __restrict__ lc) {
-  u64 pending = __ballot(valid);
-  while (pending) {
-    const int leader = __ffsll((unsigned long long)pending) - 1;
-    const u32 lo = __shfl(o, leader);
-    const bool mine = valid && o == lo;
-    pending &= ~__ballot(mine);
-#pragma unroll
-    for (int q = 0; q < kQ; q++) {
-      const u64 sum = jyscan::wave_sum<u64>(mine ? v[q] : 0ull);
-      if (__lane_id() == (u32)leader && sum) atomicAdd(&lc[lo * kQ + q], (unsigned long long)sum);
-    }
-  }
+__device__ __forceinline__ u64 readlane64(u64 x, u32 lane) {
+  const u32 lo = __builtin_amdgcn_readlane((u32)x, lane), hi = __builtin_amdgcn_readlane((u32)(x >> 32), lane);
+  return ((u64)hi << 32) | lo;
 }
 
-__global__ __launch_bounds__(kT) void k_rt_count(const u32* __restrict__ owner, const u64* __restrict__ lr, u64 n,
-                                                 u32 S, u64* __restrict__ tcnt) {
-  __shared__ unsigned long long lc[kMaxShards * 2];
-  for (u32 j = threadIdx.x; j < S * 2; j += kT) lc[j] = 0;
-  __syncthreads();
-  const u64 i = (u64)blockIdx.x * kT + threadIdx.x;
-  u32 o = S;
-  u64 v[2] = {0, 0};
-  if (i < n) {
-    o = owner[i];
-    const u64 len = lr[i] & JY_LR_LEN_MASK;
-    v[0] = 1;
-    v[1] = len > 8 ? round_up8(len) : 0;
+__global__ __launch_bounds__(kWG) void k_rt_count(const u32* __restrict__ owner, const u64* __restrict__ lr, u64 n,
+                                                  u32 S, u64* __restrict__ tcnt) {
+  const u64 tile = (u64)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6);
+  if (tile * kT >= n) return;  // a whole wave
+  const u32 lane = __lane_id();
+  u32 o[kSlices];
+  u64 b[kSlices];
+#pragma unroll
+  for (int u = 0; u < kSlices; u++) {
+    const u64 i = tile * kT + (u64)u * 64 + lane;
+    o[u] = S;
+    b[u] = 0;
+    if (i < n) {
+      o[u] = owner[i];
+      const u64 len = __builtin_nontemporal_load(lr + i) & JY_LR_LEN_MASK;
+      b[u] = len > 8 ? round_up8(len) : 0;
+    }
   }
-  wave_add_by_owner<2>(o, o < S, v, lc);  // one LDS atomic per (wave, owner, quantity)
-  __syncthreads();
-  u64* row = tcnt + (u64)blockIdx.x * S * 2;
-  for (u32 j = threadIdx.x; j < S * 2; j += kT) row[j] = lc[j];
+  u64 c = 0, cb = 0;  // lane d: owner d's records and bytes in this tile
+#pragma unroll
+  for (int u = 0; u < kSlices; u++) {
+    const bool anyb = __ballot(b[u] != 0) != 0;
+    u64 pending = __ballot(o[u] < S);
+    while (pending) {
+      const u32 d = __builtin_amdgcn_readlane(o[u], __ffsll((unsigned long long)pending) - 1);
+      const u64 m = __ballot(o[u] == d);
+      pending &= ~m;
+      const u64 bs = anyb ? jyscan::wave_sum<u64>(o[u] == d ? b[u] : 0ull) : 0ull;
+      if (lane == d) {
+        c += __popcll(m);
+        cb += bs;
+      }
+    }
+  }
+  if (lane < S) {
+    u64* row = tcnt + tile * S * 2;
+    row[lane * 2] = c;
+    row[lane * 2 + 1] = cb;
+  }
 }
 
 
@@ -94,21 +114,129 @@ __global__ void k_rt_hdr(const u64* __restrict__ tcnt, u64 ntiles, u32 W, unsign
   hdr[c] = hi - tcnt[c];
 }
 
-__global__ __launch_bounds__(kT) void k_rt_place(const u32* __restrict__ owner, const u32* __restrict__ slot,
+__global__ __launch_bounds__(kWG) void k_rt_place(const u32* __restrict__ owner, const u32* __restrict__ slot,
+                                                  const u64* __restrict__ ts, const u64* __restrict__ pre,
+                                                  const u64* __restrict__ lr, const uint8_t* __restrict__ arena, u64 n,
+                                                  u32 S, u64 cap, u64 cap_byte, const u64* __restrict__ tcnt,
+                                                  unsigned long long* __restrict__ hdr, u64* __restrict__ recs,
+                                                  uint8_t* __restrict__ bytes, u32* __restrict__ ovf,
+                                                  unsigned long long* __restrict__ skipped) {
+  const u64 tile = (u64)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6);
+  if (tile * kT >= n) return;  // a whole wave
+  const u32 lane = __lane_id();
+  const u64 lt = (1ull << lane) - 1;
+  // lane d: owner d's next record / byte position in its run (the tile's row
+  // of the scanned counts less the column's base, row 0)
+  u64 rb = 0, rbb = 0;
+  if (lane < S) {
+    const u64* row = tcnt + tile * S * 2;
+    rb = row[lane * 2] - tcnt[lane * 2];
+    rbb = row[lane * 2 + 1] - tcnt[lane * 2 + 1];
+  }
+  u32 o[kSlices], sl[kSlices];
+  u64 t[kSlices], p[kSlices], l[kSlices], b[kSlices];
+#pragma unroll
+  for (int u = 0; u < kSlices; u++) {
+    const u64 i = tile * kT + (u64)u * 64 + lane;
+    o[u] = 0xFFFFFFFFu;
+    sl[u] = 0;
+    t[u] = p[u] = l[u] = b[u] = 0;
+    if (i < n) {
+      o[u] = __builtin_nontemporal_load(owner + i);
+      sl[u] = __builtin_nontemporal_load(slot + i);
+      t[u] = __builtin_nontemporal_load(ts + i);
+      p[u] = __builtin_nontemporal_load(pre + i);
+      l[u] = __builtin_nontemporal_load(lr + i);
+      const u64 len = l[u] & JY_LR_LEN_MASK;
+      b[u] = len > 8 ? round_up8(len) : 0;
+      if (o[u] >= S) atomicAdd(skipped, 1ull);  // an owner outside [0, S): dropped, counted
+    }
+  }
+  // ranks: every slice's places first (ALU and cross-lane only)
+  u64 pos[kSlices], bpos[kSlices];
+#pragma unroll
+  for (int u = 0; u < kSlices; u++) {
+    const bool valid = o[u] < S;
+    const bool anyb = __ballot(b[u] != 0 && valid) != 0;
+    pos[u] = bpos[u] = 0;
+    u64 pending = __ballot(valid);
+    while (pending) {
+      const u32 d = __builtin_amdgcn_readlane(o[u], __ffsll((unsigned long long)pending) - 1);
+      const bool mine = o[u] == d;
+      const u64 m = __ballot(mine);
+      pending &= ~m;
+      const u64 x = mine ? b[u] : 0ull;
+      const u64 inc = anyb ? jyscan::wave_incl<u64>(x) : 0ull;
+      const u64 tot = anyb ? readlane64(inc, 63) : 0ull;
+      if (mine) {
+        pos[u] = readlane64(rb, d) + __popcll(m & lt);
+        bpos[u] = readlane64(rbb, d) + inc - x;
+      }
+      if (lane == d) {
+        rb += __popcll(m);
+        rbb += tot;
+      }
+    }
+  }
+  // the long values' first two granules of every slice, loaded together
+  // (values of <= 16 bytes -- the common long value -- need nothing else)
+  bool fits[kSlices];
+  u64 g0[kSlices], g1[kSlices];
+#pragma unroll
+  for (int u = 0; u < kSlices; u++) {
+    fits[u] = o[u] < S && pos[u] < cap && bpos[u] + b[u] <= cap_byte;
+    g0[u] = g1[u] = 0;
+    if (fits[u] && b[u]) {
+      const u64* src = reinterpret_cast<const u64*>(arena + (l[u] >> JY_LR_LEN_BITS));
+      g0[u] = src[0];
+      g1[u] = src[1];  // b >= 16: a value longer than 8 bytes takes two granules at least
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kSlices; u++) {
+    if (o[u] >= S) continue;
+    if (!fits[u]) {
+      const u64 i = tile * kT + (u64)u * 64 + lane;
+      ovf[1 + atomicAdd(ovf, 1u)] = (u32)i;
+      if (pos[u] == 0 || (pos[u] - 1 < cap && bpos[u] <= cap_byte)) {  // the first of its owner that does not fit
+        hdr[2 * o[u]] = pos[u];
+        hdr[2 * o[u] + 1] = bpos[u];
+      }
+      continue;
+    }
+    u64 out_lr = l[u];
+    if (b[u]) {  // the value's 8-B granules into the run's byte section
+      u64* dst = reinterpret_cast<u64*>(bytes + (u64)o[u] * cap_byte + bpos[u]);
+      dst[0] = g0[u];
+      dst[1] = g1[u];
+      const u64* src = reinterpret_cast<const u64*>(arena + (l[u] >> JY_LR_LEN_BITS));
+      for (u64 w = 2; w < b[u] / 8; w++) dst[w] = src[w];
+      out_lr = (bpos[u] << JY_LR_LEN_BITS) | (l[u] & JY_LR_LEN_MASK);
+    }
+    u64x2* r = reinterpret_cast<u64x2*>(recs + ((u64)o[u] * cap + pos[u]) * 4);  // 32-B records, two 16-B stores
+    r[0] = u64x2{(u64)sl[u], t[u]};
+    r[1] = u64x2{p[u], out_lr};
+  }
+}
+
+#if JY_RT_PLACE_WG
+// A/B: round 2's placement, a 256-thread workgroup per 256-entry tile (one
+// entry per thread, per-wave counts in LDS)
+__global__ __launch_bounds__(256) void k_rt_place_wg(const u32* __restrict__ owner, const u32* __restrict__ slot,
                                                  const u64* __restrict__ ts, const u64* __restrict__ pre,
                                                  const u64* __restrict__ lr, const uint8_t* __restrict__ arena, u64 n,
                                                  u32 S, u64 cap, u64 cap_byte, const u64* __restrict__ tcnt,
                                                  unsigned long long* __restrict__ hdr, u64* __restrict__ recs,
                                                  uint8_t* __restrict__ bytes, u32* __restrict__ ovf,
                                                  unsigned long long* __restrict__ skipped) {
-  constexpr int kW = kT / 64;
+  constexpr int kW = 256 / 64;
   __shared__ u64 wt[kW][kMaxShards * 2];
   for (u32 j = threadIdx.x; j < S * 2; j += kT) {
 #pragma unroll
     for (int w = 0; w < kW; w++) wt[w][j] = 0;
   }
   __syncthreads();
-  const u64 i = (u64)blockIdx.x * kT + threadIdx.x;
+  const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
   const int lane = __lane_id(), wv = threadIdx.x >> 6;
   const u64 lt = (1ull << lane) - 1;
   u32 o = 0xFFFFFFFFu, sl = 0;
@@ -172,6 +300,7 @@ __global__ __launch_bounds__(kT) void k_rt_place(const u32* __restrict__ owner, 
   r[0] = u64x2{(u64)sl, t};
   r[1] = u64x2{p, out_lr};
 }
+#endif
 
 }  // namespace
 
@@ -211,7 +340,8 @@ int32_t jy_treg_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, co
   u64* tcnt = static_cast<u64*>(p);
   const u32* own = static_cast<const u32*>(dow);
   const u64* l = static_cast<const u64*>(dlr);
-  hipLaunchKernelGGL(k_rt_count, dim3((u32)ntiles), dim3(kT), 0, eng->stream, own, l, n, nshards, tcnt);
+  const u32 nwg = (u32)((ntiles + kWG / 64 - 1) / (kWG / 64));
+  hipLaunchKernelGGL(k_rt_count, dim3(nwg), dim3(kWG), 0, eng->stream, own, l, n, nshards, tcnt);
   JY_HIP(eng, hipGetLastError());
   {
     // the tile counts of every (owner, quantity) column in ONE device-wide
@@ -224,10 +354,18 @@ int32_t jy_treg_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, co
                        reinterpret_cast<unsigned long long*>(hdr_dev));
     JY_HIP(eng, hipGetLastError());
   }
-  hipLaunchKernelGGL(k_rt_place, dim3((u32)ntiles), dim3(kT), 0, eng->stream, own, static_cast<const u32*>(dsl),
+#if JY_RT_PLACE_WG
+  static_assert(kT == 256, "the workgroup placement takes 256-entry tiles");
+  hipLaunchKernelGGL(k_rt_place_wg, dim3((u32)ntiles), dim3(256), 0, eng->stream, own, static_cast<const u32*>(dsl),
                      static_cast<const u64*>(dts), static_cast<const u64*>(dpre), l, eng->arena[JY_TREG].p, n, nshards,
                      cap, cap_byte, tcnt, reinterpret_cast<unsigned long long*>(hdr_dev), recs_dev, bytes_dev, ovf_dev,
                      reinterpret_cast<unsigned long long*>(eng->skipped_dev));
+#else
+  hipLaunchKernelGGL(k_rt_place, dim3(nwg), dim3(kWG), 0, eng->stream, own, static_cast<const u32*>(dsl),
+                     static_cast<const u64*>(dts), static_cast<const u64*>(dpre), l, eng->arena[JY_TREG].p, n, nshards,
+                     cap, cap_byte, tcnt, reinterpret_cast<unsigned long long*>(hdr_dev), recs_dev, bytes_dev, ovf_dev,
+                     reinterpret_cast<unsigned long long*>(eng->skipped_dev));
+#endif
   JY_HIP(eng, hipGetLastError());
   return JY_OK;
 }

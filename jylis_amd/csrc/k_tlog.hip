@@ -163,9 +163,13 @@ __global__ __launch_bounds__(kThreads) void k_tlog_prep(TlogArgs A) {
 
 // first position in [lo, hi) of the log at pool[base..] whose timestamp is
 // >= x (the log ascends): 16-ary probes, every probe of a round loaded at
-// once -- one round trip for a log of <= 16 entries, two up to 256
+// once -- one round trip for a log of <= 16 entries, two up to 256.
+// at_ts: the timestamp at the returned position (every position a round
+// narrows to was probed: the last round probes all of [lo, hi), and a
+// narrowed hi is a block end probed >= x), or ~0 when it is hi
 constexpr u32 kProbe = 16;
-__device__ __forceinline__ u32 ts_lower(const TRec* __restrict__ pool, u64 base, u32 lo, u32 hi, u64 x) {
+__device__ __forceinline__ u32 ts_lower(const TRec* __restrict__ pool, u64 base, u32 lo, u32 hi, u64 x, u64& at_ts) {
+  at_ts = ~0ull;
   while (hi > lo) {
     const u32 n = hi - lo;
     const u32 step = (n + kProbe - 1) / kProbe;  // probe i looks at lo + i * step + step - 1
@@ -173,7 +177,11 @@ __device__ __forceinline__ u32 ts_lower(const TRec* __restrict__ pool, u64 base,
 #pragma unroll
     for (u32 i = 0; i < kProbe; i++) {
       const u32 at = lo + i * step + step - 1;
-      if (at < hi) c += pool[base + at].ts < x;
+      if (at < hi) {
+        const u64 v = pool[base + at].ts;
+        c += v < x;
+        if (v >= x && v < at_ts) at_ts = v;  // ascending: the smallest probe >= x is the first one
+      }
     }
     // c whole blocks of `step` lie below x; the answer is inside block c
     const u32 nlo = lo + c * step;
@@ -326,8 +334,14 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
       if (M) A.meta[s] = TMeta{m.base, m.len + M, m.cap, m.cut, (m.len == 0 || ft[0] > m.newest) ? ft[0] : m.newest};
     } else {
       u32 drop = 0;
-      if (cd > m.cut && m.len > 0) drop = ts_lower(A.pool, m.base, 0, m.len, cut);  // oldest first: a prefix
-      l_oldest[tid] = m.len > drop ? A.pool[m.base + drop].ts : 0;  // for the interpolated searches
+      u64 oldest = 0;
+      if (cd > m.cut && m.len > 0) {
+        drop = ts_lower(A.pool, m.base, 0, m.len, cut, oldest);  // oldest first: a prefix
+        if (drop == m.len) oldest = 0;
+      } else if (m.len > 0) {
+        oldest = A.pool[m.base].ts;
+      }
+      l_oldest[tid] = oldest;  // for the interpolated searches
       sc = hole ? 0 : ne;  // a hole's entries (a spill's unspilled keys) are never walked
       l_base[tid] = m.base;
       l_newest[tid] = m.newest;

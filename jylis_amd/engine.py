@@ -281,6 +281,34 @@ class Engine:
         mem = _same_mem(ma, mb, mc)
         self._check(self.lib.jy_gcount_converge(self.h, len(a), pa, pb, pc, mem))
 
+    def counter_converge_keys(self, ctype, keys, col, val, cell_key=None, sign=None):
+        """one peer batch with its key strings (jy_counter_converge_keys):
+        keys interned on the device, cells merged with the device slots.
+        Host keys (list or (bytes, offs)) with host cells, or CUDA tensors
+        throughout (keys as (uint8 bytes, int64 offs))."""
+        if isinstance(keys, tuple) and hasattr(keys[0], "data_ptr"):
+            kb, ko = keys
+            nk = int(ko.numel()) - 1
+            pkb, pko = C.c_void_p(kb.data_ptr()), C.c_void_p(ko.data_ptr())
+            km = DEVICE
+        else:
+            kb, ko = self._keys(keys)
+            nk = len(ko) - 1
+            pkb, pko = kb.ctypes.data, ko.ctypes.data
+            km = HOST
+        c, pc, mc = _arg(col, np.uint16)
+        v, pv, mv = _arg(val, np.uint64)
+        args = [(c, mc), (v, mv)]
+        pk = ps = None
+        if cell_key is not None:
+            k_, pk, mk = _arg(cell_key, np.uint32)
+            args.append((k_, mk))
+        if sign is not None:
+            s_, ps, ms = _arg(sign, np.uint8)
+            args.append((s_, ms))
+        mem = _same_mem(km, *[m for _, m in args])
+        self._check(self.lib.jy_counter_converge_keys(self.h, ctype, nk, pkb, pko, len(c), pk, ps, pc, pv, mem))
+
     def gcount_converge_block(self, cols, slot0, vals):
         cols = np.ascontiguousarray(cols, np.uint16)
         v, pv, mv = _arg(vals, np.uint64)

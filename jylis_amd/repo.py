@@ -138,14 +138,18 @@ class RepoGCOUNT(_GpuRepo):
     def converge_deltas(self, batch, ctype=GCOUNT):
         if ctype != self.ctype:
             return
-        slots = self._intern(batch)
+        kb, ko = _keys_of(batch)
         offs = np.asarray(batch["offs"], np.uint64)
         ids = np.asarray(batch["ids"], np.uint64)
         if len(ids) == 0:
+            self._intern(batch)  # converge creates the keys (_data_for) even with no cells
             return
         cols = self.eng.replica_cols(ids.tolist())
-        cell_slot = np.repeat(slots, np.diff(offs).astype(np.int64))
-        self.eng.gcount_converge(cell_slot, cols, np.asarray(batch["vals"], np.uint64))
+        nk = len(ko) - 1
+        cell_key = np.repeat(np.arange(nk, dtype=np.uint32), np.diff(offs).astype(np.int64))
+        # one call: the keys interned on the device feed the merge (no slot round trip);
+        # the host learns new keys' names lazily (_sync_names)
+        self.eng.counter_converge_keys(GCOUNT, (kb, ko), cols, np.asarray(batch["vals"], np.uint64), cell_key=cell_key)
 
     def get(self, keys):
         """GCOUNT GET (repo_gcount.pony:53-55): missing key -> 0"""
@@ -185,18 +189,23 @@ class RepoPNCOUNT(_GpuRepo):
     def converge_deltas(self, batch, ctype=PNCOUNT):
         if ctype != self.ctype:
             return
-        slots = self._intern(batch)
-        parts = []
-        for pre in ("p_", "n_"):
+        kb, ko = _keys_of(batch)
+        nk = len(ko) - 1
+        keys, signs, cols, vals = [], [], [], []
+        for sg, pre in enumerate(("p_", "n_")):
             offs = np.asarray(batch[pre + "offs"], np.uint64)
             ids = np.asarray(batch[pre + "ids"], np.uint64)
             if len(ids) == 0:
-                parts.append(None)
                 continue
-            cols = self.eng.replica_cols(ids.tolist())
-            parts.append((np.repeat(slots, np.diff(offs).astype(np.int64)), cols,
-                          np.asarray(batch[pre + "vals"], np.uint64)))
-        self.eng.pncount_converge(parts[0], parts[1])
+            keys.append(np.repeat(np.arange(nk, dtype=np.uint32), np.diff(offs).astype(np.int64)))
+            signs.append(np.full(len(ids), sg, np.uint8))
+            cols.append(self.eng.replica_cols(ids.tolist()))
+            vals.append(np.asarray(batch[pre + "vals"], np.uint64))
+        if not keys:
+            self._intern(batch)  # converge creates the keys (_data_for) even with no cells
+            return
+        self.eng.counter_converge_keys(PNCOUNT, (kb, ko), np.concatenate(cols), np.concatenate(vals),
+                                       cell_key=np.concatenate(keys), sign=np.concatenate(signs))
 
     def get(self, keys):
         """PNCOUNT GET (repo_pncount.pony:55-57): (sum P - sum N) as i64, missing -> 0"""

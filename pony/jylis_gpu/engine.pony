@@ -34,6 +34,7 @@ class _Engine
 
   fun ref intern(ty: I32, keys: Array[String] box): Array[U32] ? =>
     """slots of `keys`, creating missing ones (Repo._data_for)"""
+    sync_names(ty)  // keys a one-call converge interned on the device
     let m = _Strs(keys)
     let slots = Array[U32].init(0, keys.size())
     check(@jy_keys_intern(ptr, ty, keys.size().u64(), m.bytes.cpointer(), m.offs.cpointer(),
@@ -52,6 +53,29 @@ class _Engine
     s
 
   fun name(slot: U32): String => try _names(slot.usize())? else "" end
+
+  fun ref sync_names(ty: I32) =>
+    """names of keys interned on the device (jy_counter_converge_keys) come
+    back from the directory (jy_keys_export) before a flush needs them"""
+    let n = @jy_keys_count(ptr, ty)
+    let have = _names.size().u64()
+    if n <= have then return end
+    let offs = Array[U64].init(0, (n - have).usize() + 1)
+    @jy_keys_export(ptr, ty, have, n - have, offs.cpointer(), Pointer[U8], 0)  // sizes first
+    let total = try offs(offs.size() - 1)? else 0 end
+    let bytes = Array[U8].init(0, total.usize())
+    if @jy_keys_export(ptr, ty, have, n - have, offs.cpointer(), bytes.cpointer(), total) != 0 then return end
+    var i: USize = 0
+    while (i + 1) < offs.size() do
+      try
+        let a = offs(i)?.usize()
+        let b = offs(i + 1)?.usize()
+        let k = recover String(b - a) end
+        for j in Range(a, b) do k.push(bytes(j)?) end
+        _names.push(consume k)
+      end
+      i = i + 1
+    end
 
   fun replica(col': U32): U64 =>
     var id: U64 = 0

@@ -34,6 +34,13 @@ use @jy_gcount_converge[I32](eng: Pointer[None] tag, n: U64, slot: Pointer[U32] 
   col: Pointer[U16] tag, value: Pointer[U64] tag, mem: I32)
 use @jy_gcount_converge_block[I32](eng: Pointer[None] tag, ncols: U32, cols: Pointer[U16] tag,
   slot0: U32, nslots: U32, vals: Pointer[U64] tag, mem: I32)
+use @jy_counter_converge_keys[I32](eng: Pointer[None] tag, ty: I32, nkeys: U64,
+  key_bytes: Pointer[U8] tag, key_offs: Pointer[U64] tag, ncells: U64, cell_key: Pointer[U32] tag,
+  sign: Pointer[U8] tag, col: Pointer[U16] tag, value: Pointer[U64] tag, mem: I32)
+use @jy_replica_count[U32](eng: Pointer[None] tag)
+use @jy_keys_count[U64](eng: Pointer[None] tag, ty: I32)
+use @jy_keys_export[I32](eng: Pointer[None] tag, ty: I32, slot0: U64, n: U64, offs: Pointer[U64] tag,
+  bytes: Pointer[U8] tag, cap: U64)
 use @jy_gcount_get[I32](eng: Pointer[None] tag, n: U64, slots: Pointer[U32] tag,
   out: Pointer[U64] tag, mem: I32)
 use @jy_pncount_converge[I32](eng: Pointer[None] tag,

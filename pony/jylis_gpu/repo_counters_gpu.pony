@@ -50,6 +50,7 @@ class RepoGCOUNTGpu
     match _eng
     | let e: _Engine =>
       try
+        e.sync_names(JyGCOUNT())
         let f = _CounterFlush(e, JyGCOUNT())?
         for (i, s) in f.slots.pairs() do
           let d = GCounter(_identity)
@@ -139,6 +140,7 @@ class RepoPNCOUNTGpu
     match _eng
     | let e: _Engine =>
       try
+        e.sync_names(JyPNCOUNT())
         let f = _CounterFlush(e, JyPNCOUNT())?
         for (i, s) in f.slots.pairs() do
           let d = PNCounter(_identity)
@@ -233,6 +235,41 @@ primitive _CounterIn
       end
     end
     if keys.size() == 0 then return end
+    // A sparse batch (the usual flushed peer delta: a few replica entries per
+    // key) goes out in ONE call with its key strings: interned on the device,
+    // merged with the device slots, no slot back to the host.  A batch that
+    // carries about every replica of every key (a full-state sync) is
+    // interned first, so its slot run can take the dense column-block path.
+    var ncell: USize = 0
+    for d' in ds.values() do
+      match d'
+      | let d: GCounter box => for _ in d.pairs() do ncell = ncell + 1 end
+      | let d: PNCounter box =>
+        for _ in d.pos_pairs() do ncell = ncell + 1 end
+        for _ in d.neg_pairs() do ncell = ncell + 1 end
+      end
+    end
+    let nrep = @jy_replica_count(e.ptr).usize().max(1)
+    if (ncell * 2) < (keys.size() * nrep) then
+      let m = _Strs(keys)
+      let ck = Array[U32]
+      let sg = Array[U8]
+      let cc = Array[U16]
+      let cv = Array[U64]
+      for (i, d') in ds.pairs() do
+        match d'
+        | let d: GCounter box =>
+          for (id, v) in d.pairs() do ck.push(i.u32()); cc.push(e.replica_col(id)?); cv.push(v) end
+        | let d: PNCounter box =>
+          for (id, v) in d.pos_pairs() do ck.push(i.u32()); sg.push(0); cc.push(e.replica_col(id)?); cv.push(v) end
+          for (id, v) in d.neg_pairs() do ck.push(i.u32()); sg.push(1); cc.push(e.replica_col(id)?); cv.push(v) end
+        end
+      end
+      let sp = if ty == JyGCOUNT() then Pointer[U8] else sg.cpointer() end
+      e.check(@jy_counter_converge_keys(e.ptr, ty, keys.size().u64(), m.bytes.cpointer(), m.offs.cpointer(),
+        ck.size().u64(), ck.cpointer(), sp, cc.cpointer(), cv.cpointer(), JyHost()))?
+      return
+    end
     let slots = e.intern(ty, keys)?
     // cells per sign: (slot, column, value)
     let cs = [Array[U32]; Array[U32]]

@@ -112,3 +112,36 @@ def test_device_interned_keys_converge(engine, oracle_mod):
     vals = np.arange(len(keys), dtype=np.uint64) * np.uint64(3)
     engine.gcount_converge(slots, col, vals)
     np.testing.assert_array_equal(engine.gcount_get(engine.lookup(GCOUNT, keys)), vals)
+
+
+def test_large_host_batches_through_copy_pool(engine):
+    """Host batches of several MiB go through the chunked parallel staging
+    (host_copy.hip: worker threads copy 1-MiB chunks into pinned memory, each
+    chunk's DMA issued as it lands) and the pinned slot readback.  Odd sizes
+    leave a partial last chunk; the result must equal the first-occurrence
+    slots and the COO converge must equal a numpy max over the same cells."""
+    from jylis_amd._lib import GCOUNT
+    rng = np.random.default_rng(7)
+    n = 700_001  # key bytes ~8.4 MB, offsets 5.6 MB, slots 2.8 MB: every stage is chunked
+    ids = rng.integers(0, 400_000, n)
+    ks = [b"big-key-%07d" % i for i in ids.tolist()]
+    table = {}
+    want = first_occurrence(ks, table)
+    got = engine.intern(GCOUNT, ks)
+    np.testing.assert_array_equal(got, want)
+    assert engine.nkeys(GCOUNT) == len(table)
+    # cells from host memory: slots 2.8 MB, columns 1.4 MB, values 5.6 MB
+    cols = engine.replica_cols([11, 22, 33]).astype(np.uint16)
+    first_col = cols[rng.integers(0, 3, n)]
+    val = rng.integers(1, 1 << 62, n, dtype=np.uint64)
+    engine.gcount_converge(got, first_col, val)
+    which = rng.integers(0, 3, n)
+    col = cols[which]
+    engine.gcount_converge(got, col, val)  # again, with other columns: max-merge per cell
+    sums = engine.gcount_get(np.arange(len(table), dtype=np.uint32))
+    cell = np.zeros((len(table), 3), np.uint64)
+    ci = {int(c): i for i, c in enumerate(cols)}
+    first_cols = np.array([ci[int(c)] for c in first_col], np.int64)
+    np.maximum.at(cell, (got.astype(np.int64), first_cols), val)
+    np.maximum.at(cell, (got.astype(np.int64), which), val)
+    np.testing.assert_array_equal(np.asarray(sums, np.uint64), cell.sum(axis=1, dtype=np.uint64))
