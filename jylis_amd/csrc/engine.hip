@@ -123,24 +123,35 @@ int32_t jy_stage(jy_engine* eng, int idx, const void* src, u64 bytes, int32_t me
   if (!eng->pin_used) {
     // next region of the ring: its copies (kPinRing calls ago) must have drained
     eng->pin_slot = (eng->pin_slot + 1) % jy_engine::kPinRing;
+    const double tw = jy_tracing() ? jy_now_us() : 0;
     JY_HIP(eng, hipEventSynchronize(eng->pins[eng->pin_slot].ready));
+    if (jy_tracing() && jy_now_us() - tw > 20) JY_TRACE("pinned ring slot %d: waited %.1f us", eng->pin_slot, jy_now_us() - tw);
     eng->pin_cursor = 0;
     eng->pin_used = true;
   }
   jy_engine::PinSlot& ps = eng->pins[eng->pin_slot];
   u64 need = round_up(eng->pin_cursor, 256) + bytes;
   if (need > ps.bytes) {
-    // grow this region: drain everything that may read it
+    // grow this region: drain everything that may read it.  Every other
+    // region of the ring that is smaller grows with it (all are idle after
+    // the drain), so a larger batch shape costs one pinned allocation pause
+    // (hipHostMalloc of tens of MB takes milliseconds), not one per region
+    // as the ring comes round.
     JY_HIP(eng, hipStreamSynchronize(eng->stream));
-    u64 nb = std::max<u64>(need * 2, 1ull << 20);
-    void* np = nullptr;
-    JY_HIP(eng, hipHostMalloc(&np, nb, hipHostMallocDefault));
-    if (ps.p) {
-      std::memcpy(np, ps.p, eng->pin_cursor);  // earlier inputs of this call stay valid
-      JY_HIP(eng, hipHostFree(ps.p));
+    const u64 nb = std::max<u64>(need * 2, 1ull << 20);
+    for (int r = 0; r < jy_engine::kPinRing; r++) {
+      jy_engine::PinSlot& q = eng->pins[r];
+      if (q.bytes >= nb) continue;
+      void* np = nullptr;
+      JY_HIP(eng, hipHostMalloc(&np, nb, hipHostMallocDefault));
+      if (q.p) {
+        if (r == eng->pin_slot) std::memcpy(np, q.p, eng->pin_cursor);  // earlier inputs of this call stay valid
+        JY_HIP(eng, hipHostFree(q.p));
+      }
+      q.p = np;
+      q.bytes = nb;
     }
-    ps.p = np;
-    ps.bytes = nb;
+    JY_TRACE("pinned ring grown to %llu B per region", (unsigned long long)nb);
   }
   u64 at = round_up(eng->pin_cursor, 256);
   // chunked: large copies run on the copy pool, each chunk's DMA issued as it lands
@@ -254,6 +265,17 @@ int32_t jy_engine_create(const jy_config* cfg, jy_engine** out) {
     return JY_EHIP;
   }
   eng->stream = eng->own_stream;
+  {
+    // the stream-ordered allocator keeps what it frees: with the default
+    // release threshold (0) every synchronisation hands freed blocks back and
+    // the next growth of a scratch array re-maps memory (0.1-1 ms of host
+    // time inside a merge call, GPU idle meanwhile: round-3 UJSON trace)
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, eng->device) == hipSuccess) {
+      uint64_t keep = UINT64_MAX;
+      hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
+  }
   std::memset(eng->pin_total, 0, 64);
   for (auto& ps : eng->pins) {
     if (hipEventCreateWithFlags(&ps.ready, hipEventDisableTiming) != hipSuccess) {
@@ -700,9 +722,13 @@ int32_t jy_counter_converge_keys(jy_engine* eng, int32_t type, uint64_t nkeys, c
   void* ds;
   JY_TRY(jy_scratch(eng, 2, nkeys * 4, &ds));
   u64 created = 0;
+  const double t1 = jy_tracing() ? jy_now_us() : 0;
   JY_TRY(jy_keydir_run(eng, type, nkeys, static_cast<const uint8_t*>(db), static_cast<const u64*>(dofs),
                        static_cast<u32*>(ds), true, &created));
+  const double t2 = jy_tracing() ? jy_now_us() : 0;
   JY_TRY(keys_created(eng, type, created));  // grows the slabs before the merge is enqueued
+  JY_TRACE("converge_keys: staging %.1f us, directory %.1f us, %llu created", t1 - t0, t2 - t1,
+           (unsigned long long)created);
   JY_TRACE("converge_keys: %llu keys, %llu cells: %.1f us after the host checks", (unsigned long long)nkeys,
            (unsigned long long)ncells, jy_now_us() - t0);
   return jy_counter_coo_keyed(eng, which, ncells, static_cast<const u32*>(ds), static_cast<const u32*>(dk),

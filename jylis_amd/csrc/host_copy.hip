@@ -15,6 +15,7 @@
 // of workers (default 6; 0 = copy on the calling thread only).
 
 #include <atomic>
+#include <immintrin.h>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -105,6 +106,12 @@ class CopyPool {
   void copy_chunk(const Job& j, u64 c, u32 tag) {
     const u64 off = c * kChunk;
     std::memcpy(j.dst + off, j.src + off, std::min<u64>(kChunk, j.bytes - off));
+    // memcpy may use weakly ordered (non-temporal / fast-string) stores,
+    // which a release store does not order: fence them, so that the DMA the
+    // calling thread enqueues once it sees `done` reads the copied bytes
+#ifndef JY_COPY_NO_FENCE  // A/B only
+    _mm_sfence();
+#endif
     done_[c].store(tag, std::memory_order_release);
   }
 

@@ -369,6 +369,7 @@ int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, co
   JY_HIP(eng, hipStreamSynchronize(eng->stream));
   JY_TRACE("keydir %llu keys: probe counts after %.1f us of waiting", (unsigned long long)n, jy_now_us() - t0);
   const u64 m = hc[0], mbytes = hc[1];
+  JY_TRACE("keydir %llu keys: %llu misses (create %d)", (unsigned long long)n, (unsigned long long)m, (int)create);
   if (!create || m == 0) {
     LAUNCH(k_key_copy_res, n, n, res, slots);
     return JY_OK;

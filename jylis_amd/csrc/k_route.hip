@@ -35,33 +35,20 @@ __device__ __forceinline__ u64 round_up8(u64 x) { return (x + kArenaAlign - 1) &
 //   scan        every (owner, quantity) column of tile counts in one
 //               device-wide scan taken column after column (jy_dscan.hpp);
 //               k_rt_hdr takes the grand totals to the header
-//   k_rt_place  per entry: its place in its owner's run = tile base + its
-//               rank among the tile's earlier entries for the same owner
-//               (one ballot per distinct owner and 64-entry slice); an entry
-//               that fits is written, else listed in ovf -- and the first
-//               entry of an owner that does not fit writes the header (the
-//               placed entries are the prefix before it: the ends grow along
-//               an owner's sequence)
-// A tile is ONE WAVE (4 entries per lane, slice u = entries u*64 + lane, so
-// the slices run in input order).  Owner d's running counts live in lane d's
-// registers (S <= 64): no LDS, no barrier, and the tile's bases are loaded
-// together with the entries, so placing an entry needs one round trip.
-// (Round 2's form, a 256-thread workgroup per tile with LDS counts per wave,
-// took 45 us (count) + 134 us (place) at 8M entries.)
-#ifndef JY_RT_PLACE_WG
-#define JY_RT_PLACE_WG 0
-#endif
-#ifndef JY_RT_SLICES
-#define JY_RT_SLICES 4
-#endif
-constexpr int kSlices = JY_RT_SLICES;  // 64-entry slices per tile (one wave)
-constexpr int kT = 64 * kSlices;       // entries per tile
-constexpr int kWG = 256;      // threads per workgroup = 4 tiles
-
-__device__ __forceinline__ u64 readlane64(u64 x, u32 lane) {
-  const u32 lo = __builtin_amdgcn_readlane((u32)x, lane), hi = __builtin_amdgcn_readlane((u32)(x >> 32), lane);
-  return ((u64)hi << 32) | lo;
-}
+//   k_rt_place  per entry: its place in its owner's run = tile base + the
+//               waves before it + its rank among its wave's entries for the
+//               same owner (one ballot per distinct owner, masked scans);
+//               an entry that fits is written, else listed in ovf -- and the
+//               first entry of an owner that does not fit writes the header
+//               (the placed entries are the prefix before it: the ends grow
+//               along an owner's sequence)
+// The count is ONE WAVE per tile (4 entries per lane, slice u = entries
+// u*64 + lane): owner d's counts live in lane d's registers (S <= 64), no LDS
+// and no barrier (45 -> 29 us at 8M entries against a 256-thread workgroup
+// with LDS counts per wave).
+constexpr int kSlices = 4;        // 64-entry slices per count tile (one wave)
+constexpr int kT = 64 * kSlices;  // entries per tile (count and place)
+constexpr int kWG = 256;          // count: threads per workgroup = 4 tiles
 
 __global__ __launch_bounds__(kWG) void k_rt_count(const u32* __restrict__ owner, const u64* __restrict__ lr, u64 n,
                                                   u32 S, u64* __restrict__ tcnt) {
@@ -114,115 +101,11 @@ __global__ void k_rt_hdr(const u64* __restrict__ tcnt, u64 ntiles, u32 W, unsign
   hdr[c] = hi - tcnt[c];
 }
 
-__global__ __launch_bounds__(kWG) void k_rt_place(const u32* __restrict__ owner, const u32* __restrict__ slot,
-                                                  const u64* __restrict__ ts, const u64* __restrict__ pre,
-                                                  const u64* __restrict__ lr, const uint8_t* __restrict__ arena, u64 n,
-                                                  u32 S, u64 cap, u64 cap_byte, const u64* __restrict__ tcnt,
-                                                  unsigned long long* __restrict__ hdr, u64* __restrict__ recs,
-                                                  uint8_t* __restrict__ bytes, u32* __restrict__ ovf,
-                                                  unsigned long long* __restrict__ skipped) {
-  const u64 tile = (u64)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6);
-  if (tile * kT >= n) return;  // a whole wave
-  const u32 lane = __lane_id();
-  const u64 lt = (1ull << lane) - 1;
-  // lane d: owner d's next record / byte position in its run (the tile's row
-  // of the scanned counts less the column's base, row 0)
-  u64 rb = 0, rbb = 0;
-  if (lane < S) {
-    const u64* row = tcnt + tile * S * 2;
-    rb = row[lane * 2] - tcnt[lane * 2];
-    rbb = row[lane * 2 + 1] - tcnt[lane * 2 + 1];
-  }
-  u32 o[kSlices], sl[kSlices];
-  u64 t[kSlices], p[kSlices], l[kSlices], b[kSlices];
-#pragma unroll
-  for (int u = 0; u < kSlices; u++) {
-    const u64 i = tile * kT + (u64)u * 64 + lane;
-    o[u] = 0xFFFFFFFFu;
-    sl[u] = 0;
-    t[u] = p[u] = l[u] = b[u] = 0;
-    if (i < n) {
-      o[u] = __builtin_nontemporal_load(owner + i);
-      sl[u] = __builtin_nontemporal_load(slot + i);
-      t[u] = __builtin_nontemporal_load(ts + i);
-      p[u] = __builtin_nontemporal_load(pre + i);
-      l[u] = __builtin_nontemporal_load(lr + i);
-      const u64 len = l[u] & JY_LR_LEN_MASK;
-      b[u] = len > 8 ? round_up8(len) : 0;
-      if (o[u] >= S) atomicAdd(skipped, 1ull);  // an owner outside [0, S): dropped, counted
-    }
-  }
-  // ranks: every slice's places first (ALU and cross-lane only)
-  u64 pos[kSlices], bpos[kSlices];
-#pragma unroll
-  for (int u = 0; u < kSlices; u++) {
-    const bool valid = o[u] < S;
-    const bool anyb = __ballot(b[u] != 0 && valid) != 0;
-    pos[u] = bpos[u] = 0;
-    u64 pending = __ballot(valid);
-    while (pending) {
-      const u32 d = __builtin_amdgcn_readlane(o[u], __ffsll((unsigned long long)pending) - 1);
-      const bool mine = o[u] == d;
-      const u64 m = __ballot(mine);
-      pending &= ~m;
-      const u64 x = mine ? b[u] : 0ull;
-      const u64 inc = anyb ? jyscan::wave_incl<u64>(x) : 0ull;
-      const u64 tot = anyb ? readlane64(inc, 63) : 0ull;
-      if (mine) {
-        pos[u] = readlane64(rb, d) + __popcll(m & lt);
-        bpos[u] = readlane64(rbb, d) + inc - x;
-      }
-      if (lane == d) {
-        rb += __popcll(m);
-        rbb += tot;
-      }
-    }
-  }
-  // the long values' first two granules of every slice, loaded together
-  // (values of <= 16 bytes -- the common long value -- need nothing else)
-  bool fits[kSlices];
-  u64 g0[kSlices], g1[kSlices];
-#pragma unroll
-  for (int u = 0; u < kSlices; u++) {
-    fits[u] = o[u] < S && pos[u] < cap && bpos[u] + b[u] <= cap_byte;
-    g0[u] = g1[u] = 0;
-    if (fits[u] && b[u]) {
-      const u64* src = reinterpret_cast<const u64*>(arena + (l[u] >> JY_LR_LEN_BITS));
-      g0[u] = src[0];
-      g1[u] = src[1];  // b >= 16: a value longer than 8 bytes takes two granules at least
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < kSlices; u++) {
-    if (o[u] >= S) continue;
-    if (!fits[u]) {
-      const u64 i = tile * kT + (u64)u * 64 + lane;
-      ovf[1 + atomicAdd(ovf, 1u)] = (u32)i;
-      if (pos[u] == 0 || (pos[u] - 1 < cap && bpos[u] <= cap_byte)) {  // the first of its owner that does not fit
-        hdr[2 * o[u]] = pos[u];
-        hdr[2 * o[u] + 1] = bpos[u];
-      }
-      continue;
-    }
-    u64 out_lr = l[u];
-    if (b[u]) {  // the value's 8-B granules into the run's byte section
-      u64* dst = reinterpret_cast<u64*>(bytes + (u64)o[u] * cap_byte + bpos[u]);
-      dst[0] = g0[u];
-      dst[1] = g1[u];
-      const u64* src = reinterpret_cast<const u64*>(arena + (l[u] >> JY_LR_LEN_BITS));
-      for (u64 w = 2; w < b[u] / 8; w++) dst[w] = src[w];
-      out_lr = (bpos[u] << JY_LR_LEN_BITS) | (l[u] & JY_LR_LEN_MASK);
-    }
-    u64x2* r = reinterpret_cast<u64x2*>(recs + ((u64)o[u] * cap + pos[u]) * 4);  // 32-B records, two 16-B stores
-    r[0] = u64x2{(u64)sl[u], t[u]};
-    r[1] = u64x2{p[u], out_lr};
-  }
-}
-
-#if JY_RT_PLACE_WG
-// A/B: round 2's placement, a 256-thread workgroup per 256-entry tile (one
-// entry per thread, per-wave counts in LDS)
-__global__ __launch_bounds__(256) void k_rt_place_wg(const u32* __restrict__ owner, const u32* __restrict__ slot,
+// placement: a 256-thread workgroup per tile, one entry per thread, per-wave
+// counts in LDS.  (A one-wave-per-tile form with four entries per lane and
+// the running bases in lane registers, like k_rt_count, measured slower:
+// in-box A/B of the routed TREG step 0.358 vs 0.341 ms.)
+__global__ __launch_bounds__(256) void k_rt_place(const u32* __restrict__ owner, const u32* __restrict__ slot,
                                                  const u64* __restrict__ ts, const u64* __restrict__ pre,
                                                  const u64* __restrict__ lr, const uint8_t* __restrict__ arena, u64 n,
                                                  u32 S, u64 cap, u64 cap_byte, const u64* __restrict__ tcnt,
@@ -300,7 +183,7 @@ __global__ __launch_bounds__(256) void k_rt_place_wg(const u32* __restrict__ own
   r[0] = u64x2{(u64)sl, t};
   r[1] = u64x2{p, out_lr};
 }
-#endif
+
 
 }  // namespace
 
@@ -354,18 +237,11 @@ int32_t jy_treg_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, co
                        reinterpret_cast<unsigned long long*>(hdr_dev));
     JY_HIP(eng, hipGetLastError());
   }
-#if JY_RT_PLACE_WG
   static_assert(kT == 256, "the workgroup placement takes 256-entry tiles");
-  hipLaunchKernelGGL(k_rt_place_wg, dim3((u32)ntiles), dim3(256), 0, eng->stream, own, static_cast<const u32*>(dsl),
+  hipLaunchKernelGGL(k_rt_place, dim3((u32)ntiles), dim3(256), 0, eng->stream, own, static_cast<const u32*>(dsl),
                      static_cast<const u64*>(dts), static_cast<const u64*>(dpre), l, eng->arena[JY_TREG].p, n, nshards,
                      cap, cap_byte, tcnt, reinterpret_cast<unsigned long long*>(hdr_dev), recs_dev, bytes_dev, ovf_dev,
                      reinterpret_cast<unsigned long long*>(eng->skipped_dev));
-#else
-  hipLaunchKernelGGL(k_rt_place, dim3(nwg), dim3(kWG), 0, eng->stream, own, static_cast<const u32*>(dsl),
-                     static_cast<const u64*>(dts), static_cast<const u64*>(dpre), l, eng->arena[JY_TREG].p, n, nshards,
-                     cap, cap_byte, tcnt, reinterpret_cast<unsigned long long*>(hdr_dev), recs_dev, bytes_dev, ovf_dev,
-                     reinterpret_cast<unsigned long long*>(eng->skipped_dev));
-#endif
   JY_HIP(eng, hipGetLastError());
   return JY_OK;
 }

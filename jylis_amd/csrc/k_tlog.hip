@@ -239,7 +239,8 @@ __device__ __forceinline__ u32 pow2_cap(u32 n) {
 }
 
 // last idx in [0, n] with a[idx] <= x (a non-decreasing, a[0] <= x)
-__device__ __forceinline__ u32 lds_last_le(const u64* a, u32 n, u64 x) {
+template <class T>
+__device__ __forceinline__ u32 lds_last_le(const T* a, u32 n, u64 x) {
   u32 lo = 0, hi = n;
   while (lo < hi) {
     const u32 m = (lo + hi + 1) >> 1;
@@ -275,15 +276,20 @@ constexpr u32 kKept = 0x80000000u;  // eqx: kept flag | # kept entries of the ke
 //   4. appends: kept entries to the tail, oldest first (the first kCache
 //      passes from registers)
 // rank / q of the slow entries go to HBM for the rebuild in k_tlog_commit.
-#ifndef JY_TLOG_TILE_ATTR
+#ifndef JY_TLOG_WAVES
 // 80 VGPRs: 6 waves per SIMD (one cached pass; 2 cached passes took 90 VGPRs / 5 waves)
-#define JY_TLOG_TILE_ATTR __attribute__((amdgpu_waves_per_eu(6)))
+#define JY_TLOG_WAVES 6
+#endif
+#ifndef JY_TLOG_TILE_ATTR
+#define JY_TLOG_TILE_ATTR __attribute__((amdgpu_waves_per_eu(JY_TLOG_WAVES)))
 #endif
 __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs A, TRec* __restrict__ pool,
                                                                         u32* __restrict__ erank,
                                                                         u32* __restrict__ eqx) {
-  __shared__ u64 l_soff[kTile + 1];  // flattened offsets of the slow keys' entries
-  __shared__ u64 l_gb[kTile];        // first delta entry of each key
+  // u32 offsets inside the tile (its entries are < 2^32): 5.9 -> 4.9 KB of LDS
+  // per one-wave tile, under 160 KB / 32 waves per CU
+  __shared__ u32 l_soff[kTile + 1];  // flattened offsets of the slow keys' entries
+  __shared__ u32 l_gb[kTile];        // first delta entry of each key, less the tile's first (gb0)
   __shared__ u32 l_slot[kTile];
   __shared__ u64 l_oldest[kTile];  // oldest surviving timestamp of a slow key's log
   __shared__ u64 l_base[kTile], l_newest[kTile], l_cut[kTile], l_tn[kTile];
@@ -293,6 +299,7 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
   const u64 lanelt = (1ull << tid) - 1;
   const u64 k0 = (u64)blockIdx.x * kTile;
   const u32 nt = (u32)(A.nd - k0 < kTile ? A.nd - k0 : kTile);
+  const u64 gb0 = A.doff[k0];  // the tile's first delta entry
   // 1. keys
   u64 sc = 0;  // slow entries of this lane's key
   if (tid < nt) {
@@ -354,15 +361,15 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
       l_minrank[tid] = 0xFFFFFFFFu;
       l_tn[tid] = 0;
     }
-    l_gb[tid] = b0;
+    l_gb[tid] = (u32)(b0 - A.doff[k0]);
     l_slot[tid] = s;
     l_mode[tid] = fast ? kFast : kSkip;
   }
   {
     const u64 inc = jyscan::wave_incl<u64>(sc);
     const u64 tot = __shfl(inc, 63);  // every lane: a shuffle reads only active lanes
-    if (tid < nt) l_soff[tid] = inc - sc;
-    if (tid == 0) l_soff[nt] = tot;
+    if (tid < nt) l_soff[tid] = (u32)(inc - sc);
+    if (tid == 0) l_soff[nt] = (u32)tot;
   }
   __syncthreads();
 #ifdef JY_TLOG_AB_NOSLOW  // A/B only: the cost of stage 1 alone (WRONG results)
@@ -384,7 +391,7 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
     u64 t = 0, pp = 0, ll = 0, j = 0;
     if (f < F) {
       idx = lds_last_le(l_soff, nt - 1, f);
-      j = l_gb[idx] + (f - l_soff[idx]);
+      j = gb0 + l_gb[idx] + (f - l_soff[idx]);
       t = A.dts[j];
       pp = A.dpre[j];
       ll = A.dlr[j];
@@ -515,7 +522,7 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
     } else {
       idx = lds_last_le(l_soff, nt - 1, f);
       if (l_mode[idx] != kAppend) continue;
-      const u64 j = l_gb[idx] + (f - l_soff[idx]);
+      const u64 j = gb0 + l_gb[idx] + (f - l_soff[idx]);
       qx = eqx[j];
       if (!(qx & kKept)) continue;
       t = A.dts[j], pp = A.dpre[j], ll = A.dlr[j];
@@ -626,21 +633,13 @@ __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __
         i = l_s0[a] + r;
         j = l_blo[a] + (r - l_ns[a]);
       }
-      if (st) {  // first delta entry with rank <= i
-        lo = l_blo[a];
-        hi = l_bhi[a];
-        while (lo < hi) {
-          const u64 m = (lo + hi) >> 1;
-          if (erank[m] <= i) hi = m;
-          else lo = m + 1;
-        }
-      }
     }
+    // the item's record first: it does not depend on the rank search below,
+    // so its load is in flight with the search's
     u32 qx = 0;
     TRec x{};
     if (live) {
       if (st) {
-        qx = lo < l_bhi[a] ? eqx[lo] : 0u;
         x = load_rec(A.pool + l_src[a] + i);
       } else {
         qx = eqx[j];
@@ -649,6 +648,31 @@ __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __
         x.lr = A.dlr[j];
         x.pad = erank[j];
       }
+    }
+    if (live && st) {
+      // first delta entry with rank <= i: the ranks do not increase along
+      // the (newest-first) delta segment, so the entries ranked above i are
+      // a prefix.  A short segment is counted with its ranks loaded at once
+      // (one round trip), a long one bisected.
+      lo = l_blo[a];
+      hi = l_bhi[a];
+      constexpr u64 kLin = 4;
+      if (hi - lo <= kLin) {
+        u32 rk[kLin];
+#pragma unroll
+        for (u64 q = 0; q < kLin; q++) rk[q] = lo + q < hi ? erank[lo + q] : 0u;
+        u64 c = 0;
+#pragma unroll
+        for (u64 q = 0; q < kLin; q++) c += (lo + q < hi) & (rk[q] > i);
+        lo += c;
+      } else {
+        while (lo < hi) {
+          const u64 m = (lo + hi) >> 1;
+          if (erank[m] <= i) hi = m;
+          else lo = m + 1;
+        }
+      }
+      qx = lo < l_bhi[a] ? eqx[lo] : 0u;
     }
     if (live) {
       const u32 M = l_M[a];

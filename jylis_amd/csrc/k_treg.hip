@@ -199,14 +199,12 @@ struct RoutedIn {
   unsigned long long* skipped;
 };
 
-// the record and its run's count are loaded together (the record is inside
-// the run's buffer whatever the count says): one round trip
 __device__ __forceinline__ bool routed_get(const RoutedIn& R, u64 i, u32& s, u64& t, u64& p, u64& l) {
   const u64 src = i / R.cap, j = i - src * R.cap;
   const u64 cnt = R.hdr[2 * src];
+  if (j >= (cnt < R.cap ? cnt : R.cap)) return false;
   const u64x2 a = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(R.recs + i * 4));
   const u64x2 b = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(R.recs + i * 4) + 1);
-  if (j >= (cnt < R.cap ? cnt : R.cap)) return false;
   if (a.x == ~0ull) return false;  // hole
   if (a.x >= R.nslots) {
     atomicAdd(R.skipped, 1ull);
@@ -221,18 +219,11 @@ __device__ __forceinline__ bool routed_get(const RoutedIn& R, u64 i, u32& s, u64
   return true;
 }
 
-#ifndef JY_TREG_ROUTED_V2
-#define JY_TREG_ROUTED_V2 0
-#endif
-#ifndef JY_TREG_ROUTED_U
-#define JY_TREG_ROUTED_U 4
-#endif
-#ifndef JY_TREG_ROUTED_REWRITE
-#define JY_TREG_ROUTED_REWRITE 1
-#endif
-constexpr int kRoutedU = JY_TREG_ROUTED_U;  // records per lane
+// (Measured and dropped in round 3: four records per lane, each record loaded
+// together with its run's count, every record rewriting its ts word -- in-box
+// A/B of the routed TREG step 0.352 vs 0.341 ms.)
 __global__ __launch_bounds__(kThreads) void k_treg_lww_routed(TregK K, RoutedIn R) {
-  constexpr int U = kRoutedU;
+  constexpr int U = 2;
   const u64 base = (u64)blockIdx.x * (kThreads * U) + (threadIdx.x >> 6) * (64 * U) + (threadIdx.x & 63);
   const u64 n = (u64)R.S * R.cap;
   u32 s[U];
@@ -256,68 +247,12 @@ __global__ __launch_bounds__(kThreads) void k_treg_lww_routed(TregK K, RoutedIn 
       push_dup(K, s[u], t[u], p[u], l[u]);
       continue;
     }
-    // as k_treg_lww<false>: every record rewrites its ts word (whole lines)
-    const bool w = t[u] >= t0[u] && lww_wins(t[u], t0[u], p[u], l[u], K.val, s[u], K.arena);
-    if (JY_TREG_ROUTED_REWRITE || w) K.ts[s[u]] = w ? t[u] : t0[u];
-    if (w) K.val[s[u]] = TVal{p[u], l[u]};
-  }
-}
-
-#if JY_TREG_ROUTED_V2
-// A/B: round 2's receiver (two records per lane, the count read before the record)
-__device__ __forceinline__ bool routed_get_v2(const RoutedIn& R, u64 i, u32& s, u64& t, u64& p, u64& l) {
-  const u64 src = i / R.cap, j = i - src * R.cap;
-  const u64 cnt = R.hdr[2 * src];
-  if (j >= (cnt < R.cap ? cnt : R.cap)) return false;
-  const u64x2 a = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(R.recs + i * 4));
-  const u64x2 b = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(R.recs + i * 4) + 1);
-  if (a.x == ~0ull) return false;  // hole
-  if (a.x >= R.nslots) {
-    atomicAdd(R.skipped, 1ull);
-    return false;
-  }
-  s = (u32)a.x;
-  t = a.y;
-  p = b.x;
-  l = b.y;
-  if ((l & JY_LR_LEN_MASK) > 8)
-    l = (((l >> JY_LR_LEN_BITS) + R.rebase + src * R.cap_byte) << JY_LR_LEN_BITS) | (l & JY_LR_LEN_MASK);
-  return true;
-}
-
-__global__ __launch_bounds__(kThreads) void k_treg_lww_routed_v2(TregK K, RoutedIn R) {
-  constexpr int U = 2;
-  const u64 base = (u64)blockIdx.x * (kThreads * U) + (threadIdx.x >> 6) * (64 * U) + (threadIdx.x & 63);
-  const u64 n = (u64)R.S * R.cap;
-  u32 s[U];
-  u64 t[U], p[U], l[U], t0[U];
-  bool valid[U], first[U];
-#pragma unroll
-  for (int u = 0; u < U; u++) {
-    const u64 i = base + (u64)u * 64;
-    s[u] = 0;
-    valid[u] = i < n && routed_get_v2(R, i, s[u], t[u], p[u], l[u]);
-  }
-#pragma unroll
-  for (int u = 0; u < U; u++)
-    if (valid[u]) t0[u] = K.ts[s[u]];
-  jy_claim_rows<U>(valid, s, K.seen, first);
-  clear_slice(K);
-#pragma unroll
-  for (int u = 0; u < U; u++) {
-    if (!valid[u]) continue;
-    if (!first[u]) {
-      push_dup(K, s[u], t[u], p[u], l[u]);
-      continue;
-    }
     if (t[u] >= t0[u] && lww_wins(t[u], t0[u], p[u], l[u], K.val, s[u], K.arena)) {
       K.ts[s[u]] = t[u];
       K.val[s[u]] = TVal{p[u], l[u]};
     }
   }
 }
-
-#endif
 
 // The duplicate list, folded in by ONE wave: a chunk of 64 records per pass
 // (lane = record); records of one slot inside a chunk run in rounds by their
@@ -619,17 +554,13 @@ int32_t jy_treg_merge_routed(jy_engine* eng, u32 S, u64 cap, u64 cap_byte, const
   JyTimed tm(eng);
   // one source's run per launch: a key that several peers flushed in the same
   // step is merged launch after launch (stream order), never a duplicate
-  const u32 grid = blocks(cap, kThreads * kRoutedU);
+  const u32 grid = blocks(cap, kThreads * 2);
   for (u32 src = 0; src < S; src++) {
     TregK K{};
     JY_TRY(claim_begin(eng, cap, grid, K));
     RoutedIn R{recs + (u64)src * cap * 4, hdr + 2 * (u64)src, 1, cap, cap_byte, rebase + (u64)src * cap_byte,
                eng->nkeys[JY_TREG], reinterpret_cast<unsigned long long*>(eng->skipped_dev)};
-#if JY_TREG_ROUTED_V2
-    hipLaunchKernelGGL(k_treg_lww_routed_v2, dim3(blocks(cap, kThreads * 2)), dim3(kThreads), 0, eng->stream, K, R);
-#else
     hipLaunchKernelGGL(k_treg_lww_routed, dim3(grid), dim3(kThreads), 0, eng->stream, K, R);
-#endif
     JY_HIP(eng, hipGetLastError());
   }
   return JY_OK;

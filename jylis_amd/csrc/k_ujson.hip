@@ -1184,8 +1184,21 @@ int32_t ujson_compact(jy_engine* eng, UjsonState& u, u64 room_e, u64 room_c) {
   JY_TRY(jy_scan_u64(eng, se, eo, nk));
   JY_TRY(jy_scan_u64(eng, sc, co, nk));
   const u64 be = u.live_e, bc = u.live_c;  // >= the compacted sizes
-  const u64 ecap = std::max<u64>({be + 8 * room_e, 3 * be, eng->cfg.entry_capacity[JY_UJSON], 1024});
-  const u64 ccap = std::max<u64>({bc + 8 * room_c, 3 * bc, eng->cfg.entry_capacity[JY_UJSON], 1024});
+  // Headroom: `room` is one converge's WORST case (every live entry touched),
+  // so the element pool's 16x lasts ~70 config-5 converges.  The cloud pool
+  // is small but every converge rewrites its touched documents' clouds
+  // (~0.7M dots against ~1.3M worst case), so 8x lasted ~10 converges and a
+  // compaction (~0.25 ms + a host wait) landed every few bench steps; 64x
+  // is ~0.7 GB at config 5 -- HBM is plentiful, compactions are not free.
+#ifndef JY_UJ_ROOM_E
+#define JY_UJ_ROOM_E 16
+#endif
+#ifndef JY_UJ_ROOM_C
+#define JY_UJ_ROOM_C 64
+#endif
+  constexpr u64 kRoomE = JY_UJ_ROOM_E, kRoomC = JY_UJ_ROOM_C;
+  const u64 ecap = std::max<u64>({be + kRoomE * room_e, 3 * be, eng->cfg.entry_capacity[JY_UJSON], 1024});
+  const u64 ccap = std::max<u64>({bc + kRoomC * room_c, 3 * bc, eng->cfg.entry_capacity[JY_UJSON], 1024});
   JY_TRACE("ujson compact: <= %llu elements, <= %llu cloud dots -> pools %llu / %llu", (unsigned long long)be,
            (unsigned long long)bc, (unsigned long long)ecap, (unsigned long long)ccap);
   if (u.spare_ecap < ecap) {
@@ -1340,7 +1353,9 @@ int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* sl
   if (nd >= 0xFFFFFFFFull) return eng->fail(JY_ERANGE, "ujson converge: more than 2^32 - 1 documents in one call");
   const u32 R = u.R;
   const u64 live_e = u.live_e, live_c = u.live_c;  // bounds of the touched state, before this converge
+  const double th0 = jy_tracing() ? jy_now_us() : 0;
   JY_TRY(ujson_plan(eng, u, nel, ncloud));
+  const double th1 = jy_tracing() ? jy_now_us() : 0;
   const u64 le = std::min(u.live_e, live_e), lc = std::min(u.live_c, live_c);  // (a compaction makes them exact)
   if (le + nel + ncloud + 2 >= (1ull << 32) || lc + ncloud + 2 >= (1ull << 32))
     return eng->fail(JY_ERANGE, "ujson converge: more than 2^32 touched items");
@@ -1469,6 +1484,8 @@ int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* sl
   const u64 g5 = gf + gk + (nvv + kTile - 1) / kTile + (nd + kTile - 1) / kTile + 2;
   hipLaunchKernelGGL(k_uj_scatter, dim3((u32)g5), dim3(kItemThreads), 0, eng->stream, A);
   JY_HIP(eng, hipGetLastError());
+  JY_TRACE("ujson merge %llu docs: plan %.1f us, rest of the host side %.1f us", (unsigned long long)nd, th1 - th0,
+           jy_now_us() - th1);
 #ifdef JY_UJ_PROBE
   if (const char* path = getenv("JY_UJ_PROBE_OUT")) {
     static std::vector<u64> buf(kProbe * 6);
