@@ -437,10 +437,12 @@ struct LongRun {
 // per delta item (validation, dense delta vv) ---------------------------------
 __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_el, u64 t_cl, u64 t_vv) {
   __shared__ Shared S;
-  // 64 runs staged (1 KB): U1's LDS stays small enough for every tile of a
-  // converge to be resident at once; a tile with more long runs has the
-  // owning threads fill the rest themselves
-  constexpr u32 kLongCap = 64;
+  // Every long run of the tile staged (16 KB).  (Round 3 tried 64 staged
+  // runs, 1 KB, owners filling the rest themselves: no speed-up.)
+#ifndef JY_UJ_LONG_CAP
+#define JY_UJ_LONG_CAP (4 * kDocTile)
+#endif
+  constexpr u32 kLongCap = JY_UJ_LONG_CAP;
   __shared__ LongRun l_long[kLongCap];
   __shared__ u32 l_nlong;
   if (blockIdx.x < ndt) {  // doc tiles: ticketed (the look-back walks tickets)
@@ -774,7 +776,14 @@ __device__ __forceinline__ void uj_compact_long(const UjArgs& A, bool sa, u64 k,
   if (live) x = sa ? A.cloud[pi] : A.dcloud[i];
   const u64 x0 = __shfl(x, 0), x1 = __shfl(x, lastl) + 1;
   const u32 cf = dcol(x0), cl = dcol(x1 - 1);
-  const u64 lof = mkdot(cf, merged_vv(A, k, cf) + 1), lol = mkdot(cl, merged_vv(A, k, cl) + 1);
+  // the merged vv of the wave's first and last column, read ONCE: the run
+  // starts below are searched from them, and an item of those columns must
+  // test its fold against the same value.  (Other waves' folds raise the row
+  // meanwhile; the fold test is exact for any value the row takes, but only
+  // with its run start and its count taken from that same value -- re-reading
+  // the row here made config-5 converges nondeterministic in round 3.)
+  const u64 vf = merged_vv(A, k, cf), vl = cl == cf ? vf : merged_vv(A, k, cl);
+  const u64 lof = mkdot(cf, vf + 1), lol = mkdot(cl, vl + 1);
   // [0, 1]: run starts on the state side, [2, 3]: on the delta side, [4, 5]:
   // the other side's bounds of the wave's dots
   WSearch s[6] = {{A.cloud, 1, alo, ahi, lof},  {A.cloud, 1, alo, ahi, lol}, {A.dcloud, 1, blo, bhi, lof},
@@ -783,7 +792,7 @@ __device__ __forceinline__ void uj_compact_long(const UjArgs& A, bool sa, u64 k,
   wave_lbs<6>(s);
   if (!live) return;
   const u32 c = dcol(x);
-  const u64 q = dseq(x), v = merged_vv(A, k, c);
+  const u64 q = dseq(x), v = c == cf ? vf : c == cl ? vl : merged_vv(A, k, c);
   if (q <= v) return;
   const u64 lo = mkdot(c, v + 1);
   const u64 ra0 = c == cf ? s[0].lo : c == cl ? s[1].lo : lower_bound(A.cloud, alo, ahi, lo);
