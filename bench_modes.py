@@ -27,19 +27,25 @@ def _timed(steps, warmup, step, dist, dev, eng=None, before_timed=None):
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    # with `eng`, the engine's own timing events (no system-scope fence) are the
+    # per-step device time; otherwise one pair of torch events brackets all the
+    # steps (a torch event record writes back and invalidates the caches: one
+    # pair per step put ~19 us of idle GPU into every short step)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if before_timed is not None:
         before_timed()
     if eng is not None:
         eng.timing(True)
     host = []
     t0 = time.perf_counter()
+    if eng is None:
+        ev0.record()
     for i in range(steps):
-        evs[i][0].record()
         h0 = time.perf_counter()
         step(warmup + i)
         host.append(time.perf_counter() - h0)
-        evs[i][1].record()
+    if eng is None:
+        ev1.record()
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -52,7 +58,7 @@ def _timed(steps, warmup, step, dist, dev, eng=None, before_timed=None):
         eng.timing(False)
         per_step = float(np.sum(calls)) / 1e3 / steps
         return elapsed, [per_step] * steps
-    return elapsed, [a.elapsed_time(b) / 1e3 for a, b in evs]
+    return elapsed, [ev0.elapsed_time(ev1) / 1e3 / steps] * steps
 
 
 def _max_over_ranks(x, dist, dev):

@@ -373,6 +373,10 @@ void jy_engine_destroy(jy_engine* eng) {
   }
   if (eng->pin_total) hipHostFree(eng->pin_total);
   if (eng->pin_rb) hipHostFree(eng->pin_rb);
+  if (eng->treg.dupflag) {
+    hipHostFree(eng->treg.dupflag);
+    for (auto& e : eng->treg.mev) hipEventDestroy(e);
+  }
   for (auto& ev : eng->tm_ev) {
     hipEventDestroy(ev.first);
     hipEventDestroy(ev.second);

@@ -234,6 +234,19 @@ struct TregState {  // per slot: ts u64 (read by every merge) + TVal (written by
   u64* dups_alt = nullptr;
   u64 dup_cap = 0;
   u64 dup_bound = 0;
+  // "a duplicate was pushed since the last fold": a host-mapped word the
+  // kernels set (only when they push, i.e. rarely) and the fold clears, plus
+  // a ring of the claim launches in flight (event, entries).  A full bound
+  // with the flag clear means the list is empty but for launches still in
+  // flight: the host waits for the oldest of those (the GPU keeps running the
+  // rest) instead of enqueueing a fold of nothing (~36 us of GPU time).
+  u32* dupflag = nullptr;
+  u32* dupflag_dev = nullptr;
+  static constexpr int kRing = 8;
+  hipEvent_t mev[kRing] = {};
+  u64 mn[kRing] = {};
+  int mhead = 0, mcount = 0;
+  u64 pending_n = 0;
 };
 
 // one TLOG entry: 32 B so a lane moves it with two 16-B accesses and an
@@ -439,7 +452,11 @@ struct JyTimed {
     if (!eng->timing || eng->tm_depth++ > 0) return;
     if (eng->tm_used == eng->tm_ev.size()) {
       std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
-      if (hipEventCreate(&ev.first) != hipSuccess || hipEventCreate(&ev.second) != hipSuccess) return;
+      // timing-only events: no system-scope fence on record (that fence writes
+      // back and invalidates the caches, ~19 us between two TREG merges)
+      if (hipEventCreateWithFlags(&ev.first, hipEventDisableSystemFence) != hipSuccess ||
+          hipEventCreateWithFlags(&ev.second, hipEventDisableSystemFence) != hipSuccess)
+        return;
       eng->tm_ev.push_back(ev);
     }
     on = hipEventRecord(eng->tm_ev[eng->tm_used].first, eng->stream) == hipSuccess;

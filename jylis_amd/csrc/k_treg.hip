@@ -41,6 +41,7 @@
 // handles, 32 B more per loser: see k_treg_lww).
 
 #include <algorithm>
+#include <cstring>
 
 
 #include "jy_dscan.hpp"
@@ -82,6 +83,7 @@ struct TregK {
   u64 clear_bytes;
   u32* dupn;     // duplicate list: count, then 32-B records {slot, ts, pre, lr}
   u64* dups;
+  u32* dupflag;  // host-mapped: set when a duplicate is pushed
   // RepoTREG._deltas (SET path only)
   u64* pts;
   TVal* pval;
@@ -111,6 +113,7 @@ __device__ __forceinline__ void push_dup(const TregK& K, u32 s, u64 t, u64 p, u6
   u64x2* r = reinterpret_cast<u64x2*>(K.dups + (u64)at * 4);
   r[0] = u64x2{(u64)s, t};
   r[1] = u64x2{p, l};
+  if (K.dupflag) __hip_atomic_store(K.dupflag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // this workgroup's slice of the other claim bitmap (16-B stores)
@@ -398,7 +401,52 @@ TregK state_of(jy_engine* eng) {
   K.arena = eng->arena[JY_TREG].p;
   K.dupn = t.dupn;
   K.dups = t.dups;
+  K.dupflag = t.dupflag_dev;
   return K;
+}
+
+// the claim launches in flight: retire those whose event has fired
+void ring_retire(TregState& t, bool wait_oldest) {
+  while (t.mcount > 0) {
+    hipEvent_t& ev = t.mev[t.mhead];
+    if (wait_oldest) {
+      hipEventSynchronize(ev);
+      wait_oldest = false;
+    } else if (hipEventQuery(ev) != hipSuccess) {
+      return;
+    }
+    t.pending_n -= t.mn[t.mhead];
+    t.mhead = (t.mhead + 1) % TregState::kRing;
+    t.mcount--;
+  }
+}
+
+// a claim launch of n entries was enqueued: note it in the ring
+int32_t ring_note(jy_engine* eng, u64 n) {
+  TregState& t = eng->treg;
+  if (!t.dupflag) return JY_OK;
+  if (t.mcount == TregState::kRing) ring_retire(t, true);
+  const int at = (t.mhead + t.mcount) % TregState::kRing;
+  JY_HIP(eng, hipEventRecord(t.mev[at], eng->stream));
+  t.mn[at] = n;
+  t.mcount++;
+  t.pending_n += n;
+  return JY_OK;
+}
+
+int32_t flag_init(jy_engine* eng) {
+  TregState& t = eng->treg;
+  if (t.dupflag) return JY_OK;
+  void* h = nullptr;
+  JY_HIP(eng, hipHostMalloc(&h, 64, hipHostMallocMapped));
+  std::memset(h, 0, 64);
+  void* d = nullptr;
+  JY_HIP(eng, hipHostGetDevicePointer(&d, h, 0));
+  // completion markers only (the flag is written with system-scope stores): no cache fence
+  for (auto& e : t.mev) JY_HIP(eng, hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence));
+  t.dupflag = static_cast<u32*>(h);
+  t.dupflag_dev = static_cast<u32*>(d);
+  return JY_OK;
 }
 
 // the claim bitmaps of one launch: this launch's (clean) and the other one,
@@ -457,6 +505,17 @@ int32_t fold_rounds(jy_engine* eng, int rounds, bool set) {
 // batch (whose pending-delta test must see them) or an arena move.  Parallel
 // rounds first; one wave then folds what is left (a slot repeated more often
 // than the rounds cover) and resets the list.
+// after a fold (stream order): the list is empty, and every launch enqueued
+// so far is before the fold, so the ring's launches no longer bound it
+void flag_clear_after_fold(jy_engine* eng) {
+  TregState& t = eng->treg;
+  t.dup_bound = 0;
+  if (!t.dupflag) return;
+  hipMemsetAsync(t.dupflag_dev, 0, 4, eng->stream);
+  t.mhead = t.mcount = 0;
+  t.pending_n = 0;
+}
+
 constexpr int kFoldRounds = 3;
 int32_t fold_now(jy_engine* eng) {
   TregState& t = eng->treg;
@@ -464,7 +523,7 @@ int32_t fold_now(jy_engine* eng) {
   JY_TRY(fold_rounds(eng, kFoldRounds, false));
   hipLaunchKernelGGL((k_treg_fold<false>), dim3(1), dim3(64), 0, eng->stream, state_of(eng));
   JY_HIP(eng, hipGetLastError());
-  t.dup_bound = 0;
+  flag_clear_after_fold(eng);
   return JY_OK;
 }
 
@@ -473,6 +532,18 @@ int32_t fold_now(jy_engine* eng) {
 // launch's bitmap and the other one to clear
 int32_t claim_begin(jy_engine* eng, u64 n, u32 nblocks, TregK& K) {
   TregState& t = eng->treg;
+  JY_TRY(flag_init(eng));
+  if (t.dup_bound + n > t.dup_cap && t.dup_cap) {
+    // nothing pushed since the last fold (the flag is set by the pushing
+    // kernel itself, and only launches still in flight may push): the list's
+    // bound is what those launches could add -- wait for the oldest of them
+    // while that does not fit, rather than fold an empty list
+    ring_retire(t, false);
+    if (__atomic_load_n(t.dupflag, __ATOMIC_ACQUIRE) == 0) {
+      while (t.mcount > 0 && t.pending_n + n > t.dup_cap) ring_retire(t, true);
+      if (__atomic_load_n(t.dupflag, __ATOMIC_ACQUIRE) == 0) t.dup_bound = t.pending_n;
+    }
+  }
   if (t.dup_bound + n > t.dup_cap) {
     JY_TRY(fold_now(eng));
     if (n > t.dup_cap) {
@@ -545,7 +616,7 @@ int32_t jy_treg_merge(jy_engine* eng, u64 n, const u32* slot, const u64* ts, con
     hipLaunchKernelGGL((k_treg_lww<false, false>), dim3(grid), dim3(kThreads), 0,
                        eng->stream, K, slot, ts, pre, lr, n);
   JY_HIP(eng, hipGetLastError());
-  return JY_OK;
+  return ring_note(eng, n);
 }
 
 int32_t jy_treg_merge_routed(jy_engine* eng, u32 S, u64 cap, u64 cap_byte, const u64* recs, const u64* hdr,
@@ -562,6 +633,7 @@ int32_t jy_treg_merge_routed(jy_engine* eng, u32 S, u64 cap, u64 cap_byte, const
                eng->nkeys[JY_TREG], reinterpret_cast<unsigned long long*>(eng->skipped_dev)};
     hipLaunchKernelGGL(k_treg_lww_routed, dim3(grid), dim3(kThreads), 0, eng->stream, K, R);
     JY_HIP(eng, hipGetLastError());
+    JY_TRY(ring_note(eng, cap));
   }
   return JY_OK;
 }
@@ -624,7 +696,7 @@ int32_t jy_treg_set_batch(jy_engine* eng, u64 n, const u32* slot, const u64* ts,
   K.pcount = t.dcount;
   hipLaunchKernelGGL((k_treg_fold<true>), dim3(1), dim3(64), 0, eng->stream, K);
   JY_HIP(eng, hipGetLastError());
-  t.dup_bound = 0;
+  flag_clear_after_fold(eng);
   return JY_OK;
 }
 

@@ -101,3 +101,42 @@ def test_large_random(oracle_mod, engine):
         want.converge(b)
         got.converge_deltas(b)
     assert_state_equal(O.TREG, want.state(), got.state())
+
+
+@pytest.mark.parametrize("dup_rounds", [(), (5,), (2, 9)])
+def test_many_merges_between_reads(engine, dup_rounds):
+    """Device batches merged back to back with no read in between: the
+    duplicate list's bound passes its capacity every few launches.  With no
+    duplicate pushed since the last fold the engine waits for launches in
+    flight instead of folding an empty list; batches listed in `dup_rounds`
+    repeat slots (in-launch duplicates), which must still be folded exactly.
+    Checked against a numpy LWW over every applied batch (8-byte values:
+    the (ts, value) order is (ts, prefix))."""
+    import torch
+    from jylis_amd._lib import TREG
+    rng = np.random.default_rng(17 + len(dup_rounds))
+    n = 200_000
+    slots = engine.intern(TREG, [b"m%07d" % i for i in range(n)])
+    assert (slots == np.arange(n)).all()
+    best_ts = np.zeros(n, np.uint64)
+    best_pre = np.zeros(n, np.uint64)
+    dev = torch.device("cuda", 0)
+    for r in range(14):
+        s = np.arange(n, dtype=np.uint32)
+        if r in dup_rounds:
+            s = rng.integers(0, n, n).astype(np.uint32)  # repeats inside the launch
+        ts = rng.integers(1, 1 << 12, n).astype(np.uint64) + np.uint64(r << 10)
+        pre = rng.integers(1 << 56, 1 << 63, n, dtype=np.uint64)  # 8 nonzero-leading bytes
+        lr = np.full(n, 8, np.uint64)
+        engine.treg_converge(*(torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a.view(np.int32)).to(dev)
+                               for a in (s, ts, pre, lr)))
+        order = np.lexsort((pre, ts))
+        cand_ts, cand_pre = best_ts[s[order]], best_pre[s[order]]
+        win = (ts[order] > cand_ts) | ((ts[order] == cand_ts) & (pre[order] > cand_pre))
+        # apply in ascending order so the last assignment per slot is the maximum
+        so, to, po = s[order][win], ts[order][win], pre[order][win]
+        best_ts[so] = to
+        best_pre[so] = po
+    gts, gpre, glr = engine.treg_read(np.arange(n, dtype=np.uint32))
+    np.testing.assert_array_equal(gts, best_ts)
+    np.testing.assert_array_equal(gpre, best_pre)
