@@ -714,21 +714,36 @@ int32_t jy_counter_converge_keys(jy_engine* eng, int32_t type, uint64_t nkeys, c
   }
   JY_TRY(counter_cols_check(eng, which, ncells, col, mem));
   const double t0 = jy_tracing() ? jy_now_us() : 0;
-  const void *db, *dofs, *dk = nullptr, *dsg = nullptr, *dc, *dv;
+  // the keys first: the directory's probe starts once they are up, and the
+  // cells are staged (host copies, their DMAs) while it runs
+  const void *db, *dofs;
   JY_TRY(stage_begin(eng));
   JY_TRY(jy_stage(eng, 0, kb, mem == JY_HOST ? ko[nkeys] : 0, mem, &db));  // device: used in place
   JY_TRY(jy_stage(eng, 1, ko, (nkeys + 1) * 8, mem, &dofs));
-  if (cell_key) JY_TRY(jy_stage(eng, 3, cell_key, ncells * 4, mem, &dk));
-  if (sign) JY_TRY(jy_stage(eng, 4, sign, ncells, mem, &dsg));
-  JY_TRY(jy_stage(eng, 5, col, ncells * 2, mem, &dc));
-  JY_TRY(jy_stage(eng, 6, val, ncells * 8, mem, &dv));
   JY_TRY(stage_end(eng));
+  struct Cells {
+    jy_engine* eng;
+    u64 n;
+    const void *key, *sign, *col, *val;
+    int32_t mem;
+    const void *dk = nullptr, *dsg = nullptr, *dc = nullptr, *dv = nullptr;
+  } C{eng, ncells, cell_key, sign, col, val, mem};
+  auto stage_cells = [](void* p) -> int32_t {
+    Cells& c = *static_cast<Cells*>(p);
+    JY_TRY(stage_begin(c.eng));
+    if (c.key) JY_TRY(jy_stage(c.eng, 3, c.key, c.n * 4, c.mem, &c.dk));
+    if (c.sign) JY_TRY(jy_stage(c.eng, 4, c.sign, c.n, c.mem, &c.dsg));
+    JY_TRY(jy_stage(c.eng, 5, c.col, c.n * 2, c.mem, &c.dc));
+    JY_TRY(jy_stage(c.eng, 6, c.val, c.n * 8, c.mem, &c.dv));
+    return stage_end(c.eng);
+  };
   void* ds;
   JY_TRY(jy_scratch(eng, 2, nkeys * 4, &ds));
   u64 created = 0;
   const double t1 = jy_tracing() ? jy_now_us() : 0;
   JY_TRY(jy_keydir_run(eng, type, nkeys, static_cast<const uint8_t*>(db), static_cast<const u64*>(dofs),
-                       static_cast<u32*>(ds), true, &created));
+                       static_cast<u32*>(ds), true, &created, stage_cells, &C));
+  const void *dk = C.dk, *dsg = C.dsg, *dc = C.dc, *dv = C.dv;
   const double t2 = jy_tracing() ? jy_now_us() : 0;
   JY_TRY(keys_created(eng, type, created));  // grows the slabs before the merge is enqueued
   JY_TRACE("converge_keys: staging %.1f us, directory %.1f us, %llu created", t1 - t0, t2 - t1,

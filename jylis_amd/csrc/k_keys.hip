@@ -342,8 +342,11 @@ void jy_keydir_free(jy_engine* eng, KeyDir& K) {
 // Device interning / lookup of n keys (device pointers).  Returns the number
 // of keys created in *created.  Synchronises (the host must know the new
 // key count before any call sizes work by it).
+// after_probe (optional) runs on the host once the probe is enqueued and
+// before the host waits for its counts: a caller stages its next inputs there
+// while the GPU probes
 int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, const u64* ko, u32* slots, bool create,
-                      u64* created) {
+                      u64* created, int32_t (*after_probe)(void*), void* arg) {
   *created = 0;
   if (n == 0) return JY_OK;
   if (n >= kIdxMask) return eng->fail(JY_ERANGE, "too many keys in one call");
@@ -363,9 +366,10 @@ int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, co
   LAUNCH(k_key_probe, n, I, dir_of(K), res, th, parts);
   hipLaunchKernelGGL(k_key_sum, dim3(1), dim3(kThreads), 0, eng->stream, parts, nb, counts);
   JY_HIP(eng, hipGetLastError());
+  if (after_probe) JY_TRY(after_probe(arg));  // (a pageable read-back below may block at once)
   u64 hc[3];
-  const double t0 = jy_tracing() ? jy_now_us() : 0;
   JY_HIP(eng, hipMemcpyAsync(hc, counts, 24, hipMemcpyDeviceToHost, eng->stream));
+  const double t0 = jy_tracing() ? jy_now_us() : 0;
   JY_HIP(eng, hipStreamSynchronize(eng->stream));
   JY_TRACE("keydir %llu keys: probe counts after %.1f us of waiting", (unsigned long long)n, jy_now_us() - t0);
   const u64 m = hc[0], mbytes = hc[1];
