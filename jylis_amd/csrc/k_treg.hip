@@ -222,9 +222,10 @@ __device__ __forceinline__ bool routed_get(const RoutedIn& R, u64 i, u32& s, u64
   return true;
 }
 
-// (Measured and dropped in round 3: four records per lane, each record loaded
-// together with its run's count, every record rewriting its ts word -- in-box
-// A/B of the routed TREG step 0.352 vs 0.341 ms.)
+// (Measured and dropped in round 3, in-box A/B of the routed TREG step: four
+// records per lane, each record loaded together with its run's count, every
+// record rewriting its ts word -- 0.352 vs 0.341 ms together; separately, the
+// ts rewrite 0.332 and four records per lane 0.333 vs 0.330 ms.)
 __global__ __launch_bounds__(kThreads) void k_treg_lww_routed(TregK K, RoutedIn R) {
   constexpr int U = 2;
   const u64 base = (u64)blockIdx.x * (kThreads * U) + (threadIdx.x >> 6) * (64 * U) + (threadIdx.x & 63);
