@@ -83,7 +83,8 @@ struct TregK {
   u64 clear_bytes;
   u32* dupn;     // duplicate list: count, then 32-B records {slot, ts, pre, lr}
   u64* dups;
-  u32* dupflag;  // host-mapped: set when a duplicate is pushed
+  u32* dupflag;  // host-mapped: [0] set when a duplicate is pushed, [1] when the list was full
+  u64 dup_cap;   // records the list holds
   // RepoTREG._deltas (SET path only)
   u64* pts;
   TVal* pval;
@@ -108,8 +109,15 @@ __device__ __forceinline__ void set_one(const TregK& K, u32 s, u64 t, u64 p, u64
   K.pval[s] = TVal{p, l};
 }
 
+// (the host's bound keeps the list from filling; a record past its capacity
+// is never written -- the overflow bit makes the next call fail loudly
+// instead of corrupting memory)
 __device__ __forceinline__ void push_dup(const TregK& K, u32 s, u64 t, u64 p, u64 l) {
   const u32 at = atomicAdd(K.dupn, 1u);
+  if ((u64)at >= K.dup_cap) {
+    if (K.dupflag) __hip_atomic_store(K.dupflag + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
   u64x2* r = reinterpret_cast<u64x2*>(K.dups + (u64)at * 4);
   r[0] = u64x2{(u64)s, t};
   r[1] = u64x2{p, l};
@@ -403,6 +411,7 @@ TregK state_of(jy_engine* eng) {
   K.dupn = t.dupn;
   K.dups = t.dups;
   K.dupflag = t.dupflag_dev;
+  K.dup_cap = t.dup_cap;
   return K;
 }
 
@@ -432,6 +441,13 @@ int32_t ring_note(jy_engine* eng, u64 n) {
   t.mn[at] = n;
   t.mcount++;
   t.pending_n += n;
+  return JY_OK;
+}
+
+int32_t overflow_check(jy_engine* eng) {
+  const TregState& t = eng->treg;
+  if (t.dupflag && __atomic_load_n(t.dupflag + 1, __ATOMIC_ACQUIRE) != 0)
+    return eng->fail(JY_ERANGE, "treg duplicate list overflowed (a bound was wrong): state may miss duplicates");
   return JY_OK;
 }
 
@@ -534,6 +550,7 @@ int32_t fold_now(jy_engine* eng) {
 int32_t claim_begin(jy_engine* eng, u64 n, u32 nblocks, TregK& K) {
   TregState& t = eng->treg;
   JY_TRY(flag_init(eng));
+  JY_TRY(overflow_check(eng));
   if (t.dup_bound + n > t.dup_cap && t.dup_cap) {
     // nothing pushed since the last fold (the flag is set by the pushing
     // kernel itself, and only launches still in flight may push): the list's
@@ -643,6 +660,8 @@ int32_t jy_treg_gather(jy_engine* eng, u64 n, const u32* slots, u64* ots, u64* o
   if (n == 0) return JY_OK;
   TregState& t = eng->treg;
   JY_TRY(fold_now(eng));
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));  // (the read-back waits for the stream anyway)
+  JY_TRY(overflow_check(eng));
   hipLaunchKernelGGL(k_treg_gather, dim3(blocks(n, kThreads)), dim3(kThreads), 0, eng->stream, t.ts, t.val, slots, n,
                      ots, opre, olr);
   JY_HIP(eng, hipGetLastError());
