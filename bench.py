@@ -53,8 +53,9 @@ def parse():
     ap.add_argument("--batches", type=int, default=4, help="distinct delta batches held in HBM")
     ap.add_argument("--cpu-keys", type=int, default=65536, help="cpu_baseline sample: keys (x replicas x 2)")
     ap.add_argument("--cpu-rounds", type=int, default=6, help="cpu_baseline sample: peer-batch rounds")
-    ap.add_argument("--cpu-threads", type=int, default=16,
-                    help="key-partitioned CPU baseline threads (the GPU box's CPU share); 1 = off")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="key-partitioned CPU baseline threads; 0 = every CPU this process may run on "
+                         "(cpu_share()); 1 = off")
     ap.add_argument("--cpu-keys-per-thread", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=None, help="per-launch HBM bytes from a PMC run (json)")
@@ -137,6 +138,24 @@ def cpu_baseline(args, seed):
             "host_cpus": os.cpu_count()}
 
 
+def cpu_share():
+    """CPUs this process may really use: its affinity set, capped by a cgroup
+    CPU quota if one is set (a GPU box shares its host: os.cpu_count() there
+    reports the whole machine) -> (threads, how it was found)"""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    how = f"sched_getaffinity {n} of os.cpu_count() {os.cpu_count()}"
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            q = max(1, int(int(quota) / int(period)))
+            if q < n:
+                n, how = q, how + f", cgroup cpu.max quota {quota}/{period}"
+    except (OSError, ValueError):
+        pass
+    return n, how
+
+
 def cpu_baseline_parallel(args, seed):
     """The stronger CPU baseline of SURVEY 8d: the oracle key-partitioned over
     `cpu_threads` threads, each converging its own partition's peer batches
@@ -148,6 +167,9 @@ def cpu_baseline_parallel(args, seed):
     import oracle as O
     from jylis_amd import synth as S
     T, kt, R, rounds = args.cpu_threads, args.cpu_keys_per_thread, args.replicas, 2
+    how = "--cpu-threads"
+    if T <= 0:
+        T, how = cpu_share()
     rids = S.replica_ids(R, seed)
     repos, batches = [], []
     for t in range(T):
@@ -178,7 +200,8 @@ def cpu_baseline_parallel(args, seed):
     cells = T * kt * R * 2 * rounds
     return {"value": cells / dt, "unit": "merges/s", "cores": T, "kind": "port",
             "sample": f"PNCOUNT {T} key partitions x {kt} keys x {R} replicas x 2 signs x {rounds} rounds of {R} "
-                      f"peer batches ({cells} cell merges, {dt:.2f} s, oracle/jy_oracle.cpp, {T} threads)"}
+                      f"peer batches ({cells} cell merges, {dt:.2f} s, oracle/jy_oracle.cpp, {T} threads)",
+            "threads_from": how, "host_cpus": os.cpu_count()}
 
 
 def _owner_seed(seed, owner):
@@ -345,7 +368,7 @@ def main():
     cpu = cpu_par = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, seed)
-        cpu_par = cpu_baseline_parallel(args, seed) if args.cpu_threads > 1 else None
+        cpu_par = cpu_baseline_parallel(args, seed) if args.cpu_threads != 1 else None
 
     line = {
         "metric": METRIC,
@@ -385,6 +408,28 @@ def main():
         dist.destroy_process_group()
 
 
+WATCHDOG_EXIT = 3
+
+
+def watchdog(limit, line, rank, key="routed"):
+    """A phase that may hang in a collective: after `limit` seconds rank 0
+    prints the line with an error under `key`, and every rank exits with
+    WATCHDOG_EXIT -- a hang is a failure, never a clean exit.  Cancel the
+    returned timer when the phase finished."""
+    import threading
+
+    def fire():
+        if rank == 0:
+            line[key] = {"error": f"{key} phase did not finish within {limit:.0f} s"}
+            print(json.dumps(line), flush=True)
+        os._exit(WATCHDOG_EXIT)
+
+    dog = threading.Timer(limit, fire)
+    dog.daemon = True
+    dog.start()
+    return dog
+
+
 XGMI_LINK_GBPS = 153.0  # per xGMI link and direction, nominal (MI355X: 7 links per GPU)
 
 
@@ -402,22 +447,11 @@ def routed_phase(args, eng, dev, dist, rank, world, routed, peer, fabric, cells_
     (N - 1) / N of the batch, as many bytes as the merge reads, so the step
     is bound by the links, not by HBM.  Timed apart from `value` with its own
     few steps; a watchdog prints the line without it if a collective hangs."""
-    import threading
-
     import torch
     from jylis_amd._lib import PNCOUNT
     from jylis_amd.route import CounterRouter
     limit = float(os.environ.get("JY_ROUTED_LIMIT_S", "240"))
-
-    def fire():
-        if rank == 0:
-            line["routed"] = {"error": f"routed phase did not finish within {limit:.0f} s"}
-            print(json.dumps(line), flush=True)
-        os._exit(0)
-
-    dog = threading.Timer(limit, fire)
-    dog.daemon = True
-    dog.start()
+    dog = watchdog(limit, line, rank)
     router = CounterRouter([eng], fabric, PNCOUNT)
     nbr = len(routed)
     warm, steps = 1, max(1, min(args.steps, 4))

@@ -52,6 +52,8 @@ typedef struct jy_engine jy_engine;
 /* jy_config.flags: test switches that force a kernel form the engine would
  * otherwise pick by state size (the parity tests reach every form) */
 #define JY_CFG_TREG_WHOLE_LINES 1u /* k_treg_lww<true>: every handle line rewritten */
+#define JY_CFG_TREG_DUP_TEST 2u    /* a fixed 64-record TREG duplicate list the host never folds
+                                      ahead of time: a test overflows it and expects JY_ERANGE */
 
 typedef struct jy_config {
   int32_t device;            /* HIP device ordinal                                   */
@@ -396,6 +398,100 @@ int32_t jy_ujson_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, c
                             uint64_t* hdr_dev, uint32_t* ovf_dev);
 int32_t jy_ujson_converge_routed(jy_engine* eng, uint32_t nsrc, uint64_t cap_k, uint64_t cap_e, uint64_t cap_v,
                                  uint64_t cap_c, const uint64_t* runs_dev);
+
+/* ---- the node: every GPU of one Jylis node behind one handle (jy_node.hip) ----
+ * Replaces, for the whole node, Database.converge_deltas (jylis/database.pony:50-51)
+ * -> RepoManager.converge_deltas -> RepoManagerCore.converge_deltas
+ * (jylis/repo_manager.pony:30-31,92-93): ONE call per decoded peer batch, its
+ * keys hash-sharded over the node's GPUs (owner = jy_key_owner(key, S)).  The
+ * reference has no sharding (every node holds every key); the exchange step
+ * is the intra-node analogue of Cluster.broadcast_deltas (cluster.pony:205-213).
+ *
+ * A node has S shards (one engine each).  One process may drive all of them
+ * (the Pony host: nlocal = S) or several processes one each (nlocal = 1,
+ * rank0 = the process's rank, one ncclUniqueId shared by all of them).
+ * Per converge call, per shard: the batch the process passed is cut into
+ * nlocal contiguous key ranges, one per local shard (its ingest); each ingest
+ * shard hashes its keys on the device and regroups keys and payload by owner;
+ * the per-owner counts are exchanged (RCCL, or a host transposition for the
+ * copy fabric) and read back once; the payload moves with grouped
+ * ncclSend/ncclRecv over xGMI (or device copies); each owner interns the keys
+ * it received in its device directory (_data_for, create on miss) and
+ * merges them -- TREG and counters all sources in one launch (LWW / max are
+ * joins, repeats are exact), TLOG and UJSON one source after another (a key
+ * two peers sent is merged twice, exactly).  No slot crosses the host and
+ * no key is resolved by a round trip: the key bytes travel with their delta.
+ *
+ * Every process of a multi-process node makes the same node calls in the
+ * same order (they are collectives), each with its own batch (possibly
+ * empty).  Errors: JY_* codes, detail in jy_node_last_error.  Reads, local
+ * writes and flushes go to the owner's engine (jy_node_engine). */
+typedef struct jy_node jy_node;
+#define JY_NODE_MAX_SHARDS 64
+#define JY_FABRIC_RCCL 0 /* RCCL communicator over the shards' GPUs (one GPU per shard)   */
+#define JY_FABRIC_COPY 1 /* device copies: one process, shards may share a GPU (tests)      */
+typedef struct jy_node_config {
+  uint32_t nshards;                     /* S: key shards of the node                        */
+  uint32_t nlocal;                      /* shards this process drives: rank0 .. rank0+nlocal-1 */
+  uint32_t rank0;                       /* first local shard                               */
+  uint32_t fabric;                      /* JY_FABRIC_*                                     */
+  int32_t devices[JY_NODE_MAX_SHARDS];  /* HIP device of each local shard                  */
+  uint8_t unique_id[128];               /* RCCL: one ncclUniqueId for every process of the
+                                           node (jy_node_unique_id on one of them); with
+                                           nlocal == nshards an all-zero id means "make one" */
+  jy_config engine;                     /* each shard's engine (device overridden)         */
+} jy_node_config;
+
+int32_t jy_node_unique_id(uint8_t* id_out /* 128 bytes */);
+int32_t jy_node_create(const jy_node_config* cfg, jy_node** out);
+void jy_node_destroy(jy_node* node);
+const char* jy_node_last_error(const jy_node* node);
+uint32_t jy_node_nshards(const jy_node* node);
+/* the engine of local shard `shard` (global index), NULL if not local */
+jy_engine* jy_node_engine(jy_node* node, uint32_t shard);
+uint32_t jy_node_shard_of(const jy_node* node, const uint8_t* key, uint64_t len);
+/* register a replica identity on every local shard (the same column on all:
+ * every process registers the cluster's identities in one order) */
+int32_t jy_node_replica_col(jy_node* node, uint64_t replica_id, uint32_t* col_out);
+int32_t jy_node_sync(jy_node* node);
+
+/* Converge one decoded peer batch (per process).  Keys: n strings (key_bytes,
+ * key_offs[n + 1]).  `mem` = JY_HOST (staged per ingest shard) or JY_DEVICE
+ * (readable by every local shard's GPU).  Offsets may start above 0.
+ *   counters: key i's cells are [cell_offs[i], cell_offs[i+1]) of (sign 0 = P /
+ *             1 = N, NULL: all P; col = jy_node_replica_col; val): s = max(s, val)
+ *   TREG:     (ts[i], value bytes [val_offs[i], val_offs[i+1]))
+ *   TLOG:     cutoff[i]; entries [ent_offs[i], ent_offs[i+1]) of (ts, value bytes
+ *             [val_offs[e], val_offs[e+1])), canonical order (as jy_tlog_converge)
+ *   UJSON:    as jy_ujson_converge, per document (dots carry node columns) */
+int32_t jy_node_counter_converge(jy_node* node, int32_t type, uint64_t n, const uint8_t* key_bytes,
+                                 const uint64_t* key_offs, const uint64_t* cell_offs, const uint8_t* sign,
+                                 const uint16_t* col, const uint64_t* val, int32_t mem);
+int32_t jy_node_treg_converge(jy_node* node, uint64_t n, const uint8_t* key_bytes, const uint64_t* key_offs,
+                              const uint64_t* ts, const uint8_t* val_bytes, const uint64_t* val_offs, int32_t mem);
+int32_t jy_node_tlog_converge(jy_node* node, uint64_t n, const uint8_t* key_bytes, const uint64_t* key_offs,
+                              const uint64_t* cutoff, const uint64_t* ent_offs, const uint64_t* ts,
+                              const uint8_t* val_bytes, const uint64_t* val_offs, int32_t mem);
+int32_t jy_node_ujson_converge(jy_node* node, uint64_t n, const uint8_t* key_bytes, const uint64_t* key_offs,
+                               const uint64_t* el_offs, const uint64_t* dots, const uint64_t* elems,
+                               const uint64_t* vv_offs, const uint64_t* vv, const uint64_t* cloud_offs,
+                               const uint64_t* cloud, int32_t mem);
+/* Dense counter blocks arriving MIXED (the bench's routed PNCOUNT step, and a
+ * peer that shards like this node: it flushes shard by shard).  This process
+ * ingests ncols peer columns for the keys of every owner: vals_p / vals_n
+ * are device arrays [ncols][S][nslots] (vals_n NULL for GCOUNT), block
+ * [c][d] holding owner d's slots [slot0, slot0 + nslots).  cols_all[r * ncols
+ * + c] is the column of shard r's c-th peer (every process passes the whole
+ * table).  Column c of every shard crosses in one exchange; the owner merges
+ * the S received columns with one block converge while column c + 1 is in
+ * flight on a second stream.  Device memory only. */
+int32_t jy_node_counter_converge_block(jy_node* node, int32_t type, uint32_t ncols, const uint16_t* cols_all,
+                                       uint32_t slot0, uint32_t nslots, const uint64_t* vals_p,
+                                       const uint64_t* vals_n);
+/* telemetry of the node's last converge call (not on the reference's
+ * surface): [0] keys ingested, [1] keys received, [2] bytes sent, [3] bytes
+ * received (this process's local shards), [4] exchange calls so far */
+int32_t jy_node_stats(jy_node* node, uint64_t* out5);
 
 #ifdef __cplusplus
 }

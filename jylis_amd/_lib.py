@@ -16,6 +16,7 @@ GCOUNT, PNCOUNT, TREG, TLOG, UJSON = 0, 1, 2, 3, 4
 TYPE_NAMES = {"GCOUNT": GCOUNT, "PNCOUNT": PNCOUNT, "TREG": TREG, "TLOG": TLOG, "UJSON": UJSON}
 HOST, DEVICE = 0, 1
 CFG_TREG_WHOLE_LINES = 1
+CFG_TREG_DUP_TEST = 2
 TLOG_INS, TLOG_TRIMAT, TLOG_TRIM, TLOG_CLR = 0, 1, 2, 3
 UJSON_INS, UJSON_RM, UJSON_CLR = 0, 1, 2
 
@@ -29,6 +30,22 @@ class JyConfig(C.Structure):
         ("key_capacity", C.c_uint64 * 5),
         ("entry_capacity", C.c_uint64 * 5),
         ("arena_capacity", C.c_uint64 * 5),
+    ]
+
+
+NODE_MAX_SHARDS = 64
+FABRIC_RCCL, FABRIC_COPY = 0, 1
+
+
+class JyNodeConfig(C.Structure):
+    _fields_ = [
+        ("nshards", C.c_uint32),
+        ("nlocal", C.c_uint32),
+        ("rank0", C.c_uint32),
+        ("fabric", C.c_uint32),
+        ("devices", C.c_int32 * NODE_MAX_SHARDS),
+        ("unique_id", C.c_uint8 * 128),
+        ("engine", JyConfig),
     ]
 
 
@@ -106,6 +123,21 @@ SIGNATURES = {
     "jy_ujson_route_part": (I32, [P, U64, P, P, P, U64, P, P, P, U64, P, P, U64, P, U32, U64, U64, U64, U64, U64,
                                   I32, P, P, P]),
     "jy_ujson_converge_routed": (I32, [P, U32, U64, U64, U64, U64, P]),
+    "jy_node_unique_id": (I32, [P]),
+    "jy_node_create": (I32, [P, P]),
+    "jy_node_destroy": (None, [P]),
+    "jy_node_last_error": (C.c_char_p, [P]),
+    "jy_node_nshards": (U32, [P]),
+    "jy_node_engine": (P, [P, U32]),
+    "jy_node_shard_of": (U32, [P, P, U64]),
+    "jy_node_replica_col": (I32, [P, U64, P]),
+    "jy_node_sync": (I32, [P]),
+    "jy_node_counter_converge": (I32, [P, I32, U64, P, P, P, P, P, P, I32]),
+    "jy_node_treg_converge": (I32, [P, U64, P, P, P, P, P, I32]),
+    "jy_node_tlog_converge": (I32, [P, U64, P, P, P, P, P, P, P, I32]),
+    "jy_node_ujson_converge": (I32, [P, U64, P, P, P, P, P, P, P, P, P, I32]),
+    "jy_node_counter_converge_block": (I32, [P, I32, U32, P, U32, U32, P, P]),
+    "jy_node_stats": (I32, [P, P]),
 }
 
 # include/jylis_host.h: the C++ host mirror (Database / RepoManagerCore / Repo*)

@@ -32,7 +32,7 @@ int32_t check_type(jy_engine* eng, int32_t type) {
 // before the stream-ordered free takes effect), so the host can enqueue the
 // next merge while the GPU runs the previous one.
 int32_t jy_dev_alloc(jy_engine* eng, void** p, u64 bytes, const char* what) {
-  hipError_t e = hipMallocAsync(p, bytes ? bytes : 8, eng->stream);
+  hipError_t e = hipMallocFromPoolAsync(p, bytes ? bytes : 8, eng->pool, eng->stream);
   if (e != hipSuccess) {
     *p = nullptr;
     return eng->fail(JY_ENOMEM, std::string(what) + " hipMallocAsync(" + std::to_string(bytes) + "): " +
@@ -266,14 +266,28 @@ int32_t jy_engine_create(const jy_config* cfg, jy_engine** out) {
   }
   eng->stream = eng->own_stream;
   {
-    // the stream-ordered allocator keeps what it frees: with the default
-    // release threshold (0) every synchronisation hands freed blocks back and
-    // the next growth of a scratch array re-maps memory (0.1-1 ms of host
-    // time inside a merge call, GPU idle meanwhile: round-3 UJSON trace)
-    hipMemPool_t pool;
-    if (hipDeviceGetDefaultMemPool(&pool, eng->device) == hipSuccess) {
-      uint64_t keep = UINT64_MAX;
-      hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    // The engine's own stream-ordered pool.  It keeps what it frees: with
+    // the default release threshold (0) every synchronisation hands freed
+    // blocks back and the next growth of a scratch array re-maps memory
+    // (0.1-1 ms of host time inside a merge call, GPU idle meanwhile:
+    // round-3 UJSON trace).  Being the engine's, what it keeps is not taken
+    // from torch's or RCCL's allocations (the device's default pool is shared
+    // by the whole process), and jy_engine_destroy returns all of it.
+    hipMemPoolProps props;
+    std::memset(&props, 0, sizeof(props));
+    props.allocType = hipMemAllocationTypePinned;
+    props.handleTypes = hipMemHandleTypeNone;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = eng->device;
+    uint64_t keep = UINT64_MAX;
+    if (hipMemPoolCreate(&eng->pool, &props) != hipSuccess ||
+        hipMemPoolSetAttribute(eng->pool, hipMemPoolAttrReleaseThreshold, &keep) != hipSuccess) {
+      std::fprintf(stderr, "jy_engine_create: hipMemPoolCreate failed\n");
+      if (eng->pool) hipMemPoolDestroy(eng->pool);
+      eng->pool = nullptr;
+      hipStreamDestroy(eng->own_stream);
+      delete eng;
+      return JY_EHIP;
     }
   }
   std::memset(eng->pin_total, 0, 64);
@@ -382,6 +396,8 @@ void jy_engine_destroy(jy_engine* eng) {
     hipEventDestroy(ev.second);
   }
   if (eng->total_ready) hipEventDestroy(eng->total_ready);
+  if (eng->stream) hipStreamSynchronize(eng->stream);  // the frees above have happened
+  if (eng->pool) hipMemPoolDestroy(eng->pool);          // everything it kept goes back
   if (eng->own_stream) hipStreamDestroy(eng->own_stream);
   delete eng;
 }
@@ -702,7 +718,17 @@ int32_t jy_counter_converge_keys(jy_engine* eng, int32_t type, uint64_t nkeys, c
   if (mem != JY_HOST && mem != JY_DEVICE) return eng->fail(JY_EINVAL, "mem must be JY_HOST or JY_DEVICE");
   if (!cell_key && ncells != nkeys) return eng->fail(JY_EINVAL, "without cell_key, cell i is key i: ncells == nkeys");
   if (type == JY_GCOUNT && sign) return eng->fail(JY_EINVAL, "GCOUNT cells have no sign");
-  if (nkeys == 0 || ncells == 0) return JY_OK;
+  if (nkeys == 0) return JY_OK;
+  if (ncells == 0) {
+    // keys with no cells are still created (_data_for, repo_gcount.pony:36-41)
+    if (mem == JY_DEVICE) {
+      void* ds;
+      JY_TRY(jy_scratch(eng, 2, nkeys * 4, &ds));
+      return jy_keys_intern_mem(eng, type, nkeys, kb, ko, static_cast<u32*>(ds), JY_DEVICE);
+    }
+    std::vector<u32> slots(nkeys);
+    return jy_keys_intern_mem(eng, type, nkeys, kb, ko, slots.data(), JY_HOST);
+  }
   const int which = type == JY_GCOUNT ? 0 : 1;
   if (mem == JY_HOST) {
     if (cell_key)
@@ -750,7 +776,7 @@ int32_t jy_counter_converge_keys(jy_engine* eng, int32_t type, uint64_t nkeys, c
            (unsigned long long)created);
   JY_TRACE("converge_keys: %llu keys, %llu cells: %.1f us after the host checks", (unsigned long long)nkeys,
            (unsigned long long)ncells, jy_now_us() - t0);
-  return jy_counter_coo_keyed(eng, which, ncells, static_cast<const u32*>(ds), static_cast<const u32*>(dk),
+  return jy_counter_coo_keyed(eng, which, ncells, nkeys, static_cast<const u32*>(ds), static_cast<const u32*>(dk),
                               static_cast<const uint8_t*>(dsg), static_cast<const u16*>(dc),
                               static_cast<const u64*>(dv));
 }
@@ -1028,7 +1054,10 @@ int32_t jy_treg_read(jy_engine* eng, uint64_t n, const uint32_t* slots, uint64_t
   JY_HIP(eng, hipMemcpyAsync(pre, d + n, n * 8, hipMemcpyDeviceToHost, eng->stream));
   JY_HIP(eng, hipMemcpyAsync(lr, d + 2 * n, n * 8, hipMemcpyDeviceToHost, eng->stream));
   JY_HIP(eng, hipStreamSynchronize(eng->stream));
-  return JY_OK;
+  // every launch before this read has finished: an overflow of the
+  // duplicate list fails the read (the outputs are written, but may miss an
+  // update that was dropped)
+  return jy_treg_overflow_check(eng);
 }
 
 }  // extern "C"

@@ -55,6 +55,22 @@ __device__ __forceinline__ int jy_value_cmp(u64 pa, u64 la, u64 pb, u64 lb, cons
   return na < nb ? -1 : 1;
 }
 
+// include/jylis_gpu.h jy_key_owner on the device: FNV-1a 64 over the key
+// bytes, splitmix64 finaliser, mod S (the node's key sharding)
+__device__ __forceinline__ u32 jy_dev_key_owner(const uint8_t* __restrict__ p, u64 len, u32 S) {
+  u64 h = 0xCBF29CE484222325ull;
+  for (u64 i = 0; i < len; i++) {
+    h ^= p[i];
+    h *= 0x100000001B3ull;
+  }
+  h ^= h >> 30;
+  h *= 0xBF58476D1CE4E5B9ull;
+  h ^= h >> 27;
+  h *= 0x94D049BB133111EBull;
+  h ^= h >> 31;
+  return (u32)(h % S);
+}
+
 // adds the number of active lanes with f to *c: one atomic per wave (a
 // same-address atomic per lane serialises at L2, ~15 ns each)
 __device__ __forceinline__ void jy_wave_count(bool f, unsigned long long* c) {
@@ -365,6 +381,7 @@ struct jy_engine {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t own_stream = nullptr;
+  hipMemPool_t pool = nullptr;  // the engine's stream-ordered pool (jy_dev_alloc)
   std::string err;
   u64 skipped_host = 0;
   u64* skipped_dev = nullptr;  // device counter of skipped entries
@@ -522,7 +539,7 @@ int32_t jy_realloc(jy_engine* eng, void** p, u64 old_bytes, u64 new_bytes, bool 
 // kernel-side entry points (k_*.hip)
 int32_t jy_counter_grow(jy_engine* eng, int which, u32 need_cols, u64 need_slots);
 int32_t jy_counter_coo(jy_engine* eng, int which, int sign, u64 n, const u32* slot, const u16* col, const u64* val);
-int32_t jy_counter_coo_keyed(jy_engine* eng, int which, u64 n, const u32* kslot, const u32* cell_key,
+int32_t jy_counter_coo_keyed(jy_engine* eng, int which, u64 n, u64 nkeys, const u32* kslot, const u32* cell_key,
                              const uint8_t* sign, const u16* col, const u64* val);
 int32_t jy_counter_block(jy_engine* eng, int which, u32 ncols, const u16* cols_dev, u32 slot0, u32 nslots,
                          const u64* vals_p, const u64* vals_n);
@@ -536,6 +553,8 @@ int32_t jy_cnt_pending(jy_engine* eng, int which, u64* count_host);
 int32_t jy_treg_grow(jy_engine* eng, u64 need_slots);
 int32_t jy_treg_merge(jy_engine* eng, u64 n, const u32* slot, const u64* ts, const u64* pre, const u64* lr);
 int32_t jy_treg_gather(jy_engine* eng, u64 n, const u32* slots, u64* ts, u64* pre, u64* lr);
+// JY_ERANGE once a duplicate list overflowed (sticky: the state may miss an update)
+int32_t jy_treg_overflow_check(jy_engine* eng);
 // routed runs: S sources x cap records (slot, ts, pre, lr'), counts in hdr
 // (device, 2 u64 per source); source src's value bytes at arena offset
 // rebase + src * cap_byte

@@ -1,0 +1,1333 @@
+// jy_node.hip -- the node: every GPU of one Jylis node behind one handle.
+//
+// Boundary (include/jylis_gpu.h, "the node"): one call per decoded peer batch
+// replaces Database.converge_deltas (jylis/database.pony:50-51) ->
+// RepoManager.converge_deltas -> RepoManagerCore.converge_deltas
+// (jylis/repo_manager.pony:30-31,92-93) for the whole node.  Keys are
+// hash-sharded over S engines (owner = jy_key_owner(key, S)); the
+// reference holds every key on every node, so the exchange below has no
+// counterpart there -- it is the intra-node analogue of
+// Cluster.broadcast_deltas (cluster.pony:205-213).
+//
+// One converge call, per local shard (the batch cut into nlocal key ranges):
+//
+//   ingest     the shard's key range (staged through pinned memory, or in HBM)
+//              is hashed on the device (k_nd_owner), stably partitioned by
+//              owner (k_nd_count, a column-major look-back scan, k_nd_place:
+//              no same-address global atomics), and every wire column is
+//              written in owner order: key lengths and bytes, the per-key
+//              columns, and each CSR level of the payload (TLOG entries and
+//              their long value bytes, UJSON elements / vv / cloud, counter
+//              cells) -- k_nd_seg_lens + scan + k_nd_seg_copy.  A value longer
+//              than 8 bytes travels as its bytes in 8-byte granules; its
+//              8-byte prefix and length travel as words (k_nd_val_head).
+//   counts     per destination and granule (keys, key bytes, level elements),
+//              exchanged with grouped ncclSend/ncclRecv (or transposed on the
+//              host for the copy fabric) and read back: the one host
+//              synchronisation of the exchange.  Sizes are exact: no fixed
+//              capacities, no overflow rounds.
+//   exchange   grouped ncclSend/ncclRecv of every wire column, source-major
+//              into one receive buffer per column (RCCL over xGMI), or
+//              device copies (JY_FABRIC_COPY: one process, shards may share a
+//              GPU -- the single-GPU tests of the multi-shard path).
+//   owner      the received keys are interned in the shard's device directory
+//              (_data_for, repo_*.pony: create on miss); the received value
+//              bytes are appended to its arena and their handles rebuilt; then
+//              the engine's own merge kernels run: TREG (k_treg) and counters
+//              (k_coo_max_keyed) over all sources at once -- LWW and max are
+//              joins, a key two sources sent is exact -- TLOG (k_tlog) and
+//              UJSON (k_ujson) one source after another (their device batches
+//              name a key once).
+//
+// Roofline: the exchange moves (S - 1) / S of the batch over xGMI (7 links x
+// ~153 GB/s per GPU at S = 8) and the ingest regroup reads the batch once and
+// writes it once in HBM; the merges are the engine's.
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <type_traits>
+#include <vector>
+
+#include "jy_dscan.hpp"
+#include "jy_internal.hpp"
+
+namespace {
+
+constexpr int kT = 256;
+constexpr u32 kMaxS = JY_NODE_MAX_SHARDS;
+constexpr int kMaxLvl = 3;           // CSR levels of a payload (UJSON: elements, vv, cloud)
+constexpr int kMaxW = 2 + kMaxLvl;   // count granules: keys, key bytes, one per level
+
+u32 grid_of(u64 n) { return (u32)std::max<u64>(1, (n + kT - 1) / kT); }
+u64 round8(u64 x) { return (x + 7) & ~7ull; }
+
+// ---------------------------------------------------------------------------
+// kernels: ingest
+
+__global__ __launch_bounds__(kT) void k_nd_owner(const uint8_t* __restrict__ kb, const u64* __restrict__ ko, u64 obase,
+                                                 u64 n, u32 S, u32* __restrict__ owner) {
+  const u64 i = (u64)blockIdx.x * kT + threadIdx.x;
+  if (i >= n) return;
+  const u64 a = ko[i];
+  owner[i] = jy_dev_key_owner(kb + (a - obase), ko[i + 1] - a, S);
+}
+
+// per tile of kT items: items per owner (one LDS atomic per wave and owner)
+__global__ __launch_bounds__(kT) void k_nd_count(const u32* __restrict__ owner, u64 n, u32 S, u64* __restrict__ tcnt) {
+  __shared__ unsigned long long lc[kMaxS];
+  for (u32 j = threadIdx.x; j < S; j += kT) lc[j] = 0;
+  __syncthreads();
+  const u64 i = (u64)blockIdx.x * kT + threadIdx.x;
+  const bool valid = i < n;
+  const u32 o = valid ? owner[i] : 0u;
+  u64 pending = __ballot(valid);
+  while (pending) {
+    const int leader = __ffsll((unsigned long long)pending) - 1;
+    const u32 d = __shfl(o, leader);
+    const u64 m = __ballot(valid && o == d);
+    if (__lane_id() == (u32)leader) atomicAdd(&lc[d], (unsigned long long)__popcll(m));
+    pending &= ~m;
+  }
+  __syncthreads();
+  u64* row = tcnt + (u64)blockIdx.x * S;
+  for (u32 j = threadIdx.x; j < S; j += kT) row[j] = lc[j];
+}
+
+// after the column-major exclusive scan of tcnt: where every owner's items
+// begin in owner order (kbeg[S] = n)
+__global__ void k_nd_kbeg(const u64* __restrict__ tcnt, u64 ntiles, u32 S, u64* __restrict__ kbeg) {
+  const u32 d = threadIdx.x;
+  if (d < S) kbeg[d] = tcnt[d];
+  if (d == S) kbeg[S] = tcnt[ntiles * S];
+}
+
+// stable placement: perm[position in owner order] = input index
+__global__ __launch_bounds__(kT) void k_nd_place(const u32* __restrict__ owner, u64 n, u32 S,
+                                                 const u64* __restrict__ tcnt, u32* __restrict__ perm) {
+  __shared__ u32 wt[kT / 64][kMaxS];
+  for (u32 j = threadIdx.x; j < S; j += kT)
+#pragma unroll
+    for (int w = 0; w < kT / 64; w++) wt[w][j] = 0;
+  __syncthreads();
+  const u64 i = (u64)blockIdx.x * kT + threadIdx.x;
+  const int lane = __lane_id(), wv = threadIdx.x >> 6;
+  const bool valid = i < n;
+  const u32 o = valid ? owner[i] : 0u;
+  u32 rk = 0;
+  u64 pending = __ballot(valid);
+  while (pending) {
+    const int leader = __ffsll((unsigned long long)pending) - 1;
+    const u32 d = __shfl(o, leader);
+    const bool mine = valid && o == d;
+    const u64 m = __ballot(mine);
+    if (mine) rk = (u32)__popcll(m & ((1ull << lane) - 1));
+    if (lane == leader) wt[wv][d] = (u32)__popcll(m);
+    pending &= ~m;
+  }
+  __syncthreads();
+  if (!valid) return;
+  u64 p = tcnt[(u64)blockIdx.x * S + o] + rk;
+  for (int w = 0; w < wv; w++) p += wt[w][o];
+  perm[p] = (u32)i;
+}
+
+// segments of an item: [start, start + len) copied into plen >= len slots
+// (the tail zero).  SegCsr: a CSR level (offs indexed by item, minus obase).
+// SegLong: a value's bytes when it is longer than 8 (else nothing), padded to
+// 8-byte granules (the receiver's arena keeps long values on granules).
+struct SegCsr {
+  const u64* offs;
+  u64 obase;
+  __device__ __forceinline__ void get(u64 i, u64& start, u64& len, u64& plen) const {
+    const u64 a = offs[i];
+    start = a - obase;
+    len = plen = offs[i + 1] - a;
+  }
+};
+struct SegLong {
+  const u64* offs;
+  u64 obase;
+  __device__ __forceinline__ void get(u64 i, u64& start, u64& len, u64& plen) const {
+    const u64 a = offs[i], l = offs[i + 1] - a;
+    start = a - obase;
+    len = l > 8 ? l : 0;
+    plen = l > 8 ? (l + 7) & ~7ull : 0;
+  }
+};
+
+// output item j's segment length (item perm[j]); lens[n] = 0 for the scan
+template <class Seg>
+__global__ __launch_bounds__(kT) void k_nd_seg_lens(u64 n, const u32* __restrict__ perm, Seg sg, u64* __restrict__ lens) {
+  const u64 j = (u64)blockIdx.x * kT + threadIdx.x;
+  if (j > n) return;
+  if (j == n) {
+    lens[n] = 0;
+    return;
+  }
+  u64 st, len, plen;
+  sg.get(perm[j], st, len, plen);
+  lens[j] = plen;
+}
+
+// column readers of the payload
+template <int N>
+struct InU64 {
+  const u64* p[N];
+  __device__ __forceinline__ u64 get(int c, u64 k) const { return p[c][k]; }
+};
+struct InBytes {
+  const uint8_t* p;
+};
+// counter cells: (sign << 16 | col) and the value, so every column is a word
+struct InCells {
+  const uint8_t* sign;
+  const u16* col;
+  const u64* val;
+  __device__ __forceinline__ u64 get(int c, u64 k) const {
+    if (c == 1) return val[k];
+    return ((u64)(sign ? sign[k] : 0) << 16) | col[k];
+  }
+};
+
+// output item j (thread): its segment copied to newoffs[j]; esrc (optional)
+// gets each copied element's source index (the next level's item index)
+template <int N, class In, class Seg>
+__global__ __launch_bounds__(kT) void k_nd_seg_copy(u64 n, const u32* __restrict__ perm, Seg sg,
+                                                    const u64* __restrict__ newoffs, In in, u64* o0, u64* o1, u64* o2,
+                                                    u32* __restrict__ esrc) {
+  const u64 j = (u64)blockIdx.x * kT + threadIdx.x;
+  if (j >= n) return;
+  u64 st, len, plen;
+  sg.get(perm[j], st, len, plen);
+  u64* out[3] = {o0, o1, o2};
+  const u64 d = newoffs[j];
+  for (u64 r = 0; r < len; r++) {
+#pragma unroll
+    for (int c = 0; c < N; c++) out[c][d + r] = in.get(c, st + r);
+    if (esrc) esrc[d + r] = (u32)(st + r);
+  }
+}
+
+template <class Seg>
+__global__ __launch_bounds__(kT) void k_nd_seg_bytes(u64 n, const u32* __restrict__ perm, Seg sg,
+                                                     const u64* __restrict__ newoffs, const uint8_t* __restrict__ in,
+                                                     uint8_t* __restrict__ out) {
+  const u64 j = (u64)blockIdx.x * kT + threadIdx.x;
+  if (j >= n) return;
+  u64 st, len, plen;
+  sg.get(perm[j], st, len, plen);
+  const u64 d = newoffs[j];
+  for (u64 r = 0; r < plen; r++) out[d + r] = r < len ? in[st + r] : 0;
+}
+
+// per-key word columns in owner order
+template <int N>
+__global__ __launch_bounds__(kT) void k_nd_perm(u64 n, const u32* __restrict__ perm, InU64<N> in, u64* o0, u64* o1,
+                                                u64* o2) {
+  const u64 j = (u64)blockIdx.x * kT + threadIdx.x;
+  if (j >= n) return;
+  const u32 i = perm[j];
+  u64* out[3] = {o0, o1, o2};
+#pragma unroll
+  for (int c = 0; c < N; c++) out[c][j] = in.get(c, i);
+}
+
+// a value's 8-byte big-endian prefix (zero padded) and its length, item perm[j]
+__global__ __launch_bounds__(kT) void k_nd_val_head(u64 n, const u32* __restrict__ perm, const u64* __restrict__ vo,
+                                                    u64 vbase, const uint8_t* __restrict__ vb, u64* __restrict__ pre,
+                                                    u64* __restrict__ vlen) {
+  const u64 j = (u64)blockIdx.x * kT + threadIdx.x;
+  if (j >= n) return;
+  const u32 i = perm[j];
+  const u64 a = vo[i], l = vo[i + 1] - a;
+  const uint8_t* p = vb + (a - vbase);
+  u64 x = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) x = (x << 8) | (u64)((u64)q < l ? p[q] : 0);
+  pre[j] = x;
+  vlen[j] = l;
+}
+
+// per destination d and granule: keys, key bytes, then the elements of each
+// level (a level's items are the keys or the elements of its parent level)
+struct LvlArgs {
+  const u64* offs[kMaxLvl];  // owner-order offsets over the parent's items
+  int parent[kMaxLvl];       // -1: keys
+  u32 nl;
+};
+__global__ void k_nd_counts(u32 S, const u64* __restrict__ kbeg, const u64* __restrict__ kofs, LvlArgs L,
+                            u64* __restrict__ cnt) {
+  const u32 d = threadIdx.x;
+  if (d >= S) return;
+  const u32 W = 2 + L.nl;
+  const u64 klo = kbeg[d], khi = kbeg[d + 1];
+  cnt[d * W + 0] = khi - klo;
+  cnt[d * W + 1] = kofs[khi] - kofs[klo];
+  u64 lo[kMaxLvl], hi[kMaxLvl];
+  for (u32 l = 0; l < L.nl; l++) {
+    const int p = L.parent[l];
+    const u64 plo = p < 0 ? klo : lo[p], phi = p < 0 ? khi : hi[p];
+    lo[l] = L.offs[l][plo];
+    hi[l] = L.offs[l][phi];
+    cnt[d * W + 2 + l] = hi[l] - lo[l];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// kernels: owner side
+
+// per-source local CSR offsets (the engine's merges take batches whose
+// offsets start at 0): out[kb[s] + s + j] = offs[kb[s] + j] - offs[kb[s]]
+struct SrcRanges {
+  u64 kb[kMaxS + 1];
+  u32 S;
+};
+__global__ __launch_bounds__(kT) void k_nd_local_offs(const u64* __restrict__ offs, u64 n, SrcRanges R,
+                                                      u64* __restrict__ out) {
+  const u64 t = (u64)blockIdx.x * kT + threadIdx.x;
+  if (t >= n + R.S) return;
+  u32 s = R.S - 1;
+  while (s > 0 && t < R.kb[s] + s) s--;
+  const u64 j = t - R.kb[s] - s;
+  out[t] = offs[R.kb[s] + j] - offs[R.kb[s]];
+}
+
+__global__ __launch_bounds__(kT) void k_nd_plen(u64 n, const u64* __restrict__ vlen, u64* __restrict__ plen) {
+  const u64 j = (u64)blockIdx.x * kT + threadIdx.x;
+  if (j > n) return;
+  const u64 l = j < n ? vlen[j] : 0;
+  plen[j] = l > 8 ? (l + 7) & ~7ull : 0;
+}
+
+// value handles in the owner's arena: long values at rebase + their offset in
+// the received byte block (granule aligned), short ones by length alone
+__global__ __launch_bounds__(kT) void k_nd_lr(u64 n, const u64* __restrict__ vlen, const u64* __restrict__ voff,
+                                              u64 rebase, u64* __restrict__ lr) {
+  const u64 j = (u64)blockIdx.x * kT + threadIdx.x;
+  if (j >= n) return;
+  const u64 l = vlen[j] & JY_LR_LEN_MASK;
+  lr[j] = l > 8 ? ((rebase + voff[j]) << JY_LR_LEN_BITS) | l : l;
+}
+
+__global__ __launch_bounds__(kT) void k_nd_cells(u64 n, const u64* __restrict__ packed, uint8_t* __restrict__ sign,
+                                                 u16* __restrict__ col) {
+  const u64 j = (u64)blockIdx.x * kT + threadIdx.x;
+  if (j >= n) return;
+  const u64 w = packed[j];
+  sign[j] = (uint8_t)(w >> 16);
+  col[j] = (u16)w;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// host side
+
+namespace {
+
+// node-owned device buffers (hipMalloc: RCCL may address them from a peer in
+// one process; the engines' stream-ordered pools are not peer-mapped)
+enum Buf {
+  B_OWNER, B_PERM, B_TCNT, B_KBEG, B_CNT, B_KLEN, B_KOFF, B_KBYTES, B_F0, B_F1, B_F2,
+  B_LLEN0, B_LLEN1, B_LLEN2, B_LOFF0, B_LOFF1, B_LOFF2,
+  B_LC00, B_LC01, B_LC10, B_LC11, B_LC20, B_LC21, B_ESRC,
+  R_KLEN, R_KBYTES, R_F0, R_F1, R_F2, R_LC00, R_LC01, R_LC10, R_LC11, R_LC20, R_LC21,
+  R_KOFF, R_SLOTS, R_LOFF0, R_LOFF1, R_LOFF2, R_LOC0, R_LOC1, R_LOC2, R_PLEN, R_VOFF, R_LR, R_AUX0, R_AUX1, R_AUX2,
+  X_BUF0, X_BUF1,
+  kNumBufs
+};
+
+struct NdBuf {
+  void* p = nullptr;
+  u64 bytes = 0;
+};
+
+struct NdShard {
+  u32 rank = 0;
+  int dev = 0;
+  jy_engine* eng = nullptr;
+  ncclComm_t comm = nullptr;
+  hipStream_t xs = nullptr;    // exchange stream of the block converge
+  hipEvent_t ev_in = nullptr;  // this shard's send columns are ready (copy fabric)
+  hipEvent_t ev_out = nullptr; // this shard's receives have landed (copy fabric)
+  hipEvent_t ev_x[2] = {nullptr, nullptr}, ev_m[2] = {nullptr, nullptr};
+  NdBuf b[kNumBufs];
+  u64* pin = nullptr;  // pinned: [2][kMaxS][kMaxW] send / recv counts, then 16 words of readbacks
+  // the current call's sizes
+  u64 n = 0;                 // keys ingested
+  u64 tot[kMaxW] = {};       // elements per granule ingested (send side), upper bounds
+  u64 rtot[kMaxW] = {};      // received per granule
+};
+
+}  // namespace
+
+struct jy_node {
+  jy_node_config cfg;
+  u32 S = 0, nlocal = 0, rank0 = 0, fabric = JY_FABRIC_RCCL;
+  std::vector<NdShard> sh;
+  std::string err;
+  u64 stats[5] = {};
+  int32_t fail(int32_t code, const std::string& m) {
+    err = m;
+    return code;
+  }
+};
+
+namespace {
+
+#define ND_HIP(nd, call)                                                                                  \
+  do {                                                                                                    \
+    hipError_t e_ = (call);                                                                               \
+    if (e_ != hipSuccess) return (nd)->fail(JY_EHIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+#define ND_NCCL(nd, call)                                                                                     \
+  do {                                                                                                        \
+    ncclResult_t r_ = (call);                                                                                 \
+    if (r_ != ncclSuccess) return (nd)->fail(JY_EHIP, std::string(#call) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+// an engine call inside a node call: its error becomes the node's
+#define ND_ENG(nd, sh, expr)                                                    \
+  do {                                                                          \
+    int32_t rc_ = (expr);                                                       \
+    if (rc_ != JY_OK) return (nd)->fail(rc_, std::string("shard ") +            \
+                                                 std::to_string((sh).rank) + ": " + (sh).eng->err); \
+  } while (0)
+
+int32_t buf(jy_node* nd, NdShard& sh, int idx, u64 bytes, void** out) {
+  NdBuf& b = sh.b[idx];
+  if (b.bytes < bytes || !b.p) {
+    ND_HIP(nd, hipSetDevice(sh.dev));
+    // growth: whatever still reads the old buffer has to finish
+    ND_HIP(nd, hipStreamSynchronize(sh.eng->stream));
+    if (sh.xs) ND_HIP(nd, hipStreamSynchronize(sh.xs));
+    if (b.p) ND_HIP(nd, hipFree(b.p));
+    b.p = nullptr;
+    b.bytes = 0;
+    const u64 nb = std::max<u64>(((bytes + bytes / 4) + 4095) & ~4095ull, 4096);
+    ND_HIP(nd, hipMalloc(&b.p, nb));
+    b.bytes = nb;
+  }
+  *out = b.p;
+  return JY_OK;
+}
+template <class T>
+int32_t bufT(jy_node* nd, NdShard& sh, int idx, u64 count, T** out) {
+  void* p;
+  JY_TRY(buf(nd, sh, idx, count * sizeof(T), &p));
+  *out = static_cast<T*>(p);
+  return JY_OK;
+}
+
+// two words read back from device (or host) memory: a CSR's first and last offset
+int32_t read2(jy_node* nd, NdShard& sh, const u64* a, const u64* b, int32_t mem, u64& x, u64& y) {
+  if (mem == JY_HOST) {
+    x = *a;
+    y = *b;
+    return JY_OK;
+  }
+  u64* pw = sh.pin + 2 * kMaxS * kMaxW;
+  ND_HIP(nd, hipMemcpyAsync(pw, a, 8, hipMemcpyDefault, sh.eng->stream));
+  ND_HIP(nd, hipMemcpyAsync(pw + 1, b, 8, hipMemcpyDefault, sh.eng->stream));
+  ND_HIP(nd, hipStreamSynchronize(sh.eng->stream));
+  x = pw[0];
+  y = pw[1];
+  return JY_OK;
+}
+
+// ---- a CSR level of the ingest: item offsets (n_items + 1, relative to the
+// staged elements by obase) and its element columns
+struct Level {
+  const u64* offs = nullptr;  // device, indexed by item (relative)
+  u64 obase = 0;              // subtracted from offs to index the staged columns
+  u64 nel = 0;                // elements of this chunk (upper bound for SegLong)
+  int parent = -1;            // -1: items are keys; else the level whose elements they are
+  bool longval = false;       // items' value bytes (SegLong) instead of a CSR of words
+};
+
+struct Ingest {
+  // keys of the chunk
+  const uint8_t* kb = nullptr;
+  const u64* ko = nullptr;
+  u64 kobase = 0, nkb = 0;
+};
+
+// owners, the stable partition and the key columns (lens, offsets, bytes)
+int32_t ingest_keys(jy_node* nd, NdShard& sh, const Ingest& in) {
+  jy_engine* eng = sh.eng;
+  const u64 n = sh.n, S = nd->S;
+  const u64 nt = std::max<u64>(1, (n + kT - 1) / kT);
+  u32 *owner, *perm;
+  u64 *tcnt, *kbeg, *klen, *koff;
+  uint8_t* kbytes;
+  JY_TRY(bufT(nd, sh, B_OWNER, std::max<u64>(n, 1), &owner));
+  JY_TRY(bufT(nd, sh, B_PERM, std::max<u64>(n, 1), &perm));
+  JY_TRY(bufT(nd, sh, B_TCNT, nt * S + 1, &tcnt));
+  JY_TRY(bufT(nd, sh, B_KBEG, S + 1, &kbeg));
+  JY_TRY(bufT(nd, sh, B_KLEN, n + 1, &klen));
+  JY_TRY(bufT(nd, sh, B_KOFF, n + 1, &koff));
+  JY_TRY(bufT(nd, sh, B_KBYTES, std::max<u64>(in.nkb, 1), &kbytes));
+  if (n == 0) {
+    ND_HIP(nd, hipMemsetAsync(kbeg, 0, (S + 1) * 8, eng->stream));
+    ND_HIP(nd, hipMemsetAsync(koff, 0, 8, eng->stream));
+    return JY_OK;
+  }
+  hipLaunchKernelGGL(k_nd_owner, dim3(grid_of(n)), dim3(kT), 0, eng->stream, in.kb, in.ko, in.kobase, n, (u32)S, owner);
+  hipLaunchKernelGGL(k_nd_count, dim3((u32)nt), dim3(kT), 0, eng->stream, (const u32*)owner, n, (u32)S, tcnt);
+  ND_HIP(nd, hipGetLastError());
+  ND_ENG(nd, sh, (jydscan::scan<jydscan::OpSum, false>(eng, nt * S + 1, jydscan::LdColMajor{tcnt, nt, S},
+                                                       jydscan::StColMajor{tcnt, nt, S})));
+  hipLaunchKernelGGL(k_nd_kbeg, dim3(1), dim3(128), 0, eng->stream, (const u64*)tcnt, nt, (u32)S, kbeg);
+  hipLaunchKernelGGL(k_nd_place, dim3((u32)nt), dim3(kT), 0, eng->stream, (const u32*)owner, n, (u32)S,
+                     (const u64*)tcnt, perm);
+  const SegCsr ks{in.ko, in.kobase};
+  hipLaunchKernelGGL(k_nd_seg_lens<SegCsr>, dim3(grid_of(n + 1)), dim3(kT), 0, eng->stream, n, (const u32*)perm, ks,
+                     klen);
+  ND_HIP(nd, hipGetLastError());
+  ND_ENG(nd, sh, jy_scan_u64(eng, klen, koff, n));
+  hipLaunchKernelGGL(k_nd_seg_bytes<SegCsr>, dim3(grid_of(n)), dim3(kT), 0, eng->stream, n, (const u32*)perm, ks,
+                     (const u64*)koff, in.kb, kbytes);
+  ND_HIP(nd, hipGetLastError());
+  return JY_OK;
+}
+
+// the counts of every destination and granule (device [S][W] at B_CNT)
+int32_t ingest_counts(jy_node* nd, NdShard& sh, const Level* L, u32 nl) {
+  u64* cnt;
+  JY_TRY(bufT(nd, sh, B_CNT, 2 * kMaxS * kMaxW, &cnt));
+  LvlArgs A{};
+  A.nl = nl;
+  for (u32 l = 0; l < nl; l++) {
+    A.offs[l] = static_cast<const u64*>(sh.b[B_LOFF0 + l].p);
+    A.parent[l] = L[l].parent;
+  }
+  hipLaunchKernelGGL(k_nd_counts, dim3(1), dim3(kMaxS), 0, sh.eng->stream, nd->S,
+                     (const u64*)sh.b[B_KBEG].p, (const u64*)sh.b[B_KOFF].p, A, cnt);
+  ND_HIP(nd, hipGetLastError());
+  return JY_OK;
+}
+
+// one level in owner order: lengths, offsets and (for word levels) its
+// columns through `in`; `items` = the parent's output items, `perm` maps them
+// to input items (keys: B_PERM; a nested level: the parent's element sources)
+template <int N, class In>
+int32_t ingest_level(jy_node* nd, NdShard& sh, u32 l, const Level& L, u64 items, const u32* perm, const In& in,
+                     bool want_src) {
+  jy_engine* eng = sh.eng;
+  u64 *len, *off;
+  JY_TRY(bufT(nd, sh, B_LLEN0 + l, items + 1, &len));
+  JY_TRY(bufT(nd, sh, B_LOFF0 + l, items + 1, &off));
+  const u64 cap = L.longval ? round8(L.nel) + 8 * items : L.nel;  // padded bytes bound
+  sh.tot[2 + l] = cap;
+  void* unused;
+  if (items == 0) {
+    ND_HIP(nd, hipMemsetAsync(off, 0, 8, eng->stream));
+    for (int c = 0; c < N; c++) JY_TRY(buf(nd, sh, B_LC00 + 2 * l + c, 8, &unused));
+    if (want_src) JY_TRY(buf(nd, sh, B_ESRC, 8, &unused));
+    return JY_OK;
+  }
+  if constexpr (std::is_same<In, InBytes>::value) {
+    const SegLong sg{L.offs, L.obase};
+    hipLaunchKernelGGL(k_nd_seg_lens<SegLong>, dim3(grid_of(items + 1)), dim3(kT), 0, eng->stream, items, perm, sg, len);
+    ND_HIP(nd, hipGetLastError());
+    ND_ENG(nd, sh, jy_scan_u64(eng, len, off, items));
+    uint8_t* o;
+    JY_TRY(bufT(nd, sh, B_LC00 + 2 * l, std::max<u64>(cap, 1), &o));
+    hipLaunchKernelGGL(k_nd_seg_bytes<SegLong>, dim3(grid_of(items)), dim3(kT), 0, eng->stream, items, perm, sg,
+                       (const u64*)off, in.p, o);
+    ND_HIP(nd, hipGetLastError());
+    return JY_OK;
+  } else {
+    const SegCsr sg{L.offs, L.obase};
+    hipLaunchKernelGGL(k_nd_seg_lens<SegCsr>, dim3(grid_of(items + 1)), dim3(kT), 0, eng->stream, items, perm, sg,
+                       len);
+    ND_HIP(nd, hipGetLastError());
+    ND_ENG(nd, sh, jy_scan_u64(eng, len, off, items));
+    u64* o[3] = {nullptr, nullptr, nullptr};
+    for (int c = 0; c < N; c++) JY_TRY(bufT(nd, sh, B_LC00 + 2 * l + c, std::max<u64>(L.nel, 1), &o[c]));
+    u32* src = nullptr;
+    if (want_src) JY_TRY(bufT(nd, sh, B_ESRC, std::max<u64>(L.nel, 1), &src));
+    hipLaunchKernelGGL((k_nd_seg_copy<N, In, SegCsr>), dim3(grid_of(items)), dim3(kT), 0, eng->stream, items, perm,
+                       sg, (const u64*)off, in, o[0], o[1], o[2], src);
+    ND_HIP(nd, hipGetLastError());
+    return JY_OK;
+  }
+}
+
+// per-key word columns in owner order (B_F0..)
+template <int N>
+int32_t ingest_fixed(jy_node* nd, NdShard& sh, const InU64<N>& in, int first = 0) {
+  u64* o[3] = {nullptr, nullptr, nullptr};
+  for (int c = 0; c < N; c++) JY_TRY(bufT(nd, sh, B_F0 + first + c, std::max<u64>(sh.n, 1), &o[c]));
+  if (sh.n == 0) return JY_OK;
+  hipLaunchKernelGGL((k_nd_perm<N>), dim3(grid_of(sh.n)), dim3(kT), 0, sh.eng->stream, sh.n,
+                     (const u32*)sh.b[B_PERM].p, in, o[0], o[1], o[2]);
+  ND_HIP(nd, hipGetLastError());
+  return JY_OK;
+}
+
+// ---- the exchange ----
+// a wire column: granule (0 keys, 1 key bytes, 2 + l level l), element size,
+// send and receive buffers
+struct Wire {
+  int gran, esize, sidx, ridx;
+};
+
+int32_t exchange(jy_node* nd, u32 W, const std::vector<Wire>& wires, u32 nl) {
+  const u32 S = nd->S;
+  // 1. counts: per destination and granule -> per source and granule
+  if (nd->fabric == JY_FABRIC_RCCL) {
+    ND_NCCL(nd, ncclGroupStart());
+    for (NdShard& sh : nd->sh) {
+      u64* cnt = static_cast<u64*>(sh.b[B_CNT].p);
+      for (u32 d = 0; d < S; d++) {
+        ND_NCCL(nd, ncclSend(cnt + (u64)d * W, W, ncclUint64, (int)d, sh.comm, sh.eng->stream));
+        ND_NCCL(nd, ncclRecv(cnt + (u64)(kMaxS + d) * W, W, ncclUint64, (int)d, sh.comm, sh.eng->stream));
+      }
+    }
+    ND_NCCL(nd, ncclGroupEnd());
+    for (NdShard& sh : nd->sh) {
+      ND_HIP(nd, hipSetDevice(sh.dev));
+      ND_HIP(nd, hipMemcpyAsync(sh.pin, sh.b[B_CNT].p, 2 * kMaxS * kMaxW * 8, hipMemcpyDeviceToHost, sh.eng->stream));
+    }
+    for (NdShard& sh : nd->sh) ND_HIP(nd, hipStreamSynchronize(sh.eng->stream));
+  } else {
+    for (NdShard& sh : nd->sh) {
+      ND_HIP(nd, hipSetDevice(sh.dev));
+      ND_HIP(nd, hipMemcpyAsync(sh.pin, sh.b[B_CNT].p, (u64)S * W * 8, hipMemcpyDeviceToHost, sh.eng->stream));
+      ND_HIP(nd, hipEventRecord(sh.ev_in, sh.eng->stream));
+    }
+    for (NdShard& sh : nd->sh) ND_HIP(nd, hipStreamSynchronize(sh.eng->stream));
+    for (NdShard& dst : nd->sh)
+      for (const NdShard& src : nd->sh)
+        std::memcpy(dst.pin + (u64)(kMaxS + src.rank) * W, src.pin + (u64)dst.rank * W, W * 8);
+  }
+  // 2. receive buffers, source-major per wire column
+  for (NdShard& sh : nd->sh) {
+    const u64* rc = sh.pin + (u64)kMaxS * W;
+    for (u32 g = 0; g < W; g++) {
+      u64 t = 0;
+      for (u32 s = 0; s < S; s++) t += rc[(u64)s * W + g];
+      sh.rtot[g] = t;
+    }
+    for (const Wire& w : wires) {
+      void* p;
+      // a key-length column gets one word more (the scan's last input)
+      const u64 extra = (w.ridx == R_KLEN) ? 1 : 0;
+      JY_TRY(buf(nd, sh, w.ridx, (sh.rtot[w.gran] + extra) * w.esize + 8, &p));
+    }
+    nd->stats[1] += sh.rtot[0];
+    u64 sb = 0, rb = 0;
+    for (const Wire& w : wires)
+      for (u32 d = 0; d < S; d++) {
+        sb += sh.pin[(u64)d * W + w.gran] * w.esize;
+        rb += rc[(u64)d * W + w.gran] * w.esize;
+      }
+    nd->stats[2] += sb;
+    nd->stats[3] += rb;
+  }
+  // 3. payload
+  if (nd->fabric == JY_FABRIC_RCCL) {
+    ND_NCCL(nd, ncclGroupStart());
+    for (NdShard& sh : nd->sh) {
+      const u64* sc = sh.pin;
+      const u64* rc = sh.pin + (u64)kMaxS * W;
+      for (const Wire& w : wires) {
+        const uint8_t* sp = static_cast<const uint8_t*>(sh.b[w.sidx].p);
+        uint8_t* rp = static_cast<uint8_t*>(sh.b[w.ridx].p);
+        u64 so = 0, ro = 0;
+        for (u32 d = 0; d < S; d++) {
+          const u64 sn = sc[(u64)d * W + w.gran] * w.esize, rn = rc[(u64)d * W + w.gran] * w.esize;
+          if (sn) ND_NCCL(nd, ncclSend(sp + so, sn, ncclUint8, (int)d, sh.comm, sh.eng->stream));
+          if (rn) ND_NCCL(nd, ncclRecv(rp + ro, rn, ncclUint8, (int)d, sh.comm, sh.eng->stream));
+          so += sn;
+          ro += rn;
+        }
+      }
+    }
+    ND_NCCL(nd, ncclGroupEnd());
+  } else {
+    // pull: each destination waits for every source's columns, copies its
+    // parts on its own stream, and records that its receives landed (the next
+    // call's ingest on a source waits for it before rewriting its columns)
+    for (NdShard& dst : nd->sh) {
+      ND_HIP(nd, hipSetDevice(dst.dev));
+      for (NdShard& src : nd->sh) ND_HIP(nd, hipStreamWaitEvent(dst.eng->stream, src.ev_in, 0));
+      const u64* rc = dst.pin + (u64)kMaxS * W;
+      for (const Wire& w : wires) {
+        uint8_t* rp = static_cast<uint8_t*>(dst.b[w.ridx].p);
+        u64 ro = 0;
+        for (NdShard& src : nd->sh) {
+          // where dst's part starts in src's owner-order column
+          u64 so = 0;
+          for (u32 d = 0; d < dst.rank; d++) so += src.pin[(u64)d * W + w.gran];
+          const u64 rn = rc[(u64)src.rank * W + w.gran] * w.esize;
+          if (rn) {
+            const uint8_t* sp = static_cast<const uint8_t*>(src.b[w.sidx].p) + so * w.esize;
+            if (src.dev == dst.dev)
+              ND_HIP(nd, hipMemcpyAsync(rp + ro, sp, rn, hipMemcpyDeviceToDevice, dst.eng->stream));
+            else
+              ND_HIP(nd, hipMemcpyPeerAsync(rp + ro, dst.dev, sp, src.dev, rn, dst.eng->stream));
+          }
+          ro += rn;
+        }
+      }
+      ND_HIP(nd, hipEventRecord(dst.ev_out, dst.eng->stream));
+    }
+  }
+  nd->stats[4]++;
+  (void)nl;
+  return JY_OK;
+}
+
+// the next ingest rewrites the send columns: with the copy fabric the other
+// shards' pulls of the previous call must have happened first
+int32_t ingest_begin(jy_node* nd, NdShard& sh) {
+  ND_HIP(nd, hipSetDevice(sh.dev));
+  if (nd->fabric == JY_FABRIC_COPY)
+    for (NdShard& o : nd->sh) ND_HIP(nd, hipStreamWaitEvent(sh.eng->stream, o.ev_out, 0));
+  for (auto& t : sh.tot) t = 0;
+  return JY_OK;
+}
+
+// key ranges per local shard: contiguous, as even as the key count allows
+void split(const jy_node* nd, u64 n, std::vector<u64>& at) {
+  at.assign(nd->nlocal + 1, 0);
+  for (u32 L = 0; L <= nd->nlocal; L++) at[L] = n * L / nd->nlocal;
+}
+
+// stage a chunk: host memory through the engine's pinned ring, device
+// memory in place
+int32_t stage(jy_node* nd, NdShard& sh, int slot, const void* src, u64 bytes, int32_t mem, const void** out) {
+  ND_ENG(nd, sh, jy_stage(sh.eng, slot, src, bytes, mem, out));
+  return JY_OK;
+}
+
+// the received keys interned in the owner's directory -> R_SLOTS
+int32_t owner_keys(jy_node* nd, NdShard& sh, int32_t type, u32** slots) {
+  const u64 n = sh.rtot[0];
+  u64* koff;
+  JY_TRY(bufT(nd, sh, R_KOFF, n + 1, &koff));
+  JY_TRY(bufT(nd, sh, R_SLOTS, std::max<u64>(n, 1), slots));
+  if (n == 0) return JY_OK;
+  u64* klen = static_cast<u64*>(sh.b[R_KLEN].p);
+  ND_HIP(nd, hipMemsetAsync(klen + n, 0, 8, sh.eng->stream));
+  ND_ENG(nd, sh, jy_scan_u64(sh.eng, klen, koff, n));
+  ND_ENG(nd, sh, jy_keys_intern_mem(sh.eng, type, n, static_cast<const uint8_t*>(sh.b[R_KBYTES].p), koff, *slots,
+                                    JY_DEVICE));
+  return JY_OK;
+}
+
+// a received CSR level: its per-item lengths (received per-key column
+// `lens_idx`, n items) -> global offsets (R_LOFF l) and per-source local
+// offsets (R_LOC l, n + S words); per-source item and element starts on the host
+int32_t owner_level(jy_node* nd, NdShard& sh, u32 l, int lens_idx, u64 n, u32 gran_items, u32 gran_el, u32 W,
+                    SrcRanges& R, std::vector<u64>& ebase) {
+  const u32 S = nd->S;
+  const u64* rc = sh.pin + (u64)kMaxS * W;
+  u64 *lens = static_cast<u64*>(sh.b[lens_idx].p), *goff, *loc;
+  JY_TRY(bufT(nd, sh, R_LOFF0 + l, n + 1, &goff));
+  JY_TRY(bufT(nd, sh, R_LOC0 + l, n + S, &loc));
+  R.S = S;
+  ebase.assign(S + 1, 0);
+  u64 k = 0, e = 0;
+  for (u32 s = 0; s < S; s++) {
+    R.kb[s] = k;
+    ebase[s] = e;
+    k += rc[(u64)s * W + gran_items];
+    e += rc[(u64)s * W + gran_el];
+  }
+  R.kb[S] = k;
+  ebase[S] = e;
+  if (n == 0) return JY_OK;
+  // lens has room for one word more (buf() sizes receive columns with + 8 B)
+  ND_HIP(nd, hipMemsetAsync(lens + n, 0, 8, sh.eng->stream));
+  ND_ENG(nd, sh, jy_scan_u64(sh.eng, lens, goff, n));
+  hipLaunchKernelGGL(k_nd_local_offs, dim3(grid_of(n + S)), dim3(kT), 0, sh.eng->stream, (const u64*)goff, n, R, loc);
+  ND_HIP(nd, hipGetLastError());
+  return JY_OK;
+}
+
+// received value bytes (a long-value level) into the owner's arena; handles
+// from the lengths column `vlen` (n items) -> R_LR
+int32_t owner_values(jy_node* nd, NdShard& sh, int32_t type, const u64* vlen, u64 n, int bytes_idx, u64 nbytes,
+                     u64** lr) {
+  u64 *plen, *voff;
+  JY_TRY(bufT(nd, sh, R_PLEN, n + 1, &plen));
+  JY_TRY(bufT(nd, sh, R_VOFF, n + 1, &voff));
+  JY_TRY(bufT(nd, sh, R_LR, std::max<u64>(n, 1), lr));
+  if (n == 0) return JY_OK;
+  u64 rebase = 0;
+  ND_ENG(nd, sh, jy_arena_append_dev(sh.eng, type, static_cast<const uint8_t*>(sh.b[bytes_idx].p), nbytes, &rebase));
+  hipLaunchKernelGGL(k_nd_plen, dim3(grid_of(n + 1)), dim3(kT), 0, sh.eng->stream, n, vlen, plen);
+  ND_HIP(nd, hipGetLastError());
+  ND_ENG(nd, sh, jy_scan_u64(sh.eng, plen, voff, n));
+  hipLaunchKernelGGL(k_nd_lr, dim3(grid_of(n)), dim3(kT), 0, sh.eng->stream, n, vlen, (const u64*)voff, rebase, *lr);
+  ND_HIP(nd, hipGetLastError());
+  return JY_OK;
+}
+
+int32_t node_check(jy_node* nd, int32_t mem, u64 n) {
+  if (!nd) return JY_EINVAL;
+  if (mem != JY_HOST && mem != JY_DEVICE) return nd->fail(JY_EINVAL, "mem must be JY_HOST or JY_DEVICE");
+  if (n >= 0xFFFFFFFFull) return nd->fail(JY_ERANGE, "more than 2^32 - 1 keys in one call");
+  return JY_OK;
+}
+
+// host value lengths fit a handle (the device form trusts its caller)
+int32_t values_check(jy_node* nd, const u64* vo, u64 a, u64 e, int32_t mem) {
+  if (mem != JY_HOST) return JY_OK;
+  for (u64 i = a; i < e; i++) {
+    if (vo[i + 1] < vo[i]) return nd->fail(JY_EINVAL, "value offsets are not ascending");
+    if (vo[i + 1] - vo[i] > JY_MAX_VALUE_LEN) return nd->fail(JY_ERANGE, "value longer than 16 MiB");
+  }
+  return JY_OK;
+}
+
+// per local shard: keys chunk (staged) -> Ingest
+int32_t stage_keys(jy_node* nd, NdShard& sh, u64 a, u64 e, const uint8_t* kb, const u64* ko, int32_t mem, Ingest& in) {
+  sh.n = e - a;
+  const void *dkb, *dko;
+  u64 k0, k1;
+  JY_TRY(read2(nd, sh, ko + a, ko + e, mem, k0, k1));
+  if (k1 < k0) return nd->fail(JY_EINVAL, "key offsets are not ascending");
+  JY_TRY(stage(nd, sh, 0, mem == JY_HOST ? kb + k0 : kb, k1 - k0, mem, &dkb));
+  JY_TRY(stage(nd, sh, 1, ko + a, (sh.n + 1) * 8, mem, &dko));
+  in.kb = static_cast<const uint8_t*>(dkb);
+  in.ko = static_cast<const u64*>(dko);
+  in.kobase = mem == JY_HOST ? k0 : 0;
+  in.nkb = k1 - k0;
+  sh.tot[0] = sh.n;
+  sh.tot[1] = in.nkb;
+  return JY_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C ABI
+
+extern "C" {
+
+int32_t jy_node_unique_id(uint8_t* id_out) {
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return JY_EHIP;
+  std::memcpy(id_out, &id, sizeof(id));
+  return JY_OK;
+}
+
+void jy_node_destroy(jy_node* nd) {
+  if (!nd) return;
+  for (NdShard& sh : nd->sh) {
+    hipSetDevice(sh.dev);
+    if (sh.eng) hipStreamSynchronize(sh.eng->stream);
+    if (sh.xs) hipStreamSynchronize(sh.xs);
+  }
+  for (NdShard& sh : nd->sh)
+    if (sh.comm) ncclCommDestroy(sh.comm);
+  for (NdShard& sh : nd->sh) {
+    hipSetDevice(sh.dev);
+    for (NdBuf& b : sh.b)
+      if (b.p) hipFree(b.p);
+    if (sh.pin) hipHostFree(sh.pin);
+    for (hipEvent_t e : {sh.ev_in, sh.ev_out, sh.ev_x[0], sh.ev_x[1], sh.ev_m[0], sh.ev_m[1]})
+      if (e) hipEventDestroy(e);
+    if (sh.xs) hipStreamDestroy(sh.xs);
+    jy_engine_destroy(sh.eng);
+  }
+  delete nd;
+}
+
+int32_t jy_node_create(const jy_node_config* cfg, jy_node** out) {
+  *out = nullptr;
+  if (!cfg || cfg->nshards == 0 || cfg->nshards > kMaxS || cfg->nlocal == 0 ||
+      cfg->rank0 + cfg->nlocal > cfg->nshards)
+    return JY_EINVAL;
+  if (cfg->fabric != JY_FABRIC_RCCL && cfg->fabric != JY_FABRIC_COPY) return JY_EINVAL;
+  if (cfg->fabric == JY_FABRIC_COPY && cfg->nlocal != cfg->nshards) return JY_EINVAL;  // one process
+  jy_node* nd = new jy_node();
+  nd->cfg = *cfg;
+  nd->S = cfg->nshards;
+  nd->nlocal = cfg->nlocal;
+  nd->rank0 = cfg->rank0;
+  nd->fabric = cfg->fabric;
+  nd->sh.resize(nd->nlocal);
+  for (u32 L = 0; L < nd->nlocal; L++) {
+    NdShard& sh = nd->sh[L];
+    sh.rank = nd->rank0 + L;
+    sh.dev = cfg->devices[L];
+    jy_config ec = cfg->engine;
+    ec.device = sh.dev;
+    if (jy_engine_create(&ec, &sh.eng) != JY_OK || !sh.eng ||
+        hipHostMalloc(reinterpret_cast<void**>(&sh.pin), (2 * kMaxS * kMaxW + 16) * 8, hipHostMallocDefault) !=
+            hipSuccess ||
+        hipStreamCreateWithFlags(&sh.xs, hipStreamNonBlocking) != hipSuccess) {
+      std::fprintf(stderr, "jy_node_create: shard %u on device %d failed\n", sh.rank, sh.dev);
+      jy_node_destroy(nd);
+      return JY_EHIP;
+    }
+    for (hipEvent_t* e : {&sh.ev_in, &sh.ev_out, &sh.ev_x[0], &sh.ev_x[1], &sh.ev_m[0], &sh.ev_m[1]})
+      if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
+        jy_node_destroy(nd);
+        return JY_EHIP;
+      }
+    hipEventRecord(sh.ev_out, sh.eng->stream);
+  }
+  if (nd->fabric == JY_FABRIC_RCCL) {
+    ncclUniqueId id;
+    std::memcpy(&id, cfg->unique_id, sizeof(id));
+    bool zero = true;
+    for (u64 i = 0; i < sizeof(id); i++) zero = zero && cfg->unique_id[i] == 0;
+    if (zero) {
+      if (nd->nlocal != nd->S) {
+        std::fprintf(stderr, "jy_node_create: a multi-process node needs the shared unique_id\n");
+        jy_node_destroy(nd);
+        return JY_EINVAL;
+      }
+      if (ncclGetUniqueId(&id) != ncclSuccess) {
+        jy_node_destroy(nd);
+        return JY_EHIP;
+      }
+    }
+    ncclResult_t r = ncclGroupStart();
+    for (NdShard& sh : nd->sh) {
+      if (r != ncclSuccess) break;
+      hipSetDevice(sh.dev);
+      r = ncclCommInitRank(&sh.comm, (int)nd->S, id, (int)sh.rank);
+    }
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess) {
+      std::fprintf(stderr, "jy_node_create: ncclCommInitRank: %s\n",
+                   ncclGetErrorString(r != ncclSuccess ? r : r2));
+      jy_node_destroy(nd);
+      return JY_EHIP;
+    }
+  }
+  *out = nd;
+  return JY_OK;
+}
+
+const char* jy_node_last_error(const jy_node* nd) { return nd ? nd->err.c_str() : "null node"; }
+uint32_t jy_node_nshards(const jy_node* nd) { return nd ? nd->S : 0; }
+
+jy_engine* jy_node_engine(jy_node* nd, uint32_t shard) {
+  if (!nd || shard < nd->rank0 || shard >= nd->rank0 + nd->nlocal) return nullptr;
+  return nd->sh[shard - nd->rank0].eng;
+}
+
+uint32_t jy_node_shard_of(const jy_node* nd, const uint8_t* key, uint64_t len) {
+  return jy_key_owner(key, len, nd ? nd->S : 1);
+}
+
+int32_t jy_node_replica_col(jy_node* nd, uint64_t id, uint32_t* col) {
+  if (!nd) return JY_EINVAL;
+  u32 c0 = 0;
+  for (u32 L = 0; L < nd->nlocal; L++) {
+    u32 c = 0;
+    ND_ENG(nd, nd->sh[L], jy_replica_col(nd->sh[L].eng, id, &c));
+    if (L == 0) c0 = c;
+    else if (c != c0) return nd->fail(JY_EINVAL, "shards disagree on a replica column (register on the node only)");
+  }
+  *col = c0;
+  return JY_OK;
+}
+
+int32_t jy_node_sync(jy_node* nd) {
+  if (!nd) return JY_EINVAL;
+  for (NdShard& sh : nd->sh) {
+    ND_ENG(nd, sh, jy_sync(sh.eng));
+    ND_HIP(nd, hipStreamSynchronize(sh.xs));
+  }
+  return JY_OK;
+}
+
+int32_t jy_node_stats(jy_node* nd, uint64_t* out5) {
+  if (!nd) return JY_EINVAL;
+  std::memcpy(out5, nd->stats, sizeof(nd->stats));
+  return JY_OK;
+}
+
+// ---- TREG: key bytes | ts, pre, vlen | long value bytes ----
+int32_t jy_node_treg_converge(jy_node* nd, uint64_t n, const uint8_t* kb, const uint64_t* ko, const uint64_t* ts,
+                              const uint8_t* vb, const uint64_t* vo, int32_t mem) {
+  JY_TRY(node_check(nd, mem, n));
+  std::vector<u64> at;
+  split(nd, n, at);
+  nd->stats[0] = n;
+  nd->stats[1] = nd->stats[2] = nd->stats[3] = 0;
+  constexpr u32 W = 3;  // keys, key bytes, value bytes
+  for (u32 L = 0; L < nd->nlocal; L++) {
+    NdShard& sh = nd->sh[L];
+    JY_TRY(ingest_begin(nd, sh));
+    Ingest in;
+    ND_ENG(nd, sh, jy_stage_begin(sh.eng));
+    JY_TRY(stage_keys(nd, sh, at[L], at[L + 1], kb, ko, mem, in));
+    const u64 a = at[L], m = sh.n;
+    u64 v0, v1;
+    JY_TRY(values_check(nd, vo, a, at[L + 1], mem));
+    JY_TRY(read2(nd, sh, vo + a, vo + at[L + 1], mem, v0, v1));
+    const void *dts, *dvo, *dvb;
+    JY_TRY(stage(nd, sh, 2, ts + a, m * 8, mem, &dts));
+    JY_TRY(stage(nd, sh, 3, vo + a, (m + 1) * 8, mem, &dvo));
+    JY_TRY(stage(nd, sh, 4, mem == JY_HOST ? vb + v0 : vb, v1 - v0, mem, &dvb));
+    ND_ENG(nd, sh, jy_stage_end(sh.eng));
+    JY_TRY(ingest_keys(nd, sh, in));
+    const u64 vbase = mem == JY_HOST ? v0 : 0;
+    JY_TRY(ingest_fixed<1>(nd, sh, InU64<1>{{static_cast<const u64*>(dts)}}));
+    u64 *pre, *vlen;
+    JY_TRY(bufT(nd, sh, B_F1, std::max<u64>(m, 1), &pre));
+    JY_TRY(bufT(nd, sh, B_F2, std::max<u64>(m, 1), &vlen));
+    if (m)
+      hipLaunchKernelGGL(k_nd_val_head, dim3(grid_of(m)), dim3(kT), 0, sh.eng->stream, m,
+                         (const u32*)sh.b[B_PERM].p, static_cast<const u64*>(dvo), vbase,
+                         static_cast<const uint8_t*>(dvb), pre, vlen);
+    ND_HIP(nd, hipGetLastError());
+    Level lv;
+    lv.offs = static_cast<const u64*>(dvo);
+    lv.obase = vbase;
+    lv.nel = v1 - v0;
+    lv.longval = true;
+    JY_TRY(ingest_level<1>(nd, sh, 0, lv, m, (const u32*)sh.b[B_PERM].p, InBytes{static_cast<const uint8_t*>(dvb)},
+                           false));
+    JY_TRY(ingest_counts(nd, sh, &lv, 1));
+  }
+  const std::vector<Wire> wires = {{0, 8, B_KLEN, R_KLEN}, {1, 1, B_KBYTES, R_KBYTES}, {0, 8, B_F0, R_F0},
+                                   {0, 8, B_F1, R_F1},     {0, 8, B_F2, R_F2},         {2, 1, B_LC00, R_LC00}};
+  JY_TRY(exchange(nd, W, wires, 1));
+  for (NdShard& sh : nd->sh) {
+    ND_HIP(nd, hipSetDevice(sh.dev));
+    u32* slots;
+    JY_TRY(owner_keys(nd, sh, JY_TREG, &slots));
+    const u64 m = sh.rtot[0];
+    u64* lr;
+    JY_TRY(owner_values(nd, sh, JY_TREG, static_cast<const u64*>(sh.b[R_F2].p), m, R_LC00, sh.rtot[2], &lr));
+    ND_ENG(nd, sh, jy_treg_merge(sh.eng, m, slots, static_cast<const u64*>(sh.b[R_F0].p),
+                                 static_cast<const u64*>(sh.b[R_F1].p), lr));
+  }
+  return JY_OK;
+}
+
+// ---- counters: key bytes | cell count | cells (sign << 16 | col, val) ----
+int32_t jy_node_counter_converge(jy_node* nd, int32_t type, uint64_t n, const uint8_t* kb, const uint64_t* ko,
+                                 const uint64_t* co, const uint8_t* sign, const uint16_t* col, const uint64_t* val,
+                                 int32_t mem) {
+  JY_TRY(node_check(nd, mem, n));
+  if (type != JY_GCOUNT && type != JY_PNCOUNT) return nd->fail(JY_EINVAL, "type must be JY_GCOUNT or JY_PNCOUNT");
+  if (type == JY_GCOUNT && sign) return nd->fail(JY_EINVAL, "GCOUNT cells have no sign");
+  std::vector<u64> at;
+  split(nd, n, at);
+  nd->stats[0] = n;
+  nd->stats[1] = nd->stats[2] = nd->stats[3] = 0;
+  constexpr u32 W = 3;  // keys, key bytes, cells
+  for (u32 L = 0; L < nd->nlocal; L++) {
+    NdShard& sh = nd->sh[L];
+    JY_TRY(ingest_begin(nd, sh));
+    Ingest in;
+    ND_ENG(nd, sh, jy_stage_begin(sh.eng));
+    JY_TRY(stage_keys(nd, sh, at[L], at[L + 1], kb, ko, mem, in));
+    const u64 a = at[L], m = sh.n;
+    u64 c0, c1;
+    JY_TRY(read2(nd, sh, co + a, co + at[L + 1], mem, c0, c1));
+    if (c1 < c0) return nd->fail(JY_EINVAL, "cell offsets are not ascending");
+    if (mem == JY_HOST) {
+      const u32 nrep = jy_replica_count(sh.eng);
+      for (u64 c = c0; c < c1; c++) {
+        if (col[c] >= nrep) return nd->fail(JY_ERANGE, "column names no registered replica");
+        if (sign && sign[c] > 1) return nd->fail(JY_ERANGE, "sign must be 0 (P) or 1 (N)");
+      }
+    }
+    const u64 cb = mem == JY_HOST ? c0 : 0;
+    const void *dco, *dsg = nullptr, *dcol, *dval;
+    JY_TRY(stage(nd, sh, 2, co + a, (m + 1) * 8, mem, &dco));
+    if (sign) JY_TRY(stage(nd, sh, 3, sign + cb, c1 - c0, mem, &dsg));
+    JY_TRY(stage(nd, sh, 4, col + cb, (c1 - c0) * 2, mem, &dcol));
+    JY_TRY(stage(nd, sh, 5, val + cb, (c1 - c0) * 8, mem, &dval));
+    ND_ENG(nd, sh, jy_stage_end(sh.eng));
+    JY_TRY(ingest_keys(nd, sh, in));
+    Level lv;
+    lv.offs = static_cast<const u64*>(dco);
+    lv.obase = cb;
+    lv.nel = c1 - c0;
+    const InCells cells{static_cast<const uint8_t*>(dsg), static_cast<const u16*>(dcol), static_cast<const u64*>(dval)};
+    JY_TRY(ingest_level<2>(nd, sh, 0, lv, m, (const u32*)sh.b[B_PERM].p, cells, false));
+    JY_TRY(ingest_counts(nd, sh, &lv, 1));
+  }
+  const std::vector<Wire> wires = {{0, 8, B_KLEN, R_KLEN},   {1, 1, B_KBYTES, R_KBYTES}, {0, 8, B_LLEN0, R_F0},
+                                   {2, 8, B_LC00, R_LC00}, {2, 8, B_LC01, R_LC01}};
+  JY_TRY(exchange(nd, W, wires, 1));
+  const int which = type == JY_GCOUNT ? 0 : 1;
+  for (NdShard& sh : nd->sh) {
+    ND_HIP(nd, hipSetDevice(sh.dev));
+    u32* slots;
+    JY_TRY(owner_keys(nd, sh, type, &slots));
+    const u64 m = sh.rtot[0], nc = sh.rtot[2];
+    if (nc == 0) continue;
+    u64* off;
+    u32* ckey;
+    uint8_t* sg;
+    u16* cl;
+    JY_TRY(bufT(nd, sh, R_LOFF0, m + 1, &off));
+    JY_TRY(bufT(nd, sh, R_AUX0, nc, &ckey));
+    JY_TRY(bufT(nd, sh, R_AUX1, nc, &sg));
+    JY_TRY(bufT(nd, sh, R_AUX2, nc, &cl));
+    u64* lens = static_cast<u64*>(sh.b[R_F0].p);
+    ND_HIP(nd, hipMemsetAsync(lens + m, 0, 8, sh.eng->stream));
+    ND_ENG(nd, sh, jy_scan_u64(sh.eng, lens, off, m));
+    ND_ENG(nd, sh, jy_seg_ids(sh.eng, off, m, nc, ckey));
+    hipLaunchKernelGGL(k_nd_cells, dim3(grid_of(nc)), dim3(kT), 0, sh.eng->stream, nc,
+                       (const u64*)sh.b[R_LC00].p, sg, cl);
+    ND_HIP(nd, hipGetLastError());
+    ND_ENG(nd, sh, jy_counter_grow(sh.eng, which, jy_replica_count(sh.eng), 0));
+    ND_ENG(nd, sh, jy_counter_coo_keyed(sh.eng, which, nc, m, slots, ckey, type == JY_PNCOUNT ? sg : nullptr, cl,
+                                        static_cast<const u64*>(sh.b[R_LC01].p)));
+  }
+  return JY_OK;
+}
+
+// ---- TLOG: key bytes | cutoff, entry count | entries (ts, pre, vlen) | long value bytes ----
+int32_t jy_node_tlog_converge(jy_node* nd, uint64_t n, const uint8_t* kb, const uint64_t* ko, const uint64_t* cutoff,
+                              const uint64_t* eo, const uint64_t* ts, const uint8_t* vb, const uint64_t* vo,
+                              int32_t mem) {
+  JY_TRY(node_check(nd, mem, n));
+  std::vector<u64> at;
+  split(nd, n, at);
+  nd->stats[0] = n;
+  nd->stats[1] = nd->stats[2] = nd->stats[3] = 0;
+  constexpr u32 W = 4;  // keys, key bytes, entries, value bytes
+  for (u32 L = 0; L < nd->nlocal; L++) {
+    NdShard& sh = nd->sh[L];
+    JY_TRY(ingest_begin(nd, sh));
+    Ingest in;
+    ND_ENG(nd, sh, jy_stage_begin(sh.eng));
+    JY_TRY(stage_keys(nd, sh, at[L], at[L + 1], kb, ko, mem, in));
+    const u64 a = at[L], m = sh.n;
+    u64 e0, e1, v0, v1;
+    JY_TRY(read2(nd, sh, eo + a, eo + at[L + 1], mem, e0, e1));
+    if (e1 < e0) return nd->fail(JY_EINVAL, "entry offsets are not ascending");
+    if (e1 - e0 >= 0xFFFFFFFFull) return nd->fail(JY_ERANGE, "more than 2^32 - 1 entries in one shard's range");
+    JY_TRY(values_check(nd, vo, e0, e1, mem));
+    JY_TRY(read2(nd, sh, vo + e0, vo + e1, mem, v0, v1));
+    if (v1 < v0) return nd->fail(JY_EINVAL, "value offsets are not ascending");
+    const u64 eb = mem == JY_HOST ? e0 : 0, vbase = mem == JY_HOST ? v0 : 0;
+    const void *dcut, *deo, *dts, *dvo, *dvb;
+    JY_TRY(stage(nd, sh, 2, cutoff + a, m * 8, mem, &dcut));
+    JY_TRY(stage(nd, sh, 3, eo + a, (m + 1) * 8, mem, &deo));
+    JY_TRY(stage(nd, sh, 4, ts + eb, (e1 - e0) * 8, mem, &dts));
+    JY_TRY(stage(nd, sh, 5, vo + eb, (e1 - e0 + 1) * 8, mem, &dvo));
+    JY_TRY(stage(nd, sh, 6, mem == JY_HOST ? vb + v0 : vb, v1 - v0, mem, &dvb));
+    ND_ENG(nd, sh, jy_stage_end(sh.eng));
+    JY_TRY(ingest_keys(nd, sh, in));
+    JY_TRY(ingest_fixed<1>(nd, sh, InU64<1>{{static_cast<const u64*>(dcut)}}));
+    Level lv[2];
+    lv[0].offs = static_cast<const u64*>(deo);
+    lv[0].obase = eb;
+    lv[0].nel = e1 - e0;
+    // entries: ts in owner order, element sources for the value level
+    JY_TRY(ingest_level<1>(nd, sh, 0, lv[0], m, (const u32*)sh.b[B_PERM].p,
+                           InU64<1>{{static_cast<const u64*>(dts)}}, true));
+    const u64 ne = e1 - e0;
+    u64 *pre, *vlen;
+    JY_TRY(bufT(nd, sh, B_LC01, std::max<u64>(ne, 1), &pre));
+    // (the value lengths ride in the level-1 slot's second column)
+    JY_TRY(bufT(nd, sh, B_LC11, std::max<u64>(ne, 1), &vlen));
+    if (ne)
+      hipLaunchKernelGGL(k_nd_val_head, dim3(grid_of(ne)), dim3(kT), 0, sh.eng->stream, ne,
+                         (const u32*)sh.b[B_ESRC].p, static_cast<const u64*>(dvo), vbase,
+                         static_cast<const uint8_t*>(dvb), pre, vlen);
+    ND_HIP(nd, hipGetLastError());
+    lv[1].offs = static_cast<const u64*>(dvo);
+    lv[1].obase = vbase;
+    lv[1].nel = v1 - v0;
+    lv[1].parent = 0;
+    lv[1].longval = true;
+    JY_TRY(ingest_level<1>(nd, sh, 1, lv[1], ne, (const u32*)sh.b[B_ESRC].p,
+                           InBytes{static_cast<const uint8_t*>(dvb)}, false));
+    JY_TRY(ingest_counts(nd, sh, lv, 2));
+  }
+  const std::vector<Wire> wires = {{0, 8, B_KLEN, R_KLEN}, {1, 1, B_KBYTES, R_KBYTES}, {0, 8, B_F0, R_F0},
+                                   {0, 8, B_LLEN0, R_F1},  {2, 8, B_LC00, R_LC00},     {2, 8, B_LC01, R_LC01},
+                                   {2, 8, B_LC11, R_LC11}, {3, 1, B_LC10, R_LC10}};
+  JY_TRY(exchange(nd, W, wires, 2));
+  for (NdShard& sh : nd->sh) {
+    ND_HIP(nd, hipSetDevice(sh.dev));
+    u32* slots;
+    JY_TRY(owner_keys(nd, sh, JY_TLOG, &slots));
+    const u64 m = sh.rtot[0], ne = sh.rtot[2];
+    SrcRanges R;
+    std::vector<u64> ebase;
+    JY_TRY(owner_level(nd, sh, 0, R_F1, m, 0, 2, W, R, ebase));
+    u64* lr;
+    JY_TRY(owner_values(nd, sh, JY_TLOG, static_cast<const u64*>(sh.b[R_LC11].p), ne, R_LC10, sh.rtot[3], &lr));
+    const u64* cut = static_cast<const u64*>(sh.b[R_F0].p);
+    const u64* loc = static_cast<const u64*>(sh.b[R_LOC0].p);
+    const u64* rts = static_cast<const u64*>(sh.b[R_LC00].p);
+    const u64* rpre = static_cast<const u64*>(sh.b[R_LC01].p);
+    for (u32 s = 0; s < nd->S; s++) {
+      const u64 k0 = R.kb[s], nk = R.kb[s + 1] - k0;
+      if (nk == 0) continue;
+      ND_ENG(nd, sh, jy_tlog_merge(sh.eng, nk, slots + k0, cut + k0, loc + k0 + s, ebase[s + 1] - ebase[s],
+                                   rts + ebase[s], rpre + ebase[s], lr + ebase[s]));
+    }
+  }
+  return JY_OK;
+}
+
+// ---- UJSON: key bytes | element, vv, cloud counts | (dots, elems), vv, cloud ----
+int32_t jy_node_ujson_converge(jy_node* nd, uint64_t n, const uint8_t* kb, const uint64_t* ko, const uint64_t* eo,
+                               const uint64_t* dots, const uint64_t* elems, const uint64_t* vvo, const uint64_t* vv,
+                               const uint64_t* clo, const uint64_t* cloud, int32_t mem) {
+  JY_TRY(node_check(nd, mem, n));
+  std::vector<u64> at;
+  split(nd, n, at);
+  nd->stats[0] = n;
+  nd->stats[1] = nd->stats[2] = nd->stats[3] = 0;
+  constexpr u32 W = 5;  // keys, key bytes, elements, vv entries, cloud dots
+  for (u32 L = 0; L < nd->nlocal; L++) {
+    NdShard& sh = nd->sh[L];
+    JY_TRY(ingest_begin(nd, sh));
+    Ingest in;
+    ND_ENG(nd, sh, jy_stage_begin(sh.eng));
+    JY_TRY(stage_keys(nd, sh, at[L], at[L + 1], kb, ko, mem, in));
+    const u64 a = at[L], e = at[L + 1], m = sh.n;
+    const u64* offs[3] = {eo, vvo, clo};
+    u64 lo[3], hi[3];
+    for (int l = 0; l < 3; l++) {
+      JY_TRY(read2(nd, sh, offs[l] + a, offs[l] + e, mem, lo[l], hi[l]));
+      if (hi[l] < lo[l]) return nd->fail(JY_EINVAL, "element / vv / cloud offsets are not ascending");
+    }
+    const void *deo, *dd, *de, *dvo, *dv, *dco, *dc;
+    const u64 b0 = mem == JY_HOST ? lo[0] : 0, b1 = mem == JY_HOST ? lo[1] : 0, b2 = mem == JY_HOST ? lo[2] : 0;
+    JY_TRY(stage(nd, sh, 2, eo + a, (m + 1) * 8, mem, &deo));
+    JY_TRY(stage(nd, sh, 3, dots + b0, (hi[0] - lo[0]) * 8, mem, &dd));
+    JY_TRY(stage(nd, sh, 4, elems + b0, (hi[0] - lo[0]) * 8, mem, &de));
+    JY_TRY(stage(nd, sh, 5, vvo + a, (m + 1) * 8, mem, &dvo));
+    JY_TRY(stage(nd, sh, 6, vv + b1, (hi[1] - lo[1]) * 8, mem, &dv));
+    JY_TRY(stage(nd, sh, 7, clo + a, (m + 1) * 8, mem, &dco));
+    JY_TRY(stage(nd, sh, 8, cloud + b2, (hi[2] - lo[2]) * 8, mem, &dc));
+    ND_ENG(nd, sh, jy_stage_end(sh.eng));
+    JY_TRY(ingest_keys(nd, sh, in));
+    Level lv[3];
+    const void* lo_p[3] = {deo, dvo, dco};
+    const u64 bases[3] = {b0, b1, b2};
+    for (int l = 0; l < 3; l++) {
+      lv[l].offs = static_cast<const u64*>(lo_p[l]);
+      lv[l].obase = bases[l];
+      lv[l].nel = hi[l] - lo[l];
+    }
+    const u32* perm = static_cast<const u32*>(sh.b[B_PERM].p);
+    JY_TRY(ingest_level<2>(nd, sh, 0, lv[0], m, perm,
+                           InU64<2>{{static_cast<const u64*>(dd), static_cast<const u64*>(de)}}, false));
+    JY_TRY(ingest_level<1>(nd, sh, 1, lv[1], m, perm, InU64<1>{{static_cast<const u64*>(dv)}}, false));
+    JY_TRY(ingest_level<1>(nd, sh, 2, lv[2], m, perm, InU64<1>{{static_cast<const u64*>(dc)}}, false));
+    JY_TRY(ingest_counts(nd, sh, lv, 3));
+  }
+  const std::vector<Wire> wires = {{0, 8, B_KLEN, R_KLEN},  {1, 1, B_KBYTES, R_KBYTES}, {0, 8, B_LLEN0, R_F0},
+                                   {0, 8, B_LLEN1, R_F1},   {0, 8, B_LLEN2, R_F2},     {2, 8, B_LC00, R_LC00},
+                                   {2, 8, B_LC01, R_LC01}, {3, 8, B_LC10, R_LC10},     {4, 8, B_LC20, R_LC20}};
+  JY_TRY(exchange(nd, W, wires, 3));
+  for (NdShard& sh : nd->sh) {
+    ND_HIP(nd, hipSetDevice(sh.dev));
+    u32* slots;
+    JY_TRY(owner_keys(nd, sh, JY_UJSON, &slots));
+    const u64 m = sh.rtot[0];
+    SrcRanges R[3];
+    std::vector<u64> eb[3];
+    JY_TRY(owner_level(nd, sh, 0, R_F0, m, 0, 2, W, R[0], eb[0]));
+    JY_TRY(owner_level(nd, sh, 1, R_F1, m, 0, 3, W, R[1], eb[1]));
+    JY_TRY(owner_level(nd, sh, 2, R_F2, m, 0, 4, W, R[2], eb[2]));
+    const u64* loc[3] = {static_cast<const u64*>(sh.b[R_LOC0].p), static_cast<const u64*>(sh.b[R_LOC1].p),
+                         static_cast<const u64*>(sh.b[R_LOC2].p)};
+    const u64 *rd = static_cast<const u64*>(sh.b[R_LC00].p), *re = static_cast<const u64*>(sh.b[R_LC01].p),
+              *rv = static_cast<const u64*>(sh.b[R_LC10].p), *rcl = static_cast<const u64*>(sh.b[R_LC20].p);
+    for (u32 s = 0; s < nd->S; s++) {
+      const u64 k0 = R[0].kb[s], nk = R[0].kb[s + 1] - k0;
+      if (nk == 0) continue;
+      ND_ENG(nd, sh, jy_ujson_merge(sh.eng, nk, slots + k0, loc[0] + k0 + s, eb[0][s + 1] - eb[0][s], rd + eb[0][s],
+                                    re + eb[0][s], loc[1] + k0 + s, eb[1][s + 1] - eb[1][s], rv + eb[1][s],
+                                    loc[2] + k0 + s, eb[2][s + 1] - eb[2][s], rcl + eb[2][s]));
+    }
+  }
+  return JY_OK;
+}
+
+// ---- dense counter blocks arriving mixed ----
+int32_t jy_node_counter_converge_block(jy_node* nd, int32_t type, uint32_t ncols, const uint16_t* cols_all,
+                                       uint32_t slot0, uint32_t nslots, const uint64_t* vals_p,
+                                       const uint64_t* vals_n) {
+  if (!nd) return JY_EINVAL;
+  if (type != JY_GCOUNT && type != JY_PNCOUNT) return nd->fail(JY_EINVAL, "type must be JY_GCOUNT or JY_PNCOUNT");
+  if ((type == JY_PNCOUNT) != (vals_n != nullptr)) return nd->fail(JY_EINVAL, "vals_n is given iff PNCOUNT");
+  const u32 S = nd->S, G = type == JY_PNCOUNT ? 2 : 1;
+  if (ncols == 0 || nslots == 0) return JY_OK;
+  const u64 blk = (u64)nslots;                // words of one (column, owner) block
+  const u64 per_local = (u64)ncols * S * blk; // words per sign per local shard
+  for (NdShard& sh : nd->sh) {
+    ND_HIP(nd, hipSetDevice(sh.dev));
+    for (int k = 0; k < 2; k++) {
+      void* p;
+      JY_TRY(buf(nd, sh, X_BUF0 + k, (u64)G * S * blk * 8, &p));
+    }
+    // the exchange stream starts after the engine stream's work so far (the
+    // inputs were produced there) and after the previous call's merges
+    ND_HIP(nd, hipEventRecord(sh.ev_in, sh.eng->stream));
+    ND_HIP(nd, hipStreamWaitEvent(sh.xs, sh.ev_in, 0));
+  }
+  std::vector<u16> cols(S);
+  for (u32 c = 0; c < ncols; c++) {
+    const int k = c & 1;
+    // column c: block [g][c][d] of local shard L goes to d, lands as [g][s] at d
+    if (c >= 2)
+      for (NdShard& sh : nd->sh) {
+        ND_HIP(nd, hipSetDevice(sh.dev));
+        ND_HIP(nd, hipStreamWaitEvent(sh.xs, sh.ev_m[k], 0));  // merge c - 2 has read this buffer
+      }
+    if (nd->fabric == JY_FABRIC_RCCL) {
+      ND_NCCL(nd, ncclGroupStart());
+      for (u32 L = 0; L < nd->nlocal; L++) {
+        NdShard& sh = nd->sh[L];
+        u64* rb = static_cast<u64*>(sh.b[X_BUF0 + k].p);
+        for (u32 g = 0; g < G; g++) {
+          const u64* in = (g ? vals_n : vals_p) + (u64)L * per_local + ((u64)c * S) * blk;
+          for (u32 d = 0; d < S; d++) {
+            ND_NCCL(nd, ncclSend(in + (u64)d * blk, blk, ncclUint64, (int)d, sh.comm, sh.xs));
+            ND_NCCL(nd, ncclRecv(rb + ((u64)g * S + d) * blk, blk, ncclUint64, (int)d, sh.comm, sh.xs));
+          }
+        }
+      }
+      ND_NCCL(nd, ncclGroupEnd());
+    } else {
+      // every source's input must be ready before a destination pulls it
+      for (NdShard& sh : nd->sh) ND_HIP(nd, hipEventRecord(sh.ev_in, sh.xs));
+      for (u32 L = 0; L < nd->nlocal; L++) {
+        NdShard& dst = nd->sh[L];
+        ND_HIP(nd, hipSetDevice(dst.dev));
+        for (NdShard& src : nd->sh) ND_HIP(nd, hipStreamWaitEvent(dst.xs, src.ev_in, 0));
+        u64* rb = static_cast<u64*>(dst.b[X_BUF0 + k].p);
+        for (u32 g = 0; g < G; g++)
+          for (u32 s = 0; s < nd->nlocal; s++) {
+            const u64* in = (g ? vals_n : vals_p) + (u64)s * per_local + ((u64)c * S + dst.rank) * blk;
+            ND_HIP(nd, hipMemcpyAsync(rb + ((u64)g * S + s) * blk, in, blk * 8, hipMemcpyDefault, dst.xs));
+          }
+      }
+    }
+    for (u32 L = 0; L < nd->nlocal; L++) {
+      NdShard& sh = nd->sh[L];
+      ND_HIP(nd, hipSetDevice(sh.dev));
+      ND_HIP(nd, hipEventRecord(sh.ev_x[k], sh.xs));
+      ND_HIP(nd, hipStreamWaitEvent(sh.eng->stream, sh.ev_x[k], 0));
+      for (u32 s = 0; s < S; s++) cols[s] = cols_all[(u64)s * ncols + c];
+      const u64* rb = static_cast<const u64*>(sh.b[X_BUF0 + k].p);
+      if (type == JY_PNCOUNT)
+        ND_ENG(nd, sh, jy_pncount_converge_block(sh.eng, S, cols.data(), slot0, nslots, rb, rb + (u64)S * blk,
+                                                 JY_DEVICE));
+      else
+        ND_ENG(nd, sh, jy_gcount_converge_block(sh.eng, S, cols.data(), slot0, nslots, rb, JY_DEVICE));
+      ND_HIP(nd, hipEventRecord(sh.ev_m[k], sh.eng->stream));
+    }
+  }
+  nd->stats[4] += ncols;
+  return JY_OK;
+}
+
+}  // extern "C"

@@ -94,17 +94,30 @@ __global__ __launch_bounds__(kThreads) void k_coo_max(u64* __restrict__ slab, u6
 
 // COO cells whose slots come from a device key interning of the same call
 // (jy_counter_converge_keys): cell i belongs to key cell_key[i] (identity
-// when null) and to slab `sign[i]` (P when null)
+// when null) and to slab `sign[i]` (P when null).  Device batches are not
+// validated on the host: a cell naming no key of the batch, a sign other
+// than 0/1, a column past the registered replicas or a key the directory
+// could not place is skipped and counted (jy_skipped), like a malformed
+// entry of the reference's swallowed converge (repo_gcount.pony:51).
 __global__ __launch_bounds__(kThreads) void k_coo_max_keyed(u64* __restrict__ slab, u64 row_pitch, u64 sign_pitch,
                                                             const u32* __restrict__ kslot,
                                                             const u32* __restrict__ cell_key,
                                                             const uint8_t* __restrict__ sign,
                                                             const u16* __restrict__ col,
-                                                            const u64* __restrict__ val, u64 n) {
+                                                            const u64* __restrict__ val, u64 n, u64 nkeys,
+                                                            u32 nsigns, u32 ncols,
+                                                            unsigned long long* __restrict__ skipped) {
   const u64 i = (u64)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
-  const u32 s = kslot[cell_key ? cell_key[i] : i];
-  u64* p = slab + (sign && sign[i] ? sign_pitch : 0) + (u64)col[i] * row_pitch + s;
+  const u64 k = cell_key ? (u64)cell_key[i] : i;
+  const u32 g = sign ? (u32)sign[i] : 0u;
+  const u32 c = col[i];
+  const u32 s = k < nkeys ? kslot[k] : JY_NO_SLOT;
+  if (s >= row_pitch || g >= nsigns || c >= ncols) {
+    atomicAdd(skipped, 1ull);
+    return;
+  }
+  u64* p = slab + (g ? sign_pitch : 0) + (u64)c * row_pitch + s;
   const u64 v = val[i];
   if (v > *p) __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -215,14 +228,16 @@ int32_t jy_counter_coo(jy_engine* eng, int which, int sign, u64 n, const u32* sl
   return JY_OK;
 }
 
-int32_t jy_counter_coo_keyed(jy_engine* eng, int which, u64 n, const u32* kslot, const u32* cell_key,
+int32_t jy_counter_coo_keyed(jy_engine* eng, int which, u64 n, u64 nkeys, const u32* kslot, const u32* cell_key,
                              const uint8_t* sign, const u16* col, const u64* val) {
   if (n == 0) return JY_OK;
   JyTimed tm(eng);
   CounterState& c = eng->cnt[which];
   const u64 blocks = (n + kThreads - 1) / kThreads;
+  const u32 ncols = std::min<u32>((u32)eng->rep_id.size(), c.ccap);
   hipLaunchKernelGGL(k_coo_max_keyed, dim3((u32)blocks), dim3(kThreads), 0, eng->stream, c.slab, c.kcap,
-                     c.ccap * c.kcap, kslot, cell_key, sign, col, val, n);
+                     c.ccap * c.kcap, kslot, cell_key, sign, col, val, n, nkeys, (u32)(which + 1), ncols,
+                     reinterpret_cast<unsigned long long*>(eng->skipped_dev));
   JY_HIP(eng, hipGetLastError());
   return JY_OK;
 }

@@ -38,19 +38,8 @@ namespace {
 constexpr int kT = 256;
 constexpr u32 kMaxShards = 64;
 
-// include/jylis_gpu.h jy_key_owner, on the device (FNV-1a 64 + splitmix64 finaliser)
 __device__ __forceinline__ u32 owner_of(const uint8_t* __restrict__ p, u64 len, u32 S) {
-  u64 h = 0xCBF29CE484222325ull;
-  for (u64 i = 0; i < len; i++) {
-    h ^= p[i];
-    h *= 0x100000001B3ull;
-  }
-  h ^= h >> 30;
-  h *= 0xBF58476D1CE4E5B9ull;
-  h ^= h >> 27;
-  h *= 0x94D049BB133111EBull;
-  h ^= h >> 31;
-  return (u32)(h % S);
+  return jy_dev_key_owner(p, len, S);
 }
 
 // per tile: keys and bytes per owner, one LDS atomic per (wave, owner, quantity)

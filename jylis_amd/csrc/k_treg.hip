@@ -110,19 +110,39 @@ __device__ __forceinline__ void set_one(const TregK& K, u32 s, u64 t, u64 p, u64
 }
 
 // (the host's bound keeps the list from filling; a record past its capacity
-// is never written -- the overflow bit makes the next call fail loudly
-// instead of corrupting memory)
-__device__ __forceinline__ void push_dup(const TregK& K, u32 s, u64 t, u64 p, u64 l) {
+// is never written, the count may pass the capacity but every reader clamps
+// it (fold_count), and the overflow word makes the next call fail loudly --
+// the state then misses that duplicate, memory is never touched past the
+// list).  Returns 1 if pushed, 2 if it overflowed: the wave publishes both
+// through dup_publish.
+__device__ __forceinline__ u32 push_dup(const TregK& K, u32 s, u64 t, u64 p, u64 l) {
   const u32 at = atomicAdd(K.dupn, 1u);
-  if ((u64)at >= K.dup_cap) {
-    if (K.dupflag) __hip_atomic_store(K.dupflag + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    return;
-  }
+  if ((u64)at >= K.dup_cap) return 2u;
   u64x2* r = reinterpret_cast<u64x2*>(K.dups + (u64)at * 4);
   r[0] = u64x2{(u64)s, t};
   r[1] = u64x2{p, l};
-  if (K.dupflag) __hip_atomic_store(K.dupflag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return 1u;
 }
+
+// The host-mapped words behind the host's "nothing was pushed" shortcut
+// (claim_begin): ONE lane of a wave that pushed (or overflowed) stores them
+// with system scope and then waits for the stores to be performed at system
+// scope (release fence) before the wave may end, so by the time the launch's
+// completion event fires the host sees them.  Called by every lane of the
+// wave together; the fence only runs on this rare path.
+__device__ __forceinline__ void dup_publish(const TregK& K, u32 what) {
+  const u32 any = jy_wave_or(what);
+  if (!any || !K.dupflag) return;
+  if (__lane_id() == 0) {
+    if (any & 1u) __hip_atomic_store(K.dupflag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (any & 2u) __hip_atomic_store(K.dupflag + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __atomic_thread_fence(__ATOMIC_RELEASE);  // system scope: the stores above are performed
+  }
+}
+
+// records a fold may read: the count clamped to the list's capacity (a count
+// past it means records were dropped; the overflow word reports that)
+__device__ __forceinline__ u64 fold_count(u32 n, u64 cap) { return (u64)n < cap ? (u64)n : cap; }
 
 // this workgroup's slice of the other claim bitmap (16-B stores)
 __device__ __forceinline__ void clear_slice(const TregK& K) {
@@ -173,11 +193,12 @@ __global__ __launch_bounds__(kThreads) void k_treg_lww(TregK K, const u32* __res
   }
   jy_claim_rows<kUnroll>(valid, s, K.seen, first);
   clear_slice(K);
+  u32 pushed = 0;
 #pragma unroll
   for (int u = 0; u < kUnroll; u++) {
     if (!valid[u]) continue;
     if (!first[u]) {
-      push_dup(K, s[u], t[u], p[u], l[u]);
+      pushed |= push_dup(K, s[u], t[u], p[u], l[u]);
       continue;
     }
     if (kSet) {
@@ -193,6 +214,7 @@ __global__ __launch_bounds__(kThreads) void k_treg_lww(TregK K, const u32* __res
       K.val[s[u]] = TVal{p[u], l[u]};
     }
   }
+  dup_publish(K, pushed);
 }
 
 // Routed runs (receiver side of the exchange, k_route.hip): S source runs
@@ -252,11 +274,12 @@ __global__ __launch_bounds__(kThreads) void k_treg_lww_routed(TregK K, RoutedIn 
     if (valid[u]) t0[u] = K.ts[s[u]];
   jy_claim_rows<U>(valid, s, K.seen, first);
   clear_slice(K);
+  u32 pushed = 0;
 #pragma unroll
   for (int u = 0; u < U; u++) {
     if (!valid[u]) continue;
     if (!first[u]) {
-      push_dup(K, s[u], t[u], p[u], l[u]);
+      pushed |= push_dup(K, s[u], t[u], p[u], l[u]);
       continue;
     }
     if (t[u] >= t0[u] && lww_wins(t[u], t0[u], p[u], l[u], K.val, s[u], K.arena)) {
@@ -264,6 +287,7 @@ __global__ __launch_bounds__(kThreads) void k_treg_lww_routed(TregK K, RoutedIn 
       K.val[s[u]] = TVal{p[u], l[u]};
     }
   }
+  dup_publish(K, pushed);
 }
 
 // The duplicate list, folded in by ONE wave: a chunk of 64 records per pass
@@ -272,7 +296,7 @@ __global__ __launch_bounds__(kThreads) void k_treg_lww_routed(TregK K, RoutedIn 
 // at once and chunks run in list order.  Resets the list.
 template <bool kSet>
 __global__ __launch_bounds__(64) void k_treg_fold(TregK K) {
-  const u32 n = *K.dupn;
+  const u32 n = (u32)fold_count(*K.dupn, K.dup_cap);
   const int lane = threadIdx.x;
   for (u32 j0 = 0; j0 < n; j0 += 64) {
     const u32 j = j0 + lane;
@@ -322,7 +346,8 @@ __global__ __launch_bounds__(kThreads) void k_treg_fold_round(TregK K, const u32
                                                               const u64* __restrict__ in) {
   constexpr int U = 2;
   clear_slice(K);
-  const u64 n = *in_n;
+  const u64 n = fold_count(*in_n, K.dup_cap);  // the input list has the capacity of K's
+  u32 pushed = 0;
   for (u64 b0 = (u64)blockIdx.x * (kThreads * U); b0 < n; b0 += (u64)gridDim.x * (kThreads * U)) {
     const u64 base = b0 + (threadIdx.x >> 6) * (64 * U) + (threadIdx.x & 63);
     u32 s[U];
@@ -352,7 +377,7 @@ __global__ __launch_bounds__(kThreads) void k_treg_fold_round(TregK K, const u32
     for (int u = 0; u < U; u++) {
       if (!valid[u]) continue;
       if (!first[u]) {
-        push_dup(K, s[u], t[u], p[u], l[u]);
+        pushed |= push_dup(K, s[u], t[u], p[u], l[u]);
         continue;
       }
       if (kSet) {
@@ -363,6 +388,7 @@ __global__ __launch_bounds__(kThreads) void k_treg_fold_round(TregK K, const u32
       }
     }
   }
+  dup_publish(K, pushed);
 }
 
 __global__ __launch_bounds__(kThreads) void k_treg_gather(const u64* __restrict__ ts, const TVal* __restrict__ val,
@@ -444,12 +470,17 @@ int32_t ring_note(jy_engine* eng, u64 n) {
   return JY_OK;
 }
 
-int32_t overflow_check(jy_engine* eng) {
+}  // namespace
+
+int32_t jy_treg_overflow_check(jy_engine* eng) {
   const TregState& t = eng->treg;
   if (t.dupflag && __atomic_load_n(t.dupflag + 1, __ATOMIC_ACQUIRE) != 0)
     return eng->fail(JY_ERANGE, "treg duplicate list overflowed (a bound was wrong): state may miss duplicates");
   return JY_OK;
 }
+
+namespace {
+int32_t overflow_check(jy_engine* eng) { return jy_treg_overflow_check(eng); }
 
 int32_t flag_init(jy_engine* eng) {
   TregState& t = eng->treg;
@@ -459,7 +490,9 @@ int32_t flag_init(jy_engine* eng) {
   std::memset(h, 0, 64);
   void* d = nullptr;
   JY_HIP(eng, hipHostGetDevicePointer(&d, h, 0));
-  // completion markers only (the flag is written with system-scope stores): no cache fence
+  // completion markers only: no cache fence on record.  The flag is written
+  // with system-scope stores that the pushing wave waits to be performed
+  // before it ends (dup_publish), so a completed launch's flag is visible
   for (auto& e : t.mev) JY_HIP(eng, hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence));
   t.dupflag = static_cast<u32*>(h);
   t.dupflag_dev = static_cast<u32*>(d);
@@ -547,10 +580,26 @@ int32_t fold_now(jy_engine* eng) {
 // claim state of one launch over n entries: room for n more duplicates
 // (folding the list first when the bound says it might overflow), this
 // launch's bitmap and the other one to clear
+// JY_CFG_TREG_DUP_TEST: a fixed list of this many records that the host
+// never folds or grows ahead of time, so a test can overflow it on purpose
+constexpr u64 kDupTestCap = 64;
+
 int32_t claim_begin(jy_engine* eng, u64 n, u32 nblocks, TregK& K) {
   TregState& t = eng->treg;
   JY_TRY(flag_init(eng));
   JY_TRY(overflow_check(eng));
+  if (eng->cfg.flags & JY_CFG_TREG_DUP_TEST) {
+    if (!t.dups) {
+      JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.dups), kDupTestCap * 32, "treg duplicate list"));
+      JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.dups_alt), kDupTestCap * 32, "treg duplicate list"));
+      if (!t.dupn_alt) JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.dupn_alt), 64, "treg duplicate count"));
+      t.dup_cap = kDupTestCap;
+    }
+    K = state_of(eng);
+    JY_TRY(claim_bits(eng, nblocks, K));
+    t.dup_bound += n;
+    return JY_OK;
+  }
   if (t.dup_bound + n > t.dup_cap && t.dup_cap) {
     // nothing pushed since the last fold (the flag is set by the pushing
     // kernel itself, and only launches still in flight may push): the list's
@@ -659,9 +708,10 @@ int32_t jy_treg_merge_routed(jy_engine* eng, u32 S, u64 cap, u64 cap_byte, const
 int32_t jy_treg_gather(jy_engine* eng, u64 n, const u32* slots, u64* ots, u64* opre, u64* olr) {
   if (n == 0) return JY_OK;
   TregState& t = eng->treg;
+  // the fold is memory-safe after an overflow (fold_count); the caller
+  // reports the overflow once the launches before it have finished
+  // (jy_treg_read after its read-back; a merge's claim_begin)
   JY_TRY(fold_now(eng));
-  JY_HIP(eng, hipStreamSynchronize(eng->stream));  // (the read-back waits for the stream anyway)
-  JY_TRY(overflow_check(eng));
   hipLaunchKernelGGL(k_treg_gather, dim3(blocks(n, kThreads)), dim3(kThreads), 0, eng->stream, t.ts, t.val, slots, n,
                      ots, opre, olr);
   JY_HIP(eng, hipGetLastError());

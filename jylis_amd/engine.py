@@ -92,10 +92,23 @@ class Engine:
         self.device = device
         self.ujson_columns = ujson_columns
 
+    @classmethod
+    def attach(cls, handle, device, ujson_columns=16):
+        """a view of an engine someone else owns (a node's shard, jy_node_engine):
+        close() leaves it alone"""
+        self = cls.__new__(cls)
+        self.lib = _lib.load()
+        self.h = C.c_void_p(handle)
+        self.device = device
+        self.ujson_columns = ujson_columns
+        self._borrowed = True
+        return self
+
     # -- lifecycle ---------------------------------------------------------
     def close(self):
         if getattr(self, "h", None):
-            self.lib.jy_engine_destroy(self.h)
+            if not getattr(self, "_borrowed", False):
+                self.lib.jy_engine_destroy(self.h)
             self.h = None
 
     def __del__(self):

@@ -159,3 +159,28 @@ def collect(procs, q, n, deadline_s=150.0):
         for p in procs:
             p.join(timeout=30)
     return msgs
+
+
+
+def join_rows(ctype, rows):
+    """{key: one-key row} (or split_rows' pairs) -> one table sorted by key
+    (jylis_amd.repo.concat_rows); empty -> an empty table of the type"""
+    from jylis_amd.repo import concat_rows
+    rows = dict(rows)
+    if rows:
+        return concat_rows(sorted(rows.items()))
+    per_key, groups = ROW_SCHEMA[ctype]
+    t = {"key_bytes": np.zeros(0, np.uint8), "key_offs": np.zeros(1, np.uint64)}
+    for c in per_key:
+        t[c] = np.zeros(0, np.uint64)
+    for offs, cols, nested in groups:
+        t[offs] = np.zeros(1, np.uint64)
+        for c in cols:
+            t[c] = np.zeros(0, np.uint64)
+        if nested:
+            t[nested[0]] = np.zeros(1, np.uint64)
+            for c in nested[1]:
+                t[c] = np.zeros(0, np.uint8)
+    if ctype == 2:
+        t["val_bytes"] = np.zeros(0, np.uint8)
+    return t

@@ -140,3 +140,49 @@ def test_many_merges_between_reads(engine, dup_rounds):
     gts, gpre, glr = engine.treg_read(np.arange(n, dtype=np.uint32))
     np.testing.assert_array_equal(gts, best_ts)
     np.testing.assert_array_equal(gpre, best_pre)
+
+
+def test_duplicate_list_overflow_fails_loudly():
+    """A device batch that repeats slots more often than the duplicate list
+    holds (a test-only 64-record list the host never folds ahead of time,
+    JY_CFG_TREG_DUP_TEST): the records past the capacity are dropped, the
+    next call fails with JY_ERANGE, and no memory outside the list is
+    touched -- every slot the batch does not name reads as before."""
+    import torch
+    from jylis_amd._lib import CFG_TREG_DUP_TEST, JY_ERANGE, TREG
+    from jylis_amd.engine import Engine, EngineError
+    eng = Engine(device=0, flags=CFG_TREG_DUP_TEST)
+    try:
+        n = 4096
+        slots = eng.intern(TREG, [b"o%05d" % i for i in range(n)])
+        assert (slots == np.arange(n)).all()
+        rng = np.random.default_rng(3)
+        ts0 = rng.integers(1, 1 << 20, n).astype(np.uint64)
+        pre0 = rng.integers(1, 1 << 63, n, dtype=np.uint64)
+        lr0 = np.full(n, 8, np.uint64)
+        eng.treg_converge(np.arange(n, dtype=np.uint32), ts0, pre0, lr0)
+        before = eng.treg_read(np.arange(n, dtype=np.uint32))
+        # 1,000 entries on 8 slots: 992 duplicates, past the 64-record list
+        m = 1000
+        s = (np.arange(m) % 8).astype(np.uint32)
+        ts = np.full(m, 1 << 40, np.uint64) + np.arange(m, dtype=np.uint64)
+        pre = rng.integers(1, 1 << 63, m, dtype=np.uint64)
+        lr = np.full(m, 8, np.uint64)
+        dev = torch.device("cuda", 0)
+        args = [torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a.view(np.int32)).to(dev)
+                for a in (s, ts, pre, lr)]
+        eng.treg_converge(*args)
+        torch.cuda.synchronize()
+        # the read fails loudly; its outputs are still written: every slot
+        # outside the batch is bit-identical to before
+        out = [np.zeros(n, np.uint64) for _ in range(3)]
+        idx = np.arange(n, dtype=np.uint32)
+        rc = eng.lib.jy_treg_read(eng.h, n, idx.ctypes.data, *(o.ctypes.data for o in out))
+        assert rc == JY_ERANGE, rc
+        for o, b in zip(out, before):
+            np.testing.assert_array_equal(o[8:], b[8:])
+        with pytest.raises(EngineError) as ei:  # sticky: later merges refuse too
+            eng.treg_converge(np.arange(8, dtype=np.uint32), ts0[:8], pre0[:8], lr0[:8])
+        assert ei.value.code == JY_ERANGE
+    finally:
+        eng.close()
