@@ -294,6 +294,128 @@ def ujson_tables(D, seed, rounds=1, R=16, leaves=8, zipf=1.1, ops_per_round=None
     seen = vv.copy()
     np.maximum.at(seen, (cd, cc), cq)
 
+    perm = rng.permutation(D)
+    deltas = []
+    nops = ops_per_round or max(1, D // 2)
+    for _ in range(rounds):
+        deltas.append(_ujson_round(D, R, ids, kb, ko, e_off, ec, eq, ee, vv, seen, perm, rng, nops, zipf))
+    return state, deltas
+
+
+def _ujson_round(D, R, ids, kb, ko, e_off, ec, eq, ee, vv, seen, perm, rng, nops, zipf):
+    """one round of ops (70% INS, 20% RM, 10% CLR on Zipf-hit docs) folded
+    into one delta per doc, vectorised.  Draws the same random numbers in the
+    same order as the per-op form (_ujson_round_ref) and returns the same
+    table bit for bit (tests/test_synth.py); `seen` advances in place."""
+    hit = perm[(rng.zipf(zipf, nops) - 1) % D].astype(np.int64)
+    kinds = rng.random(nops)
+    reps = rng.integers(0, R, nops).astype(np.int64)
+    u = rng.random((nops, 4))
+    u0, u1, u2, u3 = u[:, 0], u[:, 1], u[:, 2], u[:, 3]
+    n_el = (e_off[1:] - e_off[:-1]).astype(np.int64)
+    nd = n_el[hit]
+    seen_f = seen.reshape(-1)  # [D * R] view
+    # INS: a fresh dot of replica r (sometimes past a gap); per (doc, replica)
+    # the seqs continue from `seen` in op order
+    ins = np.nonzero(kinds < 0.7)[0]
+    key = hit[ins] * R + reps[ins]
+    inc = 1 + np.where(u0[ins] < 0.2, 1 + (u1[ins] * 2).astype(np.int64), 0)
+    order = np.argsort(key, kind="stable")
+    ks, io = key[order], inc[order]
+    cs = np.cumsum(io)
+    start = np.r_[True, ks[1:] != ks[:-1]] if len(ks) else np.zeros(0, bool)
+    base = (cs - io)[np.maximum.accumulate(np.where(start, np.arange(len(ks)), 0))] if len(ks) else cs
+    run = cs - base  # inclusive cumsum within each (doc, replica) run
+    q = np.empty(len(ins), np.int64)
+    q[order] = seen_f[ks] + run
+    if len(ks):
+        last = np.r_[ks[1:] != ks[:-1], True]
+        seen_f[ks[last]] = seen_f[ks[last]] + run[last]
+    d_parts, c_parts, q_parts, e_parts = [hit[ins]], [reps[ins]], [q], [1 + (u2[ins] * 63).astype(np.int64)]
+    cl_d, cl_c, cl_q = [hit[ins]], [reps[ins]], [q]
+
+    def expand(sel):
+        """every element of the docs of ops `sel`: (op index, element index)"""
+        cnt = nd[sel]
+        rep = np.repeat(np.arange(len(sel)), cnt)
+        j = np.repeat(e_off[hit[sel]], cnt) + (np.arange(len(rep)) - np.repeat(np.cumsum(cnt) - cnt, cnt))
+        return rep, j.astype(np.int64)
+    # RM one element value of the doc: every dot holding it
+    rm = np.nonzero((kinds >= 0.7) & (kinds < 0.9) & (nd > 0))[0]
+    val = ee[e_off[hit[rm]] + (u1[rm] * nd[rm]).astype(np.int64)]
+    rep, j = expand(rm)
+    m = ee[j] == val[rep]
+    cl_d.append(hit[rm][rep][m])
+    cl_c.append(ec[j][m])
+    cl_q.append(eq[j][m])
+    # CLR: every dot of the doc
+    clr = np.nonzero(kinds >= 0.9)[0]
+    rep, j = expand(clr)
+    cl_d.append(hit[clr][rep])
+    cl_c.append(ec[j])
+    cl_q.append(eq[j])
+    # a version-vector entry carried along (any op kind)
+    vo = np.nonzero(u3 < 0.1)[0]
+    vc = (u2[vo] * R).astype(np.int64)
+    vval = vv[hit[vo], vc]
+    keep = vval > 0
+    vd, vc, vval = hit[vo][keep], vc[keep], vval[keep]
+    # an element the state holds, re-sent
+    rs = np.nonzero((u3 > 0.95) & (nd > 0))[0]
+    j = e_off[hit[rs]] + (u0[rs] * nd[rs]).astype(np.int64)
+    d_parts.append(hit[rs])
+    c_parts.append(ec[j])
+    q_parts.append(eq[j])
+    e_parts.append(ee[j])
+    cl_d.append(hit[rs])
+    cl_c.append(ec[j])
+    cl_q.append(eq[j])
+    return _ujson_fold(D, R, ids, kb, ko, np.unique(hit),
+                       (np.concatenate(d_parts), np.concatenate(c_parts), np.concatenate(q_parts),
+                        np.concatenate(e_parts)),
+                       (vd, vc, vval),
+                       (np.concatenate(cl_d), np.concatenate(cl_c), np.concatenate(cl_q)))
+
+
+def _ujson_fold(D, R, ids, kb, ko, docs, els, vvs, cls):
+    """one round's ops folded into one delta per doc: element dots (a set; a
+    dot always carries one value), vv entries (the state's value), cloud dots
+    (a set), each segment sorted by (column, seq); docs ascending"""
+    def uniq(d, c, q):
+        """first occurrence of every distinct (d, c, q), sorted by (d, c, q)"""
+        o = np.lexsort((q, c, d))
+        if len(o) == 0:
+            return o
+        ds, cs, qs = d[o], c[o], q[o]
+        new = np.r_[True, (ds[1:] != ds[:-1]) | (cs[1:] != cs[:-1]) | (qs[1:] != qs[:-1])]
+        return o[new]
+    ed, ec, eq, ee = els
+    f = uniq(ed, ec, eq)
+    ed, ec, eq, ee = ed[f], ec[f], eq[f], ee[f]
+    vd, vc, vq = vvs
+    f = uniq(vd, vc, np.zeros_like(vd))
+    vd, vc, vq = vd[f], vc[f], vq[f]
+    cd, cc, cq = cls
+    f = uniq(cd, cc, cq)
+    cd, cc, cq = cd[f], cc[f], cq[f]
+    pos = np.full(D, -1, np.int64)
+    pos[docs] = np.arange(len(docs))
+
+    def offs(d):
+        return _excl_cumsum(np.bincount(pos[d], minlength=len(docs)))
+    t = {}
+    t["key_bytes"], t["key_offs"] = gather_bytes(kb, ko, docs) if len(docs) else (np.zeros(0, np.uint8),
+                                                                                  np.zeros(1, np.uint64))
+    t["dot_ids"], t["dot_seqs"], t["elems"] = ids[ec], eq.astype(np.uint64), ee.astype(np.uint64)
+    t["vv_ids"], t["vv_seqs"] = ids[vc], vq.astype(np.uint64)
+    t["cloud_ids"], t["cloud_seqs"] = ids[cc], cq.astype(np.uint64)
+    t["el_offs"], t["vv_offs"], t["cloud_offs"] = offs(ed), offs(vd), offs(cd)
+    return t
+
+
+def _ujson_round_ref(D, R, ids, kb, ko, e_off, ec, eq, ee, vv, seen, perm, rng, nops, zipf):
+    """the per-op form of one ujson_tables round (rounds 1-3 generated with
+    it): the reference _ujson_round is checked against"""
     def doc_elems(d):
         lo, hi = e_off[d], e_off[d + 1]
         return list(zip(ec[lo:hi].tolist(), eq[lo:hi].tolist(), ee[lo:hi].tolist()))
@@ -326,39 +448,34 @@ def ujson_tables(D, seed, rounds=1, R=16, leaves=8, zipf=1.1, ops_per_round=None
         t["el_offs"], t["vv_offs"], t["cloud_offs"] = (np.array(x, np.uint64) for x in (eo, vo, co))
         return t
 
-    perm = rng.permutation(D)
-    deltas = []
-    nops = ops_per_round or max(1, D // 2)
-    for _ in range(rounds):
-        hit = perm[(rng.zipf(zipf, nops) - 1) % D].tolist()
-        kinds = rng.random(nops).tolist()
-        reps = rng.integers(0, R, nops).tolist()
-        u = rng.random((nops, 4)).tolist()
-        folded = {}
-        for d, x, r, (u0, u1, u2, u3) in zip(hit, kinds, reps, u):
-            dvv, dels, dcl = folded.setdefault(d, ({}, {}, set()))
-            els = doc_elems(d)
-            if x < 0.7:  # INS: a fresh dot of replica r (sometimes past a gap)
-                q = int(seen[d, r]) + 1 + (1 + int(u1 * 2) if u0 < 0.2 else 0)
-                seen[d, r] = q
-                dels[(r, q)] = 1 + int(u2 * 63)
-                dcl.add((r, q))
-            elif x < 0.9:  # RM one element value: every dot holding it
-                if els:
-                    e = els[int(u1 * len(els))][2]
-                    dcl.update((c, q) for c, q, v in els if v == e)
-            else:  # CLR
-                dcl.update((c, q) for c, q, _ in els)
-            if u3 < 0.1:  # carry a version-vector entry too
-                c = int(u2 * R)
-                if vv[d, c]:
-                    dvv[c] = max(dvv.get(c, 0), int(vv[d, c]))
-            if u3 > 0.95 and els:  # re-send an element the state holds
-                c, q, v = els[int(u0 * len(els))]
-                dels[(c, q)] = v
-                dcl.add((c, q))
-        deltas.append(table(folded))
-    return state, deltas
+    hit = perm[(rng.zipf(zipf, nops) - 1) % D].tolist()
+    kinds = rng.random(nops).tolist()
+    reps = rng.integers(0, R, nops).tolist()
+    u = rng.random((nops, 4)).tolist()
+    folded = {}
+    for d, x, r, (u0, u1, u2, u3) in zip(hit, kinds, reps, u):
+        dvv, dels, dcl = folded.setdefault(d, ({}, {}, set()))
+        els = doc_elems(d)
+        if x < 0.7:  # INS: a fresh dot of replica r (sometimes past a gap)
+            q = int(seen[d, r]) + 1 + (1 + int(u1 * 2) if u0 < 0.2 else 0)
+            seen[d, r] = q
+            dels[(r, q)] = 1 + int(u2 * 63)
+            dcl.add((r, q))
+        elif x < 0.9:  # RM one element value: every dot holding it
+            if els:
+                e = els[int(u1 * len(els))][2]
+                dcl.update((c, q) for c, q, v in els if v == e)
+        else:  # CLR
+            dcl.update((c, q) for c, q, _ in els)
+        if u3 < 0.1:  # carry a version-vector entry too
+            c = int(u2 * R)
+            if vv[d, c]:
+                dvv[c] = max(dvv.get(c, 0), int(vv[d, c]))
+        if u3 > 0.95 and els:  # re-send an element the state holds
+            c, q, v = els[int(u0 * len(els))]
+            dels[(c, q)] = v
+            dcl.add((c, q))
+    return table(folded)
 
 
 def counter_batch_tables(state_or_delta, replica_id_list, key_tab, prefix=""):

@@ -899,4 +899,194 @@ void or_ujson_touch(void* rp, const char* k, u64 n) {
   r->uj_d[key];
 }
 
+// ---- canonical state digests (the full-size pins of tests/golden) ----------
+// A digest is a wrapping sum over keys of per-key digests, so it does not
+// depend on key or slot order; inside a key a TLOG is a LIST (entry rank in
+// the canonical newest-first order is part of an entry's hash) and UJSON
+// elements, version-vector entries and cloud dots are SETS (summed).  Three
+// entry points compute the same digest: from the oracle's own maps
+// (or_digest_repo), from an oracle-format table (or_digest_table) and from
+// the engine's read-back arrays (or_digest_tlog_handles / _ujson_packed);
+// tests/test_digest.py checks they agree.  out4 = {digest, keys, entries or
+// elements, bytes or cloud dots}.
+}  // extern "C"
+
+namespace {
+inline u64 dmix(u64 x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+inline u64 dcomb(u64 a, u64 b) { return dmix(a ^ dmix(b)); }
+inline u64 dbytes(const uint8_t* p, u64 n) {
+  u64 h = 0xCBF29CE484222325ull;
+  for (u64 i = 0; i < n; i++) {
+    h ^= p[i];
+    h *= 0x100000001B3ull;
+  }
+  return dcomb(h, n);
+}
+enum : u64 { kTagLog = 0x7100, kTagEnt = 0x7200, kTagDoc = 0x7300, kTagEl = 0x7400, kTagVV = 0x7500, kTagCl = 0x7600 };
+inline u64 d_log(u64 kh, u64 cutoff) { return dcomb(kh, dcomb(kTagLog, cutoff)); }
+inline u64 d_ent(u64 kh, u64 rank, u64 ts, u64 vh) { return dcomb(kh, dcomb(kTagEnt ^ (rank << 16), dcomb(ts, vh))); }
+inline u64 d_doc(u64 kh) { return dcomb(kh, kTagDoc); }
+inline u64 d_el(u64 kh, u64 id, u64 seq, u64 elem) { return dcomb(kh, dcomb(kTagEl, dcomb(id, dcomb(seq, elem)))); }
+inline u64 d_vv(u64 kh, u64 id, u64 n) { return dcomb(kh, dcomb(kTagVV, dcomb(id, n))); }
+inline u64 d_cl(u64 kh, u64 id, u64 seq) { return dcomb(kh, dcomb(kTagCl, dcomb(id, seq))); }
+inline u64 dstr(const std::string& s) { return dbytes(reinterpret_cast<const uint8_t*>(s.data()), s.size()); }
+}  // namespace
+
+extern "C" {
+
+int32_t or_digest_repo(void* rp, u64* out4) {
+  const Repo& r = *static_cast<Repo*>(rp);
+  u64 d = 0, nk = 0, ni = 0, nb = 0;
+  if (r.type == T_TLOG) {
+    for (const auto& kv : r.tl) {
+      const u64 kh = dstr(kv.first);
+      d += d_log(kh, kv.second.cutoff);
+      u64 rank = 0;
+      for (const auto& e : kv.second.values) {
+        d += d_ent(kh, rank++, e.ts, dstr(e.value));
+        nb += e.value.size();
+      }
+      ni += kv.second.values.size();
+      nk++;
+    }
+  } else if (r.type == T_UJSON) {
+    for (const auto& kv : r.uj) {
+      const u64 kh = dstr(kv.first);
+      d += d_doc(kh);
+      for (const auto& e : kv.second.map) d += d_el(kh, e.first.id, e.first.seq, e.second);
+      for (const auto& c : kv.second.ctx.complete)
+        if (c.second) d += d_vv(kh, c.first, c.second);
+      for (const auto& c : kv.second.ctx.cloud) d += d_cl(kh, c.id, c.seq);
+      ni += kv.second.map.size();
+      nb += kv.second.ctx.cloud.size();
+      nk++;
+    }
+  } else {
+    return -1;
+  }
+  out4[0] = d;
+  out4[1] = nk;
+  out4[2] = ni;
+  out4[3] = nb;
+  return 0;
+}
+
+int32_t or_digest_table(int32_t type, void* tp, u64* out4) {
+  const Table& t = *static_cast<Table*>(tp);
+  size_t nkb, nko;
+  const uint8_t* kb = arr<uint8_t>(t, "key_bytes", &nkb);
+  const u64* ko = arr<u64>(t, "key_offs", &nko);
+  if (!ko || nko == 0) return -1;
+  const u64 n = nko - 1;
+  u64 d = 0, ni = 0, nb = 0;
+  if (type == T_TLOG) {
+    size_t a, b, c, e, f;
+    const u64* cut = arr<u64>(t, "cutoff", &a);
+    const u64* eo = arr<u64>(t, "ent_offs", &b);
+    const u64* ts = arr<u64>(t, "ts", &c);
+    const uint8_t* vb = arr<uint8_t>(t, "val_bytes", &e);
+    const u64* vo = arr<u64>(t, "val_offs", &f);
+    for (u64 i = 0; i < n; i++) {
+      const u64 kh = dbytes(kb + ko[i], ko[i + 1] - ko[i]);
+      d += d_log(kh, cut[i]);
+      for (u64 j = eo[i]; j < eo[i + 1]; j++) d += d_ent(kh, j - eo[i], ts[j], dbytes(vb + vo[j], vo[j + 1] - vo[j]));
+    }
+    ni = eo[n];
+    nb = vo[ni];
+  } else if (type == T_UJSON) {
+    size_t z;
+    const u64 *eo = arr<u64>(t, "el_offs", &z), *di = arr<u64>(t, "dot_ids", &z), *dq = arr<u64>(t, "dot_seqs", &z),
+              *el = arr<u64>(t, "elems", &z), *vo = arr<u64>(t, "vv_offs", &z), *vi = arr<u64>(t, "vv_ids", &z),
+              *vs = arr<u64>(t, "vv_seqs", &z), *co = arr<u64>(t, "cloud_offs", &z),
+              *ci = arr<u64>(t, "cloud_ids", &z), *cq = arr<u64>(t, "cloud_seqs", &z);
+    for (u64 i = 0; i < n; i++) {
+      const u64 kh = dbytes(kb + ko[i], ko[i + 1] - ko[i]);
+      d += d_doc(kh);
+      for (u64 j = eo[i]; j < eo[i + 1]; j++) d += d_el(kh, di[j], dq[j], el[j]);
+      for (u64 j = vo[i]; j < vo[i + 1]; j++)
+        if (vs[j]) d += d_vv(kh, vi[j], vs[j]);
+      for (u64 j = co[i]; j < co[i + 1]; j++) d += d_cl(kh, ci[j], cq[j]);
+    }
+    ni = eo[n];
+    nb = co[n];
+  } else {
+    return -1;
+  }
+  out4[0] = d;
+  out4[1] = n;
+  out4[2] = ni;
+  out4[3] = nb;
+  return 0;
+}
+
+// the engine's TLOG read-back: entries newest first per key (offs), values as
+// handles (pre = first 8 bytes big-endian; lr = arena offset << 24 | length)
+int32_t or_digest_tlog_handles(u64 n, const uint8_t* kb, const u64* ko, const u64* cut, const u64* eo, const u64* ts,
+                               const u64* pre, const u64* lr, const uint8_t* arena, u64 alen, u64* out4) {
+  u64 d = 0, nb = 0;
+  std::vector<uint8_t> buf;
+  for (u64 i = 0; i < n; i++) {
+    const u64 kh = dbytes(kb + ko[i], ko[i + 1] - ko[i]);
+    d += d_log(kh, cut[i]);
+    for (u64 j = eo[i]; j < eo[i + 1]; j++) {
+      const u64 len = lr[j] & ((1ull << 24) - 1), off = lr[j] >> 24;
+      u64 vh;
+      if (len <= 8) {
+        uint8_t b[8];
+        for (int q = 0; q < 8; q++) b[q] = (uint8_t)(pre[j] >> (56 - 8 * q));
+        vh = dbytes(b, len);
+      } else {
+        if (off + len > alen) return -2;
+        vh = dbytes(arena + off, len);
+      }
+      d += d_ent(kh, j - eo[i], ts[j], vh);
+      nb += len;
+    }
+  }
+  out4[0] = d;
+  out4[1] = n;
+  out4[2] = eo[n];
+  out4[3] = nb;
+  return 0;
+}
+
+// the engine's UJSON read-back: dots packed (column << 48 | seq), vv dense
+// [n][R] by column, col_ids[column] = the replica identity
+int32_t or_digest_ujson_packed(u64 n, const uint8_t* kb, const u64* ko, const u64* eo, const u64* dots,
+                               const u64* elems, const u64* vv, u64 R, const u64* co, const u64* cloud,
+                               const u64* col_ids, u64 ncols, u64* out4) {
+  const u64 mask = (1ull << 48) - 1;
+  u64 d = 0;
+  for (u64 i = 0; i < n; i++) {
+    const u64 kh = dbytes(kb + ko[i], ko[i + 1] - ko[i]);
+    d += d_doc(kh);
+    for (u64 j = eo[i]; j < eo[i + 1]; j++) {
+      const u64 c = dots[j] >> 48;
+      if (c >= ncols) return -2;
+      d += d_el(kh, col_ids[c], dots[j] & mask, elems[j]);
+    }
+    for (u64 c = 0; c < R; c++) {
+      const u64 v = vv[i * R + c];
+      if (!v) continue;
+      if (c >= ncols) return -2;
+      d += d_vv(kh, col_ids[c], v);
+    }
+    for (u64 j = co[i]; j < co[i + 1]; j++) {
+      const u64 c = cloud[j] >> 48;
+      if (c >= ncols) return -2;
+      d += d_cl(kh, col_ids[c], cloud[j] & mask);
+    }
+  }
+  out4[0] = d;
+  out4[1] = n;
+  out4[2] = eo[n];
+  out4[3] = co[n];
+  return 0;
+}
+
 }  // extern "C"

@@ -62,6 +62,10 @@ def load():
         "or_ujson_rm": (None, [P, C.c_char_p, U64, U64]),
         "or_ujson_clr": (None, [P, C.c_char_p, U64]),
         "or_ujson_touch": (None, [P, C.c_char_p, U64]),
+        "or_digest_repo": (I32, [P, P]),
+        "or_digest_table": (I32, [I32, P, P]),
+        "or_digest_tlog_handles": (I32, [U64, P, P, P, P, P, P, P, P, U64, P]),
+        "or_digest_ujson_packed": (I32, [U64, P, P, P, P, P, P, U64, P, P, P, U64, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -235,3 +239,54 @@ class Repo:
 def split_keys(table):
     kb, ko = table["key_bytes"], table["key_offs"]
     return [bytes(kb[ko[i]:ko[i + 1]]) for i in range(len(ko) - 1)]
+
+
+# ---- canonical state digests (tests/golden full-size pins; see or_digest_* in
+# jy_oracle.cpp): {digest, keys, entries / elements, value bytes / cloud dots}
+
+def _digest_out(rc, out):
+    if rc != 0:
+        raise ValueError(f"digest failed ({rc})")
+    return tuple(int(x) for x in out)
+
+
+def digest_repo(repo):
+    out = np.zeros(4, np.uint64)
+    return _digest_out(load().or_digest_repo(repo.h, out.ctypes.data), out)
+
+
+def digest_table(ctype, table):
+    out = np.zeros(4, np.uint64)
+    t = _table_in(table)
+    try:
+        return _digest_out(load().or_digest_table(ctype, t, out.ctypes.data), out)
+    finally:
+        load().or_table_free(t)
+
+
+def _c(a, dt):
+    a = np.ascontiguousarray(a, dt)
+    return a, a.ctypes.data
+
+
+def digest_tlog_handles(kb, ko, cut, eo, ts, pre, lr, arena):
+    """the engine's TLOG read-back (value handles + the arena bytes)"""
+    keep = [_c(kb, np.uint8), _c(ko, np.uint64), _c(cut, np.uint64), _c(eo, np.uint64), _c(ts, np.uint64),
+            _c(pre, np.uint64), _c(lr, np.uint64), _c(arena, np.uint8)]
+    out = np.zeros(4, np.uint64)
+    n = len(keep[1][0]) - 1
+    rc = load().or_digest_tlog_handles(n, *(p for _, p in keep[:7]), keep[7][1], len(keep[7][0]), out.ctypes.data)
+    return _digest_out(rc, out)
+
+
+def digest_ujson_packed(kb, ko, eo, dots, elems, vv, co, cloud, col_ids):
+    """the engine's UJSON read-back (packed dots, dense vv [n][R])"""
+    vv = np.ascontiguousarray(vv, np.uint64)
+    R = vv.shape[1] if vv.ndim == 2 else 0
+    keep = [_c(kb, np.uint8), _c(ko, np.uint64), _c(eo, np.uint64), _c(dots, np.uint64), _c(elems, np.uint64),
+            (vv, vv.ctypes.data), _c(co, np.uint64), _c(cloud, np.uint64), _c(col_ids, np.uint64)]
+    out = np.zeros(4, np.uint64)
+    n = len(keep[1][0]) - 1
+    rc = load().or_digest_ujson_packed(n, keep[0][1], keep[1][1], keep[2][1], keep[3][1], keep[4][1], keep[5][1], R,
+                                       keep[6][1], keep[7][1], keep[8][1], len(keep[8][0]), out.ctypes.data)
+    return _digest_out(rc, out)

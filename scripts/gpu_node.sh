@@ -5,6 +5,7 @@ set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+export JY_PROGRESS=$PWD/gpurun_out/progress_${TAG:-r04}.log
 TAG=${TAG:-r04}
 timeout -k 10 600 python -u -m pytest tests/test_node_gpu.py tests/test_parity_treg.py -x -v --timeout 240 \
   --timeout-method thread > gpurun_out/pytest_node_$TAG.log 2>&1

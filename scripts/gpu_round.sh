@@ -6,6 +6,7 @@ set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+export JY_PROGRESS=$PWD/gpurun_out/progress_${TAG:-r04}.log
 TAG=${TAG:-r03}
 if [ -z "${SKIP_TESTS:-}" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread \

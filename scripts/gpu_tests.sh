@@ -5,6 +5,7 @@ set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+export JY_PROGRESS=$PWD/gpurun_out/progress_${TAG:-r04}.log
 TAG=${TAG:-r02}
 timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread \
   ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu_$TAG.log 2>&1
