@@ -444,6 +444,13 @@ typedef struct jy_node_config {
 
 int32_t jy_node_unique_id(uint8_t* id_out /* 128 bytes */);
 int32_t jy_node_create(const jy_node_config* cfg, jy_node** out);
+/* the one-process node of an FFI host without struct layouts (the Pony
+ * host): nshards shards on devices[0..nshards), every one local, an RCCL
+ * communicator of its own (fabric JY_FABRIC_RCCL) or device copies */
+int32_t jy_node_create_local(uint32_t nshards, const int32_t* devices, uint32_t fabric, const jy_config* engine,
+                             jy_node** out);
+/* GPUs visible to this process (0 without a GPU or HIP runtime) */
+int32_t jy_device_count(void);
 void jy_node_destroy(jy_node* node);
 const char* jy_node_last_error(const jy_node* node);
 uint32_t jy_node_nshards(const jy_node* node);

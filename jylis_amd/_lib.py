@@ -125,6 +125,8 @@ SIGNATURES = {
     "jy_ujson_converge_routed": (I32, [P, U32, U64, U64, U64, U64, P]),
     "jy_node_unique_id": (I32, [P]),
     "jy_node_create": (I32, [P, P]),
+    "jy_node_create_local": (I32, [U32, P, U32, P, P]),
+    "jy_device_count": (I32, []),
     "jy_node_destroy": (None, [P]),
     "jy_node_last_error": (C.c_char_p, [P]),
     "jy_node_nshards": (U32, [P]),

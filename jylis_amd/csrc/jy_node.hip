@@ -908,6 +908,27 @@ int32_t jy_node_create(const jy_node_config* cfg, jy_node** out) {
   return JY_OK;
 }
 
+int32_t jy_node_create_local(uint32_t nshards, const int32_t* devices, uint32_t fabric, const jy_config* engine,
+                             jy_node** out) {
+  *out = nullptr;
+  if (nshards == 0 || nshards > kMaxS || !devices) return JY_EINVAL;
+  jy_node_config cfg;
+  std::memset(&cfg, 0, sizeof(cfg));
+  cfg.nshards = cfg.nlocal = nshards;
+  cfg.rank0 = 0;
+  cfg.fabric = fabric;
+  for (u32 i = 0; i < nshards; i++) cfg.devices[i] = devices[i];
+  if (engine) cfg.engine = *engine;
+  else jy_config_default(&cfg.engine);
+  return jy_node_create(&cfg, out);
+}
+
+int32_t jy_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
 const char* jy_node_last_error(const jy_node* nd) { return nd ? nd->err.c_str() : "null node"; }
 uint32_t jy_node_nshards(const jy_node* nd) { return nd ? nd->S : 0; }
 

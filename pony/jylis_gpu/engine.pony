@@ -2,31 +2,67 @@
 The engine handle and the marshalling every GPU repo shares (package jylis).
 NOT COMPILE-CHECKED: unbuilt here (no ponyc); see INTEGRATION.md.
 
-A GPU repo holds `(_Engine | None)`: `RepoAny.create` (repo_manager.pony:6)
+A GPU repo holds `(_Node | None)`: `RepoAny.create` (repo_manager.pony:6)
 is not partial, so a missing GPU is reported per call (`_Fail`), not at
 construction.
 """
 use "collections"
 use "resp"
 
+class _Node
+  """Every GPU of this Jylis node behind one handle (jy_node_*), one node per
+  Database and type: keys are hash-sharded over the GPUs (jy_node_shard_of).
+  A decoded peer batch goes out in ONE call (jy_node_*_converge): the library
+  hashes and regroups the keys on the device, moves each owner's part over
+  RCCL, interns and merges it there.  Reads, local writes and flushes go to
+  the key's owner shard (`owner`, `shards`).  Owned by the RepoManager actor
+  that owns the repo, so calls are never concurrent."""
+  let ptr: Pointer[None] tag
+  let shards: Array[_Engine] = shards.create()   // one view per GPU, index = shard
+  let _col: U32                                   // this replica's column (the same on every shard)
+
+  new create(identity: U64) ? =>
+    let ndev = @jy_device_count()
+    if ndev <= 0 then error end
+    let devs = Array[I32]
+    for d in Range[I32](0, ndev) do devs.push(d) end
+    let cfg = JyConfig
+    @jy_config_default(cfg)
+    var p = Pointer[None]
+    if @jy_node_create_local(ndev.u32(), devs.cpointer(), JyFabricRccl(), cfg, addressof p) != 0 then error end
+    ptr = p
+    var c: U32 = 0
+    if @jy_node_replica_col(ptr, identity, addressof c) != 0 then error end
+    _col = c
+    for s in Range[U32](0, ndev.u32()) do shards.push(_Engine.view(@jy_node_engine(ptr, s), c)) end
+
+  fun col(): U32 => _col
+
+  fun check(rc: I32) ? => if rc != 0 then error end
+
+  fun owner(key: String): _Engine ? =>
+    """the shard that owns `key` (jy_key_owner over the node's GPUs)"""
+    shards(@jy_node_shard_of(ptr, key.cpointer(), key.size().u64()).usize())?
+
+  fun ref replica_col(id: U64): U16 ? =>
+    """a peer's column, registered on every shard in one order"""
+    var c: U32 = 0
+    check(@jy_node_replica_col(ptr, id, addressof c))?
+    c.u16()
+
+  fun _final() => @jy_node_destroy(ptr)
+
 class _Engine
-  """One engine per Database and type (one GPU, one key shard); owned by the
-  RepoManager actor that owns the repo, so calls are never concurrent."""
+  """One shard's engine (one GPU): a view the node owns.  Slot -> key names
+  are kept per shard for flushes and GETs."""
   let ptr: Pointer[None] tag
   let _names: Array[String] = _names.create()    // slot -> key (slots are dense)
   let _col: U32                                   // this replica's column
   var _arena_live: Array[U64] = Array[U64].init(0, 5)  // bytes kept by the last collect, per type
 
-  new create(identity: U64, device: I32 = 0) ? =>
-    let cfg = JyConfig
-    @jy_config_default(cfg)
-    cfg.device = device
-    var p = Pointer[None]
-    if @jy_engine_create(cfg, addressof p) != 0 then error end
+  new view(p: Pointer[None] tag, col': U32) =>
     ptr = p
-    var c: U32 = 0
-    if @jy_replica_col(ptr, identity, addressof c) != 0 then error end
-    _col = c
+    _col = col'
 
   fun col(): U32 => _col
 
@@ -82,10 +118,6 @@ class _Engine
     @jy_replica_id(ptr, col', addressof id)
     id
 
-  fun ref replica_col(id: U64): U16 ? =>
-    var c: U32 = 0
-    check(@jy_replica_col(ptr, id, addressof c))?
-    c.u16()
 
   fun ref pack(ty: I32, values: Array[String] box): (Array[U64], Array[U64]) ? =>
     """value strings -> (pre, lr) handles (long values into the arena)"""
@@ -130,8 +162,6 @@ class _Engine
       end
     end
 
-  fun _final() => @jy_engine_destroy(ptr)
-
 class _Strs
   """strings marshalled as bytes + offsets (the C-ABI's key / value columns)"""
   let bytes: Array[U8] = bytes.create()
@@ -143,6 +173,15 @@ class _Strs
       bytes.append(k)
       offs.push(bytes.size().u64())
     end
+
+class _Vals
+  """value strings marshalled as bytes + offsets, built as they come"""
+  let bytes: Array[U8] = bytes.create()
+  let offs: Array[U64] = [0]
+
+  fun ref push(v: String box) =>
+    bytes.append(v)
+    offs.push(bytes.size().u64())
 
 primitive _Fail
   fun apply(resp: Respond): Bool =>

@@ -103,6 +103,31 @@ use @jy_ujson_flush[I32](eng: Pointer[None] tag, cap_docs: U64, cap_el: U64, cap
   cloud_out: Pointer[U64] tag, ndocs_out: Pointer[U64] tag, nel_out: Pointer[U64] tag,
   ncloud_out: Pointer[U64] tag, mem: I32)
 
+// ---- the node: every GPU of this Jylis node (jy_node.hip) ---------------------
+use @jy_device_count[I32]()
+use @jy_node_create_local[I32](nshards: U32, devices: Pointer[I32] tag, fabric: U32, cfg: JyConfig tag,
+  out: Pointer[Pointer[None] tag] tag)
+use @jy_node_destroy[None](node: Pointer[None] tag)
+use @jy_node_last_error[Pointer[U8] val](node: Pointer[None] tag)
+use @jy_node_engine[Pointer[None] tag](node: Pointer[None] tag, shard: U32)
+use @jy_node_shard_of[U32](node: Pointer[None] tag, key: Pointer[U8] tag, len: U64)
+use @jy_node_replica_col[I32](node: Pointer[None] tag, id: U64, col: Pointer[U32] tag)
+use @jy_node_sync[I32](node: Pointer[None] tag)
+use @jy_node_counter_converge[I32](node: Pointer[None] tag, ty: I32, n: U64, key_bytes: Pointer[U8] tag,
+  key_offs: Pointer[U64] tag, cell_offs: Pointer[U64] tag, sign: Pointer[U8] tag, col: Pointer[U16] tag,
+  value: Pointer[U64] tag, mem: I32)
+use @jy_node_treg_converge[I32](node: Pointer[None] tag, n: U64, key_bytes: Pointer[U8] tag,
+  key_offs: Pointer[U64] tag, ts: Pointer[U64] tag, val_bytes: Pointer[U8] tag, val_offs: Pointer[U64] tag,
+  mem: I32)
+use @jy_node_tlog_converge[I32](node: Pointer[None] tag, n: U64, key_bytes: Pointer[U8] tag,
+  key_offs: Pointer[U64] tag, cutoff: Pointer[U64] tag, ent_offs: Pointer[U64] tag, ts: Pointer[U64] tag,
+  val_bytes: Pointer[U8] tag, val_offs: Pointer[U64] tag, mem: I32)
+use @jy_node_ujson_converge[I32](node: Pointer[None] tag, n: U64, key_bytes: Pointer[U8] tag,
+  key_offs: Pointer[U64] tag, el_offs: Pointer[U64] tag, dots: Pointer[U64] tag, elems: Pointer[U64] tag,
+  vv_offs: Pointer[U64] tag, vv: Pointer[U64] tag, cloud_offs: Pointer[U64] tag, cloud: Pointer[U64] tag,
+  mem: I32)
+
+primitive JyFabricRccl fun apply(): U32 => 0
 primitive JyHost fun apply(): I32 => 0
 primitive JyGCOUNT fun apply(): I32 => 0
 primitive JyPNCOUNT fun apply(): I32 => 1

@@ -4,42 +4,50 @@ and jylis/repo_tlog.pony behind RepoAny (jylis/repo_manager.pony:5-10).
 NOT COMPILE-CHECKED: unbuilt here (no ponyc); INTEGRATION.md.
 
 converge queues the pair and the next entry point merges the whole queue in
-one engine call (see repo_counters_gpu.pony).  Writes and flush_deltas run on
-the engine (jy_treg_set / _flush, jy_tlog_write / _flush); flush rebuilds the
-pony-crdt deltas from the engine's pending registers / logs.  Values travel
-as (pre, lr) handles (jy_values_pack); reads turn them back into Strings.
+ONE node call (jy_node_treg_converge / jy_node_tlog_converge: key strings,
+timestamps and value strings as bytes + offsets; the library routes every
+key to the GPU that owns it, where its value bytes land in that shard's
+arena).  Writes and reads go to the key's owner shard (jy_treg_set / _read,
+jy_tlog_write / _read); deltas_size and flush_deltas walk every shard, and
+flush rebuilds the pony-crdt deltas from the pending registers / logs.
+Values travel as (pre, lr) handles on a shard (jy_values_pack); reads turn
+them back into Strings.
 """
 use "collections"
 use "crdt"
 use "resp"
 
 class RepoTREGGpu
-  let _eng: (_Engine | None)
+  let _node: (_Node | None)
   embed _in: Array[(String, Any box)] = _in.create()
 
   new create(identity': U64) =>
-    _eng = try _Engine(identity')? else None end
+    _node = try _Node(identity')? else None end
 
   fun ref deltas_size(): USize =>
     """the heartbeat's call (repo_manager.pony:86-90): applies every queued
     peer pair first, so a replica with no local commands still converges
     each tick"""
     _drain()
-    match _eng
-    | let e: _Engine =>
-      var n: U64 = 0
-      @jy_treg_deltas_size(e.ptr, addressof n)
-      n.usize()
-    else 0
+    var total: USize = 0
+    match _node
+    | let n: _Node =>
+      for e in n.shards.values() do
+        var k: U64 = 0
+        @jy_treg_deltas_size(e.ptr, addressof k)
+        total = total + k.usize()
+      end
     end
+    total
 
   fun ref flush_deltas(): Array[(String, Any box)] box =>
     """repo_treg.pony:18-22: every pending key with its delta register"""
     _drain()
     let out = Array[(String, Any box)]
-    match _eng
-    | let e: _Engine =>
-      try
+    match _node
+    | let node: _Node =>
+      for e in node.shards.values() do try
+        e.sync_names(JyTREG())
         var n: U64 = 0
         e.check(@jy_treg_deltas_size(e.ptr, addressof n))?
         let cap = n.usize().max(1)
@@ -55,7 +63,7 @@ class RepoTREGGpu
           d.update(e.unpack(JyTREG(), pre(i)?, lr(i)?), ts(i)?)
           out.push((e.name(slots(i)?), d))
         end
-      end
+      end end
     end
     out
 
@@ -67,11 +75,11 @@ class RepoTREGGpu
 
   fun ref _drain() =>
     if _in.size() == 0 then return end
-    match _eng
-    | let e: _Engine =>
+    match _node
+    | let n: _Node =>
       try
         let keys = Array[String]
-        let vals = Array[String]
+        let vals = _Vals
         let ts = Array[U64]
         for (k, d') in _in.values() do
           match d'
@@ -79,13 +87,12 @@ class RepoTREGGpu
           end
         end
         if keys.size() > 0 then
-          let slots = e.intern(JyTREG(), keys)?
-          (let pre, let lr) = e.pack(JyTREG(), vals)?
-          e.check(@jy_treg_converge(e.ptr, slots.size().u64(), slots.cpointer(), ts.cpointer(),
-            pre.cpointer(), lr.cpointer(), JyHost()))?
+          let m = _Strs(keys)
+          n.check(@jy_node_treg_converge(n.ptr, keys.size().u64(), m.bytes.cpointer(), m.offs.cpointer(),
+            ts.cpointer(), vals.bytes.cpointer(), vals.offs.cpointer(), JyHost()))?
         end
       end
-      e.maybe_collect(JyTREG())
+      for e in n.shards.values() do e.maybe_collect(JyTREG()) end
     end
     _in.clear()
 
@@ -99,8 +106,9 @@ class RepoTREGGpu
   fun ref get(resp: Respond, key: String): Bool =>
     """repo_treg.pony:54-63: [value, timestamp], or null for a missing key"""
     _drain()
-    match _eng
-    | let e: _Engine =>
+    match _node
+    | let n: _Node =>
+      let e = try n.owner(key)? else return _Fail(resp) end
       var slot = e.lookup(JyTREG(), key)
       if slot == JyNoSlot() then resp.null(); return false end
       var ts: U64 = 0
@@ -117,9 +125,10 @@ class RepoTREGGpu
   fun ref set(resp: Respond, key: String, value: String, timestamp: U64): Bool =>
     """repo_treg.pony:65-68"""
     _drain()
-    match _eng
-    | let e: _Engine =>
+    match _node
+    | let n: _Node =>
       try
+        let e = n.owner(key)?
         let slots = e.intern(JyTREG(), [key])?
         (let pre, let lr) = e.pack(JyTREG(), [value])?
         var ts = timestamp
@@ -140,37 +149,41 @@ primitive _TlogOp
   fun clr(): U8 => 3
 
 class RepoTLOGGpu
-  let _eng: (_Engine | None)
+  let _node: (_Node | None)
   embed _in: Array[(String, Any box)] = _in.create()
 
   new create(identity': U64) =>
-    _eng = try _Engine(identity')? else None end
+    _node = try _Node(identity')? else None end
 
   fun ref deltas_size(): USize =>
     """the heartbeat's call (repo_manager.pony:86-90): applies every queued
     peer pair first, so a replica with no local commands still converges
     each tick"""
     _drain()
-    match _eng
-    | let e: _Engine =>
-      var n: U64 = 0
-      @jy_tlog_deltas_size(e.ptr, addressof n)
-      n.usize()
-    else 0
+    var total: USize = 0
+    match _node
+    | let n: _Node =>
+      for e in n.shards.values() do
+        var k: U64 = 0
+        @jy_tlog_deltas_size(e.ptr, addressof k)
+        total = total + k.usize()
+      end
     end
+    total
 
   fun ref flush_deltas(): Array[(String, Any box)] box =>
     """repo_tlog.pony:21-25: every pending key with its delta log"""
     _drain()
     let out = Array[(String, Any box)]
-    match _eng
-    | let e: _Engine =>
-      try
+    match _node
+    | let node: _Node =>
+      for e in node.shards.values() do try
+        e.sync_names(JyTLOG())
         var nk: U64 = 0
         var ne: U64 = 0
         e.check(@jy_tlog_flush(e.ptr, 0, 0, Pointer[U32], Pointer[U64], Pointer[U64], Pointer[U64],
           Pointer[U64], Pointer[U64], addressof nk, addressof ne, JyHost()))?
-        if nk == 0 then return out end
+        if nk == 0 then continue end
         let slots = Array[U32].init(0, nk.usize())
         let cut = Array[U64].init(0, nk.usize())
         let offs = Array[U64].init(0, nk.usize() + 1)
@@ -187,7 +200,7 @@ class RepoTLOGGpu
           end
           out.push((e.name(slots(i)?), d))
         end
-      end
+      end end
     end
     out
 
@@ -198,15 +211,16 @@ class RepoTLOGGpu
     if _in.size() >= _DrainBound() then _drain() end
 
   fun ref _drain() =>
-    """every queued TLog delta in one jy_tlog_converge (CSR of entries)"""
+    """every queued TLog delta in one node call (CSR of entries, values as
+    bytes + offsets; jy_node_tlog_converge routes each log to its owner)"""
     if _in.size() == 0 then return end
-    match _eng
-    | let e: _Engine =>
+    match _node
+    | let n: _Node =>
       try
         let keys = Array[String]
         let cut = Array[U64]
         let offs: Array[U64] = [0]
-        let vals = Array[String]
+        let vals = _Vals
         let ts = Array[U64]
         for (k, d') in _in.values() do
           match d'
@@ -214,17 +228,17 @@ class RepoTLOGGpu
             keys.push(k)
             cut.push(d.cutoff())
             for (v, t) in d.entries() do vals.push(v); ts.push(t) end   // newest first
-            offs.push(vals.size().u64())
+            offs.push(ts.size().u64())
           end
         end
         if keys.size() > 0 then
-          let slots = e.intern(JyTLOG(), keys)?
-          (let pre, let lr) = e.pack(JyTLOG(), vals)?
-          e.check(@jy_tlog_converge(e.ptr, slots.size().u64(), slots.cpointer(), cut.cpointer(),
-            offs.cpointer(), vals.size().u64(), ts.cpointer(), pre.cpointer(), lr.cpointer(), JyHost()))?
+          let m = _Strs(keys)
+          n.check(@jy_node_tlog_converge(n.ptr, keys.size().u64(), m.bytes.cpointer(), m.offs.cpointer(),
+            cut.cpointer(), offs.cpointer(), ts.cpointer(), vals.bytes.cpointer(), vals.offs.cpointer(),
+            JyHost()))?
         end
       end
-      e.maybe_collect(JyTLOG())
+      for e in n.shards.values() do e.maybe_collect(JyTLOG()) end
     end
     _in.clear()
 
@@ -248,8 +262,9 @@ class RepoTLOGGpu
     (repo_tlog.pony:85-111): one jy_tlog_write command"""
     var ts = ts'
     _drain()
-    match _eng
-    | let e: _Engine =>
+    match _node
+    | let n: _Node =>
+      let e = n.owner(key)?
       let slots = e.intern(JyTLOG(), [key])?
       (let pre, let lr) = e.pack(JyTLOG(), [value])?
       var o = op
@@ -265,8 +280,9 @@ class RepoTLOGGpu
   fun ref get(resp: Respond, key: String, count: USize): Bool =>
     """repo_tlog.pony:69-83: at most `count` entries, newest first"""
     _drain()
-    match _eng
-    | let e: _Engine =>
+    match _node
+    | let n: _Node =>
+      let e = try n.owner(key)? else return _Fail(resp) end
       var slot = e.lookup(JyTLOG(), key)
       if slot == JyNoSlot() then resp.array_start(0); return false end
       var len: U64 = 0
@@ -292,8 +308,9 @@ class RepoTLOGGpu
   fun ref size(resp: Respond, key: String, cutoff: Bool): Bool =>
     """SIZE / CUTOFF (repo_tlog.pony:90-96): 0 for a missing key"""
     _drain()
-    match _eng
-    | let e: _Engine =>
+    match _node
+    | let n: _Node =>
+      let e = try n.owner(key)? else return _Fail(resp) end
       var slot = e.lookup(JyTLOG(), key)
       var len: U64 = 0
       var cut: U64 = 0

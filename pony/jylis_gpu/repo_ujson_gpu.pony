@@ -8,8 +8,10 @@ element handles; this class owns the (path, value) leaves: a handle is the
 FNV-1a 64 hash of the leaf's encoding (identical on every replica and in the
 Python mirror), and `_leaves` maps handles back for GET.
 
-* converge queues the pair; the next entry point converges the queue in one
-  jy_ujson_converge (dots, elements, vv, cloud per doc).  Reading a peer UJSON
+* converge queues the pair; the next entry point converges the queue in ONE
+  node call, jy_node_ujson_converge (dots, elements, vv, cloud per doc): the
+  library routes every document to the GPU that owns it.  Reads and writes
+  go to the key's owner shard; deltas_size and flush walk every shard.  Reading a peer UJSON
   delta's dots and context, and rebuilding one on flush, use accessors a
   vendored pony-crdt fork adds (`dots()`, `vv_pairs()`, `cloud()`,
   `from_dot()`, `from_vv()`, `from_cloud()`): upstream keeps the dot kernel
@@ -49,13 +51,13 @@ primitive _LeafHash
 
 class RepoUJSONGpu
   let _identity: U64
-  let _eng: (_Engine | None)
+  let _node: (_Node | None)
   embed _in: Array[(String, Any box)] = _in.create()
   embed _leaves: Map[U64, (Array[String] val, String)] = _leaves.create()
 
   new create(identity': U64) =>
     _identity = identity'
-    _eng = try _Engine(identity')? else None end
+    _node = try _Node(identity')? else None end
 
   fun ref _handle(path: Array[String] val, value: String): U64 ? =>
     let h = _LeafHash(path, value)
@@ -68,27 +70,31 @@ class RepoUJSONGpu
     peer pair first, so a replica with no local commands still converges
     each tick"""
     _drain()
-    match _eng
-    | let e: _Engine =>
-      var n: U64 = 0
-      @jy_ujson_deltas_size(e.ptr, addressof n)
-      n.usize()
-    else 0
+    var total: USize = 0
+    match _node
+    | let n: _Node =>
+      for e in n.shards.values() do
+        var k: U64 = 0
+        @jy_ujson_deltas_size(e.ptr, addressof k)
+        total = total + k.usize()
+      end
     end
+    total
 
   fun ref flush_deltas(): Array[(String, Any box)] box =>
     """repo_ujson.pony:22-26: every pending doc with its delta document"""
     _drain()
     let out = Array[(String, Any box)]
-    match _eng
-    | let e: _Engine =>
-      try
+    match _node
+    | let node: _Node =>
+      for e in node.shards.values() do try
+        e.sync_names(JyUJSON())
         var nd: U64 = 0
         var ne: U64 = 0
         var nc: U64 = 0
         e.check(@jy_ujson_flush(e.ptr, 0, 0, 0, Pointer[U32], Pointer[U64], Pointer[U64], Pointer[U64],
           Pointer[U64], Pointer[U64], Pointer[U64], addressof nd, addressof ne, addressof nc, JyHost()))?
-        if nd == 0 then return out end
+        if nd == 0 then continue end
         let r: USize = 16   // jy_config.ujson_columns
         let slots = Array[U32].init(0, nd.usize())
         let eo = Array[U64].init(0, nd.usize() + 1)
@@ -115,7 +121,7 @@ class RepoUJSONGpu
           end
           out.push((e.name(slots(i)?), d))
         end
-      end
+      end end
     end
     out
 
@@ -126,10 +132,10 @@ class RepoUJSONGpu
     if _in.size() >= _DrainBound() then _drain() end
 
   fun ref _drain() =>
-    """every queued UJSON delta in one jy_ujson_converge"""
+    """every queued UJSON delta in one node call (jy_node_ujson_converge)"""
     if _in.size() == 0 then return end
-    match _eng
-    | let e: _Engine =>
+    match _node
+    | let e: _Node =>
       try
         let keys = Array[String]
         let eo: Array[U64] = [0]
@@ -167,10 +173,10 @@ class RepoUJSONGpu
           end
         end
         if keys.size() > 0 then
-          let slots = e.intern(JyUJSON(), keys)?
-          e.check(@jy_ujson_converge(e.ptr, slots.size().u64(), slots.cpointer(), eo.cpointer(),
-            dots.size().u64(), dots.cpointer(), elems.cpointer(), vo.cpointer(), vv.size().u64(),
-            vv.cpointer(), co.cpointer(), cloud.size().u64(), cloud.cpointer(), JyHost()))?
+          let m = _Strs(keys)
+          e.check(@jy_node_ujson_converge(e.ptr, keys.size().u64(), m.bytes.cpointer(), m.offs.cpointer(),
+            eo.cpointer(), dots.cpointer(), elems.cpointer(), vo.cpointer(), vv.cpointer(), co.cpointer(),
+            cloud.cpointer(), JyHost()))?
         end
       end
     end
@@ -231,13 +237,14 @@ class RepoUJSONGpu
     let keys = Array[String].init(key, ops.size())
     let slots = e.intern(JyUJSON(), keys)?
     e.check(@jy_ujson_write(e.ptr, ops.size().u64(), ops.cpointer(), slots.cpointer(), elems.cpointer(),
-      e.col(), JyHost()))?
+      e.col(), JyHost()))?   // the key's owner shard
 
   fun ref get(resp: Respond, key: String, path: Array[String] val): Bool =>
     """repo_ujson.pony:68-72: the render, or '' for nothing"""
     _drain()
-    match _eng
-    | let e: _Engine =>
+    match _node
+    | let n: _Node =>
+      let e = try n.owner(key)? else return _Fail(resp) end
       let leaves = Array[(Array[String] val, String)]
       for h in _under(e, key, path).values() do
         try
@@ -253,8 +260,9 @@ class RepoUJSONGpu
   fun ref ins_rm(resp: Respond, key: String, path: Array[String] val, text: String, op: U8): Bool ? =>
     """INS / RM (repo_ujson.pony:90-110): the value parses as a UJSON primitive"""
     _drain()
-    match _eng
-    | let e: _Engine =>
+    match _node
+    | let n: _Node =>
+      let e = try n.owner(key)? else return _Fail(resp) end
       if (op == _UjOp.rm()) and (e.lookup(JyUJSON(), key) == JyNoSlot()) then resp.ok(); return true end
       let h = _handle(path, _Canon.value(text)?)?
       _write(e, key, [op], [h])?
@@ -266,8 +274,9 @@ class RepoUJSONGpu
   fun ref clr(resp: Respond, key: String, path: Array[String] val): Bool =>
     """CLR (repo_ujson.pony:85-88): no key creation"""
     _drain()
-    match _eng
-    | let e: _Engine =>
+    match _node
+    | let n: _Node =>
+      let e = try n.owner(key)? else return _Fail(resp) end
       if e.lookup(JyUJSON(), key) != JyNoSlot() then
         try
           if path.size() == 0 then
@@ -287,8 +296,9 @@ class RepoUJSONGpu
   fun ref set(resp: Respond, key: String, path: Array[String] val, text: String): Bool ? =>
     """SET (repo_ujson.pony:74-83): clear the path, insert the node's leaves"""
     _drain()
-    match _eng
-    | let e: _Engine =>
+    match _node
+    | let n: _Node =>
+      let e = try n.owner(key)? else return _Fail(resp) end
       let ops = Array[U8]
       let hs = Array[U64]
       if e.lookup(JyUJSON(), key) != JyNoSlot() then

@@ -13,11 +13,11 @@ def strip_zero_counters(t, prefixes):
         keep = vals != 0
         new_offs = np.zeros(n + 1, np.uint64)
         if len(offs) > 1:
-            cnt = np.add.reduceat(keep.astype(np.uint64), offs[:-1].astype(np.int64)) if len(vals) else np.zeros(n)
-            # reduceat misreports empty segments: fix them
-            seg = np.diff(offs.astype(np.int64))
-            cnt = np.where(seg == 0, 0, cnt)
-            new_offs[1:] = np.cumsum(cnt, dtype=np.uint64)
+            # kept entries per segment from a running count (empty segments,
+            # trailing ones included, count 0)
+            run = np.concatenate([[0], np.cumsum(keep.astype(np.int64))])
+            o = np.asarray(offs, np.int64)
+            new_offs[1:] = np.cumsum(run[o[1:]] - run[o[:-1]]).astype(np.uint64)
         t[p + "offs"], t[p + "ids"], t[p + "vals"] = new_offs, ids[keep], vals[keep]
     return t
 
