@@ -69,6 +69,10 @@ def parse():
     ap.add_argument("--resolve", action="store_true",
                     help="treg --route: every timed step first resolves its batch's key strings on the GPU "
                          "(route.KeyResolver), 1/16 of them new to the node")
+    ap.add_argument("--node", action="store_true",
+                    help="treg: every step is one jy_node_treg_converge of key strings (the node C-ABI)")
+    ap.add_argument("--node-shards", type=int, default=1,
+                    help="--node at N = 1: shards on this GPU (1: RCCL; more: the copy fabric)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1 collectives: nccl (RCCL over xGMI); gloo only rehearses the routed path "
                          "with several ranks on one GPU")
@@ -240,7 +244,18 @@ def main():
     seed = S.BASE_SEED + 2  # config 2
     seed_me = _owner_seed(seed, rank)
     dev = torch.device("cuda", local)
-    eng = Engine(device=local, counter_columns=R, key_capacity=[1024, K, 1024, 1024, 1024])
+    node = None
+    routed_on = world > 1 or args.route
+    if routed_on:
+        # the node (jy_node_*): this process's shard of an RCCL communicator
+        # over every rank (one shard on this GPU at N = 1, --route); its
+        # engine holds the state, so the native routed phase merges into it
+        from bench_modes import node_for
+        node, _ = node_for(args, dev, dist, rank, world, counter_columns=R,
+                           key_capacity=[1024, K, 1024, 1024, 1024])
+        eng = node.engines[0]
+    else:
+        eng = Engine(device=local, counter_columns=R, key_capacity=[1024, K, 1024, 1024, 1024])
     # one non-default stream shared by torch (generation, collectives, timing
     # events) and the engine, so the HIP events bracket the engine's launches
     stream = torch.cuda.Stream(dev)
@@ -284,7 +299,7 @@ def main():
     # the keys of EVERY owner, [sign][c][owner][K] per round, and routes them
     nbr = min(nb, 2)
     routed = []
-    if world > 1:
+    if routed_on:
         routed = [torch.empty((2, Cn, world, K), dtype=torch.int64, device=dev) for _ in range(nbr)]
         for d in range(world):
             for c in range(Cn):
@@ -398,12 +413,14 @@ def main():
         "first_cycle_changes": {"cells_changed": changed, "cells_sampled": 2 * R * min(K, 1 << 16)},
         "verified": ok,
     }
-    if world > 1:
-        line["routed"] = routed_phase(args, eng, dev, dist, rank, world, routed, peer, fabric_of(dist, cpu_group),
-                                      cells_per_step, line, verify, applied)
+    if routed_on:
+        routed_phase(args, eng, node, dev, dist, rank, world, routed, peer, fabric_of(dist, cpu_group, world),
+                     cells_per_step, line, verify, applied)
     if rank == 0:
         print(json.dumps(line), flush=True)
     eng.close()
+    if node is not None:
+        node.close()
     if dist:
         dist.destroy_process_group()
 
@@ -433,55 +450,79 @@ def watchdog(limit, line, rank, key="routed"):
 XGMI_LINK_GBPS = 153.0  # per xGMI link and direction, nominal (MI355X: 7 links per GPU)
 
 
-def fabric_of(dist, cpu_group):
-    from jylis_amd.route import DistFabric
-    return DistFabric(dist, cpu_group=cpu_group)
+def fabric_of(dist, cpu_group, world):
+    from jylis_amd.route import DistFabric, LocalFabric
+    return DistFabric(dist, cpu_group=cpu_group) if world > 1 else LocalFabric(1)
 
 
-def routed_phase(args, eng, dev, dist, rank, world, routed, peer, fabric, cells_per_step, line, verify, applied):
+def routed_phase(args, eng, node, dev, dist, rank, world, routed, peer, fabric, cells_per_step, line, verify,
+                 applied):
     """The same converge with the peer batches arriving MIXED: rank r holds
-    whole peer columns (the keys of every owner) and route.CounterRouter moves
-    each owner's part to it with equal-split RCCL all-to-alls over xGMI,
-    double-buffered against the owner's merge.  Every cell a
-    shard merges then crosses xGMI once unless the ingesting rank owns it:
-    (N - 1) / N of the batch, as many bytes as the merge reads, so the step
-    is bound by the links, not by HBM.  Timed apart from `value` with its own
-    few steps; a watchdog prints the line without it if a collective hangs."""
+    whole peer columns (the keys of every owner) and each owner's part moves
+    to it over xGMI, double-buffered against the owner's merge.
+    Every cell a shard merges then crosses xGMI once unless the ingesting rank
+    owns it: (N - 1) / N of the batch, as many bytes as the merge reads, so the
+    step is bound by the links, not by HBM.  Timed twice, apart from `value`,
+    with a few steps each:
+      routed        the node C-ABI (jy_node_counter_converge_block): native
+                    RCCL ncclSend / ncclRecv per column on a second stream,
+                    the engine's block merge of column c while c + 1 moves
+      routed_torch  route.CounterRouter: the same exchange as torch
+                    all_to_all_single calls (DistFabric) from Python
+    A watchdog exits non-zero (printing the line with an error) if a
+    collective hangs.  At N = 1 (--route) both run against one shard."""
     import torch
     from jylis_amd._lib import PNCOUNT
     from jylis_amd.route import CounterRouter
     limit = float(os.environ.get("JY_ROUTED_LIMIT_S", "240"))
     dog = watchdog(limit, line, rank)
-    router = CounterRouter([eng], fabric, PNCOUNT)
     nbr = len(routed)
     warm, steps = 1, max(1, min(args.steps, 4))
-    for i in range(warm):
-        router.step([routed[i % nbr]], peer)
-    torch.cuda.synchronize(dev)
-    dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(steps):
-        router.step([routed[(warm + i) % nbr]], peer)
-    torch.cuda.synchronize(dev)
-    dist.barrier()
-    torch.cuda.synchronize(dev)
-    el = time.perf_counter() - t0
-    tt = torch.tensor([el], dtype=torch.float64, device=dev)
-    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    t = float(tt[0])
-    ok = verify(applied | {i % nbr for i in range(warm + steps)})
-    dog.cancel()
     _, Cn, _, K = routed[0].shape
     xbytes = 2 * Cn * (world - 1) * K * 8  # sent (= received) per rank per step
-    ms = t / steps * 1e3
-    return {"value": world * cells_per_step * steps / t, "unit": "merges/s", "steps": steps, "warmup": warm,
-            "ms_per_step": ms, "verified": ok,
-            "exchange_bytes_per_gpu_per_step": xbytes, "exchange_GBps_per_gpu": xbytes / (ms / 1e3) / 1e9,
-            "xgmi_links_used": world - 1, "xgmi_link_GBps_nominal": XGMI_LINK_GBPS,
-            "exchange_frac_of_links": xbytes / (ms / 1e3) / 1e9 / ((world - 1) * XGMI_LINK_GBPS),
-            "note": "peer batches ingested mixed: rank r holds peer columns c % N == r for every owner and routes "
-                    "them (route.CounterRouter, RCCL all-to-all, double-buffered against the merge)"}
+
+    def run(step_fn, k0):
+        for i in range(warm):
+            step_fn(routed[(k0 + i) % nbr])
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step_fn(routed[(k0 + warm + i) % nbr])
+        node.sync()
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        if dist:
+            tt = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt[0])
+        ms = el / steps * 1e3
+        res = {"value": world * cells_per_step * steps / el, "unit": "merges/s", "steps": steps, "warmup": warm,
+               "ms_per_step": ms, "exchange_bytes_per_gpu_per_step": xbytes,
+               "exchange_GBps_per_gpu": xbytes / (ms / 1e3) / 1e9, "xgmi_links_used": world - 1,
+               "xgmi_link_GBps_nominal": XGMI_LINK_GBPS}
+        if world > 1:
+            res["exchange_frac_of_links"] = xbytes / (ms / 1e3) / 1e9 / ((world - 1) * XGMI_LINK_GBPS)
+        return res
+
+    cols_all = np.array(peer, np.uint16)  # [rank][c]: the column of rank r's c-th peer
+    native = run(lambda b: node.counter_converge_block(PNCOUNT, cols_all, 0, K, b[0], b[1]), 0)
+    native["verified"] = verify(applied | {i % nbr for i in range(warm + steps)})
+    native["note"] = ("peer batches ingested mixed: rank r holds peer columns c % N == r for every owner; "
+                      "jy_node_counter_converge_block moves each column to its owners with native RCCL "
+                      "send/recv and block-merges it, column c + 1 in flight on a second stream")
+    line["routed"] = native
+    router = CounterRouter([eng], fabric, PNCOUNT)
+    tor = run(lambda b: router.step([b], peer), 1)
+    tor["verified"] = verify(applied | {i % nbr for i in range(2 * (warm + steps) + 1)})
+    tor["note"] = "the same exchange through route.CounterRouter (torch all_to_all_single, RCCL, from Python)"
+    line["routed_torch"] = tor
+    dog.cancel()
 
 
 if __name__ == "__main__":

@@ -371,6 +371,8 @@ def bench_treg(args, eng, dev, dist, rank, world):
     unless --route (then it runs the same kernels against itself)."""
     if args.overlap is not None:
         return bench_treg_overlap(args, eng, dev, dist, rank, world)
+    if args.node:
+        return bench_treg_node(args, eng, dev, dist, rank, world)
     import torch
     from jylis_amd import synth as S
     from jylis_amd._lib import TREG
@@ -504,6 +506,112 @@ def bench_treg(args, eng, dev, dist, rank, world):
                                                "MALL: every handle written, losers' read)"}
     else:
         out["step_ms_avg_events"] = k * 1e3
+    return out
+
+
+def node_for(args, dev, dist, rank, world, **engine_kw):
+    """the node of a --node run: one process per GPU over RCCL at N > 1 (the
+    rank-0 ncclUniqueId shared over the CPU group), or --node-shards shards on
+    this GPU at N = 1 (RCCL for one shard, the copy fabric for more)"""
+    from jylis_amd.node import Node, unique_id
+    if world > 1:
+        import torch.distributed as tdist
+        cpu = tdist.new_group(backend="gloo")
+        box = [unique_id() if rank == 0 else None]
+        tdist.broadcast_object_list(box, src=0, group=cpu)
+        return Node(world, "rccl", devices=[dev.index], nlocal=1, rank0=rank, uid=box[0], **engine_kw), cpu
+    S = max(1, args.node_shards)
+    return Node(S, "rccl" if S == 1 else "copy", devices=[dev.index] * S, **engine_kw), None
+
+
+def bench_treg_node(args, eng, dev, dist, rank, world):
+    """TREG through the node (jy_node_treg_converge): every step is ONE call
+    per process with a peer batch of KEY STRINGS and values in HBM -- the
+    library hashes the keys, regroups them by owner, exchanges (RCCL over
+    xGMI at N > 1), interns them on the owner and LWW-merges there.  Nothing
+    is pre-resolved: the step pays for the key probe (_data_for) on every
+    key, as RepoManagerCore.converge_deltas does (repo_treg.pony:37-42)."""
+    import torch
+    from jylis_amd import synth as S
+    from jylis_amd._lib import TREG
+    Kper = args.keys or (8 << 20)
+    node, cpu = node_for(args, dev, dist, rank, world, key_capacity=[1024, 1024, 2 * Kper, 1024, 1024])
+    shards = node.S
+    G = Kper * max(world, shards)
+    nproc_keys = G // world  # keys this process ingests per step
+    rng = np.random.default_rng(S.BASE_SEED + 3 + 1000 * rank)
+    idx = np.arange(rank, G, world, dtype=np.uint64)[:nproc_keys]
+    kb, ko = _key_strings(idx, b"t")
+    kb_d, ko_d = _to_dev(kb, dev), _to_dev(ko, dev)
+    nb = max(1, args.batches, args.warmup + args.steps) + 1
+    batches = []
+    for j in range(nb):
+        vb, vo = _treg_values(rng, nproc_keys)
+        ts = (rng.integers(0, 1 << 20, nproc_keys) + (j << 18)).astype(np.uint64)
+        batches.append((ts, vb, vo, _to_dev(ts, dev), _to_dev(vb, dev), _to_dev(vo, dev)))
+
+    def step(i):
+        b = batches[i]
+        node.treg_converge(kb_d, ko_d, b[3], b[4], b[5])
+
+    t0 = time.perf_counter()
+    step(0)  # batch 0 creates every key (the setup converge)
+    node.sync()
+    setup_s = time.perf_counter() - t0
+    elapsed, _ = _timed(args.steps, args.warmup, lambda i: step(1 + i % (nb - 1)), dist, dev)
+    node.sync()
+    t = _max_over_ranks(elapsed, dist, dev)
+    st = node.stats()
+    # sampled keys of this process's ingest: LWW over every applied batch
+    # against the owner's register (asked over the CPU group at N > 1)
+    samp = np.random.default_rng(6 + rank).integers(0, nproc_keys, 96)
+    applied = [0] + [1 + i % (nb - 1) for i in range(args.warmup + args.steps)]
+    best = {}
+    for j in applied:
+        ts, vb, vo = batches[j][:3]
+        for q in samp:
+            cand = (int(ts[q]), bytes(vb[int(vo[q]):int(vo[q + 1])]))
+            if int(q) not in best or cand > best[int(q)]:
+                best[int(q)] = cand
+    keys = [bytes(kb[int(ko[q]):int(ko[q + 1])]) for q in samp]
+    if world == 1:
+        ok = True
+        for q, k in zip(samp, keys):
+            e = node.engine(node.shard_of(k))
+            s = e.lookup(TREG, [k])
+            gts, gpre, glr = e.treg_read(s)
+            ok = ok and (int(gts[0]), e.value_bytes(TREG, gpre[0], glr[0])) == best[int(q)]
+    else:
+        e = node.engine(rank)
+
+        def answer(slots):
+            gts, gpre, glr = e.treg_read(slots)
+            return [(int(a), e.value_bytes(TREG, p_, q_)) for a, p_, q_ in zip(gts, gpre, glr)]
+        reqs = []
+        for k in keys:  # the owner's slot: every owner interned every key it received
+            reqs.append((node.shard_of(k), k))
+        every = [None] * world
+        dist.all_gather_object(every, reqs, group=cpu)
+        mine = [(src, i, k) for src, rq in enumerate(every) for i, (o, k) in enumerate(rq) if o == rank]
+        ans = answer(e.lookup(TREG, [k for _, _, k in mine])) if mine else []
+        back = [None] * world
+        dist.all_gather_object(back, [(src, i, a) for (src, i, _), a in zip(mine, ans)], group=cpu)
+        got = {}
+        for lst in back:
+            for src, i, a in lst:
+                if src == rank:
+                    got[i] = a
+        ok = all(got[i] == best[int(q)] for i, q in enumerate(samp))
+    verified = _all_true(ok, dist, dev)
+    ms = t / args.steps * 1e3
+    out = {"workload": f"TREG through the node: {G} keys over {shards} shard(s) ({'RCCL' if world > 1 or shards == 1 else 'copy fabric, one GPU'}), "
+                       f"every process converges {nproc_keys} key strings + values per step in ONE jy_node_treg_converge "
+                       f"(hash, regroup by owner, exchange, intern on the owner, LWW) (SURVEY 8d config 3, 8e)",
+           "unit_of_work": "key LWW select (keyed, routed)", "value": world * nproc_keys * args.steps / t,
+           "ms_per_step": ms, "setup_s": setup_s, "node_shards": shards,
+           "exchange_bytes_sent_per_step": st["bytes_sent"], "keys_received_per_step": st["keys_received"],
+           "verified_sampled_keys": verified}
+    node.close()
     return out
 
 

@@ -336,6 +336,7 @@ void jy_engine_destroy(jy_engine* eng) {
   F(eng->treg.dups);
   F(eng->treg.dupn_alt);
   F(eng->treg.dups_alt);
+  F(eng->treg.fold_bits);
   for (TlogState* t : {&eng->tlog, &eng->tlog_d}) {
     F(t->meta);
     F(t->pool);
@@ -387,10 +388,7 @@ void jy_engine_destroy(jy_engine* eng) {
   }
   if (eng->pin_total) hipHostFree(eng->pin_total);
   if (eng->pin_rb) hipHostFree(eng->pin_rb);
-  if (eng->treg.dupflag) {
-    hipHostFree(eng->treg.dupflag);
-    for (auto& e : eng->treg.mev) hipEventDestroy(e);
-  }
+  if (eng->treg.dupflag) hipHostFree(eng->treg.dupflag);
   for (auto& ev : eng->tm_ev) {
     hipEventDestroy(ev.first);
     hipEventDestroy(ev.second);

@@ -250,19 +250,14 @@ struct TregState {  // per slot: ts u64 (read by every merge) + TVal (written by
   u64* dups_alt = nullptr;
   u64 dup_cap = 0;
   u64 dup_bound = 0;
-  // "a duplicate was pushed since the last fold": a host-mapped word the
-  // kernels set (only when they push, i.e. rarely) and the fold clears, plus
-  // a ring of the claim launches in flight (event, entries).  A full bound
-  // with the flag clear means the list is empty but for launches still in
-  // flight: the host waits for the oldest of those (the GPU keeps running the
-  // rest) instead of enqueueing a fold of nothing (~36 us of GPU time).
+  // host-mapped: [1] set when a push overflowed the list (a wrong bound:
+  // the next call fails loudly)
   u32* dupflag = nullptr;
   u32* dupflag_dev = nullptr;
-  static constexpr int kRing = 8;
-  hipEvent_t mev[kRing] = {};
-  u64 mn[kRing] = {};
-  int mhead = 0, mcount = 0;
-  u64 pending_n = 0;
+  // the cooperative fold (k_treg_fold_coop): its claim bitmap and grid
+  u32* fold_bits = nullptr;
+  u64 fold_words = 0;
+  u32 fold_grid = 0, fold_grid_set = 0;
 };
 
 // one TLOG entry: 32 B so a lane moves it with two 16-B accesses and an

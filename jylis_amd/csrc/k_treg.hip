@@ -20,12 +20,15 @@
 // key) is resolved EXACTLY: the first entry of each slot (jy_claim_rows, one
 // bit per slot) is merged by the wide kernel; the others are copied into a
 // duplicate list that is folded in later -- before the next read or SET of
-// the register file, since LWW is a join and the fold's timing and order do
-// not change the result.  The fold runs in parallel ROUNDS over the whole
-// GPU (k_treg_fold_round: each round merges the first record of every slot
-// in the list and moves the rest to the next round's list), so a key that
-// arrives many times costs one round per extra occurrence, not a serial walk;
-// one wave folds whatever a few rounds leave (unbounded repeats only).
+// the register file, or when the list could fill -- since LWW is a join and
+// the fold's timing and order do not change the result.  The fold is ONE
+// cooperative launch (k_treg_fold_coop): parallel ROUNDS over the whole GPU
+// with a grid barrier between them (each round merges the first record of
+// every slot in the list and moves the rest to the other list), so a key
+// that arrives many times costs one round per extra occurrence, not a serial
+// walk; one wave folds whatever the rounds leave (unbounded repeats only).
+// An empty list costs the launch alone: every workgroup reads the count and
+// returns.  No merge records an event, so merges run back to back.
 // Routed runs are merged one source per launch: keys that several peers
 // flushed in the same step never become duplicates.  A dense batch in slot
 // order costs the claim one atomic instruction per wave.  Two claim bitmaps
@@ -43,6 +46,8 @@
 #include <algorithm>
 #include <cstring>
 
+
+#include <hip/hip_cooperative_groups.h>
 
 #include "jy_dscan.hpp"
 #include "jy_internal.hpp"
@@ -124,19 +129,18 @@ __device__ __forceinline__ u32 push_dup(const TregK& K, u32 s, u64 t, u64 p, u64
   return 1u;
 }
 
-// The host-mapped words behind the host's "nothing was pushed" shortcut
-// (claim_begin): ONE lane of a wave that pushed (or overflowed) stores them
-// with system scope and then waits for the stores to be performed at system
-// scope (release fence) before the wave may end, so by the time the launch's
-// completion event fires the host sees them.  Called by every lane of the
-// wave together; the fence only runs on this rare path.
+// An overflow (a push past the list's capacity: a wrong bound) is published
+// to a host-mapped word: ONE lane of a wave that overflowed stores it with
+// system scope and waits for the store to be performed at system scope
+// before the wave may end, so a completed launch's overflow is visible to
+// the host (jy_treg_overflow_check).  Called by every lane of the wave
+// together; the fence runs only on that path.
 __device__ __forceinline__ void dup_publish(const TregK& K, u32 what) {
   const u32 any = jy_wave_or(what);
-  if (!any || !K.dupflag) return;
+  if (!(any & 2u) || !K.dupflag) return;
   if (__lane_id() == 0) {
-    if (any & 1u) __hip_atomic_store(K.dupflag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (any & 2u) __hip_atomic_store(K.dupflag + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __atomic_thread_fence(__ATOMIC_RELEASE);  // system scope: the stores above are performed
+    __hip_atomic_store(K.dupflag + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __atomic_thread_fence(__ATOMIC_RELEASE);  // system scope: the store above is performed
   }
 }
 
@@ -290,13 +294,12 @@ __global__ __launch_bounds__(kThreads) void k_treg_lww_routed(TregK K, RoutedIn 
   dup_publish(K, pushed);
 }
 
-// The duplicate list, folded in by ONE wave: a chunk of 64 records per pass
-// (lane = record); records of one slot inside a chunk run in rounds by their
-// rank among the chunk's records of that slot, so no two lanes touch a slot
-// at once and chunks run in list order.  Resets the list.
+// The rest of a duplicate list, folded in by ONE wave: a chunk of 64 records
+// per pass (lane = record); records of one slot inside a chunk run in rounds
+// by their rank among the chunk's records of that slot, so no two lanes
+// touch a slot at once and chunks run in list order.
 template <bool kSet>
-__global__ __launch_bounds__(64) void k_treg_fold(TregK K) {
-  const u32 n = (u32)fold_count(*K.dupn, K.dup_cap);
+__device__ void fold_wave(const TregK& K, const u64* __restrict__ list, u32 n) {
   const int lane = threadIdx.x;
   for (u32 j0 = 0; j0 < n; j0 += 64) {
     const u32 j = j0 + lane;
@@ -304,8 +307,8 @@ __global__ __launch_bounds__(64) void k_treg_fold(TregK K) {
     u32 s = 0xFFFFFFFFu;
     u64 t = 0, p = 0, l = 0;
     if (live) {
-      const u64x2 a = reinterpret_cast<const u64x2*>(K.dups + (u64)j * 4)[0];
-      const u64x2 b = reinterpret_cast<const u64x2*>(K.dups + (u64)j * 4)[1];
+      const u64x2 a = reinterpret_cast<const u64x2*>(list + (u64)j * 4)[0];
+      const u64x2 b = reinterpret_cast<const u64x2*>(list + (u64)j * 4)[1];
       s = (u32)a.x;
       t = a.y;
       p = b.x;
@@ -334,61 +337,109 @@ __global__ __launch_bounds__(64) void k_treg_fold(TregK K) {
       __builtin_amdgcn_wave_barrier();
     }
   }
-  if (lane == 0) *K.dupn = 0;
 }
 
-// One round of the parallel fold, grid-stride over the list's count: the
-// first record of each slot (this launch's claim bitmap) is merged, the
-// others are pushed to K's list (the next round's input).  Every lane of a
-// wave runs the same iterations (jy_claim_rows is wave-collective).
+// The fold: ONE cooperative launch over the pending duplicate list (list 0;
+// list 1 is the other round's).  Round r merges the first record of every
+// slot (a claim bitmap of its own, cleared by the round's items after the
+// grid barrier) and pushes the others to the other list; after kRounds
+// rounds, one wave folds what is left (a slot repeated more often).  Both
+// counts are zero afterwards.  Every workgroup reads the same counts, so an
+// empty list (the usual case) returns everywhere before any barrier.
+constexpr int kFoldRounds = 3;
+struct FoldK {
+  TregK K;      // state (and the pending registers for kSet)
+  u32* cnt0;    // list 0 count (the pending list)
+  u64* lst0;
+  u32* cnt1;    // list 1 count
+  u64* lst1;
+  u32* bits;    // the fold's claim bitmap (zero between folds)
+};
 template <bool kSet>
-__global__ __launch_bounds__(kThreads) void k_treg_fold_round(TregK K, const u32* __restrict__ in_n,
-                                                              const u64* __restrict__ in) {
+__global__ __launch_bounds__(kThreads) void k_treg_fold_coop(FoldK F) {
+  namespace cg = cooperative_groups;
+  cg::grid_group grid = cg::this_grid();
   constexpr int U = 2;
-  clear_slice(K);
-  const u64 n = fold_count(*in_n, K.dup_cap);  // the input list has the capacity of K's
-  u32 pushed = 0;
-  for (u64 b0 = (u64)blockIdx.x * (kThreads * U); b0 < n; b0 += (u64)gridDim.x * (kThreads * U)) {
-    const u64 base = b0 + (threadIdx.x >> 6) * (64 * U) + (threadIdx.x & 63);
-    u32 s[U];
-    u64 t[U], p[U], l[U], t0[U];
-    bool valid[U], first[U];
+  u64 n = fold_count(*F.cnt0, F.K.dup_cap);
+  if (n == 0) return;
+  u32* cin = F.cnt0;
+  u64* lin = F.lst0;
+  u32* cout = F.cnt1;
+  u64* lout = F.lst1;
+  for (int r = 0; r < kFoldRounds && n > 0; r++) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *cout = 0;
+    grid.sync();  // the output count is zero before anyone pushes
+    TregK K = F.K;
+    K.seen = F.bits;
+    K.dupn = cout;
+    K.dups = lout;
+    u32 pushed = 0;
+    for (u64 b0 = (u64)blockIdx.x * (kThreads * U); b0 < n; b0 += (u64)gridDim.x * (kThreads * U)) {
+      const u64 base = b0 + (threadIdx.x >> 6) * (64 * U) + (threadIdx.x & 63);
+      u32 s[U];
+      u64 t[U], p[U], l[U], t0[U];
+      bool valid[U], first[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-      const u64 i = base + (u64)u * 64;
-      valid[u] = i < n;
-      s[u] = 0;
-      if (valid[u]) {
-        const u64x2 a = reinterpret_cast<const u64x2*>(in + i * 4)[0];
-        const u64x2 b = reinterpret_cast<const u64x2*>(in + i * 4)[1];
-        s[u] = (u32)a.x;
-        t[u] = a.y;
-        p[u] = b.x;
-        l[u] = b.y;
+      for (int u = 0; u < U; u++) {
+        const u64 i = base + (u64)u * 64;
+        valid[u] = i < n;
+        s[u] = 0;
+        if (valid[u]) {
+          const u64x2 a = reinterpret_cast<const u64x2*>(lin + i * 4)[0];
+          const u64x2 b = reinterpret_cast<const u64x2*>(lin + i * 4)[1];
+          s[u] = (u32)a.x;
+          t[u] = a.y;
+          p[u] = b.x;
+          l[u] = b.y;
+        }
+      }
+      if (!kSet) {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+          if (valid[u]) t0[u] = K.ts[s[u]];
+      }
+      jy_claim_rows<U>(valid, s, K.seen, first);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        if (!valid[u]) continue;
+        if (!first[u]) {
+          pushed |= push_dup(K, s[u], t[u], p[u], l[u]);
+          continue;
+        }
+        if (kSet) {
+          set_one(K, s[u], t[u], p[u], l[u]);
+        } else if (t[u] >= t0[u] && lww_wins(t[u], t0[u], p[u], l[u], K.val, s[u], K.arena)) {
+          K.ts[s[u]] = t[u];
+          K.val[s[u]] = TVal{p[u], l[u]};
+        }
       }
     }
-    if (!kSet) {
-#pragma unroll
-      for (int u = 0; u < U; u++)
-        if (valid[u]) t0[u] = K.ts[s[u]];
+    dup_publish(K, pushed);
+    grid.sync();  // every merge and push of the round is done
+    // the round's claim bits back to zero (each item its own slot's bit;
+    // repeats clear the same bit)
+    for (u64 i = (u64)blockIdx.x * kThreads + threadIdx.x; i < n; i += (u64)gridDim.x * kThreads) {
+      const u32 s = (u32)lin[i * 4];
+      atomicAnd(F.bits + (s >> 5), ~(1u << (s & 31)));
     }
-    jy_claim_rows<U>(valid, s, K.seen, first);
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      if (!valid[u]) continue;
-      if (!first[u]) {
-        pushed |= push_dup(K, s[u], t[u], p[u], l[u]);
-        continue;
-      }
-      if (kSet) {
-        set_one(K, s[u], t[u], p[u], l[u]);
-      } else if (t[u] >= t0[u] && lww_wins(t[u], t0[u], p[u], l[u], K.val, s[u], K.arena)) {
-        K.ts[s[u]] = t[u];
-        K.val[s[u]] = TVal{p[u], l[u]};
-      }
+    n = fold_count(__hip_atomic_load(cout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), F.K.dup_cap);
+    u32* tc = cin;
+    cin = cout;
+    cout = tc;
+    u64* tl = lin;
+    lin = lout;
+    lout = tl;
+  }
+  grid.sync();  // every workgroup has read the counts; the clears are done
+  if (blockIdx.x != 0) return;
+  if (threadIdx.x < 64) {
+    TregK K = F.K;
+    if (n) fold_wave<kSet>(K, lin, (u32)n);
+    if (threadIdx.x == 0) {
+      *F.cnt0 = 0;
+      *F.cnt1 = 0;
     }
   }
-  dup_publish(K, pushed);
 }
 
 __global__ __launch_bounds__(kThreads) void k_treg_gather(const u64* __restrict__ ts, const TVal* __restrict__ val,
@@ -441,35 +492,6 @@ TregK state_of(jy_engine* eng) {
   return K;
 }
 
-// the claim launches in flight: retire those whose event has fired
-void ring_retire(TregState& t, bool wait_oldest) {
-  while (t.mcount > 0) {
-    hipEvent_t& ev = t.mev[t.mhead];
-    if (wait_oldest) {
-      hipEventSynchronize(ev);
-      wait_oldest = false;
-    } else if (hipEventQuery(ev) != hipSuccess) {
-      return;
-    }
-    t.pending_n -= t.mn[t.mhead];
-    t.mhead = (t.mhead + 1) % TregState::kRing;
-    t.mcount--;
-  }
-}
-
-// a claim launch of n entries was enqueued: note it in the ring
-int32_t ring_note(jy_engine* eng, u64 n) {
-  TregState& t = eng->treg;
-  if (!t.dupflag) return JY_OK;
-  if (t.mcount == TregState::kRing) ring_retire(t, true);
-  const int at = (t.mhead + t.mcount) % TregState::kRing;
-  JY_HIP(eng, hipEventRecord(t.mev[at], eng->stream));
-  t.mn[at] = n;
-  t.mcount++;
-  t.pending_n += n;
-  return JY_OK;
-}
-
 }  // namespace
 
 int32_t jy_treg_overflow_check(jy_engine* eng) {
@@ -482,6 +504,7 @@ int32_t jy_treg_overflow_check(jy_engine* eng) {
 namespace {
 int32_t overflow_check(jy_engine* eng) { return jy_treg_overflow_check(eng); }
 
+// the host-mapped overflow word (dupflag[1], dup_publish)
 int32_t flag_init(jy_engine* eng) {
   TregState& t = eng->treg;
   if (t.dupflag) return JY_OK;
@@ -490,10 +513,6 @@ int32_t flag_init(jy_engine* eng) {
   std::memset(h, 0, 64);
   void* d = nullptr;
   JY_HIP(eng, hipHostGetDevicePointer(&d, h, 0));
-  // completion markers only: no cache fence on record.  The flag is written
-  // with system-scope stores that the pushing wave waits to be performed
-  // before it ends (dup_publish), so a completed launch's flag is visible
-  for (auto& e : t.mev) JY_HIP(eng, hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence));
   t.dupflag = static_cast<u32*>(h);
   t.dupflag_dev = static_cast<u32*>(d);
   return JY_OK;
@@ -517,64 +536,74 @@ int32_t claim_bits(jy_engine* eng, u32 nblocks, TregK& K) {
   return JY_OK;
 }
 
-// parallel fold rounds over the pending duplicate list (k_treg_fold_round):
-// after `rounds` rounds no slot is left that appeared at most `rounds` + 1
-// times in the list
-int32_t fold_rounds(jy_engine* eng, int rounds, bool set) {
+// the second list, its count and the fold's claim bitmap (zero between folds)
+int32_t fold_bufs(jy_engine* eng) {
   TregState& t = eng->treg;
   if (!t.dups_alt) {
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.dups_alt), std::max<u64>(t.dup_cap, 1) * 32,
                         "treg duplicate list"));
-    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.dupn_alt), 64, "treg duplicate count"));
   }
-  const u32 grid = (u32)std::min<u64>(blocks(std::max<u64>(t.dup_bound, 1), kThreads * 2), 1024);
-  for (int r = 0; r < rounds; r++) {
-    TregK K = state_of(eng);
-    K.dupn = t.dupn_alt;
-    K.dups = t.dups_alt;
-    if (set) {
-      K.pts = t.dts;
-      K.pval = t.dval;
-      K.pflag = t.dflag;
-      K.pcount = t.dcount;
-    }
-    JY_TRY(claim_bits(eng, grid, K));
-    JY_HIP(eng, hipMemsetAsync(t.dupn_alt, 0, 4, eng->stream));
-    if (set)
-      hipLaunchKernelGGL((k_treg_fold_round<true>), dim3(grid), dim3(kThreads), 0, eng->stream, K, t.dupn, t.dups);
-    else
-      hipLaunchKernelGGL((k_treg_fold_round<false>), dim3(grid), dim3(kThreads), 0, eng->stream, K, t.dupn, t.dups);
-    JY_HIP(eng, hipGetLastError());
-    std::swap(t.dupn, t.dupn_alt);
-    std::swap(t.dups, t.dups_alt);
+  if (!t.dupn_alt) {
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.dupn_alt), 64, "treg duplicate count"));
+    JY_HIP(eng, hipMemsetAsync(t.dupn_alt, 0, 64, eng->stream));
+  }
+  if (t.fold_words < t.seen_words || !t.fold_bits) {
+    jy_dev_free(eng, t.fold_bits);
+    t.fold_words = t.seen_words;
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.fold_bits), (t.fold_words + 16) * 4, "treg fold bitmap"));
+    JY_HIP(eng, hipMemsetAsync(t.fold_bits, 0, (t.fold_words + 16) * 4, eng->stream));
   }
   return JY_OK;
 }
 
-// fold the pending duplicates (converge paths) now: before a read, a SET
-// batch (whose pending-delta test must see them) or an arena move.  Parallel
-// rounds first; one wave then folds what is left (a slot repeated more often
-// than the rounds cover) and resets the list.
-// after a fold (stream order): the list is empty, and every launch enqueued
-// so far is before the fold, so the ring's launches no longer bound it
-void flag_clear_after_fold(jy_engine* eng) {
-  TregState& t = eng->treg;
-  t.dup_bound = 0;
-  if (!t.dupflag) return;
-  hipMemsetAsync(t.dupflag_dev, 0, 4, eng->stream);
-  t.mhead = t.mcount = 0;
-  t.pending_n = 0;
+// workgroups of the cooperative fold: every one resident at once
+template <bool kSet>
+u32 fold_grid(jy_engine* eng) {
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_treg_fold_coop<kSet>),
+                                                   kThreads, 0) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, eng->device) != hipSuccess)
+    return 0;
+  return (u32)std::max(1, std::min(per_cu, 2) * cus);
 }
 
-constexpr int kFoldRounds = 3;
+// the fold (stream order): one cooperative launch folds every pending
+// duplicate; an empty list returns at once on the device
+int32_t fold_launch(jy_engine* eng, bool set) {
+  TregState& t = eng->treg;
+  if (!t.dups) return JY_OK;  // nothing was ever claimed
+  JY_TRY(fold_bufs(eng));
+  FoldK F{};
+  F.K = state_of(eng);
+  if (set) {
+    F.K.pts = t.dts;
+    F.K.pval = t.dval;
+    F.K.pflag = t.dflag;
+    F.K.pcount = t.dcount;
+  }
+  F.cnt0 = t.dupn;
+  F.lst0 = t.dups;
+  F.cnt1 = t.dupn_alt;
+  F.lst1 = t.dups_alt;
+  F.bits = t.fold_bits;
+  u32& grid = set ? t.fold_grid_set : t.fold_grid;
+  if (!grid) grid = set ? fold_grid<true>(eng) : fold_grid<false>(eng);
+  if (!grid) return eng->fail(JY_EHIP, "treg fold: occupancy query failed");
+  void* args[] = {&F};
+  const void* fn = set ? reinterpret_cast<const void*>(&k_treg_fold_coop<true>)
+                       : reinterpret_cast<const void*>(&k_treg_fold_coop<false>);
+  JY_HIP(eng, hipLaunchCooperativeKernel(fn, dim3(grid), dim3(kThreads), args, 0, eng->stream));
+  t.dup_bound = 0;
+  return JY_OK;
+}
+
+// fold the pending converge duplicates now: before a read, a SET batch
+// (whose pending-delta test must see them), an arena move, or when the list
+// could fill
 int32_t fold_now(jy_engine* eng) {
   TregState& t = eng->treg;
   if (t.dup_bound == 0) return JY_OK;
-  JY_TRY(fold_rounds(eng, kFoldRounds, false));
-  hipLaunchKernelGGL((k_treg_fold<false>), dim3(1), dim3(64), 0, eng->stream, state_of(eng));
-  JY_HIP(eng, hipGetLastError());
-  flag_clear_after_fold(eng);
-  return JY_OK;
+  return fold_launch(eng, false);
 }
 
 // claim state of one launch over n entries: room for n more duplicates
@@ -592,26 +621,17 @@ int32_t claim_begin(jy_engine* eng, u64 n, u32 nblocks, TregK& K) {
     if (!t.dups) {
       JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.dups), kDupTestCap * 32, "treg duplicate list"));
       JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.dups_alt), kDupTestCap * 32, "treg duplicate list"));
-      if (!t.dupn_alt) JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.dupn_alt), 64, "treg duplicate count"));
       t.dup_cap = kDupTestCap;
+      JY_TRY(fold_bufs(eng));
     }
     K = state_of(eng);
     JY_TRY(claim_bits(eng, nblocks, K));
     t.dup_bound += n;
     return JY_OK;
   }
-  if (t.dup_bound + n > t.dup_cap && t.dup_cap) {
-    // nothing pushed since the last fold (the flag is set by the pushing
-    // kernel itself, and only launches still in flight may push): the list's
-    // bound is what those launches could add -- wait for the oldest of them
-    // while that does not fit, rather than fold an empty list
-    ring_retire(t, false);
-    if (__atomic_load_n(t.dupflag, __ATOMIC_ACQUIRE) == 0) {
-      while (t.mcount > 0 && t.pending_n + n > t.dup_cap) ring_retire(t, true);
-      if (__atomic_load_n(t.dupflag, __ATOMIC_ACQUIRE) == 0) t.dup_bound = t.pending_n;
-    }
-  }
   if (t.dup_bound + n > t.dup_cap) {
+    // the list could fill: fold it first (one launch; nothing to do on the
+    // device when no duplicate was pushed, the usual case)
     JY_TRY(fold_now(eng));
     if (n > t.dup_cap) {
       const u64 cap = std::max<u64>(4 * n, 1 << 16);
@@ -621,8 +641,8 @@ int32_t claim_begin(jy_engine* eng, u64 n, u32 nblocks, TregK& K) {
       t.dup_cap = 0;
       JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.dups), cap * 32, "treg duplicate list"));
       JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.dups_alt), cap * 32, "treg duplicate list"));
-      if (!t.dupn_alt) JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.dupn_alt), 64, "treg duplicate count"));
       t.dup_cap = cap;
+      JY_TRY(fold_bufs(eng));
     }
   }
   K = state_of(eng);
@@ -683,7 +703,7 @@ int32_t jy_treg_merge(jy_engine* eng, u64 n, const u32* slot, const u64* ts, con
     hipLaunchKernelGGL((k_treg_lww<false, false>), dim3(grid), dim3(kThreads), 0,
                        eng->stream, K, slot, ts, pre, lr, n);
   JY_HIP(eng, hipGetLastError());
-  return ring_note(eng, n);
+  return JY_OK;
 }
 
 int32_t jy_treg_merge_routed(jy_engine* eng, u32 S, u64 cap, u64 cap_byte, const u64* recs, const u64* hdr,
@@ -700,7 +720,6 @@ int32_t jy_treg_merge_routed(jy_engine* eng, u32 S, u64 cap, u64 cap_byte, const
                eng->nkeys[JY_TREG], reinterpret_cast<unsigned long long*>(eng->skipped_dev)};
     hipLaunchKernelGGL(k_treg_lww_routed, dim3(grid), dim3(kThreads), 0, eng->stream, K, R);
     JY_HIP(eng, hipGetLastError());
-    JY_TRY(ring_note(eng, cap));
   }
   return JY_OK;
 }
@@ -758,16 +777,7 @@ int32_t jy_treg_set_batch(jy_engine* eng, u64 n, const u32* slot, const u64* ts,
   K.pcount = t.dcount;
   hipLaunchKernelGGL((k_treg_lww<false, true>), dim3(grid), dim3(kThreads), 0, eng->stream, K, slot, ts, pre, lr, n);
   JY_HIP(eng, hipGetLastError());
-  JY_TRY(fold_rounds(eng, kFoldRounds, true));
-  K = state_of(eng);
-  K.pts = t.dts;
-  K.pval = t.dval;
-  K.pflag = t.dflag;
-  K.pcount = t.dcount;
-  hipLaunchKernelGGL((k_treg_fold<true>), dim3(1), dim3(64), 0, eng->stream, K);
-  JY_HIP(eng, hipGetLastError());
-  flag_clear_after_fold(eng);
-  return JY_OK;
+  return fold_launch(eng, true);  // the batch's own repeats, with SET semantics
 }
 
 int32_t jy_treg_pending(jy_engine* eng, u64* count) {
