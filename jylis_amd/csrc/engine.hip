@@ -336,7 +336,7 @@ void jy_engine_destroy(jy_engine* eng) {
   F(eng->treg.dups);
   F(eng->treg.dupn_alt);
   F(eng->treg.dups_alt);
-  F(eng->treg.fold_bits);
+  F(eng->treg.fold_claim);
   for (TlogState* t : {&eng->tlog, &eng->tlog_d}) {
     F(t->meta);
     F(t->pool);

@@ -246,7 +246,7 @@ struct TregState {  // per slot: ts u64 (read by every merge) + TVal (written by
   int parity = 0;
   u32* dupn = nullptr;
   u64* dups = nullptr;
-  u32* dupn_alt = nullptr;  // the other list of a parallel fold round (k_treg_fold_round)
+  u32* dupn_alt = nullptr;  // the fold rounds' output counts; dups_alt the other list (k_treg_fold_round)
   u64* dups_alt = nullptr;
   u64 dup_cap = 0;
   u64 dup_bound = 0;
@@ -254,10 +254,11 @@ struct TregState {  // per slot: ts u64 (read by every merge) + TVal (written by
   // the next call fails loudly)
   u32* dupflag = nullptr;
   u32* dupflag_dev = nullptr;
-  // the cooperative fold (k_treg_fold_coop): its claim bitmap and grid
-  u32* fold_bits = nullptr;
-  u64 fold_words = 0;
-  u32 fold_grid = 0, fold_grid_set = 0;
+  // the fold's rounds (k_treg_fold_round): a claim word per slot holding the
+  // epoch of the round that last claimed it, and the last epoch handed out
+  u32* fold_claim = nullptr;
+  u64 fold_slots = 0;
+  u32 fold_epoch = 0;
 };
 
 // one TLOG entry: 32 B so a lane moves it with two 16-B accesses and an

@@ -21,14 +21,14 @@
 // bit per slot) is merged by the wide kernel; the others are copied into a
 // duplicate list that is folded in later -- before the next read or SET of
 // the register file, or when the list could fill -- since LWW is a join and
-// the fold's timing and order do not change the result.  The fold is ONE
-// cooperative launch (k_treg_fold_coop): parallel ROUNDS over the whole GPU
-// with a grid barrier between them (each round merges the first record of
-// every slot in the list and moves the rest to the other list), so a key
-// that arrives many times costs one round per extra occurrence, not a serial
-// walk; one wave folds whatever the rounds leave (unbounded repeats only).
-// An empty list costs the launch alone: every workgroup reads the count and
-// returns.  No merge records an event, so merges run back to back.
+// the fold's timing and order do not change the result.  The fold is a few
+// parallel ROUNDS, one ordinary launch each (k_treg_fold_round: each merges
+// the first record of every slot in its list and moves the rest to the next
+// list), so a key that arrives many times costs one round per extra
+// occurrence, not a serial walk; one wave folds whatever the rounds leave
+// (unbounded repeats only).  An empty list costs the launches alone: every
+// workgroup reads the count from HBM and returns.  No merge records an event
+// or waits for the host, so merges run back to back.
 // Routed runs are merged one source per launch: keys that several peers
 // flushed in the same step never become duplicates.  A dense batch in slot
 // order costs the claim one atomic instruction per wave.  Two claim bitmaps
@@ -46,8 +46,6 @@
 #include <algorithm>
 #include <cstring>
 
-
-#include <hip/hip_cooperative_groups.h>
 
 #include "jy_dscan.hpp"
 #include "jy_internal.hpp"
@@ -339,106 +337,80 @@ __device__ void fold_wave(const TregK& K, const u64* __restrict__ list, u32 n) {
   }
 }
 
-// The fold: ONE cooperative launch over the pending duplicate list (list 0;
-// list 1 is the other round's).  Round r merges the first record of every
-// slot (a claim bitmap of its own, cleared by the round's items after the
-// grid barrier) and pushes the others to the other list; after kRounds
-// rounds, one wave folds what is left (a slot repeated more often).  Both
-// counts are zero afterwards.  Every workgroup reads the same counts, so an
-// empty list (the usual case) returns everywhere before any barrier.
+// The fold: kFoldRounds ordinary launches and a one-wave tail, in stream
+// order behind the merges that pushed the records (the kernel boundaries are
+// the barriers between rounds).  Round r reads list r's count from the
+// device -- an empty list (the usual case) returns in every workgroup at
+// once -- merges the first record of every slot and pushes the others to
+// list r + 1.  The first record is found with a claim word per slot holding
+// the round's epoch (a number the host never reuses until it resets the
+// words), so no round clears anything.  Counts: cnt[0] is the pending list's,
+// cnt[1..kFoldRounds] the rounds' outputs (all zero between folds; the tail
+// zeroes them); the records alternate between the two lists.
 constexpr int kFoldRounds = 3;
 struct FoldK {
-  TregK K;      // state (and the pending registers for kSet)
-  u32* cnt0;    // list 0 count (the pending list)
-  u64* lst0;
-  u32* cnt1;    // list 1 count
-  u64* lst1;
-  u32* bits;    // the fold's claim bitmap (zero between folds)
+  TregK K;       // state (and the pending registers for kSet)
+  u32* cin;      // this round's input count and list
+  const u64* lin;
+  u32* claim;    // per slot: the epoch of the round that last claimed it
+  u32 epoch;
 };
 template <bool kSet>
-__global__ __launch_bounds__(kThreads) void k_treg_fold_coop(FoldK F) {
-  namespace cg = cooperative_groups;
-  cg::grid_group grid = cg::this_grid();
+__global__ __launch_bounds__(kThreads) void k_treg_fold_round(FoldK F) {
   constexpr int U = 2;
-  u64 n = fold_count(*F.cnt0, F.K.dup_cap);
+  const u64 n = fold_count(*F.cin, F.K.dup_cap);
   if (n == 0) return;
-  u32* cin = F.cnt0;
-  u64* lin = F.lst0;
-  u32* cout = F.cnt1;
-  u64* lout = F.lst1;
-  for (int r = 0; r < kFoldRounds && n > 0; r++) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *cout = 0;
-    grid.sync();  // the output count is zero before anyone pushes
-    TregK K = F.K;
-    K.seen = F.bits;
-    K.dupn = cout;
-    K.dups = lout;
-    u32 pushed = 0;
-    for (u64 b0 = (u64)blockIdx.x * (kThreads * U); b0 < n; b0 += (u64)gridDim.x * (kThreads * U)) {
-      const u64 base = b0 + (threadIdx.x >> 6) * (64 * U) + (threadIdx.x & 63);
-      u32 s[U];
-      u64 t[U], p[U], l[U], t0[U];
-      bool valid[U], first[U];
+  const TregK& K = F.K;  // K.dupn / K.dups: the round's output list
+  u32 pushed = 0;
+  for (u64 b0 = (u64)blockIdx.x * (kThreads * U); b0 < n; b0 += (u64)gridDim.x * (kThreads * U)) {
+    const u64 base = b0 + (threadIdx.x >> 6) * (64 * U) + (threadIdx.x & 63);
+    u32 s[U];
+    u64 t[U], p[U], l[U];
+    bool valid[U];
 #pragma unroll
-      for (int u = 0; u < U; u++) {
-        const u64 i = base + (u64)u * 64;
-        valid[u] = i < n;
-        s[u] = 0;
-        if (valid[u]) {
-          const u64x2 a = reinterpret_cast<const u64x2*>(lin + i * 4)[0];
-          const u64x2 b = reinterpret_cast<const u64x2*>(lin + i * 4)[1];
-          s[u] = (u32)a.x;
-          t[u] = a.y;
-          p[u] = b.x;
-          l[u] = b.y;
-        }
+    for (int u = 0; u < U; u++) {
+      const u64 i = base + (u64)u * 64;
+      valid[u] = i < n;
+      s[u] = 0;
+      if (valid[u]) {
+        const u64x2 a = reinterpret_cast<const u64x2*>(F.lin + i * 4)[0];
+        const u64x2 b = reinterpret_cast<const u64x2*>(F.lin + i * 4)[1];
+        s[u] = (u32)a.x;
+        t[u] = a.y;
+        p[u] = b.x;
+        l[u] = b.y;
       }
-      if (!kSet) {
+    }
 #pragma unroll
-        for (int u = 0; u < U; u++)
-          if (valid[u]) t0[u] = K.ts[s[u]];
+    for (int u = 0; u < U; u++) {
+      if (!valid[u]) continue;
+      if (atomicExch(F.claim + s[u], F.epoch) == F.epoch) {  // not the slot's first record this round
+        pushed |= push_dup(K, s[u], t[u], p[u], l[u]);
+        continue;
       }
-      jy_claim_rows<U>(valid, s, K.seen, first);
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        if (!valid[u]) continue;
-        if (!first[u]) {
-          pushed |= push_dup(K, s[u], t[u], p[u], l[u]);
-          continue;
-        }
-        if (kSet) {
-          set_one(K, s[u], t[u], p[u], l[u]);
-        } else if (t[u] >= t0[u] && lww_wins(t[u], t0[u], p[u], l[u], K.val, s[u], K.arena)) {
+      if (kSet) {
+        set_one(K, s[u], t[u], p[u], l[u]);
+      } else {
+        const u64 t0 = K.ts[s[u]];
+        if (t[u] >= t0 && lww_wins(t[u], t0, p[u], l[u], K.val, s[u], K.arena)) {
           K.ts[s[u]] = t[u];
           K.val[s[u]] = TVal{p[u], l[u]};
         }
       }
     }
-    dup_publish(K, pushed);
-    grid.sync();  // every merge and push of the round is done
-    // the round's claim bits back to zero (each item its own slot's bit;
-    // repeats clear the same bit)
-    for (u64 i = (u64)blockIdx.x * kThreads + threadIdx.x; i < n; i += (u64)gridDim.x * kThreads) {
-      const u32 s = (u32)lin[i * 4];
-      atomicAnd(F.bits + (s >> 5), ~(1u << (s & 31)));
-    }
-    n = fold_count(__hip_atomic_load(cout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), F.K.dup_cap);
-    u32* tc = cin;
-    cin = cout;
-    cout = tc;
-    u64* tl = lin;
-    lin = lout;
-    lout = tl;
   }
-  grid.sync();  // every workgroup has read the counts; the clears are done
-  if (blockIdx.x != 0) return;
-  if (threadIdx.x < 64) {
-    TregK K = F.K;
-    if (n) fold_wave<kSet>(K, lin, (u32)n);
-    if (threadIdx.x == 0) {
-      *F.cnt0 = 0;
-      *F.cnt1 = 0;
-    }
+  dup_publish(K, pushed);
+}
+
+// the tail: one wave folds what the rounds left (a slot repeated more than
+// kFoldRounds times in the list) and zeroes every count
+template <bool kSet>
+__global__ __launch_bounds__(64) void k_treg_fold_tail(TregK K, u32* cnt0, u32* rcnt, const u64* list) {
+  const u64 n = fold_count(rcnt[kFoldRounds - 1], K.dup_cap);
+  if (n) fold_wave<kSet>(K, list, (u32)n);
+  if (threadIdx.x == 0) {
+    *cnt0 = 0;
+    for (int r = 0; r < kFoldRounds; r++) rcnt[r] = 0;
   }
 }
 
@@ -536,7 +508,8 @@ int32_t claim_bits(jy_engine* eng, u32 nblocks, TregK& K) {
   return JY_OK;
 }
 
-// the second list, its count and the fold's claim bitmap (zero between folds)
+// the second list, the rounds' counts and the fold's claim words (one per
+// slot of the register file's capacity)
 int32_t fold_bufs(jy_engine* eng) {
   TregState& t = eng->treg;
   if (!t.dups_alt) {
@@ -544,55 +517,69 @@ int32_t fold_bufs(jy_engine* eng) {
                         "treg duplicate list"));
   }
   if (!t.dupn_alt) {
-    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.dupn_alt), 64, "treg duplicate count"));
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.dupn_alt), 64, "treg fold counts"));
     JY_HIP(eng, hipMemsetAsync(t.dupn_alt, 0, 64, eng->stream));
   }
-  if (t.fold_words < t.seen_words || !t.fold_bits) {
-    jy_dev_free(eng, t.fold_bits);
-    t.fold_words = t.seen_words;
-    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.fold_bits), (t.fold_words + 16) * 4, "treg fold bitmap"));
-    JY_HIP(eng, hipMemsetAsync(t.fold_bits, 0, (t.fold_words + 16) * 4, eng->stream));
+  const u64 slots = t.seen_words * 32;
+  if (t.fold_slots < slots || !t.fold_claim) {
+    jy_dev_free(eng, t.fold_claim);
+    t.fold_claim = nullptr;
+    t.fold_slots = slots;
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&t.fold_claim), std::max<u64>(slots, 1) * 4,
+                        "treg fold claim words"));
+    JY_HIP(eng, hipMemsetAsync(t.fold_claim, 0, std::max<u64>(slots, 1) * 4, eng->stream));
+    t.fold_epoch = 0;
   }
   return JY_OK;
 }
 
-// workgroups of the cooperative fold: every one resident at once
-template <bool kSet>
-u32 fold_grid(jy_engine* eng) {
-  int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_treg_fold_coop<kSet>),
-                                                   kThreads, 0) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, eng->device) != hipSuccess)
-    return 0;
-  return (u32)std::max(1, std::min(per_cu, 2) * cus);
-}
-
-// the fold (stream order): one cooperative launch folds every pending
-// duplicate; an empty list returns at once on the device
+// the fold (stream order): kFoldRounds round launches and the tail; with
+// nothing pushed every launch reads a zero count and returns.  Round 0's grid
+// covers the records that may be pending (dup_bound); later rounds hold the
+// repeats of repeats, a small grid strides over them.
 int32_t fold_launch(jy_engine* eng, bool set) {
   TregState& t = eng->treg;
   if (!t.dups) return JY_OK;  // nothing was ever claimed
   JY_TRY(fold_bufs(eng));
-  FoldK F{};
-  F.K = state_of(eng);
-  if (set) {
-    F.K.pts = t.dts;
-    F.K.pval = t.dval;
-    F.K.pflag = t.dflag;
-    F.K.pcount = t.dcount;
+  if (t.fold_epoch > 0xFFFFFFF0u) {  // epochs are never reused: reset the words
+    JY_HIP(eng, hipMemsetAsync(t.fold_claim, 0, std::max<u64>(t.fold_slots, 1) * 4, eng->stream));
+    t.fold_epoch = 0;
   }
-  F.cnt0 = t.dupn;
-  F.lst0 = t.dups;
-  F.cnt1 = t.dupn_alt;
-  F.lst1 = t.dups_alt;
-  F.bits = t.fold_bits;
-  u32& grid = set ? t.fold_grid_set : t.fold_grid;
-  if (!grid) grid = set ? fold_grid<true>(eng) : fold_grid<false>(eng);
-  if (!grid) return eng->fail(JY_EHIP, "treg fold: occupancy query failed");
-  void* args[] = {&F};
-  const void* fn = set ? reinterpret_cast<const void*>(&k_treg_fold_coop<true>)
-                       : reinterpret_cast<const void*>(&k_treg_fold_coop<false>);
-  JY_HIP(eng, hipLaunchCooperativeKernel(fn, dim3(grid), dim3(kThreads), args, 0, eng->stream));
+  TregK K = state_of(eng);
+  if (set) {
+    K.pts = t.dts;
+    K.pval = t.dval;
+    K.pflag = t.dflag;
+    K.pcount = t.dcount;
+  }
+  u32* cnt[kFoldRounds + 1];
+  cnt[0] = t.dupn;
+  for (int r = 1; r <= kFoldRounds; r++) cnt[r] = t.dupn_alt + (r - 1);
+  u64* lst[2] = {t.dups, t.dups_alt};
+  const u64 pending = std::min<u64>(t.dup_bound, t.dup_cap);
+  for (int r = 0; r < kFoldRounds; r++) {
+    FoldK F{};
+    F.K = K;
+    F.K.dupn = cnt[r + 1];
+    F.K.dups = lst[(r + 1) & 1];
+    F.cin = cnt[r];
+    F.lin = lst[r & 1];
+    F.claim = t.fold_claim;
+    F.epoch = ++t.fold_epoch;
+    const u32 grid = r == 0 ? std::min<u32>(blocks(pending, kThreads * 2), 4096) : 256;
+    if (set)
+      hipLaunchKernelGGL(k_treg_fold_round<true>, dim3(grid), dim3(kThreads), 0, eng->stream, F);
+    else
+      hipLaunchKernelGGL(k_treg_fold_round<false>, dim3(grid), dim3(kThreads), 0, eng->stream, F);
+    JY_HIP(eng, hipGetLastError());
+  }
+  if (set)
+    hipLaunchKernelGGL(k_treg_fold_tail<true>, dim3(1), dim3(64), 0, eng->stream, K, t.dupn, t.dupn_alt,
+                       lst[kFoldRounds & 1]);
+  else
+    hipLaunchKernelGGL(k_treg_fold_tail<false>, dim3(1), dim3(64), 0, eng->stream, K, t.dupn, t.dupn_alt,
+                       lst[kFoldRounds & 1]);
+  JY_HIP(eng, hipGetLastError());
   t.dup_bound = 0;
   return JY_OK;
 }
