@@ -338,6 +338,16 @@ int32_t jy_treg_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, co
                            uint64_t* hdr_dev, uint32_t* ovf_dev);
 int32_t jy_treg_converge_routed(jy_engine* eng, uint32_t nsrc, uint64_t cap, uint64_t cap_byte,
                                 const uint64_t* recs_dev, const uint8_t* bytes_dev, const uint64_t* hdr_dev);
+/* The same merge when the byte runs were received straight into this
+ * engine's arena: jy_arena_reserve(eng, JY_TREG, nsrc * cap_byte, &dst,
+ * &rebase) hands out the arena's tail (dst stays valid until the next call
+ * that grows that arena), the exchange (or, for the sender's own run,
+ * jy_treg_route_part with bytes_dev = dst) writes there, and
+ * jy_treg_converge_routed_at merges with the runs at arena offset `rebase`
+ * -- no append copy of the byte runs. */
+int32_t jy_arena_reserve(jy_engine* eng, int32_t type, uint64_t bytes, uint8_t** dev_out, uint64_t* rebase_out);
+int32_t jy_treg_converge_routed_at(jy_engine* eng, uint32_t nsrc, uint64_t cap, uint64_t cap_byte,
+                                   const uint64_t* recs_dev, const uint64_t* hdr_dev, uint64_t rebase);
 
 /* ---- cross-shard key resolution (k_keyroute.hip): `_data_for(key)`
  * (repo_treg.pony:37-42, every repo_*.pony) when the key's slot lives on

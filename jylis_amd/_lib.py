@@ -117,6 +117,8 @@ SIGNATURES = {
     "jy_keys_route_back": (I32, [P, U64, P, P, P]),
     "jy_treg_route_part": (I32, [P, U64, P, P, P, P, P, U32, U64, U64, I32, P, P, P, P]),
     "jy_treg_converge_routed": (I32, [P, U32, U64, U64, P, P, P]),
+    "jy_arena_reserve": (I32, [P, I32, U64, P, P]),
+    "jy_treg_converge_routed_at": (I32, [P, U32, U64, U64, P, P, U64]),
     "jy_route_words": (U64, [I32, U64, P]),
     "jy_tlog_route_part": (I32, [P, U64, P, P, P, P, U64, P, P, P, U32, U64, U64, U64, U64, I32, P, P, P, P]),
     "jy_tlog_converge_routed": (I32, [P, U32, U64, U64, U64, P, P]),

@@ -117,6 +117,31 @@ int32_t jy_arena_append_dev(jy_engine* eng, int32_t type, const uint8_t* src, u6
   return JY_OK;
 }
 
+// room for `bytes` more at the tail of a type's arena (8-byte granule): the
+// device pointer to write them through and their arena offset.  The pointer
+// stays valid until the next call that grows this arena (an append, a pack,
+// a collection); a routed receiver lands its byte runs there directly
+// (jy_treg_converge_routed_at) instead of appending a copy.
+extern "C" int32_t jy_arena_reserve(jy_engine* eng, int32_t type, uint64_t bytes, uint8_t** dev_out,
+                                    uint64_t* rebase_out) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (type != JY_TREG && type != JY_TLOG) return eng->fail(JY_EINVAL, "only TREG and TLOG hold an arena");
+  Arena& a = eng->arena[type];
+  const u64 at = (a.len + kArenaAlign - 1) / kArenaAlign * kArenaAlign;
+  if ((at + bytes) >> (64 - JY_LR_LEN_BITS)) return eng->fail(JY_ERANGE, "arena offset overflow");
+  if (at + bytes > a.cap || !a.p) {
+    const u64 nc = std::max<u64>(std::max<u64>(a.cap * 2, at + bytes), 1 << 16);
+    void* p = a.p;
+    JY_TRY(jy_realloc(eng, &p, a.len, nc, false));
+    a.p = static_cast<uint8_t*>(p);
+    a.cap = nc;
+  }
+  a.len = at + bytes;
+  *dev_out = a.p + at;
+  *rebase_out = at;
+  return JY_OK;
+}
+
 extern "C" int32_t jy_arena_usage(jy_engine* eng, int32_t type, uint64_t* len_out, uint64_t* cap_out) {
   if (type < 0 || type >= JY_NTYPES) return eng->fail(JY_EINVAL, "bad type");
   *len_out = eng->arena[type].len;

@@ -46,6 +46,13 @@ __device__ __forceinline__ u64 round_up8(u64 x) { return (x + kArenaAlign - 1) &
 // u*64 + lane): owner d's counts live in lane d's registers (S <= 64), no LDS
 // and no barrier (45 -> 29 us at 8M entries against a 256-thread workgroup
 // with LDS counts per wave).
+// Measured and dropped in round 4 (routed TREG step at 8M entries, kernel
+// trace): ONE pass with a decoupled look-back over ticketed tiles -- 0.41-
+// 0.54 ms for the pass, the tickets (one same-address atomic per workgroup,
+// 32K of them) serialise; 1024-entry tiles, four per ticket, chained every
+// workgroup behind the previous one's last tile (60 ms); block sums added
+// atomically by the count instead of the scan -- the count went 29 -> 120 us
+// (the block rows share a few lines) and the placement's base sums cost 18 us.
 constexpr int kSlices = 4;        // 64-entry slices per count tile (one wave)
 constexpr int kT = 64 * kSlices;  // entries per tile (count and place)
 constexpr int kWG = 256;          // count: threads per workgroup = 4 tiles
@@ -255,6 +262,18 @@ int32_t jy_treg_converge_routed(jy_engine* eng, uint32_t nsrc, uint64_t cap, uin
   // records address them relative to their run
   u64 rebase;
   JY_TRY(jy_arena_append_dev(eng, JY_TREG, bytes_dev, (u64)nsrc * cap_byte, &rebase));
+  return jy_treg_merge_routed(eng, nsrc, cap, cap_byte, recs_dev, hdr_dev, rebase);
+}
+
+// the received byte runs already sit in this engine's TREG arena at `rebase`
+// (jy_arena_reserve; the exchange landed them there): no append copy
+int32_t jy_treg_converge_routed_at(jy_engine* eng, uint32_t nsrc, uint64_t cap, uint64_t cap_byte,
+                                   const uint64_t* recs_dev, const uint64_t* hdr_dev, uint64_t rebase) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (nsrc == 0 || cap == 0) return JY_OK;
+  if (cap_byte % kArenaAlign || rebase % kArenaAlign) return eng->fail(JY_EINVAL, "cap_byte and rebase: multiples of 8");
+  if (rebase + (u64)nsrc * cap_byte > eng->arena[JY_TREG].len)
+    return eng->fail(JY_ERANGE, "the byte runs lie outside the arena's reserved bytes");
   return jy_treg_merge_routed(eng, nsrc, cap, cap_byte, recs_dev, hdr_dev, rebase);
 }
 

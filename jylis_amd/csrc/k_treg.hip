@@ -219,25 +219,21 @@ __global__ __launch_bounds__(kThreads) void k_treg_lww(TregK K, const u32* __res
   dup_publish(K, pushed);
 }
 
-// Routed runs (receiver side of the exchange, k_route.hip): S source runs
-// of 32-B records {slot on this owner, ts, pre, lr'} at recs[src * cap ..],
-// each holding hdr[2 * src] records (counts travel with the data: no host
-// round trip).  A hole (slot ~0) is a record whose value bytes overflowed
-// the sender's byte run; a slot this shard never handed out is counted as
-// skipped.  lr' offsets are relative to the source's byte run, which sits at
-// arena offset rebase + src * cap_byte.
+// Routed runs (receiver side of the exchange, k_route.hip): one source's run
+// per launch, 32-B records {slot on this owner, ts, pre, lr'} at recs[0 ..],
+// hdr[0] of them (counts travel with the data: no host round trip).  A hole
+// (slot ~0) is a record whose value bytes overflowed the sender's byte run;
+// a slot this shard never handed out is counted as skipped.  lr' offsets are
+// relative to the source's byte run, which sits at arena offset `rebase`.
 struct RoutedIn {
   const u64* recs;
   const u64* hdr;
-  u32 S;
-  u64 cap, cap_byte, rebase, nslots;
+  u64 cap, rebase, nslots;
   unsigned long long* skipped;
 };
 
-__device__ __forceinline__ bool routed_get(const RoutedIn& R, u64 i, u32& s, u64& t, u64& p, u64& l) {
-  const u64 src = i / R.cap, j = i - src * R.cap;
-  const u64 cnt = R.hdr[2 * src];
-  if (j >= (cnt < R.cap ? cnt : R.cap)) return false;
+__device__ __forceinline__ bool routed_get(const RoutedIn& R, u64 cnt, u64 i, u32& s, u64& t, u64& p, u64& l) {
+  if (i >= cnt) return false;
   const u64x2 a = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(R.recs + i * 4));
   const u64x2 b = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(R.recs + i * 4) + 1);
   if (a.x == ~0ull) return false;  // hole
@@ -249,8 +245,7 @@ __device__ __forceinline__ bool routed_get(const RoutedIn& R, u64 i, u32& s, u64
   t = a.y;
   p = b.x;
   l = b.y;
-  if ((l & JY_LR_LEN_MASK) > 8)
-    l = (((l >> JY_LR_LEN_BITS) + R.rebase + src * R.cap_byte) << JY_LR_LEN_BITS) | (l & JY_LR_LEN_MASK);
+  if ((l & JY_LR_LEN_MASK) > 8) l = (((l >> JY_LR_LEN_BITS) + R.rebase) << JY_LR_LEN_BITS) | (l & JY_LR_LEN_MASK);
   return true;
 }
 
@@ -261,7 +256,7 @@ __device__ __forceinline__ bool routed_get(const RoutedIn& R, u64 i, u32& s, u64
 __global__ __launch_bounds__(kThreads) void k_treg_lww_routed(TregK K, RoutedIn R) {
   constexpr int U = 2;
   const u64 base = (u64)blockIdx.x * (kThreads * U) + (threadIdx.x >> 6) * (64 * U) + (threadIdx.x & 63);
-  const u64 n = (u64)R.S * R.cap;
+  const u64 cnt = R.hdr[0] < R.cap ? R.hdr[0] : R.cap;
   u32 s[U];
   u64 t[U], p[U], l[U], t0[U];
   bool valid[U], first[U];
@@ -269,7 +264,7 @@ __global__ __launch_bounds__(kThreads) void k_treg_lww_routed(TregK K, RoutedIn 
   for (int u = 0; u < U; u++) {
     const u64 i = base + (u64)u * 64;
     s[u] = 0;
-    valid[u] = i < n && routed_get(R, i, s[u], t[u], p[u], l[u]);
+    valid[u] = routed_get(R, cnt, i, s[u], t[u], p[u], l[u]);
   }
 #pragma unroll
   for (int u = 0; u < U; u++)
@@ -703,7 +698,7 @@ int32_t jy_treg_merge_routed(jy_engine* eng, u32 S, u64 cap, u64 cap_byte, const
   for (u32 src = 0; src < S; src++) {
     TregK K{};
     JY_TRY(claim_begin(eng, cap, grid, K));
-    RoutedIn R{recs + (u64)src * cap * 4, hdr + 2 * (u64)src, 1, cap, cap_byte, rebase + (u64)src * cap_byte,
+    RoutedIn R{recs + (u64)src * cap * 4, hdr + 2 * (u64)src, cap, rebase + (u64)src * cap_byte,
                eng->nkeys[JY_TREG], reinterpret_cast<unsigned long long*>(eng->skipped_dev)};
     hipLaunchKernelGGL(k_treg_lww_routed, dim3(grid), dim3(kThreads), 0, eng->stream, K, R);
     JY_HIP(eng, hipGetLastError());

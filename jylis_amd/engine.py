@@ -261,6 +261,13 @@ class Engine:
         self._check(self.lib.jy_arena_usage(self.h, ctype, C.byref(n), C.byref(c)))
         return n.value, c.value
 
+    def arena_reserve(self, ctype, nbytes):
+        """room for `nbytes` at the tail of a type's value arena (jy_arena_reserve):
+        (device pointer, arena offset); valid until the arena next grows"""
+        p, r = C.c_void_p(), C.c_uint64()
+        self._check(self.lib.jy_arena_reserve(self.h, ctype, nbytes, C.byref(p), C.byref(r)))
+        return p.value or 0, r.value
+
     def arena_collect(self, ctype):
         """reclaim dead value bytes (jy_arena_collect); unmerged packed handles become invalid.
         Refused while a router holds rounds of this engine's batches in flight: their

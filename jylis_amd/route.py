@@ -248,6 +248,23 @@ def round8(x):
     return (int(x) + 7) // 8 * 8
 
 
+class _CudaBytes:
+    """__cuda_array_interface__ of `n` bytes of device memory the engine owns"""
+    def __init__(self, ptr, n):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (ptr, False), "version": 2,
+                                         "strides": None}
+
+
+def _device_bytes(ptr, n, device):
+    """a uint8 tensor over engine-owned device memory (no copy, not owned by torch)"""
+    import torch
+    if n == 0:
+        return torch.empty(0, dtype=torch.uint8, device=torch.device("cuda", device))
+    t = torch.as_tensor(_CudaBytes(ptr, n), device=torch.device("cuda", device))
+    assert t.data_ptr() == ptr and t.dtype == torch.uint8
+    return t
+
+
 def long_bytes(lr):
     """padded bytes of the values longer than 8 bytes among value handles
     `lr` (numpy uint64 or CUDA int64 tensor): what their runs' byte sections take"""
@@ -363,7 +380,7 @@ class _RunRouter:
                     self._merge(eng, snd, caps)
         else:
             def issue(c):
-                recv = [tuple(torch.empty_like(x) for x in snd) for snd in sends[c]]
+                recv = [self._recv_bufs(eng, snd, caps) for eng, snd in zip(self.engs, sends[c])]
                 works = [fab.a2a([r[k] for r in recv], [s_[k] for s_ in sends[c]], async_op=True)
                          for k in range(len(sends[c][0]))]
                 return recv, works
@@ -379,6 +396,11 @@ class _RunRouter:
                     self._merge(eng, rcv, caps)
         self.routed += 1
         return ovfs
+
+    def _recv_bufs(self, eng, snd, caps):
+        """the receive buffers of one local rank (shaped like its send buffers)"""
+        import torch
+        return tuple(torch.empty_like(x) for x in snd)
 
     def _publish(self, batches, ovfs):
         """global max of the overflow counts, copied to pinned memory behind an event"""
@@ -445,6 +467,23 @@ class TregRouter(_RunRouter):
     def _drain_caps(self, m):
         return (max(m[0], 1), round8(max(m[1], 8)))
 
+    # The receivers' byte runs land straight in their TREG arenas
+    # (jy_arena_reserve): one shard sends to itself by writing there from the
+    # partition, several receive there through the exchange, and the merge
+    # (jy_treg_converge_routed_at) addresses them in place -- no append copy.
+    def _arena_bytes(self, eng, nbytes):
+        """this engine's arena tail for `nbytes` received bytes: (uint8 tensor over it, rebase)"""
+        import torch
+        dst, rebase = eng.arena_reserve(_lib.TREG, nbytes)
+        self._rebase[id(eng)] = rebase
+        return _device_bytes(dst, nbytes, eng.device), rebase
+
+    def _recv_bufs(self, eng, snd, caps):
+        import torch
+        hdr, recs, _ = snd
+        byts, _ = self._arena_bytes(eng, self.S * caps[1])
+        return (torch.empty_like(hdr), torch.empty_like(recs), byts)
+
     def _part(self, eng, b, caps, a, e, ovf):
         import torch
         S = self.S
@@ -454,7 +493,12 @@ class TregRouter(_RunRouter):
         assert (a, e) == (0, n), "TREG rounds are not chunked"
         dev = torch.device("cuda", eng.device)
         recs = torch.empty((S * cap, 4), dtype=torch.int64, device=dev)
-        byts = torch.empty(S * capb, dtype=torch.uint8, device=dev)
+        if not hasattr(self, "_rebase"):
+            self._rebase = {}
+        if S == 1:  # its own receiver: the run's bytes go to the arena directly
+            byts, _ = self._arena_bytes(eng, capb)
+        else:
+            byts = torch.empty(S * capb, dtype=torch.uint8, device=dev)
         hdr = torch.empty((S, 2), dtype=torch.int64, device=dev)
         if n:
             for t in (own, slot, ts, pre, lr):
@@ -468,8 +512,8 @@ class TregRouter(_RunRouter):
 
     def _merge(self, eng, rcv, caps):
         hdr, recs, byts = rcv
-        eng._check(eng.lib.jy_treg_converge_routed(eng.h, self.S, caps[0], caps[1], self._ptr(recs), self._ptr(byts),
-                                                   self._ptr(hdr)))
+        eng._check(eng.lib.jy_treg_converge_routed_at(eng.h, self.S, caps[0], caps[1], self._ptr(recs),
+                                                      self._ptr(hdr), self._rebase.pop(id(eng))))
 
     def _subset(self, b, idx):
         own, slot, ts, pre, lr = (t.index_select(0, idx).contiguous() for t in b[:5])
