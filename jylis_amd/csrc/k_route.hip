@@ -121,9 +121,13 @@ __global__ __launch_bounds__(256) void k_rt_place(const u32* __restrict__ owner,
                                                  unsigned long long* __restrict__ skipped) {
   constexpr int kW = 256 / 64;
   __shared__ u64 wt[kW][kMaxShards * 2];
+  __shared__ u64 tbase[kMaxShards * 2];
   for (u32 j = threadIdx.x; j < S * 2; j += kT) {
 #pragma unroll
     for (int w = 0; w < kW; w++) wt[w][j] = 0;
+    // the tile's base per column (less the column's base, row 0): loaded
+    // before the entries' ranks are known, in flight with their loads
+    tbase[j] = tcnt[(u64)blockIdx.x * S * 2 + j] - tcnt[j];
   }
   __syncthreads();
   const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
@@ -131,6 +135,7 @@ __global__ __launch_bounds__(256) void k_rt_place(const u32* __restrict__ owner,
   const u64 lt = (1ull << lane) - 1;
   u32 o = 0xFFFFFFFFu, sl = 0;
   u64 t = 0, p = 0, l = 0, b = 0;
+  u64 g0 = 0, g1 = 0;  // a long value's first two 8-B granules, loaded early
   if (i < n) {
     o = owner[i];
     sl = slot[i];
@@ -139,6 +144,11 @@ __global__ __launch_bounds__(256) void k_rt_place(const u32* __restrict__ owner,
     l = lr[i];
     const u64 len = l & JY_LR_LEN_MASK;
     b = len > 8 ? round_up8(len) : 0;
+    if (b) {
+      const u64* src = reinterpret_cast<const u64*>(arena + (l >> JY_LR_LEN_BITS));
+      g0 = src[0];
+      g1 = src[1];
+    }
   }
   const bool valid = i < n && o < S;
   if (i < n && !valid) atomicAdd(skipped, 1ull);  // an owner outside [0, S): dropped, counted
@@ -164,8 +174,7 @@ __global__ __launch_bounds__(256) void k_rt_place(const u32* __restrict__ owner,
   }
   __syncthreads();
   if (!valid) return;
-  const u64* tb = tcnt + (u64)blockIdx.x * S * 2 + o * 2;  // less the column's base (row 0)
-  u64 pos = tb[0] - tcnt[o * 2] + rk, bpos = tb[1] - tcnt[o * 2 + 1] + bk;
+  u64 pos = tbase[o * 2] + rk, bpos = tbase[o * 2 + 1] + bk;
   for (int w = 0; w < wv; w++) {
     pos += wt[w][o * 2];
     bpos += wt[w][o * 2 + 1];
@@ -183,7 +192,9 @@ __global__ __launch_bounds__(256) void k_rt_place(const u32* __restrict__ owner,
   if (b) {  // the value's 8-B granules into the run's byte section
     const u64* src = reinterpret_cast<const u64*>(arena + (l >> JY_LR_LEN_BITS));
     u64* dst = reinterpret_cast<u64*>(bytes + (u64)o * cap_byte + bpos);
-    for (u64 w = 0; w < b / 8; w++) dst[w] = src[w];
+    dst[0] = g0;  // b >= 16: a long value has two granules at least
+    dst[1] = g1;
+    for (u64 w = 2; w < b / 8; w++) dst[w] = src[w];
     out_lr = (bpos << JY_LR_LEN_BITS) | (l & JY_LR_LEN_MASK);
   }
   u64x2* r = reinterpret_cast<u64x2*>(recs + ((u64)o * cap + pos) * 4);  // 32-B records, two 16-B stores
