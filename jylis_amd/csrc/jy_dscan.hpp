@@ -73,6 +73,13 @@ __device__ __forceinline__ u64 block_excl(u64 x, u64* lds, u64& total) {
   return op(off, lane == 0 ? Op::kId : ex);
 }
 
+// sum over the workgroup (every thread calls; every thread gets it)
+__device__ __forceinline__ u64 block_total(u64 x, u64* lds) {
+  u64 tot;
+  block_excl<OpSum>(x, lds, tot);
+  return tot;
+}
+
 // the look-back of jy_scan.hpp, generic over the operator (values < 2^40)
 template <class Op>
 __device__ __forceinline__ u64 lookback(const Ctx& c, u32 tile, u64 agg, u64* lds) {
@@ -117,83 +124,144 @@ __device__ __forceinline__ u64 lookback(const Ctx& c, u32 tile, u64 agg, u64* ld
   return r;
 }
 
+// Tiles of kTileItems items; a workgroup takes ONE ticket for G consecutive
+// tiles (G = 1 up to kMaxTickets tiles): a ticket is a same-address atomic,
+// and those serialise at ~11 ns each (tools/mb_ticket.hip: 4096 tickets
+// 48 us, 32768 tickets 373 us), so an 8M-item scan spent half its time
+// drawing them.  With G > 1 the workgroup first reduces its G tiles (its
+// look-back aggregate), then scans them again from the top (the re-read is
+// its own recent loads, mostly still in the caches).
+constexpr u64 kMaxTickets = 1024;
+
 // out[i] = Op-prefix of ld(0..i-1) (exclusive) or of ld(0..i) (inclusive),
 // for i < n; items thread-consecutive within a tile
 template <class Op, bool kIncl, class Ld, class St>
-__global__ __launch_bounds__(kThreads) void k_scan(Ctx c, u64 n, u64 ntiles, Ld ld, St st) {
+__global__ __launch_bounds__(kThreads) void k_scan(Ctx c, u64 n, u64 ntiles, u64 G, Ld ld, St st) {
   __shared__ u64 red[kThreads / 64];
   __shared__ u64 pre;
   __shared__ u32 tk;
   Op op;
   const u32 t = jyscan::ticket(c.tick, &tk);
-  if (t == ntiles - 1 && threadIdx.x == 0) *c.tick = 0;  // the launch's last ticket: all are drawn
-  const u64 i0 = (u64)t * kTileItems + (u64)threadIdx.x * kPer;
+  if (t == gridDim.x - 1 && threadIdx.x == 0) *c.tick = 0;  // the launch's last ticket: all are drawn
+  const u64 s0 = (u64)t * G, s1 = s0 + G < ntiles ? s0 + G : ntiles;
   u64 v[kPer], acc = Op::kId;
+  if (s1 - s0 == 1) {  // one tile: loaded once
+    const u64 i0 = s0 * kTileItems + (u64)threadIdx.x * kPer;
 #pragma unroll
-  for (int u = 0; u < kPer; u++) {
-    v[u] = i0 + u < n ? ld(i0 + u) : Op::kId;
-    acc = op(acc, v[u]);
+    for (int u = 0; u < kPer; u++) {
+      v[u] = i0 + u < n ? ld(i0 + u) : Op::kId;
+      acc = op(acc, v[u]);
+    }
+    u64 tot;
+    const u64 off = block_excl<Op>(acc, red, tot);
+    const u64 p = lookback<Op>(c, t, tot, &pre);
+    u64 run = op(p, off);
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+      const u64 i = i0 + u;
+      const u64 nx = op(run, v[u]);
+      if (i < n) st(i, kIncl ? nx : run);
+      run = nx;
+    }
+    return;
+  }
+  for (u64 s = s0; s < s1; s++) {
+    const u64 i0 = s * kTileItems + (u64)threadIdx.x * kPer;
+#pragma unroll
+    for (int u = 0; u < kPer; u++) acc = op(acc, i0 + u < n ? ld(i0 + u) : Op::kId);
   }
   u64 tot;
-  const u64 off = block_excl<Op>(acc, red, tot);
-  const u64 p = lookback<Op>(c, t, tot, &pre);
-  u64 run = op(p, off);
+  block_excl<Op>(acc, red, tot);
+  u64 base = lookback<Op>(c, t, tot, &pre);
+  for (u64 s = s0; s < s1; s++) {
+    const u64 i0 = s * kTileItems + (u64)threadIdx.x * kPer;
+    u64 a = Op::kId;
 #pragma unroll
-  for (int u = 0; u < kPer; u++) {
-    const u64 i = i0 + u;
-    const u64 nx = op(run, v[u]);
-    if (i < n) st(i, kIncl ? nx : run);
-    run = nx;
+    for (int u = 0; u < kPer; u++) {
+      v[u] = i0 + u < n ? ld(i0 + u) : Op::kId;
+      a = op(a, v[u]);
+    }
+    u64 ts;
+    const u64 off = block_excl<Op>(a, red, ts);
+    u64 run = op(base, off);
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+      const u64 i = i0 + u;
+      const u64 nx = op(run, v[u]);
+      if (i < n) st(i, kIncl ? nx : run);
+      run = nx;
+    }
+    base = op(base, ts);
   }
 }
 
 // indices i < n with pred(i), in order, into out; the count into *count
 template <class Pred>
-__global__ __launch_bounds__(kThreads) void k_select(Ctx c, u64 n, u64 ntiles, Pred pred, u32* __restrict__ out,
-                                                     u32* __restrict__ count) {
+__global__ __launch_bounds__(kThreads) void k_select(Ctx c, u64 n, u64 ntiles, u64 G, Pred pred,
+                                                     u32* __restrict__ out, u32* __restrict__ count) {
   __shared__ u64 red[kThreads / 64];
   __shared__ u64 pre;
   __shared__ u32 tk;
   const u32 t = jyscan::ticket(c.tick, &tk);
-  if (t == ntiles - 1 && threadIdx.x == 0) *c.tick = 0;
-  const u64 i0 = (u64)t * kTileItems + (u64)threadIdx.x * kPer;
-  u32 f = 0;
-  u64 acc = 0;
+  if (t == gridDim.x - 1 && threadIdx.x == 0) *c.tick = 0;
+  const u64 s0 = (u64)t * G, s1 = s0 + G < ntiles ? s0 + G : ntiles;
+  u64 agg = 0;  // several tiles: their count first (the look-back aggregate)
+  if (s1 - s0 > 1) {
+    u64 acc = 0;
+    for (u64 s = s0; s < s1; s++) {
+      const u64 i0 = s * kTileItems + (u64)threadIdx.x * kPer;
 #pragma unroll
-  for (int u = 0; u < kPer; u++) {
-    const bool s = i0 + u < n && pred(i0 + u);
-    f |= (u32)s << u;
-    acc += s;
+      for (int u = 0; u < kPer; u++) acc += i0 + u < n && pred(i0 + u);
+    }
+    agg = block_total(acc, red);
   }
-  u64 tot;
-  const u64 off = block_excl<OpSum>(acc, red, tot);
-  const u64 p = lookback<OpSum>(c, t, tot, &pre);
-  u64 pos = p + off;
+  u64 base = 0;
+  for (u64 s = s0; s < s1; s++) {
+    const u64 i0 = s * kTileItems + (u64)threadIdx.x * kPer;
+    u32 f = 0;
+    u64 a = 0;
 #pragma unroll
-  for (int u = 0; u < kPer; u++)
-    if (f >> u & 1) out[pos++] = (u32)(i0 + u);
-  if (t == ntiles - 1 && threadIdx.x == 0) *count = (u32)(p + tot);
+    for (int u = 0; u < kPer; u++) {
+      const bool sel = i0 + u < n && pred(i0 + u);
+      f |= (u32)sel << u;
+      a += sel;
+    }
+    u64 ts;
+    const u64 off = block_excl<OpSum>(a, red, ts);
+    if (s == s0) base = lookback<OpSum>(c, t, s1 - s0 > 1 ? agg : ts, &pre);
+    u64 pos = base + off;
+#pragma unroll
+    for (int u = 0; u < kPer; u++)
+      if (f >> u & 1) out[pos++] = (u32)(i0 + u);
+    base += ts;
+  }
+  if (t == gridDim.x - 1 && threadIdx.x == 0) *count = (u32)base;
 }
 
 inline u64 tiles_of(u64 n) { return n == 0 ? 1 : (n + kTileItems - 1) / kTileItems; }
 
 // a scan launch over n items: ld(i) -> u64, st(i, prefix)
+// tiles per workgroup (one ticket each workgroup) and the workgroups
+inline u64 group_of(u64 nt) { return (nt + kMaxTickets - 1) / kMaxTickets; }
+
 template <class Op, bool kIncl, class Ld, class St>
 int32_t scan(jy_engine* eng, u64 n, Ld ld, St st) {
   if (n == 0) return JY_OK;
-  const u64 nt = tiles_of(n);
+  const u64 nt = tiles_of(n), G = group_of(nt), nwg = (nt + G - 1) / G;
   Ctx c;
-  JY_TRY(jy_dscan_ctx(eng, nt, &c.status, &c.tick, &c.epoch));
-  hipLaunchKernelGGL((k_scan<Op, kIncl, Ld, St>), dim3((u32)nt), dim3(kThreads), 0, eng->stream, c, n, nt, ld, st);
+  JY_TRY(jy_dscan_ctx(eng, nwg, &c.status, &c.tick, &c.epoch));
+  hipLaunchKernelGGL((k_scan<Op, kIncl, Ld, St>), dim3((u32)nwg), dim3(kThreads), 0, eng->stream, c, n, nt, G, ld,
+                     st);
   JY_HIP(eng, hipGetLastError());
   return JY_OK;
 }
 template <class Pred>
 int32_t select(jy_engine* eng, u64 n, Pred pred, u32* out, u32* count) {
-  const u64 nt = tiles_of(n);
+  const u64 nt = tiles_of(n), G = group_of(nt), nwg = (nt + G - 1) / G;
   Ctx c;
-  JY_TRY(jy_dscan_ctx(eng, nt, &c.status, &c.tick, &c.epoch));
-  hipLaunchKernelGGL((k_select<Pred>), dim3((u32)nt), dim3(kThreads), 0, eng->stream, c, n, nt, pred, out, count);
+  JY_TRY(jy_dscan_ctx(eng, nwg, &c.status, &c.tick, &c.epoch));
+  hipLaunchKernelGGL((k_select<Pred>), dim3((u32)nwg), dim3(kThreads), 0, eng->stream, c, n, nt, G, pred, out,
+                     count);
   JY_HIP(eng, hipGetLastError());
   return JY_OK;
 }
