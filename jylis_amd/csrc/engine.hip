@@ -339,6 +339,7 @@ void jy_engine_destroy(jy_engine* eng) {
   F(eng->treg.fold_claim);
   for (TlogState* t : {&eng->tlog, &eng->tlog_d}) {
     F(t->meta);
+    F(t->hint);
     F(t->pool);
     F(t->ctr);
     if (t->pin) hipHostFree(t->pin);

@@ -281,6 +281,10 @@ struct alignas(16) TMeta {
 
 struct TlogState {  // per-slot segments of one entry pool
   TMeta* meta = nullptr;  // [kcap]
+  // [kcap] the oldest surviving timestamp of each log, a HINT for the
+  // interpolated searches (k_tlog_tile): kept by the merges that know it, never
+  // needed for correctness (a stale hint only costs the search a fallback)
+  u64* hint = nullptr;
   TRec* pool = nullptr;   // [pcap]
   u64 pcap = 0;
   u64* ctr = nullptr;     // device: [0] pool entries handed out (bump pointer)

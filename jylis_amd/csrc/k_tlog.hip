@@ -119,6 +119,7 @@ struct alignas(16) PInfo {
 
 struct TlogArgs {
   TMeta* meta;
+  u64* hint;  // [nkeys] oldest-timestamp hints (TlogState::hint)
   const TRec* pool;
   const uint8_t* arena;
   // delta batch
@@ -292,7 +293,7 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
   __shared__ u32 l_gb[kTile];        // first delta entry of each key, less the tile's first (gb0)
   __shared__ u32 l_slot[kTile];
   __shared__ u64 l_oldest[kTile];  // oldest surviving timestamp of a slow key's log
-  __shared__ u64 l_base[kTile], l_newest[kTile], l_cut[kTile], l_tn[kTile];
+  __shared__ u64 l_base[kTile], l_newest[kTile], l_cut[kTile], l_tn[kTile], l_to[kTile];
   __shared__ u32 l_len[kTile], l_cap[kTile], l_drop[kTile], l_M[kTile], l_minrank[kTile], l_bad[kTile],
       l_gstart[kTile], l_mode[kTile];
   const u32 tid = threadIdx.x;
@@ -319,6 +320,7 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
     }
     const bool hole = s == JY_NO_SLOT;  // a routed run's unused record: skipped, not counted
     const TMeta m = hole ? TMeta{0, 0, 0, 0, 0} : A.meta[s];
+    const u64 hv = hole ? 0 : A.hint[s];  // with the meta: no dependent load of the log's first record
     const u64 cd = A.dcut[k];
     const u32 bad = hole ? 4u : A.bad[k];
     const u64 cut = m.cut > cd ? m.cut : cd;
@@ -339,6 +341,13 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
       for (int u = 0; u < kFastEnt; u++)
         if ((u32)u < M) store_rec(pool + m.base + m.len + (M - 1 - u), ft[u], fp[u], fl[u]);
       if (M) A.meta[s] = TMeta{m.base, m.len + M, m.cap, m.cut, (m.len == 0 || ft[0] > m.newest) ? ft[0] : m.newest};
+      if (M && m.len == 0) {  // an empty log's oldest entry: the oldest appended one (kept entries are a prefix)
+        u64 o = ft[0];
+#pragma unroll
+        for (int u = 1; u < kFastEnt; u++)
+          if ((u32)u < M) o = ft[u];
+        A.hint[s] = o;
+      }
     } else {
       u32 drop = 0;
       u64 oldest = 0;
@@ -346,7 +355,7 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
         drop = ts_lower(A.pool, m.base, 0, m.len, cut, oldest);  // oldest first: a prefix
         if (drop == m.len) oldest = 0;
       } else if (m.len > 0) {
-        oldest = A.pool[m.base].ts;
+        oldest = hv;  // the hint (round 3 loaded pool[base].ts here: one dependent random line per slow key)
       }
       l_oldest[tid] = oldest;  // for the interpolated searches
       sc = hole ? 0 : ne;  // a hole's entries (a spill's unspilled keys) are never walked
@@ -360,6 +369,7 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
       l_M[tid] = 0;
       l_minrank[tid] = 0xFFFFFFFFu;
       l_tn[tid] = 0;
+      l_to[tid] = ~0ull;
     }
     l_gb[tid] = (u32)(b0 - A.doff[k0]);
     l_slot[tid] = s;
@@ -443,6 +453,7 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
         atomicAdd(&l_M[idx], 1u);
         atomicMin(&l_minrank[idx], rank);
         atomicMax((unsigned long long*)&l_tn[idx], (unsigned long long)t);  // newest kept
+        atomicMin((unsigned long long*)&l_to[idx], (unsigned long long)t);  // oldest kept (the hint)
       }
     }
 #pragma unroll
@@ -477,6 +488,12 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
       P.newlen = surv + M;
       P.cut = l_cut[tid];
       P.newest = nn;
+      // the merged log's oldest entry, as a hint for later searches (a
+      // spilled rebuild leaves it ahead of the state until its re-merge)
+      if (P.newlen > 0) {
+        const u64 so = l_oldest[tid], dlo = l_to[tid];
+        A.hint[P.s] = surv == 0 ? dlo : (M > 0 && dlo < so ? dlo : so);
+      }
       if ((M == 0 || l_minrank[tid] == len) && (u64)len + M <= l_cap[tid]) {
         mode = kAppend;
         A.meta[P.s] = TMeta{l_base[tid] + drop, P.newlen, l_cap[tid] - drop, P.cut, nn};
@@ -1018,6 +1035,9 @@ int32_t tlog_grow_store(jy_engine* eng, TlogState& t, u64 need) {
   void* m = t.meta;
   JY_TRY(jy_realloc(eng, &m, t.kcap * sizeof(TMeta), nk * sizeof(TMeta), true));  // empty logs
   t.meta = static_cast<TMeta*>(m);
+  void* h = t.hint;
+  JY_TRY(jy_realloc(eng, &h, t.kcap * 8, nk * 8, true));
+  t.hint = static_cast<u64*>(h);
   t.kcap = nk;
   return JY_OK;
 }
@@ -1138,6 +1158,7 @@ int32_t tlog_launch(jy_engine* eng, TlogState& t, int r, u64 nd, const u32* slot
   LAUNCH(k_tlog_prep, nd, A);
   ClaimGuard guard{eng, A.dptr, nk};
   A.meta = t.meta;
+  A.hint = t.hint;
   A.pool = t.pool;
   hipLaunchKernelGGL(k_tlog_tile, dim3(tiles), dim3(kTile), 0, eng->stream, A, t.pool, erank, eqx);
   JY_HIP(eng, hipGetLastError());

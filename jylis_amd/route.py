@@ -472,10 +472,10 @@ class TregRouter(_RunRouter):
     # partition, several receive there through the exchange, and the merge
     # (jy_treg_converge_routed_at) addresses them in place -- no append copy.
     def _arena_bytes(self, eng, nbytes):
-        """this engine's arena tail for `nbytes` received bytes: (uint8 tensor over it, rebase)"""
-        import torch
+        """this engine's arena tail for `nbytes` received bytes: (uint8 tensor over it, rebase);
+        the rebase waits in `_rebase` for the engine's merge of this round"""
         dst, rebase = eng.arena_reserve(_lib.TREG, nbytes)
-        self._rebase[id(eng)] = rebase
+        self.__dict__.setdefault("_rebase", {})[id(eng)] = rebase
         return _device_bytes(dst, nbytes, eng.device), rebase
 
     def _recv_bufs(self, eng, snd, caps):
@@ -493,8 +493,6 @@ class TregRouter(_RunRouter):
         assert (a, e) == (0, n), "TREG rounds are not chunked"
         dev = torch.device("cuda", eng.device)
         recs = torch.empty((S * cap, 4), dtype=torch.int64, device=dev)
-        if not hasattr(self, "_rebase"):
-            self._rebase = {}
         if S == 1:  # its own receiver: the run's bytes go to the arena directly
             byts, _ = self._arena_bytes(eng, capb)
         else:
