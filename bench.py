@@ -414,8 +414,11 @@ def main():
     eng.close()
     del shard
     if routed_on:
-        routed_phase(args, load_shard, dev, dist, rank, world, routed, peer, fabric_of(dist, cpu_group, world),
-                     cells_per_step, line, verify)
+        try:
+            routed_phase(args, load_shard, dev, dist, rank, world, routed, peer, fabric_of(dist, cpu_group, world),
+                         cells_per_step, line, verify)
+        except Exception as e:  # the headline stands; the routed phase's failure is reported in the line
+            line["routed_error"] = f"{type(e).__name__}: {e}"
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:
@@ -468,13 +471,21 @@ def routed_phase(args, load_shard, dev, dist, rank, world, routed, peer, fabric,
     The node is made here, after the headline (its communicator's setup is
     inside the watchdog too), with this rank's shard loaded into its engine.
     A watchdog exits non-zero (printing the line with an error) if a
-    collective hangs.  At N = 1 (--route) both run against one shard."""
+    collective hangs; an exception is reported in the line (`routed_error`),
+    the headline standing.  At N = 1 (--route) both run against one shard."""
+    limit = float(os.environ.get("JY_ROUTED_LIMIT_S", "240"))
+    dog = watchdog(limit, line, rank)
+    try:
+        _routed_phase(args, load_shard, dev, dist, rank, world, routed, peer, fabric, cells_per_step, line, verify)
+    finally:
+        dog.cancel()
+
+
+def _routed_phase(args, load_shard, dev, dist, rank, world, routed, peer, fabric, cells_per_step, line, verify):
     import torch
     from bench_modes import node_for
     from jylis_amd._lib import PNCOUNT
     from jylis_amd.route import CounterRouter
-    limit = float(os.environ.get("JY_ROUTED_LIMIT_S", "240"))
-    dog = watchdog(limit, line, rank)
     R = routed[0].shape[1] * world
     K = routed[0].shape[3]
     # a gloo rehearsal may put several ranks on one GPU: RCCL takes one rank
@@ -544,7 +555,6 @@ def routed_phase(args, load_shard, dev, dist, rank, world, routed, peer, fabric,
     eng.close()
     if node is not None:
         node.close()
-    dog.cancel()
 
 
 if __name__ == "__main__":

@@ -406,8 +406,13 @@ def bench_treg(args, eng, dev, dist, rank, world):
     n = len(slot)
     m = n // 16 if args.resolve else 0  # --resolve: keys new to the node in every step
     batches, keysets = [], []
+    # plain (not routed) and a dense slot range: the block form
+    # (jy_treg_converge_block: no slot stream), then the keyed form over a
+    # continuation of fresh batches, timed beside it
+    block = not routed and not args.resolve and bool((slot == np.arange(len(slot), dtype=slot.dtype)).all())
+    nrun = max(1, args.batches, args.warmup + args.steps)
     # batch 0 = initial state; a distinct batch for every step (no replays)
-    for j in range(max(1, args.batches, args.warmup + args.steps) + 1):
+    for j in range((2 if block else 1) * nrun + 1):
         vb, vo = _treg_values(rng, n + m)
         pre, lr = eng.pack_values(TREG, (vb, vo))
         # fresh writes: batch j's timestamps sit 2^18 above batch j-1's in a
@@ -435,15 +440,26 @@ def bench_treg(args, eng, dev, dist, rank, world):
         o, s, ts, pre, lr, nbytes = b
         if routed:
             tr.step([b])
+        elif use_block[0]:
+            eng.treg_converge_block(0, ts, pre, lr)
         else:
             eng.treg_converge(s, ts, pre, lr)
 
+    use_block = [block]
     step_of(batches[0], 0)
     # winners per step from timestamps (ties need the value compare: rare)
     cur = batches[0][2].clone() if not routed else None
-    nb = len(batches) - 1
+    nb = nrun
     elapsed, kt = _timed(args.steps, args.warmup, lambda i: step_of(batches[1 + i % nb], 1 + i % nb), dist, dev,
                          eng=None if routed else eng)
+    applied_idx = [0] + [1 + i % nb for i in range(args.warmup + args.steps)]
+    keyed = None
+    if block:  # the keyed form over the next batches (fresh timestamps: the same winner fractions)
+        use_block[0] = False
+        el2, kt2 = _timed(args.steps, args.warmup, lambda i: step_of(batches[1 + nb + i % nb], 1 + nb + i % nb),
+                          dist, dev, eng=eng)
+        applied_idx += [1 + nb + i % nb for i in range(args.warmup + args.steps)]
+        keyed = (el2, float(np.mean(kt2)))
     if cur is not None:
         for i in range(args.warmup + args.steps):
             t = batches[1 + i % nb][2]
@@ -460,7 +476,7 @@ def bench_treg(args, eng, dev, dist, rank, world):
     if routed:
         tr.drain()
     idx = np.random.default_rng(6 + rank).integers(0, n, 128)
-    applied = [batches[0]] + [batches[1 + i % nb] for i in range(args.warmup + args.steps)]
+    applied = [batches[j] for j in applied_idx]
     best = {}
     for b in applied:
         ts_h = b[2][idx].cpu().numpy().view(np.uint64)
@@ -482,7 +498,7 @@ def bench_treg(args, eng, dev, dist, rank, world):
     # actually moves in this layout is reported beside it
     bytes_per_key = 48
     whole = n * 24 > (256 << 20)  # k_treg_lww<true>: state over the Infinity Cache
-    moved = 4 + 24 + 8 + 8 + (16 if whole else 16 * wf) + (16 * (1 - wf) if whole else 0)
+    moved = (0 if block else 4) + 24 + 8 + 8 + (16 if whole else 16 * wf) + (16 * (1 - wf) if whole else 0)
     out = {"workload": f"TREG LWW converge: {G} keys over {world} GPU(s) ({Kper} per GPU), one delta per key "
                        f"per step{' routed by owner (all-to-all)' if routed else ''}"
                        + (f"; every step first resolves its {n + m} key strings ({m} new to the node) on the GPU "
@@ -498,12 +514,22 @@ def bench_treg(args, eng, dev, dist, rank, world):
     if not routed:
         out["roofline"] = {"bound": "hbm", "achieved": bytes_per_key * n / k / 1e9, "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": bytes_per_key * n / k / 1e9 / HBM_PEAK_GBS,
-                           "kernel": "k_treg_lww", "kernel_ms_avg": k * 1e3, "bytes_per_unit": bytes_per_key,
+                           "kernel": "k_treg_lww<..., dense>" if block else "k_treg_lww", "kernel_ms_avg": k * 1e3,
+                           "bytes_per_unit": bytes_per_key,
                            "bytes_note": "SURVEY 8d: 16 delta + 16 state read + 16 state write per key",
                            "bytes_moved_per_unit": moved,
-                           "bytes_moved_note": "4 slot + 24 delta (ts, pre, lr) + 8 state ts read + 8 ts rewritten "
-                                               "+ 16 handle write x winner fraction (a state over the 256 MiB "
-                                               "MALL: every handle written, losers' read)"}
+                           "bytes_moved_note": ("" if block else "4 slot + ") + "24 delta (ts, pre, lr) + 8 state ts "
+                                               "read + 8 ts rewritten + 16 handle write x winner fraction (a state "
+                                               "over the 256 MiB MALL: every handle written, losers' read)"}
+        if block:
+            out["form"] = ("block: the step's batch holds one delta for every slot in slot order "
+                           "(jy_treg_converge_block, no slot stream, no claim); the keyed form "
+                           "(jy_treg_converge, slot per entry) is timed beside it on fresh batches")
+            el2, k2 = keyed
+            out["keyed"] = {"ms_per_step": el2 / args.steps * 1e3, "kernel_ms_avg": k2 * 1e3,
+                            "value": world * (n + m) * args.steps / el2,
+                            "frac": bytes_per_key * n / k2 / 1e9 / HBM_PEAK_GBS,
+                            "bytes_moved_per_unit": moved + 4}
     else:
         out["step_ms_avg_events"] = k * 1e3
     return out

@@ -193,6 +193,12 @@ int32_t jy_counter_flush(jy_engine* eng, int32_t type, uint64_t cap, uint32_t* s
 /* ---- TREG: TRegString.converge (repo_treg.pony:51-52), LWW by (ts, value) ---- */
 int32_t jy_treg_converge(jy_engine* eng, uint64_t n, const uint32_t* slot, const uint64_t* ts,
                          const uint64_t* pre, const uint64_t* lr, int32_t mem);
+/* The same join for a BLOCK batch: entry i is the delta of slot slot0 + i
+ * (a full-state delta, or a shard's batch regrouped in slot order), so no
+ * slot stream is read and no slot can repeat.  [slot0, slot0 + n) must be
+ * interned (JY_ERANGE otherwise). */
+int32_t jy_treg_converge_block(jy_engine* eng, uint32_t slot0, uint64_t n, const uint64_t* ts,
+                               const uint64_t* pre, const uint64_t* lr, int32_t mem);
 /* read (ts, pre, lr) for n slots (host out) and fetch arena bytes */
 int32_t jy_treg_read(jy_engine* eng, uint64_t n, const uint32_t* slots, uint64_t* ts_out,
                      uint64_t* pre_out, uint64_t* lr_out);

@@ -90,6 +90,7 @@ SIGNATURES = {
     "jy_counter_deltas_size": (I32, [P, I32, P]),
     "jy_counter_flush": (I32, [P, I32, U64, P, P, P, P, I32]),
     "jy_treg_converge": (I32, [P, U64, P, P, P, P, I32]),
+    "jy_treg_converge_block": (I32, [P, U32, U64, P, P, P, I32]),
     "jy_treg_read": (I32, [P, U64, P, P, P, P]),
     "jy_treg_set": (I32, [P, U64, P, P, P, P, I32]),
     "jy_treg_deltas_size": (I32, [P, P]),

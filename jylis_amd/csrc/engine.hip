@@ -984,6 +984,22 @@ int32_t jy_treg_converge(jy_engine* eng, uint64_t n, const uint32_t* slot, const
   return jy_treg_merge(eng, n, (const u32*)ds, (const u64*)dt, (const u64*)dp, (const u64*)dl);
 }
 
+// a block batch: entry i is the delta of slot slot0 + i (no slot stream)
+int32_t jy_treg_converge_block(jy_engine* eng, uint32_t slot0, uint64_t n, const uint64_t* ts, const uint64_t* pre,
+                               const uint64_t* lr, int32_t mem) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  if (n == 0) return JY_OK;
+  if ((u64)slot0 + n > eng->nkeys[JY_TREG]) return eng->fail(JY_ERANGE, "slot run was never interned");
+  if (mem == JY_HOST) JY_TRY(treg_handles_check(eng, n, lr));
+  const void *dt, *dp, *dl;
+  JY_TRY(stage_begin(eng));
+  JY_TRY(jy_stage(eng, 1, ts, n * 8, mem, &dt));
+  JY_TRY(jy_stage(eng, 2, pre, n * 8, mem, &dp));
+  JY_TRY(jy_stage(eng, 3, lr, n * 8, mem, &dl));
+  JY_TRY(stage_end(eng));
+  return jy_treg_merge_block(eng, slot0, n, (const u64*)dt, (const u64*)dp, (const u64*)dl);
+}
+
 // local SET batch (RepoTREG.set repo_treg.pony:65-68): the state merge and
 // the pending delta in one pass (k_treg.hip set_one)
 int32_t jy_treg_set(jy_engine* eng, uint64_t n, const uint32_t* slot, const uint64_t* ts, const uint64_t* pre,

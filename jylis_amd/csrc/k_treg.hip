@@ -167,10 +167,13 @@ __device__ __forceinline__ void clear_slice(const TregK& K) {
 //   94 us).  jy_treg_merge picks by state size.
 // kSet: local SETs (RepoTREG.set): the pending delta is updated with the
 //   state (set_one); the wide form is used for cache-friendly batches.
-template <bool kRewriteAll, bool kSet>
+// kDense: a block batch -- entry i is slot slot0 + i (slot == nullptr): no
+//   slot stream to read, and no slot can repeat, so no claim and no
+//   duplicate list either.
+template <bool kRewriteAll, bool kSet, bool kDense = false>
 __global__ __launch_bounds__(kThreads) void k_treg_lww(TregK K, const u32* __restrict__ slot,
                                                        const u64* __restrict__ dts, const u64* __restrict__ dpre,
-                                                       const u64* __restrict__ dlr, u64 n) {
+                                                       const u64* __restrict__ dlr, u64 n, u32 slot0 = 0) {
   // a wave's rows are kUnroll consecutive runs of 64 entries (jy_claim_rows)
   const u64 base = (u64)blockIdx.x * (kThreads * kUnroll) + (threadIdx.x >> 6) * (64 * kUnroll) + (threadIdx.x & 63);
   u32 s[kUnroll];
@@ -182,7 +185,7 @@ __global__ __launch_bounds__(kThreads) void k_treg_lww(TregK K, const u32* __res
     valid[u] = i < n;
     s[u] = 0;
     if (valid[u]) {
-      s[u] = __builtin_nontemporal_load(slot + i);
+      s[u] = kDense ? slot0 + (u32)i : __builtin_nontemporal_load(slot + i);
       t[u] = __builtin_nontemporal_load(dts + i);
       p[u] = __builtin_nontemporal_load(dpre + i);
       l[u] = __builtin_nontemporal_load(dlr + i);
@@ -193,13 +196,18 @@ __global__ __launch_bounds__(kThreads) void k_treg_lww(TregK K, const u32* __res
     for (int u = 0; u < kUnroll; u++)
       if (valid[u]) t0[u] = K.ts[s[u]];
   }
-  jy_claim_rows<kUnroll>(valid, s, K.seen, first);
-  clear_slice(K);
+  if (kDense) {
+#pragma unroll
+    for (int u = 0; u < kUnroll; u++) first[u] = true;
+  } else {
+    jy_claim_rows<kUnroll>(valid, s, K.seen, first);
+    clear_slice(K);
+  }
   u32 pushed = 0;
 #pragma unroll
   for (int u = 0; u < kUnroll; u++) {
     if (!valid[u]) continue;
-    if (!first[u]) {
+    if (!kDense && !first[u]) {
       pushed |= push_dup(K, s[u], t[u], p[u], l[u]);
       continue;
     }
@@ -216,7 +224,7 @@ __global__ __launch_bounds__(kThreads) void k_treg_lww(TregK K, const u32* __res
       K.val[s[u]] = TVal{p[u], l[u]};
     }
   }
-  dup_publish(K, pushed);
+  if (!kDense) dup_publish(K, pushed);
 }
 
 // Routed runs (receiver side of the exchange, k_route.hip): one source's run
@@ -684,6 +692,29 @@ int32_t jy_treg_merge(jy_engine* eng, u64 n, const u32* slot, const u64* ts, con
   else
     hipLaunchKernelGGL((k_treg_lww<false, false>), dim3(grid), dim3(kThreads), 0,
                        eng->stream, K, slot, ts, pre, lr, n);
+  JY_HIP(eng, hipGetLastError());
+  return JY_OK;
+}
+
+// a block batch: entry i merges into slot slot0 + i.  No claim, no duplicate
+// list: the claim bitmaps' parity is left as it is (the next keyed launch
+// still finds its bitmap clean).
+int32_t jy_treg_merge_block(jy_engine* eng, u32 slot0, u64 n, const u64* ts, const u64* pre, const u64* lr) {
+  if (n == 0) return JY_OK;
+  TregState& t = eng->treg;
+  JyTimed tm(eng);
+  const u32 grid = blocks(n, kThreads * kUnroll);
+  JY_TRY(flag_init(eng));
+  JY_TRY(overflow_check(eng));
+  TregK K = state_of(eng);
+  const bool whole =
+      t.kcap * (8 + sizeof(TVal)) > kMallBytes || (eng->cfg.flags & JY_CFG_TREG_WHOLE_LINES) != 0;
+  if (whole)
+    hipLaunchKernelGGL((k_treg_lww<true, false, true>), dim3(grid), dim3(kThreads), 0, eng->stream, K, nullptr, ts,
+                       pre, lr, n, slot0);
+  else
+    hipLaunchKernelGGL((k_treg_lww<false, false, true>), dim3(grid), dim3(kThreads), 0, eng->stream, K, nullptr, ts,
+                       pre, lr, n, slot0);
   JY_HIP(eng, hipGetLastError());
   return JY_OK;
 }

@@ -421,6 +421,14 @@ class Engine:
         mem = _same_mem(ma, mb, mc, md)
         self._check(self.lib.jy_treg_converge(self.h, len(a), pa, pb, pc, pd, mem))
 
+    def treg_converge_block(self, slot0, ts, pre, lr):
+        """a block batch (jy_treg_converge_block): entry i is slot slot0 + i"""
+        b, pb, mb = _arg(ts, np.uint64)
+        c, pc, mc = _arg(pre, np.uint64)
+        d, pd, md = _arg(lr, np.uint64)
+        mem = _same_mem(mb, mc, md)
+        self._check(self.lib.jy_treg_converge_block(self.h, int(slot0), len(b), pb, pc, pd, mem))
+
     def treg_set(self, slot, ts, pre, lr):
         """local SETs (RepoTREG.set): state LWW + pending delta"""
         a, pa, ma = _arg(slot, np.uint32)

@@ -186,3 +186,62 @@ def test_duplicate_list_overflow_fails_loudly():
         assert ei.value.code == JY_ERANGE
     finally:
         eng.close()
+
+
+def test_block_converge_parity(oracle_mod, engine):
+    """jy_treg_converge_block (entry i -> slot slot0 + i): whole-range and
+    sub-range blocks from host memory and HBM, interleaved with keyed batches
+    that repeat slots inside a launch (the claim bitmaps' parity must
+    survive the block launches in between); ties, shared 8-byte prefixes and
+    long values, against the oracle repo"""
+    import torch
+    from jylis_amd._lib import TREG
+    from jylis_amd.engine import encode_keys
+    from jylis_amd.repo import RepoTREG
+    O = oracle_mod
+    rng = np.random.default_rng(23)
+    n = 30000
+    keys = [f"b{i}" for i in range(n)]
+    want = O.Repo(O.TREG)
+    got = RepoTREG(engine)
+    got.converge_deltas(_batch(keys, [b""] * n, np.zeros(n, np.int64)))  # interns in order
+    slots = engine.lookup(TREG, [k.encode() for k in keys])
+    assert (slots == np.arange(n)).all()
+    want.converge(_batch(keys, [b""] * n, np.zeros(n, np.int64)))
+    prefixes = [bytes(rng.integers(0, 256, 8).astype(np.uint8)) for _ in range(8)]
+
+    def vals(m):
+        out = []
+        for _ in range(m):
+            L = int(rng.integers(0, 20))
+            if rng.random() < 0.3:
+                out.append((prefixes[rng.integers(8)] + bytes(rng.integers(97, 100, 12).astype(np.uint8)))[:max(L, 9)])
+            else:
+                out.append(bytes(rng.integers(0, 256, L).astype(np.uint8)))
+        return out
+
+    dev = torch.device("cuda", 0)
+    for step in range(6):
+        if step % 3 == 2:  # keyed, with repeats inside the launch
+            idx = rng.integers(0, n, n)
+            v = vals(n)
+            ts = rng.integers(0, 6, n)
+            b = _batch([keys[i] for i in idx], v, ts)
+            want.converge(b)
+            got.converge_deltas(b)
+            continue
+        lo = 0 if step % 2 == 0 else int(rng.integers(1, n // 2))
+        hi = n if step % 2 == 0 else int(rng.integers(lo + 1, n))
+        m = hi - lo
+        v = vals(m)
+        ts = rng.integers(0, 6, m).astype(np.uint64)
+        vb, vo = encode_keys(v)
+        pre, lr = engine.pack_values(TREG, (vb, vo))
+        if step in (1, 3):
+            engine.treg_converge_block(lo, *(torch.from_numpy(a.view(np.int64)).to(dev) for a in (ts, pre, lr)))
+        else:
+            engine.treg_converge_block(lo, ts, pre, lr)
+        want.converge(_batch(keys[lo:hi], v, ts))
+    assert_state_equal(O.TREG, want.state(), got.state())
+    with pytest.raises(Exception):
+        engine.treg_converge_block(n - 1, np.zeros(2, np.uint64), np.zeros(2, np.uint64), np.zeros(2, np.uint64))
