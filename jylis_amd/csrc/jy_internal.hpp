@@ -57,11 +57,30 @@ __device__ __forceinline__ int jy_value_cmp(u64 pa, u64 la, u64 pb, u64 lb, cons
 
 // include/jylis_gpu.h jy_key_owner on the device: FNV-1a 64 over the key
 // bytes, splitmix64 finaliser, mod S (the node's key sharding)
+// the first min(8, avail) bytes at p as a little-endian word, zero filled,
+// from at most two aligned 8-byte loads (never touching an aligned word that
+// holds none of the bytes asked for, so never a page the bytes do not share)
+__device__ __forceinline__ u64 jy_ld8u(const uint8_t* p, u64 avail) {
+  if (avail == 0) return 0;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const u32 sh = (u32)(a & 7);
+  const u64* w = reinterpret_cast<const u64*>(a - sh);
+  u64 v = w[0] >> (8 * sh);
+  if (sh && avail > 8 - sh) v |= w[1] << (64 - 8 * sh);
+  if (avail < 8) v &= (1ull << (8 * avail)) - 1;
+  return v;
+}
+
+// (the key's bytes read a word at a time: jy_ld8u)
 __device__ __forceinline__ u32 jy_dev_key_owner(const uint8_t* __restrict__ p, u64 len, u32 S) {
   u64 h = 0xCBF29CE484222325ull;
-  for (u64 i = 0; i < len; i++) {
-    h ^= p[i];
-    h *= 0x100000001B3ull;
+  for (u64 i = 0; i < len; i += 8) {
+    const u64 w = jy_ld8u(p + i, len - i);
+    const u64 m = len - i < 8 ? len - i : 8;
+    for (u64 b = 0; b < m; b++) {
+      h ^= (w >> (8 * b)) & 0xFFu;
+      h *= 0x100000001B3ull;
+    }
   }
   h ^= h >> 30;
   h *= 0xBF58476D1CE4E5B9ull;

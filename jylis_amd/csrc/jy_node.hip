@@ -138,6 +138,7 @@ __global__ __launch_bounds__(kT) void k_nd_place(const u32* __restrict__ owner, 
 // SegLong: a value's bytes when it is longer than 8 (else nothing), padded to
 // 8-byte granules (the receiver's arena keeps long values on granules).
 struct SegCsr {
+  static constexpr bool kGranules = false;
   const u64* offs;
   u64 obase;
   __device__ __forceinline__ void get(u64 i, u64& start, u64& len, u64& plen) const {
@@ -147,6 +148,7 @@ struct SegCsr {
   }
 };
 struct SegLong {
+  static constexpr bool kGranules = true;  // output segments are whole 8-byte granules on 8-byte offsets
   const u64* offs;
   u64 obase;
   __device__ __forceinline__ void get(u64 i, u64& start, u64& len, u64& plen) const {
@@ -219,7 +221,12 @@ __global__ __launch_bounds__(kT) void k_nd_seg_bytes(u64 n, const u32* __restric
   u64 st, len, plen;
   sg.get(perm[j], st, len, plen);
   const u64 d = newoffs[j];
-  for (u64 r = 0; r < plen; r++) out[d + r] = r < len ? in[st + r] : 0;
+  if constexpr (Seg::kGranules) {  // word stores, two aligned word loads per granule at most
+    u64* o = reinterpret_cast<u64*>(out + d);
+    for (u64 q = 0; q < plen / 8; q++) o[q] = jy_ld8u(in + st + 8 * q, len - 8 * q);
+  } else {
+    for (u64 r = 0; r < plen; r++) out[d + r] = r < len ? in[st + r] : 0;
+  }
 }
 
 // per-key word columns in owner order
@@ -242,11 +249,7 @@ __global__ __launch_bounds__(kT) void k_nd_val_head(u64 n, const u32* __restrict
   if (j >= n) return;
   const u32 i = perm[j];
   const u64 a = vo[i], l = vo[i + 1] - a;
-  const uint8_t* p = vb + (a - vbase);
-  u64 x = 0;
-#pragma unroll
-  for (int q = 0; q < 8; q++) x = (x << 8) | (u64)((u64)q < l ? p[q] : 0);
-  pre[j] = x;
+  pre[j] = __builtin_bswap64(jy_ld8u(vb + (a - vbase), l));  // big-endian: byte 0 most significant
   vlen[j] = l;
 }
 
