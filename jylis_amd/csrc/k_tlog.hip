@@ -626,53 +626,70 @@ __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __
   if (tid == 0) l_woff[nt] = wtot;
   __syncthreads();
   if (wtot == 0) return;
-  for (long long c0 = (long long)((wtot - 1) / kTile) * kTile; c0 >= 0; c0 -= kTile) {
+  // one pass per kTile items, from the last item down.  The next (lower)
+  // pass's item and record loads are issued before this pass's stores: a
+  // lower pass reads only positions below this pass's lowest item of the
+  // same key, and this pass writes at or above it (entries only move up), so
+  // the prefetch never reads what this pass writes; every pass still reads
+  // before the passes above it have stored.
+  struct CItem {
+    bool live, st;
+    u32 a, qx;
+    u64 i, j;
+    TRec x;
+  };
+  auto fetch = [&](long long c0) {
+    CItem c{};
     const u32 item = (u32)c0 + tid;
-    const bool live = item < wtot;
-    u32 a = 0;
-    bool st = false;
-    u64 i = 0, j = 0, lo = 0, hi = 0;
-    if (live) {
+    c.live = item < wtot;
+    if (c.live) {
       u32 h = nt - 1;  // last idx with woff <= item (a key with items)
+      u32 a = 0;
       while (a < h) {
         const u32 m = (a + h + 1) >> 1;
         if (l_woff[m] <= item) a = m;
         else h = m - 1;
       }
+      c.a = a;
       const u32 r = item - (u32)l_woff[a];
       const u32 nd = (u32)(l_bhi[a] - l_blo[a]);
       if (l_dfirst[a]) {
-        st = r >= nd;
-        i = l_s0[a] + (r - nd);
-        j = l_blo[a] + r;
+        c.st = r >= nd;
+        c.i = l_s0[a] + (r - nd);
+        c.j = l_blo[a] + r;
       } else {
-        st = r < l_ns[a];
-        i = l_s0[a] + r;
-        j = l_blo[a] + (r - l_ns[a]);
+        c.st = r < l_ns[a];
+        c.i = l_s0[a] + r;
+        c.j = l_blo[a] + (r - l_ns[a]);
+      }
+      if (c.st) {
+        c.x = load_rec(A.pool + l_src[a] + c.i);
+      } else {
+        c.qx = eqx[c.j];
+        c.x.ts = A.dts[c.j];
+        c.x.pre = A.dpre[c.j];
+        c.x.lr = A.dlr[c.j];
+        c.x.pad = erank[c.j];
       }
     }
-    // the item's record first: it does not depend on the rank search below,
-    // so its load is in flight with the search's
-    u32 qx = 0;
-    TRec x{};
-    if (live) {
-      if (st) {
-        x = load_rec(A.pool + l_src[a] + i);
-      } else {
-        qx = eqx[j];
-        x.ts = A.dts[j];
-        x.pre = A.dpre[j];
-        x.lr = A.dlr[j];
-        x.pad = erank[j];
-      }
-    }
-    if (live && st) {
+    return c;
+  };
+  long long c0 = (long long)((wtot - 1) / kTile) * kTile;
+  CItem cur = fetch(c0);
+  for (; c0 >= 0; c0 -= kTile) {
+    CItem nxt{};
+    if (c0 >= kTile) nxt = fetch(c0 - kTile);
+    const u32 a = cur.a;
+    u32 qx = cur.qx;
+    u64 lo = 0;
+    if (cur.live && cur.st) {
       // first delta entry with rank <= i: the ranks do not increase along
       // the (newest-first) delta segment, so the entries ranked above i are
       // a prefix.  A short segment is counted with its ranks loaded at once
       // (one round trip), a long one bisected.
+      const u64 i = cur.i;
       lo = l_blo[a];
-      hi = l_bhi[a];
+      u64 hi = l_bhi[a];
       constexpr u64 kLin = 4;
       if (hi - lo <= kLin) {
         u32 rk[kLin];
@@ -691,18 +708,19 @@ __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __
       }
       qx = lo < l_bhi[a] ? eqx[lo] : 0u;
     }
-    if (live) {
+    if (cur.live) {
       const u32 M = l_M[a];
       u64 pos;
       bool write = true;
-      if (st) {
-        pos = (i - l_drop[a]) + (lo < l_bhi[a] ? M - (qx & ~kKept) : 0u);
+      if (cur.st) {
+        pos = (cur.i - l_drop[a]) + (lo < l_bhi[a] ? M - (qx & ~kKept) : 0u);
       } else {
         write = (qx & kKept) != 0;
-        pos = (u64)((u32)x.pad - l_drop[a]) + (M - 1 - (qx & ~kKept));
+        pos = (u64)((u32)cur.x.pad - l_drop[a]) + (M - 1 - (qx & ~kKept));
       }
-      if (write) store_rec(pool + l_dst[a] + pos, x.ts, x.pre, x.lr);
+      if (write) store_rec(pool + l_dst[a] + pos, cur.x.ts, cur.x.pre, cur.x.lr);
     }
+    cur = nxt;
   }
 }
 
