@@ -25,11 +25,22 @@ typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kUnroll = 4;                          // 16-B vectors in flight per lane
-constexpr u64 kTileCells = kThreads * 2 * kUnroll;  // 2048 cells per tile
+#ifndef JY_BLK_THREADS
+#define JY_BLK_THREADS 256
+#endif
+// One 16-B vector per lane, 512-cell tiles (in-box A/B of the PNCOUNT
+// headline, round 4, ms per 2^31-cell merge: 4 vectors per lane 8.78-8.80,
+// 2 vectors 8.53-8.54, 1 vector 8.19-8.36; 128 threads x 1 or 2 vectors
+// 8.20-8.27; 512 threads x 4 vectors 9.18; 64 threads x 2 vectors 9.71):
+// more, smaller workgroups keep the 256 CUs fed to the end of each row.
+#ifndef JY_BLK_UNROLL
+#define JY_BLK_UNROLL 1
+#endif
+constexpr int kThreads = JY_BLK_THREADS;
+constexpr int kUnroll = JY_BLK_UNROLL;              // 16-B vectors in flight per lane
+constexpr u64 kTileCells = kThreads * 2 * kUnroll;  // 512 cells per tile
 
-// Dense column-block max-merge.  Grid: x = 2048-cell tile of a row, y = row
+// Dense column-block max-merge.  Grid: x = 512-cell tile of a row, y = row
 // (sign, column); one tile per workgroup (the dispatcher keeps 256 CUs fed
 // better than a grid-stride loop here: tools/mb_stream.hip).  16 B per lane
 // per access, kUnroll independent vectors in flight per lane; every stream
