@@ -56,7 +56,10 @@ constexpr int kThreads = 256;
 // keys per lane; lanes on consecutive keys for every unroll step, so all
 // delta loads and the dependent state-ts gathers of the kUnroll keys are in
 // flight together before any decision
-constexpr int kUnroll = 4;
+#ifndef JY_TREG_UNROLL
+#define JY_TREG_UNROLL 4
+#endif
+constexpr int kUnroll = JY_TREG_UNROLL;
 constexpr u64 kMallBytes = 256ull << 20;  // MI355X Infinity Cache (MALL)
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
