@@ -169,7 +169,7 @@ __global__ __launch_bounds__(kThreads) void k_tlog_prep(TlogArgs A) {
 // narrows to was probed: the last round probes all of [lo, hi), and a
 // narrowed hi is a block end probed >= x), or ~0 when it is hi
 constexpr u32 kProbe = 16;
-__device__ __forceinline__ u32 ts_lower(const TRec* __restrict__ pool, u64 base, u32 lo, u32 hi, u64 x, u64& at_ts) {
+[[maybe_unused]] __device__ __forceinline__ u32 ts_lower(const TRec* __restrict__ pool, u64 base, u32 lo, u32 hi, u64 x, u64& at_ts) {
   at_ts = ~0ull;
   while (hi > lo) {
     const u32 n = hi - lo;
@@ -256,6 +256,9 @@ constexpr int kTile = 64;
 constexpr int kFastEnt = 4;  // delta entries a key may have for the lane-per-key fast path
 #ifndef JY_TLOG_KCACHE
 #define JY_TLOG_KCACHE 1
+#endif
+#ifndef JY_TLOG_CUT_PROBE
+#define JY_TLOG_CUT_PROBE 0  // 1: the cutoff drop by 16-ary probes (round 3)
 #endif
 constexpr int kCache = JY_TLOG_KCACHE;  // passes of slow entries kept in registers for the append stores
 
@@ -352,8 +355,16 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
       u32 drop = 0;
       u64 oldest = 0;
       if (cd > m.cut && m.len > 0) {
+#if JY_TLOG_CUT_PROBE
         drop = ts_lower(A.pool, m.base, 0, m.len, cut, oldest);  // oldest first: a prefix
         if (drop == m.len) oldest = 0;
+#else
+        // the interpolated search from the hint (one window of 2-3 lines; the
+        // 16-ary probes read 16 lines a round), then the new oldest entry --
+        // inside the window, a cache hit
+        drop = ts_interp(A.pool, m.base, 0, m.len, hv, m.newest, cut);  // oldest first: a prefix
+        oldest = drop < m.len ? A.pool[m.base + drop].ts : 0;
+#endif
       } else if (m.len > 0) {
         oldest = hv;  // the hint (round 3 loaded pool[base].ts here: one dependent random line per slow key)
       }
