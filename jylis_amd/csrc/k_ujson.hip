@@ -67,7 +67,10 @@
 
 namespace {
 
-constexpr int kThreads = 256;
+#ifndef JY_UJ_THREADS
+#define JY_UJ_THREADS 256
+#endif
+constexpr int kThreads = JY_UJ_THREADS;
 constexpr int kPer = 4;                         // items per thread in item tiles
 constexpr u64 kTile1 = (u64)kThreads * kPer;    // U1 item tiles: 1024 items
 constexpr u64 kTile = kThreads;                 // U2 / U3 / U5 item tiles: one item per thread
