@@ -67,6 +67,8 @@
 
 namespace {
 
+// (in-box A/B, round 4, ms per config-5 converge: 128 threads 0.528, 256
+// 0.494, 512 0.525 -- tiles, doc tiles and U1 item tiles all follow it)
 #ifndef JY_UJ_THREADS
 #define JY_UJ_THREADS 256
 #endif
