@@ -264,8 +264,12 @@ __device__ __forceinline__ bool routed_get(const RoutedIn& R, u64 cnt, u64 i, u3
 // records per lane, each record loaded together with its run's count, every
 // record rewriting its ts word -- 0.352 vs 0.341 ms together; separately, the
 // ts rewrite 0.332 and four records per lane 0.333 vs 0.330 ms.)
+#ifndef JY_TREG_ROUTED_U
+#define JY_TREG_ROUTED_U 2
+#endif
+constexpr int kRoutedU = JY_TREG_ROUTED_U;  // records per lane
 __global__ __launch_bounds__(kThreads) void k_treg_lww_routed(TregK K, RoutedIn R) {
-  constexpr int U = 2;
+  constexpr int U = kRoutedU;
   const u64 base = (u64)blockIdx.x * (kThreads * U) + (threadIdx.x >> 6) * (64 * U) + (threadIdx.x & 63);
   const u64 cnt = R.hdr[0] < R.cap ? R.hdr[0] : R.cap;
   u32 s[U];
@@ -728,7 +732,7 @@ int32_t jy_treg_merge_routed(jy_engine* eng, u32 S, u64 cap, u64 cap_byte, const
   JyTimed tm(eng);
   // one source's run per launch: a key that several peers flushed in the same
   // step is merged launch after launch (stream order), never a duplicate
-  const u32 grid = blocks(cap, kThreads * 2);
+  const u32 grid = blocks(cap, kThreads * kRoutedU);
   for (u32 src = 0; src < S; src++) {
     TregK K{};
     JY_TRY(claim_begin(eng, cap, grid, K));
