@@ -252,6 +252,35 @@ def tlog_tables(K, seed, rounds=1, mean_state=8, cap=64, mean_delta=2, key_prefi
     return state, deltas
 
 
+def treg_tables(K, seed, rounds=1, window=1 << 9, key_prefix=b"g"):
+    """Config-3-shaped TREG stream for the full-size pin: K
+    registers, then `rounds` delta batches holding one (ts, value) for every
+    key in key order.  Round j's timestamps are j * window / 2 + [0, window),
+    so about half the keys take each batch and ~K / window keys tie on the
+    timestamp; values are 0-16 bytes, 30 % sharing one of 16 8-byte prefixes
+    (ties then need the bytes past the prefix).  Returns (state, [deltas])."""
+    rng = np.random.default_rng(seed)
+    kb, ko = counter_keys(K, prefix=key_prefix)
+    prefixes = rng.integers(0, 256, (16, 8), dtype=np.uint8)
+
+    def values():
+        vb, vo = random_values(rng, K, 0, 16)
+        lens = np.diff(vo.astype(np.int64))
+        share = (rng.random(K) < 0.3) & (lens >= 9)
+        pick = rng.integers(0, 16, K)
+        starts = vo[:-1].astype(np.int64)
+        for j in range(8):
+            vb[starts[share] + j] = prefixes[pick[share], j]
+        return vb, vo
+
+    out = []
+    for j in range(rounds + 1):
+        vb, vo = values()
+        ts = (rng.integers(0, window, K) + j * (window // 2)).astype(np.uint64)
+        out.append({"key_bytes": kb, "key_offs": ko, "ts": ts, "val_bytes": vb, "val_offs": vo})
+    return out[0], out[1:]
+
+
 def ujson_tables(D, seed, rounds=1, R=16, leaves=8, zipf=1.1, ops_per_round=None, key_prefix=b"u", id_seed=None):
     """Config-5 stream: D docs with ~`leaves` elements over R
     replicas, then `rounds` delta batches whose ops (70% INS, 20% RM, 10% CLR)

@@ -927,7 +927,9 @@ inline u64 dbytes(const uint8_t* p, u64 n) {
   }
   return dcomb(h, n);
 }
-enum : u64 { kTagLog = 0x7100, kTagEnt = 0x7200, kTagDoc = 0x7300, kTagEl = 0x7400, kTagVV = 0x7500, kTagCl = 0x7600 };
+enum : u64 { kTagLog = 0x7100, kTagEnt = 0x7200, kTagDoc = 0x7300, kTagEl = 0x7400, kTagVV = 0x7500, kTagCl = 0x7600,
+             kTagReg = 0x7700 };
+inline u64 d_reg(u64 kh, u64 ts, u64 vh) { return dcomb(kh, dcomb(kTagReg, dcomb(ts, vh))); }
 inline u64 d_log(u64 kh, u64 cutoff) { return dcomb(kh, dcomb(kTagLog, cutoff)); }
 inline u64 d_ent(u64 kh, u64 rank, u64 ts, u64 vh) { return dcomb(kh, dcomb(kTagEnt ^ (rank << 16), dcomb(ts, vh))); }
 inline u64 d_doc(u64 kh) { return dcomb(kh, kTagDoc); }
@@ -942,7 +944,14 @@ extern "C" {
 int32_t or_digest_repo(void* rp, u64* out4) {
   const Repo& r = *static_cast<Repo*>(rp);
   u64 d = 0, nk = 0, ni = 0, nb = 0;
-  if (r.type == T_TLOG) {
+  if (r.type == T_TREG) {  // one (ts, value) register per key
+    for (const auto& kv : r.tr) {
+      d += d_reg(dstr(kv.first), kv.second.ts, dstr(kv.second.value));
+      nb += kv.second.value.size();
+      nk++;
+    }
+    ni = nk;
+  } else if (r.type == T_TLOG) {
     for (const auto& kv : r.tl) {
       const u64 kh = dstr(kv.first);
       d += d_log(kh, kv.second.cutoff);
@@ -984,7 +993,16 @@ int32_t or_digest_table(int32_t type, void* tp, u64* out4) {
   if (!ko || nko == 0) return -1;
   const u64 n = nko - 1;
   u64 d = 0, ni = 0, nb = 0;
-  if (type == T_TLOG) {
+  if (type == T_TREG) {
+    size_t a, e, f;
+    const u64* ts = arr<u64>(t, "ts", &a);
+    const uint8_t* vb = arr<uint8_t>(t, "val_bytes", &e);
+    const u64* vo = arr<u64>(t, "val_offs", &f);
+    for (u64 i = 0; i < n; i++)
+      d += d_reg(dbytes(kb + ko[i], ko[i + 1] - ko[i]), ts[i], dbytes(vb + vo[i], vo[i + 1] - vo[i]));
+    ni = n;
+    nb = vo[n];
+  } else if (type == T_TLOG) {
     size_t a, b, c, e, f;
     const u64* cut = arr<u64>(t, "cutoff", &a);
     const u64* eo = arr<u64>(t, "ent_offs", &b);
@@ -1020,6 +1038,32 @@ int32_t or_digest_table(int32_t type, void* tp, u64* out4) {
   out4[0] = d;
   out4[1] = n;
   out4[2] = ni;
+  out4[3] = nb;
+  return 0;
+}
+
+// the engine's TREG read-back: per key (ts, pre, lr) value handles (pre =
+// first 8 bytes big-endian; lr = arena offset << 24 | length)
+int32_t or_digest_treg_handles(u64 n, const uint8_t* kb, const u64* ko, const u64* ts, const u64* pre, const u64* lr,
+                               const uint8_t* arena, u64 alen, u64* out4) {
+  u64 d = 0, nb = 0;
+  for (u64 i = 0; i < n; i++) {
+    const u64 len = lr[i] & ((1ull << 24) - 1), off = lr[i] >> 24;
+    u64 vh;
+    if (len <= 8) {
+      uint8_t b[8];
+      for (int q = 0; q < 8; q++) b[q] = (uint8_t)(pre[i] >> (56 - 8 * q));
+      vh = dbytes(b, len);
+    } else {
+      if (off + len > alen) return -2;
+      vh = dbytes(arena + off, len);
+    }
+    d += d_reg(dbytes(kb + ko[i], ko[i + 1] - ko[i]), ts[i], vh);
+    nb += len;
+  }
+  out4[0] = d;
+  out4[1] = n;
+  out4[2] = n;
   out4[3] = nb;
   return 0;
 }

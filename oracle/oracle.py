@@ -65,6 +65,7 @@ def load():
         "or_digest_repo": (I32, [P, P]),
         "or_digest_table": (I32, [I32, P, P]),
         "or_digest_tlog_handles": (I32, [U64, P, P, P, P, P, P, P, P, U64, P]),
+        "or_digest_treg_handles": (I32, [U64, P, P, P, P, P, P, U64, P]),
         "or_digest_ujson_packed": (I32, [U64, P, P, P, P, P, P, U64, P, P, P, U64, P]),
     }
     for name, (res, args) in sig.items():
@@ -276,6 +277,16 @@ def digest_tlog_handles(kb, ko, cut, eo, ts, pre, lr, arena):
     out = np.zeros(4, np.uint64)
     n = len(keep[1][0]) - 1
     rc = load().or_digest_tlog_handles(n, *(p for _, p in keep[:7]), keep[7][1], len(keep[7][0]), out.ctypes.data)
+    return _digest_out(rc, out)
+
+
+def digest_treg_handles(kb, ko, ts, pre, lr, arena):
+    """the engine's TREG read-back (per key ts + value handle, the arena bytes)"""
+    keep = [_c(kb, np.uint8), _c(ko, np.uint64), _c(ts, np.uint64), _c(pre, np.uint64), _c(lr, np.uint64),
+            _c(arena, np.uint8)]
+    out = np.zeros(4, np.uint64)
+    n = len(keep[1][0]) - 1
+    rc = load().or_digest_treg_handles(n, *(p for _, p in keep[:5]), keep[5][1], len(keep[5][0]), out.ctypes.data)
     return _digest_out(rc, out)
 
 

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Full-size golden digests for SURVEY 8d configs 4 and 5 (run in the build
+"""Full-size golden digests for SURVEY 8d configs 3, 4 and 5 (run in the build
 container; the GPU box only reads the JSON this writes).
 
 The exact seeded sequences the bench converges (bench_modes.bench_tlog /
@@ -12,7 +12,10 @@ of every input batch so the GPU test can tell a changed generator from a
 wrong merge.  tests/test_fullsize_gpu.py runs the same sequences through the
 HIP path and compares.
 
-  python tests/golden/make_fullsize_digests.py [--only tlog|ujson]
+  python tests/golden/make_fullsize_digests.py [--only treg|tlog|ujson]
+
+(TREG, config 3: synth.treg_tables -- one delta per register per round over
+8.39M registers, dense timestamp ties with shared 8-byte value prefixes.)
 """
 import argparse
 import json
@@ -31,6 +34,7 @@ OUT = os.path.join(ROOT, "tests", "golden", "fullsize_digests.json")
 
 # the bench's sequences (gpu_round.sh: --warmup 2 / 6, --steps 8)
 CONFIGS = {
+    "treg": {"ctype": O.TREG, "keys": 8 << 20, "seed": S.BASE_SEED + 3, "rounds": 6},
     "tlog": {"ctype": O.TLOG, "keys": 4 << 20, "seed": S.BASE_SEED + 4, "rounds": 10},
     "ujson": {"ctype": O.UJSON, "keys": 1 << 20, "seed": S.BASE_SEED + 5, "rounds": 14, "R": 16},
 }
@@ -38,6 +42,8 @@ CONFIGS = {
 
 def sequence(name):
     c = CONFIGS[name]
+    if name == "treg":
+        return S.treg_tables(c["keys"], seed=c["seed"], rounds=c["rounds"])
     if name == "tlog":
         return S.tlog_tables(c["keys"], seed=c["seed"], rounds=c["rounds"])
     return S.ujson_tables(c["keys"], seed=c["seed"], rounds=c["rounds"], R=c["R"])

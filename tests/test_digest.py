@@ -109,3 +109,24 @@ def test_digest_sees_every_field(oracle_mod):
         u = {k: np.array(v, copy=True) for k, v in t.items()}
         u[mut][0] ^= 2
         assert O.digest_table(O.UJSON, u)[0] != base, mut
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_treg_digests_agree(oracle_mod, seed):
+    """TREG (the config-3 pin): repo, table and read-back forms agree, and a
+    changed timestamp or value byte changes the digest"""
+    O = oracle_mod
+    r = O.Repo(O.TREG)
+    for b in random_history(O, O.TREG, seed, nops=200, val_len=20):
+        r.converge(b)
+    t = r.state()
+    d = O.digest_repo(r)
+    assert d == O.digest_table(O.TREG, t)
+    pre, lr, arena = _handles(t)
+    assert d == O.digest_treg_handles(t["key_bytes"], t["key_offs"], t["ts"], pre, lr, arena)
+    assert d[1] == len(t["key_offs"]) - 1
+    j = int(np.argmax(np.diff(np.asarray(t["val_offs"], np.int64))))
+    for mut, idx in (("ts", j), ("val_bytes", int(t["val_offs"][j]))):
+        u = {k: np.array(v, copy=True) for k, v in t.items()}
+        u[mut][idx] ^= 1
+        assert O.digest_table(O.TREG, u)[0] != d[0], mut

@@ -1,4 +1,5 @@
-"""Configs 4 and 5 at FULL size against the oracle: the exact seeded
+"""Configs 3, 4 and 5 at FULL size against the oracle (config 3: TREG over
+8.39M registers, below); configs 4 and 5: the exact seeded
 sequences the bench converges (4M TLOG logs x 10 delta rounds; 1M UJSON
 documents, Zipf(1.1), x 14 delta rounds) through the HIP path, the canonical
 state digest after every converge compared with the oracle's
@@ -151,3 +152,60 @@ def test_ujson_config5_fullsize(oracle_mod):
                 assert got == states[-1], "UJSON state after the pipelined sequence differs from the oracle's"
         finally:
             eng.close()
+
+
+@pytest.mark.timeout(900)
+def test_treg_config3_fullsize(oracle_mod):
+    """Config 3 at full size: 8.39M registers, one delta per register per
+    round (synth.treg_tables: dense timestamp ties, shared 8-byte prefixes),
+    the rounds alternating between the block form (jy_treg_converge_block)
+    and the keyed form with the slots in HBM; the digest after every
+    converge against the oracle's, then the whole sequence pipelined"""
+    import torch
+    from jylis_amd import synth as S
+    from jylis_amd._lib import TREG
+    from jylis_amd.engine import Engine
+    O = oracle_mod
+    g, inputs, states = _golden("treg")
+    K = g["keys"]
+    st, dl = S.treg_tables(K, seed=g["seed"], rounds=g["rounds"])
+    batches = [st] + dl
+    _progress(f"treg: generated {len(batches)} batches")
+    for i, b in enumerate(batches):
+        assert O.digest_table(TREG, b) == inputs[i], f"generator drift at batch {i}"
+    dev = torch.device("cuda", 0)
+    for pipelined in (False, True):
+        eng = Engine(device=0, key_capacity=[1024, 1024, K, 1024, 1024])
+        try:
+            slots = eng.intern(TREG, (st["key_bytes"], st["key_offs"]))
+            assert (slots == np.arange(K)).all()
+            dslots = _dev(slots, dev)
+            devb = []
+            for b in batches:
+                pre, lr = eng.pack_values(TREG, (b["val_bytes"], b["val_offs"]))
+                devb.append(tuple(_dev(a, dev) for a in (b["ts"], pre, lr)))
+            for i, (ts, pre, lr) in enumerate(devb):
+                if i % 2 == 0:
+                    eng.treg_converge_block(0, ts, pre, lr)
+                else:
+                    eng.treg_converge(dslots, ts, pre, lr)
+                if not pipelined:
+                    got = _treg_digest(O, eng, st["key_bytes"], st["key_offs"])
+                    _progress(f"treg converge {i}: {got}")
+                    assert got == states[i], f"TREG state after converge {i} differs from the oracle's"
+            if pipelined:
+                eng.sync()
+                got = _treg_digest(O, eng, st["key_bytes"], st["key_offs"])
+                _progress(f"treg pipelined: {got}")
+                assert got == states[-1], "TREG state after the pipelined sequence differs from the oracle's"
+        finally:
+            eng.close()
+
+
+def _treg_digest(O, eng, kb, ko):
+    from jylis_amd._lib import TREG
+    K = len(ko) - 1
+    ts, pre, lr = eng.treg_read(np.arange(K, dtype=np.uint32))
+    n, _ = eng.arena_usage(TREG)
+    arena = np.frombuffer(eng.arena_read(TREG, 0, n), np.uint8) if n else np.zeros(0, np.uint8)
+    return O.digest_treg_handles(kb, ko, ts, pre, lr, arena)
