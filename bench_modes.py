@@ -532,6 +532,11 @@ def bench_treg(args, eng, dev, dist, rank, world):
                             "bytes_moved_per_unit": moved + 4}
     else:
         out["step_ms_avg_events"] = k * 1e3
+        out["self_direct"] = tr.self_direct
+        if tr.self_direct:
+            out["self_direct_note"] = ("each shard merges its own entries where they lie (jy_treg_route_part_self); "
+                                       "only the other shards' entries are placed in runs and exchanged -- at "
+                                       "1 GPU the step is owner count + partition pass + the owned merge")
     return out
 
 

@@ -342,6 +342,17 @@ int32_t jy_treg_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, co
                            const uint64_t* ts, const uint64_t* pre, const uint64_t* lr, uint32_t nshards,
                            uint64_t cap, uint64_t cap_byte, int32_t mem, uint64_t* recs_dev, uint8_t* bytes_dev,
                            uint64_t* hdr_dev, uint32_t* ovf_dev);
+/* The same partition on the shard `self` (< nshards) that owns part of its
+ * own batch: the entries with owner == self are merged into eng's registers
+ * where they lie (the keyed LWW merge, enqueued before the partition) and
+ * never enter a run; run `self` stays empty (hdr row 0), its overflow list
+ * never names them.  The receivers' merge is unchanged (an empty run costs
+ * one launch that reads its count), and at nshards == 1 the caller may skip
+ * it and the run buffers altogether. */
+int32_t jy_treg_route_part_self(jy_engine* eng, uint64_t n, const uint32_t* owner, const uint32_t* slot,
+                                const uint64_t* ts, const uint64_t* pre, const uint64_t* lr, uint32_t nshards,
+                                uint32_t self, uint64_t cap, uint64_t cap_byte, int32_t mem, uint64_t* recs_dev,
+                                uint8_t* bytes_dev, uint64_t* hdr_dev, uint32_t* ovf_dev);
 int32_t jy_treg_converge_routed(jy_engine* eng, uint32_t nsrc, uint64_t cap, uint64_t cap_byte,
                                 const uint64_t* recs_dev, const uint8_t* bytes_dev, const uint64_t* hdr_dev);
 /* The same merge when the byte runs were received straight into this

@@ -117,6 +117,7 @@ SIGNATURES = {
     "jy_keys_intern_lens": (I32, [P, I32, U64, P, P, P]),
     "jy_keys_route_back": (I32, [P, U64, P, P, P]),
     "jy_treg_route_part": (I32, [P, U64, P, P, P, P, P, U32, U64, U64, I32, P, P, P, P]),
+    "jy_treg_route_part_self": (I32, [P, U64, P, P, P, P, P, U32, U32, U64, U64, I32, P, P, P, P]),
     "jy_treg_converge_routed": (I32, [P, U32, U64, U64, P, P, P]),
     "jy_arena_reserve": (I32, [P, I32, U64, P, P]),
     "jy_treg_converge_routed_at": (I32, [P, U32, U64, U64, P, P, U64]),

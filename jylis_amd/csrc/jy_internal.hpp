@@ -578,6 +578,8 @@ int32_t jy_treg_overflow_check(jy_engine* eng);
 // (device, 2 u64 per source); source src's value bytes at arena offset
 // rebase + src * cap_byte
 int32_t jy_treg_merge_block(jy_engine* eng, u32 slot0, u64 n, const u64* ts, const u64* pre, const u64* lr);
+int32_t jy_treg_merge_owned(jy_engine* eng, u64 n, const u32* own, u32 self, const u32* slot, const u64* ts,
+                            const u64* pre, const u64* lr);
 int32_t jy_treg_merge_routed(jy_engine* eng, u32 S, u64 cap, u64 cap_byte, const u64* recs, const u64* hdr,
                              u64 rebase);
 // local SETs: state LWW + pending delta, repeated keys exact

@@ -57,8 +57,10 @@ constexpr int kSlices = 4;        // 64-entry slices per count tile (one wave)
 constexpr int kT = 64 * kSlices;  // entries per tile (count and place)
 constexpr int kWG = 256;          // count: threads per workgroup = 4 tiles
 
+// `self`: entries owned by this shard are merged where they lie
+// (jy_treg_route_part_self) and neither counted nor placed; S = none
 __global__ __launch_bounds__(kWG) void k_rt_count(const u32* __restrict__ owner, const u64* __restrict__ lr, u64 n,
-                                                  u32 S, u64* __restrict__ tcnt) {
+                                                  u32 S, u32 self, u64* __restrict__ tcnt) {
   const u64 tile = (u64)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6);
   if (tile * kT >= n) return;  // a whole wave
   const u32 lane = __lane_id();
@@ -71,8 +73,12 @@ __global__ __launch_bounds__(kWG) void k_rt_count(const u32* __restrict__ owner,
     b[u] = 0;
     if (i < n) {
       o[u] = owner[i];
-      const u64 len = __builtin_nontemporal_load(lr + i) & JY_LR_LEN_MASK;
-      b[u] = len > 8 ? round_up8(len) : 0;
+      if (o[u] == self) {
+        o[u] = S;
+      } else {
+        const u64 len = __builtin_nontemporal_load(lr + i) & JY_LR_LEN_MASK;
+        b[u] = len > 8 ? round_up8(len) : 0;
+      }
     }
   }
   u64 c = 0, cb = 0;  // lane d: owner d's records and bytes in this tile
@@ -115,7 +121,7 @@ __global__ void k_rt_hdr(const u64* __restrict__ tcnt, u64 ntiles, u32 W, unsign
 __global__ __launch_bounds__(256) void k_rt_place(const u32* __restrict__ owner, const u32* __restrict__ slot,
                                                  const u64* __restrict__ ts, const u64* __restrict__ pre,
                                                  const u64* __restrict__ lr, const uint8_t* __restrict__ arena, u64 n,
-                                                 u32 S, u64 cap, u64 cap_byte, const u64* __restrict__ tcnt,
+                                                 u32 S, u32 self, u64 cap, u64 cap_byte, const u64* __restrict__ tcnt,
                                                  unsigned long long* __restrict__ hdr, u64* __restrict__ recs,
                                                  uint8_t* __restrict__ bytes, u32* __restrict__ ovf,
                                                  unsigned long long* __restrict__ skipped) {
@@ -136,8 +142,8 @@ __global__ __launch_bounds__(256) void k_rt_place(const u32* __restrict__ owner,
   u32 o = 0xFFFFFFFFu, sl = 0;
   u64 t = 0, p = 0, l = 0, b = 0;
   u64 g0 = 0, g1 = 0;  // a long value's first two 8-B granules, loaded early
-  if (i < n) {
-    o = owner[i];
+  if (i < n) o = owner[i];
+  if (i < n && o != self) {  // this shard's own entries are merged where they lie
     sl = slot[i];
     t = ts[i];
     p = pre[i];
@@ -150,8 +156,8 @@ __global__ __launch_bounds__(256) void k_rt_place(const u32* __restrict__ owner,
       g1 = src[1];
     }
   }
-  const bool valid = i < n && o < S;
-  if (i < n && !valid) atomicAdd(skipped, 1ull);  // an owner outside [0, S): dropped, counted
+  const bool valid = i < n && o < S && o != self;
+  if (i < n && o >= S) atomicAdd(skipped, 1ull);  // an owner outside [0, S): dropped, counted
   u64 rk = 0, bk = 0;
   u64 pending = __ballot(valid);
   while (pending) {
@@ -211,12 +217,17 @@ void jy_keys_owner(uint64_t n, const uint8_t* kb, const uint64_t* ko, uint32_t n
   for (u64 i = 0; i < n; i++) out[i] = jy_key_owner(kb + ko[i], ko[i + 1] - ko[i], nshards);
 }
 
-int32_t jy_treg_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, const uint32_t* slot, const uint64_t* ts,
-                           const uint64_t* pre, const uint64_t* lr, uint32_t nshards, uint64_t cap, uint64_t cap_byte,
-                           int32_t mem, uint64_t* recs_dev, uint8_t* bytes_dev, uint64_t* hdr_dev,
-                           uint32_t* ovf_dev) {
+}  // extern "C"
+
+namespace {
+
+int32_t route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, const uint32_t* slot, const uint64_t* ts,
+                   const uint64_t* pre, const uint64_t* lr, uint32_t nshards, uint32_t self, uint64_t cap,
+                   uint64_t cap_byte, int32_t mem, uint64_t* recs_dev, uint8_t* bytes_dev, uint64_t* hdr_dev,
+                   uint32_t* ovf_dev) {
   JY_HIP(eng, hipSetDevice(eng->device));
   if (nshards == 0 || nshards > kMaxShards) return eng->fail(JY_ERANGE, "nshards must be in [1, 64]");
+  if (self != nshards && self >= nshards) return eng->fail(JY_ERANGE, "self must be in [0, nshards)");
   if (n == 0) {
     JY_HIP(eng, hipMemsetAsync(hdr_dev, 0, (u64)nshards * 16, eng->stream));
     return JY_OK;
@@ -242,7 +253,10 @@ int32_t jy_treg_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, co
   const u32* own = static_cast<const u32*>(dow);
   const u64* l = static_cast<const u64*>(dlr);
   const u32 nwg = (u32)((ntiles + kWG / 64 - 1) / (kWG / 64));
-  hipLaunchKernelGGL(k_rt_count, dim3(nwg), dim3(kWG), 0, eng->stream, own, l, n, nshards, tcnt);
+  if (self < nshards)  // this shard's share first: the partition below leaves it out
+    JY_TRY(jy_treg_merge_owned(eng, n, own, self, static_cast<const u32*>(dsl), static_cast<const u64*>(dts),
+                               static_cast<const u64*>(dpre), l));
+  hipLaunchKernelGGL(k_rt_count, dim3(nwg), dim3(kWG), 0, eng->stream, own, l, n, nshards, self, tcnt);
   JY_HIP(eng, hipGetLastError());
   {
     // the tile counts of every (owner, quantity) column in ONE device-wide
@@ -258,10 +272,31 @@ int32_t jy_treg_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, co
   static_assert(kT == 256, "the workgroup placement takes 256-entry tiles");
   hipLaunchKernelGGL(k_rt_place, dim3((u32)ntiles), dim3(256), 0, eng->stream, own, static_cast<const u32*>(dsl),
                      static_cast<const u64*>(dts), static_cast<const u64*>(dpre), l, eng->arena[JY_TREG].p, n, nshards,
-                     cap, cap_byte, tcnt, reinterpret_cast<unsigned long long*>(hdr_dev), recs_dev, bytes_dev, ovf_dev,
+                     self, cap, cap_byte, tcnt, reinterpret_cast<unsigned long long*>(hdr_dev), recs_dev, bytes_dev, ovf_dev,
                      reinterpret_cast<unsigned long long*>(eng->skipped_dev));
   JY_HIP(eng, hipGetLastError());
   return JY_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t jy_treg_route_part(jy_engine* eng, uint64_t n, const uint32_t* owner, const uint32_t* slot, const uint64_t* ts,
+                           const uint64_t* pre, const uint64_t* lr, uint32_t nshards, uint64_t cap, uint64_t cap_byte,
+                           int32_t mem, uint64_t* recs_dev, uint8_t* bytes_dev, uint64_t* hdr_dev,
+                           uint32_t* ovf_dev) {
+  return route_part(eng, n, owner, slot, ts, pre, lr, nshards, nshards, cap, cap_byte, mem, recs_dev, bytes_dev,
+                    hdr_dev, ovf_dev);
+}
+
+int32_t jy_treg_route_part_self(jy_engine* eng, uint64_t n, const uint32_t* owner, const uint32_t* slot,
+                                const uint64_t* ts, const uint64_t* pre, const uint64_t* lr, uint32_t nshards,
+                                uint32_t self, uint64_t cap, uint64_t cap_byte, int32_t mem, uint64_t* recs_dev,
+                                uint8_t* bytes_dev, uint64_t* hdr_dev, uint32_t* ovf_dev) {
+  if (self >= nshards) return eng->fail(JY_ERANGE, "self must be in [0, nshards)");
+  return route_part(eng, n, owner, slot, ts, pre, lr, nshards, self, cap, cap_byte, mem, recs_dev, bytes_dev, hdr_dev,
+                    ovf_dev);
 }
 
 int32_t jy_treg_converge_routed(jy_engine* eng, uint32_t nsrc, uint64_t cap, uint64_t cap_byte,

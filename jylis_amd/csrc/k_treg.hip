@@ -173,10 +173,23 @@ __device__ __forceinline__ void clear_slice(const TregK& K) {
 // kDense: a block batch -- entry i is slot slot0 + i (slot == nullptr): no
 //   slot stream to read, and no slot can repeat, so no claim and no
 //   duplicate list either.
-template <bool kRewriteAll, bool kSet, bool kDense = false>
+// kOwned: a routed sender's batch merged where it lies (jy_treg_route_part_self):
+//   only entries whose owner is this shard (own[i] == self) take part, and a
+//   slot this shard never handed out is counted as skipped, as a receiver
+//   does for routed records.  The owner words are loaded with the rest of
+//   the entry (at S shards 1/S of the entries are this shard's, spread over
+//   every line: the lines are fetched either way).
+struct Owned {
+  const u32* own;
+  u32 self;
+  u64 nslots;
+  unsigned long long* skipped;
+};
+template <bool kRewriteAll, bool kSet, bool kDense = false, bool kOwned = false>
 __global__ __launch_bounds__(kThreads) void k_treg_lww(TregK K, const u32* __restrict__ slot,
                                                        const u64* __restrict__ dts, const u64* __restrict__ dpre,
-                                                       const u64* __restrict__ dlr, u64 n, u32 slot0 = 0) {
+                                                       const u64* __restrict__ dlr, u64 n, u32 slot0 = 0,
+                                                       Owned O = Owned{}) {
   // a wave's rows are kUnroll consecutive runs of 64 entries (jy_claim_rows)
   const u64 base = (u64)blockIdx.x * (kThreads * kUnroll) + (threadIdx.x >> 6) * (64 * kUnroll) + (threadIdx.x & 63);
   u32 s[kUnroll];
@@ -192,7 +205,17 @@ __global__ __launch_bounds__(kThreads) void k_treg_lww(TregK K, const u32* __res
       t[u] = __builtin_nontemporal_load(dts + i);
       p[u] = __builtin_nontemporal_load(dpre + i);
       l[u] = __builtin_nontemporal_load(dlr + i);
+      if (kOwned) valid[u] = __builtin_nontemporal_load(O.own + i) == O.self;
     }
+  }
+  if (kOwned) {
+#pragma unroll
+    for (int u = 0; u < kUnroll; u++)
+      if (valid[u] && s[u] >= O.nslots) {
+        atomicAdd(O.skipped, 1ull);
+        valid[u] = false;
+        s[u] = 0;
+      }
   }
   if (!kSet) {
 #pragma unroll
@@ -699,6 +722,29 @@ int32_t jy_treg_merge(jy_engine* eng, u64 n, const u32* slot, const u64* ts, con
   else
     hipLaunchKernelGGL((k_treg_lww<false, false>), dim3(grid), dim3(kThreads), 0,
                        eng->stream, K, slot, ts, pre, lr, n);
+  JY_HIP(eng, hipGetLastError());
+  return JY_OK;
+}
+
+// the entries of a routed sender's batch that this shard owns (own[i] ==
+// self), merged in place: a shard's share of its own batch never enters a run
+int32_t jy_treg_merge_owned(jy_engine* eng, u64 n, const u32* own, u32 self, const u32* slot, const u64* ts,
+                            const u64* pre, const u64* lr) {
+  if (n == 0) return JY_OK;
+  TregState& t = eng->treg;
+  JyTimed tm(eng);
+  const u32 grid = blocks(n, kThreads * kUnroll);
+  TregK K{};
+  JY_TRY(claim_begin(eng, n, grid, K));
+  const Owned O{own, self, eng->nkeys[JY_TREG], reinterpret_cast<unsigned long long*>(eng->skipped_dev)};
+  const bool whole =
+      t.kcap * (8 + sizeof(TVal)) > kMallBytes || (eng->cfg.flags & JY_CFG_TREG_WHOLE_LINES) != 0;
+  if (whole)
+    hipLaunchKernelGGL((k_treg_lww<true, false, false, true>), dim3(grid), dim3(kThreads), 0, eng->stream, K, slot,
+                       ts, pre, lr, n, 0u, O);
+  else
+    hipLaunchKernelGGL((k_treg_lww<false, false, false, true>), dim3(grid), dim3(kThreads), 0, eng->stream, K, slot,
+                       ts, pre, lr, n, 0u, O);
   JY_HIP(eng, hipGetLastError());
   return JY_OK;
 }

@@ -455,8 +455,19 @@ class TregRouter(_RunRouter):
     `step(batches)`: batches[i] = (owner, slot, ts, pre, lr, long_bytes) for
     local rank i (CUDA tensors; owner/slot int32, the rest int64 bits;
     long_bytes = `long_bytes(lr)`, a host int).  Partition -> header +
-    records + bytes all-to-all -> one merge of every received run."""
+    records + bytes all-to-all -> one merge of every received run.
+
+    `self_direct`: a shard's own entries never enter a run; the partition
+    merges them where they lie (jy_treg_route_part_self), so run `self` stays
+    empty and one shard alone exchanges and merges nothing.  That costs one
+    more read of the whole batch (~28 B per entry: the own entries are spread
+    over every line) and saves the own share's record write + read (64 B per
+    own entry, 1/S of them), so it pays for S <= 2 only -- the default."""
     arena_type = _lib.TREG
+
+    def __init__(self, engines, fabric, self_direct=None):
+        self.self_direct = fabric.world <= 2 if self_direct is None else bool(self_direct)
+        super().__init__(engines, fabric)
 
     def _sizes(self, b):
         return (int(b[0].numel()), int(b[5]))
@@ -492,8 +503,13 @@ class TregRouter(_RunRouter):
         n = int(own.numel())
         assert (a, e) == (0, n), "TREG rounds are not chunked"
         dev = torch.device("cuda", eng.device)
-        recs = torch.empty((S * cap, 4), dtype=torch.int64, device=dev)
-        if S == 1:  # its own receiver: the run's bytes go to the arena directly
+        alone = S == 1 and self.self_direct
+        # one shard merging its own entries where they lie: the runs stay
+        # empty -- token buffers instead of S * cap records
+        recs = torch.empty((1 if alone else S * cap, 4), dtype=torch.int64, device=dev)
+        if alone:
+            byts = torch.empty(8, dtype=torch.uint8, device=dev)
+        elif S == 1:  # its own receiver: the run's bytes go to the arena directly
             byts, _ = self._arena_bytes(eng, capb)
         else:
             byts = torch.empty(S * capb, dtype=torch.uint8, device=dev)
@@ -501,14 +517,21 @@ class TregRouter(_RunRouter):
         if n:
             for t in (own, slot, ts, pre, lr):
                 assert t.is_cuda and t.is_contiguous() and t.numel() == n
-            eng._check(eng.lib.jy_treg_route_part(
-                eng.h, n, own.data_ptr(), slot.data_ptr(), ts.data_ptr(), pre.data_ptr(), lr.data_ptr(), S, cap,
-                capb, _lib.DEVICE, self._ptr(recs), self._ptr(byts), self._ptr(hdr), self._ptr(ovf)))
+            ptrs = (eng.h, n, own.data_ptr(), slot.data_ptr(), ts.data_ptr(), pre.data_ptr(), lr.data_ptr(), S)
+            outs = (_lib.DEVICE, self._ptr(recs), self._ptr(byts), self._ptr(hdr), self._ptr(ovf))
+            if self.self_direct:
+                me = self.fabric.ranks[self.engs.index(eng)]
+                eng._check(eng.lib.jy_treg_route_part_self(*ptrs, me, 1 if alone else cap, 8 if alone else capb,
+                                                           *outs))
+            else:
+                eng._check(eng.lib.jy_treg_route_part(*ptrs, cap, capb, *outs))
         else:
             hdr.zero_()
         return (hdr, recs, byts)
 
     def _merge(self, eng, rcv, caps):
+        if self.S == 1 and self.self_direct:
+            return  # the partition merged every entry where it lay: no run holds a record
         hdr, recs, byts = rcv
         eng._check(eng.lib.jy_treg_converge_routed_at(eng.h, self.S, caps[0], caps[1], self._ptr(recs),
                                                       self._ptr(hdr), self._rebase.pop(id(eng))))

@@ -5,7 +5,7 @@ set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out; export TMPDIR=/tmp
 TAG=${TAG:-r04}
-timeout -k 10 600 python -u -m pytest tests/test_route_gpu.py tests/test_parity_treg.py -x -q --timeout 240 \
+timeout -k 10 600 python -u -m pytest tests/test_route_gpu.py tests/test_route_dist_gpu.py tests/test_parity_treg.py -x -q --timeout 240 \
   --timeout-method thread > gpurun_out/pytest_route_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_route_$TAG.log; exit 1; }
 tail -1 gpurun_out/pytest_route_$TAG.log
 for v in "" "--route"; do

@@ -94,16 +94,19 @@ def _oracle_dict(O, batches):
             for i, (k, t) in enumerate(zip(O.split_keys(st), st["ts"]))}
 
 
+@pytest.mark.parametrize("direct", [None, True, False])
 @pytest.mark.parametrize("fab", sorted(FABRIC))
 @pytest.mark.parametrize("S", [1, 2, 3])
-def test_treg_routed_local_fabric(oracle_mod, S, fab):
+def test_treg_routed_local_fabric(oracle_mod, S, fab, direct):
     """every rank ingests its own batch over a shared key space; keys that
-    several ranks ingest in the same step meet in one merge launch"""
+    several ranks ingest in the same step meet in one merge launch.  `direct`:
+    each shard merges its own entries where they lie (jy_treg_route_part_self)
+    or routes them through its own run; None = the router's default (S <= 2)"""
     from jylis_amd.route import LocalFabric, TregRouter
     rng = np.random.default_rng(40 + S)
     node = _Node(S)
     try:
-        router = TregRouter(node.engs, LocalFabric(S, **FABRIC[fab]))
+        router = TregRouter(node.engs, LocalFabric(S, **FABRIC[fab]), self_direct=direct)
         seen = []
         for _ in range(4):
             bs = [_treg_batch(rng, 2500, 4000) for _ in range(S)]
