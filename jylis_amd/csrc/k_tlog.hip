@@ -198,7 +198,14 @@ constexpr u32 kProbe = 16;
 // time, so an interpolated guess and one window of kWin entries around it
 // (loaded at once: one round trip, ~2 cache lines) usually settle it; else
 // a binary search of the side the window ruled out
-constexpr u32 kWin = 8;
+// window entries (in-box A/B, round 4, ms per config-4 converge: 8 -> 0.837-
+// 0.840, 4 -> 0.828-0.830, 3 -> 0.830, 2 -> 0.826-0.827; 12 was slower still
+// than 8 on another box): the interpolated guess is close enough that fewer
+// lines per probe win
+#ifndef JY_TLOG_WIN
+#define JY_TLOG_WIN 2
+#endif
+constexpr u32 kWin = JY_TLOG_WIN;
 __device__ __forceinline__ u32 ts_interp(const TRec* __restrict__ pool, u64 base, u32 lo, u32 hi, u64 tlo, u64 thi,
                                          u64 x) {
   if (hi - lo > kWin && x > tlo && x <= thi && thi > tlo) {
@@ -366,7 +373,7 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
         drop = ts_lower(A.pool, m.base, 0, m.len, cut, oldest);  // oldest first: a prefix
         if (drop == m.len) oldest = 0;
 #else
-        // the interpolated search from the hint (one window of 2-3 lines; the
+        // the interpolated search from the hint (one window of 1-2 lines; the
         // 16-ary probes read 16 lines a round), then the new oldest entry --
         // inside the window, a cache hit
         drop = ts_interp(A.pool, m.base, 0, m.len, hv, m.newest, cut);  // oldest first: a prefix
