@@ -71,11 +71,14 @@ __device__ __forceinline__ u64 jy_ld8u(const uint8_t* p, u64 avail) {
   return v;
 }
 
-// (the key's bytes read a word at a time: jy_ld8u)
+// (the key's bytes read a word at a time: jy_ld8u; the first two words are
+// loaded together, before any byte is hashed -- one round trip for keys of
+// up to 16 bytes)
 __device__ __forceinline__ u32 jy_dev_key_owner(const uint8_t* __restrict__ p, u64 len, u32 S) {
   u64 h = 0xCBF29CE484222325ull;
+  const u64 w0 = jy_ld8u(p, len), w1 = len > 8 ? jy_ld8u(p + 8, len - 8) : 0ull;
   for (u64 i = 0; i < len; i += 8) {
-    const u64 w = jy_ld8u(p + i, len - i);
+    const u64 w = i == 0 ? w0 : i == 8 ? w1 : jy_ld8u(p + i, len - i);
     const u64 m = len - i < 8 ? len - i : 8;
     for (u64 b = 0; b < m; b++) {
       h ^= (w >> (8 * b)) & 0xFFu;

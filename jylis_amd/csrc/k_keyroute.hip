@@ -139,7 +139,7 @@ __global__ __launch_bounds__(kT) void k_kr_place(const uint8_t* __restrict__ kb,
   }
   pos_out[i] = (u32)p;
   lens[p] = len;
-  for (u64 q = 0; q < len; q++) bytes[b + q] = kb[a + q];
+  for (u64 q = 0; q < len; q++) bytes[b + q] = kb[a + q];  // (word reads + byte stores measured slower: 111 -> 153 us)
 }
 
 __global__ __launch_bounds__(kT) void k_kr_back(u64 n, const u32* __restrict__ pos, const u32* __restrict__ answers,

@@ -52,13 +52,28 @@ __device__ __forceinline__ u64 gid() { return (u64)blockIdx.x * kThreads + threa
 
 // jy_key_owner's hash (FNV-1a 64 + splitmix64 finaliser), remixed so the
 // table position is independent of the owner shard (owner = h mod S would
-// otherwise pin the low bits of every key of a shard)
-__device__ __forceinline__ u64 table_hash(const uint8_t* __restrict__ p, u64 len) {
-  u64 h = 0xCBF29CE484222325ull;
-  for (u64 i = 0; i < len; i++) {
-    h ^= p[i];
+// otherwise pin the low bits of every key of a shard).  The bytes come a
+// word at a time (jy_ld8u): the key's first two words are loaded together,
+// before any byte is hashed, and reused by the comparisons -- a byte loop
+// paid one dependent round trip per byte (K1 probe: 460 us for 8.9M keys)
+struct KeyW {
+  u64 w0, w1;  // bytes 0..7 and 8..15, zero filled past the key
+};
+__device__ __forceinline__ KeyW key_words(const uint8_t* __restrict__ p, u64 len) {
+  return KeyW{jy_ld8u(p, len), len > 8 ? jy_ld8u(p + 8, len - 8) : 0ull};
+}
+__device__ __forceinline__ u64 fnv_word(u64 h, u64 w, u64 m) {
+  for (u64 b = 0; b < m; b++) {
+    h ^= (w >> (8 * b)) & 0xFFu;
     h *= 0x100000001B3ull;
   }
+  return h;
+}
+__device__ __forceinline__ u64 table_hash(const uint8_t* __restrict__ p, u64 len, const KeyW& kw) {
+  u64 h = 0xCBF29CE484222325ull;
+  h = fnv_word(h, kw.w0, len < 8 ? len : 8);
+  if (len > 8) h = fnv_word(h, kw.w1, len - 8 < 8 ? len - 8 : 8);
+  for (u64 i = 16; i < len; i += 8) h = fnv_word(h, jy_ld8u(p + i, len - i), len - i < 8 ? len - i : 8);
   h ^= h >> 30;
   h *= 0xBF58476D1CE4E5B9ull;
   h ^= h >> 27;
@@ -73,9 +88,13 @@ __device__ __forceinline__ u64 table_hash(const uint8_t* __restrict__ p, u64 len
   return h;
 }
 
-__device__ __forceinline__ bool bytes_equal(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, u64 n) {
-  for (u64 i = 0; i < n; i++)
-    if (a[i] != b[i]) return false;
+// the n bytes at a equal the key k whose first words are kw (n = its length)
+__device__ __forceinline__ bool key_equal(const uint8_t* __restrict__ a, const uint8_t* __restrict__ k, u64 n,
+                                          const KeyW& kw) {
+  if (jy_ld8u(a, n) != kw.w0) return false;
+  if (n > 8 && jy_ld8u(a + 8, n - 8) != kw.w1) return false;
+  for (u64 i = 16; i < n; i += 8)
+    if (jy_ld8u(a + i, n - i) != jy_ld8u(k + i, n - i)) return false;
   return true;
 }
 
@@ -107,7 +126,8 @@ __global__ __launch_bounds__(kThreads) void k_key_probe(In I, Dir D, u32* __rest
   if (i < I.n) {
     const uint8_t* k = I.kb + I.ko[i];
     const u64 len = I.ko[i + 1] - I.ko[i];
-    const u64 t = table_hash(k, len);
+    const KeyW kw = key_words(k, len);
+    const u64 t = table_hash(k, len, kw);
     th[i] = t;
     u64 p = t >> D.shift;
     u32 slot = kMiss;
@@ -117,7 +137,7 @@ __global__ __launch_bounds__(kThreads) void k_key_probe(In I, Dir D, u32* __rest
       if ((u32)(e >> 32) == tag_of(t) && !(e & kPending)) {
         const u32 s = (u32)(e & kIdxMask);
         const u64 r = D.kref[s];
-        if ((r & JY_LR_LEN_MASK) == len && bytes_equal(D.bytes + (r >> JY_LR_LEN_BITS), k, len)) {
+        if ((r & JY_LR_LEN_MASK) == len && key_equal(D.bytes + (r >> JY_LR_LEN_BITS), k, len, kw)) {
           slot = s;
           break;
         }
@@ -147,16 +167,34 @@ __global__ __launch_bounds__(kThreads) void k_key_probe(In I, Dir D, u32* __rest
 }
 
 // one workgroup: the probe's partials into counts[3] (misses, their bytes, oversized keys)
-__global__ __launch_bounds__(kThreads) void k_key_sum(const u64* __restrict__ parts, u64 nb, u64* __restrict__ counts) {
-  __shared__ u64 red[kThreads / 64];
+// one workgroup of 1024 sums the [nb][3] partials: each thread walks whole
+// rows (the three quantities at once), 4 rows in flight per step (a
+// 256-thread form summing one quantity per sweep took 80 us at 35K rows)
+constexpr int kSumThreads = 1024;
+__global__ __launch_bounds__(kSumThreads) void k_key_sum(const u64* __restrict__ parts, u64 nb,
+                                                         u64* __restrict__ counts) {
+  __shared__ u64 red[3][kSumThreads / 64];
+  u64 v[3] = {0, 0, 0};
+  for (u64 b0 = threadIdx.x; b0 < nb; b0 += 4 * kSumThreads) {
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const u64 b = b0 + (u64)u * kSumThreads;
+      if (b < nb) {
+#pragma unroll
+        for (int q = 0; q < 3; q++) v[q] += parts[b * 3 + q];
+      }
+    }
+  }
+#pragma unroll
   for (int q = 0; q < 3; q++) {
-    u64 v = 0;
-    for (u64 b = threadIdx.x; b < nb; b += kThreads) v += parts[b * 3 + q];
-    v = jyscan::wave_sum<u64>(v);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) counts[q] = red[0] + red[1] + red[2] + red[3];
-    __syncthreads();
+    const u64 w = jyscan::wave_sum<u64>(v[q]);
+    if ((threadIdx.x & 63) == 0) red[q][threadIdx.x >> 6] = w;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    u64 t = 0;
+    for (int w = 0; w < kSumThreads / 64; w++) t += red[threadIdx.x][w];
+    counts[threadIdx.x] = t;
   }
 }
 
@@ -170,6 +208,7 @@ __global__ __launch_bounds__(kThreads) void k_key_claim(In I, Dir D, const u32* 
   const uint8_t* k = I.kb + I.ko[i];
   const u64 len = I.ko[i + 1] - I.ko[i];
   const u64 t = th[i];
+  const KeyW kw = key_words(k, len);
   const u64 mine = ((u64)tag_of(t) << 32) | kPending | i;
   u64 p = t >> D.shift;
   u64 e = D.table[p];
@@ -187,7 +226,7 @@ __global__ __launch_bounds__(kThreads) void k_key_claim(In I, Dir D, const u32* 
     if ((u32)(e >> 32) == tag_of(t) && (e & kPending)) {
       const u64 j = e & kIdxMask;
       const u64 lj = I.ko[j + 1] - I.ko[j];
-      if (lj == len && bytes_equal(I.kb + I.ko[j], k, len)) {
+      if (lj == len && key_equal(I.kb + I.ko[j], k, len, kw)) {
         owner[i] = (u32)j;
         return;
       }
@@ -241,7 +280,7 @@ __global__ __launch_bounds__(kThreads) void k_key_commit(In I, Dir D, uint8_t* _
     const u64 len = I.ko[i + 1] - I.ko[i];
     const u64 at = base_byte + boff[i];
     const uint8_t* src = I.kb + I.ko[i];
-    for (u64 b = 0; b < len; b++) dbytes[at + b] = src[b];
+    for (u64 b = 0; b < len; b++) dbytes[at + b] = src[b];  // (word reads + byte stores: 72 -> 79 us)
     D.kref[slot] = (at << JY_LR_LEN_BITS) | len;
     D.khash[slot] = th[i];
   }
@@ -364,7 +403,7 @@ int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, co
   JY_TRY(jy_scratch(eng, 29, nb * 24 + 64, &pp));
   u64* parts = static_cast<u64*>(pp);
   LAUNCH(k_key_probe, n, I, dir_of(K), res, th, parts);
-  hipLaunchKernelGGL(k_key_sum, dim3(1), dim3(kThreads), 0, eng->stream, parts, nb, counts);
+  hipLaunchKernelGGL(k_key_sum, dim3(1), dim3(kSumThreads), 0, eng->stream, parts, nb, counts);
   JY_HIP(eng, hipGetLastError());
   if (after_probe) JY_TRY(after_probe(arg));  // (a pageable read-back below may block at once)
   u64 hc[3];
@@ -397,6 +436,8 @@ int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, co
   JY_HIP(eng, hipMemsetAsync(first, 0xFF, n * 4, eng->stream));
   LAUNCH(k_key_claim, n, I, D, res, th, owner, pos);
   LAUNCH(k_key_first, n, n, res, owner, first);
+  // (rank and byte offset packed into one word for one scan: the look-back
+  // status words carry 40-bit values, jy_dscan.hpp -- kept as two scans)
   LAUNCH(k_key_flags, n + 1, I, res, owner, first, flag, blen);
   JY_TRY((jydscan::scan<jydscan::OpSum, false>(eng, n + 1, jydscan::LdArr<u32>{flag}, jydscan::StArr<u32>{rank})));
   JY_TRY((jydscan::scan<jydscan::OpSum, false>(eng, n + 1, jydscan::LdArr<u64>{blen}, jydscan::StArr<u64>{boff})));
