@@ -131,6 +131,9 @@ __device__ __forceinline__ u64 lookback(const Ctx& c, u32 tile, u64 agg, u64* ld
 // drawing them.  With G > 1 the workgroup first reduces its G tiles (its
 // look-back aggregate), then scans them again from the top (the re-read is
 // its own recent loads, mostly still in the caches).
+// (Round 4 tried the reduce sweep with four tiles' loads in flight and the
+// rescan loading tile s + 1 before tile s's block scan: in-box A/B of the
+// key-resolving TREG step, 2 runs each, and the TLOG step -- no difference.)
 constexpr u64 kMaxTickets = 1024;
 
 // out[i] = Op-prefix of ld(0..i-1) (exclusive) or of ld(0..i) (inclusive),
