@@ -212,12 +212,79 @@ def _owner_seed(seed, owner):
     return seed + owner * 7919  # owner 0 keeps the single-GPU stream
 
 
+LAUNCH_FAIL_EXIT = 2
+
+
+def visible_devices():
+    """GPUs this process would see, counted in a CHILD process: the launching
+    parent never touches the GPU (it starts torch.distributed.run as a child,
+    and a process that initialised HIP must not fork-exec GPU programs)"""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       capture_output=True, text=True)
+    try:
+        return int(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return 0
+
+
+def launch_cmd(argv, n, port):
+    """the torch.distributed.run command of an N-rank run (one process per GPU,
+    rendezvous on 127.0.0.1), re-running this file with the same arguments"""
+    import sys
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.abspath(__file__)] + list(argv)
+
+
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(args, argv):
+    """`--gpus N > 1` without a torch.distributed environment: start N ranks as
+    a child torch.distributed.run and exit with its code (rank 0 prints the
+    line).  Refuses (exit LAUNCH_FAIL_EXIT) when fewer than N GPUs are
+    visible: an N-GPU line must never come from fewer GPUs."""
+    import subprocess
+    import sys
+    if args.backend == "nccl":
+        have = visible_devices()
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but {have} GPU(s) visible", file=sys.stderr, flush=True)
+            return LAUNCH_FAIL_EXIT
+    return subprocess.run(launch_cmd(argv, args.gpus, free_port())).returncode
+
+
+def world_check(args, world, ndev):
+    """None if this rank's environment fits --gpus, else the reason"""
+    if world != args.gpus:
+        return f"WORLD_SIZE {world} but --gpus {args.gpus}"
+    if args.backend == "nccl" and ndev < world:
+        return f"{world} ranks over RCCL but {ndev} GPU(s) visible"
+    return None
+
+
 def main():
+    import sys
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args, sys.argv[1:]))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:  # before torch: a mismatched launch fails at once
+        print(f"bench.py: {world_check(args, world, world)}", file=sys.stderr, flush=True)
+        sys.exit(LAUNCH_FAIL_EXIT)
     import torch
+    why = world_check(args, world, torch.cuda.device_count())
+    if why:
+        print(f"bench.py: {why}", file=sys.stderr, flush=True)
+        sys.exit(LAUNCH_FAIL_EXIT)
     if args.backend == "gloo":  # rehearsal: several ranks may share one GPU
         local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
@@ -419,6 +486,14 @@ def main():
                          cells_per_step, line, verify)
         except Exception as e:  # the headline stands; the routed phase's failure is reported in the line
             line["routed_error"] = f"{type(e).__name__}: {e}"
+        r = line.get("routed")
+        if isinstance(r, dict) and "value" in r:
+            # the end-to-end figure beside the key-sharded `value`: peer batches
+            # arriving mixed, each owner's part moved by the node's native RCCL
+            line["value_routed"] = r["value"]
+            line["value_routed_note"] = ("end-to-end merges/s with peer batches arriving mixed and routed to "
+                                         "their owners over RCCL (jy_node_counter_converge_block); `value` is "
+                                         "the key-sharded converge")
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:
