@@ -124,7 +124,7 @@ __device__ __forceinline__ u64 lookback(const Ctx& c, u32 tile, u64 agg, u64* ld
   return r;
 }
 
-// Tiles of kTileItems items; a workgroup takes ONE ticket for G consecutive
+// (k_select) Tiles of kTileItems items; a workgroup takes ONE ticket for G consecutive
 // tiles (G = 1 up to kMaxTickets tiles): a ticket is a same-address atomic,
 // and those serialise at ~11 ns each (tools/mb_ticket.hip: 4096 tickets
 // 48 us, 32768 tickets 373 us), so an 8M-item scan spent half its time
@@ -135,68 +135,6 @@ __device__ __forceinline__ u64 lookback(const Ctx& c, u32 tile, u64 agg, u64* ld
 // rescan loading tile s + 1 before tile s's block scan: in-box A/B of the
 // key-resolving TREG step, 2 runs each, and the TLOG step -- no difference.)
 constexpr u64 kMaxTickets = 1024;
-
-// out[i] = Op-prefix of ld(0..i-1) (exclusive) or of ld(0..i) (inclusive),
-// for i < n; items thread-consecutive within a tile
-template <class Op, bool kIncl, class Ld, class St>
-__global__ __launch_bounds__(kThreads) void k_scan(Ctx c, u64 n, u64 ntiles, u64 G, Ld ld, St st) {
-  __shared__ u64 red[kThreads / 64];
-  __shared__ u64 pre;
-  __shared__ u32 tk;
-  Op op;
-  const u32 t = jyscan::ticket(c.tick, &tk);
-  if (t == gridDim.x - 1 && threadIdx.x == 0) *c.tick = 0;  // the launch's last ticket: all are drawn
-  const u64 s0 = (u64)t * G, s1 = s0 + G < ntiles ? s0 + G : ntiles;
-  u64 v[kPer], acc = Op::kId;
-  if (s1 - s0 == 1) {  // one tile: loaded once
-    const u64 i0 = s0 * kTileItems + (u64)threadIdx.x * kPer;
-#pragma unroll
-    for (int u = 0; u < kPer; u++) {
-      v[u] = i0 + u < n ? ld(i0 + u) : Op::kId;
-      acc = op(acc, v[u]);
-    }
-    u64 tot;
-    const u64 off = block_excl<Op>(acc, red, tot);
-    const u64 p = lookback<Op>(c, t, tot, &pre);
-    u64 run = op(p, off);
-#pragma unroll
-    for (int u = 0; u < kPer; u++) {
-      const u64 i = i0 + u;
-      const u64 nx = op(run, v[u]);
-      if (i < n) st(i, kIncl ? nx : run);
-      run = nx;
-    }
-    return;
-  }
-  for (u64 s = s0; s < s1; s++) {
-    const u64 i0 = s * kTileItems + (u64)threadIdx.x * kPer;
-#pragma unroll
-    for (int u = 0; u < kPer; u++) acc = op(acc, i0 + u < n ? ld(i0 + u) : Op::kId);
-  }
-  u64 tot;
-  block_excl<Op>(acc, red, tot);
-  u64 base = lookback<Op>(c, t, tot, &pre);
-  for (u64 s = s0; s < s1; s++) {
-    const u64 i0 = s * kTileItems + (u64)threadIdx.x * kPer;
-    u64 a = Op::kId;
-#pragma unroll
-    for (int u = 0; u < kPer; u++) {
-      v[u] = i0 + u < n ? ld(i0 + u) : Op::kId;
-      a = op(a, v[u]);
-    }
-    u64 ts;
-    const u64 off = block_excl<Op>(a, red, ts);
-    u64 run = op(base, off);
-#pragma unroll
-    for (int u = 0; u < kPer; u++) {
-      const u64 i = i0 + u;
-      const u64 nx = op(run, v[u]);
-      if (i < n) st(i, kIncl ? nx : run);
-      run = nx;
-    }
-    base = op(base, ts);
-  }
-}
 
 // indices i < n with pred(i), in order, into out; the count into *count
 template <class Pred>
@@ -243,18 +181,149 @@ __global__ __launch_bounds__(kThreads) void k_select(Ctx c, u64 n, u64 ntiles, u
 
 inline u64 tiles_of(u64 n) { return n == 0 ? 1 : (n + kTileItems - 1) / kTileItems; }
 
-// a scan launch over n items: ld(i) -> u64, st(i, prefix)
 // tiles per workgroup (one ticket each workgroup) and the workgroups
 inline u64 group_of(u64 nt) { return (nt + kMaxTickets - 1) / kMaxTickets; }
 
+// ---- reduce-then-scan (round 5): three launches, no look-back, no tickets.
+// A tile is kRows rows of kThreads items; lane t of a row holds item
+// row * kThreads + t, so every load and store is coalesced (the look-back
+// form above gave each thread 8 consecutive items: 64-B lane strides).  A
+// chunk is T consecutive tiles, at most kMaxChunks chunks per scan:
+//   k_scan_part   each chunk's reduction           (reads the input once)
+//   k_scan_mid    one workgroup: exclusive scan of the chunk totals
+//   k_scan_down   each chunk scanned from its base (reads it again: mostly
+//                 the caches' -- a chunk is 4-64 KB, read moments before)
+// The look-back scan of an 8M-item u64 column took 80-97 us on MI355X (node
+// TREG trace, round 5): one ticket per workgroup, 1024 workgroups of 4 tiles,
+// strided lanes.  Values are full 64-bit (no 40-bit look-back words).
+constexpr int kRows = kPer;
+constexpr u64 kMaxChunks = kThreads * kRows;  // k_scan_mid scans them as one tile
+
+// one tile's rows, scanned in place: x[u] (row u's item of this lane) becomes
+// its exclusive (or inclusive) prefix from `carry`; returns the tile total
+template <class Op, bool kIncl>
+__device__ __forceinline__ u64 tile_rows(u64 (&x)[kRows], u64 carry, u64 (*wt)[kThreads / 64]) {
+  Op op;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  u64 inc[kRows];
+#pragma unroll
+  for (int u = 0; u < kRows; u++) {
+    inc[u] = wave_incl<Op>(x[u]);
+    if (lane == 63) wt[u][w] = inc[u];
+  }
+  __syncthreads();
+  u64 base = carry;
+#pragma unroll
+  for (int u = 0; u < kRows; u++) {
+    u64 off = base, row = Op::kId;
+#pragma unroll
+    for (int q = 0; q < kThreads / 64; q++) {
+      const u64 v = wt[u][q];
+      if (q < w) off = op(off, v);
+      row = op(row, v);
+    }
+    const u64 ex = __shfl_up(inc[u], 1);
+    x[u] = kIncl ? op(off, inc[u]) : op(off, lane == 0 ? Op::kId : ex);
+    base = op(base, row);
+  }
+  __syncthreads();  // wt is reused by the next tile
+  return base;
+}
+
+template <class Op, class Ld>
+__global__ __launch_bounds__(kThreads) void k_scan_part(u64 n, u64 T, Ld ld, u64* __restrict__ part) {
+  __shared__ u64 red[kThreads / 64];
+  Op op;
+  const u64 i0 = (u64)blockIdx.x * T * kTileItems;
+  const u64 i1 = i0 + T * kTileItems < n ? i0 + T * kTileItems : n;
+  u64 acc = Op::kId;
+  for (u64 b = i0; b < i1; b += kTileItems) {
+    u64 v[kRows];
+#pragma unroll
+    for (int u = 0; u < kRows; u++) {
+      const u64 i = b + (u64)u * kThreads + threadIdx.x;
+      v[u] = i < i1 ? ld(i) : Op::kId;
+    }
+#pragma unroll
+    for (int u = 0; u < kRows; u++) acc = op(acc, v[u]);
+  }
+  acc = wave_reduce<Op>(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u64 t = Op::kId;
+#pragma unroll
+    for (int q = 0; q < kThreads / 64; q++) t = op(t, red[q]);
+    part[blockIdx.x] = t;
+  }
+}
+
+// the nc chunk totals -> their exclusive prefixes (in place; part[nc] = all)
+template <class Op>
+__global__ __launch_bounds__(kThreads) void k_scan_mid(u64 nc, u64* __restrict__ part) {
+  __shared__ u64 wt[kRows][kThreads / 64];
+  u64 x[kRows];
+#pragma unroll
+  for (int u = 0; u < kRows; u++) {
+    const u64 i = (u64)u * kThreads + threadIdx.x;
+    x[u] = i < nc ? part[i] : Op::kId;
+  }
+  const u64 tot = tile_rows<Op, false>(x, Op::kId, wt);
+#pragma unroll
+  for (int u = 0; u < kRows; u++) {
+    const u64 i = (u64)u * kThreads + threadIdx.x;
+    if (i < nc) part[i] = x[u];
+  }
+  if (threadIdx.x == 0) part[nc] = tot;
+}
+
+// chunk blockIdx.x scanned from part[blockIdx.x] (nullptr: from the identity,
+// the one-workgroup form of a small scan)
+template <class Op, bool kIncl, class Ld, class St>
+__global__ __launch_bounds__(kThreads) void k_scan_down(u64 n, u64 T, Ld ld, St st, const u64* __restrict__ part) {
+  __shared__ u64 wt[kRows][kThreads / 64];
+  const u64 i0 = (u64)blockIdx.x * T * kTileItems;
+  const u64 i1 = i0 + T * kTileItems < n ? i0 + T * kTileItems : n;
+  u64 carry = part ? part[blockIdx.x] : Op::kId;
+  for (u64 b = i0; b < i1; b += kTileItems) {
+    u64 x[kRows];
+#pragma unroll
+    for (int u = 0; u < kRows; u++) {
+      const u64 i = b + (u64)u * kThreads + threadIdx.x;
+      x[u] = i < i1 ? ld(i) : Op::kId;
+    }
+    carry = tile_rows<Op, kIncl>(x, carry, wt);
+#pragma unroll
+    for (int u = 0; u < kRows; u++) {
+      const u64 i = b + (u64)u * kThreads + threadIdx.x;
+      if (i < i1) st(i, x[u]);
+    }
+  }
+}
+
+// small scans stay in one workgroup (one launch): up to this many tiles
+constexpr u64 kOneGroupTiles = 8;
+
+// a scan over n items: ld(i) -> u64, st(i, prefix).  In place (st writing
+// what ld reads) is allowed: every item is read before it is written.
 template <class Op, bool kIncl, class Ld, class St>
 int32_t scan(jy_engine* eng, u64 n, Ld ld, St st) {
   if (n == 0) return JY_OK;
-  const u64 nt = tiles_of(n), G = group_of(nt), nwg = (nt + G - 1) / G;
-  Ctx c;
-  JY_TRY(jy_dscan_ctx(eng, nwg, &c.status, &c.tick, &c.epoch));
-  hipLaunchKernelGGL((k_scan<Op, kIncl, Ld, St>), dim3((u32)nwg), dim3(kThreads), 0, eng->stream, c, n, nt, G, ld,
-                     st);
+  const u64 nt = tiles_of(n);
+  if (nt <= kOneGroupTiles) {
+    hipLaunchKernelGGL((k_scan_down<Op, kIncl, Ld, St>), dim3(1), dim3(kThreads), 0, eng->stream, n, nt, ld, st,
+                       (const u64*)nullptr);
+    JY_HIP(eng, hipGetLastError());
+    return JY_OK;
+  }
+  const u64 T = (nt + kMaxChunks - 1) / kMaxChunks, nc = (nt + T - 1) / T;
+  void* p;
+  JY_TRY(jy_scratch(eng, 31, (nc + 1) * 8, &p));
+  u64* part = static_cast<u64*>(p);
+  hipLaunchKernelGGL((k_scan_part<Op, Ld>), dim3((u32)nc), dim3(kThreads), 0, eng->stream, n, T, ld, part);
+  hipLaunchKernelGGL((k_scan_mid<Op>), dim3(1), dim3(kThreads), 0, eng->stream, nc, part);
+  hipLaunchKernelGGL((k_scan_down<Op, kIncl, Ld, St>), dim3((u32)nc), dim3(kThreads), 0, eng->stream, n, T, ld, st,
+                     (const u64*)part);
   JY_HIP(eng, hipGetLastError());
   return JY_OK;
 }
