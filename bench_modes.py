@@ -15,7 +15,7 @@ import numpy as np
 HBM_PEAK_GBS = 8000.0
 
 
-def _timed(steps, warmup, step, dist, dev, eng=None, before_timed=None):
+def _timed(steps, warmup, step, dist, dev, eng=None, before_timed=None, drain=None):
     """warmup, then exactly `steps` steps bracketed by barrier + synchronize.
     Per-step device time: with `eng`, the engine's own HIP events around each
     merge call's device work (jy_timing_enable; host launch gaps excluded),
@@ -23,6 +23,8 @@ def _timed(steps, warmup, step, dist, dev, eng=None, before_timed=None):
     import torch
     for i in range(warmup):
         step(i)
+    if drain is not None:
+        drain()
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -46,6 +48,8 @@ def _timed(steps, warmup, step, dist, dev, eng=None, before_timed=None):
         host.append(time.perf_counter() - h0)
     if eng is None:
         ev1.record()
+    if drain is not None:  # a node's calls only enqueue: its queued work is inside the timed region
+        drain()
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -589,7 +593,7 @@ def bench_treg_node(args, eng, dev, dist, rank, world):
     step(0)  # batch 0 creates every key (the setup converge)
     node.sync()
     setup_s = time.perf_counter() - t0
-    elapsed, _ = _timed(args.steps, args.warmup, lambda i: step(1 + i % (nb - 1)), dist, dev)
+    elapsed, _ = _timed(args.steps, args.warmup, lambda i: step(1 + i % (nb - 1)), dist, dev, drain=node.sync)
     node.sync()
     t = _max_over_ranks(elapsed, dist, dev)
     st = node.stats()

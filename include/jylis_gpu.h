@@ -452,7 +452,26 @@ int32_t jy_ujson_converge_routed(jy_engine* eng, uint32_t nsrc, uint64_t cap_k, 
  * Every process of a multi-process node makes the same node calls in the
  * same order (they are collectives), each with its own batch (possibly
  * empty).  Errors: JY_* codes, detail in jy_node_last_error.  Reads, local
- * writes and flushes go to the owner's engine (jy_node_engine). */
+ * writes and flushes go to the owner's engine (jy_node_engine).
+ *
+ * One node per process, shared by every CRDT type (round 5).  The converge
+ * calls ENQUEUE: a call checks its arguments, copies host inputs into a
+ * pinned block the node owns (JY_HOST inputs are free to reuse when it
+ * returns) and queues a job; one worker thread per node runs the jobs in call
+ * order -- the count exchange, the key directory's miss count and every other
+ * host wait of a converge happen there, never on the caller's thread (a Pony
+ * scheduler thread).  The five RepoManager actors may call from five threads
+ * at once: their jobs run one at a time, so the node's ONE communicator sees
+ * one group at a time, issued from one thread (database.pony:18-23 makes the
+ * five actors; cluster.pony:205-213 is the broadcast this replaces).  A
+ * queued job's failure is returned by the node's next call (converge, fence,
+ * lock, sync, stats, replica_col) and its detail by jy_node_last_error.
+ * JY_DEVICE inputs are read by the worker later: they must stay valid and
+ * unchanged until jy_node_fence (every queued job issued to its streams) or
+ * jy_node_sync returns.  The engines of a node (jy_node_engine) are shared
+ * with the worker: use them between jy_node_lock and jy_node_unlock (the
+ * lock first waits for every job queued before it), or after jy_node_sync
+ * with no node call in flight. */
 typedef struct jy_node jy_node;
 #define JY_NODE_MAX_SHARDS 64
 #define JY_FABRIC_RCCL 0 /* RCCL communicator over the shards' GPUs (one GPU per shard)   */
@@ -476,6 +495,14 @@ int32_t jy_node_create(const jy_node_config* cfg, jy_node** out);
  * communicator of its own (fabric JY_FABRIC_RCCL) or device copies */
 int32_t jy_node_create_local(uint32_t nshards, const int32_t* devices, uint32_t fabric, const jy_config* engine,
                              jy_node** out);
+/* The process's shared node (round 5): the first call makes a one-process
+ * node over every visible GPU (jy_node_create_local, RCCL, `engine` for each
+ * shard); later calls return the same node.  Reference counted: the last
+ * jy_node_release destroys it.  The five GPU repos of a Jylis process (one
+ * RepoManager actor each, database.pony:18-22) share it, so one communicator
+ * and one engine per GPU serve every CRDT type. */
+int32_t jy_node_acquire_local(const jy_config* engine, jy_node** out);
+void jy_node_release(jy_node* node);
 /* GPUs visible to this process (0 without a GPU or HIP runtime) */
 int32_t jy_device_count(void);
 void jy_node_destroy(jy_node* node);
@@ -487,7 +514,17 @@ uint32_t jy_node_shard_of(const jy_node* node, const uint8_t* key, uint64_t len)
 /* register a replica identity on every local shard (the same column on all:
  * every process registers the cluster's identities in one order) */
 int32_t jy_node_replica_col(jy_node* node, uint64_t replica_id, uint32_t* col_out);
+/* every queued job issued and its GPU work finished (blocks) */
 int32_t jy_node_sync(jy_node* node);
+/* every job queued before this call issued to the GPU streams (blocks until
+ * the worker took them, not for the GPU); device inputs of those calls are
+ * no longer read by the host side, and the GPU reads them in stream order */
+int32_t jy_node_fence(jy_node* node);
+/* exclusive use of the node's engines: waits for the jobs queued before it
+ * (as jy_node_fence), then holds the node's lock until jy_node_unlock.  The
+ * lock is held even when an earlier job's failure is returned. */
+int32_t jy_node_lock(jy_node* node);
+void jy_node_unlock(jy_node* node);
 
 /* Converge one decoded peer batch (per process).  Keys: n strings (key_bytes,
  * key_offs[n + 1]).  `mem` = JY_HOST (staged per ingest shard) or JY_DEVICE

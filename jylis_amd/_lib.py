@@ -131,6 +131,8 @@ SIGNATURES = {
     "jy_node_create": (I32, [P, P]),
     "jy_node_create_local": (I32, [U32, P, U32, P, P]),
     "jy_device_count": (I32, []),
+    "jy_node_acquire_local": (I32, [P, P]),
+    "jy_node_release": (None, [P]),
     "jy_node_destroy": (None, [P]),
     "jy_node_last_error": (C.c_char_p, [P]),
     "jy_node_nshards": (U32, [P]),
@@ -138,6 +140,9 @@ SIGNATURES = {
     "jy_node_shard_of": (U32, [P, P, U64]),
     "jy_node_replica_col": (I32, [P, U64, P]),
     "jy_node_sync": (I32, [P]),
+    "jy_node_fence": (I32, [P]),
+    "jy_node_lock": (I32, [P]),
+    "jy_node_unlock": (None, [P]),
     "jy_node_counter_converge": (I32, [P, I32, U64, P, P, P, P, P, P, I32]),
     "jy_node_treg_converge": (I32, [P, U64, P, P, P, P, P, I32]),
     "jy_node_tlog_converge": (I32, [P, U64, P, P, P, P, P, P, P, I32]),

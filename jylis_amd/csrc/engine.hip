@@ -553,6 +553,20 @@ static int32_t keys_host(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb,
   return JY_OK;
 }
 
+// device keys interned (create on miss), with the directory's hook: `after`
+// runs once the probe is enqueued, before the host waits for its counts (the
+// node's one-shard path lands another read-back in that same wait)
+}  // extern "C"
+int32_t jy_keys_intern_dev(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, const u64* ko, u32* slots,
+                           int32_t (*after)(void*), void* arg) {
+  JY_TRY(check_type(eng, type));
+  JY_HIP(eng, hipSetDevice(eng->device));
+  u64 created = 0;
+  JY_TRY(jy_keydir_run(eng, type, n, kb, ko, slots, true, &created, after, arg));
+  return keys_created(eng, type, created);
+}
+extern "C" {
+
 int32_t jy_keys_intern(jy_engine* eng, int32_t type, uint64_t n, const uint8_t* kb, const uint64_t* ko,
                        uint32_t* slots) {
   return jy_keys_intern_mem(eng, type, n, kb, ko, slots, JY_HOST);

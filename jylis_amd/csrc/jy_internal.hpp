@@ -223,7 +223,7 @@ struct KeyDir {
   u64* kref = nullptr;   // [scap] offset << 24 | length
   u64* khash = nullptr;  // [scap] table hash
   u64 n = 0, scap = 0;   // keys, slot capacity
-  u64* table = nullptr;  // [tcap] tag << 32 | slot, ~0 empty
+  u64* table = nullptr;  // [tcap] 32-B records (k_keys.hip TRec): tag << 32 | slot (~0 empty), len, 2 key words
   u64 tcap = 0;
   u32 lg = 0;
 };
@@ -617,6 +617,8 @@ int32_t jy_keydir_reserve(jy_engine* eng, int32_t type, u64 cap);
 void jy_keydir_free(jy_engine* eng, KeyDir& K);
 int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, const u64* ko, u32* slots, bool create,
                       u64* created, int32_t (*after_probe)(void*) = nullptr, void* arg = nullptr);
+int32_t jy_keys_intern_dev(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, const u64* ko, u32* slots,
+                           int32_t (*after)(void*), void* arg);
 int32_t jy_ujson_grow(jy_engine* eng, u64 need_slots);
 int32_t jy_ujson_extend(jy_engine* eng, u64 from, u64 to);
 int32_t jy_ujson_sizes(jy_engine* eng, u64 n, const u32* slots, u64* ne, u64* nc);

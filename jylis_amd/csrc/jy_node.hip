@@ -46,7 +46,12 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <initializer_list>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <mutex>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -314,6 +319,15 @@ __global__ __launch_bounds__(kT) void k_nd_lr(u64 n, const u64* __restrict__ vle
   lr[j] = l > 8 ? ((rebase + voff[j]) << JY_LR_LEN_BITS) | l : l;
 }
 
+// device inputs: the longest value over 16 MiB, if any (the host form refuses
+// such a batch in values_check; a handle's length has 24 bits)
+__global__ __launch_bounds__(kT) void k_nd_maxlen(const u64* __restrict__ vo, u64 n, unsigned long long* __restrict__ out) {
+  const u64 i = (u64)blockIdx.x * kT + threadIdx.x;
+  if (i >= n) return;
+  const u64 l = vo[i + 1] - vo[i];
+  if (l > JY_MAX_VALUE_LEN) atomicMax(out, (unsigned long long)l);
+}
+
 __global__ __launch_bounds__(kT) void k_nd_cells(u64 n, const u64* __restrict__ packed, uint8_t* __restrict__ sign,
                                                  u16* __restrict__ col) {
   const u64 j = (u64)blockIdx.x * kT + threadIdx.x;
@@ -321,6 +335,50 @@ __global__ __launch_bounds__(kT) void k_nd_cells(u64 n, const u64* __restrict__ 
   const u64 w = packed[j];
   sign[j] = (uint8_t)(w >> 16);
   col[j] = (u16)w;
+}
+
+// ---------------------------------------------------------------------------
+// kernels: one shard (S = 1) -- the owner reads the staged inputs in place
+
+// value heads: the 8-byte big-endian prefix, and the padded length of a long
+// value (plen[n] = 0: the scan's last input)
+__global__ __launch_bounds__(kT) void k_nd1_head(u64 n, const u64* __restrict__ vo, u64 vbase,
+                                                 const uint8_t* __restrict__ vb, u64* __restrict__ pre,
+                                                 u64* __restrict__ plen) {
+  const u64 j = (u64)blockIdx.x * kT + threadIdx.x;
+  if (j > n) return;
+  if (j == n) {
+    plen[n] = 0;
+    return;
+  }
+  const u64 a = vo[j], l = vo[j + 1] - a;
+  pre[j] = __builtin_bswap64(jy_ld8u(vb + (a - vbase), l));
+  plen[j] = l > 8 ? (l + 7) & ~7ull : 0;
+}
+
+// long values' bytes into the arena (dst = the reserved tail, voff from the
+// scan of plen: 8-byte granules, word stores) and every value's handle
+__global__ __launch_bounds__(kT) void k_nd1_long(u64 n, const u64* __restrict__ vo, u64 vbase,
+                                                 const uint8_t* __restrict__ vb, const u64* __restrict__ voff,
+                                                 uint8_t* __restrict__ dst, u64 rebase, u64* __restrict__ lr) {
+  const u64 j = (u64)blockIdx.x * kT + threadIdx.x;
+  if (j >= n) return;
+  const u64 a = vo[j], l = vo[j + 1] - a;
+  if (l <= 8) {
+    lr[j] = l;
+    return;
+  }
+  const u64 d = voff[j];
+  u64* o = reinterpret_cast<u64*>(dst + d);
+  const uint8_t* src = vb + (a - vbase);
+  for (u64 q = 0; q < (l + 7) / 8; q++) o[q] = jy_ld8u(src + 8 * q, l - 8 * q);
+  lr[j] = ((rebase + d) << JY_LR_LEN_BITS) | l;
+}
+
+// a CSR's offsets from 0: out[j] = offs[j] - offs[0], j <= n
+__global__ __launch_bounds__(kT) void k_nd1_rebase(u64 n, const u64* __restrict__ offs, u64* __restrict__ out) {
+  const u64 j = (u64)blockIdx.x * kT + threadIdx.x;
+  if (j <= n) out[j] = offs[j] - offs[0];
 }
 
 }  // namespace
@@ -366,17 +424,72 @@ struct NdShard {
 
 }  // namespace
 
+// ---- the node's executor (round 5) ----
+// A converge call validates its arguments, copies host inputs into a pinned
+// block the node owns (parallel host copies) and queues a job; ONE worker
+// thread per node runs the jobs in call order.  So a call returns without
+// waiting for the GPU (the exchange's count read-back, the key directory's
+// miss count and the CSR ends of device inputs are the worker's waits, not
+// the caller's), and every call of every CRDT type -- the five RepoManager
+// actors of one Jylis process share ONE node -- issues its RCCL groups from
+// the same thread in one order: one communicator, no interleaving.
+namespace {
+
+constexpr int32_t kPinned = 2;  // internal mem mode: host memory the node owns (pinned), DMA'd in place
+constexpr int kJobDepth = 3;    // pinned blocks: jobs queued or running at once (a caller waits beyond)
+inline bool on_host(int32_t mem) { return mem != JY_DEVICE; }
+
+enum JobKind { K_COUNTER, K_TREG, K_TLOG, K_UJSON, K_BLOCK };
+struct NdJob {
+  int kind = 0;
+  int32_t type = 0, mem = JY_DEVICE;
+  u64 n = 0;
+  const void* a[11] = {};  // the call's arrays (host inputs: rebased into the pinned block)
+  int pin = -1;
+  u32 ncols = 0, slot0 = 0, nslots = 0;  // K_BLOCK
+  std::vector<u16> cols;
+};
+struct NdPin {
+  void* p = nullptr;
+  u64 bytes = 0;
+  bool busy = false;
+  std::vector<hipEvent_t> ev;  // per local shard: the job's DMAs out of this block are done
+};
+
+}  // namespace
+
 struct jy_node {
   jy_node_config cfg;
   u32 S = 0, nlocal = 0, rank0 = 0, fabric = JY_FABRIC_RCCL;
   std::vector<NdShard> sh;
-  std::string err;
+  std::string err;   // callers' errors (jy_node_last_error)
+  std::string werr;  // the worker's (moved to err when a call reports it)
   u64 stats[5] = {};
+  u32 nrep = 0;  // replica columns registered (host-side checks of counter cells)
+  // executor
+  std::mutex mu;  // held while a job runs, by jy_node_lock holders, and by locked entry points
+  std::mutex qmu;
+  std::condition_variable qcv, dcv;
+  std::deque<NdJob> q;
+  u64 submitted = 0, finished = 0;
+  bool stop = false, inline_jobs = false;
+  bool regroup_one = false;  // JY_NODE_REGROUP_ONE=1: S = 1 through the regroup + exchange (A/B, tests)
+  std::thread worker;
+  std::thread::id wid;
+  int32_t aerr = JY_OK;  // first failure of a queued job, reported by the next call
+  std::string aerr_msg;
+  NdPin pins[kJobDepth];
   int32_t fail(int32_t code, const std::string& m) {
-    err = m;
+    (std::this_thread::get_id() == wid ? werr : err) = m;
     return code;
   }
 };
+
+namespace {
+void exec_start(jy_node* nd);
+void exec_stop(jy_node* nd);
+int32_t exec_fence(jy_node* nd);  // every queued job issued; a queued job's failure, if any
+}  // namespace
 
 namespace {
 
@@ -397,6 +510,25 @@ namespace {
     if (rc_ != JY_OK) return (nd)->fail(rc_, std::string("shard ") +            \
                                                  std::to_string((sh).rank) + ": " + (sh).eng->err); \
   } while (0)
+
+// an RCCL group that is ended on every exit: an error return inside an open
+// group would leave this thread's group depth raised, and the next node call's
+// sends and receives would pile into a group that never launches
+struct NcclGroup {
+  bool open = false;
+  ncclResult_t start() {
+    const ncclResult_t r = ncclGroupStart();
+    open = r == ncclSuccess;
+    return r;
+  }
+  ncclResult_t end() {
+    open = false;
+    return ncclGroupEnd();
+  }
+  ~NcclGroup() {
+    if (open) ncclGroupEnd();
+  }
+};
 
 int32_t buf(jy_node* nd, NdShard& sh, int idx, u64 bytes, void** out) {
   NdBuf& b = sh.b[idx];
@@ -425,7 +557,7 @@ int32_t bufT(jy_node* nd, NdShard& sh, int idx, u64 count, T** out) {
 
 // two words read back from device (or host) memory: a CSR's first and last offset
 int32_t read2(jy_node* nd, NdShard& sh, const u64* a, const u64* b, int32_t mem, u64& x, u64& y) {
-  if (mem == JY_HOST) {
+  if (on_host(mem)) {
     x = *a;
     y = *b;
     return JY_OK;
@@ -581,7 +713,8 @@ int32_t exchange(jy_node* nd, u32 W, const std::vector<Wire>& wires, u32 nl) {
   const u32 S = nd->S;
   // 1. counts: per destination and granule -> per source and granule
   if (nd->fabric == JY_FABRIC_RCCL) {
-    ND_NCCL(nd, ncclGroupStart());
+    NcclGroup grp;  // ends the group on every return
+    ND_NCCL(nd, grp.start());
     for (NdShard& sh : nd->sh) {
       u64* cnt = static_cast<u64*>(sh.b[B_CNT].p);
       for (u32 d = 0; d < S; d++) {
@@ -589,7 +722,7 @@ int32_t exchange(jy_node* nd, u32 W, const std::vector<Wire>& wires, u32 nl) {
         ND_NCCL(nd, ncclRecv(cnt + (u64)(kMaxS + d) * W, W, ncclUint64, (int)d, sh.comm, sh.eng->stream));
       }
     }
-    ND_NCCL(nd, ncclGroupEnd());
+    ND_NCCL(nd, grp.end());
     for (NdShard& sh : nd->sh) {
       ND_HIP(nd, hipSetDevice(sh.dev));
       ND_HIP(nd, hipMemcpyAsync(sh.pin, sh.b[B_CNT].p, 2 * kMaxS * kMaxW * 8, hipMemcpyDeviceToHost, sh.eng->stream));
@@ -632,7 +765,8 @@ int32_t exchange(jy_node* nd, u32 W, const std::vector<Wire>& wires, u32 nl) {
   }
   // 3. payload
   if (nd->fabric == JY_FABRIC_RCCL) {
-    ND_NCCL(nd, ncclGroupStart());
+    NcclGroup grp;  // ends the group on every return
+    ND_NCCL(nd, grp.start());
     for (NdShard& sh : nd->sh) {
       ND_HIP(nd, hipSetDevice(sh.dev));  // (the self copies below)
       const u64* sc = sh.pin;
@@ -656,7 +790,7 @@ int32_t exchange(jy_node* nd, u32 W, const std::vector<Wire>& wires, u32 nl) {
         }
       }
     }
-    ND_NCCL(nd, ncclGroupEnd());
+    ND_NCCL(nd, grp.end());
   } else {
     // pull: each destination waits for every source's columns, copies its
     // parts on its own stream, and records that its receives landed (the next
@@ -710,6 +844,13 @@ void split(const jy_node* nd, u64 n, std::vector<u64>& at) {
 // stage a chunk: host memory through the engine's pinned ring, device
 // memory in place
 int32_t stage(jy_node* nd, NdShard& sh, int slot, const void* src, u64 bytes, int32_t mem, const void** out) {
+  if (mem == kPinned) {  // the node's pinned block: one DMA, no second host copy
+    void* d;
+    ND_ENG(nd, sh, jy_scratch(sh.eng, slot, std::max<u64>(bytes, 8), &d));
+    if (bytes) ND_HIP(nd, hipMemcpyAsync(d, src, bytes, hipMemcpyHostToDevice, sh.eng->stream));
+    *out = d;
+    return JY_OK;
+  }
   ND_ENG(nd, sh, jy_stage(sh.eng, slot, src, bytes, mem, out));
   return JY_OK;
 }
@@ -795,6 +936,30 @@ int32_t values_check(jy_node* nd, const u64* vo, u64 a, u64 e, int32_t mem) {
   return JY_OK;
 }
 
+// device inputs: the n value lengths at vo checked on the device; the
+// verdict lands in the pinned read-back area with the next read2's sync
+// (values_dev_ok after it)
+int32_t values_dev_enqueue(jy_node* nd, NdShard& sh, const u64* vo, u64 n, int32_t mem) {
+  if (mem != JY_DEVICE || n == 0) return JY_OK;
+  u64* w;
+  JY_TRY(bufT(nd, sh, B_CNT, 2 * kMaxS * kMaxW + 1, &w));
+  w += 2 * kMaxS * kMaxW;  // (past the counts)
+  ND_HIP(nd, hipMemsetAsync(w, 0, 8, sh.eng->stream));
+  hipLaunchKernelGGL(k_nd_maxlen, dim3(grid_of(n)), dim3(kT), 0, sh.eng->stream, vo, n,
+                     reinterpret_cast<unsigned long long*>(w));
+  ND_HIP(nd, hipGetLastError());
+  ND_HIP(nd, hipMemcpyAsync(sh.pin + 2 * kMaxS * kMaxW + 2, w, 8, hipMemcpyDeviceToHost, sh.eng->stream));
+  return JY_OK;
+}
+int32_t values_dev_ok(jy_node* nd, NdShard& sh, int32_t mem) {
+  if (mem != JY_DEVICE) return JY_OK;
+  u64& v = sh.pin[2 * kMaxS * kMaxW + 2];
+  const u64 l = v;
+  v = 0;
+  if (l > JY_MAX_VALUE_LEN) return nd->fail(JY_ERANGE, "value longer than 16 MiB");
+  return JY_OK;
+}
+
 // per local shard: keys chunk (staged) -> Ingest
 int32_t stage_keys(jy_node* nd, NdShard& sh, u64 a, u64 e, const uint8_t* kb, const u64* ko, int32_t mem, Ingest& in) {
   sh.n = e - a;
@@ -802,11 +967,11 @@ int32_t stage_keys(jy_node* nd, NdShard& sh, u64 a, u64 e, const uint8_t* kb, co
   u64 k0, k1;
   JY_TRY(read2(nd, sh, ko + a, ko + e, mem, k0, k1));
   if (k1 < k0) return nd->fail(JY_EINVAL, "key offsets are not ascending");
-  JY_TRY(stage(nd, sh, 0, mem == JY_HOST ? kb + k0 : kb, k1 - k0, mem, &dkb));
+  JY_TRY(stage(nd, sh, 0, on_host(mem) ? kb + k0 : kb, k1 - k0, mem, &dkb));
   JY_TRY(stage(nd, sh, 1, ko + a, (sh.n + 1) * 8, mem, &dko));
   in.kb = static_cast<const uint8_t*>(dkb);
   in.ko = static_cast<const u64*>(dko);
-  in.kobase = mem == JY_HOST ? k0 : 0;
+  in.kobase = on_host(mem) ? k0 : 0;
   in.nkb = k1 - k0;
   sh.tot[0] = sh.n;
   sh.tot[1] = in.nkb;
@@ -829,6 +994,7 @@ int32_t jy_node_unique_id(uint8_t* id_out) {
 
 void jy_node_destroy(jy_node* nd) {
   if (!nd) return;
+  exec_stop(nd);  // the queued jobs run first
   for (NdShard& sh : nd->sh) {
     hipSetDevice(sh.dev);
     if (sh.eng) hipStreamSynchronize(sh.eng->stream);
@@ -845,6 +1011,11 @@ void jy_node_destroy(jy_node* nd) {
       if (e) hipEventDestroy(e);
     if (sh.xs) hipStreamDestroy(sh.xs);
     jy_engine_destroy(sh.eng);
+  }
+  for (NdPin& pb : nd->pins) {
+    for (hipEvent_t e : pb.ev)
+      if (e) hipEventDestroy(e);
+    if (pb.p) hipHostFree(pb.p);
   }
   delete nd;
 }
@@ -914,6 +1085,20 @@ int32_t jy_node_create(const jy_node_config* cfg, jy_node** out) {
       return JY_EHIP;
     }
   }
+  // one process driving several GPUs: a shard's kernels read JY_DEVICE inputs
+  // that live on another local GPU (the header's "readable by every local
+  // shard's GPU"), so every local pair gets peer access (over xGMI)
+  for (const NdShard& a : nd->sh)
+    for (const NdShard& b : nd->sh)
+      if (a.dev != b.dev) {
+        hipSetDevice(a.dev);
+        const hipError_t e = hipDeviceEnablePeerAccess(b.dev, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+          std::fprintf(stderr, "jy_node_create: peer access %d -> %d: %s\n", a.dev, b.dev, hipGetErrorString(e));
+          (void)hipGetLastError();
+        }
+      }
+  exec_start(nd);
   *out = nd;
   return JY_OK;
 }
@@ -931,6 +1116,40 @@ int32_t jy_node_create_local(uint32_t nshards, const int32_t* devices, uint32_t 
   if (engine) cfg.engine = *engine;
   else jy_config_default(&cfg.engine);
   return jy_node_create(&cfg, out);
+}
+
+// the process's shared node (round 5): the five GPU repos of one Jylis
+// process (database.pony:18-22 makes one RepoManager per type) take the same
+// node, so one communicator and one engine per GPU serve all five types
+namespace {
+std::mutex g_shared_mu;
+jy_node* g_shared = nullptr;
+u64 g_shared_refs = 0;
+}  // namespace
+
+int32_t jy_node_acquire_local(const jy_config* engine, jy_node** out) {
+  std::lock_guard<std::mutex> lk(g_shared_mu);
+  *out = nullptr;
+  if (!g_shared) {
+    const int32_t n = jy_device_count();
+    if (n <= 0) return JY_EHIP;
+    int32_t devs[kMaxS];
+    const u32 S = std::min<u32>((u32)n, kMaxS);
+    for (u32 i = 0; i < S; i++) devs[i] = (int32_t)i;
+    JY_TRY(jy_node_create_local(S, devs, JY_FABRIC_RCCL, engine, &g_shared));
+  }
+  g_shared_refs++;
+  *out = g_shared;
+  return JY_OK;
+}
+
+void jy_node_release(jy_node* nd) {
+  std::lock_guard<std::mutex> lk(g_shared_mu);
+  if (!nd || nd != g_shared || g_shared_refs == 0) return;
+  if (--g_shared_refs == 0) {
+    jy_node_destroy(g_shared);
+    g_shared = nullptr;
+  }
 }
 
 int32_t jy_device_count(void) {
@@ -953,6 +1172,8 @@ uint32_t jy_node_shard_of(const jy_node* nd, const uint8_t* key, uint64_t len) {
 
 int32_t jy_node_replica_col(jy_node* nd, uint64_t id, uint32_t* col) {
   if (!nd) return JY_EINVAL;
+  JY_TRY(exec_fence(nd));
+  std::lock_guard<std::mutex> g(nd->mu);
   u32 c0 = 0;
   for (u32 L = 0; L < nd->nlocal; L++) {
     u32 c = 0;
@@ -961,11 +1182,14 @@ int32_t jy_node_replica_col(jy_node* nd, uint64_t id, uint32_t* col) {
     else if (c != c0) return nd->fail(JY_EINVAL, "shards disagree on a replica column (register on the node only)");
   }
   *col = c0;
+  nd->nrep = std::max<u32>(nd->nrep, c0 + 1);
   return JY_OK;
 }
 
 int32_t jy_node_sync(jy_node* nd) {
   if (!nd) return JY_EINVAL;
+  JY_TRY(exec_fence(nd));
+  std::lock_guard<std::mutex> g(nd->mu);
   for (NdShard& sh : nd->sh) {
     ND_ENG(nd, sh, jy_sync(sh.eng));
     ND_HIP(nd, hipStreamSynchronize(sh.xs));
@@ -975,14 +1199,268 @@ int32_t jy_node_sync(jy_node* nd) {
 
 int32_t jy_node_stats(jy_node* nd, uint64_t* out5) {
   if (!nd) return JY_EINVAL;
+  JY_TRY(exec_fence(nd));
+  std::lock_guard<std::mutex> g(nd->mu);
   std::memcpy(out5, nd->stats, sizeof(nd->stats));
   return JY_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// ---- one shard (S = 1) ----
+// The node's only shard owns every key: no regroup, no exchange, no copy of
+// any wire column.  The owner phase reads the staged inputs in place; the
+// long values' total (the arena's reservation) rides on the key directory's
+// probe wait.  (Through the regroup + self exchange, an 8.39M-key TREG call
+// spent ~0.9 ms of its 1.6 ms before the key probe: profiles/r05_*.)
+
+// up to 8 words of device (or host) memory, one wait
+int32_t readn(jy_node* nd, NdShard& sh, int32_t mem, std::initializer_list<const u64*> src, u64* out) {
+  int i = 0;
+  if (on_host(mem)) {
+    for (const u64* p : src) out[i++] = *p;
+    return JY_OK;
+  }
+  u64* pw = sh.pin + 2 * kMaxS * kMaxW + 8;  // [8, 16) of the read-back words
+  for (const u64* p : src) ND_HIP(nd, hipMemcpyAsync(pw + i++, p, 8, hipMemcpyDefault, sh.eng->stream));
+  ND_HIP(nd, hipStreamSynchronize(sh.eng->stream));
+  for (int k = 0; k < i; k++) out[k] = pw[k];
+  return JY_OK;
+}
+
+struct TotalHook {
+  NdShard* sh;
+  const u64* src;
+  u64* dst;
+};
+int32_t total_hook(void* p) {
+  TotalHook* h = static_cast<TotalHook*>(p);
+  return hipMemcpyAsync(h->dst, h->src, 8, hipMemcpyDeviceToHost, h->sh->eng->stream) == hipSuccess ? JY_OK : JY_EHIP;
+}
+
+// keys interned on the one shard; with `vals`, the ne values' heads, their
+// long bytes in the arena and their handles (pre, lr at R_F1 / R_LR)
+struct OneVals {
+  u64 ne = 0;
+  const u64* vo = nullptr;  // device, indexed from the first value
+  u64 vbase = 0;
+  const uint8_t* vb = nullptr;
+};
+int32_t one_keys_values(jy_node* nd, NdShard& sh, int32_t type, u64 n, const uint8_t* kbase, const u64* ko,
+                        const OneVals* vals, u32** slots, u64** pre, u64** lr) {
+  jy_engine* eng = sh.eng;
+  JY_TRY(bufT(nd, sh, R_SLOTS, std::max<u64>(n, 1), slots));
+  TotalHook hk{&sh, nullptr, sh.pin + 2 * kMaxS * kMaxW + 3};
+  const u64 ne = vals ? vals->ne : 0;
+  u64 *plen = nullptr, *voff = nullptr;
+  if (vals) {
+    JY_TRY(bufT(nd, sh, R_F1, std::max<u64>(ne, 1), pre));
+    JY_TRY(bufT(nd, sh, R_PLEN, ne + 1, &plen));
+    JY_TRY(bufT(nd, sh, R_VOFF, ne + 1, &voff));
+    JY_TRY(bufT(nd, sh, R_LR, std::max<u64>(ne, 1), lr));
+    *hk.dst = 0;
+    if (ne) {
+      hipLaunchKernelGGL(k_nd1_head, dim3(grid_of(ne + 1)), dim3(kT), 0, eng->stream, ne, vals->vo, vals->vbase,
+                         vals->vb, *pre, plen);
+      ND_HIP(nd, hipGetLastError());
+      ND_ENG(nd, sh, jy_scan_u64(eng, plen, voff, ne));
+      hk.src = voff + ne;
+    }
+  }
+  if (n) {
+    ND_ENG(nd, sh, jy_keys_intern_dev(eng, type, n, kbase, ko, *slots, hk.src ? total_hook : nullptr, &hk));
+  } else if (hk.src) {
+    ND_HIP(nd, hipMemcpyAsync(hk.dst, hk.src, 8, hipMemcpyDeviceToHost, eng->stream));
+    ND_HIP(nd, hipStreamSynchronize(eng->stream));
+  }
+  if (ne) {
+    uint8_t* dst;
+    u64 rebase;
+    ND_ENG(nd, sh, jy_arena_reserve(eng, type, *hk.dst, &dst, &rebase));
+    hipLaunchKernelGGL(k_nd1_long, dim3(grid_of(ne)), dim3(kT), 0, eng->stream, ne, vals->vo, vals->vbase, vals->vb,
+                       (const u64*)voff, dst, rebase, *lr);
+    ND_HIP(nd, hipGetLastError());
+  }
+  return JY_OK;
+}
+
+const uint8_t* rebased(const void* p, u64 by) {
+  return reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) - by);
+}
+
+void one_stats(jy_node* nd, u64 n) {
+  nd->stats[0] = nd->stats[1] = n;
+  nd->stats[2] = nd->stats[3] = 0;
+  nd->stats[4]++;
+}
+
+int32_t run_treg_one(jy_node* nd, u64 n, const uint8_t* kb, const u64* ko, const u64* ts, const uint8_t* vb,
+                     const u64* vo, int32_t mem) {
+  NdShard& sh = nd->sh[0];
+  ND_HIP(nd, hipSetDevice(sh.dev));
+  one_stats(nd, n);
+  if (n == 0) return JY_OK;
+  u64 w[4];
+  JY_TRY(values_dev_enqueue(nd, sh, vo, n, mem));
+  JY_TRY(readn(nd, sh, mem, {ko, ko + n, vo, vo + n}, w));
+  JY_TRY(values_dev_ok(nd, sh, mem));
+  const u64 k0 = w[0], k1 = w[1], v0 = w[2], v1 = w[3];
+  if (k1 < k0 || v1 < v0) return nd->fail(JY_EINVAL, "key or value offsets are not ascending");
+  const void *dkb, *dko, *dts, *dvo, *dvb;
+  ND_ENG(nd, sh, jy_stage_begin(sh.eng));
+  JY_TRY(stage(nd, sh, 0, on_host(mem) ? kb + k0 : kb, k1 - k0, mem, &dkb));
+  JY_TRY(stage(nd, sh, 1, ko, (n + 1) * 8, mem, &dko));
+  JY_TRY(stage(nd, sh, 2, ts, n * 8, mem, &dts));
+  JY_TRY(stage(nd, sh, 3, vo, (n + 1) * 8, mem, &dvo));
+  JY_TRY(stage(nd, sh, 4, on_host(mem) ? vb + v0 : vb, v1 - v0, mem, &dvb));
+  ND_ENG(nd, sh, jy_stage_end(sh.eng));
+  OneVals vals{n, static_cast<const u64*>(dvo), on_host(mem) ? v0 : 0, static_cast<const uint8_t*>(dvb)};
+  u32* slots;
+  u64 *pre, *lr;
+  JY_TRY(one_keys_values(nd, sh, JY_TREG, n, rebased(dkb, on_host(mem) ? k0 : 0), static_cast<const u64*>(dko),
+                         &vals, &slots, &pre, &lr));
+  ND_ENG(nd, sh, jy_treg_merge(sh.eng, n, slots, static_cast<const u64*>(dts), pre, lr));
+  return JY_OK;
+}
+
+int32_t run_counter_one(jy_node* nd, int32_t type, u64 n, const uint8_t* kb, const u64* ko, const u64* co,
+                        const uint8_t* sign, const u16* col, const u64* val, int32_t mem) {
+  NdShard& sh = nd->sh[0];
+  jy_engine* eng = sh.eng;
+  ND_HIP(nd, hipSetDevice(sh.dev));
+  one_stats(nd, n);
+  if (n == 0) return JY_OK;
+  u64 w[4];
+  JY_TRY(readn(nd, sh, mem, {ko, ko + n, co, co + n}, w));
+  const u64 k0 = w[0], k1 = w[1], c0 = w[2], c1 = w[3], nc = c1 - c0;
+  if (k1 < k0 || c1 < c0) return nd->fail(JY_EINVAL, "key or cell offsets are not ascending");
+  if (nc >= 0xFFFFFFFFull) return nd->fail(JY_ERANGE, "more than 2^32 - 1 cells in one call");
+  const u64 cb = on_host(mem) ? c0 : 0;  // staged cells start at c0; device cells are indexed from 0
+  const void *dkb, *dko, *dco, *dsg = nullptr, *dcol, *dval;
+  ND_ENG(nd, sh, jy_stage_begin(eng));
+  JY_TRY(stage(nd, sh, 0, on_host(mem) ? kb + k0 : kb, k1 - k0, mem, &dkb));
+  JY_TRY(stage(nd, sh, 1, ko, (n + 1) * 8, mem, &dko));
+  JY_TRY(stage(nd, sh, 2, co, (n + 1) * 8, mem, &dco));
+  if (sign) JY_TRY(stage(nd, sh, 3, sign + cb, nc, mem, &dsg));
+  JY_TRY(stage(nd, sh, 4, col + cb, nc * 2, mem, &dcol));
+  JY_TRY(stage(nd, sh, 5, val + cb, nc * 8, mem, &dval));
+  ND_ENG(nd, sh, jy_stage_end(eng));
+  const u64 cel = on_host(mem) ? 0 : c0;  // the batch's first cell in the staged columns
+  u64* rel;
+  u32* ckey;
+  JY_TRY(bufT(nd, sh, R_LOC0, n + 1, &rel));
+  JY_TRY(bufT(nd, sh, R_AUX0, std::max<u64>(nc, 1), &ckey));
+  hipLaunchKernelGGL(k_nd1_rebase, dim3(grid_of(n + 1)), dim3(kT), 0, eng->stream, n, static_cast<const u64*>(dco),
+                     rel);
+  ND_HIP(nd, hipGetLastError());
+  u32* slots;
+  JY_TRY(one_keys_values(nd, sh, type, n, rebased(dkb, on_host(mem) ? k0 : 0), static_cast<const u64*>(dko), nullptr,
+                         &slots, nullptr, nullptr));
+  if (nc == 0) return JY_OK;
+  ND_ENG(nd, sh, jy_seg_ids(eng, rel, n, nc, ckey));
+  const int which = type == JY_GCOUNT ? 0 : 1;
+  ND_ENG(nd, sh, jy_counter_grow(eng, which, jy_replica_count(eng), 0));
+  ND_ENG(nd, sh, jy_counter_coo_keyed(eng, which, nc, n, slots, ckey,
+                                      dsg ? static_cast<const uint8_t*>(dsg) + cel : nullptr,
+                                      static_cast<const u16*>(dcol) + cel, static_cast<const u64*>(dval) + cel));
+  return JY_OK;
+}
+
+int32_t run_tlog_one(jy_node* nd, u64 n, const uint8_t* kb, const u64* ko, const u64* cutoff, const u64* eo,
+                     const u64* ts, const uint8_t* vb, const u64* vo, int32_t mem) {
+  NdShard& sh = nd->sh[0];
+  jy_engine* eng = sh.eng;
+  ND_HIP(nd, hipSetDevice(sh.dev));
+  one_stats(nd, n);
+  if (n == 0) return JY_OK;
+  u64 w[4], v[2];
+  JY_TRY(readn(nd, sh, mem, {ko, ko + n, eo, eo + n}, w));
+  const u64 k0 = w[0], k1 = w[1], e0 = w[2], e1 = w[3], ne = e1 - e0;
+  if (k1 < k0 || e1 < e0) return nd->fail(JY_EINVAL, "key or entry offsets are not ascending");
+  if (ne >= 0xFFFFFFFFull) return nd->fail(JY_ERANGE, "more than 2^32 - 1 entries in one call");
+  JY_TRY(values_dev_enqueue(nd, sh, vo + e0, ne, mem));
+  JY_TRY(readn(nd, sh, mem, {vo + e0, vo + e1}, v));
+  JY_TRY(values_dev_ok(nd, sh, mem));
+  const u64 v0 = v[0], v1 = v[1];
+  if (v1 < v0) return nd->fail(JY_EINVAL, "value offsets are not ascending");
+  const u64 eb = on_host(mem) ? e0 : 0;
+  const void *dkb, *dko, *dcut, *deo, *dts, *dvo, *dvb;
+  ND_ENG(nd, sh, jy_stage_begin(eng));
+  JY_TRY(stage(nd, sh, 0, on_host(mem) ? kb + k0 : kb, k1 - k0, mem, &dkb));
+  JY_TRY(stage(nd, sh, 1, ko, (n + 1) * 8, mem, &dko));
+  JY_TRY(stage(nd, sh, 2, cutoff, n * 8, mem, &dcut));
+  JY_TRY(stage(nd, sh, 3, eo, (n + 1) * 8, mem, &deo));
+  JY_TRY(stage(nd, sh, 4, ts + eb, ne * 8, mem, &dts));
+  JY_TRY(stage(nd, sh, 5, vo + eb, (ne + 1) * 8, mem, &dvo));
+  JY_TRY(stage(nd, sh, 6, on_host(mem) ? vb + v0 : vb, v1 - v0, mem, &dvb));
+  ND_ENG(nd, sh, jy_stage_end(eng));
+  const u64 ent = on_host(mem) ? 0 : e0;  // the batch's first entry in the staged columns
+  u64* rel;
+  JY_TRY(bufT(nd, sh, R_LOC0, n + 1, &rel));
+  hipLaunchKernelGGL(k_nd1_rebase, dim3(grid_of(n + 1)), dim3(kT), 0, eng->stream, n, static_cast<const u64*>(deo),
+                     rel);
+  ND_HIP(nd, hipGetLastError());
+  OneVals vals{ne, static_cast<const u64*>(dvo) + ent, on_host(mem) ? v0 : 0, static_cast<const uint8_t*>(dvb)};
+  u32* slots;
+  u64 *pre, *lr;
+  JY_TRY(one_keys_values(nd, sh, JY_TLOG, n, rebased(dkb, on_host(mem) ? k0 : 0), static_cast<const u64*>(dko),
+                         &vals, &slots, &pre, &lr));
+  ND_ENG(nd, sh, jy_tlog_merge(eng, n, slots, static_cast<const u64*>(dcut), rel, ne,
+                               static_cast<const u64*>(dts) + ent, pre, lr));
+  return JY_OK;
+}
+
+int32_t run_ujson_one(jy_node* nd, u64 n, const uint8_t* kb, const u64* ko, const u64* eo, const u64* dots,
+                      const u64* elems, const u64* vvo, const u64* vv, const u64* clo, const u64* cloud,
+                      int32_t mem) {
+  NdShard& sh = nd->sh[0];
+  jy_engine* eng = sh.eng;
+  ND_HIP(nd, hipSetDevice(sh.dev));
+  one_stats(nd, n);
+  if (n == 0) return JY_OK;
+  u64 w[8];
+  JY_TRY(readn(nd, sh, mem, {ko, ko + n, eo, eo + n, vvo, vvo + n, clo, clo + n}, w));
+  const u64 k0 = w[0], k1 = w[1];
+  if (k1 < k0 || w[3] < w[2] || w[5] < w[4] || w[7] < w[6])
+    return nd->fail(JY_EINVAL, "key / element / vv / cloud offsets are not ascending");
+  const u64 lo[3] = {w[2], w[4], w[6]}, cnt[3] = {w[3] - w[2], w[5] - w[4], w[7] - w[6]};
+  const u64 hb[3] = {on_host(mem) ? lo[0] : 0, on_host(mem) ? lo[1] : 0, on_host(mem) ? lo[2] : 0};
+  const void *dkb, *dko, *deo, *dd, *de, *dvo, *dv, *dco, *dc;
+  ND_ENG(nd, sh, jy_stage_begin(eng));
+  JY_TRY(stage(nd, sh, 0, on_host(mem) ? kb + k0 : kb, k1 - k0, mem, &dkb));
+  JY_TRY(stage(nd, sh, 1, ko, (n + 1) * 8, mem, &dko));
+  JY_TRY(stage(nd, sh, 2, eo, (n + 1) * 8, mem, &deo));
+  JY_TRY(stage(nd, sh, 3, dots + hb[0], cnt[0] * 8, mem, &dd));
+  JY_TRY(stage(nd, sh, 4, elems + hb[0], cnt[0] * 8, mem, &de));
+  JY_TRY(stage(nd, sh, 5, vvo, (n + 1) * 8, mem, &dvo));
+  JY_TRY(stage(nd, sh, 6, vv + hb[1], cnt[1] * 8, mem, &dv));
+  JY_TRY(stage(nd, sh, 7, clo, (n + 1) * 8, mem, &dco));
+  JY_TRY(stage(nd, sh, 8, cloud + hb[2], cnt[2] * 8, mem, &dc));
+  ND_ENG(nd, sh, jy_stage_end(eng));
+  const void* offs[3] = {deo, dvo, dco};
+  u64* rel[3];
+  for (int l = 0; l < 3; l++) {
+    JY_TRY(bufT(nd, sh, R_LOC0 + l, n + 1, &rel[l]));
+    hipLaunchKernelGGL(k_nd1_rebase, dim3(grid_of(n + 1)), dim3(kT), 0, eng->stream, n,
+                       static_cast<const u64*>(offs[l]), rel[l]);
+  }
+  ND_HIP(nd, hipGetLastError());
+  u32* slots;
+  JY_TRY(one_keys_values(nd, sh, JY_UJSON, n, rebased(dkb, on_host(mem) ? k0 : 0), static_cast<const u64*>(dko),
+                         nullptr, &slots, nullptr, nullptr));
+  const u64 f[3] = {on_host(mem) ? 0 : lo[0], on_host(mem) ? 0 : lo[1], on_host(mem) ? 0 : lo[2]};
+  ND_ENG(nd, sh, jy_ujson_merge(eng, n, slots, rel[0], cnt[0], static_cast<const u64*>(dd) + f[0],
+                                static_cast<const u64*>(de) + f[0], rel[1], cnt[1], static_cast<const u64*>(dv) + f[1],
+                                rel[2], cnt[2], static_cast<const u64*>(dc) + f[2]));
+  return JY_OK;
+}
+
 // ---- TREG: key bytes | ts, pre, vlen | long value bytes ----
-int32_t jy_node_treg_converge(jy_node* nd, uint64_t n, const uint8_t* kb, const uint64_t* ko, const uint64_t* ts,
-                              const uint8_t* vb, const uint64_t* vo, int32_t mem) {
-  JY_TRY(node_check(nd, mem, n));
+int32_t run_treg(jy_node* nd, uint64_t n, const uint8_t* kb, const uint64_t* ko, const uint64_t* ts, const uint8_t* vb,
+                 const uint64_t* vo, int32_t mem) {
+  if (nd->S == 1 && !nd->regroup_one) return run_treg_one(nd, n, kb, ko, ts, vb, vo, mem);
   std::vector<u64> at;
   split(nd, n, at);
   nd->stats[0] = n;
@@ -997,14 +1475,16 @@ int32_t jy_node_treg_converge(jy_node* nd, uint64_t n, const uint8_t* kb, const 
     const u64 a = at[L], m = sh.n;
     u64 v0, v1;
     JY_TRY(values_check(nd, vo, a, at[L + 1], mem));
+    JY_TRY(values_dev_enqueue(nd, sh, vo + a, m, mem));
     JY_TRY(read2(nd, sh, vo + a, vo + at[L + 1], mem, v0, v1));
+    JY_TRY(values_dev_ok(nd, sh, mem));
     const void *dts, *dvo, *dvb;
     JY_TRY(stage(nd, sh, 2, ts + a, m * 8, mem, &dts));
     JY_TRY(stage(nd, sh, 3, vo + a, (m + 1) * 8, mem, &dvo));
-    JY_TRY(stage(nd, sh, 4, mem == JY_HOST ? vb + v0 : vb, v1 - v0, mem, &dvb));
+    JY_TRY(stage(nd, sh, 4, on_host(mem) ? vb + v0 : vb, v1 - v0, mem, &dvb));
     ND_ENG(nd, sh, jy_stage_end(sh.eng));
     JY_TRY(ingest_keys(nd, sh, in));
-    const u64 vbase = mem == JY_HOST ? v0 : 0;
+    const u64 vbase = on_host(mem) ? v0 : 0;
     JY_TRY(ingest_fixed<1>(nd, sh, InU64<1>{{static_cast<const u64*>(dts)}}));
     u64 *pre, *vlen;
     JY_TRY(bufT(nd, sh, B_F1, std::max<u64>(m, 1), &pre));
@@ -1040,12 +1520,9 @@ int32_t jy_node_treg_converge(jy_node* nd, uint64_t n, const uint8_t* kb, const 
 }
 
 // ---- counters: key bytes | cell count | cells (sign << 16 | col, val) ----
-int32_t jy_node_counter_converge(jy_node* nd, int32_t type, uint64_t n, const uint8_t* kb, const uint64_t* ko,
-                                 const uint64_t* co, const uint8_t* sign, const uint16_t* col, const uint64_t* val,
-                                 int32_t mem) {
-  JY_TRY(node_check(nd, mem, n));
-  if (type != JY_GCOUNT && type != JY_PNCOUNT) return nd->fail(JY_EINVAL, "type must be JY_GCOUNT or JY_PNCOUNT");
-  if (type == JY_GCOUNT && sign) return nd->fail(JY_EINVAL, "GCOUNT cells have no sign");
+int32_t run_counter(jy_node* nd, int32_t type, uint64_t n, const uint8_t* kb, const uint64_t* ko, const uint64_t* co,
+                    const uint8_t* sign, const uint16_t* col, const uint64_t* val, int32_t mem) {
+  if (nd->S == 1 && !nd->regroup_one) return run_counter_one(nd, type, n, kb, ko, co, sign, col, val, mem);
   std::vector<u64> at;
   split(nd, n, at);
   nd->stats[0] = n;
@@ -1061,14 +1538,14 @@ int32_t jy_node_counter_converge(jy_node* nd, int32_t type, uint64_t n, const ui
     u64 c0, c1;
     JY_TRY(read2(nd, sh, co + a, co + at[L + 1], mem, c0, c1));
     if (c1 < c0) return nd->fail(JY_EINVAL, "cell offsets are not ascending");
-    if (mem == JY_HOST) {
+    if (mem == JY_HOST) {  // (kPinned: checked by the call)
       const u32 nrep = jy_replica_count(sh.eng);
       for (u64 c = c0; c < c1; c++) {
         if (col[c] >= nrep) return nd->fail(JY_ERANGE, "column names no registered replica");
         if (sign && sign[c] > 1) return nd->fail(JY_ERANGE, "sign must be 0 (P) or 1 (N)");
       }
     }
-    const u64 cb = mem == JY_HOST ? c0 : 0;
+    const u64 cb = on_host(mem) ? c0 : 0;
     const void *dco, *dsg = nullptr, *dcol, *dval;
     JY_TRY(stage(nd, sh, 2, co + a, (m + 1) * 8, mem, &dco));
     if (sign) JY_TRY(stage(nd, sh, 3, sign + cb, c1 - c0, mem, &dsg));
@@ -1117,10 +1594,9 @@ int32_t jy_node_counter_converge(jy_node* nd, int32_t type, uint64_t n, const ui
 }
 
 // ---- TLOG: key bytes | cutoff, entry count | entries (ts, pre, vlen) | long value bytes ----
-int32_t jy_node_tlog_converge(jy_node* nd, uint64_t n, const uint8_t* kb, const uint64_t* ko, const uint64_t* cutoff,
-                              const uint64_t* eo, const uint64_t* ts, const uint8_t* vb, const uint64_t* vo,
-                              int32_t mem) {
-  JY_TRY(node_check(nd, mem, n));
+int32_t run_tlog(jy_node* nd, uint64_t n, const uint8_t* kb, const uint64_t* ko, const uint64_t* cutoff, const uint64_t* eo,
+                 const uint64_t* ts, const uint8_t* vb, const uint64_t* vo, int32_t mem) {
+  if (nd->S == 1 && !nd->regroup_one) return run_tlog_one(nd, n, kb, ko, cutoff, eo, ts, vb, vo, mem);
   std::vector<u64> at;
   split(nd, n, at);
   nd->stats[0] = n;
@@ -1138,15 +1614,17 @@ int32_t jy_node_tlog_converge(jy_node* nd, uint64_t n, const uint8_t* kb, const 
     if (e1 < e0) return nd->fail(JY_EINVAL, "entry offsets are not ascending");
     if (e1 - e0 >= 0xFFFFFFFFull) return nd->fail(JY_ERANGE, "more than 2^32 - 1 entries in one shard's range");
     JY_TRY(values_check(nd, vo, e0, e1, mem));
+    JY_TRY(values_dev_enqueue(nd, sh, vo + e0, e1 - e0, mem));
     JY_TRY(read2(nd, sh, vo + e0, vo + e1, mem, v0, v1));
+    JY_TRY(values_dev_ok(nd, sh, mem));
     if (v1 < v0) return nd->fail(JY_EINVAL, "value offsets are not ascending");
-    const u64 eb = mem == JY_HOST ? e0 : 0, vbase = mem == JY_HOST ? v0 : 0;
+    const u64 eb = on_host(mem) ? e0 : 0, vbase = on_host(mem) ? v0 : 0;
     const void *dcut, *deo, *dts, *dvo, *dvb;
     JY_TRY(stage(nd, sh, 2, cutoff + a, m * 8, mem, &dcut));
     JY_TRY(stage(nd, sh, 3, eo + a, (m + 1) * 8, mem, &deo));
     JY_TRY(stage(nd, sh, 4, ts + eb, (e1 - e0) * 8, mem, &dts));
     JY_TRY(stage(nd, sh, 5, vo + eb, (e1 - e0 + 1) * 8, mem, &dvo));
-    JY_TRY(stage(nd, sh, 6, mem == JY_HOST ? vb + v0 : vb, v1 - v0, mem, &dvb));
+    JY_TRY(stage(nd, sh, 6, on_host(mem) ? vb + v0 : vb, v1 - v0, mem, &dvb));
     ND_ENG(nd, sh, jy_stage_end(sh.eng));
     JY_TRY(ingest_keys(nd, sh, in));
     JY_TRY(ingest_fixed<1>(nd, sh, InU64<1>{{static_cast<const u64*>(dcut)}}));
@@ -1205,10 +1683,11 @@ int32_t jy_node_tlog_converge(jy_node* nd, uint64_t n, const uint8_t* kb, const 
 }
 
 // ---- UJSON: key bytes | element, vv, cloud counts | (dots, elems), vv, cloud ----
-int32_t jy_node_ujson_converge(jy_node* nd, uint64_t n, const uint8_t* kb, const uint64_t* ko, const uint64_t* eo,
-                               const uint64_t* dots, const uint64_t* elems, const uint64_t* vvo, const uint64_t* vv,
-                               const uint64_t* clo, const uint64_t* cloud, int32_t mem) {
-  JY_TRY(node_check(nd, mem, n));
+int32_t run_ujson(jy_node* nd, uint64_t n, const uint8_t* kb, const uint64_t* ko, const uint64_t* eo, const uint64_t* dots,
+                  const uint64_t* elems, const uint64_t* vvo, const uint64_t* vv, const uint64_t* clo,
+                  const uint64_t* cloud, int32_t mem) {
+  if (nd->S == 1 && !nd->regroup_one)
+    return run_ujson_one(nd, n, kb, ko, eo, dots, elems, vvo, vv, clo, cloud, mem);
   std::vector<u64> at;
   split(nd, n, at);
   nd->stats[0] = n;
@@ -1228,7 +1707,7 @@ int32_t jy_node_ujson_converge(jy_node* nd, uint64_t n, const uint8_t* kb, const
       if (hi[l] < lo[l]) return nd->fail(JY_EINVAL, "element / vv / cloud offsets are not ascending");
     }
     const void *deo, *dd, *de, *dvo, *dv, *dco, *dc;
-    const u64 b0 = mem == JY_HOST ? lo[0] : 0, b1 = mem == JY_HOST ? lo[1] : 0, b2 = mem == JY_HOST ? lo[2] : 0;
+    const u64 b0 = on_host(mem) ? lo[0] : 0, b1 = on_host(mem) ? lo[1] : 0, b2 = on_host(mem) ? lo[2] : 0;
     JY_TRY(stage(nd, sh, 2, eo + a, (m + 1) * 8, mem, &deo));
     JY_TRY(stage(nd, sh, 3, dots + b0, (hi[0] - lo[0]) * 8, mem, &dd));
     JY_TRY(stage(nd, sh, 4, elems + b0, (hi[0] - lo[0]) * 8, mem, &de));
@@ -1283,12 +1762,8 @@ int32_t jy_node_ujson_converge(jy_node* nd, uint64_t n, const uint8_t* kb, const
 }
 
 // ---- dense counter blocks arriving mixed ----
-int32_t jy_node_counter_converge_block(jy_node* nd, int32_t type, uint32_t ncols, const uint16_t* cols_all,
-                                       uint32_t slot0, uint32_t nslots, const uint64_t* vals_p,
-                                       const uint64_t* vals_n) {
-  if (!nd) return JY_EINVAL;
-  if (type != JY_GCOUNT && type != JY_PNCOUNT) return nd->fail(JY_EINVAL, "type must be JY_GCOUNT or JY_PNCOUNT");
-  if ((type == JY_PNCOUNT) != (vals_n != nullptr)) return nd->fail(JY_EINVAL, "vals_n is given iff PNCOUNT");
+int32_t run_block(jy_node* nd, int32_t type, uint32_t ncols, const uint16_t* cols_all, uint32_t slot0, uint32_t nslots,
+                  const uint64_t* vals_p, const uint64_t* vals_n) {
   const u32 S = nd->S, G = type == JY_PNCOUNT ? 2 : 1;
   if (ncols == 0 || nslots == 0) return JY_OK;
   const u64 blk = (u64)nslots;                // words of one (column, owner) block
@@ -1324,7 +1799,8 @@ int32_t jy_node_counter_converge_block(jy_node* nd, int32_t type, uint32_t ncols
         ND_HIP(nd, hipStreamWaitEvent(sh.xs, sh.ev_m[k], 0));  // merge c - 2 has read this buffer
       }
     if (So && nd->fabric == JY_FABRIC_RCCL) {
-      ND_NCCL(nd, ncclGroupStart());
+      NcclGroup grp;  // ends the group on every return
+      ND_NCCL(nd, grp.start());
       for (u32 L = 0; L < nd->nlocal; L++) {
         NdShard& sh = nd->sh[L];
         u64* rb = static_cast<u64*>(sh.b[X_BUF0 + k].p);
@@ -1337,7 +1813,7 @@ int32_t jy_node_counter_converge_block(jy_node* nd, int32_t type, uint32_t ncols
           }
         }
       }
-      ND_NCCL(nd, ncclGroupEnd());
+      ND_NCCL(nd, grp.end());
     } else if (So) {
       // every source's input must be ready before a destination pulls it
       for (NdShard& sh : nd->sh) ND_HIP(nd, hipEventRecord(sh.ev_in, sh.xs));
@@ -1382,8 +1858,406 @@ int32_t jy_node_counter_converge_block(jy_node* nd, int32_t type, uint32_t ncols
       ND_HIP(nd, hipEventRecord(sh.ev_m[k], sh.eng->stream));
     }
   }
+  if (So && nd->fabric == JY_FABRIC_COPY) {
+    // a destination's pulls read the other shards' inputs on its exchange
+    // stream: every shard's engine stream (the one a caller syncs or reuses
+    // its input on) waits for every destination's last pull
+    for (NdShard& dst : nd->sh) {
+      ND_HIP(nd, hipSetDevice(dst.dev));
+      ND_HIP(nd, hipEventRecord(dst.ev_out, dst.xs));
+    }
+    for (NdShard& src : nd->sh) {
+      ND_HIP(nd, hipSetDevice(src.dev));
+      for (NdShard& dst : nd->sh) ND_HIP(nd, hipStreamWaitEvent(src.eng->stream, dst.ev_out, 0));
+    }
+  }
   nd->stats[4] += ncols;
   return JY_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// the executor
+
+namespace {
+
+int32_t run_job(jy_node* nd, const NdJob& j) {
+  const int32_t mem = j.mem == JY_HOST ? kPinned : j.mem;
+  const auto U8 = [&](int i) { return static_cast<const uint8_t*>(j.a[i]); };
+  const auto U64 = [&](int i) { return static_cast<const u64*>(j.a[i]); };
+  switch (j.kind) {
+    case K_COUNTER:
+      return run_counter(nd, j.type, j.n, U8(0), U64(1), U64(2), U8(3), static_cast<const u16*>(j.a[4]), U64(5), mem);
+    case K_TREG:
+      return run_treg(nd, j.n, U8(0), U64(1), U64(2), U8(3), U64(4), mem);
+    case K_TLOG:
+      return run_tlog(nd, j.n, U8(0), U64(1), U64(2), U64(3), U64(4), U8(5), U64(6), mem);
+    case K_UJSON:
+      return run_ujson(nd, j.n, U8(0), U64(1), U64(2), U64(3), U64(4), U64(5), U64(6), U64(7), U64(8), mem);
+    case K_BLOCK:
+      return run_block(nd, j.type, j.ncols, j.cols.data(), j.slot0, j.nslots, U64(0), U64(1));
+  }
+  return nd->fail(JY_EINVAL, "unknown node job");
+}
+
+// one job, under the node lock: its pinned block is released with events
+// that fire once the job's DMAs out of it are done
+int32_t run_locked(jy_node* nd, const NdJob& j) {
+  int32_t rc = run_job(nd, j);
+  if (j.pin >= 0) {
+    NdPin& pb = nd->pins[j.pin];
+    for (u32 L = 0; L < nd->nlocal; L++) {
+      NdShard& sh = nd->sh[L];
+      hipSetDevice(sh.dev);
+      if (rc != JY_OK) hipStreamSynchronize(sh.eng->stream);  // a failed job's staging may be in flight
+      else if (hipEventRecord(pb.ev[L], sh.eng->stream) != hipSuccess) {
+        hipStreamSynchronize(sh.eng->stream);
+        hipEventRecord(pb.ev[L], nullptr);
+      }
+    }
+  }
+  return rc;
+}
+
+void finish(jy_node* nd, const NdJob& j, int32_t rc) {
+  std::lock_guard<std::mutex> lk(nd->qmu);
+  if (j.pin >= 0) nd->pins[j.pin].busy = false;
+  if (rc != JY_OK && nd->aerr == JY_OK) {
+    nd->aerr = rc;
+    nd->aerr_msg = std::this_thread::get_id() == nd->wid ? nd->werr : nd->err;
+  }
+  nd->finished++;
+  nd->dcv.notify_all();
+}
+
+void worker_loop(jy_node* nd) {
+  for (;;) {
+    NdJob j;
+    {
+      std::unique_lock<std::mutex> lk(nd->qmu);
+      nd->qcv.wait(lk, [&] { return nd->stop || !nd->q.empty(); });
+      if (nd->q.empty()) return;  // stop, and nothing left
+      j = std::move(nd->q.front());
+      nd->q.pop_front();
+    }
+    int32_t rc;
+    {
+      std::lock_guard<std::mutex> g(nd->mu);
+      rc = run_locked(nd, j);
+    }
+    finish(nd, j, rc);
+  }
+}
+
+void exec_start(jy_node* nd) {
+  const char* e = std::getenv("JY_NODE_INLINE");
+  nd->inline_jobs = e && *e && *e != '0';
+  const char* r = std::getenv("JY_NODE_REGROUP_ONE");
+  nd->regroup_one = r && *r && *r != '0';
+  if (nd->inline_jobs) return;
+  nd->worker = std::thread([nd] { worker_loop(nd); });
+  nd->wid = nd->worker.get_id();
+}
+
+void exec_stop(jy_node* nd) {
+  if (!nd->worker.joinable()) return;
+  {
+    std::lock_guard<std::mutex> lk(nd->qmu);
+    nd->stop = true;
+  }
+  nd->qcv.notify_all();
+  nd->worker.join();
+}
+
+// every job queued so far has been issued; then the first failure of a
+// queued job since the last report, if any (moved to jy_node_last_error)
+int32_t exec_fence(jy_node* nd) {
+  std::unique_lock<std::mutex> lk(nd->qmu);
+  nd->dcv.wait(lk, [&] { return nd->finished == nd->submitted; });
+  if (nd->aerr == JY_OK) return JY_OK;
+  const int32_t rc = nd->aerr;
+  nd->err = nd->aerr_msg;
+  nd->aerr = JY_OK;
+  return rc;
+}
+
+// a failure a queued job left behind, reported without waiting
+int32_t exec_pending(jy_node* nd) {
+  std::lock_guard<std::mutex> lk(nd->qmu);
+  if (nd->aerr == JY_OK) return JY_OK;
+  const int32_t rc = nd->aerr;
+  nd->err = nd->aerr_msg;
+  nd->aerr = JY_OK;
+  return rc;
+}
+
+// ---- packing host inputs into a pinned block ----
+struct Pack {
+  struct Arr {
+    const void* src;  // the caller's array (index 0 = element 0)
+    u64 esize, lo, hi;  // elements [lo, hi) are read
+    int slot;           // NdJob::a index
+  };
+  std::vector<Arr> arr;
+  void add(int slot, const void* src, u64 esize, u64 lo, u64 hi) { arr.push_back({src, esize, lo, hi, slot}); }
+};
+
+// a free pinned block of at least `bytes` (waits while every block is busy,
+// then for the DMAs of its previous job)
+int32_t pin_acquire(jy_node* nd, u64 bytes, int* out) {
+  int b = -1;
+  {
+    std::unique_lock<std::mutex> lk(nd->qmu);
+    nd->dcv.wait(lk, [&] {
+      for (int i = 0; i < kJobDepth; i++)
+        if (!nd->pins[i].busy) return true;
+      return false;
+    });
+    for (int i = 0; i < kJobDepth && b < 0; i++)
+      if (!nd->pins[i].busy) b = i;
+    nd->pins[b].busy = true;
+  }
+  NdPin& pb = nd->pins[b];
+  auto release = [&](int32_t rc) {
+    std::lock_guard<std::mutex> lk(nd->qmu);
+    pb.busy = false;
+    nd->dcv.notify_all();
+    return rc;
+  };
+  if (pb.ev.empty()) {
+    pb.ev.assign(nd->nlocal, nullptr);
+    for (u32 L = 0; L < nd->nlocal; L++) {
+      hipSetDevice(nd->sh[L].dev);
+      if (hipEventCreateWithFlags(&pb.ev[L], hipEventDisableTiming) != hipSuccess ||
+          hipEventRecord(pb.ev[L], nullptr) != hipSuccess)
+        return release(nd->fail(JY_EHIP, "node: pinned block events"));
+    }
+  }
+  for (hipEvent_t e : pb.ev)
+    if (hipEventSynchronize(e) != hipSuccess) return release(nd->fail(JY_EHIP, "node: pinned block wait"));
+  if (pb.bytes < bytes) {
+    if (pb.p) hipHostFree(pb.p);
+    pb.p = nullptr;
+    pb.bytes = 0;
+    const u64 nb = std::max<u64>((bytes + bytes / 4 + 4095) & ~4095ull, 1 << 20);
+    if (hipHostMalloc(&pb.p, nb, hipHostMallocDefault) != hipSuccess)
+      return release(nd->fail(JY_EHIP, "node: hipHostMalloc of the pinned input block"));
+    pb.bytes = nb;
+  }
+  *out = b;
+  return JY_OK;
+}
+
+// copy every array's read range into one pinned block; the job's pointers
+// are rebased so that the original indices (offsets above 0 included) work
+int32_t pack_host(jy_node* nd, const Pack& pk, NdJob& j) {
+  u64 total = 0;
+  for (const Pack::Arr& a : pk.arr) total = round8(total) + (a.hi - a.lo) * a.esize + 8;
+  int b;
+  JY_TRY(pin_acquire(nd, total, &b));
+  j.pin = b;
+  uint8_t* base = static_cast<uint8_t*>(nd->pins[b].p);
+  u64 at = 0;
+  for (const Pack::Arr& a : pk.arr) {
+    at = round8(at);
+    const u64 nb = (a.hi - a.lo) * a.esize;
+    if (nb) jy_copy_host(base + at, static_cast<const uint8_t*>(a.src) + a.lo * a.esize, nb);
+    // element lo lives at base + at
+    j.a[a.slot] = reinterpret_cast<const void*>(reinterpret_cast<uintptr_t>(base + at) - a.lo * a.esize);
+    at += nb + 8;
+  }
+  return JY_OK;
+}
+
+int32_t submit(jy_node* nd, NdJob&& j) {
+  if (nd->inline_jobs) {
+    int32_t rc;
+    {
+      std::lock_guard<std::mutex> g(nd->mu);
+      rc = run_locked(nd, j);
+    }
+    {
+      std::lock_guard<std::mutex> lk(nd->qmu);
+      nd->submitted++;
+    }
+    finish(nd, j, JY_OK);
+    return rc;
+  }
+  {
+    std::lock_guard<std::mutex> lk(nd->qmu);
+    nd->q.push_back(std::move(j));
+    nd->submitted++;
+  }
+  nd->qcv.notify_one();
+  return JY_OK;
+}
+
+// the public entry's checks common to every converge (a queued job's earlier
+// failure is reported here first)
+int32_t call_check(jy_node* nd, int32_t mem, u64 n) {
+  JY_TRY(node_check(nd, mem, n));
+  return exec_pending(nd);
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t jy_node_counter_converge(jy_node* nd, int32_t type, uint64_t n, const uint8_t* kb, const uint64_t* ko,
+                                 const uint64_t* co, const uint8_t* sign, const uint16_t* col, const uint64_t* val,
+                                 int32_t mem) {
+  JY_TRY(call_check(nd, mem, n));
+  if (type != JY_GCOUNT && type != JY_PNCOUNT) return nd->fail(JY_EINVAL, "type must be JY_GCOUNT or JY_PNCOUNT");
+  if (type == JY_GCOUNT && sign) return nd->fail(JY_EINVAL, "GCOUNT cells have no sign");
+  NdJob j;
+  j.kind = K_COUNTER;
+  j.type = type;
+  j.n = n;
+  j.mem = mem;
+  if (mem == JY_DEVICE) {
+    const void* a[6] = {kb, ko, co, sign, col, val};
+    std::copy(a, a + 6, j.a);
+    return submit(nd, std::move(j));
+  }
+  if (ko[n] < ko[0]) return nd->fail(JY_EINVAL, "key offsets are not ascending");
+  if (co[n] < co[0]) return nd->fail(JY_EINVAL, "cell offsets are not ascending");
+  u32 nrep;
+  {
+    std::lock_guard<std::mutex> g(nd->mu);
+    nrep = nd->nrep;
+  }
+  for (u64 c = co[0]; c < co[n]; c++) {
+    if (col[c] >= nrep) return nd->fail(JY_ERANGE, "column names no registered replica");
+    if (sign && sign[c] > 1) return nd->fail(JY_ERANGE, "sign must be 0 (P) or 1 (N)");
+  }
+  Pack pk;
+  pk.add(0, kb, 1, ko[0], ko[n]);
+  pk.add(1, ko, 8, 0, n + 1);
+  pk.add(2, co, 8, 0, n + 1);
+  if (sign) pk.add(3, sign, 1, co[0], co[n]);
+  pk.add(4, col, 2, co[0], co[n]);
+  pk.add(5, val, 8, co[0], co[n]);
+  JY_TRY(pack_host(nd, pk, j));
+  return submit(nd, std::move(j));
+}
+
+int32_t jy_node_treg_converge(jy_node* nd, uint64_t n, const uint8_t* kb, const uint64_t* ko, const uint64_t* ts,
+                              const uint8_t* vb, const uint64_t* vo, int32_t mem) {
+  JY_TRY(call_check(nd, mem, n));
+  NdJob j;
+  j.kind = K_TREG;
+  j.n = n;
+  j.mem = mem;
+  if (mem == JY_DEVICE) {
+    const void* a[5] = {kb, ko, ts, vb, vo};
+    std::copy(a, a + 5, j.a);
+    return submit(nd, std::move(j));
+  }
+  if (ko[n] < ko[0]) return nd->fail(JY_EINVAL, "key offsets are not ascending");
+  JY_TRY(values_check(nd, vo, 0, n, JY_HOST));
+  Pack pk;
+  pk.add(0, kb, 1, ko[0], ko[n]);
+  pk.add(1, ko, 8, 0, n + 1);
+  pk.add(2, ts, 8, 0, n);
+  pk.add(3, vb, 1, vo[0], vo[n]);
+  pk.add(4, vo, 8, 0, n + 1);
+  JY_TRY(pack_host(nd, pk, j));
+  return submit(nd, std::move(j));
+}
+
+int32_t jy_node_tlog_converge(jy_node* nd, uint64_t n, const uint8_t* kb, const uint64_t* ko, const uint64_t* cutoff,
+                              const uint64_t* eo, const uint64_t* ts, const uint8_t* vb, const uint64_t* vo,
+                              int32_t mem) {
+  JY_TRY(call_check(nd, mem, n));
+  NdJob j;
+  j.kind = K_TLOG;
+  j.n = n;
+  j.mem = mem;
+  if (mem == JY_DEVICE) {
+    const void* a[7] = {kb, ko, cutoff, eo, ts, vb, vo};
+    std::copy(a, a + 7, j.a);
+    return submit(nd, std::move(j));
+  }
+  if (ko[n] < ko[0]) return nd->fail(JY_EINVAL, "key offsets are not ascending");
+  if (eo[n] < eo[0]) return nd->fail(JY_EINVAL, "entry offsets are not ascending");
+  JY_TRY(values_check(nd, vo, eo[0], eo[n], JY_HOST));
+  Pack pk;
+  pk.add(0, kb, 1, ko[0], ko[n]);
+  pk.add(1, ko, 8, 0, n + 1);
+  pk.add(2, cutoff, 8, 0, n);
+  pk.add(3, eo, 8, 0, n + 1);
+  pk.add(4, ts, 8, eo[0], eo[n]);
+  pk.add(5, vb, 1, vo[eo[0]], vo[eo[n]]);
+  pk.add(6, vo, 8, eo[0], eo[n] + 1);
+  JY_TRY(pack_host(nd, pk, j));
+  return submit(nd, std::move(j));
+}
+
+int32_t jy_node_ujson_converge(jy_node* nd, uint64_t n, const uint8_t* kb, const uint64_t* ko, const uint64_t* eo,
+                               const uint64_t* dots, const uint64_t* elems, const uint64_t* vvo, const uint64_t* vv,
+                               const uint64_t* clo, const uint64_t* cloud, int32_t mem) {
+  JY_TRY(call_check(nd, mem, n));
+  NdJob j;
+  j.kind = K_UJSON;
+  j.n = n;
+  j.mem = mem;
+  if (mem == JY_DEVICE) {
+    const void* a[9] = {kb, ko, eo, dots, elems, vvo, vv, clo, cloud};
+    std::copy(a, a + 9, j.a);
+    return submit(nd, std::move(j));
+  }
+  if (ko[n] < ko[0]) return nd->fail(JY_EINVAL, "key offsets are not ascending");
+  if (eo[n] < eo[0] || vvo[n] < vvo[0] || clo[n] < clo[0])
+    return nd->fail(JY_EINVAL, "element / vv / cloud offsets are not ascending");
+  Pack pk;
+  pk.add(0, kb, 1, ko[0], ko[n]);
+  pk.add(1, ko, 8, 0, n + 1);
+  pk.add(2, eo, 8, 0, n + 1);
+  pk.add(3, dots, 8, eo[0], eo[n]);
+  pk.add(4, elems, 8, eo[0], eo[n]);
+  pk.add(5, vvo, 8, 0, n + 1);
+  pk.add(6, vv, 8, vvo[0], vvo[n]);
+  pk.add(7, clo, 8, 0, n + 1);
+  pk.add(8, cloud, 8, clo[0], clo[n]);
+  JY_TRY(pack_host(nd, pk, j));
+  return submit(nd, std::move(j));
+}
+
+int32_t jy_node_counter_converge_block(jy_node* nd, int32_t type, uint32_t ncols, const uint16_t* cols_all,
+                                       uint32_t slot0, uint32_t nslots, const uint64_t* vals_p,
+                                       const uint64_t* vals_n) {
+  if (!nd) return JY_EINVAL;
+  JY_TRY(exec_pending(nd));
+  if (type != JY_GCOUNT && type != JY_PNCOUNT) return nd->fail(JY_EINVAL, "type must be JY_GCOUNT or JY_PNCOUNT");
+  if ((type == JY_PNCOUNT) != (vals_n != nullptr)) return nd->fail(JY_EINVAL, "vals_n is given iff PNCOUNT");
+  if (ncols == 0 || nslots == 0) return JY_OK;
+  NdJob j;
+  j.kind = K_BLOCK;
+  j.type = type;
+  j.ncols = ncols;
+  j.slot0 = slot0;
+  j.nslots = nslots;
+  j.cols.assign(cols_all, cols_all + (u64)nd->S * ncols);
+  j.a[0] = vals_p;
+  j.a[1] = vals_n;
+  return submit(nd, std::move(j));
+}
+
+int32_t jy_node_fence(jy_node* nd) {
+  if (!nd) return JY_EINVAL;
+  return exec_fence(nd);
+}
+
+int32_t jy_node_lock(jy_node* nd) {
+  if (!nd) return JY_EINVAL;
+  const int32_t rc = exec_fence(nd);
+  nd->mu.lock();
+  return rc;
+}
+
+void jy_node_unlock(jy_node* nd) {
+  if (nd) nd->mu.unlock();
 }
 
 }  // extern "C"

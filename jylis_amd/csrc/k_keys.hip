@@ -9,9 +9,14 @@
 //   kref[slot]   (byte offset << 24) | length
 //   khash[slot]  64-bit table hash (kept for rehashing)
 //   table[tcap]  open addressing, linear probing, tcap a power of two kept
-//                >= 2x the keys: entry = tag32 << 32 | slot, EMPTY = ~0.
-//                The slot position is the top bits of the hash, the tag its
-//                low 32 bits, so most probes of a foreign key stop at the tag.
+//                >= 2x the keys: a 32-B record {tag32 << 32 | slot, length,
+//                key bytes 0..7, key bytes 8..15} (EMPTY: e = ~0).  The slot
+//                position is the top bits of the hash, the tag its low 32
+//                bits.  A key of up to 16 bytes is found with ONE dependent
+//                access -- its record -- instead of three (entry, the slot's
+//                kref, the directory's bytes: 350 us for 8.39M keys of the
+//                node TREG call, round 5); longer keys compare the rest of
+//                their bytes in the directory.
 //
 // Interning n keys is deterministic and lock-free (no thread ever waits on
 // another):
@@ -27,9 +32,9 @@
 //   K4 commit     slot = old count + rank; first occurrences copy their bytes
 //                 and fill kref / khash; claimers turn PENDING into final
 //
-// Roofline: HBM/latency.  Per key: its bytes read twice (hash, compare), one
-// table probe chain (8 B entries), 4 B slot out; a new key adds its bytes +
-// 16 B written.
+// Roofline: HBM/latency.  Per key: its bytes read once (hash and compare
+// words), one table probe chain (32-B records), 4 B slot out; a new key adds
+// its bytes + 16 B of kref / khash + its 32-B record written.
 
 
 #include <algorithm>
@@ -98,14 +103,28 @@ __device__ __forceinline__ bool key_equal(const uint8_t* __restrict__ a, const u
   return true;
 }
 
+struct alignas(32) TRec {
+  u64 e;       // tag32 << 32 | slot (kPending: a claim of this launch, slot = its input index); EMPTY ~0
+  u64 len;     // the key's length
+  u64 w0, w1;  // its bytes 0..7 and 8..15, zero filled (key_words)
+};
+static_assert(sizeof(TRec) == 32, "32-B key records");
+
 struct Dir {
   const uint8_t* bytes;
   u64* kref;
   u64* khash;
-  u64* table;
+  TRec* table;
   u64 mask;
   u32 shift;  // 64 - log2(tcap)
 };
+
+// one record, two 16-B loads issued together
+__device__ __forceinline__ TRec load_rec(const TRec* __restrict__ t, u64 p) {
+  const ulonglong2* q = reinterpret_cast<const ulonglong2*>(t + p);
+  const ulonglong2 a = q[0], b = q[1];
+  return TRec{a.x, a.y, b.x, b.y};
+}
 
 struct In {
   const uint8_t* kb;
@@ -132,12 +151,11 @@ __global__ __launch_bounds__(kThreads) void k_key_probe(In I, Dir D, u32* __rest
     u64 p = t >> D.shift;
     u32 slot = kMiss;
     for (;;) {
-      const u64 e = D.table[p];
-      if (e == kEmpty) break;
-      if ((u32)(e >> 32) == tag_of(t) && !(e & kPending)) {
-        const u32 s = (u32)(e & kIdxMask);
-        const u64 r = D.kref[s];
-        if ((r & JY_LR_LEN_MASK) == len && key_equal(D.bytes + (r >> JY_LR_LEN_BITS), k, len, kw)) {
+      const TRec r = load_rec(D.table, p);
+      if (r.e == kEmpty) break;
+      if ((u32)(r.e >> 32) == tag_of(t) && !(r.e & kPending) && r.len == len && r.w0 == kw.w0 && r.w1 == kw.w1) {
+        const u32 s = (u32)(r.e & kIdxMask);
+        if (len <= 16 || key_equal(D.bytes + (D.kref[s] >> JY_LR_LEN_BITS), k, len, kw)) {
           slot = s;
           break;
         }
@@ -211,10 +229,10 @@ __global__ __launch_bounds__(kThreads) void k_key_claim(In I, Dir D, const u32* 
   const KeyW kw = key_words(k, len);
   const u64 mine = ((u64)tag_of(t) << 32) | kPending | i;
   u64 p = t >> D.shift;
-  u64 e = D.table[p];
+  u64 e = D.table[p].e;
   for (;;) {
     if (e == kEmpty) {
-      const u64 prev = atomicCAS(reinterpret_cast<unsigned long long*>(D.table + p), kEmpty, mine);
+      const u64 prev = atomicCAS(reinterpret_cast<unsigned long long*>(&D.table[p].e), kEmpty, mine);
       if (prev == kEmpty) {
         owner[i] = (u32)i;
         pos[i] = p;
@@ -232,7 +250,7 @@ __global__ __launch_bounds__(kThreads) void k_key_claim(In I, Dir D, const u32* 
       }
     }
     p = (p + 1) & D.mask;
-    e = D.table[p];
+    e = D.table[p].e;
   }
 }
 
@@ -284,7 +302,15 @@ __global__ __launch_bounds__(kThreads) void k_key_commit(In I, Dir D, uint8_t* _
     D.kref[slot] = (at << JY_LR_LEN_BITS) | len;
     D.khash[slot] = th[i];
   }
-  if (o == (u32)i) D.table[pos[i]] = ((u64)tag_of(th[i]) << 32) | slot;
+  if (o == (u32)i) {  // (probes and claims of other keys run in other launches)
+    TRec& r = D.table[pos[i]];
+    const u64 len = I.ko[i + 1] - I.ko[i];
+    const KeyW kw = key_words(I.kb + I.ko[i], len);
+    r.len = len;
+    r.w0 = kw.w0;
+    r.w1 = kw.w1;
+    r.e = ((u64)tag_of(th[i]) << 32) | slot;
+  }
 }
 
 // lookup only: slots of present keys, JY_NO_SLOT otherwise
@@ -300,7 +326,12 @@ __global__ __launch_bounds__(kThreads) void k_key_rehash(Dir D, u64 nk) {
   const u64 t = D.khash[s];
   const u64 e = ((u64)tag_of(t) << 32) | s;
   u64 p = t >> D.shift;
-  while (atomicCAS(reinterpret_cast<unsigned long long*>(D.table + p), kEmpty, e) != kEmpty) p = (p + 1) & D.mask;
+  while (atomicCAS(reinterpret_cast<unsigned long long*>(&D.table[p].e), kEmpty, e) != kEmpty) p = (p + 1) & D.mask;
+  const u64 r = D.kref[s], len = r & JY_LR_LEN_MASK;
+  const KeyW kw = key_words(D.bytes + (r >> JY_LR_LEN_BITS), len);
+  D.table[p].len = len;
+  D.table[p].w0 = kw.w0;
+  D.table[p].w1 = kw.w1;
 }
 
 u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kThreads - 1) / kThreads); }
@@ -316,7 +347,7 @@ Dir dir_of(KeyDir& K) {
   D.bytes = K.bytes;
   D.kref = K.kref;
   D.khash = K.khash;
-  D.table = K.table;
+  D.table = reinterpret_cast<TRec*>(K.table);
   D.mask = K.tcap - 1;
   D.shift = 64 - K.lg;
   return D;
@@ -332,10 +363,10 @@ int32_t grow_table(jy_engine* eng, KeyDir& K, u64 need_keys) {
   if (K.table && want <= K.tcap) return JY_OK;
   jy_dev_free(eng, K.table);
   K.table = nullptr;
-  JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&K.table), want * 8, "key table"));
+  JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&K.table), want * sizeof(TRec), "key table"));
   K.tcap = want;
   K.lg = lg;
-  JY_HIP(eng, hipMemsetAsync(K.table, 0xFF, want * 8, eng->stream));
+  JY_HIP(eng, hipMemsetAsync(K.table, 0xFF, want * sizeof(TRec), eng->stream));
   if (K.n) LAUNCH(k_key_rehash, K.n, dir_of(K), K.n);
   return JY_OK;
 }

@@ -9,8 +9,16 @@ device copies for the single-GPU tests), interned on their owner and merged
 there -- all inside the library; the host only reads the per-owner counts
 once.  This class is a thin ctypes caller (tests, bench); the Pony host binds
 the same entry points.
+
+The converge calls enqueue (round 5): host arrays are copied before a call
+returns; device arrays (CUDA tensors) are read later by the node's worker,
+so this wrapper keeps them alive until fence() / sync().  The engines
+(`engines`, `engine()`) are shared with the worker: use them after sync(),
+or inside `with node.locked():`.
 """
+import contextlib
 import ctypes as C
+import threading
 
 import numpy as np
 
@@ -75,6 +83,8 @@ class Node:
         self.ujson_columns = ujson_columns
         self.engines = [Engine.attach(self.lib.jy_node_engine(h, rank0 + i), devices[i], ujson_columns)
                         for i in range(nlocal)]
+        self._held = []  # device inputs of queued calls (the worker reads them later)
+        self._held_mu = threading.Lock()
 
     def close(self):
         if getattr(self, "h", None):
@@ -94,7 +104,30 @@ class Node:
             raise EngineError(rc, self.lib.jy_node_last_error(self.h).decode(errors="replace"))
 
     def sync(self):
-        self._check(self.lib.jy_node_sync(self.h))
+        """every queued call done, GPU work included"""
+        with self._held_mu:
+            held, self._held = self._held, []
+        rc = self.lib.jy_node_sync(self.h)
+        if rc != 0:  # a queued call failed: drain the streams before the inputs go
+            msg = self.lib.jy_node_last_error(self.h).decode(errors="replace")
+            self.lib.jy_node_sync(self.h)
+            raise EngineError(rc, msg)
+        del held
+
+    def fence(self):
+        """every queued call issued to the GPU streams (their device inputs are
+        then ordered on the node's streams; still alive until the GPU ran)"""
+        self._check(self.lib.jy_node_fence(self.h))
+
+    @contextlib.contextmanager
+    def locked(self):
+        """exclusive use of the node's engines (jy_node_lock / jy_node_unlock)"""
+        rc = self.lib.jy_node_lock(self.h)
+        try:
+            self._check(rc)
+            yield self
+        finally:
+            self.lib.jy_node_unlock(self.h)
 
     def stats(self):
         out = np.zeros(5, np.uint64)
@@ -120,10 +153,12 @@ class Node:
         return np.array([self.replica_col(r) for r in rids], dtype=np.uint16)
 
     # -- raw calls (numpy arrays: host; CUDA tensors: device) ----------------
-    @staticmethod
-    def _args(spec):
+    def _args(self, spec):
         out = [_arg(x, t) for x, t in spec]
         mem = _same_mem(*[m for (k, _, m) in out if k is not None])
+        if mem == DEVICE:
+            with self._held_mu:
+                self._held.append([k for (k, _, _) in out])
         return out, mem
 
     def counter_converge(self, ctype, kb, ko, cell_offs, col, val, sign=None):
@@ -158,6 +193,8 @@ class Node:
         cols_all[r][c] = the column of shard r's c-th peer"""
         cols = np.ascontiguousarray(cols_all, np.uint16)
         ncols = cols.shape[1]
+        with self._held_mu:
+            self._held.append([vals_p, vals_n])
         self._check(self.lib.jy_node_counter_converge_block(
             self.h, ctype, ncols, cols.ctypes.data, slot0, nslots, C.c_void_p(vals_p.data_ptr()),
             None if vals_n is None else C.c_void_p(vals_n.data_ptr())))

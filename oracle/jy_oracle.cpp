@@ -38,6 +38,8 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <array>
+#include <thread>
 #include <unordered_map>
 #include <unordered_set>
 #include <utility>
@@ -928,7 +930,7 @@ inline u64 dbytes(const uint8_t* p, u64 n) {
   return dcomb(h, n);
 }
 enum : u64 { kTagLog = 0x7100, kTagEnt = 0x7200, kTagDoc = 0x7300, kTagEl = 0x7400, kTagVV = 0x7500, kTagCl = 0x7600,
-             kTagReg = 0x7700 };
+             kTagReg = 0x7700, kTagCnt = 0x7800, kTagCell = 0x7900 };
 inline u64 d_reg(u64 kh, u64 ts, u64 vh) { return dcomb(kh, dcomb(kTagReg, dcomb(ts, vh))); }
 inline u64 d_log(u64 kh, u64 cutoff) { return dcomb(kh, dcomb(kTagLog, cutoff)); }
 inline u64 d_ent(u64 kh, u64 rank, u64 ts, u64 vh) { return dcomb(kh, dcomb(kTagEnt ^ (rank << 16), dcomb(ts, vh))); }
@@ -937,6 +939,11 @@ inline u64 d_el(u64 kh, u64 id, u64 seq, u64 elem) { return dcomb(kh, dcomb(kTag
 inline u64 d_vv(u64 kh, u64 id, u64 n) { return dcomb(kh, dcomb(kTagVV, dcomb(id, n))); }
 inline u64 d_cl(u64 kh, u64 id, u64 seq) { return dcomb(kh, dcomb(kTagCl, dcomb(id, seq))); }
 inline u64 dstr(const std::string& s) { return dbytes(reinterpret_cast<const uint8_t*>(s.data()), s.size()); }
+// counters: a key, and each (sign, replica id, value) entry with a value
+// other than 0 -- a 0 entry and an absent one read alike (max and sum), and
+// the engine's dense columns cannot tell them apart
+inline u64 d_cnt(u64 kh) { return dcomb(kh, kTagCnt); }
+inline u64 d_cell(u64 kh, u64 sign, u64 id, u64 v) { return dcomb(kh, dcomb(kTagCell ^ (sign << 16), dcomb(id, v))); }
 }  // namespace
 
 extern "C" {
@@ -944,7 +951,31 @@ extern "C" {
 int32_t or_digest_repo(void* rp, u64* out4) {
   const Repo& r = *static_cast<Repo*>(rp);
   u64 d = 0, nk = 0, ni = 0, nb = 0;
-  if (r.type == T_TREG) {  // one (ts, value) register per key
+  if (r.type == T_GCOUNT || r.type == T_PNCOUNT) {  // nb: the wrapping sum of every entry
+    auto cells = [&](u64 kh, u64 sign, const GCounter& g) {
+      for (const auto& kv : g.data)
+        if (kv.second) {
+          d += d_cell(kh, sign, kv.first, kv.second);
+          nb += kv.second;
+          ni++;
+        }
+    };
+    if (r.type == T_GCOUNT)
+      for (const auto& kv : r.gc) {
+        const u64 kh = dstr(kv.first);
+        d += d_cnt(kh);
+        cells(kh, 0, kv.second);
+        nk++;
+      }
+    else
+      for (const auto& kv : r.pn) {
+        const u64 kh = dstr(kv.first);
+        d += d_cnt(kh);
+        cells(kh, 0, kv.second.p);
+        cells(kh, 1, kv.second.n);
+        nk++;
+      }
+  } else if (r.type == T_TREG) {  // one (ts, value) register per key
     for (const auto& kv : r.tr) {
       d += d_reg(dstr(kv.first), kv.second.ts, dstr(kv.second.value));
       nb += kv.second.value.size();
@@ -982,6 +1013,45 @@ int32_t or_digest_repo(void* rp, u64* out4) {
   out4[1] = nk;
   out4[2] = ni;
   out4[3] = nb;
+  return 0;
+}
+
+// the engine's dense counter read-back: n keys (kb / ko), vals[(sign * ncols
+// + col) * pitch + i] with column col holding replica ids[col]; the same
+// digest as or_digest_repo of a GCOUNT (nsigns 1) / PNCOUNT (2) repo holding
+// those keys.  Key ranges digest on up to `threads` threads (a full-size
+// config-2 state is 2^31 cells).
+int32_t or_digest_counter_dense(u64 n, const uint8_t* kb, const u64* ko, uint32_t nsigns, uint32_t ncols, const u64* ids,
+                                const u64* vals, u64 pitch, uint32_t threads, u64* out4) {
+  if (nsigns < 1 || nsigns > 2) return -1;
+  const uint32_t T = std::max<uint32_t>(1, std::min<uint32_t>(threads, 64));
+  std::vector<std::array<u64, 4>> part(T, std::array<u64, 4>{0, 0, 0, 0});
+  auto work = [&](uint32_t t) {
+    const u64 a = n * t / T, b = n * (t + 1) / T;
+    u64 d = 0, ni = 0, nb = 0;
+    for (u64 i = a; i < b; i++) {
+      const u64 kh = dbytes(kb + ko[i], ko[i + 1] - ko[i]);
+      d += d_cnt(kh);
+      for (uint32_t sg = 0; sg < nsigns; sg++)
+        for (uint32_t c = 0; c < ncols; c++) {
+          const u64 v = vals[((u64)sg * ncols + c) * pitch + i];
+          if (v) {
+            d += d_cell(kh, sg, ids[c], v);
+            nb += v;
+            ni++;
+          }
+        }
+    }
+    part[t] = {d, b - a, ni, nb};
+  };
+  std::vector<std::thread> th;
+  for (uint32_t t = 1; t < T; t++) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+  u64 o[4] = {0, 0, 0, 0};
+  for (const auto& p : part)
+    for (int q = 0; q < 4; q++) o[q] += p[q];
+  std::memcpy(out4, o, sizeof(o));
   return 0;
 }
 

@@ -36,7 +36,7 @@ def load():
     if not os.path.exists(LIB):
         build()
     lib = C.CDLL(LIB)
-    P, U64, I64, I32 = C.c_void_p, C.c_uint64, C.c_int64, C.c_int32
+    P, U64, I64, I32, U32 = C.c_void_p, C.c_uint64, C.c_int64, C.c_int32, C.c_uint32
     sig = {
         "or_table_new": (P, []), "or_table_free": (None, [P]),
         "or_table_set": (None, [P, C.c_char_p, P, U64, U64]),
@@ -63,6 +63,7 @@ def load():
         "or_ujson_clr": (None, [P, C.c_char_p, U64]),
         "or_ujson_touch": (None, [P, C.c_char_p, U64]),
         "or_digest_repo": (I32, [P, P]),
+        "or_digest_counter_dense": (I32, [U64, P, P, U32, U32, P, P, U64, U32, P]),
         "or_digest_table": (I32, [I32, P, P]),
         "or_digest_tlog_handles": (I32, [U64, P, P, P, P, P, P, P, P, U64, P]),
         "or_digest_treg_handles": (I32, [U64, P, P, P, P, P, P, U64, P]),
@@ -254,6 +255,23 @@ def _digest_out(rc, out):
 def digest_repo(repo):
     out = np.zeros(4, np.uint64)
     return _digest_out(load().or_digest_repo(repo.h, out.ctypes.data), out)
+
+
+def digest_counter_dense(kb, ko, ids, vals, threads=None):
+    """the engine's dense counter read-back: vals [nsigns][ncols][n] (nsigns 1:
+    GCOUNT, 2: PNCOUNT), column c holding replica ids[c]"""
+    import os
+    vals = np.ascontiguousarray(vals, np.uint64)
+    if vals.ndim == 2:
+        vals = vals[None]
+    nsigns, ncols, n = vals.shape
+    keep = [_c(kb, np.uint8), _c(ko, np.uint64), _c(ids, np.uint64)]
+    assert len(keep[1][0]) == n + 1 and len(keep[2][0]) >= ncols
+    out = np.zeros(4, np.uint64)
+    T = threads or min(32, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 1)
+    rc = load().or_digest_counter_dense(n, keep[0][1], keep[1][1], nsigns, ncols, keep[2][1], vals.ctypes.data, n, T,
+                                        out.ctypes.data)
+    return _digest_out(rc, out)
 
 
 def digest_table(ctype, table):

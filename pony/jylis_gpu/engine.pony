@@ -4,41 +4,46 @@ NOT COMPILE-CHECKED: unbuilt here (no ponyc); see INTEGRATION.md.
 
 A GPU repo holds `(_Node | None)`: `RepoAny.create` (repo_manager.pony:6)
 is not partial, so a missing GPU is reported per call (`_Fail`), not at
-construction.
+construction.  Every repo's `_Node` wraps the process's one library node
+(jy_node_acquire_local / jy_node_release).
 """
 use "collections"
 use "resp"
 
 class _Node
-  """Every GPU of this Jylis node behind one handle (jy_node_*), one node per
-  Database and type: keys are hash-sharded over the GPUs (jy_node_shard_of).
-  A decoded peer batch goes out in ONE call (jy_node_*_converge): the library
-  hashes and regroups the keys on the device, moves each owner's part over
-  RCCL, interns and merges it there.  Reads, local writes and flushes go to
-  the key's owner shard (`owner`, `shards`).  Owned by the RepoManager actor
-  that owns the repo, so calls are never concurrent."""
+  """Every GPU of this Jylis process behind one handle (jy_node_*).  ONE node
+  per process, shared by the five GPU repos (database.pony:18-22 makes one
+  RepoManager actor per type): jy_node_acquire_local hands every repo the
+  same library node, so one RCCL communicator and one engine per GPU serve
+  every CRDT type.  Keys are hash-sharded over the GPUs (jy_node_shard_of).
+  A decoded peer batch goes out in ONE call (jy_node_*_converge) that only
+  enqueues: the node's worker thread regroups, exchanges and merges, one job
+  at a time in call order, so the five actors' calls never interleave on the
+  communicator and no scheduler thread waits for the GPU.  Reads, local
+  writes and flushes use the key's owner shard (`owner`, `shards`) between
+  `lock` and `unlock` (jy_node_lock waits for the jobs queued before it).
+  Never call a jy_node_* entry point while holding the lock."""
   let ptr: Pointer[None] tag
   let shards: Array[_Engine] = shards.create()   // one view per GPU, index = shard
   let _col: U32                                   // this replica's column (the same on every shard)
 
   new create(identity: U64) ? =>
-    let ndev = @jy_device_count()
-    if ndev <= 0 then error end
-    let devs = Array[I32]
-    for d in Range[I32](0, ndev) do devs.push(d) end
     let cfg = JyConfig
     @jy_config_default(cfg)
     var p = Pointer[None]
-    if @jy_node_create_local(ndev.u32(), devs.cpointer(), JyFabricRccl(), cfg, addressof p) != 0 then error end
+    if @jy_node_acquire_local(cfg, addressof p) != 0 then error end
     ptr = p
     var c: U32 = 0
     if @jy_node_replica_col(ptr, identity, addressof c) != 0 then error end
     _col = c
-    for s in Range[U32](0, ndev.u32()) do shards.push(_Engine.view(@jy_node_engine(ptr, s), c)) end
+    for s in Range[U32](0, @jy_node_nshards(ptr)) do shards.push(_Engine.view(@jy_node_engine(ptr, s), c)) end
 
   fun col(): U32 => _col
 
   fun check(rc: I32) ? => if rc != 0 then error end
+
+  fun lock() => @jy_node_lock(ptr)
+  fun unlock() => @jy_node_unlock(ptr)
 
   fun owner(key: String): _Engine ? =>
     """the shard that owns `key` (jy_key_owner over the node's GPUs)"""
@@ -50,7 +55,14 @@ class _Node
     check(@jy_node_replica_col(ptr, id, addressof c))?
     c.u16()
 
-  fun _final() => @jy_node_destroy(ptr)
+  fun _final() => @jy_node_release(ptr)
+
+primitive _Lock
+  """the shared node's engines, exclusively (a repo holds no node: no-op)"""
+  fun apply(node: (_Node box | None)) => match node | let n: _Node box => n.lock() end
+
+primitive _Unlock
+  fun apply(node: (_Node box | None)) => match node | let n: _Node box => n.unlock() end
 
 class _Engine
   """One shard's engine (one GPU): a view the node owns.  Slot -> key names

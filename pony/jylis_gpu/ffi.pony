@@ -113,6 +113,13 @@ use @jy_node_engine[Pointer[None] tag](node: Pointer[None] tag, shard: U32)
 use @jy_node_shard_of[U32](node: Pointer[None] tag, key: Pointer[U8] tag, len: U64)
 use @jy_node_replica_col[I32](node: Pointer[None] tag, id: U64, col: Pointer[U32] tag)
 use @jy_node_sync[I32](node: Pointer[None] tag)
+use @jy_node_nshards[U32](node: Pointer[None] tag)
+// one node per process, shared by the five repos; the calls enqueue
+use @jy_node_acquire_local[I32](cfg: JyConfig tag, out: Pointer[Pointer[None] tag] tag)
+use @jy_node_release[None](node: Pointer[None] tag)
+use @jy_node_fence[I32](node: Pointer[None] tag)
+use @jy_node_lock[I32](node: Pointer[None] tag)
+use @jy_node_unlock[None](node: Pointer[None] tag)
 use @jy_node_counter_converge[I32](node: Pointer[None] tag, ty: I32, n: U64, key_bytes: Pointer[U8] tag,
   key_offs: Pointer[U64] tag, cell_offs: Pointer[U64] tag, sign: Pointer[U8] tag, col: Pointer[U16] tag,
   value: Pointer[U64] tag, mem: I32)

@@ -36,11 +36,23 @@ class RepoGCOUNTGpu
     peer pair first, so a replica with no local commands still converges
     each tick"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = _deltas_size()
+    _Unlock(_node)
+    r
+
+  fun ref _deltas_size(): USize =>
     _CounterPending(_node, JyGCOUNT())
 
   fun ref flush_deltas(): Array[(String, Any box)] box =>
     """repo_gcount.pony:18-23: every pending key with its post-write total"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = _flush_deltas()
+    _Unlock(_node)
+    r
+
+  fun ref _flush_deltas(): Array[(String, Any box)] box =>
     let out = Array[(String, Any box)]
     match _node
     | let n: _Node =>
@@ -81,6 +93,12 @@ class RepoGCOUNTGpu
   fun ref get(resp: Respond, key: String): Bool =>
     """repo_gcount.pony:53-55: a missing key reads 0"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = _get(resp, key)
+    _Unlock(_node)
+    r
+
+  fun ref _get(resp: Respond, key: String): Bool =>
     match _node
     | let n: _Node =>
       try
@@ -98,6 +116,12 @@ class RepoGCOUNTGpu
   fun ref inc(resp: Respond, key: String, value: U64): Bool =>
     """repo_gcount.pony:57-60, on the key's owner shard"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = _inc(resp, key, value)
+    _Unlock(_node)
+    r
+
+  fun ref _inc(resp: Respond, key: String, value: U64): Bool =>
     match _node
     | let n: _Node =>
       try
@@ -127,11 +151,23 @@ class RepoPNCOUNTGpu
     peer pair first, so a replica with no local commands still converges
     each tick"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = _deltas_size()
+    _Unlock(_node)
+    r
+
+  fun ref _deltas_size(): USize =>
     _CounterPending(_node, JyPNCOUNT())
 
   fun ref flush_deltas(): Array[(String, Any box)] box =>
     """repo_pncount.pony:19-24"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = _flush_deltas()
+    _Unlock(_node)
+    r
+
+  fun ref _flush_deltas(): Array[(String, Any box)] box =>
     let out = Array[(String, Any box)]
     match _node
     | let n: _Node =>
@@ -175,6 +211,12 @@ class RepoPNCOUNTGpu
   fun ref get(resp: Respond, key: String): Bool =>
     """repo_pncount.pony:55-57: (sum P - sum N) as i64; a missing key reads 0"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = _get(resp, key)
+    _Unlock(_node)
+    r
+
+  fun ref _get(resp: Respond, key: String): Bool =>
     match _node
     | let n: _Node =>
       try
@@ -192,6 +234,12 @@ class RepoPNCOUNTGpu
   fun ref write(resp: Respond, key: String, value: I64, sign: I32): Bool =>
     """INC / DEC (repo_pncount.pony:59-67): the i64 argument bit-cast to u64"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = _write(resp, key, value, sign)
+    _Unlock(_node)
+    r
+
+  fun ref _write(resp: Respond, key: String, value: I64, sign: I32): Bool =>
     match _node
     | let n: _Node =>
       try

@@ -29,6 +29,12 @@ class RepoTREGGpu
     peer pair first, so a replica with no local commands still converges
     each tick"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = _deltas_size()
+    _Unlock(_node)
+    r
+
+  fun ref _deltas_size(): USize =>
     var total: USize = 0
     match _node
     | let n: _Node =>
@@ -43,6 +49,12 @@ class RepoTREGGpu
   fun ref flush_deltas(): Array[(String, Any box)] box =>
     """repo_treg.pony:18-22: every pending key with its delta register"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = _flush_deltas()
+    _Unlock(_node)
+    r
+
+  fun ref _flush_deltas(): Array[(String, Any box)] box =>
     let out = Array[(String, Any box)]
     match _node
     | let node: _Node =>
@@ -92,7 +104,9 @@ class RepoTREGGpu
             ts.cpointer(), vals.bytes.cpointer(), vals.offs.cpointer(), JyHost()))?
         end
       end
+      n.lock()  // (the converge above only enqueued; the engines are shared)
       for e in n.shards.values() do e.maybe_collect(JyTREG()) end
+      n.unlock()
     end
     _in.clear()
 
@@ -106,6 +120,12 @@ class RepoTREGGpu
   fun ref get(resp: Respond, key: String): Bool =>
     """repo_treg.pony:54-63: [value, timestamp], or null for a missing key"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = _get(resp, key)
+    _Unlock(_node)
+    r
+
+  fun ref _get(resp: Respond, key: String): Bool =>
     match _node
     | let n: _Node =>
       let e = try n.owner(key)? else return _Fail(resp) end
@@ -125,6 +145,12 @@ class RepoTREGGpu
   fun ref set(resp: Respond, key: String, value: String, timestamp: U64): Bool =>
     """repo_treg.pony:65-68"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = _set(resp, key, value, timestamp)
+    _Unlock(_node)
+    r
+
+  fun ref _set(resp: Respond, key: String, value: String, timestamp: U64): Bool =>
     match _node
     | let n: _Node =>
       try
@@ -160,6 +186,12 @@ class RepoTLOGGpu
     peer pair first, so a replica with no local commands still converges
     each tick"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = _deltas_size()
+    _Unlock(_node)
+    r
+
+  fun ref _deltas_size(): USize =>
     var total: USize = 0
     match _node
     | let n: _Node =>
@@ -174,6 +206,12 @@ class RepoTLOGGpu
   fun ref flush_deltas(): Array[(String, Any box)] box =>
     """repo_tlog.pony:21-25: every pending key with its delta log"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = _flush_deltas()
+    _Unlock(_node)
+    r
+
+  fun ref _flush_deltas(): Array[(String, Any box)] box =>
     let out = Array[(String, Any box)]
     match _node
     | let node: _Node =>
@@ -238,7 +276,9 @@ class RepoTLOGGpu
             JyHost()))?
         end
       end
+      n.lock()  // (the converge above only enqueued; the engines are shared)
       for e in n.shards.values() do e.maybe_collect(JyTLOG()) end
+      n.unlock()
     end
     _in.clear()
 
@@ -260,8 +300,14 @@ class RepoTLOGGpu
   fun ref write(resp: Respond, key: String, op: U8, value: String, ts': U64, count: U64): Bool ? =>
     """INS key value ts / TRIMAT key ts / TRIM key count / CLR key
     (repo_tlog.pony:85-111): one jy_tlog_write command"""
-    var ts = ts'
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = try _write(resp, key, op, value, ts', count)? else _Unlock(_node); error end
+    _Unlock(_node)
+    r
+
+  fun ref _write(resp: Respond, key: String, op: U8, value: String, ts': U64, count: U64): Bool ? =>
+    var ts = ts'
     match _node
     | let n: _Node =>
       let e = n.owner(key)?
@@ -280,6 +326,12 @@ class RepoTLOGGpu
   fun ref get(resp: Respond, key: String, count: USize): Bool =>
     """repo_tlog.pony:69-83: at most `count` entries, newest first"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = _get(resp, key, count)
+    _Unlock(_node)
+    r
+
+  fun ref _get(resp: Respond, key: String, count: USize): Bool =>
     match _node
     | let n: _Node =>
       let e = try n.owner(key)? else return _Fail(resp) end
@@ -308,6 +360,12 @@ class RepoTLOGGpu
   fun ref size(resp: Respond, key: String, cutoff: Bool): Bool =>
     """SIZE / CUTOFF (repo_tlog.pony:90-96): 0 for a missing key"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = _size(resp, key, cutoff)
+    _Unlock(_node)
+    r
+
+  fun ref _size(resp: Respond, key: String, cutoff: Bool): Bool =>
     match _node
     | let n: _Node =>
       let e = try n.owner(key)? else return _Fail(resp) end

@@ -70,6 +70,12 @@ class RepoUJSONGpu
     peer pair first, so a replica with no local commands still converges
     each tick"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = _deltas_size()
+    _Unlock(_node)
+    r
+
+  fun ref _deltas_size(): USize =>
     var total: USize = 0
     match _node
     | let n: _Node =>
@@ -84,6 +90,12 @@ class RepoUJSONGpu
   fun ref flush_deltas(): Array[(String, Any box)] box =>
     """repo_ujson.pony:22-26: every pending doc with its delta document"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = _flush_deltas()
+    _Unlock(_node)
+    r
+
+  fun ref _flush_deltas(): Array[(String, Any box)] box =>
     let out = Array[(String, Any box)]
     match _node
     | let node: _Node =>
@@ -242,6 +254,12 @@ class RepoUJSONGpu
   fun ref get(resp: Respond, key: String, path: Array[String] val): Bool =>
     """repo_ujson.pony:68-72: the render, or '' for nothing"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = _get(resp, key, path)
+    _Unlock(_node)
+    r
+
+  fun ref _get(resp: Respond, key: String, path: Array[String] val): Bool =>
     match _node
     | let n: _Node =>
       let e = try n.owner(key)? else return _Fail(resp) end
@@ -260,6 +278,12 @@ class RepoUJSONGpu
   fun ref ins_rm(resp: Respond, key: String, path: Array[String] val, text: String, op: U8): Bool ? =>
     """INS / RM (repo_ujson.pony:90-110): the value parses as a UJSON primitive"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = try _ins_rm(resp, key, path, text, op)? else _Unlock(_node); error end
+    _Unlock(_node)
+    r
+
+  fun ref _ins_rm(resp: Respond, key: String, path: Array[String] val, text: String, op: U8): Bool ? =>
     match _node
     | let n: _Node =>
       let e = try n.owner(key)? else return _Fail(resp) end
@@ -274,6 +298,12 @@ class RepoUJSONGpu
   fun ref clr(resp: Respond, key: String, path: Array[String] val): Bool =>
     """CLR (repo_ujson.pony:85-88): no key creation"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = _clr(resp, key, path)
+    _Unlock(_node)
+    r
+
+  fun ref _clr(resp: Respond, key: String, path: Array[String] val): Bool =>
     match _node
     | let n: _Node =>
       let e = try n.owner(key)? else return _Fail(resp) end
@@ -296,6 +326,12 @@ class RepoUJSONGpu
   fun ref set(resp: Respond, key: String, path: Array[String] val, text: String): Bool ? =>
     """SET (repo_ujson.pony:74-83): clear the path, insert the node's leaves"""
     _drain()
+    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    let r = try _set(resp, key, path, text)? else _Unlock(_node); error end
+    _Unlock(_node)
+    r
+
+  fun ref _set(resp: Respond, key: String, path: Array[String] val, text: String): Bool ? =>
     match _node
     | let n: _Node =>
       let e = try n.owner(key)? else return _Fail(resp) end
@@ -392,7 +428,7 @@ primitive _Render
   """leaves (relative path, canonical value) -> UJSON text ('' when empty)"""
   fun apply(leaves: Array[(Array[String] val, String)] box): String =>
     if leaves.size() == 0 then return "" end
-    let root = _Node
+    let root = _JsonNode
     for (p, v) in leaves.values() do
       var n = root
       for s in p.values() do n = n.child(s) end
@@ -400,12 +436,12 @@ primitive _Render
     end
     root.render()
 
-class _Node
+class _JsonNode
   embed values: Set[String] = values.create()
-  embed map: Map[String, _Node] = map.create()
+  embed map: Map[String, _JsonNode] = map.create()
 
-  fun ref child(k: String): _Node =>
-    try map(k)? else let c = _Node; map(k) = c; c end
+  fun ref child(k: String): _JsonNode =>
+    try map(k)? else let c = _JsonNode; map(k) = c; c end
 
   fun nonempty(): Bool =>
     if values.size() > 0 then return true end

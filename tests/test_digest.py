@@ -130,3 +130,38 @@ def test_treg_digests_agree(oracle_mod, seed):
         u = {k: np.array(v, copy=True) for k, v in t.items()}
         u[mut][idx] ^= 1
         assert O.digest_table(O.TREG, u)[0] != d[0], mut
+
+
+@pytest.mark.parametrize("ctype", [0, 1])
+@pytest.mark.parametrize("seed", [4, 5])
+def test_counter_dense_digest_agrees(oracle_mod, ctype, seed):
+    """the engine's dense read-back ([sign][col][key], any column order, zero
+    cells = absent) digests like the oracle's maps (configs 1 and 2 pins)"""
+    O = oracle_mod
+    r = O.Repo(ctype)
+    for b in random_history(O, ctype, seed, nops=200, nkeys=30):
+        r.converge(b)
+    t = r.state()
+    d = O.digest_repo(r)
+    kb, ko = np.asarray(t["key_bytes"], np.uint8), np.asarray(t["key_offs"], np.uint64)
+    n = len(ko) - 1
+    pres = ("",) if ctype == O.GCOUNT else ("p_", "n_")
+    ids = np.unique(np.concatenate([np.asarray(t[p + "ids"], np.uint64) for p in pres]))
+    ids = ids[np.random.default_rng(seed).permutation(len(ids))]
+    col = {int(x): c for c, x in enumerate(ids)}
+    vals = np.zeros((len(pres), len(ids) + 2, n), np.uint64)  # two unused columns
+    for s_, p in enumerate(pres):
+        offs = np.asarray(t[p + "offs"], np.int64)
+        for i in range(n):
+            for j in range(offs[i], offs[i + 1]):
+                vals[s_, col[int(t[p + "ids"][j])], i] = t[p + "vals"][j]
+    allids = np.concatenate([ids, np.array([7, 9], np.uint64)])
+    assert O.digest_counter_dense(kb, ko, allids, vals, threads=3) == d
+    assert d[1] == n
+    # every field is seen: a value, a key, a column's replica
+    v2 = vals.copy()
+    v2[0, 0, n // 2] ^= np.uint64(1 << 40)
+    assert O.digest_counter_dense(kb, ko, allids, v2)[0] != d[0]
+    ids2 = allids.copy()
+    ids2[0] ^= np.uint64(1)
+    assert O.digest_counter_dense(kb, ko, ids2, vals)[0] != d[0]

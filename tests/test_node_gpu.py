@@ -20,7 +20,21 @@ from helpers import assert_state_equal, join_rows, random_history, split_rows
 pytestmark = pytest.mark.gpu
 
 TYPES = [0, 1, 2, 3, 4]
-LAYOUTS = [(1, "rccl"), (2, "copy"), (3, "copy")]
+# "rccl1": S = 1 through the regroup + RCCL self exchange that S > 1 runs
+# (JY_NODE_REGROUP_ONE); plain S = 1 reads its inputs in place
+LAYOUTS = [(1, "rccl"), (1, "rccl1"), (2, "copy"), (3, "copy")]
+
+
+def _node(S, fabric, **kw):
+    import os
+    from jylis_amd.node import Node
+    if fabric != "rccl1":
+        return Node(S, fabric, **kw)
+    os.environ["JY_NODE_REGROUP_ONE"] = "1"
+    try:
+        return Node(S, "rccl", **kw)
+    finally:
+        del os.environ["JY_NODE_REGROUP_ONE"]
 
 
 def _union(O, ctype, node):
@@ -50,7 +64,7 @@ def test_node_history(oracle_mod, ctype, S, fabric):
     state deltas), every flushed batch one node call"""
     from jylis_amd.node import Node
     O = oracle_mod
-    node = Node(S, fabric)
+    node = _node(S, fabric)
     try:
         batches = random_history(O, ctype, seed=100 + 10 * ctype + S, nops=160, nkeys=40)
         for b in batches:
@@ -95,7 +109,7 @@ def test_node_treg_large(oracle_mod, S, fabric, mem):
     from jylis_amd.node import Node
     O = oracle_mod
     rng = np.random.default_rng(7 + S)
-    node = Node(S, fabric)
+    node = _node(S, fabric)
     try:
         seen = []
         for step in range(4):
@@ -140,7 +154,7 @@ def test_node_tlog_large(oracle_mod, S, fabric, mem):
     from jylis_amd.node import Node
     O = oracle_mod
     rng = np.random.default_rng(70 + S)
-    node = Node(S, fabric)
+    node = _node(S, fabric)
     try:
         seen = []
         for step in range(4):
@@ -161,7 +175,7 @@ def test_node_counter_device(oracle_mod, S, fabric):
     from jylis_amd.node import Node
     O = oracle_mod
     rng = np.random.default_rng(5 + S)
-    node = Node(S, fabric)
+    node = _node(S, fabric)
     try:
         rids = [int(x) for x in rng.integers(1, 2**63, 6)]
         cols = node.replica_cols(rids)
@@ -209,7 +223,7 @@ def test_node_counter_block(S, fabric):
     from jylis_amd._lib import PNCOUNT
     from jylis_amd.node import Node
     K, C = 4096, 3
-    node = Node(S, fabric, counter_columns=S * C)
+    node = _node(S, fabric, counter_columns=S * C)
     try:
         cols = node.replica_cols(list(range(1, S * C + 1))).reshape(S, C)  # shard r's peers
         for r, eng in enumerate(node.engines):
