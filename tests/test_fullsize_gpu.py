@@ -209,3 +209,82 @@ def _treg_digest(O, eng, kb, ko):
     n, _ = eng.arena_usage(TREG)
     arena = np.frombuffer(eng.arena_read(TREG, 0, n), np.uint8) if n else np.zeros(0, np.uint8)
     return O.digest_treg_handles(kb, ko, ts, pre, lr, arena)
+
+
+def _counter_digest(O, eng, ctype, kb, ko, ids, R, chunk=1 << 20):
+    """the engine's dense counter state of every key, digested in key chunks
+    (the digest is a wrapping sum over keys)"""
+    K = len(ko) - 1
+    tot = [0, 0, 0, 0]
+    for s0 in range(0, K, chunk):
+        n = min(chunk, K - s0)
+        vals = eng.counter_export(ctype, R, s0, n)
+        a, b = int(ko[s0]), int(ko[s0 + n])
+        d = O.digest_counter_dense(kb[a:b], ko[s0:s0 + n + 1] - np.uint64(a), ids, vals)
+        tot = [(x + y) % (1 << 64) for x, y in zip(tot, d)]
+    return tuple(tot)
+
+
+@pytest.mark.timeout(1500)
+@pytest.mark.parametrize("name", ["gcount", "pncount"])
+def test_counter_config_fullsize(oracle_mod, name):
+    """Configs 1 and 2 at full size: the bench's exact sequences (bench_gcount:
+    1M keys x 16 replicas; bench.py's headline: 16M keys x 64 replicas x
+    {P, N}) -- the state, then the chain of distinct delta batches, each one
+    block converge of every peer column -- with the canonical digest of the
+    WHOLE state after every converge against the oracle's (made key range by
+    key range by tests/golden/make_fullsize_digests.py), then every batch
+    re-applied (idempotence: the digest must not move).
+    Reference: RepoGCOUNT.converge / RepoPNCOUNT.converge
+    (jylis/repo_gcount.pony:50-51, repo_pncount.pony:52-53)."""
+    import torch
+    from jylis_amd import synth as S
+    from jylis_amd.engine import Engine
+    O = oracle_mod
+    gj = json.load(open(GOLDEN))
+    if name not in gj:
+        pytest.fail(f"tests/golden/fullsize_digests.json has no {name}: run make_fullsize_digests.py --only {name}")
+    g = gj[name]
+    states = [tuple(int(x) for x in d) for d in g["states"]]
+    ctype, K, R, G, seed = g["ctype"], g["keys"], g["R"], g["nsigns"], g["seed"]
+    kb, ko = S.counter_keys(K, prefix=g["prefix"].encode(), width=g["width"])
+    ids = S.replica_ids(R, seed)
+    dev = torch.device("cuda", 0)
+    caps = [1024] * 5
+    caps[ctype] = K
+    eng = Engine(device=0, counter_columns=R, key_capacity=caps)
+    try:
+        slots = eng.intern(ctype, (kb, ko))
+        assert slots[0] == 0 and slots[-1] == K - 1
+        cols = eng.replica_cols(ids.tolist())
+        assert (cols == np.arange(R)).all()
+
+        def apply(x):
+            if G == 2:
+                eng.pncount_converge_block(cols, 0, x[0], x[1])
+            else:
+                eng.gcount_converge_block(cols, 0, x[0])
+        cur = torch.empty((G, R, K), dtype=torch.int64, device=dev)
+        S.counter_rows_torch(cur, seed, wrap_frac=g["wrap_frac"])
+        apply(cur)
+        got = _counter_digest(O, eng, ctype, kb, ko, ids, R)
+        _progress(f"{name} state: {got}")
+        assert got == states[0], f"{name}: the loaded state differs from the oracle's"
+        first = None
+        for j in range(g["rounds"]):
+            nxt = torch.empty_like(cur)
+            S.counter_rows_torch(nxt, seed, rnd=j, prev=cur)
+            if j == 0:
+                first = nxt
+            apply(nxt)
+            got = _counter_digest(O, eng, ctype, kb, ko, ids, R)
+            _progress(f"{name} converge {j + 1}: {got}")
+            assert got == states[j + 1], f"{name}: state after delta batch {j} differs from the oracle's"
+            if j > 0:
+                del cur
+            cur = nxt
+        apply(first)  # the bench cycles its batches: nothing moves
+        apply(cur)
+        assert _counter_digest(O, eng, ctype, kb, ko, ids, R) == states[-1], f"{name}: a re-applied batch moved"
+    finally:
+        eng.close()
