@@ -604,25 +604,51 @@ __device__ __forceinline__ void uj_flags_long(const UjArgs& A, int kind, u64 k, 
   }
   const u64 d0 = __shfl(d, 0), d1 = __shfl(d, (int)lastl) + 1;  // the wave's dots lie in [d0, d1)
   if (kind == 0) {
-    // the delta's elements, the delta's cloud and the state cloud over [d0, d1)
+    // the delta's elements and the delta's cloud over [d0, d1)
     const u64 lo = A.deoff[k], hi = A.deoff[k + 1], blo = A.dcoff[k], bhi = A.dcoff[k + 1];
-    WSearch s[6] = {{A.ddots, 1, lo, hi, d0},  {A.ddots, 1, lo, hi, d1},  {A.dcloud, 1, blo, bhi, d0},
-                    {A.dcloud, 1, blo, bhi, d1}, {A.cloud, 1, clo, chi, d0}, {A.cloud, 1, clo, chi, d1}};
-    wave_lbs<6>(s);
-    if (!live) return;
-    // the item's three lookups inside the wave's bounds, issued together
+    WSearch s[4] = {{A.ddots, 1, lo, hi, d0}, {A.ddots, 1, lo, hi, d1}, {A.dcloud, 1, blo, bhi, d0},
+                    {A.dcloud, 1, blo, bhi, d1}};
+    wave_lbs<4>(s);
+    if (s[0].lo == s[1].lo && s[2].lo == s[3].lo) {
+      // (round 5) no delta element and no delta cloud dot falls in the
+      // wave's range -- the usual wave of a long document, far from the
+      // delta's few insertion points: no item has its dot in the delta's map
+      // or cloud, so only the delta vv can drop it, its merge position on the
+      // delta side is the range's, and the state cloud is never searched
+      // (~4 dependent 64-ary rounds over a hot document's cloud)
+      if (!live) return;
+      f = A.keep_all || !(dseq(d) <= A.vvd[k * A.R + dcol(d)]);
+      A.xr[gbase + i] = (u32)(s[0].lo - lo);
+      return;
+    }
+    // the item's delta lookups inside the wave's bounds, issued together
     // with its vv entries (the bounds hold every dot of [d0, d1), so a dot
     // equal to d lies inside them)
     Win<8> wb;
-    Win<4> wdc, wsc;
-    win_load<false>(wb, A.ddots, s[0].lo, s[1].lo, d);
-    win_load<false>(wdc, A.dcloud, s[2].lo, s[3].lo, d);
-    win_load<false>(wsc, A.cloud, s[4].lo, s[5].lo, d);
-    const u64 vd = A.vvd[k * A.R + dcol(d)], vs = state_vv(A, k, dcol(d));
-    bool eqb, indc, insc;
-    const u64 p = win_rank(wb, d, eqb);
-    win_rank(wdc, d, indc);
-    win_rank(wsc, d, insc);
+    Win<4> wdc;
+    u64 vd = 0, vs = 0, p = 0;
+    bool eqb = false, indc = false, insc = false;
+    if (live) {
+      win_load<false>(wb, A.ddots, s[0].lo, s[1].lo, d);
+      win_load<false>(wdc, A.dcloud, s[2].lo, s[3].lo, d);
+      vd = A.vvd[k * A.R + dcol(d)];
+      vs = state_vv(A, k, dcol(d));
+      p = win_rank(wb, d, eqb);
+      win_rank(wdc, d, indc);
+    }
+    // the state cloud decides only for a dot the delta also holds, above the
+    // state vv: searched by the waves that have one
+    const bool need = live && eqb && !(dseq(d) <= vs);
+    if (__ballot(need)) {
+      WSearch sc[2] = {{A.cloud, 1, clo, chi, d0}, {A.cloud, 1, clo, chi, d1}};
+      wave_lbs<2>(sc);
+      if (need) {
+        Win<4> wsc;
+        win_load<false>(wsc, A.cloud, sc[0].lo, sc[1].lo, d);
+        win_rank(wsc, d, insc);
+      }
+    }
+    if (!live) return;
     u32 xr = (u32)(p - lo);
     if (eqb) {
       f = 1;
@@ -969,34 +995,69 @@ __global__ __launch_bounds__(kThreads) void k_uj_sizes(UjArgs A, u64 ndt) {
 }
 
 // ---- U5: scatter into the fresh runs; vv rows, metas; zero state for the next converge
-// (no scan: one item per thread; the grid is the host's bound, surplus
-// workgroups exit at once)
-__device__ __forceinline__ void uj_scatter_kind(const UjArgs& A, int kind, u64 lt, u64 ta, u64 tc, const ScanSp& sp,
-                                                const ScanSp& kp, const u32* xrb, const u32* krb, u64 nv);
-__device__ __forceinline__ void uj_scatter_tile(const UjArgs& A, const u64 t) {
-  const u64 ta = A.ao[A.nd], tc = A.co[A.nd];
-  const ScanSp sp = sc_space(A), kp = ksc_space(A);
-  const u32* xrb = A.xr + ta;
-  const u32* krb = A.kr + tc;
-  const u64 nv = A.nvv;
-  const u64 tl[6] = {cdiv(ta), cdiv(A.nb), cdiv(tc), cdiv(A.cb), cdiv(nv), cdiv(A.nd)};
-  int kind = 0;
-  u64 lt = t;
-  while (kind < 6 && lt >= tl[kind]) lt -= tl[kind++];
-  if (kind == 6) return;
-  JY_CLK(c0);
-  uj_scatter_kind(A, kind, lt, ta, tc, sp, kp, xrb, krb, nv);
-  JY_CLK(c2);
-#ifdef JY_UJ_PROBE
-  const u64* tmk = kind == 0 ? A.tmA : kind == 1 ? A.tmB : kind == 2 ? A.tmC : A.tmD;
-  const bool lng = kind < 4 && (u32)(tmk[lt] >> 32) == A.epoch;
+// (no scan.)  A workgroup of kScatterThreads lanes takes a tile of kTile
+// items, kScatterU items per lane: a lane first issues the dependent loads of
+// all its items (scatter_prep: loads only), then stores them.  (Round 5,
+// in-box A/B, ms per config-5 converge, 2 runs each: 1 item per lane 0.380 /
+// 0.382, 2 items 0.381 / 0.381, 4 items 0.382 / 0.382 -- more chains in
+// flight per wave do not help: 1.)
+#ifndef JY_UJ_SCATTER_U
+#define JY_UJ_SCATTER_U 1
 #endif
-  JY_PROBE(5, kind + (lng ? 8 : 0), (u32)lt, c0, c2, c2);
-}
-__device__ __forceinline__ void uj_scatter_kind(const UjArgs& A, int kind, u64 lt, u64 ta, u64 tc, const ScanSp& sp,
-                                                const ScanSp& kp, const u32* xrb, const u32* krb, u64 nv) {
-  const u64 i = lt * kTile + threadIdx.x;
+constexpr int kScatterU = JY_UJ_SCATTER_U;
+constexpr int kScatterThreads = (int)kTile / kScatterU;
+
+struct ScOut {
+  u32 what;  // 0 nothing, 1 an element record, 2 a cloud dot
+  u64 at;    // pool index
+  u64 a, b;  // dot, element
+};
+
+// an element / cloud item's destination and payload (kinds 0..3; loads only)
+__device__ __forceinline__ ScOut scatter_prep(const UjArgs& A, int kind, u64 lt, u64 i, u64 ta, u64 tc,
+                                              const ScanSp& sp, const ScanSp& kp, const u32* xrb, const u32* krb) {
   const u64 eb0 = A.base[0], cb0 = A.base[1];
+  ScOut o{0, 0, 0, 0};
+  if (kind == 0) {  // state element
+    if (i >= ta) return o;
+    const u64 si = sp.at(i);
+    if (sp.at(i + 1) == si) return o;
+    const u64 k = doc_at(A, A.tmA, lt, A.sidA, i);
+    const URec x = load_rec(A.rec + A.abase[k] + (i - A.ao[k]));
+    const u32 xv = A.xr[i];
+    const u64 lo = A.deoff[k], p = lo + (xv & 0x7FFFFFFFu);
+    o = ScOut{1, eb0 + A.neo[k] + (si - sp.at(A.ao[k])) + (sp.at(ta + p) - sp.at(ta + lo)), x.dot,
+              (xv >> 31) ? A.delems[p] : x.elem};
+  } else if (kind == 1) {  // delta element
+    if (i >= A.nb) return o;
+    const u64 si = sp.at(ta + i);
+    if (sp.at(ta + i + 1) == si) return o;
+    const u64 k = doc_at(A, A.tmB, lt, A.sidB, i);
+    const u64 pa = A.ao[k] + xrb[i];
+    o = ScOut{1, eb0 + A.neo[k] + (si - sp.at(ta + A.deoff[k])) + (sp.at(pa) - sp.at(A.ao[k])), A.ddots[i],
+              A.delems[i]};
+  } else if (kind == 2) {  // state cloud dot
+    if (i >= tc) return o;
+    const u64 si = kp.at(i);
+    if (kp.at(i + 1) == si) return o;
+    const u64 k = doc_at(A, A.tmC, lt, A.sidC, i);
+    const u64 x = A.cloud[A.cbs[k] + (i - A.co[k])];
+    const u64 lo = A.dcoff[k];
+    o = ScOut{2, cb0 + A.nco[k] + (si - kp.at(A.co[k])) + (kp.at(tc + lo + A.kr[i]) - kp.at(tc + lo)), x, 0};
+  } else {  // delta cloud dot
+    if (i >= A.cb) return o;
+    const u64 si = kp.at(tc + i);
+    if (kp.at(tc + i + 1) == si) return o;
+    const u64 k = doc_at(A, A.tmD, lt, A.sidD, i);
+    const u64 pa = A.co[k] + krb[i];
+    o = ScOut{2, cb0 + A.nco[k] + (si - kp.at(tc + A.dcoff[k])) + (kp.at(pa) - kp.at(A.co[k])), A.dcloud[i], 0};
+  }
+  return o;
+}
+
+__device__ __forceinline__ void scatter_small(const UjArgs& A, int kind, u64 i) {
+  const u64 eb0 = A.base[0], cb0 = A.base[1];
+  const u64 nv = A.nvv;
   if (kind == 4) {  // the delta's sparse vv entries into the state rows; the dense delta vv back to zero
     if (i >= nv) return;
     const u64 x = A.dvv[i];
@@ -1013,51 +1074,47 @@ __device__ __forceinline__ void uj_scatter_kind(const UjArgs& A, int kind, u64 l
     A.vvd[k * A.R + c] = 0;
     return;
   }
-  if (kind == 5) {  // metas
-    if (i >= A.nd || is_bad(A, i)) return;
-    const u32 ne = (u32)(A.neo[i + 1] - A.neo[i]), nc = (u32)(A.nco[i + 1] - A.nco[i]);
-    A.meta[A.slot[i]] = UMeta{eb0 + A.neo[i], ne, ne, cb0 + A.nco[i], nc, nc};
-    return;
-  }
-  if (kind == 0) {  // state element
-    if (i >= ta) return;
-    const u64 si = sp.at(i);
-    if (sp.at(i + 1) == si) return;
-    const u64 k = doc_at(A, A.tmA, lt, A.sidA, i);
-    const URec x = load_rec(A.rec + A.abase[k] + (i - A.ao[k]));
-    const u32 xv = A.xr[i];
-    const u64 lo = A.deoff[k], p = lo + (xv & 0x7FFFFFFFu);
-    const u64 pos = A.neo[k] + (si - sp.at(A.ao[k])) + (sp.at(ta + p) - sp.at(ta + lo));
-    store_rec(A.epool_out + eb0 + pos, x.dot, (xv >> 31) ? A.delems[p] : x.elem);
-  } else if (kind == 1) {  // delta element
-    if (i >= A.nb) return;
-    const u64 si = sp.at(ta + i);
-    if (sp.at(ta + i + 1) == si) return;
-    const u64 k = doc_at(A, A.tmB, lt, A.sidB, i);
-    const u64 pa = A.ao[k] + xrb[i];
-    const u64 pos = A.neo[k] + (si - sp.at(ta + A.deoff[k])) + (sp.at(pa) - sp.at(A.ao[k]));
-    store_rec(A.epool_out + eb0 + pos, A.ddots[i], A.delems[i]);
-  } else if (kind == 2) {  // state cloud dot
-    if (i >= tc) return;
-    const u64 si = kp.at(i);
-    if (kp.at(i + 1) == si) return;
-    const u64 k = doc_at(A, A.tmC, lt, A.sidC, i);
-    const u64 x = A.cloud[A.cbs[k] + (i - A.co[k])];
-    const u64 lo = A.dcoff[k];
-    const u64 pos = A.nco[k] + (si - kp.at(A.co[k])) + (kp.at(tc + lo + A.kr[i]) - kp.at(tc + lo));
-    A.cpool_out[cb0 + pos] = x;
-  } else {  // delta cloud dot
-    if (i >= A.cb) return;
-    const u64 si = kp.at(tc + i);
-    if (kp.at(tc + i + 1) == si) return;
-    const u64 k = doc_at(A, A.tmD, lt, A.sidD, i);
-    const u64 pa = A.co[k] + krb[i];
-    const u64 pos = A.nco[k] + (si - kp.at(tc + A.dcoff[k])) + (kp.at(pa) - kp.at(A.co[k]));
-    A.cpool_out[cb0 + pos] = A.dcloud[i];
-  }
+  // kind 5: metas
+  if (i >= A.nd || is_bad(A, i)) return;
+  const u32 ne = (u32)(A.neo[i + 1] - A.neo[i]), nc = (u32)(A.nco[i + 1] - A.nco[i]);
+  A.meta[A.slot[i]] = UMeta{eb0 + A.neo[i], ne, ne, cb0 + A.nco[i], nc, nc};
 }
 
-__global__ __launch_bounds__(kItemThreads) void k_uj_scatter(UjArgs A) {
+__device__ __forceinline__ void uj_scatter_tile(const UjArgs& A, const u64 t) {
+  const u64 ta = A.ao[A.nd], tc = A.co[A.nd];
+  const ScanSp sp = sc_space(A), kp = ksc_space(A);
+  const u32* xrb = A.xr + ta;
+  const u32* krb = A.kr + tc;
+  const u64 nv = A.nvv;
+  const u64 tl[6] = {cdiv(ta), cdiv(A.nb), cdiv(tc), cdiv(A.cb), cdiv(nv), cdiv(A.nd)};
+  int kind = 0;
+  u64 lt = t;
+  while (kind < 6 && lt >= tl[kind]) lt -= tl[kind++];
+  if (kind == 6) return;
+  JY_CLK(c0);
+  if (kind >= 4) {
+#pragma unroll
+    for (int u = 0; u < kScatterU; u++) scatter_small(A, kind, lt * kTile + (u64)u * kScatterThreads + threadIdx.x);
+  } else {
+    ScOut o[kScatterU];
+#pragma unroll
+    for (int u = 0; u < kScatterU; u++)
+      o[u] = scatter_prep(A, kind, lt, lt * kTile + (u64)u * kScatterThreads + threadIdx.x, ta, tc, sp, kp, xrb, krb);
+#pragma unroll
+    for (int u = 0; u < kScatterU; u++) {
+      if (o[u].what == 1) store_rec(A.epool_out + o[u].at, o[u].a, o[u].b);
+      else if (o[u].what == 2) A.cpool_out[o[u].at] = o[u].a;
+    }
+  }
+  JY_CLK(c2);
+#ifdef JY_UJ_PROBE
+  const u64* tmk = kind == 0 ? A.tmA : kind == 1 ? A.tmB : kind == 2 ? A.tmC : A.tmD;
+  const bool lng = kind < 4 && (u32)(tmk[lt] >> 32) == A.epoch;
+#endif
+  JY_PROBE(5, kind + (lng ? 8 : 0), (u32)lt, c0, c2, c2);
+}
+
+__global__ __launch_bounds__(kScatterThreads) void k_uj_scatter(UjArgs A) {
   if (blockIdx.x == 0 && threadIdx.x == 0)
     for (int c = T_U1; c <= T_U4; c++) A.tick[c] = 0;  // U1..U4 of this converge are done
   const u64 T = cdiv(A.ao[A.nd]) + cdiv(A.nb) + cdiv(A.co[A.nd]) + cdiv(A.cb) + cdiv(A.nvv) + cdiv(A.nd);
@@ -1496,7 +1553,7 @@ int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* sl
   hipLaunchKernelGGL(k_uj_tscan, dim3(1), dim3(1024), 0, eng->stream, A, 1);
   hipLaunchKernelGGL(k_uj_sizes, dim3((u32)ndt), dim3(kThreads), 0, eng->stream, A, ndt);
   const u64 g5 = gf + gk + (nvv + kTile - 1) / kTile + (nd + kTile - 1) / kTile + 2;
-  hipLaunchKernelGGL(k_uj_scatter, dim3((u32)g5), dim3(kItemThreads), 0, eng->stream, A);
+  hipLaunchKernelGGL(k_uj_scatter, dim3((u32)g5), dim3(kScatterThreads), 0, eng->stream, A);
   JY_HIP(eng, hipGetLastError());
   JY_TRACE("ujson merge %llu docs: plan %.1f us, rest of the host side %.1f us", (unsigned long long)nd, th1 - th0,
            jy_now_us() - th1);
