@@ -136,37 +136,83 @@ __device__ __forceinline__ u32 tag_of(u64 t) { return (u32)t; }
 
 // K1: look every key up; misses counted with their bytes.  The counts are
 // per-workgroup partials (summed by k_key_sum): one global atomic per miss on
-// three shared words serialised ~65K misses per 1M-key batch (~0.6 ms)
+// three shared words serialised ~65K misses per 1M-key batch (~0.6 ms).
+// kProbeU keys per lane, their loads issued together at every step (offsets,
+// key words, then each probe round's records).  Round 5, in-box A/B of the
+// node TREG call (8.39M keys, ms per call, 2 runs each): 1 key per lane 0.738
+// / 0.741, 2 keys 0.742 / 0.747, 4 keys 0.809 / 0.806, 8 keys 0.968 / 0.962
+// -- the extra registers cost more occupancy than the chains in flight gain.
+#ifndef JY_KEY_PROBE_U
+#define JY_KEY_PROBE_U 1
+#endif
+constexpr int kProbeU = JY_KEY_PROBE_U;
+constexpr u64 kProbeKeys = (u64)kThreads * kProbeU;  // keys per probe workgroup
 __global__ __launch_bounds__(kThreads) void k_key_probe(In I, Dir D, u32* __restrict__ res, u64* __restrict__ th,
                                                         u64* __restrict__ parts) {
   __shared__ u64 red[3][kThreads / 64];
-  const u64 i = gid();
+  constexpr int U = kProbeU;
   u64 c[3] = {0, 0, 0};
-  if (i < I.n) {
-    const uint8_t* k = I.kb + I.ko[i];
-    const u64 len = I.ko[i + 1] - I.ko[i];
-    const KeyW kw = key_words(k, len);
-    const u64 t = table_hash(k, len, kw);
-    th[i] = t;
-    u64 p = t >> D.shift;
-    u32 slot = kMiss;
-    for (;;) {
-      const TRec r = load_rec(D.table, p);
-      if (r.e == kEmpty) break;
-      if ((u32)(r.e >> 32) == tag_of(t) && !(r.e & kPending) && r.len == len && r.w0 == kw.w0 && r.w1 == kw.w1) {
-        const u32 s = (u32)(r.e & kIdxMask);
-        if (len <= 16 || key_equal(D.bytes + (D.kref[s] >> JY_LR_LEN_BITS), k, len, kw)) {
-          slot = s;
-          break;
+  u64 i[U], a[U], len[U], t[U], p[U];
+  KeyW kw[U];
+  bool act[U];
+  u32 slot[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    i[u] = (u64)blockIdx.x * kProbeKeys + (u64)u * kThreads + threadIdx.x;
+    act[u] = i[u] < I.n;
+    a[u] = len[u] = 0;
+    if (act[u]) {
+      a[u] = I.ko[i[u]];
+      len[u] = I.ko[i[u] + 1] - a[u];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) kw[u] = act[u] ? key_words(I.kb + a[u], len[u]) : KeyW{0, 0};
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    slot[u] = kMiss;
+    t[u] = p[u] = 0;
+    if (act[u]) {
+      t[u] = table_hash(I.kb + a[u], len[u], kw[u]);
+      th[i[u]] = t[u];
+      p[u] = t[u] >> D.shift;
+    }
+  }
+  for (;;) {
+    TRec r[U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (act[u]) r[u] = load_rec(D.table, p[u]);
+    bool more = false;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (!act[u]) continue;
+      if (r[u].e == kEmpty) {
+        act[u] = false;
+        continue;
+      }
+      if ((u32)(r[u].e >> 32) == tag_of(t[u]) && !(r[u].e & kPending) && r[u].len == len[u] && r[u].w0 == kw[u].w0 &&
+          r[u].w1 == kw[u].w1) {
+        const u32 s = (u32)(r[u].e & kIdxMask);
+        if (len[u] <= 16 || key_equal(D.bytes + (D.kref[s] >> JY_LR_LEN_BITS), I.kb + a[u], len[u], kw[u])) {
+          slot[u] = s;
+          act[u] = false;
+          continue;
         }
       }
-      p = (p + 1) & D.mask;
+      p[u] = (p[u] + 1) & D.mask;
+      more = true;
     }
-    res[i] = slot;
-    if (slot == kMiss) {
-      c[0] = 1;
-      c[1] = len;
-      c[2] = len > JY_LR_LEN_MASK;
+    if (!more) break;
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    if (i[u] >= I.n) continue;
+    res[i[u]] = slot[u];
+    if (slot[u] == kMiss) {
+      c[0] += 1;
+      c[1] += len[u];
+      c[2] += len[u] > JY_LR_LEN_MASK;
     }
   }
   const int w = threadIdx.x >> 6;
@@ -429,11 +475,12 @@ int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, co
   u64* th = reinterpret_cast<u64*>((reinterpret_cast<uintptr_t>(res + n) + 15) & ~uintptr_t(15));
   u64* counts = th + n;  // [3] misses, their bytes, oversized keys
   In I{kb, ko, n};
-  const u64 nb = (n + kThreads - 1) / kThreads;
+  const u64 nb = (n + kProbeKeys - 1) / kProbeKeys;
   void* pp;
   JY_TRY(jy_scratch(eng, 29, nb * 24 + 64, &pp));
   u64* parts = static_cast<u64*>(pp);
-  LAUNCH(k_key_probe, n, I, dir_of(K), res, th, parts);
+  hipLaunchKernelGGL(k_key_probe, dim3((u32)nb), dim3(kThreads), 0, eng->stream, I, dir_of(K), res, th, parts);
+  JY_HIP(eng, hipGetLastError());
   hipLaunchKernelGGL(k_key_sum, dim3(1), dim3(kSumThreads), 0, eng->stream, parts, nb, counts);
   JY_HIP(eng, hipGetLastError());
   if (after_probe) JY_TRY(after_probe(arg));  // (a pageable read-back below may block at once)
