@@ -264,13 +264,9 @@ constexpr int kFastEnt = 4;  // delta entries a key may have for the lane-per-ke
 #ifndef JY_TLOG_KCACHE
 #define JY_TLOG_KCACHE 1
 #endif
-// 1: stage 2 loads the next pass's entry during this pass's search.  In-box
-// A/B (round 4, ms per config-4 converge, 2 runs each): off 0.837 / 0.841; on
-// at 6 waves per SIMD 0.865 / 0.865 (the extra registers spill: 32 B of
-// scratch per lane); on at 5 waves 0.834 / 0.836 -- within noise: off
-#ifndef JY_TLOG_PF
-#define JY_TLOG_PF 0
-#endif
+// (a next-pass prefetch of stage 2's entry measured no gain in round 4: 0.837
+// / 0.841 ms without, 0.865 with at 6 waves per SIMD (spills), 0.834 / 0.836
+// at 5 waves; removed)
 #ifndef JY_TLOG_CUT_PROBE
 #define JY_TLOG_CUT_PROBE 0  // 1: the cutoff drop by 16-ary probes (round 3)
 #endif
@@ -420,43 +416,17 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
 #pragma unroll
   for (int c = 0; c < kCache; c++) c_q[c] = c_i[c] = 0, c_t[c] = c_p[c] = c_l[c] = 0;
   int pass = 0;
-#if JY_TLOG_PF
-  // the next pass's entry (its key, position and delta words) is loaded
-  // while this pass searches the log: one dependent round trip less per pass
-  // (the timestamps only: the value words are loaded with the search window)
-  u32 n_idx = 0;
-  u64 n_j = 0, n_t = 0, n_pt = ~0ull;
-  auto fetch = [&](u64 f) {
-    if (f >= F) return;
-    n_idx = lds_last_le(l_soff, nt - 1, f);
-    n_j = gb0 + l_gb[n_idx] + (f - l_soff[n_idx]);
-    n_t = A.dts[n_j];
-    n_pt = f > l_soff[n_idx] ? A.dts[n_j - 1] : ~0ull;
-  };
-  fetch(tid);
-#endif
   for (u64 c0 = 0; c0 < F; c0 += kTile, pass++) {
     const u64 f = c0 + tid;
     u32 idx = 0, flag = 0, rank = 0, lo = 0, hi = 0;
     u64 t = 0, pp = 0, ll = 0, j = 0;
-#if JY_TLOG_PF
-    const u64 pt = n_pt;
-    idx = n_idx, j = n_j, t = n_t;
-    fetch(f + kTile);
-#endif
     if (f < F) {
-#if JY_TLOG_PF
-      pp = A.dpre[j];
-      ll = A.dlr[j];
-#endif
-#if !JY_TLOG_PF
       idx = lds_last_le(l_soff, nt - 1, f);
       j = gb0 + l_gb[idx] + (f - l_soff[idx]);
       t = A.dts[j];
       pp = A.dpre[j];
       ll = A.dlr[j];
       const u64 pt = f > l_soff[idx] ? A.dts[j - 1] : ~0ull;
-#endif
       // strictly newest first; the previous value is read only on a ts tie
       if (f > l_soff[idx] && (pt < t || (pt == t && jy_value_cmp(A.dpre[j - 1], A.dlr[j - 1], pp, ll, A.arena) <= 0)))
         atomicOr(&l_bad[idx], 2u);

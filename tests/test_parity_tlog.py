@@ -80,6 +80,53 @@ def test_edge_cases(oracle_mod, engine):
     assert got.get("missing") == [] and got.size("missing") == 0 and got.cutoff("missing") == 0
 
 
+def test_slow_key_mixes(oracle_mod, engine):
+    """slow keys (k_tlog_tile stage 2) whose deltas start with entries newer
+    than the log and go on with: a timestamp tie right after them, a duplicate
+    or an interleaving entry (in-place insert), a cutoff raise, more than four
+    newer entries, a segment that overflows (rebuild, one entry searched),
+    each against the oracle over two deltas"""
+    from jylis_amd.repo import RepoTLOG
+    O = oracle_mod
+    base = [(b"v%d" % i, i) for i in range(1, 11)]  # ts 1..10
+    state = [("tie", 0, _canon(base)), ("dup", 0, _canon(base)), ("ins", 0, _canon(base)),
+             ("cut", 0, _canon(base)), ("many", 0, _canon(base)), ("grow", 0, [(b"g", 1)]),
+             ("grow2", 0, [(b"g", 1)]), ("grow3", 0, [(b"g", 5)])]
+    d1 = [("tie", 0, [(b"n2", 20), (b"t", 15), (b"n1", 15)]),          # tie after the prefix (value order)
+          ("dup", 0, [(b"x", 30), (b"y", 25), (b"v3", 3)]),            # a duplicate of a state entry
+          ("ins", 0, [(b"x", 30), (b"z", 5), (b"a", 4)]),              # interleaves: inserted in place
+          ("cut", 6, [(b"x", 40), (b"y", 35), (b"old", 2)]),           # cutoff raise: old dropped
+          ("many", 0, [(b"m%d" % i, 60 - i) for i in range(7)]),     # 7 newer entries (prefix of 4)
+          ("grow", 0, [(b"n%d" % i, 100 - i) for i in range(12)]),   # past the segment: rebuilt
+          ("grow2", 0, [(b"p%d" % i, 50 - i) for i in range(4)] + [(b"o", 1)]),  # prefix + a tie at 1
+          ("grow3", 0, [(b"p%d" % i, 50 - i) for i in range(8)] + [(b"h", 3)])]  # rebuilt, one entry searched
+    d2 = [("tie", 0, [(b"n3", 21), (b"n2", 20), (b"t", 15)]),          # the prefix, then duplicates
+          ("dup", 0, [(b"q", 31), (b"x", 30)]),
+          ("ins", 0, [(b"w", 33), (b"v7", 7), (b"v6", 6)]),
+          ("many", 0, [(b"m%d" % i, 70 - i) for i in range(9)])]
+    want = O.Repo(O.TLOG)
+    got = RepoTLOG(engine)
+    for logs in (state, d1, d2):
+        b = _log_batch(logs)
+        want.converge(b)
+        got.converge_deltas(b)
+        assert_state_equal(O.TLOG, want.state(), got.state())
+    assert got.get("cut", 100)[-1] == (b"v6", 6) and got.size("grow") == 13
+    assert engine.skipped() == 0
+
+
+def test_malformed_after_newer_entries_is_skipped(engine):
+    """an ordering error after a few valid newer-than-the-log entries (or in
+    the value order of equal timestamps) still skips the whole key"""
+    from jylis_amd.repo import RepoTLOG
+    got = RepoTLOG(engine)
+    got.converge_deltas(_log_batch([("k", 0, [(b"s", 1)])]))
+    got.converge_deltas(_log_batch([("k", 0, [(b"x", 30), (b"y", 20), (b"z", 25)]),
+                                    ("k2", 0, [(b"x", 30), (b"y", 20), (b"z", 20), (b"a", 20)])]))
+    assert engine.skipped() == 2
+    assert got.get("k") == [(b"s", 1)] and got.get("k2") == []
+
+
 def test_clr_at_max_timestamp_and_trim_past_end(oracle_mod, engine):
     """CLR with newest ts 2^64-1 sets cutoff ts+1 = 0 (U64 wrap): no effect;
     TRIM n > size raises nothing (repo_tlog.pony:103-111; parity unpinned)"""
