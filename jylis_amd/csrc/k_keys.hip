@@ -103,6 +103,19 @@ __device__ __forceinline__ bool key_equal(const uint8_t* __restrict__ a, const u
   return true;
 }
 
+// bytes 16.. of a key longer than 16 (its record matched its length and
+// first 16 bytes).  NOT inlined: inlined into k_key_probe's loop, this
+// compiler (ROCm 7.2 clang, gfx950) lost the matched slot on the long-key
+// path -- the structurised loop's exit copied the old "miss" value over it --
+// so no key over 16 bytes was ever found again and each was re-created on
+// every call (tests/test_keys_gpu.py::test_long_keys_found_again)
+__device__ __attribute__((noinline)) bool key_tail_equal(const uint8_t* __restrict__ a, const uint8_t* __restrict__ k,
+                                                         u64 n) {
+  for (u64 i = 16; i < n; i += 8)
+    if (jy_ld8u(a + i, n - i) != jy_ld8u(k + i, n - i)) return false;
+  return true;
+}
+
 struct alignas(32) TRec {
   u64 e;       // tag32 << 32 | slot (kPending: a claim of this launch, slot = its input index); EMPTY ~0
   u64 len;     // the key's length
@@ -194,7 +207,7 @@ __global__ __launch_bounds__(kThreads) void k_key_probe(In I, Dir D, u32* __rest
       if ((u32)(r[u].e >> 32) == tag_of(t[u]) && !(r[u].e & kPending) && r[u].len == len[u] && r[u].w0 == kw[u].w0 &&
           r[u].w1 == kw[u].w1) {
         const u32 s = (u32)(r[u].e & kIdxMask);
-        if (len[u] <= 16 || key_equal(D.bytes + (D.kref[s] >> JY_LR_LEN_BITS), I.kb + a[u], len[u], kw[u])) {
+        if (len[u] <= 16 || key_tail_equal(D.bytes + (D.kref[s] >> JY_LR_LEN_BITS), I.kb + a[u], len[u])) {
           slot[u] = s;
           act[u] = false;
           continue;

@@ -78,6 +78,38 @@ def test_device_intern_and_cross_lookup(engine):
     assert engine.nkeys(TREG) == len(table)
 
 
+@pytest.mark.parametrize("mem", ["host", "device"])
+def test_long_keys_found_again(engine, mem):
+    """keys of every length class around the 16 bytes a table record holds,
+    interned through the device directory (> 1024 keys: no host cache), are
+    found again by a later probe -- lookup and a second intern give the same
+    slots and create nothing; then again after the table has grown (rehash).
+    (A miscompiled probe once lost every key over 16 bytes.)"""
+    import torch
+    from jylis_amd._lib import TLOG
+    from jylis_amd.engine import encode_keys
+    lens = [0, 1, 7, 8, 9, 15, 16, 17, 23, 24, 25, 31, 32, 33, 100, 1200, 4097]
+    special = [(b"%d:" % n + b"x" * n)[:n] for n in lens] + [b"long" * 300, b"abcdefghijklmnopq"]
+    filler = [b"f%d" % i for i in range(1100)]
+
+    def intern(ks, create=True):
+        if mem == "host":
+            return engine.intern(TLOG, ks) if create else engine.lookup(TLOG, ks)
+        kb, ko = encode_keys(ks)
+        return engine.intern_device(TLOG, torch.from_numpy(kb.copy()).cuda(),
+                                    torch.from_numpy(ko.astype(np.int64)).cuda(),
+                                    create=create).cpu().numpy().view(np.uint32)
+    table = {}
+    for rnd in range(3):
+        ks = special + filler + [b"grow%d-%d" % (rnd, i) for i in range(rnd * 3000)]
+        s1 = intern(ks)
+        np.testing.assert_array_equal(s1, first_occurrence(ks, table), err_msg=f"round {rnd}")
+        assert engine.nkeys(TLOG) == len(table)
+        np.testing.assert_array_equal(intern(ks, create=False), s1)
+        np.testing.assert_array_equal(intern(ks), s1)
+        assert engine.nkeys(TLOG) == len(table)
+
+
 def test_heavy_duplicates_and_growth(engine):
     """many lanes racing on the same few keys, then enough keys to rehash
     the table several times"""
