@@ -506,6 +506,8 @@ void jy_node_release(jy_node* node);
 /* GPUs visible to this process (0 without a GPU or HIP runtime) */
 int32_t jy_device_count(void);
 void jy_node_destroy(jy_node* node);
+/* the detail of the calling thread's last failed node call (per thread, like
+ * errno: the repos call one node from their own threads) */
 const char* jy_node_last_error(const jy_node* node);
 uint32_t jy_node_nshards(const jy_node* node);
 /* the engine of local shard `shard` (global index), NULL if not local */

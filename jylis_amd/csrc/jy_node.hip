@@ -462,8 +462,7 @@ struct jy_node {
   jy_node_config cfg;
   u32 S = 0, nlocal = 0, rank0 = 0, fabric = JY_FABRIC_RCCL;
   std::vector<NdShard> sh;
-  std::string err;   // callers' errors (jy_node_last_error)
-  std::string werr;  // the worker's (moved to err when a call reports it)
+  std::string werr;  // the worker's (moved to the reporting caller's when a call reports it)
   u64 stats[5] = {};
   u32 nrep = 0;  // replica columns registered (host-side checks of counter cells)
   // executor
@@ -479,8 +478,14 @@ struct jy_node {
   int32_t aerr = JY_OK;  // first failure of a queued job, reported by the next call
   std::string aerr_msg;
   NdPin pins[kJobDepth];
+  // callers' errors are per calling thread (errno-like, jy_node_last_error):
+  // the five repos of a process call one node from their own threads
+  static std::string& caller_err() {
+    static thread_local std::string e;
+    return e;
+  }
   int32_t fail(int32_t code, const std::string& m) {
-    (std::this_thread::get_id() == wid ? werr : err) = m;
+    (std::this_thread::get_id() == wid ? werr : caller_err()) = m;
     return code;
   }
 };
@@ -1158,7 +1163,7 @@ int32_t jy_device_count(void) {
   return n;
 }
 
-const char* jy_node_last_error(const jy_node* nd) { return nd ? nd->err.c_str() : "null node"; }
+const char* jy_node_last_error(const jy_node* nd) { return nd ? jy_node::caller_err().c_str() : "null node"; }
 uint32_t jy_node_nshards(const jy_node* nd) { return nd ? nd->S : 0; }
 
 jy_engine* jy_node_engine(jy_node* nd, uint32_t shard) {
@@ -1925,7 +1930,7 @@ void finish(jy_node* nd, const NdJob& j, int32_t rc) {
   if (j.pin >= 0) nd->pins[j.pin].busy = false;
   if (rc != JY_OK && nd->aerr == JY_OK) {
     nd->aerr = rc;
-    nd->aerr_msg = std::this_thread::get_id() == nd->wid ? nd->werr : nd->err;
+    nd->aerr_msg = std::this_thread::get_id() == nd->wid ? nd->werr : jy_node::caller_err();
   }
   nd->finished++;
   nd->dcv.notify_all();
@@ -1977,7 +1982,7 @@ int32_t exec_fence(jy_node* nd) {
   nd->dcv.wait(lk, [&] { return nd->finished == nd->submitted; });
   if (nd->aerr == JY_OK) return JY_OK;
   const int32_t rc = nd->aerr;
-  nd->err = nd->aerr_msg;
+  jy_node::caller_err() = nd->aerr_msg;
   nd->aerr = JY_OK;
   return rc;
 }
@@ -1987,7 +1992,7 @@ int32_t exec_pending(jy_node* nd) {
   std::lock_guard<std::mutex> lk(nd->qmu);
   if (nd->aerr == JY_OK) return JY_OK;
   const int32_t rc = nd->aerr;
-  nd->err = nd->aerr_msg;
+  jy_node::caller_err() = nd->aerr_msg;
   nd->aerr = JY_OK;
   return rc;
 }
