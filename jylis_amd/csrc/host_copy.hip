@@ -109,9 +109,7 @@ class CopyPool {
     // memcpy may use weakly ordered (non-temporal / fast-string) stores,
     // which a release store does not order: fence them, so that the DMA the
     // calling thread enqueues once it sees `done` reads the copied bytes
-#ifndef JY_COPY_NO_FENCE  // A/B only
     _mm_sfence();
-#endif
     done_[c].store(tag, std::memory_order_release);
   }
 

@@ -85,9 +85,6 @@ __device__ __forceinline__ T wave_sum(T x) {
 // published something, and stops at the nearest inclusive prefix: with the
 // predecessors' aggregates published early, a tile waits about one load.
 __device__ __forceinline__ u64 lookback(u64* status, u32 tile, u32 epoch, u64 agg, u64* lds) {
-#ifdef JY_FAKE_LOOKBACK  // A/B only: the cost of a scan without its look-back (WRONG results)
-  return 0;
-#endif
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     const u64 ep = (u64)(epoch & ((1u << kEpochBits) - 1));

@@ -150,82 +150,41 @@ __device__ __forceinline__ u32 tag_of(u64 t) { return (u32)t; }
 // K1: look every key up; misses counted with their bytes.  The counts are
 // per-workgroup partials (summed by k_key_sum): one global atomic per miss on
 // three shared words serialised ~65K misses per 1M-key batch (~0.6 ms).
-// kProbeU keys per lane, their loads issued together at every step (offsets,
-// key words, then each probe round's records).  Round 5, in-box A/B of the
-// node TREG call (8.39M keys, ms per call, 2 runs each): 1 key per lane 0.738
-// / 0.741, 2 keys 0.742 / 0.747, 4 keys 0.809 / 0.806, 8 keys 0.968 / 0.962
-// -- the extra registers cost more occupancy than the chains in flight gain.
-#ifndef JY_KEY_PROBE_U
-#define JY_KEY_PROBE_U 1
-#endif
-constexpr int kProbeU = JY_KEY_PROBE_U;
-constexpr u64 kProbeKeys = (u64)kThreads * kProbeU;  // keys per probe workgroup
+// One key per lane.  (Round 5 measured 2, 4 and 8 keys per lane with their
+// loads issued together, in-box A/B of the node TREG call, 8.39M keys, ms per
+// call: 1 key 0.738 / 0.741, 2 keys 0.742 / 0.747, 4 keys 0.809 / 0.806, 8
+// keys 0.968 / 0.962 -- the registers cost more occupancy than the chains in
+// flight gain.)
+constexpr u64 kProbeKeys = kThreads;  // keys per probe workgroup
 __global__ __launch_bounds__(kThreads) void k_key_probe(In I, Dir D, u32* __restrict__ res, u64* __restrict__ th,
                                                         u64* __restrict__ parts) {
   __shared__ u64 red[3][kThreads / 64];
-  constexpr int U = kProbeU;
   u64 c[3] = {0, 0, 0};
-  u64 i[U], a[U], len[U], t[U], p[U];
-  KeyW kw[U];
-  bool act[U];
-  u32 slot[U];
-#pragma unroll
-  for (int u = 0; u < U; u++) {
-    i[u] = (u64)blockIdx.x * kProbeKeys + (u64)u * kThreads + threadIdx.x;
-    act[u] = i[u] < I.n;
-    a[u] = len[u] = 0;
-    if (act[u]) {
-      a[u] = I.ko[i[u]];
-      len[u] = I.ko[i[u] + 1] - a[u];
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < U; u++) kw[u] = act[u] ? key_words(I.kb + a[u], len[u]) : KeyW{0, 0};
-#pragma unroll
-  for (int u = 0; u < U; u++) {
-    slot[u] = kMiss;
-    t[u] = p[u] = 0;
-    if (act[u]) {
-      t[u] = table_hash(I.kb + a[u], len[u], kw[u]);
-      th[i[u]] = t[u];
-      p[u] = t[u] >> D.shift;
-    }
-  }
-  for (;;) {
-    TRec r[U];
-#pragma unroll
-    for (int u = 0; u < U; u++)
-      if (act[u]) r[u] = load_rec(D.table, p[u]);
-    bool more = false;
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      if (!act[u]) continue;
-      if (r[u].e == kEmpty) {
-        act[u] = false;
-        continue;
-      }
-      if ((u32)(r[u].e >> 32) == tag_of(t[u]) && !(r[u].e & kPending) && r[u].len == len[u] && r[u].w0 == kw[u].w0 &&
-          r[u].w1 == kw[u].w1) {
-        const u32 s = (u32)(r[u].e & kIdxMask);
-        if (len[u] <= 16 || key_tail_equal(D.bytes + (D.kref[s] >> JY_LR_LEN_BITS), I.kb + a[u], len[u])) {
-          slot[u] = s;
-          act[u] = false;
-          continue;
+  const u64 i = gid();
+  if (i < I.n) {
+    const u64 a = I.ko[i], len = I.ko[i + 1] - a;
+    const KeyW kw = key_words(I.kb + a, len);
+    const u64 t = table_hash(I.kb + a, len, kw);
+    th[i] = t;
+    u64 p = t >> D.shift;
+    u32 slot = kMiss;
+    for (;;) {
+      const TRec r = load_rec(D.table, p);
+      if (r.e == kEmpty) break;
+      if ((u32)(r.e >> 32) == tag_of(t) && !(r.e & kPending) && r.len == len && r.w0 == kw.w0 && r.w1 == kw.w1) {
+        const u32 s = (u32)(r.e & kIdxMask);
+        if (len <= 16 || key_tail_equal(D.bytes + (D.kref[s] >> JY_LR_LEN_BITS), I.kb + a, len)) {
+          slot = s;
+          break;
         }
       }
-      p[u] = (p[u] + 1) & D.mask;
-      more = true;
+      p = (p + 1) & D.mask;
     }
-    if (!more) break;
-  }
-#pragma unroll
-  for (int u = 0; u < U; u++) {
-    if (i[u] >= I.n) continue;
-    res[i[u]] = slot[u];
-    if (slot[u] == kMiss) {
-      c[0] += 1;
-      c[1] += len[u];
-      c[2] += len[u] > JY_LR_LEN_MASK;
+    res[i] = slot;
+    if (slot == kMiss) {
+      c[0] = 1;
+      c[1] = len;
+      c[2] = len > JY_LR_LEN_MASK;
     }
   }
   const int w = threadIdx.x >> 6;
@@ -243,24 +202,19 @@ __global__ __launch_bounds__(kThreads) void k_key_probe(In I, Dir D, u32* __rest
   }
 }
 
-// one workgroup: the probe's partials into counts[3] (misses, their bytes, oversized keys)
-// one workgroup of 1024 sums the [nb][3] partials: each thread walks whole
-// rows (the three quantities at once), 4 rows in flight per step (a
-// 256-thread form summing one quantity per sweep took 80 us at 35K rows)
-constexpr int kSumThreads = 1024;
+// the probe's [nb][3] partials (misses, their bytes, oversized keys) summed
+// by kSumGroups workgroups of 256 into [kSumGroups][3]; the host adds those
+// up with its read-back.  (One workgroup of 1024 walking all the rows took 19
+// us at 32.8K rows, the node TREG call's 8.39M keys: its loads wait in line.)
+constexpr int kSumThreads = 256;
+constexpr u32 kSumGroups = 128;
 __global__ __launch_bounds__(kSumThreads) void k_key_sum(const u64* __restrict__ parts, u64 nb,
                                                          u64* __restrict__ counts) {
   __shared__ u64 red[3][kSumThreads / 64];
   u64 v[3] = {0, 0, 0};
-  for (u64 b0 = threadIdx.x; b0 < nb; b0 += 4 * kSumThreads) {
+  for (u64 b = (u64)blockIdx.x * kSumThreads + threadIdx.x; b < nb; b += (u64)gridDim.x * kSumThreads) {
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const u64 b = b0 + (u64)u * kSumThreads;
-      if (b < nb) {
-#pragma unroll
-        for (int q = 0; q < 3; q++) v[q] += parts[b * 3 + q];
-      }
-    }
+    for (int q = 0; q < 3; q++) v[q] += parts[b * 3 + q];
   }
 #pragma unroll
   for (int q = 0; q < 3; q++) {
@@ -271,7 +225,7 @@ __global__ __launch_bounds__(kSumThreads) void k_key_sum(const u64* __restrict__
   if (threadIdx.x < 3) {
     u64 t = 0;
     for (int w = 0; w < kSumThreads / 64; w++) t += red[threadIdx.x][w];
-    counts[threadIdx.x] = t;
+    counts[(u64)blockIdx.x * 3 + threadIdx.x] = t;
   }
 }
 
@@ -338,17 +292,14 @@ __global__ __launch_bounds__(kThreads) void k_key_flags(In I, const u32* __restr
 
 // K4: slots out; first occurrences store their key; claimers publish
 __global__ __launch_bounds__(kThreads) void k_key_commit(In I, Dir D, uint8_t* __restrict__ dbytes, u64 base_slot,
-                                                         u64 base_byte, const u32* __restrict__ res,
+                                                         u64 base_byte, const u32* res,  // (res aliases slots)
                                                          const u64* __restrict__ th, const u32* __restrict__ owner,
                                                          const u64* __restrict__ pos, const u32* __restrict__ first,
                                                          const u32* __restrict__ rank, const u64* __restrict__ boff,
-                                                         u32* __restrict__ slots) {
+                                                         u32* slots) {
   const u64 i = gid();
   if (i >= I.n) return;
-  if (res[i] != kMiss) {
-    slots[i] = res[i];
-    return;
-  }
+  if (res[i] != kMiss) return;  // found by the probe, already in slots[i]
   const u32 o = owner[i];
   const u32 f = first[o];
   const u64 slot = base_slot + rank[f];
@@ -370,12 +321,6 @@ __global__ __launch_bounds__(kThreads) void k_key_commit(In I, Dir D, uint8_t* _
     r.w1 = kw.w1;
     r.e = ((u64)tag_of(th[i]) << 32) | slot;
   }
-}
-
-// lookup only: slots of present keys, JY_NO_SLOT otherwise
-__global__ __launch_bounds__(kThreads) void k_key_copy_res(u64 n, const u32* __restrict__ res, u32* __restrict__ out) {
-  const u64 i = gid();
-  if (i < n) out[i] = res[i];
 }
 
 // rebuild the table from the per-slot hashes
@@ -483,10 +428,14 @@ int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, co
   JY_TRY(grow_slots(eng, K, std::max<u64>(K.n, 1)));
   JY_TRY(grow_table(eng, K, std::max<u64>(K.n, 1)));
   void* p;
-  JY_TRY(jy_scratch(eng, 20, n * 4 + n * 8 + 64, &p));
-  u32* res = static_cast<u32*>(p);
-  u64* th = reinterpret_cast<u64*>((reinterpret_cast<uintptr_t>(res + n) + 15) & ~uintptr_t(15));
-  u64* counts = th + n;  // [3] misses, their bytes, oversized keys
+  JY_TRY(jy_scratch(eng, 20, n * 8 + kSumGroups * 24 + 64, &p));
+  // the probe's answers go straight to the caller's slots (a found key's slot
+  // or kMiss): every later kernel reads and rewrites index i in the same
+  // thread, so a lookup, or an intern that finds every key, is done after the
+  // probe (no copy of n words: 19 us at 8.39M keys)
+  u32* res = slots;
+  u64* th = static_cast<u64*>(p);
+  u64* counts = th + n;  // [sum groups][3] misses, their bytes, oversized keys
   In I{kb, ko, n};
   const u64 nb = (n + kProbeKeys - 1) / kProbeKeys;
   void* pp;
@@ -494,20 +443,21 @@ int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, co
   u64* parts = static_cast<u64*>(pp);
   hipLaunchKernelGGL(k_key_probe, dim3((u32)nb), dim3(kThreads), 0, eng->stream, I, dir_of(K), res, th, parts);
   JY_HIP(eng, hipGetLastError());
-  hipLaunchKernelGGL(k_key_sum, dim3(1), dim3(kSumThreads), 0, eng->stream, parts, nb, counts);
+  const u32 ng = (u32)std::min<u64>(kSumGroups, (nb + kSumThreads - 1) / kSumThreads);
+  hipLaunchKernelGGL(k_key_sum, dim3(ng), dim3(kSumThreads), 0, eng->stream, parts, nb, counts);
   JY_HIP(eng, hipGetLastError());
   if (after_probe) JY_TRY(after_probe(arg));  // (a pageable read-back below may block at once)
-  u64 hc[3];
-  JY_HIP(eng, hipMemcpyAsync(hc, counts, 24, hipMemcpyDeviceToHost, eng->stream));
+  u64 hg[kSumGroups * 3];
+  JY_HIP(eng, hipMemcpyAsync(hg, counts, ng * 24, hipMemcpyDeviceToHost, eng->stream));
   const double t0 = jy_tracing() ? jy_now_us() : 0;
   JY_HIP(eng, hipStreamSynchronize(eng->stream));
   JY_TRACE("keydir %llu keys: probe counts after %.1f us of waiting", (unsigned long long)n, jy_now_us() - t0);
+  u64 hc[3] = {0, 0, 0};
+  for (u32 g = 0; g < ng; g++)
+    for (int q = 0; q < 3; q++) hc[q] += hg[g * 3 + q];
   const u64 m = hc[0], mbytes = hc[1];
   JY_TRACE("keydir %llu keys: %llu misses (create %d)", (unsigned long long)n, (unsigned long long)m, (int)create);
-  if (!create || m == 0) {
-    LAUNCH(k_key_copy_res, n, n, res, slots);
-    return JY_OK;
-  }
+  if (!create || m == 0) return JY_OK;  // (a miss's kMiss is JY_NO_SLOT)
   if (hc[2]) return eng->fail(JY_ERANGE, "key longer than 16 MiB");
   if (K.n + m >= kIdxMask) return eng->fail(JY_ERANGE, "slot space exhausted");
   JY_TRY(grow_table(eng, K, K.n + m));

@@ -162,37 +162,6 @@ __global__ __launch_bounds__(kThreads) void k_tlog_prep(TlogArgs A) {
   }
 }
 
-// first position in [lo, hi) of the log at pool[base..] whose timestamp is
-// >= x (the log ascends): 16-ary probes, every probe of a round loaded at
-// once -- one round trip for a log of <= 16 entries, two up to 256.
-// at_ts: the timestamp at the returned position (every position a round
-// narrows to was probed: the last round probes all of [lo, hi), and a
-// narrowed hi is a block end probed >= x), or ~0 when it is hi
-constexpr u32 kProbe = 16;
-[[maybe_unused]] __device__ __forceinline__ u32 ts_lower(const TRec* __restrict__ pool, u64 base, u32 lo, u32 hi, u64 x, u64& at_ts) {
-  at_ts = ~0ull;
-  while (hi > lo) {
-    const u32 n = hi - lo;
-    const u32 step = (n + kProbe - 1) / kProbe;  // probe i looks at lo + i * step + step - 1
-    u32 c = 0;
-#pragma unroll
-    for (u32 i = 0; i < kProbe; i++) {
-      const u32 at = lo + i * step + step - 1;
-      if (at < hi) {
-        const u64 v = pool[base + at].ts;
-        c += v < x;
-        if (v >= x && v < at_ts) at_ts = v;  // ascending: the smallest probe >= x is the first one
-      }
-    }
-    // c whole blocks of `step` lie below x; the answer is inside block c
-    const u32 nlo = lo + c * step;
-    if (step == 1) return nlo;
-    hi = nlo + step - 1 < hi ? nlo + step - 1 : hi;  // the block's last entry was probed >= x (or is hi)
-    lo = nlo;
-  }
-  return lo;
-}
-
 // first position in [lo, hi) of a log whose timestamps ascend from `tlo`
 // (at lo) to `thi` (at hi - 1) with timestamp >= x.  Timestamps follow wall
 // time, so an interpolated guess and one window of kWin entries around it
@@ -267,9 +236,6 @@ constexpr int kFastEnt = 4;  // delta entries a key may have for the lane-per-ke
 // (a next-pass prefetch of stage 2's entry measured no gain in round 4: 0.837
 // / 0.841 ms without, 0.865 with at 6 waves per SIMD (spills), 0.834 / 0.836
 // at 5 waves; removed)
-#ifndef JY_TLOG_CUT_PROBE
-#define JY_TLOG_CUT_PROBE 0  // 1: the cutoff drop by 16-ary probes (round 3)
-#endif
 constexpr int kCache = JY_TLOG_KCACHE;  // passes of slow entries kept in registers for the append stores
 
 constexpr u32 kKept = 0x80000000u;  // eqx: kept flag | # kept entries of the key before this one
@@ -365,16 +331,11 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
       u32 drop = 0;
       u64 oldest = 0;
       if (cd > m.cut && m.len > 0) {
-#if JY_TLOG_CUT_PROBE
-        drop = ts_lower(A.pool, m.base, 0, m.len, cut, oldest);  // oldest first: a prefix
-        if (drop == m.len) oldest = 0;
-#else
         // the interpolated search from the hint (one window of 1-2 lines; the
         // 16-ary probes read 16 lines a round), then the new oldest entry --
         // inside the window, a cache hit
         drop = ts_interp(A.pool, m.base, 0, m.len, hv, m.newest, cut);  // oldest first: a prefix
         oldest = drop < m.len ? A.pool[m.base + drop].ts : 0;
-#endif
       } else if (m.len > 0) {
         oldest = hv;  // the hint (round 3 loaded pool[base].ts here: one dependent random line per slow key)
       }
@@ -403,11 +364,7 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
     if (tid == 0) l_soff[nt] = (u32)tot;
   }
   __syncthreads();
-#ifdef JY_TLOG_AB_NOSLOW  // A/B only: the cost of stage 1 alone (WRONG results)
-  const u64 F = 0;
-#else
   const u64 F = l_soff[nt];
-#endif
   // 2. slow entries, one per lane per pass
   u32 carry = 0;
   constexpr int kCacheN = kCache > 0 ? kCache : 1;

@@ -1001,10 +1001,7 @@ __global__ __launch_bounds__(kThreads) void k_uj_sizes(UjArgs A, u64 ndt) {
 // in-box A/B, ms per config-5 converge, 2 runs each: 1 item per lane 0.380 /
 // 0.382, 2 items 0.381 / 0.381, 4 items 0.382 / 0.382 -- more chains in
 // flight per wave do not help: 1.)
-#ifndef JY_UJ_SCATTER_U
-#define JY_UJ_SCATTER_U 1
-#endif
-constexpr int kScatterU = JY_UJ_SCATTER_U;
+constexpr int kScatterU = 1;  // (the loop form below is kept: the compiler's code for it measured faster)
 constexpr int kScatterThreads = (int)kTile / kScatterU;
 
 struct ScOut {
@@ -1542,9 +1539,8 @@ int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* sl
   hipLaunchKernelGGL(k_uj_docs, dim3((u32)g1), dim3(kThreads), 0, eng->stream, A, ndt, (nel + kTile1 - 1) / kTile1,
                      (ncloud + kTile1 - 1) / kTile1, (nvv + kTile1 - 1) / kTile1);
   // grids from the newest finished converge's touched sizes (+25 %), never above the safe bound
-  static const bool safe_grid = getenv("JY_UJ_SAFE_GRID") != nullptr;  // A/B: the bound's grid
-  const u64 pa = u.has_pred && !safe_grid ? std::min(le, u.pred_ta + u.pred_ta / 4 + 4096) : le;
-  const u64 pc = u.has_pred && !safe_grid ? std::min(lc, u.pred_tc + u.pred_tc / 4 + 4096) : lc;
+  const u64 pa = u.has_pred ? std::min(le, u.pred_ta + u.pred_ta / 4 + 4096) : le;
+  const u64 pc = u.has_pred ? std::min(lc, u.pred_tc + u.pred_tc / 4 + 4096) : lc;
   const u64 gf = cdiv_h(pa) + cdiv_h(nel) + cdiv_h(ncloud) + 2;
   const u64 gk = cdiv_h(pc) + cdiv_h(ncloud) + 2;
   hipLaunchKernelGGL(k_uj_flags, dim3((u32)gf), dim3(kItemThreads), 0, eng->stream, A);
