@@ -60,7 +60,6 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr u32 kNone = 0xFFFFFFFFu;
 
 __device__ __forceinline__ u64 gid() { return (u64)blockIdx.x * kThreads + threadIdx.x; }
 
@@ -131,7 +130,8 @@ struct TlogArgs {
   const u64* dpre;
   const u64* dlr;
   // temporaries
-  u32* dptr;      // [nkeys] delta key merging into each slot
+  u64* dptr;      // [nkeys] epoch << 32 | the delta key merging into each slot (last claimer)
+  u32 epoch;      // this merge's claim epoch (never 0)
   u32* bad;       // [nd] repeated slot in the batch
   PInfo* pinfo;   // [nd] written for rebuilt and inserted keys only
   u32* rz;        // [nd + 1] pool entries a rebuilt key takes (0 otherwise)
@@ -148,17 +148,20 @@ struct TlogArgs {
 
 // A slot named twice in one device batch breaks the one-delta-per-key
 // contract: both deltas are skipped (counted once), the key is left untouched.
-// dptr[] is all kNone on entry (k_tlog_commit restores that after the
-// merge's last reader, k_tlog_tile); bad[] is cleared before this launch.
+// The claims carry the merge's epoch, so nothing resets them: a claimer that
+// finds this epoch's tag marks itself and the key it displaced (with three or
+// more copies every copy is marked by the next one).  bad[] is cleared before
+// this launch.
 __global__ __launch_bounds__(kThreads) void k_tlog_prep(TlogArgs A) {
   const u64 k = gid();
   if (k >= A.nd) return;
   const u32 s = A.slot[k];
   if (s == JY_NO_SLOT) return;  // a hole of a routed run (k_route_csr.hip)
-  const u32 prev = atomicCAS(A.dptr + s, kNone, (u32)k);
-  if (prev != kNone) {
+  const u64 tag = (u64)A.epoch << 32;
+  const u64 prev = atomicExch(reinterpret_cast<unsigned long long*>(A.dptr + s), (unsigned long long)(tag | k));
+  if ((prev & ~0xFFFFFFFFull) == tag) {
     A.bad[k] = 1;
-    A.bad[prev] = 1;
+    A.bad[(u32)prev] = 1;
   }
 }
 
@@ -451,7 +454,8 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
     P.s = l_slot[tid];
     if (l_bad[tid]) {
       mode = kSkip;
-      if (P.s != JY_NO_SLOT && A.dptr[P.s] == (u32)k) atomicAdd(A.skipped, 1ull);  // once per slot
+      // once per slot: the last claimer counts it
+      if (P.s != JY_NO_SLOT && A.dptr[P.s] == (((u64)A.epoch << 32) | k)) atomicAdd(A.skipped, 1ull);
     } else {
       const u32 len = l_len[tid], drop = l_drop[tid], M = l_M[tid];
       const u32 surv = len - drop;
@@ -552,11 +556,7 @@ __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __
   const u32 nt = (u32)(A.nd - k0 < kTile ? A.nd - k0 : kTile);
   u32 cap = tid < nt ? A.rz[k0 + tid] : 0u;
   const u32 ins = tid < nt ? A.ins[k0 + tid] : 0u;
-  u32 s = JY_NO_SLOT;
-  if (tid < nt) {  // the batch's slot claims back to kNone (k_tlog_tile, their last reader, is done)
-    s = A.slot[k0 + tid];
-    if (s != JY_NO_SLOT) A.dptr[s] = kNone;  // every copy of a repeated slot writes the same value
-  }
+  // (the slot claims carry the merge's epoch: nothing to release here)
   // the pool check (uniform: k_tlog_bump moves ctr only after every tile)
   if (ctr[0] + rtile[gridDim.x] > A.pcap) {
     // no room for this merge's rebuilt logs: they stay as they are and their
@@ -564,7 +564,7 @@ __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __
     if (tid < nt) {
       const u64 k = k0 + tid;
       const u64 b0 = A.doff[k], b1 = A.doff[k + 1];
-      A.sp_slot[k] = cap ? s : JY_NO_SLOT;
+      A.sp_slot[k] = cap ? A.slot[k] : JY_NO_SLOT;
       A.sp_cut[k] = A.dcut[k];
       A.sp_off[k] = b0;
       if (k + 1 == A.nd) A.sp_off[A.nd] = b1;
@@ -1055,19 +1055,6 @@ int32_t jy_tlog_merge(jy_engine* eng, u64 nd, const u32* slot, const u64* dcut, 
 
 namespace {
 
-// the slot claims a merge takes in k_tlog_prep are released by k_tlog_commit;
-// an error exit between the two releases them here (every later merge would
-// otherwise find those slots claimed and skip them)
-struct ClaimGuard {
-  jy_engine* eng;
-  u32* dptr;
-  u64 nk;
-  bool armed = true;
-  ~ClaimGuard() {
-    if (armed) (void)hipMemsetAsync(dptr, 0xFF, nk * 4, eng->stream);
-  }
-};
-
 // spill buffer views of ring slot r sized for (nd, nent)
 int32_t spill_reserve(jy_engine* eng, TlogState::Spill& sp, u64 nd, u64 nent) {
   const u64 bytes = ((nd * 4 + 15) & ~15ull) + (2 * nd + 1) * 8 + 3 * std::max<u64>(nent, 1) * 8 + 64;
@@ -1127,16 +1114,21 @@ int32_t tlog_launch(jy_engine* eng, TlogState& t, int r, u64 nd, const u32* slot
   void* p;
   {
     DevArray& c = eng->tl_claim;
-    if (c.bytes < nk * 4) {  // grows rarely: the whole array (re)set to kNone once
-      const u64 nb = std::max<u64>(nk * 4, c.bytes * 2);
+    if (c.bytes < nk * 8) {  // grows rarely: the whole array (re)set to epoch 0 once
+      const u64 nb = std::max<u64>(nk * 8, c.bytes * 2);
       jy_dev_free(eng, c.p);
       c.p = nullptr;
       c.bytes = 0;
       JY_TRY(jy_dev_alloc(eng, &c.p, nb, "tlog slot claims"));
       c.bytes = nb;
-      JY_HIP(eng, hipMemsetAsync(c.p, 0xFF, nb, eng->stream));
+      JY_HIP(eng, hipMemsetAsync(c.p, 0, nb, eng->stream));
     }
-    A.dptr = static_cast<u32*>(c.p);
+    if (++eng->tl_epoch == 0) {  // wrapped: no old tag may match a new epoch
+      JY_HIP(eng, hipMemsetAsync(c.p, 0, c.bytes, eng->stream));
+      eng->tl_epoch = 1;
+    }
+    A.dptr = static_cast<u64*>(c.p);
+    A.epoch = eng->tl_epoch;
   }
   JY_TRY(jy_scratch(eng, 9, nd * (sizeof(PInfo) + 12) + 64, &p));
   A.pinfo = static_cast<PInfo*>(p);
@@ -1152,7 +1144,6 @@ int32_t tlog_launch(jy_engine* eng, TlogState& t, int r, u64 nd, const u32* slot
   JY_HIP(eng, hipMemsetAsync(A.bad, 0, nd * 4, eng->stream));
   JY_HIP(eng, hipMemsetAsync(A.rsum + tiles, 0, 8, eng->stream));
   LAUNCH(k_tlog_prep, nd, A);
-  ClaimGuard guard{eng, A.dptr, nk};
   A.meta = t.meta;
   A.hint = t.hint;
   A.pool = t.pool;
@@ -1164,7 +1155,6 @@ int32_t tlog_launch(jy_engine* eng, TlogState& t, int r, u64 nd, const u32* slot
                                                 jydscan::StArr<u64>{A.rsum})));
   hipLaunchKernelGGL(k_tlog_commit, dim3(tiles), dim3(kTile), 0, eng->stream, A, A.rsum, t.ctr, t.pool, erank, eqx);
   JY_HIP(eng, hipGetLastError());
-  guard.armed = false;  // k_tlog_commit released the claims
   hipLaunchKernelGGL(k_tlog_bump, dim3(1), dim3(1), 0, eng->stream, t.ctr, A.rsum, (u64)tiles, t.pcap,
                      t.pin_dev + 8 + 4 * r);
   JY_HIP(eng, hipGetLastError());
