@@ -29,11 +29,12 @@
 //   k_tlog_prep    repeated slots in the batch (both copies skipped)
 //   k_tlog_tile    validate (strictly newest first), cutoff drop, kept flag
 //                  and state rank per entry (no search for the usual entry,
-//                  newer than the log), append or rebuild per key; appends
-//                  are written at the tail here
-//   k_tlog_commit  publish the new meta; rebuilt keys are written into the
-//                  fresh space the scan of their sizes gave them, one lane
-//                  per output entry (merge-path positions from the ranks)
+//                  newer than the log), append / insert / rebuild per key;
+//                  appends are written at the tail and in-place inserts
+//                  moved here
+//   k_tlog_commit  rebuilt keys are written into the fresh space the scan of
+//                  their sizes gave them, one lane per output entry
+//                  (merge-path positions from the ranks), metas published
 // Pool space for rebuilt keys is only known on the device after that scan,
 // so the host never waits for it: k_tlog_commit checks on the device that the
 // rebuilt logs fit the pool.  If they do not, those keys are left untouched
@@ -101,8 +102,8 @@ __device__ __forceinline__ TRec load_rec(const TRec* __restrict__ p) {
 
 enum : u32 { kSkip = 0, kAppend = 1, kRebuild = 2, kFast = 3, kInsert = 4 };
 
-// per REBUILT key (a worklist entry): what k_tlog_tile decided; the log's
-// current base is read from its meta at commit (a compaction may move it)
+// per REBUILT key: what k_tlog_tile decided; the log's current base is read
+// from its meta at commit
 struct alignas(16) PInfo {
   u64 newest;  // newest ts after the merge
   u64 cut;     // merged cutoff
@@ -111,9 +112,7 @@ struct alignas(16) PInfo {
   u32 len;     // old length
   u32 drop;    // state entries dropped by the cutoff (a prefix)
   u32 newlen;  // entries after the merge
-  u32 cap;     // the new segment's capacity (rebuild) or the old one (insert)
-  u32 minrank; // insert: the first log position that moves
-  u32 ins;     // 1: inserted in place (the segment has room), 0: rebuilt
+  u32 cap;     // the new segment's capacity
 };
 
 struct TlogArgs {
@@ -135,7 +134,6 @@ struct TlogArgs {
   u32* bad;       // [nd] repeated slot in the batch
   PInfo* pinfo;   // [nd] written for rebuilt and inserted keys only
   u32* rz;        // [nd + 1] pool entries a rebuilt key takes (0 otherwise)
-  u32* ins;       // [nd] 1: the key's delta interleaves with its log and fits its segment
   u64* rsum;      // [tiles + 1] rebuilt pool entries per key tile (scanned in place before k_tlog_commit)
   unsigned long long* skipped;
   // the device-side pool check: when the rebuilt logs do not fit pcap, the
@@ -480,17 +478,13 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
         mode = kAppend;
         A.meta[P.s] = TMeta{l_base[tid] + drop, P.newlen, l_cap[tid] - drop, P.cut, nn};
       } else if ((u64)len + M <= l_cap[tid]) {
-        // interleaves, but the segment has room: k_tlog_commit shifts the
-        // log's suffix from minrank up in place (no fresh space)
+        // interleaves, but the segment has room: the log's suffix from
+        // minrank moves up in place (no fresh space)
         mode = kInsert;
-        P.cap = l_cap[tid];
-        P.minrank = l_minrank[tid];
-        P.ins = 1;
-        A.pinfo[k] = P;
+        A.meta[P.s] = TMeta{l_base[tid] + drop, P.newlen, l_cap[tid] - drop, P.cut, nn};  // moved in stage 5
       } else {
         mode = kRebuild;
         P.cap = pow2_cap(surv + M);
-        P.ins = 0;
         A.pinfo[k] = P;
       }
     }
@@ -498,7 +492,6 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
   }
   if (tid < nt) {
     A.rz[k0 + tid] = mode == kRebuild ? P.cap : 0u;
-    A.ins[k0 + tid] = mode == kInsert;
   }
   {  // the tile's rebuilt space: k_tlog_commit offsets its keys from the scan of these
     const u64 r = jyscan::wave_sum<u64>(tid < nt && mode == kRebuild ? (u64)P.cap : 0ull);
@@ -529,6 +522,79 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
     const u64 tail = l_base[idx] + l_len[idx] + l_M[idx] - 1;
     store_rec(pool + tail - (qx & ~kKept), t, pp, ll);
   }
+  // 5. in-place inserts: each insert key's delta entries, then its state
+  //    entries from minrank, flattened (a wave scan of their counts) and
+  //    moved from the last item down -- one wave, so a pass's loads all
+  //    return before its stores, and a state entry only moves up: every
+  //    entry is read before anything is written over it (as k_tlog_commit
+  //    did it for these keys).  The key's ranks and q words are this pass's
+  //    own stage-2 stores, read back after the workgroup barrier.
+  //      delta entry j: (rank_j - drop) + (M - 1 - q_j), if kept
+  //      state entry i: (i - drop) + #kept deltas with rank <= i
+  //    relative to the log's new base (base + drop).  Reads and writes both
+  //    go through `pool`.
+  {
+    u32 w = 0, ne = 0;
+    if (tid < nt && l_mode[tid] == kInsert) {
+      ne = l_soff[tid + 1] - l_soff[tid];  // an insert key walked every entry (stage 2)
+      w = ne + (l_len[tid] - l_minrank[tid]);
+    }
+    const u32 winc = jyscan::wave_incl<u32>(w);
+    const u32 wtot = __shfl(winc, 63);
+    __syncthreads();  // stage 4's reads of l_soff are done
+    if (tid < nt) {
+      l_soff[tid] = winc - w;  // reused: the keys' first items
+      l_gstart[tid] = ne;      // reused: their delta entry counts
+    }
+    if (tid == 0) l_soff[nt] = wtot;
+    __syncthreads();
+    for (long long c0 = wtot ? (long long)((wtot - 1) / kTile) * kTile : -1; c0 >= 0; c0 -= kTile) {
+      const u32 item = (u32)c0 + tid;
+      bool write = false;
+      u64 at = 0;
+      TRec x{};
+      if (item < wtot) {
+        const u32 a = lds_last_le(l_soff, nt - 1, item);
+        const u32 r = item - l_soff[a], nek = l_gstart[a], drop = l_drop[a], M = l_M[a];
+        const u64 jb = gb0 + l_gb[a], dst = l_base[a] + drop;
+        if (r < nek) {
+          const u64 j = jb + r;
+          const u32 qx = eqx[j], rank = erank[j];
+          x.ts = A.dts[j];
+          x.pre = A.dpre[j];
+          x.lr = A.dlr[j];
+          write = (qx & kKept) != 0;
+          at = dst + (u64)(rank - drop) + (M - 1 - (qx & ~kKept));
+        } else {
+          const u64 i = l_minrank[a] + (r - nek);
+          x = load_rec(pool + l_base[a] + i);
+          // the first delta entry with rank <= i (ranks fall along the
+          // newest-first segment): a short segment counted at once, a long
+          // one bisected
+          u64 lo = jb, hi = jb + nek;
+          if (hi - lo <= 4) {
+            u32 rk[4];
+#pragma unroll
+            for (u64 q = 0; q < 4; q++) rk[q] = lo + q < hi ? erank[lo + q] : 0u;
+            u64 c = 0;
+#pragma unroll
+            for (u64 q = 0; q < 4; q++) c += (lo + q < hi) & (rk[q] > i);
+            lo += c;
+          } else {
+            while (lo < hi) {
+              const u64 m = (lo + hi) >> 1;
+              if (erank[m] <= i) hi = m;
+              else lo = m + 1;
+            }
+          }
+          const u32 q = lo < jb + nek ? (eqx[lo] & ~kKept) : 0u;
+          write = true;
+          at = dst + (i - drop) + (lo < jb + nek ? M - q : 0u);
+        }
+      }
+      if (write) store_rec(pool + at, x.ts, x.pre, x.lr);
+    }
+  }
 }
 
 // KEY TILES again, after the scan of rebuilt sizes (tiles without a rebuilt
@@ -538,25 +604,20 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
 //     the newest-first delta segment, so that is M - q of the first entry
 //     with rank <= i (binary search)
 //   kept delta entry j: (rank_j - drop) + (M - 1 - q_j)
-// relative to the log's new base.  REBUILT keys write every survivor into
-// fresh space.  INSERTED keys (the delta interleaves, the segment has room)
-// stay in place: only the suffix from minrank moves up.  Their items go
-// delta entries first, and the passes run from the last item down, so every
-// state entry is read (in its own pass, or an earlier one) before anything
-// is written over it: a pass's loads all return before its stores (one wave),
-// and a state entry only moves up.
+// relative to the log's new base: every survivor of a REBUILT key into fresh
+// space.  (In-place inserts are k_tlog_tile's stage 5 since round 5: the
+// commit re-loaded each insert key's plan, meta, delta entries and ranks,
+// and nearly every 64-key tile of config 4 has one.)
 __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __restrict__ rtile,
                                                        const u64* __restrict__ ctr, TRec* __restrict__ pool,
                                                        const u32* __restrict__ erank, const u32* __restrict__ eqx) {
   __shared__ u64 l_woff[kTile + 1];
   __shared__ u64 l_src[kTile], l_dst[kTile], l_blo[kTile], l_bhi[kTile];
-  __shared__ u32 l_drop[kTile], l_s0[kTile], l_ns[kTile], l_M[kTile], l_dfirst[kTile];
+  __shared__ u32 l_drop[kTile], l_s0[kTile], l_ns[kTile], l_M[kTile];
   const u32 tid = threadIdx.x;
   const u64 k0 = (u64)blockIdx.x * kTile;
   const u32 nt = (u32)(A.nd - k0 < kTile ? A.nd - k0 : kTile);
   u32 cap = tid < nt ? A.rz[k0 + tid] : 0u;
-  const u32 ins = tid < nt ? A.ins[k0 + tid] : 0u;
-  // (the slot claims carry the merge's epoch: nothing to release here)
   // the pool check (uniform: k_tlog_bump moves ctr only after every tile)
   if (ctr[0] + rtile[gridDim.x] > A.pcap) {
     // no room for this merge's rebuilt logs: they stay as they are and their
@@ -575,27 +636,26 @@ __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __
           A.sp_lr[j] = A.dlr[j];
         }
     }
-    cap = 0;  // in-place inserts still go ahead
+    cap = 0;
   }
-  if (__ballot(cap != 0 || ins != 0) == 0) return;
+  if (__ballot(cap != 0) == 0) return;
   const u64 roff_k = rtile[blockIdx.x] + jyscan::wave_incl<u64>(cap) - cap;  // the key's rebuilt space
   u32 w = 0;
-  if (cap || ins) {
+  if (cap) {
     const u64 k = k0 + tid;
     const PInfo P = A.pinfo[k];
-    const u64 src = A.meta[P.s].base;  // current (a compaction may have moved the log)
-    const u64 dst = ins ? src + P.drop : ctr[0] + roff_k;
-    A.meta[P.s] = TMeta{dst, P.newlen, ins ? P.cap - P.drop : P.cap, P.cut, P.newest};
+    const u64 src = A.meta[P.s].base;
+    const u64 dst = ctr[0] + roff_k;
+    A.meta[P.s] = TMeta{dst, P.newlen, P.cap, P.cut, P.newest};
     const u64 blo = A.doff[k], bhi = A.doff[k + 1];
     l_src[tid] = src;
     l_dst[tid] = dst;
     l_blo[tid] = blo;
     l_bhi[tid] = bhi;
     l_drop[tid] = P.drop;
-    l_s0[tid] = ins ? P.minrank : P.drop;
-    l_ns[tid] = P.len - (ins ? P.minrank : P.drop);
+    l_s0[tid] = P.drop;
+    l_ns[tid] = P.len - P.drop;
     l_M[tid] = P.newlen - (P.len - P.drop);
-    l_dfirst[tid] = ins;
     w = l_ns[tid] + (u32)(bhi - blo);
   }
   const u32 winc = jyscan::wave_incl<u32>(w);  // a key tile is one wave
@@ -630,16 +690,9 @@ __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __
       }
       c.a = a;
       const u32 r = item - (u32)l_woff[a];
-      const u32 nd = (u32)(l_bhi[a] - l_blo[a]);
-      if (l_dfirst[a]) {
-        c.st = r >= nd;
-        c.i = l_s0[a] + (r - nd);
-        c.j = l_blo[a] + r;
-      } else {
-        c.st = r < l_ns[a];
-        c.i = l_s0[a] + r;
-        c.j = l_blo[a] + (r - l_ns[a]);
-      }
+      c.st = r < l_ns[a];
+      c.i = l_s0[a] + r;
+      c.j = l_blo[a] + (r - l_ns[a]);
       if (c.st) {
         c.x = load_rec(A.pool + l_src[a] + c.i);
       } else {
@@ -1134,7 +1187,6 @@ int32_t tlog_launch(jy_engine* eng, TlogState& t, int r, u64 nd, const u32* slot
   A.pinfo = static_cast<PInfo*>(p);
   A.bad = reinterpret_cast<u32*>(A.pinfo + nd);
   A.rz = A.bad + nd;
-  A.ins = A.rz + nd + 1;
   const u32 tiles = (u32)((nd + kTile - 1) / kTile);
   JY_TRY(jy_scratch(eng, 16, ((u64)tiles + 1) * 8, &p));
   A.rsum = static_cast<u64*>(p);  // per key tile, then (scanned in place) each tile's offset; [tiles] = total
