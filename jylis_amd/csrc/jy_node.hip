@@ -342,37 +342,67 @@ __global__ __launch_bounds__(kT) void k_nd_cells(u64 n, const u64* __restrict__ 
 
 // value heads: the 8-byte big-endian prefix, and the padded length of a long
 // value (plen[n] = 0: the scan's last input)
+// Values in tiles of kValTile (kValU per lane, lanes on consecutive values of
+// a row): k_nd1_head writes each value's big-endian prefix and each tile's
+// long-value granule bytes; those few tile sums are scanned; k_nd1_long
+// rescans its tile's lengths in the workgroup from the tile's offset.  (A
+// scan over every value's length took ~51 us of an 8.39M-key node TREG call
+// -- three launches over 8.39M words -- and wrote and re-read 67 MB.)
+constexpr int kValU = 4;
+constexpr u64 kValTile = (u64)kT * kValU;
+__device__ __forceinline__ u64 long_bytes(u64 l) { return l > 8 ? (l + 7) & ~7ull : 0; }
+
 __global__ __launch_bounds__(kT) void k_nd1_head(u64 n, const u64* __restrict__ vo, u64 vbase,
                                                  const uint8_t* __restrict__ vb, u64* __restrict__ pre,
-                                                 u64* __restrict__ plen) {
-  const u64 j = (u64)blockIdx.x * kT + threadIdx.x;
-  if (j > n) return;
-  if (j == n) {
-    plen[n] = 0;
-    return;
+                                                 u64* __restrict__ tsum) {
+  __shared__ u64 red[kT / 64];
+  const u64 t0 = (u64)blockIdx.x * kValTile;
+  u64 acc = 0;
+#pragma unroll
+  for (int u = 0; u < kValU; u++) {
+    const u64 j = t0 + (u64)u * kT + threadIdx.x;
+    if (j < n) {
+      const u64 a = vo[j], l = vo[j + 1] - a;
+      pre[j] = __builtin_bswap64(jy_ld8u(vb + (a - vbase), l));
+      acc += long_bytes(l);
+    }
   }
-  const u64 a = vo[j], l = vo[j + 1] - a;
-  pre[j] = __builtin_bswap64(jy_ld8u(vb + (a - vbase), l));
-  plen[j] = l > 8 ? (l + 7) & ~7ull : 0;
+  u64 tot;
+  jyscan::block_excl<kT, u64>(acc, red, tot);
+  if (threadIdx.x == 0) {
+    tsum[blockIdx.x] = tot;
+    if (blockIdx.x == 0) tsum[gridDim.x] = 0;  // the scan's last input
+  }
 }
 
-// long values' bytes into the arena (dst = the reserved tail, voff from the
-// scan of plen: 8-byte granules, word stores) and every value's handle
+// long values' bytes into the arena (dst = the reserved tail; the tile's
+// offset from the scan of the tile sums, each value's within the tile from a
+// workgroup scan in value order; 8-byte granules, word stores) and every
+// value's handle
 __global__ __launch_bounds__(kT) void k_nd1_long(u64 n, const u64* __restrict__ vo, u64 vbase,
-                                                 const uint8_t* __restrict__ vb, const u64* __restrict__ voff,
+                                                 const uint8_t* __restrict__ vb, const u64* __restrict__ toff,
                                                  uint8_t* __restrict__ dst, u64 rebase, u64* __restrict__ lr) {
-  const u64 j = (u64)blockIdx.x * kT + threadIdx.x;
-  if (j >= n) return;
-  const u64 a = vo[j], l = vo[j + 1] - a;
-  if (l <= 8) {
-    lr[j] = l;
-    return;
+  __shared__ u64 red[kT / 64];
+  const u64 t0 = (u64)blockIdx.x * kValTile;
+  u64 carry = toff[blockIdx.x];
+#pragma unroll
+  for (int u = 0; u < kValU; u++) {
+    const u64 j = t0 + (u64)u * kT + threadIdx.x;
+    u64 a = 0, l = 0;
+    if (j < n) a = vo[j], l = vo[j + 1] - a;
+    u64 tot;
+    const u64 d = carry + jyscan::block_excl<kT, u64>(long_bytes(l), red, tot);
+    carry += tot;
+    if (j >= n) continue;
+    if (l <= 8) {
+      lr[j] = l;
+      continue;
+    }
+    u64* o = reinterpret_cast<u64*>(dst + d);
+    const uint8_t* src = vb + (a - vbase);
+    for (u64 q = 0; q < (l + 7) / 8; q++) o[q] = jy_ld8u(src + 8 * q, l - 8 * q);
+    lr[j] = ((rebase + d) << JY_LR_LEN_BITS) | l;
   }
-  const u64 d = voff[j];
-  u64* o = reinterpret_cast<u64*>(dst + d);
-  const uint8_t* src = vb + (a - vbase);
-  for (u64 q = 0; q < (l + 7) / 8; q++) o[q] = jy_ld8u(src + 8 * q, l - 8 * q);
-  lr[j] = ((rebase + d) << JY_LR_LEN_BITS) | l;
 }
 
 // a CSR's offsets from 0: out[j] = offs[j] - offs[0], j <= n
@@ -1259,19 +1289,20 @@ int32_t one_keys_values(jy_node* nd, NdShard& sh, int32_t type, u64 n, const uin
   JY_TRY(bufT(nd, sh, R_SLOTS, std::max<u64>(n, 1), slots));
   TotalHook hk{&sh, nullptr, sh.pin + 2 * kMaxS * kMaxW + 3};
   const u64 ne = vals ? vals->ne : 0;
-  u64 *plen = nullptr, *voff = nullptr;
+  u64 *tsum = nullptr, *toff = nullptr;
+  const u64 nvt = (ne + kValTile - 1) / kValTile;  // value tiles
   if (vals) {
     JY_TRY(bufT(nd, sh, R_F1, std::max<u64>(ne, 1), pre));
-    JY_TRY(bufT(nd, sh, R_PLEN, ne + 1, &plen));
-    JY_TRY(bufT(nd, sh, R_VOFF, ne + 1, &voff));
+    JY_TRY(bufT(nd, sh, R_PLEN, nvt + 1, &tsum));
+    JY_TRY(bufT(nd, sh, R_VOFF, nvt + 1, &toff));
     JY_TRY(bufT(nd, sh, R_LR, std::max<u64>(ne, 1), lr));
     *hk.dst = 0;
     if (ne) {
-      hipLaunchKernelGGL(k_nd1_head, dim3(grid_of(ne + 1)), dim3(kT), 0, eng->stream, ne, vals->vo, vals->vbase,
-                         vals->vb, *pre, plen);
+      hipLaunchKernelGGL(k_nd1_head, dim3((u32)nvt), dim3(kT), 0, eng->stream, ne, vals->vo, vals->vbase, vals->vb,
+                         *pre, tsum);
       ND_HIP(nd, hipGetLastError());
-      ND_ENG(nd, sh, jy_scan_u64(eng, plen, voff, ne));
-      hk.src = voff + ne;
+      ND_ENG(nd, sh, jy_scan_u64(eng, tsum, toff, nvt));
+      hk.src = toff + nvt;
     }
   }
   if (n) {
@@ -1284,8 +1315,8 @@ int32_t one_keys_values(jy_node* nd, NdShard& sh, int32_t type, u64 n, const uin
     uint8_t* dst;
     u64 rebase;
     ND_ENG(nd, sh, jy_arena_reserve(eng, type, *hk.dst, &dst, &rebase));
-    hipLaunchKernelGGL(k_nd1_long, dim3(grid_of(ne)), dim3(kT), 0, eng->stream, ne, vals->vo, vals->vbase, vals->vb,
-                       (const u64*)voff, dst, rebase, *lr);
+    hipLaunchKernelGGL(k_nd1_long, dim3((u32)nvt), dim3(kT), 0, eng->stream, ne, vals->vo, vals->vbase, vals->vb,
+                       (const u64*)toff, dst, rebase, *lr);
     ND_HIP(nd, hipGetLastError());
   }
   return JY_OK;
