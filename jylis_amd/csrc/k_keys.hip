@@ -165,7 +165,6 @@ __global__ __launch_bounds__(kThreads) void k_key_probe(In I, Dir D, u32* __rest
     const u64 a = I.ko[i], len = I.ko[i + 1] - a;
     const KeyW kw = key_words(I.kb + a, len);
     const u64 t = table_hash(I.kb + a, len, kw);
-    th[i] = t;
     u64 p = t >> D.shift;
     u32 slot = kMiss;
     for (;;) {
@@ -182,6 +181,7 @@ __global__ __launch_bounds__(kThreads) void k_key_probe(In I, Dir D, u32* __rest
     }
     res[i] = slot;
     if (slot == kMiss) {
+      th[i] = t;  // read only for misses (claim, commit): a found key writes no hash
       c[0] = 1;
       c[1] = len;
       c[2] = len > JY_LR_LEN_MASK;
