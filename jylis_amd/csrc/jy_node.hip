@@ -64,6 +64,9 @@ constexpr int kT = 256;
 constexpr u32 kMaxS = JY_NODE_MAX_SHARDS;
 constexpr int kMaxLvl = 3;           // CSR levels of a payload (UJSON: elements, vv, cloud)
 constexpr int kMaxW = 2 + kMaxLvl;   // count granules: keys, key bytes, one per level
+// read-back words after the counts: [0, 2) read2's, [2] the value-length
+// verdict, [3] the long values' total (TotalHook), [8, 16) dev_words'
+constexpr int kPinTail = 24;
 
 u32 grid_of(u64 n) { return (u32)std::max<u64>(1, (n + kT - 1) / kT); }
 u64 round8(u64 x) { return (x + 7) & ~7ull; }
@@ -328,6 +331,23 @@ __global__ __launch_bounds__(kT) void k_nd_maxlen(const u64* __restrict__ vo, u6
   if (l > JY_MAX_VALUE_LEN) atomicMax(out, (unsigned long long)l);
 }
 
+// up to kWords device words gathered into pinned host memory by one launch
+// (an 8-byte hipMemcpyAsync costs the GPU a ~5-us copy kernel each); the word
+// at `reset` (a value-length verdict) is zeroed for the next call once read
+constexpr int kWords = 8;
+struct Words {
+  const u64* src[kWords];
+  u32 n;
+  int reset;
+};
+__global__ __launch_bounds__(64) void k_nd_words(Words W, u64* __restrict__ dst) {
+  const u32 i = threadIdx.x;
+  if (i >= W.n) return;
+  const u64 v = *W.src[i];
+  __hip_atomic_store(dst + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if ((int)i == W.reset) *const_cast<u64*>(W.src[i]) = 0;
+}
+
 __global__ __launch_bounds__(kT) void k_nd_cells(u64 n, const u64* __restrict__ packed, uint8_t* __restrict__ sign,
                                                  u16* __restrict__ col) {
   const u64 j = (u64)blockIdx.x * kT + threadIdx.x;
@@ -445,7 +465,11 @@ struct NdShard {
   hipEvent_t ev_out = nullptr; // this shard's receives have landed (copy fabric)
   hipEvent_t ev_x[2] = {nullptr, nullptr}, ev_m[2] = {nullptr, nullptr};
   NdBuf b[kNumBufs];
-  u64* pin = nullptr;  // pinned: [2][kMaxS][kMaxW] send / recv counts, then 16 words of readbacks
+  u64* pin = nullptr;  // pinned: [2][kMaxS][kMaxW] send / recv counts, then kPinTail words of readbacks
+  u64* pin_dev = nullptr;  // the same memory, as the device addresses it (k_nd_words writes there)
+  u64* mlw = nullptr;      // a value-length verdict word queued by values_dev_enqueue, not yet read
+  u64* mlw_buf = nullptr;  // the verdict word's buffer (zero between calls once set up)
+  bool mlw_zero = false;
   // the current call's sizes
   u64 n = 0;                 // keys ingested
   u64 tot[kMaxW] = {};       // elements per granule ingested (send side), upper bounds
@@ -591,18 +615,43 @@ int32_t bufT(jy_node* nd, NdShard& sh, int idx, u64 count, T** out) {
 }
 
 // two words read back from device (or host) memory: a CSR's first and last offset
+// device words read with one launch and one wait; a queued value-length
+// verdict (values_dev_enqueue) rides along into the pinned verdict word
+int32_t dev_words(jy_node* nd, NdShard& sh, std::initializer_list<const u64*> src, u64* out) {
+  Words W{};
+  for (const u64* p : src) {
+    if (W.n == (u32)kWords) return nd->fail(JY_EINVAL, "node: too many device words in one read-back");
+    W.src[W.n++] = p;
+  }
+  const u32 nsrc = W.n;
+  W.reset = -1;
+  if (sh.mlw) {
+    if (W.n == (u32)kWords) return nd->fail(JY_EINVAL, "node: too many device words in one read-back");
+    W.reset = (int)W.n;
+    W.src[W.n++] = sh.mlw;
+  }
+  u64* pw = sh.pin + 2 * kMaxS * kMaxW + 8;
+  hipLaunchKernelGGL(k_nd_words, dim3(1), dim3(64), 0, sh.eng->stream, W, sh.pin_dev + 2 * kMaxS * kMaxW + 8);
+  ND_HIP(nd, hipGetLastError());
+  ND_HIP(nd, hipStreamSynchronize(sh.eng->stream));
+  for (u32 k = 0; k < nsrc; k++) out[k] = pw[k];
+  if (sh.mlw) {
+    sh.pin[2 * kMaxS * kMaxW + 2] = pw[nsrc];
+    sh.mlw = nullptr;
+  }
+  return JY_OK;
+}
+
 int32_t read2(jy_node* nd, NdShard& sh, const u64* a, const u64* b, int32_t mem, u64& x, u64& y) {
   if (on_host(mem)) {
     x = *a;
     y = *b;
     return JY_OK;
   }
-  u64* pw = sh.pin + 2 * kMaxS * kMaxW;
-  ND_HIP(nd, hipMemcpyAsync(pw, a, 8, hipMemcpyDefault, sh.eng->stream));
-  ND_HIP(nd, hipMemcpyAsync(pw + 1, b, 8, hipMemcpyDefault, sh.eng->stream));
-  ND_HIP(nd, hipStreamSynchronize(sh.eng->stream));
-  x = pw[0];
-  y = pw[1];
+  u64 w[2];
+  JY_TRY(dev_words(nd, sh, {a, b}, w));
+  x = w[0];
+  y = w[1];
   return JY_OK;
 }
 
@@ -979,11 +1028,15 @@ int32_t values_dev_enqueue(jy_node* nd, NdShard& sh, const u64* vo, u64 n, int32
   u64* w;
   JY_TRY(bufT(nd, sh, B_CNT, 2 * kMaxS * kMaxW + 1, &w));
   w += 2 * kMaxS * kMaxW;  // (past the counts)
-  ND_HIP(nd, hipMemsetAsync(w, 0, 8, sh.eng->stream));
+  // the word is zero between calls (dev_words resets it once read); zeroed
+  // here only when a verdict was never read (an error path) or on first use
+  if (sh.mlw || !sh.mlw_zero || sh.mlw_buf != w) ND_HIP(nd, hipMemsetAsync(w, 0, 8, sh.eng->stream));
+  sh.mlw_zero = true;
+  sh.mlw_buf = w;
   hipLaunchKernelGGL(k_nd_maxlen, dim3(grid_of(n)), dim3(kT), 0, sh.eng->stream, vo, n,
                      reinterpret_cast<unsigned long long*>(w));
   ND_HIP(nd, hipGetLastError());
-  ND_HIP(nd, hipMemcpyAsync(sh.pin + 2 * kMaxS * kMaxW + 2, w, 8, hipMemcpyDeviceToHost, sh.eng->stream));
+  sh.mlw = w;  // read (and reset) by the next dev_words
   return JY_OK;
 }
 int32_t values_dev_ok(jy_node* nd, NdShard& sh, int32_t mem) {
@@ -1076,8 +1129,9 @@ int32_t jy_node_create(const jy_node_config* cfg, jy_node** out) {
     jy_config ec = cfg->engine;
     ec.device = sh.dev;
     if (jy_engine_create(&ec, &sh.eng) != JY_OK || !sh.eng ||
-        hipHostMalloc(reinterpret_cast<void**>(&sh.pin), (2 * kMaxS * kMaxW + 16) * 8, hipHostMallocDefault) !=
+        hipHostMalloc(reinterpret_cast<void**>(&sh.pin), (2 * kMaxS * kMaxW + kPinTail) * 8, hipHostMallocMapped) !=
             hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&sh.pin_dev), sh.pin, 0) != hipSuccess ||
         hipStreamCreateWithFlags(&sh.xs, hipStreamNonBlocking) != hipSuccess) {
       std::fprintf(stderr, "jy_node_create: shard %u on device %d failed\n", sh.rank, sh.dev);
       jy_node_destroy(nd);
@@ -1258,11 +1312,7 @@ int32_t readn(jy_node* nd, NdShard& sh, int32_t mem, std::initializer_list<const
     for (const u64* p : src) out[i++] = *p;
     return JY_OK;
   }
-  u64* pw = sh.pin + 2 * kMaxS * kMaxW + 8;  // [8, 16) of the read-back words
-  for (const u64* p : src) ND_HIP(nd, hipMemcpyAsync(pw + i++, p, 8, hipMemcpyDefault, sh.eng->stream));
-  ND_HIP(nd, hipStreamSynchronize(sh.eng->stream));
-  for (int k = 0; k < i; k++) out[k] = pw[k];
-  return JY_OK;
+  return dev_words(nd, sh, src, out);
 }
 
 struct TotalHook {

@@ -133,6 +133,10 @@ def test_calls_return_before_the_work(oracle_mod):
             node.sync()
         assert "16 MiB" in str(ei.value)
         node.sync()  # reported once
+        # the device verdict is reset: a later device-input call goes through
+        vb2, vo2 = encode_keys([b"fine value, 24 bytes ok"])
+        node.treg_converge(dev(kb), dev(ko), dev(np.array([7], np.uint64)), dev(vb2), dev(vo2))
+        node.sync()
     finally:
         node.close()
 
