@@ -389,6 +389,7 @@ void jy_engine_destroy(jy_engine* eng) {
   }
   if (eng->pin_total) hipHostFree(eng->pin_total);
   if (eng->pin_rb) hipHostFree(eng->pin_rb);
+  if (eng->kd_words) hipHostFree(eng->kd_words);
   if (eng->treg.dupflag) hipHostFree(eng->treg.dupflag);
   for (auto& ev : eng->tm_ev) {
     hipEventDestroy(ev.first);

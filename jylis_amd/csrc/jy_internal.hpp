@@ -468,6 +468,8 @@ struct jy_engine {
   // pinned landing area of large device -> host results (slots of a host key
   // batch): DMA here, then a parallel host copy out (host_copy.hip)
   void* pin_rb = nullptr;
+  u64* kd_words = nullptr;      // mapped pinned: the key probe's partial sums, written by the GPU
+  u64* kd_words_dev = nullptr;  // the same memory as the device addresses it
   u64 pin_rb_bytes = 0;
   hipEvent_t total_ready = nullptr;
 

@@ -225,7 +225,8 @@ __global__ __launch_bounds__(kSumThreads) void k_key_sum(const u64* __restrict__
   if (threadIdx.x < 3) {
     u64 t = 0;
     for (int w = 0; w < kSumThreads / 64; w++) t += red[threadIdx.x][w];
-    counts[(u64)blockIdx.x * 3 + threadIdx.x] = t;
+    // mapped pinned memory: system-scope vector stores, read by the host after the stream sync
+    __hip_atomic_store(counts + (u64)blockIdx.x * 3 + threadIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -428,14 +429,25 @@ int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, co
   JY_TRY(grow_slots(eng, K, std::max<u64>(K.n, 1)));
   JY_TRY(grow_table(eng, K, std::max<u64>(K.n, 1)));
   void* p;
-  JY_TRY(jy_scratch(eng, 20, n * 8 + kSumGroups * 24 + 64, &p));
+  JY_TRY(jy_scratch(eng, 20, n * 8 + 64, &p));
+  if (!eng->kd_words) {  // the probe's partial sums land in mapped pinned memory: no copy back
+    void* h = nullptr;
+    JY_HIP(eng, hipHostMalloc(&h, kSumGroups * 24, hipHostMallocMapped));
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+      hipHostFree(h);
+      return eng->fail(JY_EHIP, "key directory: mapped pinned words");
+    }
+    eng->kd_words = static_cast<u64*>(h);
+    eng->kd_words_dev = static_cast<u64*>(d);
+  }
   // the probe's answers go straight to the caller's slots (a found key's slot
   // or kMiss): every later kernel reads and rewrites index i in the same
   // thread, so a lookup, or an intern that finds every key, is done after the
   // probe (no copy of n words: 19 us at 8.39M keys)
   u32* res = slots;
   u64* th = static_cast<u64*>(p);
-  u64* counts = th + n;  // [sum groups][3] misses, their bytes, oversized keys
+  u64* counts = eng->kd_words_dev;  // [sum groups][3] misses, their bytes, oversized keys (mapped)
   In I{kb, ko, n};
   const u64 nb = (n + kProbeKeys - 1) / kProbeKeys;
   void* pp;
@@ -447,8 +459,7 @@ int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, co
   hipLaunchKernelGGL(k_key_sum, dim3(ng), dim3(kSumThreads), 0, eng->stream, parts, nb, counts);
   JY_HIP(eng, hipGetLastError());
   if (after_probe) JY_TRY(after_probe(arg));  // (a pageable read-back below may block at once)
-  u64 hg[kSumGroups * 3];
-  JY_HIP(eng, hipMemcpyAsync(hg, counts, ng * 24, hipMemcpyDeviceToHost, eng->stream));
+  const u64* hg = eng->kd_words;
   const double t0 = jy_tracing() ? jy_now_us() : 0;
   JY_HIP(eng, hipStreamSynchronize(eng->stream));
   JY_TRACE("keydir %llu keys: probe counts after %.1f us of waiting", (unsigned long long)n, jy_now_us() - t0);
