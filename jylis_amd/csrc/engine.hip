@@ -374,6 +374,7 @@ void jy_engine_destroy(jy_engine* eng) {
   F(eng->uj_dcount);
   F(eng->dscan_st.p);
   F(eng->tl_claim.p);
+  F(eng->tl_bad.p);
   F(eng->dscan_tick);
   for (auto& a : eng->arena) F(a.p);
   for (auto& s : eng->scratch) F(s.p);

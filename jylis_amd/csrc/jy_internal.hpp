@@ -441,6 +441,7 @@ struct jy_engine {
   // merge resets only its batch's slots, so no per-merge memset over all keys)
   DevArray tl_claim;    // TLOG slot claims: u64 epoch << 32 | delta key (k_tlog_prep)
   u32 tl_epoch = 0;      // the claims' epoch, one per TLOG merge launch
+  DevArray tl_bad;       // TLOG: per delta key, the epoch of the merge that found its slot repeated
   // device-wide scans / selects (jy_dscan.hpp): epoch-tagged look-back words
   DevArray dscan_st;
   u32* dscan_tick = nullptr;

@@ -131,7 +131,7 @@ struct TlogArgs {
   // temporaries
   u64* dptr;      // [nkeys] epoch << 32 | the delta key merging into each slot (last claimer)
   u32 epoch;      // this merge's claim epoch (never 0)
-  u32* bad;       // [nd] repeated slot in the batch
+  u32* bad;       // [nd] == epoch: the key's slot is repeated in the batch (no reset between merges)
   PInfo* pinfo;   // [nd] written for rebuilt and inserted keys only
   u32* rz;        // [nd + 1] pool entries a rebuilt key takes (0 otherwise)
   u64* rsum;      // [tiles + 1] rebuilt pool entries per key tile (scanned in place before k_tlog_commit)
@@ -148,8 +148,8 @@ struct TlogArgs {
 // contract: both deltas are skipped (counted once), the key is left untouched.
 // The claims carry the merge's epoch, so nothing resets them: a claimer that
 // finds this epoch's tag marks itself and the key it displaced (with three or
-// more copies every copy is marked by the next one).  bad[] is cleared before
-// this launch.
+// more copies every copy is marked by the next one).  The marks carry the
+// epoch too: bad[k] == epoch.
 __global__ __launch_bounds__(kThreads) void k_tlog_prep(TlogArgs A) {
   const u64 k = gid();
   if (k >= A.nd) return;
@@ -158,8 +158,8 @@ __global__ __launch_bounds__(kThreads) void k_tlog_prep(TlogArgs A) {
   const u64 tag = (u64)A.epoch << 32;
   const u64 prev = atomicExch(reinterpret_cast<unsigned long long*>(A.dptr + s), (unsigned long long)(tag | k));
   if ((prev & ~0xFFFFFFFFull) == tag) {
-    A.bad[k] = 1;
-    A.bad[(u32)prev] = 1;
+    A.bad[k] = A.epoch;
+    A.bad[(u32)prev] = A.epoch;
   }
 }
 
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
     const TMeta m = hole ? TMeta{0, 0, 0, 0, 0} : A.meta[s];
     const u64 hv = hole ? 0 : A.hint[s];  // with the meta: no dependent load of the log's first record
     const u64 cd = A.dcut[k];
-    const u32 bad = hole ? 4u : A.bad[k];
+    const u32 bad = hole ? 4u : (A.bad[k] == A.epoch ? 1u : 0u);
     const u64 cut = m.cut > cd ? m.cut : cd;
     bool fast = !bad && ne <= kFastEnt && cd <= m.cut;
     u32 M = 0;  // kept entries newer than the log: a prefix (strictly newest first)
@@ -1176,24 +1176,34 @@ int32_t tlog_launch(jy_engine* eng, TlogState& t, int r, u64 nd, const u32* slot
       c.bytes = nb;
       JY_HIP(eng, hipMemsetAsync(c.p, 0, nb, eng->stream));
     }
+    DevArray& b = eng->tl_bad;
+    if (b.bytes < nd * 4) {  // grows rarely: zero (epoch 0) once
+      const u64 nb = std::max<u64>(nd * 4, b.bytes * 2);
+      jy_dev_free(eng, b.p);
+      b.p = nullptr;
+      b.bytes = 0;
+      JY_TRY(jy_dev_alloc(eng, &b.p, nb, "tlog repeated-slot marks"));
+      b.bytes = nb;
+      JY_HIP(eng, hipMemsetAsync(b.p, 0, nb, eng->stream));
+    }
     if (++eng->tl_epoch == 0) {  // wrapped: no old tag may match a new epoch
       JY_HIP(eng, hipMemsetAsync(c.p, 0, c.bytes, eng->stream));
+      JY_HIP(eng, hipMemsetAsync(b.p, 0, b.bytes, eng->stream));
       eng->tl_epoch = 1;
     }
+    A.bad = static_cast<u32*>(b.p);
     A.dptr = static_cast<u64*>(c.p);
     A.epoch = eng->tl_epoch;
   }
   JY_TRY(jy_scratch(eng, 9, nd * (sizeof(PInfo) + 12) + 64, &p));
   A.pinfo = static_cast<PInfo*>(p);
-  A.bad = reinterpret_cast<u32*>(A.pinfo + nd);
-  A.rz = A.bad + nd;
+  A.rz = reinterpret_cast<u32*>(A.pinfo + nd);
   const u32 tiles = (u32)((nd + kTile - 1) / kTile);
   JY_TRY(jy_scratch(eng, 16, ((u64)tiles + 1) * 8, &p));
   A.rsum = static_cast<u64*>(p);  // per key tile, then (scanned in place) each tile's offset; [tiles] = total
   JY_TRY(jy_scratch(eng, 12, std::max<u64>(nent, 1) * 8, &p));
   u32* erank = static_cast<u32*>(p);
   u32* eqx = erank + std::max<u64>(nent, 1);
-  JY_HIP(eng, hipMemsetAsync(A.bad, 0, nd * 4, eng->stream));
   JY_HIP(eng, hipMemsetAsync(A.rsum + tiles, 0, 8, eng->stream));
   LAUNCH(k_tlog_prep, nd, A);
   A.meta = t.meta;
