@@ -572,13 +572,22 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
           // newest-first segment): a short segment counted at once, a long
           // one bisected
           u64 lo = jb, hi = jb + nek;
+          u32 q = 0;  // kept delta entries before lo (segment order)
           if (hi - lo <= 4) {
-            u32 rk[4];
+            // a short segment: its ranks and kept flags in one round trip
+            u32 rk[4], kq[4];
 #pragma unroll
-            for (u64 q = 0; q < 4; q++) rk[q] = lo + q < hi ? erank[lo + q] : 0u;
+            for (u64 e = 0; e < 4; e++) {
+              rk[e] = lo + e < hi ? erank[lo + e] : 0u;
+              kq[e] = lo + e < hi ? eqx[lo + e] : 0u;
+            }
             u64 c = 0;
 #pragma unroll
-            for (u64 q = 0; q < 4; q++) c += (lo + q < hi) & (rk[q] > i);
+            for (u64 e = 0; e < 4; e++) {
+              const bool above = (lo + e < hi) & (rk[e] > i);
+              c += above;
+              q += above & ((kq[e] & kKept) != 0);
+            }
             lo += c;
           } else {
             while (lo < hi) {
@@ -586,8 +595,8 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
               if (erank[m] <= i) hi = m;
               else lo = m + 1;
             }
+            q = lo < jb + nek ? (eqx[lo] & ~kKept) : 0u;
           }
-          const u32 q = lo < jb + nek ? (eqx[lo] & ~kKept) : 0u;
           write = true;
           at = dst + (i - drop) + (lo < jb + nek ? M - q : 0u);
         }
@@ -723,21 +732,32 @@ __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __
       u64 hi = l_bhi[a];
       constexpr u64 kLin = 4;
       if (hi - lo <= kLin) {
-        u32 rk[kLin];
+        // a short segment: its ranks and kept flags in one round trip; qx
+        // gets the kept count before lo (what eqx[lo] would hold)
+        u32 rk[kLin], kq[kLin];
 #pragma unroll
-        for (u64 q = 0; q < kLin; q++) rk[q] = lo + q < hi ? erank[lo + q] : 0u;
+        for (u64 e = 0; e < kLin; e++) {
+          rk[e] = lo + e < hi ? erank[lo + e] : 0u;
+          kq[e] = lo + e < hi ? eqx[lo + e] : 0u;
+        }
         u64 c = 0;
+        u32 q = 0;
 #pragma unroll
-        for (u64 q = 0; q < kLin; q++) c += (lo + q < hi) & (rk[q] > i);
+        for (u64 e = 0; e < kLin; e++) {
+          const bool above = (lo + e < hi) & (rk[e] > i);
+          c += above;
+          q += above & ((kq[e] & kKept) != 0);
+        }
         lo += c;
+        qx = q;
       } else {
         while (lo < hi) {
           const u64 m = (lo + hi) >> 1;
           if (erank[m] <= i) hi = m;
           else lo = m + 1;
         }
+        qx = lo < l_bhi[a] ? eqx[lo] : 0u;
       }
-      qx = lo < l_bhi[a] ? eqx[lo] : 0u;
     }
     if (cur.live) {
       const u32 M = l_M[a];
