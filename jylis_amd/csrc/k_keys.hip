@@ -55,36 +55,32 @@ constexpr u64 kIdxMask = 0x7FFFFFFFull;
 
 __device__ __forceinline__ u64 gid() { return (u64)blockIdx.x * kThreads + threadIdx.x; }
 
-// jy_key_owner's hash (FNV-1a 64 + splitmix64 finaliser), remixed so the
-// table position is independent of the owner shard (owner = h mod S would
+// The table hash is the directory's own (not jy_key_owner's FNV-1a, so the
+// table position is independent of the owner shard: owner = h mod S would
 // otherwise pin the low bits of every key of a shard).  The bytes come a
 // word at a time (jy_ld8u): the key's first two words are loaded together,
 // before any byte is hashed, and reused by the comparisons -- a byte loop
-// paid one dependent round trip per byte (K1 probe: 460 us for 8.9M keys)
+// paid one dependent round trip per byte (K1 probe: 460 us for 8.9M keys).
+// They are hashed a word at a time as well: a 16-B key costs 4 64-bit
+// multiplies instead of FNV-1a's 16 + 4.
 struct KeyW {
   u64 w0, w1;  // bytes 0..7 and 8..15, zero filled past the key
 };
 __device__ __forceinline__ KeyW key_words(const uint8_t* __restrict__ p, u64 len) {
   return KeyW{jy_ld8u(p, len), len > 8 ? jy_ld8u(p + 8, len - 8) : 0ull};
 }
-__device__ __forceinline__ u64 fnv_word(u64 h, u64 w, u64 m) {
-  for (u64 b = 0; b < m; b++) {
-    h ^= (w >> (8 * b)) & 0xFFu;
-    h *= 0x100000001B3ull;
-  }
-  return h;
+// a word folds in with one multiply + xorshift, both bijections of the state,
+// so two keys of one length that differ in one word always differ before the
+// finaliser (the length seeds the state: "a" and "a\0" differ too)
+__device__ __forceinline__ u64 mix_word(u64 h, u64 w) {
+  h = (h ^ w) * 0xBF58476D1CE4E5B9ull;
+  return h ^ (h >> 31);
 }
 __device__ __forceinline__ u64 table_hash(const uint8_t* __restrict__ p, u64 len, const KeyW& kw) {
-  u64 h = 0xCBF29CE484222325ull;
-  h = fnv_word(h, kw.w0, len < 8 ? len : 8);
-  if (len > 8) h = fnv_word(h, kw.w1, len - 8 < 8 ? len - 8 : 8);
-  for (u64 i = 16; i < len; i += 8) h = fnv_word(h, jy_ld8u(p + i, len - i), len - i < 8 ? len - i : 8);
-  h ^= h >> 30;
-  h *= 0xBF58476D1CE4E5B9ull;
-  h ^= h >> 27;
-  h *= 0x94D049BB133111EBull;
-  h ^= h >> 31;
-  h += 0x9E3779B97F4A7C15ull;
+  u64 h = (len * 0x9E3779B97F4A7C15ull) ^ 0xCBF29CE484222325ull;
+  h = mix_word(h, kw.w0);
+  if (len > 8) h = mix_word(h, kw.w1);
+  for (u64 i = 16; i < len; i += 8) h = mix_word(h, jy_ld8u(p + i, len - i));
   h ^= h >> 30;
   h *= 0xBF58476D1CE4E5B9ull;
   h ^= h >> 27;
