@@ -1315,16 +1315,6 @@ int32_t readn(jy_node* nd, NdShard& sh, int32_t mem, std::initializer_list<const
   return dev_words(nd, sh, src, out);
 }
 
-struct TotalHook {
-  NdShard* sh;
-  const u64* src;
-  u64* dst;
-};
-int32_t total_hook(void* p) {
-  TotalHook* h = static_cast<TotalHook*>(p);
-  return hipMemcpyAsync(h->dst, h->src, 8, hipMemcpyDeviceToHost, h->sh->eng->stream) == hipSuccess ? JY_OK : JY_EHIP;
-}
-
 // keys interned on the one shard; with `vals`, the ne values' heads, their
 // long bytes in the arena and their handles (pre, lr at R_F1 / R_LR)
 struct OneVals {
@@ -1337,7 +1327,10 @@ int32_t one_keys_values(jy_node* nd, NdShard& sh, int32_t type, u64 n, const uin
                         const OneVals* vals, u32** slots, u64** pre, u64** lr) {
   jy_engine* eng = sh.eng;
   JY_TRY(bufT(nd, sh, R_SLOTS, std::max<u64>(n, 1), slots));
-  TotalHook hk{&sh, nullptr, sh.pin + 2 * kMaxS * kMaxW + 3};
+  // the long values' byte total (the scan's last word) comes back with the
+  // key probe's counts
+  const u64* total_dev = nullptr;
+  u64 total = 0;
   const u64 ne = vals ? vals->ne : 0;
   u64 *tsum = nullptr, *toff = nullptr;
   const u64 nvt = (ne + kValTile - 1) / kValTile;  // value tiles
@@ -1346,25 +1339,26 @@ int32_t one_keys_values(jy_node* nd, NdShard& sh, int32_t type, u64 n, const uin
     JY_TRY(bufT(nd, sh, R_PLEN, nvt + 1, &tsum));
     JY_TRY(bufT(nd, sh, R_VOFF, nvt + 1, &toff));
     JY_TRY(bufT(nd, sh, R_LR, std::max<u64>(ne, 1), lr));
-    *hk.dst = 0;
     if (ne) {
       hipLaunchKernelGGL(k_nd1_head, dim3((u32)nvt), dim3(kT), 0, eng->stream, ne, vals->vo, vals->vbase, vals->vb,
                          *pre, tsum);
       ND_HIP(nd, hipGetLastError());
       ND_ENG(nd, sh, jy_scan_u64(eng, tsum, toff, nvt));
-      hk.src = toff + nvt;
+      total_dev = toff + nvt;
     }
   }
   if (n) {
-    ND_ENG(nd, sh, jy_keys_intern_dev(eng, type, n, kbase, ko, *slots, hk.src ? total_hook : nullptr, &hk));
-  } else if (hk.src) {
-    ND_HIP(nd, hipMemcpyAsync(hk.dst, hk.src, 8, hipMemcpyDeviceToHost, eng->stream));
+    ND_ENG(nd, sh, jy_keys_intern_dev(eng, type, n, kbase, ko, *slots, total_dev, &total));
+  } else if (total_dev) {
+    u64* pin = sh.pin + 2 * kMaxS * kMaxW + 3;
+    ND_HIP(nd, hipMemcpyAsync(pin, total_dev, 8, hipMemcpyDeviceToHost, eng->stream));
     ND_HIP(nd, hipStreamSynchronize(eng->stream));
+    total = *pin;
   }
   if (ne) {
     uint8_t* dst;
     u64 rebase;
-    ND_ENG(nd, sh, jy_arena_reserve(eng, type, *hk.dst, &dst, &rebase));
+    ND_ENG(nd, sh, jy_arena_reserve(eng, type, total, &dst, &rebase));
     hipLaunchKernelGGL(k_nd1_long, dim3((u32)nvt), dim3(kT), 0, eng->stream, ne, vals->vo, vals->vbase, vals->vb,
                        (const u64*)toff, dst, rebase, *lr);
     ND_HIP(nd, hipGetLastError());

@@ -202,10 +202,17 @@ __global__ __launch_bounds__(kThreads) void k_key_probe(In I, Dir D, u32* __rest
 // by kSumGroups workgroups of 256 into [kSumGroups][3]; the host adds those
 // up with its read-back.  (One workgroup of 1024 walking all the rows took 19
 // us at 32.8K rows, the node TREG call's 8.39M keys: its loads wait in line.)
+// The words land in mapped pinned memory, [kSumGroups][3] and then two more:
+// the caller's extra word (`also`) and the completion number.  The last
+// workgroup to publish writes the completion number (system-scope release
+// after every workgroup's system fence), so the host spins on one word of
+// its own memory instead of waking from a stream synchronise.
 constexpr int kSumThreads = 256;
 constexpr u32 kSumGroups = 128;
+constexpr u32 kWordAlso = kSumGroups * 3, kWordDone = kWordAlso + 1, kSumWords = kWordDone + 1;
 __global__ __launch_bounds__(kSumThreads) void k_key_sum(const u64* __restrict__ parts, u64 nb,
-                                                         u64* __restrict__ counts) {
+                                                         u64* __restrict__ counts, const u64* __restrict__ also,
+                                                         u32* __restrict__ done, u64 seq) {
   __shared__ u64 red[3][kSumThreads / 64];
   u64 v[3] = {0, 0, 0};
   for (u64 b = (u64)blockIdx.x * kSumThreads + threadIdx.x; b < nb; b += (u64)gridDim.x * kSumThreads) {
@@ -221,8 +228,20 @@ __global__ __launch_bounds__(kSumThreads) void k_key_sum(const u64* __restrict__
   if (threadIdx.x < 3) {
     u64 t = 0;
     for (int w = 0; w < kSumThreads / 64; w++) t += red[threadIdx.x][w];
-    // mapped pinned memory: system-scope vector stores, read by the host after the stream sync
+    // mapped pinned memory: system-scope vector stores
     __hip_atomic_store(counts + (u64)blockIdx.x * 3 + threadIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 3)
+    __hip_atomic_store(counts + kWordAlso, also ? *also : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x < 4) __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const u32 prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {  // the last: every other workgroup's words are out
+      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+      __threadfence_system();
+      __hip_atomic_store(counts + kWordDone, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 }
 
@@ -335,6 +354,10 @@ __global__ __launch_bounds__(kThreads) void k_key_rehash(Dir D, u64 nk) {
   D.table[p].w1 = kw.w1;
 }
 
+// how long the host spins on the sums' completion word before it falls back
+// to a stream synchronise (a probe of 8.39M keys takes ~0.3 ms)
+constexpr double kSpinUs = 20000.0;
+
 u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kThreads - 1) / kThreads); }
 
 #define LAUNCH(k, n, ...)                                                                          \
@@ -415,9 +438,11 @@ void jy_keydir_free(jy_engine* eng, KeyDir& K) {
 // key count before any call sizes work by it).
 // after_probe (optional) runs on the host once the probe is enqueued and
 // before the host waits for its counts: a caller stages its next inputs there
-// while the GPU probes
+// while the GPU probes.  also (optional): a device word written by earlier
+// work on the stream, returned in *also_out with the probe's counts (one
+// read-back for both)
 int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, const u64* ko, u32* slots, bool create,
-                      u64* created, int32_t (*after_probe)(void*), void* arg) {
+                      u64* created, int32_t (*after_probe)(void*), void* arg, const u64* also, u64* also_out) {
   *created = 0;
   if (n == 0) return JY_OK;
   if (n >= kIdxMask) return eng->fail(JY_ERANGE, "too many keys in one call");
@@ -428,7 +453,8 @@ int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, co
   JY_TRY(jy_scratch(eng, 20, n * 8 + 64, &p));
   if (!eng->kd_words) {  // the probe's partial sums land in mapped pinned memory: no copy back
     void* h = nullptr;
-    JY_HIP(eng, hipHostMalloc(&h, kSumGroups * 24, hipHostMallocMapped));
+    JY_HIP(eng, hipHostMalloc(&h, kSumWords * 8, hipHostMallocMapped));
+    std::memset(h, 0, kSumWords * 8);
     void* d = nullptr;
     if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
       hipHostFree(h);
@@ -436,6 +462,10 @@ int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, co
     }
     eng->kd_words = static_cast<u64*>(h);
     eng->kd_words_dev = static_cast<u64*>(d);
+  }
+  if (!eng->kd_done) {
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&eng->kd_done), 64, "key probe sums' counter"));
+    JY_HIP(eng, hipMemsetAsync(eng->kd_done, 0, 64, eng->stream));
   }
   // the probe's answers go straight to the caller's slots (a found key's slot
   // or kMiss): every later kernel reads and rewrites index i in the same
@@ -452,13 +482,30 @@ int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, co
   hipLaunchKernelGGL(k_key_probe, dim3((u32)nb), dim3(kThreads), 0, eng->stream, I, dir_of(K), res, th, parts);
   JY_HIP(eng, hipGetLastError());
   const u32 ng = (u32)std::min<u64>(kSumGroups, (nb + kSumThreads - 1) / kSumThreads);
-  hipLaunchKernelGGL(k_key_sum, dim3(ng), dim3(kSumThreads), 0, eng->stream, parts, nb, counts);
+  const u64 seq = ++eng->kd_seq;
+  hipLaunchKernelGGL(k_key_sum, dim3(ng), dim3(kSumThreads), 0, eng->stream, parts, nb, counts, also, eng->kd_done,
+                     seq);
   JY_HIP(eng, hipGetLastError());
-  if (after_probe) JY_TRY(after_probe(arg));  // (a pageable read-back below may block at once)
+  if (after_probe) JY_TRY(after_probe(arg));  // (its copies follow the sums in stream order)
   const u64* hg = eng->kd_words;
-  const double t0 = jy_tracing() ? jy_now_us() : 0;
-  JY_HIP(eng, hipStreamSynchronize(eng->stream));
-  JY_TRACE("keydir %llu keys: probe counts after %.1f us of waiting", (unsigned long long)n, jy_now_us() - t0);
+  const double t0 = jy_now_us();
+  // the sums' completion number means every launch before them is done as
+  // well (what after_probe enqueued may still run: it is stream-ordered
+  // before any use).  A launch that never ends (a fault) leaves the number
+  // unwritten: past the spin budget the stream synchronise reports it.
+  bool seen = false;
+  for (u32 spin = 0;; spin++) {
+    if (__atomic_load_n(hg + kWordDone, __ATOMIC_ACQUIRE) == seq) {
+      seen = true;
+      break;
+    }
+    if ((spin & 255) == 255 && jy_now_us() - t0 > kSpinUs) break;
+    __builtin_ia32_pause();
+  }
+  if (!seen) JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  JY_TRACE("keydir %llu keys: probe counts after %.1f us of waiting (%s)", (unsigned long long)n, jy_now_us() - t0,
+           seen ? "spin" : "stream sync");
+  if (also_out) *also_out = hg[kWordAlso];
   u64 hc[3] = {0, 0, 0};
   for (u32 g = 0; g < ng; g++)
     for (int q = 0; q < 3; q++) hc[q] += hg[g * 3 + q];
