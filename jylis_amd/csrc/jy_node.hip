@@ -461,6 +461,10 @@ struct NdShard {
   jy_engine* eng = nullptr;
   ncclComm_t comm = nullptr;
   hipStream_t xs = nullptr;    // exchange stream of the block converge
+  // read-back stream: the caller's input words (k_nd_words) and the value
+  // length check (k_nd_maxlen) need none of the engine stream's earlier work,
+  // so a call reads them while the previous call's kernels still run
+  hipStream_t rs = nullptr;
   hipEvent_t ev_in = nullptr;  // this shard's send columns are ready (copy fabric)
   hipEvent_t ev_out = nullptr; // this shard's receives have landed (copy fabric)
   hipEvent_t ev_x[2] = {nullptr, nullptr}, ev_m[2] = {nullptr, nullptr};
@@ -596,6 +600,7 @@ int32_t buf(jy_node* nd, NdShard& sh, int idx, u64 bytes, void** out) {
     // growth: whatever still reads the old buffer has to finish
     ND_HIP(nd, hipStreamSynchronize(sh.eng->stream));
     if (sh.xs) ND_HIP(nd, hipStreamSynchronize(sh.xs));
+    if (sh.rs) ND_HIP(nd, hipStreamSynchronize(sh.rs));
     if (b.p) ND_HIP(nd, hipFree(b.p));
     b.p = nullptr;
     b.bytes = 0;
@@ -631,9 +636,9 @@ int32_t dev_words(jy_node* nd, NdShard& sh, std::initializer_list<const u64*> sr
     W.src[W.n++] = sh.mlw;
   }
   u64* pw = sh.pin + 2 * kMaxS * kMaxW + 8;
-  hipLaunchKernelGGL(k_nd_words, dim3(1), dim3(64), 0, sh.eng->stream, W, sh.pin_dev + 2 * kMaxS * kMaxW + 8);
+  hipLaunchKernelGGL(k_nd_words, dim3(1), dim3(64), 0, sh.rs, W, sh.pin_dev + 2 * kMaxS * kMaxW + 8);
   ND_HIP(nd, hipGetLastError());
-  ND_HIP(nd, hipStreamSynchronize(sh.eng->stream));
+  ND_HIP(nd, hipStreamSynchronize(sh.rs));
   for (u32 k = 0; k < nsrc; k++) out[k] = pw[k];
   if (sh.mlw) {
     sh.pin[2 * kMaxS * kMaxW + 2] = pw[nsrc];
@@ -1030,10 +1035,10 @@ int32_t values_dev_enqueue(jy_node* nd, NdShard& sh, const u64* vo, u64 n, int32
   w += 2 * kMaxS * kMaxW;  // (past the counts)
   // the word is zero between calls (dev_words resets it once read); zeroed
   // here only when a verdict was never read (an error path) or on first use
-  if (sh.mlw || !sh.mlw_zero || sh.mlw_buf != w) ND_HIP(nd, hipMemsetAsync(w, 0, 8, sh.eng->stream));
+  if (sh.mlw || !sh.mlw_zero || sh.mlw_buf != w) ND_HIP(nd, hipMemsetAsync(w, 0, 8, sh.rs));
   sh.mlw_zero = true;
   sh.mlw_buf = w;
-  hipLaunchKernelGGL(k_nd_maxlen, dim3(grid_of(n)), dim3(kT), 0, sh.eng->stream, vo, n,
+  hipLaunchKernelGGL(k_nd_maxlen, dim3(grid_of(n)), dim3(kT), 0, sh.rs, vo, n,
                      reinterpret_cast<unsigned long long*>(w));
   ND_HIP(nd, hipGetLastError());
   sh.mlw = w;  // read (and reset) by the next dev_words
@@ -1087,6 +1092,7 @@ void jy_node_destroy(jy_node* nd) {
     hipSetDevice(sh.dev);
     if (sh.eng) hipStreamSynchronize(sh.eng->stream);
     if (sh.xs) hipStreamSynchronize(sh.xs);
+    if (sh.rs) hipStreamSynchronize(sh.rs);
   }
   for (NdShard& sh : nd->sh)
     if (sh.comm) ncclCommDestroy(sh.comm);
@@ -1098,6 +1104,7 @@ void jy_node_destroy(jy_node* nd) {
     for (hipEvent_t e : {sh.ev_in, sh.ev_out, sh.ev_x[0], sh.ev_x[1], sh.ev_m[0], sh.ev_m[1]})
       if (e) hipEventDestroy(e);
     if (sh.xs) hipStreamDestroy(sh.xs);
+    if (sh.rs) hipStreamDestroy(sh.rs);
     jy_engine_destroy(sh.eng);
   }
   for (NdPin& pb : nd->pins) {
@@ -1132,7 +1139,8 @@ int32_t jy_node_create(const jy_node_config* cfg, jy_node** out) {
         hipHostMalloc(reinterpret_cast<void**>(&sh.pin), (2 * kMaxS * kMaxW + kPinTail) * 8, hipHostMallocMapped) !=
             hipSuccess ||
         hipHostGetDevicePointer(reinterpret_cast<void**>(&sh.pin_dev), sh.pin, 0) != hipSuccess ||
-        hipStreamCreateWithFlags(&sh.xs, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&sh.xs, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&sh.rs, hipStreamNonBlocking) != hipSuccess) {
       std::fprintf(stderr, "jy_node_create: shard %u on device %d failed\n", sh.rank, sh.dev);
       jy_node_destroy(nd);
       return JY_EHIP;
@@ -1990,7 +1998,10 @@ int32_t run_locked(jy_node* nd, const NdJob& j) {
     for (u32 L = 0; L < nd->nlocal; L++) {
       NdShard& sh = nd->sh[L];
       hipSetDevice(sh.dev);
-      if (rc != JY_OK) hipStreamSynchronize(sh.eng->stream);  // a failed job's staging may be in flight
+      if (rc != JY_OK) {  // a failed job's staging may be in flight
+        hipStreamSynchronize(sh.eng->stream);
+        hipStreamSynchronize(sh.rs);
+      }
       else if (hipEventRecord(pb.ev[L], sh.eng->stream) != hipSuccess) {
         hipStreamSynchronize(sh.eng->stream);
         hipEventRecord(pb.ev[L], nullptr);

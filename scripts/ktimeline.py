@@ -18,3 +18,5 @@ for r in rows[a:b]:
     print(f"{(s - t0) / 1e3:9.1f}us  +gap {gap:7.1f}  dur {(e - s) / 1e3:8.1f}  {name}")
     prev_end = e
 print(f"span {(prev_end - t0) / 1e3:.1f} us")
+if b < len(rows):
+    print(f"next {marker} at {(int(rows[b]['Start_Timestamp']) - t0) / 1e3:.1f} us (call period)")
