@@ -556,17 +556,16 @@ static int32_t keys_host(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb,
   return JY_OK;
 }
 
-// device keys interned (create on miss); `also` (optional): a device word
-// written by earlier work on the stream, returned in *also_out by the same
-// read-back as the probe's counts (the node's one-shard path: its long-value
-// total)
+// device keys interned (create on miss), with the directory's hook: `after`
+// runs once the probe is enqueued, before the host waits for its counts (the
+// node's one-shard path enqueues its long values there)
 }  // extern "C"
 int32_t jy_keys_intern_dev(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, const u64* ko, u32* slots,
-                           const u64* also, u64* also_out) {
+                           int32_t (*after)(void*), void* arg) {
   JY_TRY(check_type(eng, type));
   JY_HIP(eng, hipSetDevice(eng->device));
   u64 created = 0;
-  JY_TRY(jy_keydir_run(eng, type, n, kb, ko, slots, true, &created, nullptr, nullptr, also, also_out));
+  JY_TRY(jy_keydir_run(eng, type, n, kb, ko, slots, true, &created, after, arg));
   return keys_created(eng, type, created);
 }
 extern "C" {

@@ -622,10 +622,9 @@ void jy_dev_free(jy_engine* eng, void* p);
 int32_t jy_keydir_reserve(jy_engine* eng, int32_t type, u64 cap);
 void jy_keydir_free(jy_engine* eng, KeyDir& K);
 int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, const u64* ko, u32* slots, bool create,
-                      u64* created, int32_t (*after_probe)(void*) = nullptr, void* arg = nullptr,
-                      const u64* also = nullptr, u64* also_out = nullptr);
+                      u64* created, int32_t (*after_probe)(void*) = nullptr, void* arg = nullptr);
 int32_t jy_keys_intern_dev(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, const u64* ko, u32* slots,
-                           const u64* also, u64* also_out);
+                           int32_t (*after)(void*), void* arg);
 int32_t jy_ujson_grow(jy_engine* eng, u64 need_slots);
 int32_t jy_ujson_extend(jy_engine* eng, u64 from, u64 to);
 int32_t jy_ujson_sizes(jy_engine* eng, u64 n, const u32* slots, u64* ne, u64* nc);

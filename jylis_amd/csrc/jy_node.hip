@@ -425,6 +425,37 @@ __global__ __launch_bounds__(kT) void k_nd1_long(u64 n, const u64* __restrict__ 
   }
 }
 
+// the value tiles' long-byte sums scanned by one workgroup (toff[j],
+// exclusive; toff[nt] the total, also stored to mapped pinned memory for the
+// host).  A few thousand tiles per call (8.39M values: 8,192): no look-back.
+// Rows of 1024 consecutive sums, kTScanU rows' loads issued together.
+constexpr int kTScanThreads = 1024, kTScanU = 8;
+__global__ __launch_bounds__(kTScanThreads) void k_nd1_tscan(const u64* __restrict__ tsum, u64 nt,
+                                                             u64* __restrict__ toff, u64* __restrict__ total_pin) {
+  __shared__ u64 red[kTScanThreads / 64];
+  u64 carry = 0;
+  for (u64 c0 = 0; c0 < nt; c0 += (u64)kTScanThreads * kTScanU) {
+    u64 v[kTScanU];
+#pragma unroll
+    for (int u = 0; u < kTScanU; u++) {
+      const u64 i = c0 + (u64)u * kTScanThreads + threadIdx.x;
+      v[u] = i < nt ? tsum[i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kTScanU; u++) {
+      const u64 i = c0 + (u64)u * kTScanThreads + threadIdx.x;
+      u64 tot;
+      const u64 x = jyscan::block_excl<kTScanThreads, u64>(v[u], red, tot);
+      if (i < nt) toff[i] = carry + x;
+      carry += tot;
+    }
+  }
+  if (threadIdx.x == 0) {
+    toff[nt] = carry;
+    __hip_atomic_store(total_pin, carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // a CSR's offsets from 0: out[j] = offs[j] - offs[0], j <= n
 __global__ __launch_bounds__(kT) void k_nd1_rebase(u64 n, const u64* __restrict__ offs, u64* __restrict__ out) {
   const u64 j = (u64)blockIdx.x * kT + threadIdx.x;
@@ -465,6 +496,8 @@ struct NdShard {
   // length check (k_nd_maxlen) need none of the engine stream's earlier work,
   // so a call reads them while the previous call's kernels still run
   hipStream_t rs = nullptr;
+  hipEvent_t ev_rs_in = nullptr;   // the engine stream's point the read-back stream's value work starts after
+  hipEvent_t ev_rs_out = nullptr;  // the value handles are written (the engine stream waits before the merge)
   hipEvent_t ev_in = nullptr;  // this shard's send columns are ready (copy fabric)
   hipEvent_t ev_out = nullptr; // this shard's receives have landed (copy fabric)
   hipEvent_t ev_x[2] = {nullptr, nullptr}, ev_m[2] = {nullptr, nullptr};
@@ -1101,7 +1134,7 @@ void jy_node_destroy(jy_node* nd) {
     for (NdBuf& b : sh.b)
       if (b.p) hipFree(b.p);
     if (sh.pin) hipHostFree(sh.pin);
-    for (hipEvent_t e : {sh.ev_in, sh.ev_out, sh.ev_x[0], sh.ev_x[1], sh.ev_m[0], sh.ev_m[1]})
+    for (hipEvent_t e : {sh.ev_in, sh.ev_out, sh.ev_x[0], sh.ev_x[1], sh.ev_m[0], sh.ev_m[1], sh.ev_rs_in, sh.ev_rs_out})
       if (e) hipEventDestroy(e);
     if (sh.xs) hipStreamDestroy(sh.xs);
     if (sh.rs) hipStreamDestroy(sh.rs);
@@ -1145,7 +1178,8 @@ int32_t jy_node_create(const jy_node_config* cfg, jy_node** out) {
       jy_node_destroy(nd);
       return JY_EHIP;
     }
-    for (hipEvent_t* e : {&sh.ev_in, &sh.ev_out, &sh.ev_x[0], &sh.ev_x[1], &sh.ev_m[0], &sh.ev_m[1]})
+    for (hipEvent_t* e : {&sh.ev_in, &sh.ev_out, &sh.ev_x[0], &sh.ev_x[1], &sh.ev_m[0], &sh.ev_m[1], &sh.ev_rs_in,
+                          &sh.ev_rs_out})
       if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
         jy_node_destroy(nd);
         return JY_EHIP;
@@ -1324,21 +1358,48 @@ int32_t readn(jy_node* nd, NdShard& sh, int32_t mem, std::initializer_list<const
 }
 
 // keys interned on the one shard; with `vals`, the ne values' heads, their
-// long bytes in the arena and their handles (pre, lr at R_F1 / R_LR)
+// long bytes in the arena and their handles (pre, lr at R_F1 / R_LR).
+// The value work runs on the read-back stream, beside the key probe (the
+// probe waits on random table lines, the value kernels stream): heads and
+// tile sums first; once the probe is enqueued, the host waits for their total,
+// reserves the arena and enqueues the long values; the engine stream waits
+// for them before the merge.  (In one stream: 8.39M-key TREG call 0.66 ms,
+// of which ~70 us heads + scan and ~85 us long values ran after the probe.)
 struct OneVals {
   u64 ne = 0;
   const u64* vo = nullptr;  // device, indexed from the first value
   u64 vbase = 0;
   const uint8_t* vb = nullptr;
 };
+struct LongJob {
+  jy_node* nd;
+  NdShard* sh;
+  int32_t type;
+  const OneVals* vals;
+  u64 nvt;
+  const u64* toff;
+  u64* lr;
+};
+// on the host while the probe runs: the total, the arena, the long values
+int32_t long_values(void* p) {
+  LongJob& j = *static_cast<LongJob*>(p);
+  NdShard& sh = *j.sh;
+  jy_engine* eng = sh.eng;
+  if (hipStreamSynchronize(sh.rs) != hipSuccess) return eng->fail(JY_EHIP, "node: value heads");
+  const u64 total = sh.pin[2 * kMaxS * kMaxW + 3];
+  uint8_t* dst;
+  u64 rebase;
+  JY_TRY(jy_arena_reserve(eng, j.type, total, &dst, &rebase));
+  hipLaunchKernelGGL(k_nd1_long, dim3((u32)j.nvt), dim3(kT), 0, sh.rs, j.vals->ne, j.vals->vo, j.vals->vbase,
+                     j.vals->vb, j.toff, dst, rebase, j.lr);
+  if (hipGetLastError() != hipSuccess || hipEventRecord(sh.ev_rs_out, sh.rs) != hipSuccess)
+    return eng->fail(JY_EHIP, "node: long values");
+  return JY_OK;
+}
 int32_t one_keys_values(jy_node* nd, NdShard& sh, int32_t type, u64 n, const uint8_t* kbase, const u64* ko,
                         const OneVals* vals, u32** slots, u64** pre, u64** lr) {
   jy_engine* eng = sh.eng;
   JY_TRY(bufT(nd, sh, R_SLOTS, std::max<u64>(n, 1), slots));
-  // the long values' byte total (the scan's last word) comes back with the
-  // key probe's counts
-  const u64* total_dev = nullptr;
-  u64 total = 0;
   const u64 ne = vals ? vals->ne : 0;
   u64 *tsum = nullptr, *toff = nullptr;
   const u64 nvt = (ne + kValTile - 1) / kValTile;  // value tiles
@@ -1347,30 +1408,25 @@ int32_t one_keys_values(jy_node* nd, NdShard& sh, int32_t type, u64 n, const uin
     JY_TRY(bufT(nd, sh, R_PLEN, nvt + 1, &tsum));
     JY_TRY(bufT(nd, sh, R_VOFF, nvt + 1, &toff));
     JY_TRY(bufT(nd, sh, R_LR, std::max<u64>(ne, 1), lr));
-    if (ne) {
-      hipLaunchKernelGGL(k_nd1_head, dim3((u32)nvt), dim3(kT), 0, eng->stream, ne, vals->vo, vals->vbase, vals->vb,
-                         *pre, tsum);
-      ND_HIP(nd, hipGetLastError());
-      ND_ENG(nd, sh, jy_scan_u64(eng, tsum, toff, nvt));
-      total_dev = toff + nvt;
-    }
   }
-  if (n) {
-    ND_ENG(nd, sh, jy_keys_intern_dev(eng, type, n, kbase, ko, *slots, total_dev, &total));
-  } else if (total_dev) {
-    u64* pin = sh.pin + 2 * kMaxS * kMaxW + 3;
-    ND_HIP(nd, hipMemcpyAsync(pin, total_dev, 8, hipMemcpyDeviceToHost, eng->stream));
-    ND_HIP(nd, hipStreamSynchronize(eng->stream));
-    total = *pin;
-  }
+  LongJob job{nd, &sh, type, vals, nvt, toff, vals ? *lr : nullptr};
   if (ne) {
-    uint8_t* dst;
-    u64 rebase;
-    ND_ENG(nd, sh, jy_arena_reserve(eng, type, total, &dst, &rebase));
-    hipLaunchKernelGGL(k_nd1_long, dim3((u32)nvt), dim3(kT), 0, eng->stream, ne, vals->vo, vals->vbase, vals->vb,
-                       (const u64*)toff, dst, rebase, *lr);
+    // after the staged inputs and the previous call's kernels (which read
+    // pre / lr / the arena) on the engine stream
+    ND_HIP(nd, hipEventRecord(sh.ev_rs_in, eng->stream));
+    ND_HIP(nd, hipStreamWaitEvent(sh.rs, sh.ev_rs_in, 0));
+    hipLaunchKernelGGL(k_nd1_head, dim3((u32)nvt), dim3(kT), 0, sh.rs, ne, vals->vo, vals->vbase, vals->vb, *pre,
+                       tsum);
+    ND_HIP(nd, hipGetLastError());
+    hipLaunchKernelGGL(k_nd1_tscan, dim3(1), dim3(kTScanThreads), 0, sh.rs, (const u64*)tsum, nvt, toff,
+                       sh.pin_dev + 2 * kMaxS * kMaxW + 3);
     ND_HIP(nd, hipGetLastError());
   }
+  if (n)
+    ND_ENG(nd, sh, jy_keys_intern_dev(eng, type, n, kbase, ko, *slots, ne ? long_values : nullptr, &job));
+  else if (ne)
+    ND_ENG(nd, sh, long_values(&job));
+  if (ne) ND_HIP(nd, hipStreamWaitEvent(eng->stream, sh.ev_rs_out, 0));
   return JY_OK;
 }
 

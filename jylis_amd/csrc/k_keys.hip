@@ -202,17 +202,16 @@ __global__ __launch_bounds__(kThreads) void k_key_probe(In I, Dir D, u32* __rest
 // by kSumGroups workgroups of 256 into [kSumGroups][3]; the host adds those
 // up with its read-back.  (One workgroup of 1024 walking all the rows took 19
 // us at 32.8K rows, the node TREG call's 8.39M keys: its loads wait in line.)
-// The words land in mapped pinned memory, [kSumGroups][3] and then two more:
-// the caller's extra word (`also`) and the completion number.  The last
+// The words land in mapped pinned memory, [kSumGroups][3] and then the
+// completion number.  The last
 // workgroup to publish writes the completion number (system-scope release
 // after every workgroup's system fence), so the host spins on one word of
 // its own memory instead of waking from a stream synchronise.
 constexpr int kSumThreads = 256;
 constexpr u32 kSumGroups = 128;
-constexpr u32 kWordAlso = kSumGroups * 3, kWordDone = kWordAlso + 1, kSumWords = kWordDone + 1;
+constexpr u32 kWordDone = kSumGroups * 3, kSumWords = kWordDone + 1;
 __global__ __launch_bounds__(kSumThreads) void k_key_sum(const u64* __restrict__ parts, u64 nb,
-                                                         u64* __restrict__ counts, const u64* __restrict__ also,
-                                                         u32* __restrict__ done, u64 seq) {
+                                                         u64* __restrict__ counts, u32* __restrict__ done, u64 seq) {
   __shared__ u64 red[3][kSumThreads / 64];
   u64 v[3] = {0, 0, 0};
   for (u64 b = (u64)blockIdx.x * kSumThreads + threadIdx.x; b < nb; b += (u64)gridDim.x * kSumThreads) {
@@ -231,9 +230,7 @@ __global__ __launch_bounds__(kSumThreads) void k_key_sum(const u64* __restrict__
     // mapped pinned memory: system-scope vector stores
     __hip_atomic_store(counts + (u64)blockIdx.x * 3 + threadIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  if (blockIdx.x == 0 && threadIdx.x == 3)
-    __hip_atomic_store(counts + kWordAlso, also ? *also : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (threadIdx.x < 4) __threadfence_system();
+  if (threadIdx.x < 3) __threadfence_system();
   __syncthreads();
   if (threadIdx.x == 0) {
     const u32 prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
@@ -438,11 +435,9 @@ void jy_keydir_free(jy_engine* eng, KeyDir& K) {
 // key count before any call sizes work by it).
 // after_probe (optional) runs on the host once the probe is enqueued and
 // before the host waits for its counts: a caller stages its next inputs there
-// while the GPU probes.  also (optional): a device word written by earlier
-// work on the stream, returned in *also_out with the probe's counts (one
-// read-back for both)
+// while the GPU probes
 int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, const u64* ko, u32* slots, bool create,
-                      u64* created, int32_t (*after_probe)(void*), void* arg, const u64* also, u64* also_out) {
+                      u64* created, int32_t (*after_probe)(void*), void* arg) {
   *created = 0;
   if (n == 0) return JY_OK;
   if (n >= kIdxMask) return eng->fail(JY_ERANGE, "too many keys in one call");
@@ -483,10 +478,9 @@ int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, co
   JY_HIP(eng, hipGetLastError());
   const u32 ng = (u32)std::min<u64>(kSumGroups, (nb + kSumThreads - 1) / kSumThreads);
   const u64 seq = ++eng->kd_seq;
-  hipLaunchKernelGGL(k_key_sum, dim3(ng), dim3(kSumThreads), 0, eng->stream, parts, nb, counts, also, eng->kd_done,
-                     seq);
+  hipLaunchKernelGGL(k_key_sum, dim3(ng), dim3(kSumThreads), 0, eng->stream, parts, nb, counts, eng->kd_done, seq);
   JY_HIP(eng, hipGetLastError());
-  if (after_probe) JY_TRY(after_probe(arg));  // (its copies follow the sums in stream order)
+  if (after_probe) JY_TRY(after_probe(arg));  // (what it enqueues here follows the sums)
   const u64* hg = eng->kd_words;
   const double t0 = jy_now_us();
   // the sums' completion number means every launch before them is done as
@@ -505,7 +499,6 @@ int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, co
   if (!seen) JY_HIP(eng, hipStreamSynchronize(eng->stream));
   JY_TRACE("keydir %llu keys: probe counts after %.1f us of waiting (%s)", (unsigned long long)n, jy_now_us() - t0,
            seen ? "spin" : "stream sync");
-  if (also_out) *also_out = hg[kWordAlso];
   u64 hc[3] = {0, 0, 0};
   for (u32 g = 0; g < ng; g++)
     for (int q = 0; q < 3; q++) hc[q] += hg[g * 3 + q];
