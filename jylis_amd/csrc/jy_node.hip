@@ -1343,8 +1343,8 @@ namespace {
 // ---- one shard (S = 1) ----
 // The node's only shard owns every key: no regroup, no exchange, no copy of
 // any wire column.  The owner phase reads the staged inputs in place; the
-// long values' total (the arena's reservation) rides on the key directory's
-// probe wait.  (Through the regroup + self exchange, an 8.39M-key TREG call
+// value work runs beside the key probe (one_keys_values).  (Through the
+// regroup + self exchange, an 8.39M-key TREG call
 // spent ~0.9 ms of its 1.6 ms before the key probe: profiles/r05_*.)
 
 // up to 8 words of device (or host) memory, one wait
@@ -1363,8 +1363,10 @@ int32_t readn(jy_node* nd, NdShard& sh, int32_t mem, std::initializer_list<const
 // probe waits on random table lines, the value kernels stream): heads and
 // tile sums first; once the probe is enqueued, the host waits for their total,
 // reserves the arena and enqueues the long values; the engine stream waits
-// for them before the merge.  (In one stream: 8.39M-key TREG call 0.66 ms,
-// of which ~70 us heads + scan and ~85 us long values ran after the probe.)
+// for them before the merge.  (In one stream the 8.39M-key TREG call took
+// 0.651 ms, ~70 us heads + scan and ~85 us long values after the probe; side
+// by side 0.636: the probe itself slows from 329 to 438 us beside them,
+// profiles/r05_node_value_overlap_ab.txt.)
 struct OneVals {
   u64 ne = 0;
   const u64* vo = nullptr;  // device, indexed from the first value
