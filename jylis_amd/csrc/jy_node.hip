@@ -428,8 +428,10 @@ __global__ __launch_bounds__(kT) void k_nd1_long(u64 n, const u64* __restrict__ 
 // the value tiles' long-byte sums scanned by one workgroup (toff[j],
 // exclusive; toff[nt] the total, also stored to mapped pinned memory for the
 // host).  A few thousand tiles per call (8.39M values: 8,192): no look-back.
-// Rows of 1024 consecutive sums, kTScanU rows' loads issued together.
-constexpr int kTScanThreads = 1024, kTScanU = 8;
+// Rows of 256 consecutive sums, kTScanU rows' loads issued together.  (A
+// 1024-thread workgroup waited up to 245 us for a CU with 16 free wave slots
+// beside the key probe's workgroups.)
+constexpr int kTScanThreads = 256, kTScanU = 8;
 __global__ __launch_bounds__(kTScanThreads) void k_nd1_tscan(const u64* __restrict__ tsum, u64 nt,
                                                              u64* __restrict__ toff, u64* __restrict__ total_pin) {
   __shared__ u64 red[kTScanThreads / 64];
