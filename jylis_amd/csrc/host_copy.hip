@@ -40,7 +40,7 @@ class CopyPool {
   int workers() const { return (int)th_.size(); }
 
   // copy [src, src + bytes) to dst; issue(off, len) is called on the calling
-  // thread for every chunk, in order, once it and all before it are copied
+  // thread, in order, for each run of chunks copied since the last call
   template <class F>
   int32_t run(uint8_t* dst, const uint8_t* src, u64 bytes, F&& issue) {
     std::lock_guard<std::mutex> use(use_mu_);
@@ -64,10 +64,16 @@ class CopyPool {
       u64 c;
       if (claim(g, nch, c)) copy_chunk(j, c, tag);
       else if (issued < nch) std::this_thread::yield();
-      while (issued < nch && done_[issued].load(std::memory_order_acquire) == tag) {
-        const u64 off = issued * kChunk;
-        if (rc == JY_OK) rc = issue(off, std::min<u64>(kChunk, bytes - off));
-        issued++;
+      // every copied chunk from `issued` on goes out in ONE DMA: the link
+      // idles ~10 us between two DMAs (1-MB DMAs: 24.7 us each, one every
+      // ~35 us, ~30 GB/s), so the chunks the pool has finished meanwhile ride
+      // together
+      u64 k = issued;
+      while (k < nch && done_[k].load(std::memory_order_acquire) == tag) k++;
+      if (k > issued) {
+        const u64 off = issued * kChunk, end = std::min<u64>(k * kChunk, bytes);
+        if (rc == JY_OK) rc = issue(off, end - off);
+        issued = k;
       }
       if (issued == nch) break;
     }
@@ -140,8 +146,8 @@ class CopyPool {
 
 }  // namespace
 
-// host -> pinned -> device in chunks: the DMA of a chunk is enqueued on the
-// engine stream as soon as it (and every chunk before it) has been copied
+// host -> pinned -> device in chunks: the copied chunks' DMA is enqueued on
+// the engine stream as soon as they (and every chunk before them) are copied
 int32_t jy_copy_h2d_staged(jy_engine* eng, void* dev, uint8_t* pinned, const void* src, u64 bytes) {
   const uint8_t* s = static_cast<const uint8_t*>(src);
   uint8_t* d = static_cast<uint8_t*>(dev);
