@@ -312,8 +312,22 @@ int32_t jy_ujson_flush(jy_engine* eng, uint64_t cap_docs, uint64_t cap_el, uint6
  * [0] touched state elements, [1] touched state cloud dots, [2] elements
  * written, [3] cloud dots written, [4] delta elements, [5] delta cloud dots,
  * [6] delta documents, [7] converge calls.  Bench / telemetry only: the
- * bytes a converge really moved. */
+ * bytes a converge really moved.  [0..3] count the regular merge path only. */
 int32_t jy_ujson_stats(jy_engine* eng, uint64_t* out8);
+/* the same eight, then the in-place layout of long documents:
+ * [8] delta docs converged in place, [9] / [10] their state elements / cloud
+ * dots (examined by the join, never read), [11] / [12] elements / cloud dots
+ * appended, [13] cloud dots folded into the vv, [14] documents promoted to
+ * the per-column layout, [15] documents demoted to the regular path */
+int32_t jy_ujson_stats_ext(jy_engine* eng, uint64_t* out16);
+/* UJSON in-place layout (an engine choice, invisible in every result): a
+ * document whose merged state holds at least min_elems elements keeps one
+ * element run and one cloud run per replica column with room behind it, so
+ * a delta whose dots all lie above what the document's column holds (the
+ * usual case: fresh inserts) is appended where it lies instead of rewriting
+ * the document.  0 stops promotions (documents already in the layout stay).
+ * Default 128 (env JY_UJ_LONG_MIN); needs ujson_columns <= 64. */
+int32_t jy_ujson_set_inplace(jy_engine* eng, uint32_t min_elems);
 
 /* ---- multi-GPU routing: the exchange step of a key-hash-sharded node ----
  * Replaces nothing in the reference (every node holds every key there); it is
@@ -465,10 +479,13 @@ int32_t jy_ujson_converge_routed(jy_engine* eng, uint32_t nsrc, uint64_t cap_k, 
  * one group at a time, issued from one thread (database.pony:18-23 makes the
  * five actors; cluster.pony:205-213 is the broadcast this replaces).  A
  * queued job's failure is returned by the node's next call (converge, fence,
- * lock, sync, stats, replica_col) and its detail by jy_node_last_error.
- * JY_DEVICE inputs are read by the worker later: they must stay valid and
- * unchanged until jy_node_fence (every queued job issued to its streams) or
- * jy_node_sync returns.  The engines of a node (jy_node_engine) are shared
+ * lock, sync, stats) and its detail by jy_node_last_error.
+ * JY_DEVICE inputs are read by the worker later, and on streams of the node's
+ * own (the read-back stream reads offsets, value lengths and value heads
+ * beside the engine stream): they must be complete device-wide before the
+ * call (no pending write on any stream) and stay valid and unchanged until
+ * jy_node_fence (every queued job issued to its streams) AND the GPU work
+ * reading them has finished -- jy_node_sync returns after both.  The engines of a node (jy_node_engine) are shared
  * with the worker: use them between jy_node_lock and jy_node_unlock (the
  * lock first waits for every job queued before it), or after jy_node_sync
  * with no node call in flight. */
@@ -514,9 +531,13 @@ uint32_t jy_node_nshards(const jy_node* node);
 jy_engine* jy_node_engine(jy_node* node, uint32_t shard);
 uint32_t jy_node_shard_of(const jy_node* node, const uint8_t* key, uint64_t len);
 /* register a replica identity on every local shard (the same column on all:
- * every process registers the cluster's identities in one order) */
+ * every process registers the cluster's identities in one order).  A known
+ * identity is answered without waiting for the worker; a new one takes the
+ * node's lock (not a fence) */
 int32_t jy_node_replica_col(jy_node* node, uint64_t replica_id, uint32_t* col_out);
-/* every queued job issued and its GPU work finished (blocks) */
+/* every queued job issued and its GPU work finished on every shard's streams
+ * (blocks); then a queued job's failure, if any -- the streams are drained on
+ * that path too, so JY_DEVICE inputs may be freed once it returns */
 int32_t jy_node_sync(jy_node* node);
 /* every job queued before this call issued to the GPU streams (blocks until
  * the worker took them, not for the GPU); device inputs of those calls are
@@ -527,6 +548,21 @@ int32_t jy_node_fence(jy_node* node);
  * lock is held even when an earlier job's failure is returned. */
 int32_t jy_node_lock(jy_node* node);
 void jy_node_unlock(jy_node* node);
+/* the same, waiting only for the jobs of CRDT type `type` queued before it
+ * (round 6): the types' engine states are disjoint and every engine call the
+ * holder makes is ordered after the issued jobs on the engine stream, so a
+ * TREG read does not wait for queued UJSON converges.  JY_NODE_NOFENCE waits
+ * for no job (a read of state no converge changes: deltas_size, flush).  The
+ * lock is held even when a job's failure is returned. */
+#define JY_NODE_NOFENCE (-1)
+int32_t jy_node_lock_type(jy_node* node, int32_t type);
+/* jobs queued or running: of CRDT type `type`, or all with type < 0 */
+int32_t jy_node_pending(jy_node* node, int32_t type, uint64_t* n_out);
+/* the worker reclaims a shard's TREG / TLOG value arena after that type's
+ * jobs once its dead bytes pass twice the live ones (+ 1 MiB): the policy the
+ * Pony glue ran after every drain under the lock.  Off by default; callers
+ * that pack value handles must consume them under the lock. */
+int32_t jy_node_arena_gc(jy_node* node, uint32_t enable);
 
 /* Converge one decoded peer batch (per process).  Keys: n strings (key_bytes,
  * key_offs[n + 1]).  `mem` = JY_HOST (staged per ingest shard) or JY_DEVICE

@@ -103,6 +103,8 @@ SIGNATURES = {
     "jy_ujson_read_sizes": (I32, [P, U64, P, P, P]),
     "jy_ujson_read": (I32, [P, U64, P, P, P, P, P, P, P]),
     "jy_ujson_stats": (I32, [P, P]),
+    "jy_ujson_stats_ext": (I32, [P, P]),
+    "jy_ujson_set_inplace": (I32, [P, U32]),
     "jy_tlog_stats": (I32, [P, P]),
     "jy_arena_usage": (I32, [P, I32, P, P]),
     "jy_arena_collect": (I32, [P, I32, P]),
@@ -143,6 +145,9 @@ SIGNATURES = {
     "jy_node_fence": (I32, [P]),
     "jy_node_lock": (I32, [P]),
     "jy_node_unlock": (None, [P]),
+    "jy_node_lock_type": (I32, [P, I32]),
+    "jy_node_pending": (I32, [P, I32, P]),
+    "jy_node_arena_gc": (I32, [P, U32]),
     "jy_node_counter_converge": (I32, [P, I32, U64, P, P, P, P, P, P, I32]),
     "jy_node_treg_converge": (I32, [P, U64, P, P, P, P, P, I32]),
     "jy_node_tlog_converge": (I32, [P, U64, P, P, P, P, P, P, P, I32]),

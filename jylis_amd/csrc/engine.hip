@@ -366,6 +366,14 @@ void jy_engine_destroy(jy_engine* eng) {
     for (auto& a : u->st) F(a.p);
     F(u->tmap.p);
     F(u->stats);
+    F(u->lpe);
+    F(u->lpc);
+    F(u->lcol);
+    F(u->lplan);
+    F(u->jobs);
+    F(u->fast);
+    F(u->nf);
+    F(u->plist);
     if (u->pin) hipHostFree(u->pin);
     for (hipEvent_t e : u->ready)
       if (e) hipEventDestroy(e);

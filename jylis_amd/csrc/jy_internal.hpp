@@ -350,6 +350,65 @@ struct alignas(16) UMeta {
   u32 clen, ccap;
 };
 
+// ---- UJSON in-place layout of long documents (k_ujson.hip, round 6) ----
+// A document of at least UjsonState::long_min elements ("long") keeps ONE
+// element run and ONE cloud run PER REPLICA COLUMN in the long pools, each
+// with room behind it.  Its UMeta then reads {lid, elen total, kLongMark,
+// 0, clen total, kLongMark}: ebase is the long-document id, the totals stay
+// exact (sizes, reads and compaction use them).  A converge whose delta is
+// append-shaped for such a document (every delta dot above the state's
+// context in its column, or already covered and removing nothing; the
+// delta's vv adding nothing) appends the new dots at the column runs' tails
+// and folds the cloud in place: the state's runs are never read or moved.
+constexpr u32 kLongMark = 0xFFFFFFFFu;
+struct alignas(16) LCol {  // [lid][R]: column c's runs (pool indices of the long pools)
+  u64 ebase;
+  u32 elen, ecap;
+  u64 cbase;
+  u32 clen, ccap;
+};
+struct alignas(16) LPlan {  // [lid][R]: one converge's plan for column c of a long document
+  // epoch << 32 | value, written by single items (k_uj_items / k_uj_flags):
+  u64 efs, ece;    // delta elements: first fresh one, end of the column's range
+  u64 cfs, cce;    // delta cloud: the same
+  u64 nfold;       // fresh cloud dots folded into the vv (an empty cloud run only)
+  u64 treq;        // live state elements the delta removes, all in the run's first kTrimSpan (k_uj_items)
+  u64 tcut;        // how many the trim removed (k_uj_jobs)
+  // written by the document's own thread (k_uj_docs) once it is judged in place:
+  u64 erun, crun;  // the runs after this converge (moved when they had to grow)
+  u64 eapp, capp;  // where the appended items start
+  u32 ecap, ccap;  // the runs' capacities after this converge
+  u32 cz, pad;     // the cloud run was empty: fresh dots go to crun + rank (fold mode)
+};
+// a copy job of the in-place layout (k_uj_jobs), one per document: a
+// demotion (long column runs -> a regular run at e / c), the column runs of a
+// document in place that had to grow (-> LPlan erun / crun), a promotion (the
+// regular run at e / c -> the new long column runs)
+struct alignas(16) UJob {
+  u64 e, c;  // the regular run's element / cloud base (demotion: destination, promotion: source)
+  u64 n;     // items to copy (elements + cloud dots)
+  u32 what;  // UJobWhat
+  u32 lid;
+};
+enum UJobWhat : u32 { UJ_DEMOTE = 0, UJ_REGROW, UJ_PROMOTE, UJ_TRIM };
+// a document in place whose delta removes live elements near the start of a
+// column run (a vv entry covering the run's first elements, a context dot of
+// an old element): the run's first kTrimSpan elements are compacted towards
+// its end in one workgroup (k_uj_jobs), the run's start moves up
+constexpr u32 kTrimSpan = 256;
+// element (kEl) / cloud entry j of a long document, in the order of a regular
+// run (ascending dot = column-major): its index in the long pool
+template <bool kEl>
+__device__ __forceinline__ u64 uj_long_at(const LCol* lc, u32 R, u64 j) {
+  for (u32 c = 0; c < R; c++) {
+    const LCol L = lc[c];
+    const u64 n = kEl ? L.elen : L.clen;
+    if (j < n) return (kEl ? L.ebase : L.cbase) + j;
+    j -= n;
+  }
+  return 0;  // j beyond the document's total: not reached by callers
+}
+
 struct UjsonState {  // per-document pool segments + dense vv
   UMeta* meta = nullptr;  // [kcap]
   URec* epool = nullptr;  // element pool
@@ -390,7 +449,26 @@ struct UjsonState {  // per-document pool segments + dense vv
   u64 live_e = 0, live_c = 0;          // upper bounds of live elements / cloud dots
   DevArray st[6];                      // look-back status words of the scans (zeroed once)
   DevArray tmap;                       // epoch-tagged tile -> doc maps of long segments (zeroed once)
-  u64* stats = nullptr;                // [8] cumulative converge counters (jy_ujson_stats)
+  u64* stats = nullptr;                // [16] cumulative converge counters (jy_ujson_stats[_ext])
+  // in-place layout of long documents (LCol above).  ctr[2] / ctr[3]: long
+  // pool bump pointers, ctr[4]: long ids handed out, ctr[5]: copy jobs of
+  // the converge's demotions and regrowths, ctr[6]: documents to promote (=
+  // their copy jobs).  pin[24 + 3 r ..]: ctr[2..4] as converge r saw them.
+  bool allow_long = false;  // this store may promote (the state; never the pending deltas)
+  u32 long_min = 0;         // promotion threshold in elements (0: none)
+  URec* lpe = nullptr;      // long element pool
+  u64 lpe_cap = 0;
+  u64* lpc = nullptr;       // long cloud pool
+  u64 lpc_cap = 0;
+  LCol* lcol = nullptr;     // [lcap][R]
+  LPlan* lplan = nullptr;   // [lcap][R] (epoch tags: zeroed once)
+  u64 lcap = 0;
+  UJob* jobs = nullptr;     // [3][jcap]: demotion / regrowth / trim jobs (two per delta doc at most), promotion jobs (one per plist entry)
+  u64 jcap = 0;
+  u32* fast = nullptr;      // [dcap] == epoch: the delta doc converges in place
+  u32* nf = nullptr;        // [dcap] == epoch: a long doc whose delta is not append-shaped
+  u32* plist = nullptr;     // [dcap] delta docs whose merged document is promoted
+  u64 long_used_e = 0, long_used_c = 0, long_ids = 0;  // the newest readback of ctr[2..4]
 };
 
 struct Arena {
@@ -552,6 +630,7 @@ int32_t jy_treg_fold(jy_engine* eng);
 // long values start on 8-byte granules (an arena collection maps granules)
 constexpr u64 kArenaAlign = 8;
 int32_t jy_arena_append_dev(jy_engine* eng, int32_t type, const uint8_t* src, u64 bytes, u64* rebase_out);
+int32_t jy_arena_ensure(jy_engine* eng, int32_t type, u64 bytes);  // room for `bytes` more, without moving later
 // look-back status words for `ntiles` tiles, the ticket counter and a fresh epoch
 int32_t jy_dscan_ctx(jy_engine* eng, u64 ntiles, u64** status, u32** tick, u32* epoch);
 // copy a borrowed input into device memory if it is on the host; returns a

@@ -46,6 +46,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <initializer_list>
 #include <condition_variable>
 #include <cstring>
@@ -536,6 +537,7 @@ enum JobKind { K_COUNTER, K_TREG, K_TLOG, K_UJSON, K_BLOCK };
 struct NdJob {
   int kind = 0;
   int32_t type = 0, mem = JY_DEVICE;
+  int32_t fty = 0;  // the CRDT type whose state the job changes (per-type fences)
   u64 n = 0;
   const void* a[11] = {};  // the call's arrays (host inputs: rebased into the pinned block)
   int pin = -1;
@@ -564,6 +566,18 @@ struct jy_node {
   std::condition_variable qcv, dcv;
   std::deque<NdJob> q;
   u64 submitted = 0, finished = 0;
+  u64 sub_t[JY_NTYPES] = {}, fin_t[JY_NTYPES] = {};  // the same per CRDT type (jy_node_lock_type)
+  bool arena_gc = false;  // jy_node_arena_gc: the worker reclaims TREG / TLOG arenas after their jobs
+  // callers waiting in jy_node_lock[_type]: the worker lets them in before it
+  // takes the next job (std::mutex is not fair: a worker with a long queue
+  // would otherwise take the lock back every time and starve a reader)
+  std::atomic<int> lock_waiters{0};
+  std::vector<u64> arena_live;  // [local shard][2]: bytes kept by the last collection (TREG, TLOG)
+  // replica columns registered on every shard (jy_node_replica_col): a
+  // known id is answered from here, under its own small mutex, without
+  // waiting for the worker
+  std::mutex rmu;
+  std::unordered_map<u64, u32> rep;
   bool stop = false, inline_jobs = false;
   bool regroup_one = false;  // JY_NODE_REGROUP_ONE=1: S = 1 through the regroup + exchange (A/B, tests)
   std::thread worker;
@@ -587,6 +601,8 @@ namespace {
 void exec_start(jy_node* nd);
 void exec_stop(jy_node* nd);
 int32_t exec_fence(jy_node* nd);  // every queued job issued; a queued job's failure, if any
+int32_t exec_fence_type(jy_node* nd, int32_t type);  // the same for one CRDT type's jobs
+int32_t exec_pending(jy_node* nd);                   // a queued job's failure, without waiting
 }  // namespace
 
 namespace {
@@ -1303,9 +1319,20 @@ uint32_t jy_node_shard_of(const jy_node* nd, const uint8_t* key, uint64_t len) {
   return jy_key_owner(key, len, nd ? nd->S : 1);
 }
 
+// A registered id is answered from the node's own map (no wait for the
+// worker); a new one is registered on every shard under the node
+// mutex -- no fence: no job queued before it can name a column not yet
+// registered (callers register before they send cells).
 int32_t jy_node_replica_col(jy_node* nd, uint64_t id, uint32_t* col) {
   if (!nd) return JY_EINVAL;
-  JY_TRY(exec_fence(nd));
+  {
+    std::lock_guard<std::mutex> r(nd->rmu);
+    auto it = nd->rep.find(id);
+    if (it != nd->rep.end()) {
+      *col = it->second;
+      return JY_OK;
+    }
+  }
   std::lock_guard<std::mutex> g(nd->mu);
   u32 c0 = 0;
   for (u32 L = 0; L < nd->nlocal; L++) {
@@ -1316,18 +1343,35 @@ int32_t jy_node_replica_col(jy_node* nd, uint64_t id, uint32_t* col) {
   }
   *col = c0;
   nd->nrep = std::max<u32>(nd->nrep, c0 + 1);
+  std::lock_guard<std::mutex> r(nd->rmu);
+  nd->rep[id] = c0;
   return JY_OK;
 }
 
+// every queued job issued and every shard's streams drained, THEN a queued
+// job's failure (the streams are synchronised on the error path
+// too, so a caller may free its JY_DEVICE inputs once this returns)
 int32_t jy_node_sync(jy_node* nd) {
   if (!nd) return JY_EINVAL;
-  JY_TRY(exec_fence(nd));
-  std::lock_guard<std::mutex> g(nd->mu);
-  for (NdShard& sh : nd->sh) {
-    ND_ENG(nd, sh, jy_sync(sh.eng));
-    ND_HIP(nd, hipStreamSynchronize(sh.xs));
+  int32_t rc;
+  {
+    std::unique_lock<std::mutex> lk(nd->qmu);
+    nd->dcv.wait(lk, [&] { return nd->finished == nd->submitted; });
   }
-  return JY_OK;
+  {
+    std::lock_guard<std::mutex> g(nd->mu);
+    rc = JY_OK;
+    for (NdShard& sh : nd->sh) {  // (every shard, whatever failed first)
+      const int32_t re = jy_sync(sh.eng);  // spilled TLOG merges settled, the engine stream drained
+      hipSetDevice(sh.dev);
+      const hipError_t e1 = hipStreamSynchronize(sh.xs), e2 = hipStreamSynchronize(sh.rs);
+      if (rc == JY_OK && re != JY_OK) rc = nd->fail(re, std::string("shard ") + std::to_string(sh.rank) + ": " + sh.eng->err);
+      if (rc == JY_OK && (e1 != hipSuccess || e2 != hipSuccess))
+        rc = nd->fail(JY_EHIP, "node sync: a shard's stream failed");
+    }
+  }
+  const int32_t pend = exec_pending(nd);
+  return pend != JY_OK ? pend : rc;
 }
 
 int32_t jy_node_stats(jy_node* nd, uint64_t* out5) {
@@ -1374,6 +1418,7 @@ struct OneVals {
   const u64* vo = nullptr;  // device, indexed from the first value
   u64 vbase = 0;
   const uint8_t* vb = nullptr;
+  u64 vbytes = 0;  // the values' bytes in all (bounds the long values' arena total)
 };
 struct LongJob {
   jy_node* nd;
@@ -1393,7 +1438,10 @@ int32_t long_values(void* p) {
   const u64 total = sh.pin[2 * kMaxS * kMaxW + 3];
   uint8_t* dst;
   u64 rebase;
+  const u64 cap = eng->arena[j.type].cap;
   JY_TRY(jy_arena_reserve(eng, j.type, total, &dst, &rebase));
+  if (eng->arena[j.type].cap != cap)  // one_keys_values made room: never reached
+    return eng->fail(JY_EINVAL, "node: the arena moved under the read-back stream");
   hipLaunchKernelGGL(k_nd1_long, dim3((u32)j.nvt), dim3(kT), 0, sh.rs, j.vals->ne, j.vals->vo, j.vals->vbase,
                      j.vals->vb, j.toff, dst, rebase, j.lr);
   if (hipGetLastError() != hipSuccess || hipEventRecord(sh.ev_rs_out, sh.rs) != hipSuccess)
@@ -1415,6 +1463,11 @@ int32_t one_keys_values(jy_node* nd, NdShard& sh, int32_t type, u64 n, const uin
   }
   LongJob job{nd, &sh, type, vals, nvt, toff, vals ? *lr : nullptr};
   if (ne) {
+    // the arena holds the long values' total already (at most every value's
+    // bytes + a granule's padding each): long_values then only advances its
+    // length on the read-back stream -- a growth there would reallocate on
+    // the engine stream, past ev_rs_in, while k_nd1_long writes the new tail
+    ND_ENG(nd, sh, jy_arena_ensure(eng, type, vals->vbytes + kArenaAlign * ne));
     // after the staged inputs and the previous call's kernels (which read
     // pre / lr / the arena) on the engine stream
     ND_HIP(nd, hipEventRecord(sh.ev_rs_in, eng->stream));
@@ -1464,7 +1517,7 @@ int32_t run_treg_one(jy_node* nd, u64 n, const uint8_t* kb, const u64* ko, const
   JY_TRY(stage(nd, sh, 3, vo, (n + 1) * 8, mem, &dvo));
   JY_TRY(stage(nd, sh, 4, on_host(mem) ? vb + v0 : vb, v1 - v0, mem, &dvb));
   ND_ENG(nd, sh, jy_stage_end(sh.eng));
-  OneVals vals{n, static_cast<const u64*>(dvo), on_host(mem) ? v0 : 0, static_cast<const uint8_t*>(dvb)};
+  OneVals vals{n, static_cast<const u64*>(dvo), on_host(mem) ? v0 : 0, static_cast<const uint8_t*>(dvb), v1 - v0};
   u32* slots;
   u64 *pre, *lr;
   JY_TRY(one_keys_values(nd, sh, JY_TREG, n, rebased(dkb, on_host(mem) ? k0 : 0), static_cast<const u64*>(dko),
@@ -1550,7 +1603,8 @@ int32_t run_tlog_one(jy_node* nd, u64 n, const uint8_t* kb, const u64* ko, const
   hipLaunchKernelGGL(k_nd1_rebase, dim3(grid_of(n + 1)), dim3(kT), 0, eng->stream, n, static_cast<const u64*>(deo),
                      rel);
   ND_HIP(nd, hipGetLastError());
-  OneVals vals{ne, static_cast<const u64*>(dvo) + ent, on_host(mem) ? v0 : 0, static_cast<const uint8_t*>(dvb)};
+  OneVals vals{ne, static_cast<const u64*>(dvo) + ent, on_host(mem) ? v0 : 0, static_cast<const uint8_t*>(dvb),
+               v1 - v0};
   u32* slots;
   u64 *pre, *lr;
   JY_TRY(one_keys_values(nd, sh, JY_TLOG, n, rebased(dkb, on_host(mem) ? k0 : 0), static_cast<const u64*>(dko),
@@ -2079,7 +2133,28 @@ void finish(jy_node* nd, const NdJob& j, int32_t rc) {
     nd->aerr_msg = std::this_thread::get_id() == nd->wid ? nd->werr : jy_node::caller_err();
   }
   nd->finished++;
+  nd->fin_t[j.fty]++;
   nd->dcv.notify_all();
+}
+
+// the worker's arena policy (jy_node_arena_gc), after a TREG / TLOG job and
+// under the node mutex: a shard's arena whose dead bytes pass twice the live
+// ones (+ 1 MiB) is collected -- the policy of jylis_amd/repo.py _ArenaGC and
+// of the Pony glue's maybe_collect, which the glue's drains no longer run
+// (they only enqueue).  Handles callers pack are consumed under the lock, so
+// none is outstanding between jobs.
+int32_t arena_policy(jy_node* nd, int32_t type) {
+  const int t = type == JY_TREG ? 0 : 1;
+  nd->arena_live.resize(2 * nd->nlocal, 0);
+  for (u32 L = 0; L < nd->nlocal; L++) {
+    jy_engine* eng = nd->sh[L].eng;
+    u64 len = 0, cap = 0, kept = 0;
+    ND_ENG(nd, nd->sh[L], jy_arena_usage(eng, type, &len, &cap));
+    if (len <= 2 * nd->arena_live[2 * L + t] + (1ull << 20)) continue;
+    ND_ENG(nd, nd->sh[L], jy_arena_collect(eng, type, &kept));
+    nd->arena_live[2 * L + t] = kept;
+  }
+  return JY_OK;
 }
 
 void worker_loop(jy_node* nd) {
@@ -2092,10 +2167,12 @@ void worker_loop(jy_node* nd) {
       j = std::move(nd->q.front());
       nd->q.pop_front();
     }
+    while (nd->lock_waiters.load(std::memory_order_acquire) > 0) std::this_thread::yield();
     int32_t rc;
     {
       std::lock_guard<std::mutex> g(nd->mu);
       rc = run_locked(nd, j);
+      if (rc == JY_OK && nd->arena_gc && (j.fty == JY_TREG || j.fty == JY_TLOG)) rc = arena_policy(nd, j.fty);
     }
     finish(nd, j, rc);
   }
@@ -2126,6 +2203,21 @@ void exec_stop(jy_node* nd) {
 int32_t exec_fence(jy_node* nd) {
   std::unique_lock<std::mutex> lk(nd->qmu);
   nd->dcv.wait(lk, [&] { return nd->finished == nd->submitted; });
+  if (nd->aerr == JY_OK) return JY_OK;
+  const int32_t rc = nd->aerr;
+  jy_node::caller_err() = nd->aerr_msg;
+  nd->aerr = JY_OK;
+  return rc;
+}
+
+// every job of CRDT type `type` queued so far has been issued (jobs of other
+// types may still be queued: the types' engine states are disjoint and the
+// engine stream orders what the caller enqueues next after every issued
+// job); then a queued job's failure, as exec_fence
+int32_t exec_fence_type(jy_node* nd, int32_t type) {
+  std::unique_lock<std::mutex> lk(nd->qmu);
+  const u64 target = nd->sub_t[type];
+  nd->dcv.wait(lk, [&] { return nd->fin_t[type] >= target; });
   if (nd->aerr == JY_OK) return JY_OK;
   const int32_t rc = nd->aerr;
   jy_node::caller_err() = nd->aerr_msg;
@@ -2222,23 +2314,27 @@ int32_t pack_host(jy_node* nd, const Pack& pk, NdJob& j) {
 }
 
 int32_t submit(jy_node* nd, NdJob&& j) {
+  j.fty = j.kind == K_TREG ? JY_TREG : j.kind == K_TLOG ? JY_TLOG : j.kind == K_UJSON ? JY_UJSON : j.type;
   if (nd->inline_jobs) {
     int32_t rc;
     {
       std::lock_guard<std::mutex> g(nd->mu);
       rc = run_locked(nd, j);
+      if (rc == JY_OK && nd->arena_gc && (j.fty == JY_TREG || j.fty == JY_TLOG)) rc = arena_policy(nd, j.fty);
     }
     {
       std::lock_guard<std::mutex> lk(nd->qmu);
       nd->submitted++;
+      nd->sub_t[j.fty]++;
     }
     finish(nd, j, JY_OK);
     return rc;
   }
   {
     std::lock_guard<std::mutex> lk(nd->qmu);
-    nd->q.push_back(std::move(j));
     nd->submitted++;
+    nd->sub_t[j.fty]++;
+    nd->q.push_back(std::move(j));
   }
   nd->qcv.notify_one();
   return JY_OK;
@@ -2400,11 +2496,41 @@ int32_t jy_node_fence(jy_node* nd) {
   return exec_fence(nd);
 }
 
+// the node mutex for a caller: announced, so the worker steps aside between jobs
+static void lock_caller(jy_node* nd) {
+  nd->lock_waiters.fetch_add(1, std::memory_order_acq_rel);
+  nd->mu.lock();
+  nd->lock_waiters.fetch_sub(1, std::memory_order_acq_rel);
+}
+
 int32_t jy_node_lock(jy_node* nd) {
   if (!nd) return JY_EINVAL;
   const int32_t rc = exec_fence(nd);
-  nd->mu.lock();
+  lock_caller(nd);
   return rc;
+}
+
+int32_t jy_node_lock_type(jy_node* nd, int32_t type) {
+  if (!nd) return JY_EINVAL;
+  if (type != JY_NODE_NOFENCE && (type < 0 || type >= JY_NTYPES)) return nd->fail(JY_EINVAL, "bad type");
+  const int32_t rc = type == JY_NODE_NOFENCE ? exec_pending(nd) : exec_fence_type(nd, type);
+  lock_caller(nd);
+  return rc;
+}
+
+int32_t jy_node_pending(jy_node* nd, int32_t type, uint64_t* n_out) {
+  if (!nd) return JY_EINVAL;
+  if (type >= JY_NTYPES) return nd->fail(JY_EINVAL, "bad type");
+  std::lock_guard<std::mutex> lk(nd->qmu);
+  *n_out = type < 0 ? nd->submitted - nd->finished : nd->sub_t[type] - nd->fin_t[type];
+  return JY_OK;
+}
+
+int32_t jy_node_arena_gc(jy_node* nd, uint32_t enable) {
+  if (!nd) return JY_EINVAL;
+  std::lock_guard<std::mutex> g(nd->mu);
+  nd->arena_gc = enable != 0;
+  return JY_OK;
 }
 
 void jy_node_unlock(jy_node* nd) {

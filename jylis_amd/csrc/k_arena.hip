@@ -142,6 +142,23 @@ extern "C" int32_t jy_arena_reserve(jy_engine* eng, int32_t type, uint64_t bytes
   return JY_OK;
 }
 
+// capacity for `bytes` more (aligned) without moving the arena later: a
+// reserve within it only advances the length (the node reserves the long
+// values' exact total on its read-back stream, where a reallocation on the
+// engine stream would not be ordered before the writes)
+int32_t jy_arena_ensure(jy_engine* eng, int32_t type, u64 bytes) {
+  if (type != JY_TREG && type != JY_TLOG) return eng->fail(JY_EINVAL, "only TREG and TLOG hold an arena");
+  Arena& a = eng->arena[type];
+  const u64 at = (a.len + kArenaAlign - 1) / kArenaAlign * kArenaAlign;
+  if (at + bytes <= a.cap && a.p) return JY_OK;
+  const u64 nc = std::max<u64>(std::max<u64>(a.cap * 2, at + bytes), 1 << 16);
+  void* p = a.p;
+  JY_TRY(jy_realloc(eng, &p, a.len, nc, false));
+  a.p = static_cast<uint8_t*>(p);
+  a.cap = nc;
+  return JY_OK;
+}
+
 extern "C" int32_t jy_arena_usage(jy_engine* eng, int32_t type, uint64_t* len_out, uint64_t* cap_out) {
   if (type < 0 || type >= JY_NTYPES) return eng->fail(JY_EINVAL, "bad type");
   *len_out = eng->arena[type].len;

@@ -40,7 +40,23 @@ struct WArgs {
   const UMeta* meta;
   const URec* rec;
   const u64* vv;
+  const LCol* lcol;  // the in-place layout's column runs (k_ujson.hip), or nullptr
+  const URec* lpe;
 };
+
+// the element records of the doc of meta m in dot order: a regular run, or
+// a long document's column runs one after another
+template <typename Fn>
+__device__ __forceinline__ void for_each_rec(const WArgs& W, const UMeta& m, Fn&& fn) {
+  if (m.ecap == kLongMark) {
+    for (u32 c = 0; c < W.R; c++) {
+      const LCol L = W.lcol[m.ebase * W.R + c];
+      for (u64 j = 0; j < L.elen; j++) fn(W.lpe[L.ebase + j]);
+    }
+    return;
+  }
+  for (u64 j = 0; j < m.elen; j++) fn(W.rec[m.ebase + j]);
+}
 
 // delta sizes per command; every doc becomes pending
 __global__ __launch_bounds__(kThreads) void k_ujw_count(WArgs W, u64* __restrict__ ne, u64* __restrict__ nc,
@@ -58,7 +74,7 @@ __global__ __launch_bounds__(kThreads) void k_ujw_count(WArgs W, u64* __restrict
       c = m.elen;
     } else {
       const u64 h = W.elem[i];
-      for (u64 j = 0; j < m.elen; j++) c += W.rec[m.ebase + j].elem == h;
+      for_each_rec(W, m, [&](const URec& r) { c += r.elem == h; });
     }
   }
   ne[i] = e;
@@ -85,10 +101,9 @@ __global__ __launch_bounds__(kThreads) void k_ujw_fill(WArgs W, const u64* __res
   const UMeta m = W.meta[s];
   const u64 h = W.elem[i];
   u64 o = co[i];
-  for (u64 j = 0; j < m.elen; j++) {
-    const URec r = W.rec[m.ebase + j];
+  for_each_rec(W, m, [&](const URec& r) {
     if (op == JY_UJSON_CLR || r.elem == h) cloud[o++] = r.dot;
-  }
+  });
 }
 
 // flush: the pending docs' delta documents are emptied
@@ -146,7 +161,7 @@ int32_t jy_ujson_write_batch(jy_engine* eng, u64 n, const uint8_t* op, const u32
   u64* nc = ne + (n + 1);
   u64* eo = nc + (n + 1);
   u64* co = eo + (n + 1);
-  const WArgs W{op, slot, elem, n, col, u.R, u.meta, u.epool, u.vv};
+  const WArgs W{op, slot, elem, n, col, u.R, u.meta, u.epool, u.vv, u.lcol, u.lpe};
   JY_HIP(eng, hipMemsetAsync(ne + n, 0, 8, eng->stream));
   JY_HIP(eng, hipMemsetAsync(nc + n, 0, 8, eng->stream));
   LAUNCH(k_ujw_count, n, W, ne, nc, eng->uj_dflag, eng->uj_dcount);

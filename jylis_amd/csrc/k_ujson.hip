@@ -218,6 +218,7 @@ struct UjArgs {
   u64* ctr;          // bump pointers (device)
   u64* pin;          // mapped pinned: bump pointers after this converge
   u64* pin_t;        // mapped pinned: this converge's touched state elements / cloud dots
+  u64* pin_l;        // mapped pinned: the long pools' bump pointers and ids handed out
   u32 R;
   u32 epoch;
   u32 keep_all;      // context-only join: every state element stays (the write path's pending deltas)
@@ -273,9 +274,35 @@ struct UjArgs {
   u64* ktp;  // ... of ksc
   u64* st_ne;
   u64* st_nc;
+  // in-place layout of long documents (jy_internal.hpp LCol); lcol ==
+  // nullptr: the store has none and never promotes
+  LCol* lcol;
+  LPlan* lplan;
+  URec* lpe;
+  u64* lpc;
+  u64 lpe_cap, lpc_cap, lcap;
+  UJob* jobs;  // [2][jcap]
+  u64 jcap;
+  u32* fast;
+  u32* nf;
+  u32* plist;
+  u32 long_min;  // promotion threshold (0: none this converge)
 };
 
 __device__ __forceinline__ bool is_bad(const UjArgs& A, u64 k) { return A.bad[k] == A.epoch; }
+// the delta doc converges in place (k_uj_docs judged it append-shaped)
+__device__ __forceinline__ bool is_fast(const UjArgs& A, u64 k) { return A.lcol && A.fast[k] == A.epoch; }
+__device__ __forceinline__ u64 tag(const UjArgs& A, u64 v) { return ((u64)A.epoch << 32) | (u32)v; }
+__device__ __forceinline__ bool tagged(const UjArgs& A, u64 w) { return (u32)(w >> 32) == A.epoch; }
+// the long id of delta doc k's document, or ~0u (a regular document or a hole)
+__device__ __forceinline__ u32 long_id(const UjArgs& A, u64 k) {
+  const u32 s = A.slot[k];
+  if (s == JY_NO_SLOT) return ~0u;
+  const UMeta m = A.meta[s];
+  return m.ecap == kLongMark ? (u32)m.ebase : ~0u;
+}
+// capacity of a column run that must hold n: room for as many again
+__device__ __forceinline__ u32 roomy(u64 n) { return (u32)(2 * n + 16); }
 __device__ __forceinline__ void mark_bad(const UjArgs& A, u64 k) { A.bad[k] = A.epoch; }  // same value from every writer
 __device__ __forceinline__ u64 doc_at(const UjArgs& A, const u64* tm, u64 tile, const u32* sid, u64 i) {
   const u64 v = tm[tile];
@@ -372,6 +399,303 @@ struct Shared {
   u32 tk;
 };
 
+// membership of dot x in a sorted run [lo, hi) of dots
+__device__ __forceinline__ bool in_dots(const u64* a, u64 lo, u64 hi, u64 x) {
+  const u64 p = lb_g<false>(a, lo, hi, x);
+  return p < hi && a[p] == x;
+}
+
+// ---- U1a classification of one delta item of a LONG document (lid):
+// whether the delta is append-shaped in the item's column, and where the
+// column's fresh run of delta dots starts and ends (single writers: the first
+// fresh item, the column's last item).  Fresh = above everything the state's
+// column holds (vv, element and cloud runs).  A dot that is not fresh must
+// change nothing: a delta element already in the state's context (dropped, or
+// the state's own copy kept); a delta cloud dot in the state's context that
+// removes no live state element (none there, or the delta keeps it).  A vv
+// entry must not raise the state's and must lie below the column's first
+// element.  Anything else marks the doc: it is demoted (k_uj_docs).
+__device__ void uj_item_long(const UjArgs& A, int kind, u64 k, u64 i, u32 lid, u64 x) {
+  const u32 c = dcol(x);
+  if (c >= A.R) return;  // malformed: U1a marks the doc bad
+  const u32 s = A.slot[k];
+  const u64 li = (u64)lid * A.R + c;
+  const LCol L = A.lcol[li];
+  const u64 vs = A.vv[(u64)s * A.R + c], q = dseq(x);
+  if (kind == 2) {  // a vv entry of the delta: it must not raise the state's
+    if (q > vs) {
+      A.nf[k] = A.epoch;
+      return;
+    }
+    // the elements it covers (the run's prefix of seq <= q) go unless the
+    // delta holds them: a prefix within kTrimSpan is trimmed in place
+    if (L.elen && dseq(A.lpe[L.ebase].dot) <= q) {
+      const u64 cut = lb_g<true>(A.lpe, L.ebase, L.ebase + L.elen, mkdot(c, q + 1)) - L.ebase;
+      if (cut > kTrimSpan) A.nf[k] = A.epoch;
+      else A.lplan[li].treq = tag(A, 1);
+    }
+    return;
+  }
+  const u64 te = L.elen ? dseq(A.lpe[L.ebase + L.elen - 1].dot) : 0;
+  const u64 tc = L.clen ? dseq(A.lpc[L.cbase + L.clen - 1]) : 0;
+  const u64 F = vs > te ? (vs > tc ? vs : tc) : (te > tc ? te : tc);
+  const u64* a = kind == 0 ? A.ddots : A.dcloud;
+  const u64* offs = kind == 0 ? A.deoff : A.dcoff;
+  const u64 lo = offs[k], hi = offs[k + 1];
+  const u64 prev = i > lo ? a[i - 1] : 0, next = i + 1 < hi ? a[i + 1] : ~0ull;
+  const bool fresh = q > F;
+  LPlan& P = A.lplan[li];
+  if (fresh && (i == lo || dcol(prev) != c || dseq(prev) <= F)) (kind == 0 ? P.efs : P.cfs) = tag(A, i);
+  if (i + 1 == hi || dcol(next) != c) (kind == 0 ? P.ece : P.cce) = tag(A, i + 1);
+  if (fresh) return;
+  const bool seen = q <= vs || in_dots(A.lpc, L.cbase, L.cbase + L.clen, x);
+  if (!seen) {
+    A.nf[k] = A.epoch;
+    return;
+  }
+  if (kind == 1) {  // a context dot removes a live state element the delta does not hold
+    const u64 p = lb_g<true>(A.lpe, L.ebase, L.ebase + L.elen, x);
+    if (p < L.ebase + L.elen && A.lpe[p].dot == x && !in_dots(A.ddots, A.deoff[k], A.deoff[k + 1], x)) {
+      if (p - L.ebase >= kTrimSpan) A.nf[k] = A.epoch;  // too far in: the regular path
+      else P.treq = tag(A, 1);
+    }
+  }
+}
+
+// ---- U1b decision for a long document, one WAVE per document (lane c =
+// column c): in place when the delta is append-shaped; a column run that
+// overflows moves to a larger run of the long pool (a copy job, k_uj_jobs);
+// when the long pool is short, or the delta is not append-shaped, the
+// document is DEMOTED: a copy job lays its column runs out as one regular
+// run at the pools' bump pointers and the regular merge path takes it.
+// Returns (lane 0) the doc's touched state sizes for the scans (0 in place).
+__device__ void uj_docs_long(const UjArgs& A, u64 k, u64& asz, u64& csz) {
+  const u32 lane = threadIdx.x & 63, R = A.R;
+  const u32 s = A.slot[k];
+  const UMeta m = A.meta[s];
+  const u32 lid = (u32)m.ebase;
+  const u64 b = (u64)lid * R;
+  const bool act = lane < R;
+  LCol L{};
+  u64 efs = 0, ece = 0, cfs = 0, cce = 0, treq = 0;
+  if (act) {
+    L = A.lcol[b + lane];
+    const LPlan& P = A.lplan[b + lane];
+    efs = P.efs, ece = P.ece, cfs = P.cfs, cce = P.cce, treq = P.treq;
+  }
+  const bool tr = act && tagged(A, treq);
+  const u64 ne = tagged(A, efs) ? (u32)ece - (u32)efs : 0, nc = tagged(A, cfs) ? (u32)cce - (u32)cfs : 0;
+  const bool ge = act && L.elen + ne > L.ecap, gc = act && (L.clen ? L.clen + nc : nc) > L.ccap;
+  const bool broken = act && ((tagged(A, efs) && !tagged(A, ece)) || (tagged(A, cfs) && !tagged(A, cce)));
+  // (a run that moves is not trimmed in place as well)
+  bool fast = A.nf[k] != A.epoch && !__ballot(broken || (ge && tr));
+  const u64 ne_e = ge ? roomy(L.elen + ne) : 0, ne_c = gc ? roomy(L.clen + nc) : 0;
+  const u64 oe = jyscan::wave_incl<u64>(ne_e) - ne_e, oc = jyscan::wave_incl<u64>(ne_c) - ne_c;
+  const u64 NE = __shfl(oe + ne_e, 63), NC = __shfl(oc + ne_c, 63);
+  const u64 moved = jyscan::wave_sum<u64>((ge ? L.elen : 0) + (gc ? L.clen : 0));
+  u64 eb = 0, cb = 0, ok = fast;
+  if (lane == 0 && fast) {
+    // (a refused request wastes its reservation until the next compaction:
+    // the host keeps the long pools at 4x the live entries)
+    if (NE) eb = atomicAdd((unsigned long long*)(A.ctr + 2), (unsigned long long)NE), ok = eb + NE <= A.lpe_cap;
+    if (ok && NC) cb = atomicAdd((unsigned long long*)(A.ctr + 3), (unsigned long long)NC), ok = cb + NC <= A.lpc_cap;
+  }
+  fast = __shfl(ok, 0);
+  if (fast) {
+    eb = __shfl(eb, 0);
+    cb = __shfl(cb, 0);
+    if (act && (ne || nc || tr)) {
+      LPlan& P = A.lplan[b + lane];
+      const u64 erun = ge ? eb + oe : L.ebase, crun = gc ? cb + oc : L.cbase;
+      P.erun = erun;
+      P.crun = crun;
+      P.eapp = erun + L.elen;
+      P.capp = crun + L.clen;
+      P.ecap = ge ? (u32)ne_e : L.ecap;
+      P.ccap = gc ? (u32)ne_c : L.ccap;
+      P.cz = L.clen == 0;
+    }
+    const u64 trims = __popcll(__ballot(tr));
+    if (lane == 0) {
+      // the runs that grew are copied, the trims done, before any append
+      // (k_uj_jobs, then U2); a repeated doc's jobs are skipped there
+      if (moved) A.jobs[atomicAdd((unsigned long long*)(A.ctr + 5), 1ull)] = UJob{k, 0, moved, UJ_REGROW, lid};
+      if (trims) A.jobs[atomicAdd((unsigned long long*)(A.ctr + 5), 1ull)] = UJob{k, 0, R, UJ_TRIM, lid};
+      A.fast[k] = A.epoch;
+      A.abase[k] = lid;
+      asz = csz = 0;
+    }
+    return;
+  }
+  // demote: one regular run (the host's pool plan budgets it); U5 writes the
+  // merged document as usual, the long runs are left behind
+  if (lane == 0) {
+    eb = m.elen ? atomicAdd((unsigned long long*)A.ctr, (unsigned long long)m.elen) : 0;
+    cb = m.clen ? atomicAdd((unsigned long long*)(A.ctr + 1), (unsigned long long)m.clen) : 0;
+    if (m.elen + m.clen)
+      A.jobs[atomicAdd((unsigned long long*)(A.ctr + 5), 1ull)] = UJob{eb, cb, (u64)m.elen + m.clen, UJ_DEMOTE, lid};
+    A.abase[k] = eb;
+    A.cbs[k] = cb;
+    asz = m.elen;
+    csz = m.clen;
+    atomicAdd((unsigned long long*)(A.stats + 15), 1ull);
+  }
+}
+
+// ---- copy jobs of the in-place layout (demotions, regrowths, promotions),
+// one per document: its up to 2R column segments (elements, then cloud dots)
+// are laid out in LDS and copied in kJobChunk-item chunks dealt round-robin
+// over a persistent grid.  An empty list costs one load.
+constexpr u64 kJobChunk = 2048;
+constexpr int kMaxR = 64;  // the in-place layout needs R <= 64 (a lane per column)
+
+// the trim of column c of delta doc k (one workgroup): the run's first
+// min(elen, kTrimSpan) elements are staged in LDS, each keeps unless the
+// delta's context covers it (vv entry, cloud dot) and its map lacks it, and
+// the kept ones are written back right-aligned -- the run now starts
+// `removed` further up and ends where it did (appends are unaffected)
+__device__ void uj_trim_column(const UjArgs& A, u64 k, u32 lid, u32 c) {
+  __shared__ URec l_rec[kTrimSpan];
+  __shared__ u64 l_red[kThreads / 64];
+  __syncthreads();  // (the workgroup's previous trim is done with l_rec)
+  LPlan& P = A.lplan[(u64)lid * A.R + c];
+  if (!tagged(A, P.treq)) return;  // (uniform: every thread reads the same word)
+  const LCol L = A.lcol[(u64)lid * A.R + c];
+  const u32 nb = L.elen < kTrimSpan ? L.elen : kTrimSpan;
+  const u64 vd = A.vvd[k * A.R + c];
+  const u32 t = threadIdx.x;
+  u64 keep = 0;
+  if (t < nb) {
+    const URec r = A.lpe[L.ebase + t];
+    l_rec[t] = r;
+    const bool covered = dseq(r.dot) <= vd || in_dots(A.dcloud, A.dcoff[k], A.dcoff[k + 1], r.dot);
+    keep = !covered || in_dots(A.ddots, A.deoff[k], A.deoff[k + 1], r.dot);
+  }
+  u64 kept;
+  const u64 rank = jyscan::block_excl<kThreads, u64>(keep, l_red, kept);  // (syncs: l_rec is complete)
+  const u64 cut = nb - kept;
+  if (keep) A.lpe[L.ebase + cut + rank] = l_rec[t];
+  if (t == 0) P.tcut = tag(A, cut);
+}
+// one chunk of a copy job: its up to 2R column segments (elements, then
+// cloud dots) laid out in LDS, then the chunk's items copied
+__device__ void uj_job_chunk(const UjArgs& A, const UJob& J, u64 q) {
+  __shared__ u64 l_src[2 * kMaxR], l_dst[2 * kMaxR], l_pre[2 * kMaxR + 1];
+  const u32 R = A.R;
+  __syncthreads();  // (the workgroup's previous chunk is done with the table)
+  if (threadIdx.x < R) {  // lane c: column c's element and cloud segment
+    const u32 c = threadIdx.x;
+    const LCol L = A.lcol[(u64)J.lid * R + c];
+    u64 se = 0, de = 0, ne = 0, sc = 0, dc = 0, nc = 0;
+    if (J.what == UJ_REGROW) {
+      const LPlan& P = A.lplan[(u64)J.lid * R + c];
+      if (tagged(A, P.efs) || tagged(A, P.cfs)) {
+        if (P.erun != L.ebase) se = L.ebase, de = P.erun, ne = L.elen;
+        if (P.crun != L.cbase) sc = L.cbase, dc = P.crun, nc = L.clen;
+      }
+    } else {
+      ne = L.elen;
+      nc = L.clen;
+      se = de = L.ebase;  // the regular side is filled in below
+      sc = dc = L.cbase;
+    }
+    l_src[c] = se, l_dst[c] = de, l_pre[c] = ne;
+    l_src[R + c] = sc, l_dst[R + c] = dc, l_pre[R + c] = nc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // exclusive prefix over the 2R segments; the regular run's places
+    u64 acc = 0, oe = 0, oc = 0;
+    for (u32 g = 0; g < 2 * R; g++) {
+      const u64 len = l_pre[g];
+      if (J.what == UJ_DEMOTE) l_dst[g] = g < R ? J.e + oe : J.c + oc;
+      if (J.what == UJ_PROMOTE) l_src[g] = g < R ? J.e + oe : J.c + oc;
+      (g < R ? oe : oc) += len;
+      l_pre[g] = acc;
+      acc += len;
+    }
+    l_pre[2 * R] = acc;
+  }
+  __syncthreads();
+  const u64 i0 = q * kJobChunk, i1 = i0 + kJobChunk < J.n ? i0 + kJobChunk : J.n;
+  for (u64 t = i0 + threadIdx.x; t < i1; t += kThreads) {
+    u32 lo = 0, hi = 2 * R - 1;  // the last segment g with l_pre[g] <= t
+    while (lo < hi) {
+      const u32 mid = (lo + hi + 1) >> 1;
+      if (l_pre[mid] <= t) lo = mid;
+      else hi = mid - 1;
+    }
+    const u64 o = t - l_pre[lo];
+    const u64 si = l_src[lo] + o, di = l_dst[lo] + o;
+    if (lo < R) {
+      if (J.what == UJ_DEMOTE) A.epool_out[di] = A.lpe[si];
+      else if (J.what == UJ_REGROW) A.lpe[di] = A.lpe[si];
+      else A.lpe[di] = A.epool_out[si];
+    } else {
+      if (J.what == UJ_DEMOTE) A.cpool_out[di] = A.lpc[si];
+      else if (J.what == UJ_REGROW) A.lpc[di] = A.lpc[si];
+      else A.lpc[di] = A.cpool_out[si];
+    }
+  }
+}
+
+// The job list's chunks (kJobChunk items of a copy job; one column of a
+// trim) dealt round-robin over a persistent grid: the workgroups read a
+// block of job headers together, scan their chunk counts in LDS and find a
+// chunk's job by a search there (no walk over the list).  An empty list
+// costs one load.
+constexpr u32 kJobBlock = 2048;
+__global__ __launch_bounds__(kThreads) void k_uj_jobs(UjArgs A, const UJob* __restrict__ jobs,
+                                                     const u64* __restrict__ cnt, u64 cap) {
+  __shared__ u32 l_pre[kJobBlock + 1];
+  __shared__ u64 l_red[kThreads / 64];
+  const u64 n = *cnt < cap ? *cnt : cap;
+  const u64 G = gridDim.x;
+  constexpr u32 kPerT = kJobBlock / kThreads;
+  u64 base = 0;  // chunks of the blocks before
+  for (u64 j0 = 0; j0 < n; j0 += kJobBlock) {
+    const u32 m = (u32)(n - j0 < kJobBlock ? n - j0 : kJobBlock);
+    u32 v[kPerT];
+    u64 sum = 0;
+#pragma unroll
+    for (u32 u = 0; u < kPerT; u++) {  // thread t: jobs t * kPerT .. (contiguous)
+      const u32 i = threadIdx.x * kPerT + u;
+      u32 c = 0;
+      if (i < m) {
+        const UJob J = jobs[j0 + i];
+        // (a repeated doc's regrowth / trim: its runs stay; k_uj_docs' claims are final)
+        const bool skip = (J.what == UJ_REGROW || J.what == UJ_TRIM) && is_bad(A, J.e);
+        c = skip ? 0 : J.what == UJ_TRIM ? (u32)J.n : (u32)((J.n + kJobChunk - 1) / kJobChunk);
+      }
+      v[u] = c;
+      sum += c;
+    }
+    u64 tot;
+    u64 off = jyscan::block_excl<kThreads, u64>(sum, l_red, tot);
+#pragma unroll
+    for (u32 u = 0; u < kPerT; u++) {
+      const u32 i = threadIdx.x * kPerT + u;
+      if (i < m) l_pre[i] = (u32)off;
+      off += v[u];
+    }
+    if (threadIdx.x == 0) l_pre[m] = (u32)tot;
+    __syncthreads();
+    for (u64 g = (blockIdx.x + G - base % G) % G; g < tot; g += G) {  // (uniform over the workgroup)
+      u32 lo = 0, hi = m - 1;  // the last job i with l_pre[i] <= g
+      while (lo < hi) {
+        const u32 mid = (lo + hi + 1) >> 1;
+        if (l_pre[mid] <= g) lo = mid;
+        else hi = mid - 1;
+      }
+      const UJob J = jobs[j0 + lo];
+      const u64 q = g - l_pre[lo];
+      if (J.what == UJ_TRIM) uj_trim_column(A, J.e, J.lid, (u32)q);
+      else uj_job_chunk(A, J, q);
+    }
+    base += tot;
+    __syncthreads();  // (l_pre is rewritten by the next block)
+  }
+}
+
 // item kernels U2 / U3 / U5: one item per thread, a tile of kTile items per
 // workgroup, nothing staged -- full occupancy hides the searches' latency
 constexpr int kItemThreads = (int)kTile;
@@ -438,101 +762,16 @@ struct LongRun {
   u32 f0, f1, k, sp;  // whole tiles [f0, f1) of space sp lie in doc k
 };
 
-// ---- U1: per delta doc (ticketed doc tiles first, for the look-back) and
-// per delta item (validation, dense delta vv) ---------------------------------
-__global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_el, u64 t_cl, u64 t_vv) {
+// ---- U1a: per delta item: validation (strictly ascending dots per doc, col
+// < R, seq >= 1; vv entries ascending by column), the dense delta vv, and
+// the classification of the items of long documents (uj_item_long) --------
+__global__ __launch_bounds__(kThreads) void k_uj_items(UjArgs A, u64 t_el, u64 t_cl, u64 t_vv) {
   __shared__ Shared S;
-  // Every long run of the tile staged (16 KB).  (Round 3 tried 64 staged
-  // runs, 1 KB, owners filling the rest themselves: no speed-up.)
-#ifndef JY_UJ_LONG_CAP
-#define JY_UJ_LONG_CAP (4 * kDocTile)
-#endif
-  constexpr u32 kLongCap = JY_UJ_LONG_CAP;
-  __shared__ LongRun l_long[kLongCap];
-  __shared__ u32 l_nlong;
-  if (blockIdx.x < ndt) {  // doc tiles: ticketed (the look-back walks tickets)
-    if (threadIdx.x == 0) l_nlong = 0;
-    const u32 t = jyscan::ticket(A.tick + T_U1, &S.tk);
-    JY_CLK(c0);
-    const u64 k = (u64)t * kDocTile + threadIdx.x;
-    u64 asz = 0, csz = 0;
-    if (k < A.nd) {
-      const u32 s = A.slot[k];
-      const bool hole = s == JY_NO_SLOT;  // a routed run's unused record (k_route_csr.hip)
-      const UMeta m = hole ? UMeta{} : A.meta[s];
-      A.abase[k] = m.ebase;
-      A.cbs[k] = m.cbase;
-      asz = m.elen;
-      csz = m.clen;
-      // claim the slot for this converge (one delta per doc per call): a
-      // later copy marks both bad and does not count its size
-      const u64 mine = ((u64)A.epoch << 32) | (u32)k;
-      u64 old = hole ? 0 : A.dptr[s];
-      if (hole) mark_bad(A, k);
-      for (; !hole;) {
-        if ((u32)(old >> 32) == A.epoch) {
-          mark_bad(A, k);
-          mark_bad(A, (u32)old);
-          asz = csz = 0;
-          break;
-        }
-        const u64 seen = atomicCAS((unsigned long long*)(A.dptr + s), (unsigned long long)old,
-                                   (unsigned long long)mine);
-        if (seen == old) break;
-        old = seen;
-      }
-    }
-    u64 tot;
-    const u64 xa = jyscan::block_excl<kThreads, u64>(asz, S.red, tot);
-    const u64 pa = jyscan::lookback(A.st_ao, t, A.epoch, tot, &S.pre);
-    if (k < A.nd) A.ao[k] = pa + xa;
-    if (t == ndt - 1 && threadIdx.x == 0) {
-      A.ao[A.nd] = pa + tot;
-    }
-    const u64 xc = jyscan::block_excl<kThreads, u64>(csz, S.red, tot);
-    const u64 pc = jyscan::lookback(A.st_co, t, A.epoch, tot, &S.pre);
-    JY_CLK(c1);
-    if (k < A.nd) {
-      A.co[k] = pc + xc;
-      // per-item doc ids; a long segment names its doc once per whole tile
-      // in the tile map and writes ids only in its partial end tiles
-      auto ids = [&](u32* sid, u64* tm, u64 off, u64 sz) {
-        const u64 f0 = (off + kTile - 1) / kTile, f1 = (off + sz) / kTile;  // whole tiles [f0, f1)
-        if (sz <= kLongSeg || f0 >= f1) {
-          for (u64 j = 0; j < sz; j++) sid[off + j] = (u32)k;
-          return;
-        }
-        for (u64 j = off; j < f0 * kTile; j++) sid[j] = (u32)k;
-        for (u64 j = f1 * kTile; j < off + sz; j++) sid[j] = (u32)k;
-        const u32 q = atomicAdd(&l_nlong, 1u);  // the workgroup fills its tile-map run
-        if (q < kLongCap) {
-          l_long[q] = LongRun{(u32)f0, (u32)f1, (u32)k, (u32)(tm == A.tmA ? 0 : tm == A.tmB ? 1 : tm == A.tmC ? 2 : 3)};
-        } else {
-          for (u64 m = f0; m < f1; m++) tm[m] = ((u64)A.epoch << 32) | k;
-        }
-      };
-      ids(A.sidA, A.tmA, pa + xa, asz);
-      ids(A.sidC, A.tmC, pc + xc, csz);
-      const u64 b0 = A.deoff[k], d0 = A.dcoff[k];
-      ids(A.sidB, A.tmB, b0, A.deoff[k + 1] - b0);
-      ids(A.sidD, A.tmD, d0, A.dcoff[k + 1] - d0);
-    }
-    if (t == ndt - 1 && threadIdx.x == 0) {
-      A.co[A.nd] = pc + tot;
-    }
-    __syncthreads();
-    for (u32 q = 0; q < min(l_nlong, kLongCap); q++) {
-      const LongRun g = l_long[q];
-      u64* tm = g.sp == 0 ? A.tmA : g.sp == 1 ? A.tmB : g.sp == 2 ? A.tmC : A.tmD;
-      for (u64 m = g.f0 + threadIdx.x; m < g.f1; m += kThreads) tm[m] = ((u64)A.epoch << 32) | g.k;
-    }
-    JY_CLK(c2);
-    JY_PROBE(1, 0, t, c0, c1, c2);
-    return;
+  __shared__ u32 l_lid[kLdsDocs + 1];  // the tile's docs' long ids (~0u: regular)
+  if (A.lcol && blockIdx.x == 0 && threadIdx.x == 0) {
+    A.ctr[6] = 0;  // the previous converge's promotions are done (stream order)
   }
-  // delta items: strictly ascending dots per doc, col < R, seq >= 1; vv
-  // entries ascending by column
-  u64 tt = blockIdx.x - ndt;
+  u64 tt = blockIdx.x;
   const u64* offs;
   u64 n;
   int kind;
@@ -554,13 +793,19 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_e
   JY_CLK(c0);
   const u64 i0 = tt * kTile1, i1 = i0 + kTile1 < n ? i0 + kTile1 : n;
   const TileDocs T = tile_docs<kLdsDocs>(offs, A.nd, i0, i1, S.offs, S.sh);
+  if (A.lcol) {
+    if (T.lds)
+      for (u64 j = threadIdx.x; j < T.cnt; j += kThreads) l_lid[j] = long_id(A, T.k0 + j);
+    __syncthreads();
+  }
 #pragma unroll
   for (int u = 0; u < kPer; u++) {
     const u64 i = i0 + (u64)u * kThreads + threadIdx.x;
     if (i >= i1) continue;
     const u64 k = doc_of(T, offs, S.offs, i);
+    u64 x;
     if (kind == 2) {
-      const u64 x = A.dvv[i];
+      x = A.dvv[i];
       const u32 c = dcol(x);
       A.sidV[i] = (u32)k;
       if (c >= A.R || (i > A.dvoff[k] && dcol(A.dvv[i - 1]) >= c)) {
@@ -570,12 +815,132 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt, u64 t_e
       A.vvd[k * A.R + c] = dseq(x);
     } else {
       const u64* a = kind == 0 ? A.ddots : A.dcloud;
-      const u64 x = a[i];
-      if (dcol(x) >= A.R || dseq(x) < 1 || (i > offs[k] && a[i - 1] >= x)) mark_bad(A, k);
+      x = a[i];
+      if (dcol(x) >= A.R || dseq(x) < 1 || (i > offs[k] && a[i - 1] >= x)) {
+        mark_bad(A, k);
+        continue;
+      }
+    }
+    if (A.lcol) {
+      const u32 lid = T.lds ? l_lid[k - T.k0] : long_id(A, k);
+      if (lid != ~0u) uj_item_long(A, kind, k, i, lid, x);
     }
   }
   JY_CLK(c2);
   JY_PROBE(1, 1 + kind, (u32)tt, c0, c2, c2);
+}
+
+// ---- U1b: per delta doc (ticketed doc tiles, for the look-back): slot
+// claim, meta, the long documents' in-place / demote decision, scans of the
+// touched state sizes, the doc of every item (ids, or a tile map inside long
+// segments) -----------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt) {
+  __shared__ Shared S;
+  // Every long run of the tile staged (16 KB).  (Round 3 tried 64 staged
+  // runs, 1 KB, owners filling the rest themselves: no speed-up.)
+#ifndef JY_UJ_LONG_CAP
+#define JY_UJ_LONG_CAP (4 * kDocTile)
+#endif
+  constexpr u32 kLongCap = JY_UJ_LONG_CAP;
+  __shared__ LongRun l_long[kLongCap];
+  __shared__ u32 l_nlong;
+  __shared__ u32 l_lq[kThreads], l_nlq;  // the tile's long documents (thread indices)
+  __shared__ u64 l_sz[kThreads][2];
+  if (threadIdx.x == 0) l_nlong = l_nlq = 0;
+  const u32 t = jyscan::ticket(A.tick + T_U1, &S.tk);
+  if (t >= ndt) return;
+  JY_CLK(c0);
+  const u64 k = (u64)t * kDocTile + threadIdx.x;
+  u64 asz = 0, csz = 0;
+  bool lg = false;  // a long document (decided by a wave below)
+  if (k < A.nd) {
+    const u32 s = A.slot[k];
+    const bool hole = s == JY_NO_SLOT;  // a routed run's unused record (k_route_csr.hip)
+    const UMeta m = hole ? UMeta{} : A.meta[s];
+    A.abase[k] = m.ebase;
+    A.cbs[k] = m.cbase;
+    asz = m.elen;
+    csz = m.clen;
+    // claim the slot for this converge (one delta per doc per call): a
+    // later copy marks both bad and does not count its size
+    const u64 mine = ((u64)A.epoch << 32) | (u32)k;
+    u64 old = hole ? 0 : A.dptr[s];
+    if (hole) mark_bad(A, k);
+    for (; !hole;) {
+      if ((u32)(old >> 32) == A.epoch) {
+        mark_bad(A, k);
+        mark_bad(A, (u32)old);
+        break;
+      }
+      const u64 seen = atomicCAS((unsigned long long*)(A.dptr + s), (unsigned long long)old,
+                                 (unsigned long long)mine);
+      if (seen == old) break;
+      old = seen;
+    }
+    // a bad doc (malformed: U1a; repeated) is skipped: nothing of it is touched
+    if (is_bad(A, k)) asz = csz = 0;
+    else if (m.ecap == kLongMark && A.lcol) l_lq[atomicAdd(&l_nlq, 1u)] = threadIdx.x, lg = true;
+  }
+  if (A.lcol) {  // the long documents, a wave each
+    __syncthreads();
+    for (u32 q = threadIdx.x >> 6; q < l_nlq; q += kThreads / 64) {
+      const u32 i = l_lq[q];
+      u64 a = 0, c = 0;
+      uj_docs_long(A, (u64)t * kDocTile + i, a, c);
+      if ((threadIdx.x & 63) == 0) l_sz[i][0] = a, l_sz[i][1] = c;
+    }
+    __syncthreads();
+    if (lg) {
+      asz = l_sz[threadIdx.x][0];
+      csz = l_sz[threadIdx.x][1];
+    }
+  }
+  u64 tot;
+  const u64 xa = jyscan::block_excl<kThreads, u64>(asz, S.red, tot);
+  const u64 pa = jyscan::lookback(A.st_ao, t, A.epoch, tot, &S.pre);
+  if (k < A.nd) A.ao[k] = pa + xa;
+  if (t == ndt - 1 && threadIdx.x == 0) {
+    A.ao[A.nd] = pa + tot;
+  }
+  const u64 xc = jyscan::block_excl<kThreads, u64>(csz, S.red, tot);
+  const u64 pc = jyscan::lookback(A.st_co, t, A.epoch, tot, &S.pre);
+  JY_CLK(c1);
+  if (k < A.nd) {
+    A.co[k] = pc + xc;
+    // per-item doc ids; a long segment names its doc once per whole tile
+    // in the tile map and writes ids only in its partial end tiles
+    auto ids = [&](u32* sid, u64* tm, u64 off, u64 sz) {
+      const u64 f0 = (off + kTile - 1) / kTile, f1 = (off + sz) / kTile;  // whole tiles [f0, f1)
+      if (sz <= kLongSeg || f0 >= f1) {
+        for (u64 j = 0; j < sz; j++) sid[off + j] = (u32)k;
+        return;
+      }
+      for (u64 j = off; j < f0 * kTile; j++) sid[j] = (u32)k;
+      for (u64 j = f1 * kTile; j < off + sz; j++) sid[j] = (u32)k;
+      const u32 q = atomicAdd(&l_nlong, 1u);  // the workgroup fills its tile-map run
+      if (q < kLongCap) {
+        l_long[q] = LongRun{(u32)f0, (u32)f1, (u32)k, (u32)(tm == A.tmA ? 0 : tm == A.tmB ? 1 : tm == A.tmC ? 2 : 3)};
+      } else {
+        for (u64 m = f0; m < f1; m++) tm[m] = ((u64)A.epoch << 32) | k;
+      }
+    };
+    ids(A.sidA, A.tmA, pa + xa, asz);
+    ids(A.sidC, A.tmC, pc + xc, csz);
+    const u64 b0 = A.deoff[k], d0 = A.dcoff[k];
+    ids(A.sidB, A.tmB, b0, A.deoff[k + 1] - b0);
+    ids(A.sidD, A.tmD, d0, A.dcoff[k + 1] - d0);
+  }
+  if (t == ndt - 1 && threadIdx.x == 0) {
+    A.co[A.nd] = pc + tot;
+  }
+  __syncthreads();
+  for (u32 q = 0; q < min(l_nlong, kLongCap); q++) {
+    const LongRun g = l_long[q];
+    u64* tm = g.sp == 0 ? A.tmA : g.sp == 1 ? A.tmB : g.sp == 2 ? A.tmC : A.tmD;
+    for (u64 m = g.f0 + threadIdx.x; m < g.f1; m += kThreads) tm[m] = ((u64)A.epoch << 32) | g.k;
+  }
+  JY_CLK(c2);
+  JY_PROBE(1, 0, t, c0, c1, c2);
 }
 
 // ---- U2: keep flags + cross ranks ----------------------------------------------
@@ -687,6 +1052,39 @@ __device__ __forceinline__ void uj_flags_long(const UjArgs& A, int kind, u64 k, 
   }
 }
 
+// U2 for an item of a delta doc converging IN PLACE (kind 1: a delta
+// element, 2: a delta cloud dot; k_uj_docs planned the doc's columns): a
+// fresh element goes to its column run's tail; a fresh cloud dot too, unless
+// the column's cloud was empty and the dot extends the vv's run (folded: the
+// run's last dot tells U5 how many folded -- the ones that do not fold were
+// written at crun + rank, so U5 moves the run's start past the folded
+// prefix).  Dots that are not fresh change nothing (k_uj_items checked).
+__device__ __forceinline__ void uj_fast_item(const UjArgs& A, int kind, u64 k, u64 i) {
+  const u32 lid = (u32)A.abase[k];
+  if (kind == 1) {
+    const u64 x = A.ddots[i];
+    LPlan& P = A.lplan[(u64)lid * A.R + dcol(x)];
+    const u64 fs = P.efs;
+    if (!tagged(A, fs) || i < (u32)fs) return;
+    store_rec(A.lpe + P.eapp + (i - (u32)fs), x, A.delems[i]);
+    return;
+  }
+  const u64 x = A.dcloud[i];
+  const u32 c = dcol(x);
+  LPlan& P = A.lplan[(u64)lid * A.R + c];
+  const u64 fs = P.cfs;
+  if (!tagged(A, fs) || i < (u32)fs) return;
+  const u64 r = i - (u32)fs;
+  if (P.cz) {
+    const u64 v = A.vv[(u64)A.slot[k] * A.R + c];
+    if (dseq(x) == v + 1 + r) {
+      if (i + 1 == (u32)P.cce || dseq(A.dcloud[i + 1]) != v + 2 + r) P.nfold = tag(A, r + 1);
+      return;
+    }
+  }
+  A.lpc[P.capp + r] = x;
+}
+
 __device__ __forceinline__ void uj_flags_tile(const UjArgs& A, const u64 t, u64* red) {
   const u64 ta = A.ao[A.nd];
   const u64 tA = cdiv(ta), tB = cdiv(A.nb);
@@ -709,7 +1107,12 @@ __device__ __forceinline__ void uj_flags_tile(const UjArgs& A, const u64 t, u64*
   const u64 tmv = tm[lt];
   if ((u32)(tmv >> 32) == A.epoch) {
     const u64 k = (u32)tmv;
-    if (!is_bad(A, k)) uj_flags_long(A, kind, k, i, n, gbase, f);
+    if (is_bad(A, k)) {
+    } else if (is_fast(A, k)) {
+      if (kind && i < n) uj_fast_item(A, kind, k, i);
+    } else {
+      uj_flags_long(A, kind, k, i, n, gbase, f);
+    }
   } else if (i < n) {
     // small documents: every lookup of the item issued at once (the doc's
     // words, then the item's dot, then all its windows): ~4 round trips
@@ -717,7 +1120,9 @@ __device__ __forceinline__ void uj_flags_tile(const UjArgs& A, const u64 t, u64*
     const bool bad = is_bad(A, k);
     const u64 clo = A.cbs[k], chi = clo + (A.co[k + 1] - A.co[k]);
     const u32 sl = A.slot[k];
-    if (!bad) {
+    if (!bad && is_fast(A, k)) {
+      if (kind) uj_fast_item(A, kind, k, i);  // (a doc in place has no state items here)
+    } else if (!bad) {
       u32 xr;
       if (kind == 0) {
         const u64 lo = A.deoff[k], hi = A.deoff[k + 1], blo = A.dcoff[k], bhi = A.dcoff[k + 1];
@@ -780,6 +1185,7 @@ __device__ __forceinline__ void uj_flags_tile(const UjArgs& A, const u64 t, u64*
 // and every surplus workgroup paid a dispatch and a dependent load to exit.
 __global__ __launch_bounds__(kItemThreads) void k_uj_flags(UjArgs A) {
   __shared__ u64 red[kItemThreads / 64];
+  if (A.lcol && blockIdx.x == 0 && threadIdx.x == 0) A.ctr[5] = 0;  // k_uj_jobs (demotions, regrowths) is done
   const u64 T = cdiv(A.ao[A.nd]) + cdiv(A.nb) + cdiv(A.cb);
   for (u64 t = blockIdx.x; t < T; t += gridDim.x) uj_flags_tile(A, t, red);
 }
@@ -865,11 +1271,11 @@ __device__ __forceinline__ void uj_compact_tile(const UjArgs& A, const u64 t, u6
   const u64 tmv = sa ? A.tmC[lt] : A.tmD[lt];
   if ((u32)(tmv >> 32) == A.epoch) {  // a tile inside one long document
     const u64 k = (u32)tmv;
-    if (!is_bad(A, k)) uj_compact_long(A, sa, k, i, n, f);
+    if (!is_bad(A, k) && !is_fast(A, k)) uj_compact_long(A, sa, k, i, n, f);
   } else if (i < n) {
     // small documents: the item's independent lookups issued together
     const u64 k = (u32)(tmv >> 32) == A.epoch ? (u32)tmv : (sa ? A.sidC[i] : A.sidD[i]);
-    const bool bad = is_bad(A, k);
+    const bool bad = is_bad(A, k) || is_fast(A, k);
     const u64 alo = A.cbs[k], co0 = A.co[k], ahi = alo + (A.co[k + 1] - co0);
     const u64 blo = A.dcoff[k], bhi = A.dcoff[k + 1];
     const u32 sl = A.slot[k];
@@ -991,6 +1397,11 @@ __global__ __launch_bounds__(kThreads) void k_uj_sizes(UjArgs A, u64 ndt) {
     A.pin[1] = cbb + tcl;
     A.pin_t[0] = A.ao[A.nd];
     A.pin_t[1] = A.co[A.nd];
+    if (A.lcol) {
+      A.pin_l[0] = A.ctr[2];
+      A.pin_l[1] = A.ctr[3];
+      A.pin_l[2] = A.ctr[4];
+    }
   }
 }
 
@@ -1052,6 +1463,49 @@ __device__ __forceinline__ ScOut scatter_prep(const UjArgs& A, int kind, u64 lt,
   return o;
 }
 
+// U5 for a delta doc converged in place: the column runs take their new
+// lengths (and the runs that grew, their new places), a cloud run that was
+// empty starts past its folded prefix, the vv takes the folds, the meta its
+// new totals
+__device__ void uj_commit_long(const UjArgs& A, u64 i) {
+  const u32 R = A.R, s = A.slot[i], lid = (u32)A.abase[i];
+  const u64 b = (u64)lid * R;
+  u64 dE = 0, dC = 0, nfs = 0, app = 0;
+  for (u32 c = 0; c < R; c++) {
+    const LPlan& P = A.lplan[b + c];
+    const u64 efs = P.efs, ece = P.ece, cfs = P.cfs, cce = P.cce, nfw = P.nfold;
+    const u64 ne = tagged(A, efs) ? (u32)ece - (u32)efs : 0, nc = tagged(A, cfs) ? (u32)cce - (u32)cfs : 0;
+    const u64 tcw = P.tcut, cut = tagged(A, tcw) ? (u32)tcw : 0;
+    if (!ne && !nc && !cut) continue;
+    const u64 nf = tagged(A, nfw) ? (u32)nfw : 0;
+    const LCol L = A.lcol[b + c];
+    // (a trimmed run never moved: erun is its old start, now `cut` further up)
+    LCol N{P.erun + cut, (u32)(L.elen - cut + ne), (u32)(P.ecap - cut), P.crun, (u32)(L.clen + nc), P.ccap};
+    if (P.cz) {
+      N.clen = (u32)(nc - nf);
+      if (nf < nc) {
+        N.cbase = P.crun + nf;
+        N.ccap = (u32)(P.ccap - nf);
+      }
+    }
+    A.lcol[b + c] = N;
+    if (nf) A.vv[(u64)s * R + c] += nf;
+    dE += ne - cut;  // (mod 2^64: a trim may remove more than the delta adds)
+    app += ne;
+    dC += nc - nf;
+    nfs += nf;
+  }
+  const UMeta m = A.meta[s];
+  A.meta[s] = UMeta{lid, (u32)(m.elen + dE), kLongMark, 0, (u32)(m.clen + dC), kLongMark};
+  unsigned long long* st = (unsigned long long*)A.stats;
+  atomicAdd(st + 8, 1ull);
+  atomicAdd(st + 9, (unsigned long long)m.elen);
+  atomicAdd(st + 10, (unsigned long long)m.clen);
+  atomicAdd(st + 11, (unsigned long long)app);
+  atomicAdd(st + 12, (unsigned long long)dC);
+  atomicAdd(st + 13, (unsigned long long)nfs);
+}
+
 __device__ __forceinline__ void scatter_small(const UjArgs& A, int kind, u64 i) {
   const u64 eb0 = A.base[0], cb0 = A.base[1];
   const u64 nv = A.nvv;
@@ -1062,8 +1516,9 @@ __device__ __forceinline__ void scatter_small(const UjArgs& A, int kind, u64 i) 
     if (c >= A.R) return;  // never written (the doc is bad)
     const u64 k = A.sidV[i];
     // the state rows already hold U3's folds; elsewhere max(state, delta) is
-    // the state (one entry per (doc, column) unless the doc is bad)
-    if (!is_bad(A, k)) {
+    // the state (one entry per (doc, column) unless the doc is bad; a doc in
+    // place has no entry above the state's)
+    if (!is_bad(A, k) && !is_fast(A, k)) {
       u64* r = A.vv + (u64)A.slot[k] * A.R + c;
       const u64 q = dseq(x);
       if (q > *r) *r = q;
@@ -1073,8 +1528,13 @@ __device__ __forceinline__ void scatter_small(const UjArgs& A, int kind, u64 i) 
   }
   // kind 5: metas
   if (i >= A.nd || is_bad(A, i)) return;
+  if (is_fast(A, i)) {
+    uj_commit_long(A, i);
+    return;
+  }
   const u32 ne = (u32)(A.neo[i + 1] - A.neo[i]), nc = (u32)(A.nco[i + 1] - A.nco[i]);
   A.meta[A.slot[i]] = UMeta{eb0 + A.neo[i], ne, ne, cb0 + A.nco[i], nc, nc};
+  if (A.long_min && ne >= A.long_min) A.plist[atomicAdd((unsigned long long*)(A.ctr + 6), 1ull)] = (u32)i;
 }
 
 __device__ __forceinline__ void uj_scatter_tile(const UjArgs& A, const u64 t) {
@@ -1118,6 +1578,65 @@ __global__ __launch_bounds__(kScatterThreads) void k_uj_scatter(UjArgs A) {
   for (u64 t = blockIdx.x; t < T; t += gridDim.x) uj_scatter_tile(A, t);
 }
 
+// ---- P: promotion of the merged documents U5 listed (>= long_min elements):
+// one wave per document finds its column boundaries in the fresh regular run
+// (lane c: the first dot of column c), takes a long id and room in the long
+// pools (2n + 16 per column run), writes the column table and the copy jobs
+// (k_uj_jobs runs them next) and marks the meta long.  Optional: without
+// room the document simply stays regular.
+__global__ __launch_bounds__(kThreads) void k_uj_promote(UjArgs A) {
+  const u64 n = A.ctr[6];
+  const u32 lane = threadIdx.x & 63, R = A.R;
+  const u64 W = (u64)gridDim.x * (kThreads / 64);
+  UJob* jobs = A.jobs + 2 * A.jcap;  // the promotion region: job j <-> plist entry j
+  for (u64 j = (u64)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); j < n; j += W) {
+    const u64 i = A.plist[j];
+    const u32 s = A.slot[i];
+    const UMeta m = A.meta[s];
+    const bool act = lane < R;
+    u64 e0 = m.elen, c0 = m.clen;
+    if (act) {  // lane c: the first element / cloud dot of column c (the two searches in lockstep)
+      const u64 x = mkdot(lane, 0);
+      u64 elo = m.ebase, ehi = m.ebase + m.elen, clo = m.cbase, chi = m.cbase + m.clen;
+      while (elo < ehi || clo < chi) {
+        const u64 em = (elo + ehi) >> 1, cm = (clo + chi) >> 1;
+        const u64 ev = elo < ehi ? A.rec[em].dot : 0, cv = clo < chi ? A.cloud[cm] : 0;
+        if (elo < ehi) (ev < x ? elo = em + 1 : ehi = em);
+        if (clo < chi) (cv < x ? clo = cm + 1 : chi = cm);
+      }
+      e0 = elo - m.ebase;
+      c0 = clo - m.cbase;
+    }
+    u64 e1 = __shfl(e0, (int)((lane + 1) & 63)), c1 = __shfl(c0, (int)((lane + 1) & 63));
+    if (lane + 1 >= R) e1 = m.elen, c1 = m.clen;
+    const u64 ne = act ? e1 - e0 : 0, nc = act ? c1 - c0 : 0;
+    const u64 ecap = act ? roomy(ne) : 0, ccap = act ? roomy(nc) : 0;
+    const u64 oe = jyscan::wave_incl<u64>(ecap) - ecap, oc = jyscan::wave_incl<u64>(ccap) - ccap;
+    const u64 TE = __shfl(oe + ecap, 63), TC = __shfl(oc + ccap, 63);
+    u64 lid = 0, eb = 0, cb = 0, ok = 0;
+    if (lane == 0) {  // (a refused promotion wastes its reservations until the next compaction)
+      lid = atomicAdd((unsigned long long*)(A.ctr + 4), 1ull);
+      eb = atomicAdd((unsigned long long*)(A.ctr + 2), (unsigned long long)TE);
+      cb = atomicAdd((unsigned long long*)(A.ctr + 3), (unsigned long long)TC);
+      ok = j < A.jcap && lid < A.lcap && eb + TE <= A.lpe_cap && cb + TC <= A.lpc_cap;
+    }
+    ok = __shfl(ok, 0);
+    if (!ok) {
+      if (lane == 0 && j < A.jcap) jobs[j] = UJob{0, 0, 0, UJ_PROMOTE, 0};
+      continue;
+    }
+    lid = __shfl(lid, 0);
+    eb = __shfl(eb, 0);
+    cb = __shfl(cb, 0);
+    if (act) A.lcol[lid * R + lane] = LCol{eb + oe, (u32)ne, (u32)ecap, cb + oc, (u32)nc, (u32)ccap};
+    if (lane == 0) {
+      jobs[j] = UJob{m.ebase, m.cbase, (u64)m.elen + m.clen, UJ_PROMOTE, (u32)lid};
+      A.meta[s] = UMeta{lid, m.elen, kLongMark, 0, m.clen, kLongMark};
+      atomicAdd((unsigned long long*)(A.stats + 14), 1ull);
+    }
+  }
+}
+
 // ---- compaction: every document rewritten back to back into fresh pools ------------
 __global__ __launch_bounds__(kThreads) void k_uj_cmp_size(const UMeta* __restrict__ meta, u64 nk,
                                                           u64* __restrict__ se, u64* __restrict__ sc) {
@@ -1127,10 +1646,12 @@ __global__ __launch_bounds__(kThreads) void k_uj_cmp_size(const UMeta* __restric
   sc[s] = s == nk ? 0 : meta[s].clen;
 }
 constexpr u32 kTileOut = 2048;
+// (long documents are laid out regular again: compaction empties the long pools)
 template <bool kElems, typename T>
 __global__ __launch_bounds__(kThreads) void k_uj_cmp_copy(const UMeta* __restrict__ meta, u64 nk,
                                                           const u64* __restrict__ off, const T* __restrict__ src,
-                                                          T* __restrict__ dst) {
+                                                          T* __restrict__ dst, const LCol* __restrict__ lcol,
+                                                          const T* __restrict__ lsrc, u32 R) {
   __shared__ Shared S;
   const u64 total = off[nk];
   const u64 t0 = (u64)blockIdx.x * kTileOut;  // the grid is the host's bound
@@ -1140,7 +1661,8 @@ __global__ __launch_bounds__(kThreads) void k_uj_cmp_copy(const UMeta* __restric
   for (u64 t = t0 + threadIdx.x; t < t1; t += kThreads) {
     const u64 k = doc_of(D, off, S.offs, t);
     const UMeta m = meta[k];
-    dst[t] = src[(kElems ? m.ebase : m.cbase) + (t - off[k])];
+    if (m.ecap == kLongMark) dst[t] = lsrc[uj_long_at<kElems>(lcol + m.ebase * R, R, t - off[k])];
+    else dst[t] = src[(kElems ? m.ebase : m.cbase) + (t - off[k])];
   }
 }
 __global__ __launch_bounds__(kThreads) void k_uj_cmp_meta(UMeta* __restrict__ meta, u64 nk, const u64* __restrict__ eo,
@@ -1174,7 +1696,10 @@ __global__ __launch_bounds__(kThreads) void k_uj_gather_items(const UMeta* __res
                                                               const u64* __restrict__ cloud,
                                                               const u32* __restrict__ slots, u64 n,
                                                               const u64* __restrict__ ooff, u64 total,
-                                                              u64* __restrict__ oa, u64* __restrict__ ob) {
+                                                              u64* __restrict__ oa, u64* __restrict__ ob,
+                                                              const LCol* __restrict__ lcol,
+                                                              const URec* __restrict__ lpe,
+                                                              const u64* __restrict__ lpc, u32 R) {
   __shared__ u64 sh[2];
   const u64 t0 = (u64)blockIdx.x * kThreads;
   if (t0 >= total) return;
@@ -1194,12 +1719,13 @@ __global__ __launch_bounds__(kThreads) void k_uj_gather_items(const UMeta* __res
   }
   const UMeta m = meta[slots[lo]];
   const u64 j = t - ooff[lo];
+  const bool lg = m.ecap == kLongMark;
   if (kEl) {
-    const URec r = rec[m.ebase + j];
+    const URec r = lg ? lpe[uj_long_at<true>(lcol + m.ebase * R, R, j)] : rec[m.ebase + j];
     oa[t] = r.dot;
     ob[t] = r.elem;
   } else {
-    oa[t] = cloud[m.cbase + j];
+    oa[t] = lg ? lpc[uj_long_at<false>(lcol + m.ebase * R, R, j)] : cloud[m.cbase + j];
   }
 }
 
@@ -1222,13 +1748,17 @@ u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kThreads - 1) / kThrea
   } while (0)
 
 void ujson_absorb(UjsonState& u);
+int32_t ujson_long_grow(jy_engine* eng, UjsonState& u);
 
 // the compacted pools' bump pointers: on the device, and into the host's
 // mapped ring slot
 __global__ void k_uj_cmp_ctr(const u64* __restrict__ te, const u64* __restrict__ tc, u64* __restrict__ ctr,
-                             u64* __restrict__ pin) {
+                             u64* __restrict__ pin, u64* __restrict__ pin_l) {
   ctr[0] = pin[0] = *te;
   ctr[1] = pin[1] = *tc;
+  // every long document is regular again: the long pools are empty
+  ctr[2] = ctr[3] = ctr[4] = 0;
+  pin_l[0] = pin_l[1] = pin_l[2] = 0;
 }
 
 // rewrite every document back to back into the spare pools, sized for the
@@ -1283,19 +1813,22 @@ int32_t ujson_compact(jy_engine* eng, UjsonState& u, u64 room_e, u64 room_c) {
   }
   if (be)
     hipLaunchKernelGGL((k_uj_cmp_copy<true, URec>), dim3((u32)((be + kTileOut - 1) / kTileOut)), dim3(kThreads), 0,
-                       eng->stream, u.meta, nk, eo, u.epool, u.spare_e);
+                       eng->stream, u.meta, nk, eo, u.epool, u.spare_e, u.lcol, u.lpe, u.R);
   if (bc)
     hipLaunchKernelGGL((k_uj_cmp_copy<false, u64>), dim3((u32)((bc + kTileOut - 1) / kTileOut)), dim3(kThreads), 0,
-                       eng->stream, u.meta, nk, co, u.cpool, u.spare_c);
+                       eng->stream, u.meta, nk, co, u.cpool, u.spare_c, u.lcol, u.lpc, u.R);
   JY_HIP(eng, hipGetLastError());
   if (nk) LAUNCH(k_uj_cmp_meta, nk, u.meta, nk, eo, co);
   const int r = (int)(u.seq % UjsonState::kRing);
-  hipLaunchKernelGGL(k_uj_cmp_ctr, dim3(1), dim3(1), 0, eng->stream, eo + nk, co + nk, u.ctr, u.pin_dev + 8 + 2 * r);
+  hipLaunchKernelGGL(k_uj_cmp_ctr, dim3(1), dim3(1), 0, eng->stream, eo + nk, co + nk, u.ctr, u.pin_dev + 8 + 2 * r,
+                     u.pin_dev + 24 + 3 * r);
   JY_HIP(eng, hipGetLastError());
   std::swap(u.epool, u.spare_e);
   std::swap(u.epcap, u.spare_ecap);
   std::swap(u.cpool, u.spare_c);
   std::swap(u.cpcap, u.spare_ccap);
+  // the long pools are empty now (k_uj_cmp_ctr)
+  u.long_used_e = u.long_used_c = u.long_ids = 0;
   // every earlier converge is compacted in; this one's sizes are bounded by be / bc
   u.used_e = u.used_c = 0;
   u.done = u.seq;
@@ -1320,19 +1853,29 @@ void ujson_absorb(UjsonState& u) {
       u.used_c = u.pin[9 + 2 * r];
       u.pred_ta = u.pin[2 * r];
       u.pred_tc = u.pin[1 + 2 * r];
+      u.long_used_e = u.pin[24 + 3 * r];
+      u.long_used_c = u.pin[25 + 3 * r];
+      u.long_ids = u.pin[26 + 3 * r];
       u.has_pred = true;
       u.done = j;
       return;
     }
   }
 }
-int32_t ujson_plan(jy_engine* eng, UjsonState& u, u64 nel, u64 ncloud) {
+// (we / wc: the converge's worst case -- with long documents it includes a
+// demotion of every live entry; room_e / room_c: one converge's worst case
+// without it, which sizes a compaction's headroom)
+int32_t ujson_plan(jy_engine* eng, UjsonState& u, u64 we, u64 wc, u64 room_e, u64 room_c) {
   ujson_absorb(u);
   if (u.seq - u.done == UjsonState::kRing) {  // the ring slot is still in use: wait for its converge
     JY_HIP(eng, hipEventSynchronize(u.ready[u.done % UjsonState::kRing]));
     ujson_absorb(u);
   }
-  const u64 we = u.live_e + nel, wc = u.live_c + ncloud;
+  // the long pools or ids past half used (by the newest readback, which lags
+  // the converges in flight): they double, contents kept.  Until then the
+  // device refuses what does not fit -- a promotion is skipped, a document
+  // whose run cannot grow goes the regular path -- so nothing overflows.
+  if (u.lcol) JY_TRY(ujson_long_grow(eng, u));
   auto fits = [&]() {
     u64 be = u.used_e + we, bc = u.used_c + wc;
     for (u64 j = u.done; j < u.seq; j++) {
@@ -1346,7 +1889,7 @@ int32_t ujson_plan(jy_engine* eng, UjsonState& u, u64 nel, u64 ncloud) {
       JY_HIP(eng, hipEventSynchronize(u.ready[(u.seq - 1) % UjsonState::kRing]));
       ujson_absorb(u);
     }
-    if (!fits()) JY_TRY(ujson_compact(eng, u, we, wc));
+    if (!fits()) JY_TRY(ujson_compact(eng, u, room_e, room_c));
   }
   return JY_OK;
 }
@@ -1360,6 +1903,52 @@ int32_t grow_zero(jy_engine* eng, void** p, u64* cap_bytes, u64 need_bytes) {
   return JY_OK;
 }
 
+// the long layout's tables and pools, at first use: ids 4096, pools 1M
+// entries each; a compaction doubles what was more than half used
+int32_t ujson_long_init(jy_engine* eng, UjsonState& u) {
+  u.lcap = 4096;
+  u.lpe_cap = u.lpc_cap = 1ull << 20;
+  JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.lcol), u.lcap * u.R * sizeof(LCol), "ujson long columns"));
+  JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.lplan), u.lcap * u.R * sizeof(LPlan), "ujson long plans"));
+  JY_HIP(eng, hipMemsetAsync(u.lplan, 0, u.lcap * u.R * sizeof(LPlan), eng->stream));
+  JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.lpe), u.lpe_cap * sizeof(URec), "ujson long element pool"));
+  JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.lpc), u.lpc_cap * 8, "ujson long cloud pool"));
+  return JY_OK;
+}
+
+// The long pools hold every long document's runs with room (2n + 16 a run)
+// plus the runs regrowth left behind, so they are sized from the store's
+// live-entry bound (4x: HBM is plentiful, a refused regrowth demotes a hot
+// document) and from the newest readback (more than half used: double).
+// Growth keeps the contents (a stream-ordered copy).
+int32_t ujson_long_grow(jy_engine* eng, UjsonState& u) {
+  const u64 te = std::max<u64>(4 * u.live_e, 2 * u.long_used_e), tc = std::max<u64>(4 * u.live_c, 2 * u.long_used_c);
+  if (te > u.lpe_cap) {
+    const u64 nc = std::max<u64>(te, 2 * u.lpe_cap);
+    void* q = u.lpe;
+    JY_TRY(jy_realloc(eng, &q, u.lpe_cap * sizeof(URec), nc * sizeof(URec), false));
+    u.lpe = static_cast<URec*>(q);
+    u.lpe_cap = nc;
+  }
+  if (tc > u.lpc_cap) {
+    const u64 nc = std::max<u64>(tc, 2 * u.lpc_cap);
+    void* q = u.lpc;
+    JY_TRY(jy_realloc(eng, &q, u.lpc_cap * 8, nc * 8, false));
+    u.lpc = static_cast<u64*>(q);
+    u.lpc_cap = nc;
+  }
+  if (2 * u.long_ids > u.lcap) {
+    void* q = u.lcol;
+    JY_TRY(jy_realloc(eng, &q, u.lcap * u.R * sizeof(LCol), 2 * u.lcap * u.R * sizeof(LCol), false));
+    u.lcol = static_cast<LCol*>(q);
+    q = u.lplan;
+    JY_TRY(jy_realloc(eng, &q, u.lcap * u.R * sizeof(LPlan), 2 * u.lcap * u.R * sizeof(LPlan), true));
+    u.lplan = static_cast<LPlan*>(q);
+    u.lcap *= 2;
+  }
+  return JY_OK;
+}
+
 }  // namespace
 
 int32_t ujson_grow_store(jy_engine* eng, UjsonState& u, u64 need, u64 init_cap) {
@@ -1367,14 +1956,14 @@ int32_t ujson_grow_store(jy_engine* eng, UjsonState& u, u64 need, u64 init_cap) 
   if (!u.ctr) {
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.ctr), 64, "ujson counters"));
     JY_HIP(eng, hipMemsetAsync(u.ctr, 0, 64, eng->stream));
-    JY_HIP(eng, hipHostMalloc(reinterpret_cast<void**>(&u.pin), 128, hipHostMallocMapped));
-    std::memset(u.pin, 0, 128);
+    JY_HIP(eng, hipHostMalloc(reinterpret_cast<void**>(&u.pin), 512, hipHostMallocMapped));
+    std::memset(u.pin, 0, 512);
     JY_HIP(eng, hipHostGetDevicePointer(reinterpret_cast<void**>(&u.pin_dev), u.pin, 0));
     for (hipEvent_t& e : u.ready) JY_HIP(eng, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.tick), 64, "ujson tickets"));
     JY_HIP(eng, hipMemsetAsync(u.tick, 0, 64, eng->stream));
-    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.stats), 64, "ujson stats"));
-    JY_HIP(eng, hipMemsetAsync(u.stats, 0, 64, eng->stream));
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.stats), 128, "ujson stats"));
+    JY_HIP(eng, hipMemsetAsync(u.stats, 0, 128, eng->stream));
     u.epcap = u.cpcap = std::max<u64>(init_cap, 1024);
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.epool), u.epcap * sizeof(URec), "ujson element pool"));
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.cpool), u.cpcap * 8, "ujson cloud pool"));
@@ -1395,7 +1984,18 @@ int32_t ujson_grow_store(jy_engine* eng, UjsonState& u, u64 need, u64 init_cap) 
   return JY_OK;
 }
 
+// default promotion threshold of the state store (JY_UJ_LONG_MIN overrides;
+// 0 disables the in-place layout); jy_ujson_set_inplace changes it
+u32 ujson_default_long_min() {
+  if (const char* e = getenv("JY_UJ_LONG_MIN")) return (u32)strtoul(e, nullptr, 10);
+  return 128;
+}
+
 int32_t jy_ujson_grow(jy_engine* eng, u64 need) {
+  if (!eng->ujson.allow_long) {  // (jy_ujson_set_inplace before the first UJSON key keeps its choice)
+    eng->ujson.allow_long = true;
+    eng->ujson.long_min = ujson_default_long_min();
+  }
   JY_TRY(ujson_grow_store(eng, eng->ujson, need, eng->cfg.entry_capacity[JY_UJSON]));
   if (eng->ujson_d.ctr) JY_TRY(ujson_grow_store(eng, eng->ujson_d, eng->ujson.kcap, 0));
   return JY_OK;
@@ -1420,13 +2020,47 @@ int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* sl
   if (nd == 0 || nk == 0) return JY_OK;
   if (nd >= 0xFFFFFFFFull) return eng->fail(JY_ERANGE, "ujson converge: more than 2^32 - 1 documents in one call");
   const u32 R = u.R;
+  // the in-place layout of long documents: the state store, R <= 64 (a lane per column)
+  if (!u.lcol && u.allow_long && u.long_min && !keep_all && R <= (u32)kMaxR) JY_TRY(ujson_long_init(eng, u));
+  const bool lng = u.lcol != nullptr;
   const u64 live_e = u.live_e, live_c = u.live_c;  // bounds of the touched state, before this converge
   const double th0 = jy_tracing() ? jy_now_us() : 0;
-  JY_TRY(ujson_plan(eng, u, nel, ncloud));
+  // worst case: every live entry touched (and, with long documents, demoted first)
+  JY_TRY(ujson_plan(eng, u, (lng ? 2 : 1) * u.live_e + nel, (lng ? 2 : 1) * u.live_c + ncloud, u.live_e + nel,
+                    u.live_c + ncloud));
   const double th1 = jy_tracing() ? jy_now_us() : 0;
   const u64 le = std::min(u.live_e, live_e), lc = std::min(u.live_c, live_c);  // (a compaction makes them exact)
   if (le + nel + ncloud + 2 >= (1ull << 32) || lc + ncloud + 2 >= (1ull << 32))
     return eng->fail(JY_ERANGE, "ujson converge: more than 2^32 touched items");
+
+  // persistent per-delta-doc state: bad / in-place / not-append-shaped
+  // marks, the dense delta vv (zero), the promotion list, the copy jobs
+  if (nd > u.dcap) {
+    u64 bcap = u.dcap * 4, vcap = u.dcap * R * 8, fcap = u.dcap * 4, ncap = u.dcap * 4;
+    void* bp = u.bad;
+    void* v = u.vvd;
+    void* f = u.fast;
+    void* g = u.nf;
+    const u64 dcap = std::max<u64>(nd, 2 * u.dcap);
+    JY_TRY(grow_zero(eng, &bp, &bcap, dcap * 4));
+    JY_TRY(grow_zero(eng, &v, &vcap, dcap * R * 8));
+    JY_TRY(grow_zero(eng, &f, &fcap, dcap * 4));
+    JY_TRY(grow_zero(eng, &g, &ncap, dcap * 4));
+    u.bad = static_cast<u32*>(bp);
+    u.vvd = static_cast<u64*>(v);
+    u.fast = static_cast<u32*>(f);
+    u.nf = static_cast<u32*>(g);
+    u.dcap = dcap;
+  }
+  if (lng && u.jcap < u.dcap) {  // (contents never kept: a converge's jobs are its own)
+    jy_dev_free(eng, u.jobs);
+    jy_dev_free(eng, u.plist);
+    u.jobs = nullptr;
+    u.plist = nullptr;
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.jobs), 3 * u.dcap * sizeof(UJob), "ujson copy jobs"));
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.plist), u.dcap * 4, "ujson promotions"));
+    u.jcap = u.dcap;
+  }
 
   // epoch: tags claims, bad marks and look-back words (no per-converge reset)
   u.epoch++;
@@ -1435,22 +2069,13 @@ int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* sl
     u.epoch = 1;
     JY_HIP(eng, hipMemsetAsync(u.dptr, 0, u.kcap * 8, eng->stream));
     if (u.bad) JY_HIP(eng, hipMemsetAsync(u.bad, 0, u.dcap * 4, eng->stream));
+    if (u.fast) JY_HIP(eng, hipMemsetAsync(u.fast, 0, u.dcap * 4, eng->stream));
+    if (u.nf) JY_HIP(eng, hipMemsetAsync(u.nf, 0, u.dcap * 4, eng->stream));
+    if (u.lplan) JY_HIP(eng, hipMemsetAsync(u.lplan, 0, u.lcap * R * sizeof(LPlan), eng->stream));
     for (int i = 0; i < 6; i++)
       if (u.st[i].p)
         JY_HIP(eng, hipMemsetAsync(u.st[i].p, 0, u.st[i].bytes, eng->stream));
     if (u.tmap.p) JY_HIP(eng, hipMemsetAsync(u.tmap.p, 0, u.tmap.bytes, eng->stream));
-  }
-  // persistent per-delta-doc state: bad marks and the dense delta vv (zero)
-  if (nd > u.dcap) {
-    u64 bcap = u.dcap * 4, vcap = u.dcap * R * 8;
-    void* b = u.bad;
-    void* v = u.vvd;
-    const u64 dcap = std::max<u64>(nd, 2 * u.dcap);
-    JY_TRY(grow_zero(eng, &b, &bcap, dcap * 4));
-    JY_TRY(grow_zero(eng, &v, &vcap, dcap * R * 8));
-    u.bad = static_cast<u32*>(b);
-    u.vvd = static_cast<u64*>(v);
-    u.dcap = dcap;
   }
   const u64 ndt = (nd + kDocTile - 1) / kDocTile;
   const u64 tf = (le + kTile - 1) / kTile + (nel + kTile - 1) / kTile + (ncloud + kTile - 1) / kTile + 2;
@@ -1473,6 +2098,7 @@ int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* sl
   const int slot_r = (int)(u.seq % UjsonState::kRing);
   A.pin = u.pin_dev + 8 + 2 * slot_r;
   A.pin_t = u.pin_dev + 2 * slot_r;
+  A.pin_l = u.pin_dev + 24 + 3 * slot_r;
   A.R = R;
   A.epoch = u.epoch;
   A.keep_all = keep_all;
@@ -1492,6 +2118,21 @@ int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* sl
   A.dvv = dvv;
   A.dcoff = dcoff;
   A.dcloud = dcloud;
+  if (lng) {
+    A.lcol = u.lcol;
+    A.lplan = u.lplan;
+    A.lpe = u.lpe;
+    A.lpc = u.lpc;
+    A.lpe_cap = u.lpe_cap;
+    A.lpc_cap = u.lpc_cap;
+    A.lcap = u.lcap;
+    A.jobs = u.jobs;
+    A.jcap = u.jcap;
+    A.fast = u.fast;
+    A.nf = u.nf;
+    A.plist = u.plist;
+    A.long_min = keep_all ? 0 : u.long_min;
+  }
   void* p;
   JY_TRY(jy_scratch(eng, 18, (nd + 1) * 8 * 6 + 64, &p));
   u64* tb = static_cast<u64*>(p);
@@ -1535,9 +2176,17 @@ int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* sl
   A.st_ne = st[4];
   A.st_nc = st[5];
 
-  const u64 g1 = ndt + (nel + kTile1 - 1) / kTile1 + (ncloud + kTile1 - 1) / kTile1 + (nvv + kTile1 - 1) / kTile1;
-  hipLaunchKernelGGL(k_uj_docs, dim3((u32)g1), dim3(kThreads), 0, eng->stream, A, ndt, (nel + kTile1 - 1) / kTile1,
-                     (ncloud + kTile1 - 1) / kTile1, (nvv + kTile1 - 1) / kTile1);
+  // U1a items (validation, dense vv, the long documents' items), U1b doc
+  // tiles (claims, in place / demote, size scans, item docs), the copy jobs
+  // of demotions and regrowths, U2 .. U5, then promotions and their copies
+  const u64 t_el = (nel + kTile1 - 1) / kTile1, t_cl = (ncloud + kTile1 - 1) / kTile1,
+            t_vv = (nvv + kTile1 - 1) / kTile1;
+  hipLaunchKernelGGL(k_uj_items, dim3((u32)std::max<u64>(1, t_el + t_cl + t_vv)), dim3(kThreads), 0, eng->stream, A,
+                     t_el, t_cl, t_vv);
+  hipLaunchKernelGGL(k_uj_docs, dim3((u32)ndt), dim3(kThreads), 0, eng->stream, A, ndt);
+  constexpr u32 kJobGrid = 256;
+  if (lng)
+    hipLaunchKernelGGL(k_uj_jobs, dim3(kJobGrid), dim3(kThreads), 0, eng->stream, A, u.jobs, u.ctr + 5, 2 * u.jcap);
   // grids from the newest finished converge's touched sizes (+25 %), never above the safe bound
   const u64 pa = u.has_pred ? std::min(le, u.pred_ta + u.pred_ta / 4 + 4096) : le;
   const u64 pc = u.has_pred ? std::min(lc, u.pred_tc + u.pred_tc / 4 + 4096) : lc;
@@ -1550,6 +2199,11 @@ int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* sl
   hipLaunchKernelGGL(k_uj_sizes, dim3((u32)ndt), dim3(kThreads), 0, eng->stream, A, ndt);
   const u64 g5 = gf + gk + (nvv + kTile - 1) / kTile + (nd + kTile - 1) / kTile + 2;
   hipLaunchKernelGGL(k_uj_scatter, dim3((u32)g5), dim3(kScatterThreads), 0, eng->stream, A);
+  if (lng && A.long_min) {
+    hipLaunchKernelGGL(k_uj_promote, dim3(64), dim3(kThreads), 0, eng->stream, A);
+    hipLaunchKernelGGL(k_uj_jobs, dim3(kJobGrid), dim3(kThreads), 0, eng->stream, A, u.jobs + 2 * u.jcap, u.ctr + 6,
+                       u.jcap);
+  }
   JY_HIP(eng, hipGetLastError());
   JY_TRACE("ujson merge %llu docs: plan %.1f us, rest of the host side %.1f us", (unsigned long long)nd, th1 - th0,
            jy_now_us() - th1);
@@ -1572,12 +2226,30 @@ int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* sl
   }
 #endif
   // the host's pool bounds: the worst case until the mapped readback lands
-  u.ring_e[slot_r] = le + nel;
-  u.ring_c[slot_r] = lc + ncloud;
+  u.ring_e[slot_r] = (lng ? 2 : 1) * le + nel;
+  u.ring_c[slot_r] = (lng ? 2 : 1) * lc + ncloud;
   u.live_e += nel;
   u.live_c += ncloud;
   JY_HIP(eng, hipEventRecord(u.ready[slot_r], eng->stream));
   u.seq++;
+  return JY_OK;
+}
+
+int32_t jy_ujson_stats_ext(jy_engine* eng, u64* out16) {
+  JY_HIP(eng, hipSetDevice(eng->device));
+  UjsonState& u = eng->ujson;
+  if (!u.stats) {
+    std::memset(out16, 0, 128);
+    return JY_OK;
+  }
+  JY_HIP(eng, hipMemcpyAsync(out16, u.stats, 128, hipMemcpyDeviceToHost, eng->stream));
+  JY_HIP(eng, hipStreamSynchronize(eng->stream));
+  return JY_OK;
+}
+
+int32_t jy_ujson_set_inplace(jy_engine* eng, uint32_t min_elems) {
+  eng->ujson.allow_long = true;
+  eng->ujson.long_min = min_elems;
   return JY_OK;
 }
 
@@ -1607,8 +2279,12 @@ int32_t jy_ujson_gather(jy_engine* eng, u64 n, const u32* slots, const u64* oeof
 }
 int32_t jy_ujson_gather_of(jy_engine* eng, const UjsonState& u, u64 n, const u32* slots, const u64* oeoff,
                            const u64* ocoff, u64 nel, u64 ncl, u64* odots, u64* oelems, u64* ovv, u64* ocloud) {
-  if (nel) LAUNCH(k_uj_gather_items<true>, nel, u.meta, u.epool, u.cpool, slots, n, oeoff, nel, odots, oelems);
-  if (ncl) LAUNCH(k_uj_gather_items<false>, ncl, u.meta, u.epool, u.cpool, slots, n, ocoff, ncl, ocloud, ocloud);
+  if (nel)
+    LAUNCH(k_uj_gather_items<true>, nel, u.meta, u.epool, u.cpool, slots, n, oeoff, nel, odots, oelems, u.lcol,
+           u.lpe, u.lpc, u.R);
+  if (ncl)
+    LAUNCH(k_uj_gather_items<false>, ncl, u.meta, u.epool, u.cpool, slots, n, ocoff, ncl, ocloud, ocloud, u.lcol,
+           u.lpe, u.lpc, u.R);
   LAUNCH(k_uj_gather_vv, n * u.R, u.vv, u.R, slots, n, ovv);
   return JY_OK;
 }

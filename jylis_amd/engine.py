@@ -569,12 +569,22 @@ class Engine:
                                                 cloud.ctypes.data, C.byref(k), C.byref(me), C.byref(mc), HOST))
         return slots[:nk].copy(), eo, dots[:ne].copy(), elems[:ne].copy(), vv[:nk].copy(), co, cloud[:nc].copy()
 
+    UJSON_STATS = ("touched_el", "touched_cloud", "out_el", "out_cloud", "delta_el", "delta_cloud", "delta_docs",
+                   "calls", "inplace_docs", "inplace_state_el", "inplace_state_cloud", "inplace_added_el",
+                   "inplace_added_cloud", "inplace_folded", "promoted", "demoted")
+
     def ujson_stats(self):
-        """cumulative converge counters (jy_ujson_stats): dict of touched / written / delta sizes"""
-        out = np.zeros(8, np.uint64)
-        self._check(self.lib.jy_ujson_stats(self.h, out.ctypes.data))
-        keys = ("touched_el", "touched_cloud", "out_el", "out_cloud", "delta_el", "delta_cloud", "delta_docs", "calls")
-        return {k: int(v) for k, v in zip(keys, out)}
+        """cumulative converge counters (jy_ujson_stats_ext): dict of touched /
+        written / delta sizes of the regular merge path, then the in-place
+        layout's documents, their untouched state sizes, what they appended
+        and folded, promotions and demotions"""
+        out = np.zeros(16, np.uint64)
+        self._check(self.lib.jy_ujson_stats_ext(self.h, out.ctypes.data))
+        return {k: int(v) for k, v in zip(self.UJSON_STATS, out)}
+
+    def ujson_set_inplace(self, min_elems):
+        """promotion threshold of the UJSON in-place layout (0: no promotions)"""
+        self._check(self.lib.jy_ujson_set_inplace(self.h, int(min_elems)))
 
     def ujson_read(self, slots):
         """-> (el_offs, dots, elems, vv[n][R], cloud_offs, cloud)"""

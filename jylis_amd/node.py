@@ -107,12 +107,9 @@ class Node:
         """every queued call done, GPU work included"""
         with self._held_mu:
             held, self._held = self._held, []
-        rc = self.lib.jy_node_sync(self.h)
-        if rc != 0:  # a queued call failed: drain the streams before the inputs go
-            msg = self.lib.jy_node_last_error(self.h).decode(errors="replace")
-            self.lib.jy_node_sync(self.h)
-            raise EngineError(rc, msg)
+        rc = self.lib.jy_node_sync(self.h)  # (drains every stream, failure or not)
         del held
+        self._check(rc)
 
     def fence(self):
         """every queued call issued to the GPU streams (their device inputs are
@@ -120,14 +117,28 @@ class Node:
         self._check(self.lib.jy_node_fence(self.h))
 
     @contextlib.contextmanager
-    def locked(self):
-        """exclusive use of the node's engines (jy_node_lock / jy_node_unlock)"""
-        rc = self.lib.jy_node_lock(self.h)
+    def locked(self, ctype=None):
+        """exclusive use of the node's engines (jy_node_lock / jy_node_unlock);
+        with a CRDT type, after that type's queued jobs only
+        (jy_node_lock_type; NOFENCE: after none)"""
+        rc = self.lib.jy_node_lock(self.h) if ctype is None else self.lib.jy_node_lock_type(self.h, int(ctype))
         try:
             self._check(rc)
             yield self
         finally:
             self.lib.jy_node_unlock(self.h)
+
+    NOFENCE = -1
+
+    def pending(self, ctype=-1):
+        """jobs queued or running (of one CRDT type, or all)"""
+        n = C.c_uint64()
+        self._check(self.lib.jy_node_pending(self.h, int(ctype), C.byref(n)))
+        return n.value
+
+    def arena_gc(self, enable=True):
+        """the worker reclaims TREG / TLOG arenas after their jobs (jy_node_arena_gc)"""
+        self._check(self.lib.jy_node_arena_gc(self.h, 1 if enable else 0))
 
     def stats(self):
         out = np.zeros(5, np.uint64)

@@ -21,11 +21,16 @@ class _Node
   at a time in call order, so the five actors' calls never interleave on the
   communicator and no scheduler thread waits for the GPU.  Reads, local
   writes and flushes use the key's owner shard (`owner`, `shards`) between
-  `lock` and `unlock` (jy_node_lock waits for the jobs queued before it).
+  `lock(ty)` and `unlock`: jy_node_lock_type waits only for the jobs of the
+  repo's own type queued before it (a TREG read never waits for queued UJSON
+  converges), JyNoFence for none (deltas_size and flush read state no
+  converge changes).  The value arenas are reclaimed by the node's worker
+  after TREG / TLOG jobs (jy_node_arena_gc), so a drain only enqueues.
   Never call a jy_node_* entry point while holding the lock."""
   let ptr: Pointer[None] tag
   let shards: Array[_Engine] = shards.create()   // one view per GPU, index = shard
   let _col: U32                                   // this replica's column (the same on every shard)
+  embed _cols: Map[U64, U16] = _cols.create()     // replica id -> column, cached per repo
 
   new create(identity: U64) ? =>
     let cfg = JyConfig
@@ -36,13 +41,14 @@ class _Node
     var c: U32 = 0
     if @jy_node_replica_col(ptr, identity, addressof c) != 0 then error end
     _col = c
+    @jy_node_arena_gc(ptr, 1)
     for s in Range[U32](0, @jy_node_nshards(ptr)) do shards.push(_Engine.view(@jy_node_engine(ptr, s), c)) end
 
   fun col(): U32 => _col
 
   fun check(rc: I32) ? => if rc != 0 then error end
 
-  fun lock() => @jy_node_lock(ptr)
+  fun lock(ty: I32) => @jy_node_lock_type(ptr, ty)
   fun unlock() => @jy_node_unlock(ptr)
 
   fun owner(key: String): _Engine ? =>
@@ -50,16 +56,21 @@ class _Node
     shards(@jy_node_shard_of(ptr, key.cpointer(), key.size().u64()).usize())?
 
   fun ref replica_col(id: U64): U16 ? =>
-    """a peer's column, registered on every shard in one order"""
+    """a peer's column, registered on every shard in one order; cached here,
+    so a drain's per-cell lookups stay on the scheduler thread (the library
+    answers a known id without waiting for the worker as well)"""
+    try return _cols(id)? end
     var c: U32 = 0
     check(@jy_node_replica_col(ptr, id, addressof c))?
+    _cols(id) = c.u16()
     c.u16()
 
   fun _final() => @jy_node_release(ptr)
 
 primitive _Lock
-  """the shared node's engines, exclusively (a repo holds no node: no-op)"""
-  fun apply(node: (_Node box | None)) => match node | let n: _Node box => n.lock() end
+  """the shared node's engines, exclusively, after the jobs of type `ty`
+  queued before (JyNoFence: none); a repo holds no node: no-op"""
+  fun apply(node: (_Node box | None), ty: I32) => match node | let n: _Node box => n.lock(ty) end
 
 primitive _Unlock
   fun apply(node: (_Node box | None)) => match node | let n: _Node box => n.unlock() end

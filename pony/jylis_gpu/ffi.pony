@@ -120,6 +120,9 @@ use @jy_node_release[None](node: Pointer[None] tag)
 use @jy_node_fence[I32](node: Pointer[None] tag)
 use @jy_node_lock[I32](node: Pointer[None] tag)
 use @jy_node_unlock[None](node: Pointer[None] tag)
+use @jy_node_lock_type[I32](node: Pointer[None] tag, ty: I32)
+use @jy_node_pending[I32](node: Pointer[None] tag, ty: I32, n_out: Pointer[U64] tag)
+use @jy_node_arena_gc[I32](node: Pointer[None] tag, enable: U32)
 use @jy_node_counter_converge[I32](node: Pointer[None] tag, ty: I32, n: U64, key_bytes: Pointer[U8] tag,
   key_offs: Pointer[U64] tag, cell_offs: Pointer[U64] tag, sign: Pointer[U8] tag, col: Pointer[U16] tag,
   value: Pointer[U64] tag, mem: I32)
@@ -142,6 +145,7 @@ primitive JyTREG fun apply(): I32 => 2
 primitive JyTLOG fun apply(): I32 => 3
 primitive JyUJSON fun apply(): I32 => 4
 primitive JyNoSlot fun apply(): U32 => U32.max_value()
+primitive JyNoFence fun apply(): I32 => -1
 primitive JyDotSeqBits fun apply(): U64 => 48
 // queued converge pairs that force a drain before the next entry point
 primitive _DrainBound fun apply(): USize => 65536

@@ -36,7 +36,7 @@ class RepoGCOUNTGpu
     peer pair first, so a replica with no local commands still converges
     each tick"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyNoFence())  // the shared node's engines (jy_node_lock_type)
     let r = _deltas_size()
     _Unlock(_node)
     r
@@ -47,7 +47,7 @@ class RepoGCOUNTGpu
   fun ref flush_deltas(): Array[(String, Any box)] box =>
     """repo_gcount.pony:18-23: every pending key with its post-write total"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyNoFence())  // the shared node's engines (jy_node_lock_type)
     let r = _flush_deltas()
     _Unlock(_node)
     r
@@ -93,7 +93,7 @@ class RepoGCOUNTGpu
   fun ref get(resp: Respond, key: String): Bool =>
     """repo_gcount.pony:53-55: a missing key reads 0"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyGCOUNT())  // the shared node's engines (jy_node_lock_type)
     let r = _get(resp, key)
     _Unlock(_node)
     r
@@ -116,7 +116,7 @@ class RepoGCOUNTGpu
   fun ref inc(resp: Respond, key: String, value: U64): Bool =>
     """repo_gcount.pony:57-60, on the key's owner shard"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyGCOUNT())  // the shared node's engines (jy_node_lock_type)
     let r = _inc(resp, key, value)
     _Unlock(_node)
     r
@@ -151,7 +151,7 @@ class RepoPNCOUNTGpu
     peer pair first, so a replica with no local commands still converges
     each tick"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyNoFence())  // the shared node's engines (jy_node_lock_type)
     let r = _deltas_size()
     _Unlock(_node)
     r
@@ -162,7 +162,7 @@ class RepoPNCOUNTGpu
   fun ref flush_deltas(): Array[(String, Any box)] box =>
     """repo_pncount.pony:19-24"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyNoFence())  // the shared node's engines (jy_node_lock_type)
     let r = _flush_deltas()
     _Unlock(_node)
     r
@@ -211,7 +211,7 @@ class RepoPNCOUNTGpu
   fun ref get(resp: Respond, key: String): Bool =>
     """repo_pncount.pony:55-57: (sum P - sum N) as i64; a missing key reads 0"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyPNCOUNT())  // the shared node's engines (jy_node_lock_type)
     let r = _get(resp, key)
     _Unlock(_node)
     r
@@ -234,7 +234,7 @@ class RepoPNCOUNTGpu
   fun ref write(resp: Respond, key: String, value: I64, sign: I32): Bool =>
     """INC / DEC (repo_pncount.pony:59-67): the i64 argument bit-cast to u64"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyPNCOUNT())  // the shared node's engines (jy_node_lock_type)
     let r = _write(resp, key, value, sign)
     _Unlock(_node)
     r

@@ -29,7 +29,7 @@ class RepoTREGGpu
     peer pair first, so a replica with no local commands still converges
     each tick"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyNoFence())  // the shared node's engines (jy_node_lock_type)
     let r = _deltas_size()
     _Unlock(_node)
     r
@@ -49,7 +49,7 @@ class RepoTREGGpu
   fun ref flush_deltas(): Array[(String, Any box)] box =>
     """repo_treg.pony:18-22: every pending key with its delta register"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyNoFence())  // the shared node's engines (jy_node_lock_type)
     let r = _flush_deltas()
     _Unlock(_node)
     r
@@ -104,9 +104,6 @@ class RepoTREGGpu
             ts.cpointer(), vals.bytes.cpointer(), vals.offs.cpointer(), JyHost()))?
         end
       end
-      n.lock()  // (the converge above only enqueued; the engines are shared)
-      for e in n.shards.values() do e.maybe_collect(JyTREG()) end
-      n.unlock()
     end
     _in.clear()
 
@@ -120,7 +117,7 @@ class RepoTREGGpu
   fun ref get(resp: Respond, key: String): Bool =>
     """repo_treg.pony:54-63: [value, timestamp], or null for a missing key"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyTREG())  // the shared node's engines (jy_node_lock_type)
     let r = _get(resp, key)
     _Unlock(_node)
     r
@@ -145,7 +142,7 @@ class RepoTREGGpu
   fun ref set(resp: Respond, key: String, value: String, timestamp: U64): Bool =>
     """repo_treg.pony:65-68"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyTREG())  // the shared node's engines (jy_node_lock_type)
     let r = _set(resp, key, value, timestamp)
     _Unlock(_node)
     r
@@ -186,7 +183,7 @@ class RepoTLOGGpu
     peer pair first, so a replica with no local commands still converges
     each tick"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyNoFence())  // the shared node's engines (jy_node_lock_type)
     let r = _deltas_size()
     _Unlock(_node)
     r
@@ -206,7 +203,7 @@ class RepoTLOGGpu
   fun ref flush_deltas(): Array[(String, Any box)] box =>
     """repo_tlog.pony:21-25: every pending key with its delta log"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyNoFence())  // the shared node's engines (jy_node_lock_type)
     let r = _flush_deltas()
     _Unlock(_node)
     r
@@ -276,9 +273,6 @@ class RepoTLOGGpu
             JyHost()))?
         end
       end
-      n.lock()  // (the converge above only enqueued; the engines are shared)
-      for e in n.shards.values() do e.maybe_collect(JyTLOG()) end
-      n.unlock()
     end
     _in.clear()
 
@@ -301,7 +295,7 @@ class RepoTLOGGpu
     """INS key value ts / TRIMAT key ts / TRIM key count / CLR key
     (repo_tlog.pony:85-111): one jy_tlog_write command"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyTLOG())  // the shared node's engines (jy_node_lock_type)
     let r = try _write(resp, key, op, value, ts', count)? else _Unlock(_node); error end
     _Unlock(_node)
     r
@@ -326,7 +320,7 @@ class RepoTLOGGpu
   fun ref get(resp: Respond, key: String, count: USize): Bool =>
     """repo_tlog.pony:69-83: at most `count` entries, newest first"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyTLOG())  // the shared node's engines (jy_node_lock_type)
     let r = _get(resp, key, count)
     _Unlock(_node)
     r
@@ -360,7 +354,7 @@ class RepoTLOGGpu
   fun ref size(resp: Respond, key: String, cutoff: Bool): Bool =>
     """SIZE / CUTOFF (repo_tlog.pony:90-96): 0 for a missing key"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyTLOG())  // the shared node's engines (jy_node_lock_type)
     let r = _size(resp, key, cutoff)
     _Unlock(_node)
     r

@@ -70,7 +70,7 @@ class RepoUJSONGpu
     peer pair first, so a replica with no local commands still converges
     each tick"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyNoFence())  // the shared node's engines (jy_node_lock_type)
     let r = _deltas_size()
     _Unlock(_node)
     r
@@ -90,7 +90,7 @@ class RepoUJSONGpu
   fun ref flush_deltas(): Array[(String, Any box)] box =>
     """repo_ujson.pony:22-26: every pending doc with its delta document"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyNoFence())  // the shared node's engines (jy_node_lock_type)
     let r = _flush_deltas()
     _Unlock(_node)
     r
@@ -254,7 +254,7 @@ class RepoUJSONGpu
   fun ref get(resp: Respond, key: String, path: Array[String] val): Bool =>
     """repo_ujson.pony:68-72: the render, or '' for nothing"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyUJSON())  // the shared node's engines (jy_node_lock_type)
     let r = _get(resp, key, path)
     _Unlock(_node)
     r
@@ -278,7 +278,7 @@ class RepoUJSONGpu
   fun ref ins_rm(resp: Respond, key: String, path: Array[String] val, text: String, op: U8): Bool ? =>
     """INS / RM (repo_ujson.pony:90-110): the value parses as a UJSON primitive"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyUJSON())  // the shared node's engines (jy_node_lock_type)
     let r = try _ins_rm(resp, key, path, text, op)? else _Unlock(_node); error end
     _Unlock(_node)
     r
@@ -298,7 +298,7 @@ class RepoUJSONGpu
   fun ref clr(resp: Respond, key: String, path: Array[String] val): Bool =>
     """CLR (repo_ujson.pony:85-88): no key creation"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyUJSON())  // the shared node's engines (jy_node_lock_type)
     let r = _clr(resp, key, path)
     _Unlock(_node)
     r
@@ -326,7 +326,7 @@ class RepoUJSONGpu
   fun ref set(resp: Respond, key: String, path: Array[String] val, text: String): Bool ? =>
     """SET (repo_ujson.pony:74-83): clear the path, insert the node's leaves"""
     _drain()
-    _Lock(_node)  // the shared node's engines (jy_node_lock)
+    _Lock(_node, JyUJSON())  // the shared node's engines (jy_node_lock_type)
     let r = try _set(resp, key, path, text)? else _Unlock(_node); error end
     _Unlock(_node)
     r

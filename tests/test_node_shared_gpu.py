@@ -141,6 +141,42 @@ def test_calls_return_before_the_work(oracle_mod):
         node.close()
 
 
+def test_typed_lock_does_not_wait_for_other_types(oracle_mod):
+    """jy_node_lock_type (round 6): a TREG read under the lock returns once
+    the TREG jobs queued before it are done, while UJSON converges queued
+    after them are still waiting; the full lock waits for every job.  Both
+    states equal the oracle's."""
+    from jylis_amd import synth as S
+    from jylis_amd.node import Node
+    from jylis_amd.repo import REPOS
+    O = oracle_mod
+    node = Node(1, "rccl")
+    try:
+        tr = random_history(O, O.TREG, seed=93, nops=120, nkeys=40)
+        st0, dl = S.ujson_tables(30000, seed=S.BASE_SEED + 77, rounds=12, R=16)
+        uj = [st0] + dl
+        for b in tr:
+            node.converge_table(O.TREG, b)
+        for b in uj:
+            node.converge_table(O.UJSON, b)
+        with node.locked(O.TREG):
+            waiting = node.pending(O.UJSON)
+            got = join_rows(O.TREG, dict(split_rows(O.TREG, REPOS[O.TREG](node.engines[0]).state())))
+        assert waiting > 0, "the TREG lock waited for the UJSON jobs"
+        assert_state_equal(O.TREG, _want(O, O.TREG, tr), got)
+        with node.locked():
+            assert node.pending() == 0
+        node.sync()
+        assert_state_equal(O.UJSON, _want(O, O.UJSON, uj), join_rows(O.UJSON, _union_rows(O.UJSON, node)))
+        # deltas_size / flush style access: no fence at all
+        node.converge_table(O.UJSON, dl[0])
+        with node.locked(Node.NOFENCE):
+            pass
+        node.sync()
+    finally:
+        node.close()
+
+
 def test_multiprocess_form_at_world_one(oracle_mod):
     """the multi-process constructor (nlocal = 1, a shared ncclUniqueId) at
     one rank: the communicator made from a unique id another call produced"""
