@@ -563,6 +563,17 @@ int32_t jy_node_pending(jy_node* node, int32_t type, uint64_t* n_out);
  * Pony glue ran after every drain under the lock.  Off by default; callers
  * that pack value handles must consume them under the lock. */
 int32_t jy_node_arena_gc(jy_node* node, uint32_t enable);
+/* The payload schedule one shard of the exchange issues (host logic only, no
+ * GPU; the node's exchange runs exactly this): for S shards, shard `rank`,
+ * W count granules, nwires wire columns (granule, element bytes) and the
+ * shard's per-peer element counts send_cnt / recv_cnt [S][W], the ordered
+ * operations ops_out[i] = {kind (0 own part copied, 1 send, 2 receive), wire,
+ * peer, source offset, destination offset, bytes}, at most cap of them;
+ * *nops_out = how many there are.  Tests check it for S = 2..8 (every send
+ * meets a receive of the same size, one peer order on every rank). */
+int32_t jy_node_exchange_plan(uint32_t S, uint32_t rank, uint32_t W, uint32_t nwires, const int32_t* wire_gran,
+                              const int32_t* wire_esize, const uint64_t* send_cnt, const uint64_t* recv_cnt,
+                              uint64_t cap, uint64_t* ops_out, uint64_t* nops_out);
 
 /* Converge one decoded peer batch (per process).  Keys: n strings (key_bytes,
  * key_offs[n + 1]).  `mem` = JY_HOST (staged per ingest shard) or JY_DEVICE

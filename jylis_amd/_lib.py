@@ -148,6 +148,7 @@ SIGNATURES = {
     "jy_node_lock_type": (I32, [P, I32]),
     "jy_node_pending": (I32, [P, I32, P]),
     "jy_node_arena_gc": (I32, [P, U32]),
+    "jy_node_exchange_plan": (I32, [U32, U32, U32, U32, P, P, P, P, U64, P, P]),
     "jy_node_counter_converge": (I32, [P, I32, U64, P, P, P, P, P, P, I32]),
     "jy_node_treg_converge": (I32, [P, U64, P, P, P, P, P, I32]),
     "jy_node_tlog_converge": (I32, [P, U64, P, P, P, P, P, P, P, I32]),

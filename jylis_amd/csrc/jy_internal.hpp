@@ -468,6 +468,7 @@ struct UjsonState {  // per-document pool segments + dense vv
   u32* fast = nullptr;      // [dcap] == epoch: the delta doc converges in place
   u32* nf = nullptr;        // [dcap] == epoch: a long doc whose delta is not append-shaped
   u32* plist = nullptr;     // [dcap] delta docs whose merged document is promoted
+  u32* flist = nullptr;     // [dcap] delta docs converged in place (ctr[7] of them; U5 commits them)
   u64 long_used_e = 0, long_used_c = 0, long_ids = 0;  // the newest readback of ctr[2..4]
 };
 

@@ -849,6 +849,38 @@ struct Wire {
   int gran, esize, sidx, ridx;
 };
 
+// The payload schedule of one shard (pure host logic, shared with
+// jy_node_exchange_plan, which the CPU tests drive for S = 2..8): per wire
+// column, peers in ascending order -- the same order on every rank -- a
+// send of this shard's part for the peer and a receive of the peer's part,
+// each at its running offset in the source-major columns; the shard's own
+// part is a device copy.  sc / rc: [kMaxS][W] element counts sent to /
+// received from each peer (rc of shard d from s == sc of shard s for d).
+struct XOp {
+  u32 kind;  // 0 own part (device copy), 1 send, 2 receive
+  u32 wire, peer;
+  u64 soff, roff, bytes;
+};
+void plan_payload(u32 S, u32 rank, u32 W, const std::vector<Wire>& wires, const u64* sc, const u64* rc,
+                  std::vector<XOp>& ops) {
+  ops.clear();
+  for (u32 wi = 0; wi < (u32)wires.size(); wi++) {
+    const Wire& w = wires[wi];
+    u64 so = 0, ro = 0;
+    for (u32 d = 0; d < S; d++) {
+      const u64 sn = sc[(u64)d * W + w.gran] * w.esize, rn = rc[(u64)d * W + w.gran] * w.esize;
+      if (d == rank) {
+        if (sn) ops.push_back(XOp{0, wi, d, so, ro, sn});
+      } else {
+        if (sn) ops.push_back(XOp{1, wi, d, so, 0, sn});
+        if (rn) ops.push_back(XOp{2, wi, d, 0, ro, rn});
+      }
+      so += sn;
+      ro += rn;
+    }
+  }
+}
+
 int32_t exchange(jy_node* nd, u32 W, const std::vector<Wire>& wires, u32 nl) {
   const u32 S = nd->S;
   // 1. counts: per destination and granule -> per source and granule
@@ -907,27 +939,21 @@ int32_t exchange(jy_node* nd, u32 W, const std::vector<Wire>& wires, u32 nl) {
   if (nd->fabric == JY_FABRIC_RCCL) {
     NcclGroup grp;  // ends the group on every return
     ND_NCCL(nd, grp.start());
+    std::vector<XOp> ops;
     for (NdShard& sh : nd->sh) {
       ND_HIP(nd, hipSetDevice(sh.dev));  // (the self copies below)
-      const u64* sc = sh.pin;
-      const u64* rc = sh.pin + (u64)kMaxS * W;
-      for (const Wire& w : wires) {
+      plan_payload(S, sh.rank, W, wires, sh.pin, sh.pin + (u64)kMaxS * W, ops);
+      for (const XOp& o : ops) {
+        const Wire& w = wires[o.wire];
         const uint8_t* sp = static_cast<const uint8_t*>(sh.b[w.sidx].p);
         uint8_t* rp = static_cast<uint8_t*>(sh.b[w.ridx].p);
-        u64 so = 0, ro = 0;
-        for (u32 d = 0; d < S; d++) {
-          const u64 sn = sc[(u64)d * W + w.gran] * w.esize, rn = rc[(u64)d * W + w.gran] * w.esize;
-          if (d == sh.rank) {
-            // its own part: a device copy on the same stream (through RCCL it
-            // cost ~100 us per column at 8M keys, the whole exchange at S = 1)
-            if (sn) ND_HIP(nd, hipMemcpyAsync(rp + ro, sp + so, sn, hipMemcpyDeviceToDevice, sh.eng->stream));
-          } else {
-            if (sn) ND_NCCL(nd, ncclSend(sp + so, sn, ncclUint8, (int)d, sh.comm, sh.eng->stream));
-            if (rn) ND_NCCL(nd, ncclRecv(rp + ro, rn, ncclUint8, (int)d, sh.comm, sh.eng->stream));
-          }
-          so += sn;
-          ro += rn;
-        }
+        if (o.kind == 0)  // its own part: a device copy on the same stream (through RCCL it
+                          // cost ~100 us per column at 8M keys, the whole exchange at S = 1)
+          ND_HIP(nd, hipMemcpyAsync(rp + o.roff, sp + o.soff, o.bytes, hipMemcpyDeviceToDevice, sh.eng->stream));
+        else if (o.kind == 1)
+          ND_NCCL(nd, ncclSend(sp + o.soff, o.bytes, ncclUint8, (int)o.peer, sh.comm, sh.eng->stream));
+        else
+          ND_NCCL(nd, ncclRecv(rp + o.roff, o.bytes, ncclUint8, (int)o.peer, sh.comm, sh.eng->stream));
       }
     }
     ND_NCCL(nd, grp.end());
@@ -2523,6 +2549,29 @@ int32_t jy_node_pending(jy_node* nd, int32_t type, uint64_t* n_out) {
   if (type >= JY_NTYPES) return nd->fail(JY_EINVAL, "bad type");
   std::lock_guard<std::mutex> lk(nd->qmu);
   *n_out = type < 0 ? nd->submitted - nd->finished : nd->sub_t[type] - nd->fin_t[type];
+  return JY_OK;
+}
+
+int32_t jy_node_exchange_plan(uint32_t S, uint32_t rank, uint32_t W, uint32_t nwires, const int32_t* wire_gran,
+                              const int32_t* wire_esize, const uint64_t* send_cnt, const uint64_t* recv_cnt,
+                              uint64_t cap, uint64_t* ops_out, uint64_t* nops_out) {
+  if (S == 0 || S > kMaxS || rank >= S || W == 0 || W > kMaxW) return JY_EINVAL;
+  std::vector<Wire> wires(nwires);
+  for (u32 i = 0; i < nwires; i++) {
+    if (wire_gran[i] < 0 || (u32)wire_gran[i] >= W || wire_esize[i] <= 0) return JY_EINVAL;
+    wires[i] = Wire{wire_gran[i], wire_esize[i], 0, 0};
+  }
+  std::vector<u64> sc((u64)kMaxS * W, 0), rc((u64)kMaxS * W, 0);
+  std::copy(send_cnt, send_cnt + (u64)S * W, sc.begin());
+  std::copy(recv_cnt, recv_cnt + (u64)S * W, rc.begin());
+  std::vector<XOp> ops;
+  plan_payload(S, rank, W, wires, sc.data(), rc.data(), ops);
+  *nops_out = ops.size();
+  for (u64 i = 0; i < ops.size() && i < cap; i++) {
+    const XOp& o = ops[i];
+    const u64 v[6] = {o.kind, o.wire, o.peer, o.soff, o.roff, o.bytes};
+    std::copy(v, v + 6, ops_out + 6 * i);
+  }
   return JY_OK;
 }
 

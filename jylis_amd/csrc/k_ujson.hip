@@ -286,6 +286,7 @@ struct UjArgs {
   u32* fast;
   u32* nf;
   u32* plist;
+  u32* flist;    // the delta docs converging in place (ctr[7] of them)
   u32 long_min;  // promotion threshold (0: none this converge)
 };
 
@@ -399,11 +400,6 @@ struct Shared {
   u32 tk;
 };
 
-// membership of dot x in a sorted run [lo, hi) of dots
-__device__ __forceinline__ bool in_dots(const u64* a, u64 lo, u64 hi, u64 x) {
-  const u64 p = lb_g<false>(a, lo, hi, x);
-  return p < hi && a[p] == x;
-}
 
 // ---- U1a classification of one delta item of a LONG document (lid):
 // whether the delta is append-shaped in the item's column, and where the
@@ -429,10 +425,13 @@ __device__ void uj_item_long(const UjArgs& A, int kind, u64 k, u64 i, u32 lid, u
     }
     // the elements it covers (the run's prefix of seq <= q) go unless the
     // delta holds them: a prefix within kTrimSpan is trimmed in place
-    if (L.elen && dseq(A.lpe[L.ebase].dot) <= q) {
-      const u64 cut = lb_g<true>(A.lpe, L.ebase, L.ebase + L.elen, mkdot(c, q + 1)) - L.ebase;
+    if (L.elen) {  // the run's first 8 elements at once (old elements sit there); a search past them
+      u64 cut = 0;
+#pragma unroll
+      for (u32 j = 0; j < 8; j++) cut += j < L.elen && dseq(A.lpe[L.ebase + j].dot) <= q;
+      if (cut == 8 && L.elen > 8) cut = lb_g<true>(A.lpe, L.ebase + 8, L.ebase + L.elen, mkdot(c, q + 1)) - L.ebase;
       if (cut > kTrimSpan) A.nf[k] = A.epoch;
-      else A.lplan[li].treq = tag(A, 1);
+      else if (cut) atomicMax((unsigned long long*)&A.lplan[li].treq, (unsigned long long)tag(A, cut));
     }
     return;
   }
@@ -448,17 +447,29 @@ __device__ void uj_item_long(const UjArgs& A, int kind, u64 k, u64 i, u32 lid, u
   if (fresh && (i == lo || dcol(prev) != c || dseq(prev) <= F)) (kind == 0 ? P.efs : P.cfs) = tag(A, i);
   if (i + 1 == hi || dcol(next) != c) (kind == 0 ? P.ece : P.cce) = tag(A, i + 1);
   if (fresh) return;
-  const bool seen = q <= vs || in_dots(A.lpc, L.cbase, L.cbase + L.clen, x);
+  // the state's cloud run (seen?), and for a context dot the state's element
+  // run (a live element?) and the delta's elements (kept?): the three
+  // searches in lockstep, one dependent round per level
+  const bool el = kind == 1;
+  u64 clo = L.cbase, chi = q <= vs ? clo : L.cbase + L.clen;  // (covered by the vv: no cloud search)
+  u64 elo = L.ebase, ehi = el ? L.ebase + L.elen : elo;
+  u64 dlo = A.deoff[k], dhi = el ? A.deoff[k + 1] : dlo;
+  while (clo < chi || elo < ehi || dlo < dhi) {
+    const u64 cm = (clo + chi) >> 1, em = (elo + ehi) >> 1, dm = (dlo + dhi) >> 1;
+    const u64 cv = clo < chi ? A.lpc[cm] : 0, ev = elo < ehi ? A.lpe[em].dot : 0, dv = dlo < dhi ? A.ddots[dm] : 0;
+    if (clo < chi) (cv < x ? clo = cm + 1 : chi = cm);
+    if (elo < ehi) (ev < x ? elo = em + 1 : ehi = em);
+    if (dlo < dhi) (dv < x ? dlo = dm + 1 : dhi = dm);
+  }
+  const bool seen = q <= vs || (clo < L.cbase + L.clen && A.lpc[clo] == x);
   if (!seen) {
     A.nf[k] = A.epoch;
     return;
   }
-  if (kind == 1) {  // a context dot removes a live state element the delta does not hold
-    const u64 p = lb_g<true>(A.lpe, L.ebase, L.ebase + L.elen, x);
-    if (p < L.ebase + L.elen && A.lpe[p].dot == x && !in_dots(A.ddots, A.deoff[k], A.deoff[k + 1], x)) {
-      if (p - L.ebase >= kTrimSpan) A.nf[k] = A.epoch;  // too far in: the regular path
-      else P.treq = tag(A, 1);
-    }
+  if (el && elo < L.ebase + L.elen && A.lpe[elo].dot == x && !(dlo < A.deoff[k + 1] && A.ddots[dlo] == x)) {
+    // a context dot removes a live state element the delta does not hold
+    if (elo - L.ebase >= kTrimSpan) A.nf[k] = A.epoch;  // too far in: the regular path
+    else atomicMax((unsigned long long*)&P.treq, (unsigned long long)tag(A, elo - L.ebase + 1));
   }
 }
 
@@ -469,11 +480,22 @@ __device__ void uj_item_long(const UjArgs& A, int kind, u64 k, u64 i, u32 lid, u
 // document is DEMOTED: a copy job lays its column runs out as one regular
 // run at the pools' bump pointers and the regular merge path takes it.
 // Returns (lane 0) the doc's touched state sizes for the scans (0 in place).
-__device__ void uj_docs_long(const UjArgs& A, u64 k, u64& asz, u64& csz) {
+// the tile's copy jobs are gathered in LDS and reserved with one atomic per
+// tile (a same-address atomic per document serialised ~1.5K of them)
+struct JobBuf {
+  static constexpr u32 kCap = 128;
+  UJob j[kCap];
+  u32 n;
+  __device__ void push(const UjArgs& A, const UJob& x) {  // (one lane)
+    const u32 q = atomicAdd(&n, 1u);
+    if (q < kCap) j[q] = x;
+    else A.jobs[atomicAdd((unsigned long long*)(A.ctr + 5), 1ull)] = x;  // overflow: directly
+  }
+};
+__device__ void uj_docs_long(const UjArgs& A, u64 k, u32 lid, u32 melen, u32 mclen, u64& asz, u64& csz, JobBuf& jb,
+                             bool& in_place) {
   const u32 lane = threadIdx.x & 63, R = A.R;
-  const u32 s = A.slot[k];
-  const UMeta m = A.meta[s];
-  const u32 lid = (u32)m.ebase;
+  const UMeta m{lid, melen, kLongMark, 0, mclen, kLongMark};
   const u64 b = (u64)lid * R;
   const bool act = lane < R;
   LCol L{};
@@ -519,11 +541,12 @@ __device__ void uj_docs_long(const UjArgs& A, u64 k, u64& asz, u64& csz) {
     if (lane == 0) {
       // the runs that grew are copied, the trims done, before any append
       // (k_uj_jobs, then U2); a repeated doc's jobs are skipped there
-      if (moved) A.jobs[atomicAdd((unsigned long long*)(A.ctr + 5), 1ull)] = UJob{k, 0, moved, UJ_REGROW, lid};
-      if (trims) A.jobs[atomicAdd((unsigned long long*)(A.ctr + 5), 1ull)] = UJob{k, 0, R, UJ_TRIM, lid};
+      if (moved) jb.push(A, UJob{k, 0, moved, UJ_REGROW, lid});
+      if (trims) jb.push(A, UJob{k, 0, R, UJ_TRIM, lid});
       A.fast[k] = A.epoch;
       A.abase[k] = lid;
       asz = csz = 0;
+      in_place = true;
     }
     return;
   }
@@ -532,8 +555,7 @@ __device__ void uj_docs_long(const UjArgs& A, u64 k, u64& asz, u64& csz) {
   if (lane == 0) {
     eb = m.elen ? atomicAdd((unsigned long long*)A.ctr, (unsigned long long)m.elen) : 0;
     cb = m.clen ? atomicAdd((unsigned long long*)(A.ctr + 1), (unsigned long long)m.clen) : 0;
-    if (m.elen + m.clen)
-      A.jobs[atomicAdd((unsigned long long*)(A.ctr + 5), 1ull)] = UJob{eb, cb, (u64)m.elen + m.clen, UJ_DEMOTE, lid};
+    if (m.elen + m.clen) jb.push(A, UJob{eb, cb, (u64)m.elen + m.clen, UJ_DEMOTE, lid});
     A.abase[k] = eb;
     A.cbs[k] = cb;
     asz = m.elen;
@@ -561,15 +583,25 @@ __device__ void uj_trim_column(const UjArgs& A, u64 k, u32 lid, u32 c) {
   LPlan& P = A.lplan[(u64)lid * A.R + c];
   if (!tagged(A, P.treq)) return;  // (uniform: every thread reads the same word)
   const LCol L = A.lcol[(u64)lid * A.R + c];
-  const u32 nb = L.elen < kTrimSpan ? L.elen : kTrimSpan;
+  const u32 span = (u32)P.treq;  // (the furthest element a removal can reach, +1)
+  const u32 nb = L.elen < span ? L.elen : span;
   const u64 vd = A.vvd[k * A.R + c];
   const u32 t = threadIdx.x;
   u64 keep = 0;
   if (t < nb) {
     const URec r = A.lpe[L.ebase + t];
     l_rec[t] = r;
-    const bool covered = dseq(r.dot) <= vd || in_dots(A.dcloud, A.dcoff[k], A.dcoff[k + 1], r.dot);
-    keep = !covered || in_dots(A.ddots, A.deoff[k], A.deoff[k + 1], r.dot);
+    const u64 x = r.dot;
+    // the delta's cloud (covered?) and elements (kept?), searched in lockstep
+    u64 clo = A.dcoff[k], chi = dseq(x) <= vd ? clo : A.dcoff[k + 1], dlo = A.deoff[k], dhi = A.deoff[k + 1];
+    while (clo < chi || dlo < dhi) {
+      const u64 cm = (clo + chi) >> 1, dm = (dlo + dhi) >> 1;
+      const u64 cv = clo < chi ? A.dcloud[cm] : 0, dv = dlo < dhi ? A.ddots[dm] : 0;
+      if (clo < chi) (cv < x ? clo = cm + 1 : chi = cm);
+      if (dlo < dhi) (dv < x ? dlo = dm + 1 : dhi = dm);
+    }
+    const bool covered = dseq(x) <= vd || (clo < A.dcoff[k + 1] && A.dcloud[clo] == x);
+    keep = !covered || (dlo < A.deoff[k + 1] && A.ddots[dlo] == x);
   }
   u64 kept;
   const u64 rank = jyscan::block_excl<kThreads, u64>(keep, l_red, kept);  // (syncs: l_rec is complete)
@@ -769,7 +801,8 @@ __global__ __launch_bounds__(kThreads) void k_uj_items(UjArgs A, u64 t_el, u64 t
   __shared__ Shared S;
   __shared__ u32 l_lid[kLdsDocs + 1];  // the tile's docs' long ids (~0u: regular)
   if (A.lcol && blockIdx.x == 0 && threadIdx.x == 0) {
-    A.ctr[6] = 0;  // the previous converge's promotions are done (stream order)
+    A.ctr[6] = 0;  // the previous converge's promotions and commits are done (stream order)
+    A.ctr[7] = 0;
   }
   u64 tt = blockIdx.x;
   const u64* offs;
@@ -846,7 +879,11 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt) {
   __shared__ u32 l_nlong;
   __shared__ u32 l_lq[kThreads], l_nlq;  // the tile's long documents (thread indices)
   __shared__ u64 l_sz[kThreads][2];
-  if (threadIdx.x == 0) l_nlong = l_nlq = 0;
+  __shared__ JobBuf l_jb;
+  __shared__ u64 l_jbase, l_fbase;
+  __shared__ u32 l_lw[kThreads][3];  // a long document's id and totals, for its wave
+  __shared__ u32 l_fq[kThreads], l_nfq;  // the tile's documents in place
+  if (threadIdx.x == 0) l_nlong = l_nlq = l_jb.n = l_nfq = 0;
   const u32 t = jyscan::ticket(A.tick + T_U1, &S.tk);
   if (t >= ndt) return;
   JY_CLK(c0);
@@ -879,17 +916,32 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt) {
     }
     // a bad doc (malformed: U1a; repeated) is skipped: nothing of it is touched
     if (is_bad(A, k)) asz = csz = 0;
-    else if (m.ecap == kLongMark && A.lcol) l_lq[atomicAdd(&l_nlq, 1u)] = threadIdx.x, lg = true;
+    else if (m.ecap == kLongMark && A.lcol) {
+      l_lq[atomicAdd(&l_nlq, 1u)] = threadIdx.x, lg = true;
+      l_lw[threadIdx.x][0] = (u32)m.ebase, l_lw[threadIdx.x][1] = m.elen, l_lw[threadIdx.x][2] = m.clen;
+    }
   }
   if (A.lcol) {  // the long documents, a wave each
     __syncthreads();
     for (u32 q = threadIdx.x >> 6; q < l_nlq; q += kThreads / 64) {
       const u32 i = l_lq[q];
       u64 a = 0, c = 0;
-      uj_docs_long(A, (u64)t * kDocTile + i, a, c);
-      if ((threadIdx.x & 63) == 0) l_sz[i][0] = a, l_sz[i][1] = c;
+      bool ip = false;
+      uj_docs_long(A, (u64)t * kDocTile + i, l_lw[i][0], l_lw[i][1], l_lw[i][2], a, c, l_jb, ip);
+      if ((threadIdx.x & 63) == 0) {
+        l_sz[i][0] = a, l_sz[i][1] = c;
+        if (ip) l_fq[atomicAdd(&l_nfq, 1u)] = (u32)((u64)t * kDocTile + i);
+      }
     }
     __syncthreads();
+    const u32 nj = min(l_jb.n, JobBuf::kCap), nfq = l_nfq;
+    if (nj || nfq) {  // one reservation per tile: the copy jobs, the documents in place
+      if (threadIdx.x == 0 && nj) l_jbase = atomicAdd((unsigned long long*)(A.ctr + 5), (unsigned long long)nj);
+      if (threadIdx.x == 64 && nfq) l_fbase = atomicAdd((unsigned long long*)(A.ctr + 7), (unsigned long long)nfq);
+      __syncthreads();
+      for (u32 q = threadIdx.x; q < nj; q += kThreads) A.jobs[l_jbase + q] = l_jb.j[q];
+      for (u32 q = threadIdx.x; q < nfq; q += kThreads) A.flist[l_fbase + q] = l_fq[q];
+    }
     if (lg) {
       asz = l_sz[threadIdx.x][0];
       csz = l_sz[threadIdx.x][1];
@@ -1467,47 +1519,62 @@ __device__ __forceinline__ ScOut scatter_prep(const UjArgs& A, int kind, u64 lt,
 // lengths (and the runs that grew, their new places), a cloud run that was
 // empty starts past its folded prefix, the vv takes the folds, the meta its
 // new totals
-__device__ void uj_commit_long(const UjArgs& A, u64 i) {
-  const u32 R = A.R, s = A.slot[i], lid = (u32)A.abase[i];
+// U5 for a delta doc converged in place, one WAVE per document (lane c =
+// column c): the column runs take their new lengths (and the runs that grew,
+// their new places; a trimmed run starts `cut` further up), a cloud run that
+// was empty starts past its folded prefix, the vv takes the folds, the meta
+// its new totals.  Lane 0 returns the in-place counters (jy_ujson_stats_ext).
+struct CommitStats {
+  u64 v[6];  // docs, their state elements / cloud dots, appended elements / cloud dots, folded
+};
+__device__ void uj_commit_long(const UjArgs& A, u64 i, CommitStats& cs) {
+  const u32 lane = threadIdx.x & 63, R = A.R, s = A.slot[i], lid = (u32)A.abase[i];
   const u64 b = (u64)lid * R;
-  u64 dE = 0, dC = 0, nfs = 0, app = 0;
-  for (u32 c = 0; c < R; c++) {
-    const LPlan& P = A.lplan[b + c];
-    const u64 efs = P.efs, ece = P.ece, cfs = P.cfs, cce = P.cce, nfw = P.nfold;
-    const u64 ne = tagged(A, efs) ? (u32)ece - (u32)efs : 0, nc = tagged(A, cfs) ? (u32)cce - (u32)cfs : 0;
-    const u64 tcw = P.tcut, cut = tagged(A, tcw) ? (u32)tcw : 0;
-    if (!ne && !nc && !cut) continue;
-    const u64 nf = tagged(A, nfw) ? (u32)nfw : 0;
-    const LCol L = A.lcol[b + c];
-    // (a trimmed run never moved: erun is its old start, now `cut` further up)
-    LCol N{P.erun + cut, (u32)(L.elen - cut + ne), (u32)(P.ecap - cut), P.crun, (u32)(L.clen + nc), P.ccap};
-    if (P.cz) {
-      N.clen = (u32)(nc - nf);
-      if (nf < nc) {
-        N.cbase = P.crun + nf;
-        N.ccap = (u32)(P.ccap - nf);
-      }
-    }
-    A.lcol[b + c] = N;
-    if (nf) A.vv[(u64)s * R + c] += nf;
-    dE += ne - cut;  // (mod 2^64: a trim may remove more than the delta adds)
-    app += ne;
-    dC += nc - nf;
-    nfs += nf;
-  }
   const UMeta m = A.meta[s];
-  A.meta[s] = UMeta{lid, (u32)(m.elen + dE), kLongMark, 0, (u32)(m.clen + dC), kLongMark};
-  unsigned long long* st = (unsigned long long*)A.stats;
-  atomicAdd(st + 8, 1ull);
-  atomicAdd(st + 9, (unsigned long long)m.elen);
-  atomicAdd(st + 10, (unsigned long long)m.clen);
-  atomicAdd(st + 11, (unsigned long long)app);
-  atomicAdd(st + 12, (unsigned long long)dC);
-  atomicAdd(st + 13, (unsigned long long)nfs);
+  u64 ne = 0, nc = 0, cut = 0, nf = 0;
+  if (lane < R) {
+    const LPlan& P = A.lplan[b + lane];
+    const u64 efs = P.efs, ece = P.ece, cfs = P.cfs, cce = P.cce, nfw = P.nfold, tcw = P.tcut;
+    ne = tagged(A, efs) ? (u32)ece - (u32)efs : 0;
+    nc = tagged(A, cfs) ? (u32)cce - (u32)cfs : 0;
+    cut = tagged(A, tcw) ? (u32)tcw : 0;
+    if (ne || nc || cut) {
+      nf = tagged(A, nfw) ? (u32)nfw : 0;
+      const LCol L = A.lcol[b + lane];
+      // (a trimmed run never moved: erun is its old start, now `cut` further up)
+      LCol N{P.erun + cut, (u32)(L.elen - cut + ne), (u32)(P.ecap - cut), P.crun, (u32)(L.clen + nc), P.ccap};
+      if (P.cz) {
+        N.clen = (u32)(nc - nf);
+        if (nf < nc) {
+          N.cbase = P.crun + nf;
+          N.ccap = (u32)(P.ccap - nf);
+        }
+      }
+      A.lcol[b + lane] = N;
+      if (nf) A.vv[(u64)s * R + lane] += nf;
+    }
+  }
+  const u64 app = jyscan::wave_sum<u64>(ne), cuts = jyscan::wave_sum<u64>(cut);
+  const u64 dC = jyscan::wave_sum<u64>(nc - nf), nfs = jyscan::wave_sum<u64>(nf);
+  if (lane == 0) {
+    A.meta[s] = UMeta{lid, (u32)(m.elen + app - cuts), kLongMark, 0, (u32)(m.clen + dC), kLongMark};
+    cs = CommitStats{{1, m.elen, m.clen, app, dC, nfs}};
+  }
+}
+
+// U5's document tiles: regular docs get their metas (and are listed for
+// promotion when they are long enough); docs in place are committed by the
+// commit tiles (a wave per document, flist)
+__device__ void uj_meta_tile(const UjArgs& A, u64 lt) {
+  const u64 eb0 = A.base[0], cb0 = A.base[1];
+  const u64 i = lt * kTile + threadIdx.x;
+  if (i >= A.nd || is_bad(A, i) || is_fast(A, i)) return;
+  const u32 ne = (u32)(A.neo[i + 1] - A.neo[i]), nc = (u32)(A.nco[i + 1] - A.nco[i]);
+  A.meta[A.slot[i]] = UMeta{eb0 + A.neo[i], ne, ne, cb0 + A.nco[i], nc, nc};
+  if (A.long_min && ne >= A.long_min) A.plist[atomicAdd((unsigned long long*)(A.ctr + 6), 1ull)] = (u32)i;
 }
 
 __device__ __forceinline__ void scatter_small(const UjArgs& A, int kind, u64 i) {
-  const u64 eb0 = A.base[0], cb0 = A.base[1];
   const u64 nv = A.nvv;
   if (kind == 4) {  // the delta's sparse vv entries into the state rows; the dense delta vv back to zero
     if (i >= nv) return;
@@ -1526,30 +1593,32 @@ __device__ __forceinline__ void scatter_small(const UjArgs& A, int kind, u64 i) 
     A.vvd[k * A.R + c] = 0;
     return;
   }
-  // kind 5: metas
-  if (i >= A.nd || is_bad(A, i)) return;
-  if (is_fast(A, i)) {
-    uj_commit_long(A, i);
-    return;
-  }
-  const u32 ne = (u32)(A.neo[i + 1] - A.neo[i]), nc = (u32)(A.nco[i + 1] - A.nco[i]);
-  A.meta[A.slot[i]] = UMeta{eb0 + A.neo[i], ne, ne, cb0 + A.nco[i], nc, nc};
-  if (A.long_min && ne >= A.long_min) A.plist[atomicAdd((unsigned long long*)(A.ctr + 6), 1ull)] = (u32)i;
 }
 
-__device__ __forceinline__ void uj_scatter_tile(const UjArgs& A, const u64 t) {
+__device__ __forceinline__ void uj_scatter_tile(const UjArgs& A, const u64 t, const u64 nfast) {
   const u64 ta = A.ao[A.nd], tc = A.co[A.nd];
   const ScanSp sp = sc_space(A), kp = ksc_space(A);
   const u32* xrb = A.xr + ta;
   const u32* krb = A.kr + tc;
   const u64 nv = A.nvv;
-  const u64 tl[6] = {cdiv(ta), cdiv(A.nb), cdiv(tc), cdiv(A.cb), cdiv(nv), cdiv(A.nd)};
+  constexpr u64 kWpT = kScatterThreads / 64;  // commit tiles: a wave per document in place
+  const u64 tl[7] = {cdiv(ta), cdiv(A.nb), cdiv(tc), cdiv(A.cb), cdiv(nv), cdiv(A.nd), (nfast + kWpT - 1) / kWpT};
   int kind = 0;
   u64 lt = t;
-  while (kind < 6 && lt >= tl[kind]) lt -= tl[kind++];
-  if (kind == 6) return;
+  while (kind < 7 && lt >= tl[kind]) lt -= tl[kind++];
+  if (kind == 7) return;
   JY_CLK(c0);
-  if (kind >= 4) {
+  if (kind == 6) {
+    const u64 q = lt * kWpT + (threadIdx.x >> 6);
+    CommitStats cs{};
+    if (q < nfast) uj_commit_long(A, A.flist[q], cs);
+    if ((threadIdx.x & 63) == 0 && cs.v[0]) {
+#pragma unroll
+      for (int x = 0; x < 6; x++) atomicAdd((unsigned long long*)(A.stats + 8 + x), (unsigned long long)cs.v[x]);
+    }
+  } else if (kind == 5) {
+    uj_meta_tile(A, lt);
+  } else if (kind == 4) {
 #pragma unroll
     for (int u = 0; u < kScatterU; u++) scatter_small(A, kind, lt * kTile + (u64)u * kScatterThreads + threadIdx.x);
   } else {
@@ -1574,8 +1643,10 @@ __device__ __forceinline__ void uj_scatter_tile(const UjArgs& A, const u64 t) {
 __global__ __launch_bounds__(kScatterThreads) void k_uj_scatter(UjArgs A) {
   if (blockIdx.x == 0 && threadIdx.x == 0)
     for (int c = T_U1; c <= T_U4; c++) A.tick[c] = 0;  // U1..U4 of this converge are done
-  const u64 T = cdiv(A.ao[A.nd]) + cdiv(A.nb) + cdiv(A.co[A.nd]) + cdiv(A.cb) + cdiv(A.nvv) + cdiv(A.nd);
-  for (u64 t = blockIdx.x; t < T; t += gridDim.x) uj_scatter_tile(A, t);
+  const u64 nf = A.lcol ? A.ctr[7] : 0;
+  const u64 T = cdiv(A.ao[A.nd]) + cdiv(A.nb) + cdiv(A.co[A.nd]) + cdiv(A.cb) + cdiv(A.nvv) + cdiv(A.nd) +
+                (nf + kScatterThreads / 64 - 1) / (kScatterThreads / 64);
+  for (u64 t = blockIdx.x; t < T; t += gridDim.x) uj_scatter_tile(A, t, nf);
 }
 
 // ---- P: promotion of the merged documents U5 listed (>= long_min elements):
@@ -2055,10 +2126,13 @@ int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* sl
   if (lng && u.jcap < u.dcap) {  // (contents never kept: a converge's jobs are its own)
     jy_dev_free(eng, u.jobs);
     jy_dev_free(eng, u.plist);
+    jy_dev_free(eng, u.flist);
     u.jobs = nullptr;
     u.plist = nullptr;
+    u.flist = nullptr;
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.jobs), 3 * u.dcap * sizeof(UJob), "ujson copy jobs"));
     JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.plist), u.dcap * 4, "ujson promotions"));
+    JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&u.flist), u.dcap * 4, "ujson docs in place"));
     u.jcap = u.dcap;
   }
 
@@ -2131,6 +2205,7 @@ int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* sl
     A.fast = u.fast;
     A.nf = u.nf;
     A.plist = u.plist;
+    A.flist = u.flist;
     A.long_min = keep_all ? 0 : u.long_min;
   }
   void* p;
@@ -2184,7 +2259,7 @@ int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* sl
   hipLaunchKernelGGL(k_uj_items, dim3((u32)std::max<u64>(1, t_el + t_cl + t_vv)), dim3(kThreads), 0, eng->stream, A,
                      t_el, t_cl, t_vv);
   hipLaunchKernelGGL(k_uj_docs, dim3((u32)ndt), dim3(kThreads), 0, eng->stream, A, ndt);
-  constexpr u32 kJobGrid = 256;
+  constexpr u32 kJobGrid = 1024;
   if (lng)
     hipLaunchKernelGGL(k_uj_jobs, dim3(kJobGrid), dim3(kThreads), 0, eng->stream, A, u.jobs, u.ctr + 5, 2 * u.jcap);
   // grids from the newest finished converge's touched sizes (+25 %), never above the safe bound

@@ -85,9 +85,12 @@ def _run_threads(node, hist):
     assert not errors, errors
 
 
-@pytest.mark.parametrize("S,fabric", [(1, "rccl"), (2, "copy")])
+@pytest.mark.parametrize("S,fabric", [(1, "rccl"), (2, "copy"), (8, "copy")])
 def test_five_types_share_one_node(oracle_mod, S, fabric):
-    """five threads (the five RepoManager actors) call one node at once"""
+    """five threads (the five RepoManager actors) call one node at once; S = 8
+    with the copy fabric is north_star's shard count on one GPU: every
+    regroup, count and payload column of the 8-way exchange (everything but
+    the RCCL calls, whose schedule tests/test_exchange_plan.py checks)"""
     from jylis_amd.node import Node
     O = oracle_mod
     hist = _histories(O, 500 + S)
