@@ -326,7 +326,7 @@ int32_t jy_ujson_stats_ext(jy_engine* eng, uint64_t* out16);
  * a delta whose dots all lie above what the document's column holds (the
  * usual case: fresh inserts) is appended where it lies instead of rewriting
  * the document.  0 stops promotions (documents already in the layout stay).
- * Default 128 (env JY_UJ_LONG_MIN); needs ujson_columns <= 64. */
+ * Default 512 (env JY_UJ_LONG_MIN); needs ujson_columns <= 64. */
 int32_t jy_ujson_set_inplace(jy_engine* eng, uint32_t min_elems);
 
 /* ---- multi-GPU routing: the exchange step of a key-hash-sharded node ----

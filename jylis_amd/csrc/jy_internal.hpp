@@ -382,10 +382,11 @@ struct alignas(16) LPlan {  // [lid][R]: one converge's plan for column c of a l
 };
 // a copy job of the in-place layout (k_uj_jobs), one per document: a
 // demotion (long column runs -> a regular run at e / c), the column runs of a
-// document in place that had to grow (-> LPlan erun / crun), a promotion (the
-// regular run at e / c -> the new long column runs)
+// document in place that had to grow (-> LPlan erun / crun), a trim (e = the
+// delta doc), a promotion too long for its wave to copy (the regular run at
+// e / c -> the new long column runs)
 struct alignas(16) UJob {
-  u64 e, c;  // the regular run's element / cloud base (demotion: destination, promotion: source)
+  u64 e, c;  // the regular run's element / cloud base (demotion: destination, promotion: source); regrowth, trim: e = the delta doc
   u64 n;     // items to copy (elements + cloud dots)
   u32 what;  // UJobWhat
   u32 lid;
@@ -452,8 +453,9 @@ struct UjsonState {  // per-document pool segments + dense vv
   u64* stats = nullptr;                // [16] cumulative converge counters (jy_ujson_stats[_ext])
   // in-place layout of long documents (LCol above).  ctr[2] / ctr[3]: long
   // pool bump pointers, ctr[4]: long ids handed out, ctr[5]: copy jobs of
-  // the converge's demotions and regrowths, ctr[6]: documents to promote (=
-  // their copy jobs).  pin[24 + 3 r ..]: ctr[2..4] as converge r saw them.
+  // the converge's demotions, regrowths and trims, ctr[6]: documents to
+  // promote, ctr[7]: documents in place.  pin[24 + 3 r ..]: ctr[2..4] as
+  // converge r saw them.
   bool allow_long = false;  // this store may promote (the state; never the pending deltas)
   u32 long_min = 0;         // promotion threshold in elements (0: none)
   URec* lpe = nullptr;      // long element pool
@@ -463,7 +465,7 @@ struct UjsonState {  // per-document pool segments + dense vv
   LCol* lcol = nullptr;     // [lcap][R]
   LPlan* lplan = nullptr;   // [lcap][R] (epoch tags: zeroed once)
   u64 lcap = 0;
-  UJob* jobs = nullptr;     // [3][jcap]: demotion / regrowth / trim jobs (two per delta doc at most), promotion jobs (one per plist entry)
+  UJob* jobs = nullptr;     // [3 jcap]: demotion / regrowth / trim jobs (two per delta doc at most), promotions (plist order)
   u64 jcap = 0;
   u32* fast = nullptr;      // [dcap] == epoch: the delta doc converges in place
   u32* nf = nullptr;        // [dcap] == epoch: a long doc whose delta is not append-shaped

@@ -1655,11 +1655,12 @@ __global__ __launch_bounds__(kScatterThreads) void k_uj_scatter(UjArgs A) {
 // pools (2n + 16 per column run), writes the column table and the copy jobs
 // (k_uj_jobs runs them next) and marks the meta long.  Optional: without
 // room the document simply stays regular.
+constexpr u64 kSelfCopy = 4096;  // entries a promoting wave copies itself
 __global__ __launch_bounds__(kThreads) void k_uj_promote(UjArgs A) {
   const u64 n = A.ctr[6];
+  UJob* jobs = A.jobs + 2 * A.jcap;  // the promotion region: job j <-> plist entry j (n = 0: copied here)
   const u32 lane = threadIdx.x & 63, R = A.R;
   const u64 W = (u64)gridDim.x * (kThreads / 64);
-  UJob* jobs = A.jobs + 2 * A.jcap;  // the promotion region: job j <-> plist entry j
   for (u64 j = (u64)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); j < n; j += W) {
     const u64 i = A.plist[j];
     const u32 s = A.slot[i];
@@ -1689,19 +1690,31 @@ __global__ __launch_bounds__(kThreads) void k_uj_promote(UjArgs A) {
       lid = atomicAdd((unsigned long long*)(A.ctr + 4), 1ull);
       eb = atomicAdd((unsigned long long*)(A.ctr + 2), (unsigned long long)TE);
       cb = atomicAdd((unsigned long long*)(A.ctr + 3), (unsigned long long)TC);
-      ok = j < A.jcap && lid < A.lcap && eb + TE <= A.lpe_cap && cb + TC <= A.lpc_cap;
+      ok = lid < A.lcap && eb + TE <= A.lpe_cap && cb + TC <= A.lpc_cap;
     }
     ok = __shfl(ok, 0);
     if (!ok) {
-      if (lane == 0 && j < A.jcap) jobs[j] = UJob{0, 0, 0, UJ_PROMOTE, 0};
+      if (lane == 0) jobs[j] = UJob{0, 0, 0, UJ_PROMOTE, 0};
       continue;
     }
     lid = __shfl(lid, 0);
     eb = __shfl(eb, 0);
     cb = __shfl(cb, 0);
     if (act) A.lcol[lid * R + lane] = LCol{eb + oe, (u32)ne, (u32)ecap, cb + oc, (u32)nc, (u32)ccap};
+    // the copy: a short document (the usual promotion: one the regular path
+    // just rewrote past the threshold) by this wave, column after column; a
+    // long one (a demoted hot document coming back) by the copy grid
+    const bool self = (u64)m.elen + m.clen <= kSelfCopy;
+    if (self) {
+      for (u32 c = 0; c < R; c++) {
+        const u64 e0c = __shfl(e0, (int)c), nec = __shfl(ne, (int)c), dstc = eb + __shfl(oe, (int)c);
+        for (u64 x = lane; x < nec; x += 64) A.lpe[dstc + x] = A.rec[m.ebase + e0c + x];
+        const u64 c0c = __shfl(c0, (int)c), ncc = __shfl(nc, (int)c), dcc = cb + __shfl(oc, (int)c);
+        for (u64 x = lane; x < ncc; x += 64) A.lpc[dcc + x] = A.cloud[m.cbase + c0c + x];
+      }
+    }
     if (lane == 0) {
-      jobs[j] = UJob{m.ebase, m.cbase, (u64)m.elen + m.clen, UJ_PROMOTE, (u32)lid};
+      jobs[j] = UJob{m.ebase, m.cbase, self ? 0 : (u64)m.elen + m.clen, UJ_PROMOTE, (u32)lid};
       A.meta[s] = UMeta{lid, m.elen, kLongMark, 0, m.clen, kLongMark};
       atomicAdd((unsigned long long*)(A.stats + 14), 1ull);
     }
@@ -2059,7 +2072,10 @@ int32_t ujson_grow_store(jy_engine* eng, UjsonState& u, u64 need, u64 init_cap) 
 // 0 disables the in-place layout); jy_ujson_set_inplace changes it
 u32 ujson_default_long_min() {
   if (const char* e = getenv("JY_UJ_LONG_MIN")) return (u32)strtoul(e, nullptr, 10);
-  return 128;
+  // (config 5, ms per converge at --warmup 2 / 6 / 20, one box: 128 ->
+  // 0.50 / 0.55 / 0.65, 512 -> 0.47 / 0.50 / 0.55; 32: 0.81 at warmup 6 --
+  // every promotion is a pass over its document, so only hot ones pay back)
+  return 512;
 }
 
 int32_t jy_ujson_grow(jy_engine* eng, u64 need) {
@@ -2275,7 +2291,7 @@ int32_t jy_ujson_merge_into(jy_engine* eng, UjsonState& u, u64 nd, const u32* sl
   const u64 g5 = gf + gk + (nvv + kTile - 1) / kTile + (nd + kTile - 1) / kTile + 2;
   hipLaunchKernelGGL(k_uj_scatter, dim3((u32)g5), dim3(kScatterThreads), 0, eng->stream, A);
   if (lng && A.long_min) {
-    hipLaunchKernelGGL(k_uj_promote, dim3(64), dim3(kThreads), 0, eng->stream, A);
+    hipLaunchKernelGGL(k_uj_promote, dim3(256), dim3(kThreads), 0, eng->stream, A);
     hipLaunchKernelGGL(k_uj_jobs, dim3(kJobGrid), dim3(kThreads), 0, eng->stream, A, u.jobs + 2 * u.jcap, u.ctr + 6,
                        u.jcap);
   }

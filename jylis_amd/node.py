@@ -244,19 +244,27 @@ class Node:
                                np.asarray(t["ts"], np.uint64), np.asarray(t["val_bytes"], np.uint8),
                                np.asarray(t["val_offs"], np.uint64))
         elif ctype == UJSON:
-            def packed(ids, seqs, offs, *payload):
-                ids = np.asarray(ids, np.uint64)
-                seqs = np.asarray(seqs, np.uint64)
-                if len(seqs) and (seqs >> np.uint64(DOT_SEQ_BITS)).any():
-                    raise ValueError("dot sequence numbers must stay below 2^48")
-                cols = self.replica_cols(ids.tolist()).astype(np.uint64) if len(ids) else np.zeros(0, np.uint64)
-                p = pack_dot(cols, seqs)
-                order = np.lexsort((p, _seg_ids(offs)))  # ascending dots per document
-                return (p[order],) + tuple(np.asarray(x, np.uint64)[order] for x in payload)
-            eo, vo, co = (np.asarray(t[k], np.uint64) for k in ("el_offs", "vv_offs", "cloud_offs"))
-            dots, elems = packed(t["dot_ids"], t["dot_seqs"], eo, t["elems"])
-            (vv,) = packed(t["vv_ids"], t["vv_seqs"], vo)
-            (cloud,) = packed(t["cloud_ids"], t["cloud_seqs"], co)
-            self.ujson_converge(kb, ko, eo, dots, elems, vo, vv, co, cloud)
+            self.ujson_converge(*self.ujson_args(t))
         else:
             raise ValueError(f"unknown CRDT type {ctype}")
+
+    def ujson_args(self, t):
+        """a UJSON batch table -> the node call's arrays (key bytes, key offsets,
+        element offsets, dots, elements, vv offsets, vv, cloud offsets, cloud):
+        replica ids to node columns, every document's dots ascending"""
+        def packed(ids, seqs, offs, *payload):
+            ids = np.asarray(ids, np.uint64)
+            seqs = np.asarray(seqs, np.uint64)
+            if len(seqs) and (seqs >> np.uint64(DOT_SEQ_BITS)).any():
+                raise ValueError("dot sequence numbers must stay below 2^48")
+            cols = self.replica_cols(ids.tolist()).astype(np.uint64) if len(ids) else np.zeros(0, np.uint64)
+            p = pack_dot(cols, seqs)
+            order = np.lexsort((p, _seg_ids(offs)))  # ascending dots per document
+            return (p[order],) + tuple(np.asarray(x, np.uint64)[order] for x in payload)
+        kb = np.ascontiguousarray(t["key_bytes"], np.uint8)
+        ko = np.ascontiguousarray(t["key_offs"], np.uint64)
+        eo, vo, co = (np.asarray(t[k], np.uint64) for k in ("el_offs", "vv_offs", "cloud_offs"))
+        dots, elems = packed(t["dot_ids"], t["dot_seqs"], eo, t["elems"])
+        (vv,) = packed(t["vv_ids"], t["vv_seqs"], vo)
+        (cloud,) = packed(t["cloud_ids"], t["cloud_seqs"], co)
+        return kb, ko, eo, dots, elems, vo, vv, co, cloud

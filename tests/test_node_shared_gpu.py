@@ -149,19 +149,28 @@ def test_typed_lock_does_not_wait_for_other_types(oracle_mod):
     the TREG jobs queued before it are done, while UJSON converges queued
     after them are still waiting; the full lock waits for every job.  Both
     states equal the oracle's."""
+    import torch
     from jylis_amd import synth as S
     from jylis_amd.node import Node
     from jylis_amd.repo import REPOS
     O = oracle_mod
     node = Node(1, "rccl")
+
+    def dev(a):
+        a = np.ascontiguousarray(a)
+        return torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a).to("cuda:0")
     try:
         tr = random_history(O, O.TREG, seed=93, nops=120, nkeys=40)
-        st0, dl = S.ujson_tables(30000, seed=S.BASE_SEED + 77, rounds=12, R=16)
-        uj = [st0] + dl
+        st0, dl = S.ujson_tables(200000, seed=S.BASE_SEED + 77, rounds=1, R=16)
+        uj = [st0] + dl * 10  # (re-delivered deltas: idempotent)
+        args = [[dev(a) for a in node.ujson_args(b)] for b in (st0, dl[0])]
         for b in tr:
             node.converge_table(O.TREG, b)
-        for b in uj:
-            node.converge_table(O.UJSON, b)
+        # device inputs: the calls only enqueue (no pinned staging to wait
+        # for), so the UJSON jobs queue up behind the TREG ones
+        node.ujson_converge(*args[0])
+        for _ in range(10):
+            node.ujson_converge(*args[1])
         with node.locked(O.TREG):
             waiting = node.pending(O.UJSON)
             got = join_rows(O.TREG, dict(split_rows(O.TREG, REPOS[O.TREG](node.engines[0]).state())))
