@@ -340,6 +340,7 @@ void jy_engine_destroy(jy_engine* eng) {
   for (TlogState* t : {&eng->tlog, &eng->tlog_d}) {
     F(t->meta);
     F(t->hint);
+    F(t->hist);
     F(t->pool);
     F(t->ctr);
     if (t->pin) hipHostFree(t->pin);

@@ -28,16 +28,17 @@ typedef uint16_t u16;
 // prefix = first 8 bytes big-endian zero-padded, so unsigned prefix order is
 // bytewise order of the first min(8, len) bytes up to zero padding; the
 // arena holds the whole value when len > 8.
-__device__ __forceinline__ int jy_value_cmp(u64 pa, u64 la, u64 pb, u64 lb, const uint8_t* __restrict__ arena) {
-  if (pa != pb) return pa < pb ? -1 : 1;
+// (the arena bytes from `from` on, both values longer than `from`: equal
+// before it)
+__device__ __forceinline__ int jy_value_cmp_tail(u64 la, u64 lb, const uint8_t* __restrict__ arena, u64 from) {
   const u64 na = la & JY_LR_LEN_MASK, nb = lb & JY_LR_LEN_MASK;
-  if (na > 8 && nb > 8) {
+  {
     const uint8_t* a = arena + (la >> JY_LR_LEN_BITS);
     const uint8_t* b = arena + (lb >> JY_LR_LEN_BITS);
     const u64 n = na < nb ? na : nb;
     // 8 bytes per step, all 16 loads of a step issued together (one memory
     // round trip per step instead of one per byte); bytes past n read as 0
-    for (u64 i = 8; i < n; i += 8) {
+    for (u64 i = from; i < n; i += 8) {
       u64 wa = 0, wb = 0;
 #pragma unroll
       for (int q = 0; q < 8; q++) {
@@ -49,8 +50,39 @@ __device__ __forceinline__ int jy_value_cmp(u64 pa, u64 la, u64 pb, u64 lb, cons
       if (wa != wb) return wa < wb ? -1 : 1;
     }
   }
-  // equal prefix and (one side <= 8 bytes, or equal common bytes):
-  // the shorter one is a prefix of the other
+  // equal common bytes: the shorter one is a prefix of the other
+  if (na == nb) return 0;
+  return na < nb ? -1 : 1;
+}
+__device__ __forceinline__ int jy_value_cmp(u64 pa, u64 la, u64 pb, u64 lb, const uint8_t* __restrict__ arena) {
+  if (pa != pb) return pa < pb ? -1 : 1;
+  const u64 na = la & JY_LR_LEN_MASK, nb = lb & JY_LR_LEN_MASK;
+  if (na > 8 && nb > 8) return jy_value_cmp_tail(la, lb, arena, 8);
+  // equal prefix, one side <= 8 bytes: the shorter one is a prefix of the other
+  if (na == nb) return 0;
+  return na < nb ? -1 : 1;
+}
+
+// a value's second word: bytes 8..15 big-endian, zero-padded (0 for values
+// of up to 8 bytes).  Values over 8 bytes start on 8-byte arena granules, so
+// this is one aligned load inside the value's own granules.
+__device__ __forceinline__ u64 jy_value_w2(u64 lr, const uint8_t* __restrict__ arena) {
+  const u64 n = lr & JY_LR_LEN_MASK;
+  if (n <= 8) return 0;
+  u64 w = *reinterpret_cast<const u64*>(arena + (lr >> JY_LR_LEN_BITS) + 8);
+  if (n < 16) w &= (1ull << (8 * (n - 8))) - 1;
+  return __builtin_bswap64(w);
+}
+// the same order with both values' second words at hand (TLOG records
+// carry theirs): values of up to 16 bytes never touch the arena
+__device__ __forceinline__ int jy_value_cmp_w(u64 pa, u64 wa, u64 la, u64 pb, u64 wb, u64 lb,
+                                              const uint8_t* __restrict__ arena) {
+  if (pa != pb) return pa < pb ? -1 : 1;
+  const u64 na = la & JY_LR_LEN_MASK, nb = lb & JY_LR_LEN_MASK;
+  if (na > 8 && nb > 8) {
+    if (wa != wb) return wa < wb ? -1 : 1;
+    if (na > 16 && nb > 16) return jy_value_cmp_tail(la, lb, arena, 16);
+  }
   if (na == nb) return 0;
   return na < nb ? -1 : 1;
 }
@@ -284,7 +316,8 @@ struct TregState {  // per slot: ts u64 (read by every merge) + TVal (written by
 };
 
 // one TLOG entry: 32 B so a lane moves it with two 16-B accesses and an
-// entry write is one whole 32-B sector
+// entry write is one whole 32-B sector; `pad` holds the value's bytes 8..15
+// (jy_value_w2), so values of up to 16 bytes compare without the arena
 struct alignas(16) TRec {
   u64 ts, pre, lr;
   u64 pad;
@@ -292,14 +325,26 @@ struct alignas(16) TRec {
 
 // per log: a segment of the entry pool, entries OLDEST FIRST (ascending
 // (ts, value)), so the usual delta -- entries newer than the whole log --
-// is an append at the tail; a raised cutoff drops a prefix (base moves up)
+// is an append at the tail; a raised cutoff drops a prefix (base moves up).
+// The segment also keeps FRONT ROOM: free pool entries just below base (a
+// rebuild or compaction leaves some, a cutoff drop adds the dropped prefix),
+// so an entry inserted near the oldest end moves the short prefix down instead
+// of the whole rest of the log up (k_tlog.hip stage 5).
 struct alignas(16) TMeta {
-  u64 base;     // pool index of the oldest live entry
+  u64 bf;       // base | front << kBaseBits: pool index of the oldest live entry, front room (saturating)
   u32 len;      // live entries
   u32 cap;      // pool entries reserved from base
   u64 cut;      // cutoff
   u64 newest;   // ts of the newest entry (any value when len == 0)
 };
+constexpr int kBaseBits = 40;  // 2^40 pool entries (32 TB): never the bound
+constexpr u64 kBaseMask = (1ull << kBaseBits) - 1;
+constexpr u64 kFrontMax = (1ull << (64 - kBaseBits)) - 1;
+__host__ __device__ __forceinline__ u64 tm_base(const TMeta& m) { return m.bf & kBaseMask; }
+__host__ __device__ __forceinline__ u64 tm_front(const TMeta& m) { return m.bf >> kBaseBits; }
+__host__ __device__ __forceinline__ u64 tm_bf(u64 base, u64 front) {
+  return base | ((front < kFrontMax ? front : kFrontMax) << kBaseBits);
+}
 
 struct TlogState {  // per-slot segments of one entry pool
   TMeta* meta = nullptr;  // [kcap]
@@ -307,6 +352,11 @@ struct TlogState {  // per-slot segments of one entry pool
   // interpolated searches (k_tlog_tile): kept by the merges that know it, never
   // needed for correctness (a stale hint only costs the search a fallback)
   u64* hint = nullptr;
+  // [kcap] each log's update history: epoch << 32 | its length when its
+  // segment was last made (a rebuild); 0 = none yet.  Sizes the next segment
+  // (k_tlog.hip seg_cap): a log that filled its room fast gets room for
+  // kHorizon more merges at the rate it grew
+  u64* hist = nullptr;
   TRec* pool = nullptr;   // [pcap]
   u64 pcap = 0;
   u64* ctr = nullptr;     // device: [0] pool entries handed out (bump pointer)

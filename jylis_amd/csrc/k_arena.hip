@@ -63,7 +63,8 @@ __global__ __launch_bounds__(kThreads) void k_arena_tlog(const TMeta* __restrict
   const u64 s = gid();
   if (s >= n) return;
   const TMeta m = meta[s];
-  for (u64 j = m.base; j < m.base + m.len; j++) {
+  const u64 b = tm_base(m);
+  for (u64 j = b; j < b + m.len; j++) {
     if (kRewrite) pool[j].lr = moved(pool[j].lr, goff);
     else mark(pool[j].lr, glen);
   }

@@ -6,10 +6,13 @@
 //              the later timestamp first, then the greater value first
 //              (Pony String order); (ts, value) duplicates collapse.
 //
-// HBM layout: one entry pool of 32-B records {ts, pre, lr, pad} (value
-// handle as in TREG: 8-byte big-endian prefix + arena offset/length) and a
-// 32-B TMeta per slot {base, len, cap, cutoff, newest}.  A log is the pool
-// segment [base, base + len), stored OLDEST FIRST, with room up to cap.
+// HBM layout: one entry pool of 32-B records {ts, pre, lr, w2} (value
+// handle as in TREG: 8-byte big-endian prefix + arena offset/length, and
+// since round 6 the value's second 8 bytes, so comparing values of up to 16
+// bytes -- a duplicate, a timestamp tie -- never reads the arena) and a
+// 32-B TMeta per slot {base | front room, len, cap, cutoff, newest}.  A log is
+// the pool segment [base, base + len), stored OLDEST FIRST, with room up to
+// cap and `front` free entries below base.
 // Reads reverse it into the reference's newest-first order.
 //
 // Why this layout: a peer's delta is almost always entries newer than the
@@ -19,7 +22,11 @@
 // cutoff drops a prefix: base moves up, nothing is copied.  Only a key whose
 // delta interleaves with its log (an older entry, a timestamp tie) or whose
 // segment is full is REBUILT into fresh pool space (bump allocation,
-// capacity rounded to a power of two) by a merge of the two sorted runs.
+// capacity rounded to a power of two) by a merge of the two sorted runs;
+// one that interleaves but fits is rewritten in place, moving the shorter
+// side of the log: the suffix up into the tail room, or the prefix down into
+// the front room (round 6: an entry inserted near the oldest end no longer
+// moves the whole log).
 // The pool is compacted (every log rewritten back to back) when its free
 // space cannot cover the worst case of the next merge.
 //
@@ -53,6 +60,8 @@
 
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "jy_dscan.hpp"
@@ -78,13 +87,22 @@ __device__ __forceinline__ int cmp_at(const TRec* __restrict__ pool, u64 m, cons
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ void store_rec(TRec* __restrict__ p, u64 ts, u64 pre, u64 lr) {
+// JY_TLOG_W2 (A/B): records carry the value's second word (1) or 0 (0: a
+// tie compares through the arena)
+#ifndef JY_TLOG_W2
+#define JY_TLOG_W2 0
+#endif
+__device__ __forceinline__ u64 rec_w2(u64 lr, const uint8_t* __restrict__ arena) {
+  return JY_TLOG_W2 ? jy_value_w2(lr, arena) : 0ull;
+}
+
+__device__ __forceinline__ void store_rec(TRec* __restrict__ p, u64 ts, u64 pre, u64 lr, u64 w2) {
   u64x2* q = reinterpret_cast<u64x2*>(p);
   u64x2 a, b;
   a.x = ts;
   a.y = pre;
   b.x = lr;
-  b.y = 0;
+  b.y = w2;
   __builtin_nontemporal_store(a, q);
   __builtin_nontemporal_store(b, q + 1);
 }
@@ -100,7 +118,10 @@ __device__ __forceinline__ TRec load_rec(const TRec* __restrict__ p) {
   return r;
 }
 
-enum : u32 { kSkip = 0, kAppend = 1, kRebuild = 2, kFast = 3, kInsert = 4 };
+// kInsert moves the log's suffix from the smallest inserted rank up into the
+// tail room; kInsertDn moves its prefix below the largest inserted rank down
+// into the front room (an entry inserted near the oldest end)
+enum : u32 { kSkip = 0, kAppend = 1, kRebuild = 2, kFast = 3, kInsert = 4, kInsertDn = 5 };
 
 // per REBUILT key: what k_tlog_tile decided; the log's current base is read
 // from its meta at commit
@@ -118,6 +139,7 @@ struct alignas(16) PInfo {
 struct TlogArgs {
   TMeta* meta;
   u64* hint;  // [nkeys] oldest-timestamp hints (TlogState::hint)
+  u64* hist;  // [nkeys] update histories (TlogState::hist)
   const TRec* pool;
   const uint8_t* arena;
   // delta batch
@@ -163,39 +185,58 @@ __global__ __launch_bounds__(kThreads) void k_tlog_prep(TlogArgs A) {
   }
 }
 
-// first position in [lo, hi) of a log whose timestamps ascend from `tlo`
-// (at lo) to `thi` (at hi - 1) with timestamp >= x.  Timestamps follow wall
-// time, so an interpolated guess and one window of kWin entries around it
-// (loaded at once: one round trip, ~2 cache lines) usually settle it; else
-// a binary search of the side the window ruled out
-// window entries (in-box A/B, round 4, ms per config-4 converge: 8 -> 0.837-
-// 0.840, 4 -> 0.828-0.830, 3 -> 0.830, 2 -> 0.826-0.827; 12 was slower still
-// than 8 on another box): the interpolated guess is close enough that fewer
-// lines per probe win
-#ifndef JY_TLOG_WIN
-#define JY_TLOG_WIN 2
-#endif
-constexpr u32 kWin = JY_TLOG_WIN;
+// first position in [lo, hi) of a log whose timestamps ascend, with
+// timestamp >= x (hi if none); tlo < x is a lower bound of the timestamps
+// before lo, thi >= x an upper bound from hi - 1 on (the log's oldest and
+// newest timestamps to start with).  Timestamps follow wall time, so an
+// interpolated guess usually lands close: each round loads the ALIGNED
+// 128-B line of records around it (kWin = 4 timestamps for one line), which
+// either brackets x or narrows [lo, hi) to one side of the line, the next
+// guess interpolating between the timestamps just read; a range of at most
+// kWin entries is settled by one load of all of it.  Round 6: kWin 2
+// unaligned (two lines half the time) and a binary search after the first
+// miss took ~5 dependent probes per search at config 4 (the searches were
+// ~55% of a key tile's lifetime, profiles/r06_tlog_tile_probe.txt).
+constexpr u32 kWin = 4;
+constexpr int kInterpRounds = 3;
 __device__ __forceinline__ u32 ts_interp(const TRec* __restrict__ pool, u64 base, u32 lo, u32 hi, u64 tlo, u64 thi,
                                          u64 x) {
-  if (hi - lo > kWin && x > tlo && x <= thi && thi > tlo) {
-    const double f = (double)(x - tlo) / (double)(thi - tlo);
-    u32 g = lo + (u32)(f * (double)(hi - 1 - lo));
-    g = g >= lo + kWin / 2 ? g - kWin / 2 : lo;
-    if (g > hi - kWin) g = hi - kWin;
+#pragma unroll 1
+  for (int it = 0; it < kInterpRounds; it++) {
+    if (hi - lo <= kWin) {  // all of it at once
+      u64 w[kWin];
+#pragma unroll
+      for (u32 i = 0; i < kWin; i++) w[i] = lo + i < hi ? pool[base + lo + i].ts : ~0ull;
+      u32 c = 0;
+#pragma unroll
+      for (u32 i = 0; i < kWin; i++) c += w[i] < x;
+      return lo + c;
+    }
+    u64 g;
+    if (x > tlo && x <= thi && thi > tlo) {
+      const double f = (double)(x - tlo) / (double)(thi - tlo);
+      g = lo + (u64)(f * (double)(hi - 1 - lo));
+    } else {
+      g = lo + ((hi - lo) >> 1);
+    }
+    u64 ga = ((base + g) & ~(u64)(kWin - 1)) - base;  // the line holding the guess
+    if (ga < lo) ga = lo;
+    if (ga > hi - kWin) ga = hi - kWin;
     u64 w[kWin];
 #pragma unroll
-    for (u32 i = 0; i < kWin; i++) w[i] = pool[base + g + i].ts;
+    for (u32 i = 0; i < kWin; i++) w[i] = pool[base + ga + i].ts;
     u32 c = 0;
 #pragma unroll
     for (u32 i = 0; i < kWin; i++) c += w[i] < x;
     if (c == 0) {
-      if (g == lo) return lo;
-      hi = g;  // the answer is at or before g
+      if (ga == lo) return lo;
+      hi = (u32)ga;  // at or before ga
+      thi = w[0];
     } else if (c == kWin) {
-      lo = g + kWin;  // after the window
+      lo = (u32)ga + kWin;  // after the line
+      tlo = w[kWin - 1];
     } else {
-      return g + c;
+      return (u32)ga + c;
     }
   }
   while (lo < hi) {
@@ -206,15 +247,33 @@ __device__ __forceinline__ u32 ts_interp(const TRec* __restrict__ pool, u64 base
   return lo;
 }
 
-// capacity of a rebuilt segment: room to grow 4x by appends, power of two
-// (HBM is plentiful; every rebuild copies the whole log, so they should be rare)
+// capacity of a rebuilt segment, a power of two: room to grow 4x by appends
+// (HBM is plentiful; every rebuild copies the whole log, so they should be
+// rare) -- and, driven by the log's update history, room for kHorizon more
+// merges at the rate it grew since its last segment was made: a short log
+// that is appended to on every merge would otherwise be rebuilt again within
+// a few merges (round 6)
 constexpr u64 kGrow = 4;
-__device__ __forceinline__ u32 pow2_cap(u32 n) {
-  const u64 want = kGrow * (u64)n + kGrow;
+constexpr u64 kHorizon = 16;
+__device__ __forceinline__ u64 hist_room(u64 h, u32 n, u32 epoch) {
+  if (h == 0) return 0;  // no history yet
+  const u32 age = epoch - (u32)h, n0 = (u32)(h >> 32);
+  if (age == 0 || age > 1024 || n <= n0) return 0;
+  return ((u64)(n - n0) * kHorizon + age - 1) / age;
+}
+__device__ __forceinline__ u32 pow2_cap(u32 n, u64 room = 0) {
+  u64 want = kGrow * (u64)n + kGrow;
+  if ((u64)n + room > want) want = (u64)n + room;
   u64 c = 4;
   while (c < want) c <<= 1;
   return c > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)c;
 }
+
+// front room of a rebuilt segment (cap entries for n): an eighth of its free
+// room, for entries inserted near the log's oldest end (stage 5, kInsertDn)
+__device__ __forceinline__ u32 rebuild_front(u32 cap, u32 n) { return (cap - n) / 8; }
+// and of a compacted one
+__device__ __forceinline__ u32 cmp_front(u32 n) { return n ? n / 8 + 2 : 0; }
 
 // last idx in [0, n] with a[idx] <= x (a non-decreasing, a[0] <= x)
 template <class T>
@@ -238,6 +297,19 @@ constexpr int kFastEnt = 4;  // delta entries a key may have for the lane-per-ke
 // / 0.841 ms without, 0.865 with at 6 waves per SIMD (spills), 0.834 / 0.836
 // at 5 waves; removed)
 constexpr int kCache = JY_TLOG_KCACHE;  // passes of slow entries kept in registers for the append stores
+
+#ifdef JY_TLOG_PROBE  // A/B only: per-stage wall-clock latency of the key tiles (100 MHz), summed
+constexpr int kProbeSlots = 64, kProbeN = 16;
+__device__ unsigned long long g_tprobe[kProbeSlots][kProbeN];
+#define JY_TCLK(v) const u64 v = wall_clock64()
+#define JY_TCLKV(v) v = wall_clock64()
+#define JY_TPROBE(i, v) \
+  if (threadIdx.x == 0) atomicAdd(&g_tprobe[blockIdx.x % kProbeSlots][i], (unsigned long long)(v))
+#else
+#define JY_TCLK(v)
+#define JY_TCLKV(v)
+#define JY_TPROBE(i, v)
+#endif
 
 constexpr u32 kKept = 0x80000000u;  // eqx: kept flag | # kept entries of the key before this one
 
@@ -276,13 +348,16 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
   __shared__ u64 l_base[kTile], l_newest[kTile], l_cut[kTile], l_tn[kTile], l_to[kTile];
   __shared__ u32 l_len[kTile], l_cap[kTile], l_drop[kTile], l_M[kTile], l_minrank[kTile], l_bad[kTile],
       l_gstart[kTile], l_mode[kTile];
+  __shared__ u32 l_Mi[kTile], l_mx[kTile];  // kept entries inside the log (rank < len), their largest rank
   const u32 tid = threadIdx.x;
   const u64 lanelt = (1ull << tid) - 1;
   const u64 k0 = (u64)blockIdx.x * kTile;
   const u32 nt = (u32)(A.nd - k0 < kTile ? A.nd - k0 : kTile);
+  JY_TCLK(ck0);
   const u64 gb0 = A.doff[k0];  // the tile's first delta entry
   // 1. keys
-  u64 sc = 0;  // slow entries of this lane's key
+  u64 sc = 0;      // slow entries of this lane's key
+  u32 front = 0;   // its front room (stage 3 is this lane's again)
   if (tid < nt) {
     const u64 k = k0 + tid;
     const u32 s = A.slot[k];
@@ -300,6 +375,7 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
     }
     const bool hole = s == JY_NO_SLOT;  // a routed run's unused record: skipped, not counted
     const TMeta m = hole ? TMeta{0, 0, 0, 0, 0} : A.meta[s];
+    const u64 mb = tm_base(m);
     const u64 hv = hole ? 0 : A.hint[s];  // with the meta: no dependent load of the log's first record
     const u64 cd = A.dcut[k];
     const u32 bad = hole ? 4u : (A.bad[k] == A.epoch ? 1u : 0u);
@@ -319,8 +395,9 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
     if (fast) {
 #pragma unroll
       for (int u = 0; u < kFastEnt; u++)
-        if ((u32)u < M) store_rec(pool + m.base + m.len + (M - 1 - u), ft[u], fp[u], fl[u]);
-      if (M) A.meta[s] = TMeta{m.base, m.len + M, m.cap, m.cut, (m.len == 0 || ft[0] > m.newest) ? ft[0] : m.newest};
+        if ((u32)u < M)
+          store_rec(pool + mb + m.len + (M - 1 - u), ft[u], fp[u], fl[u], rec_w2(fl[u], A.arena));
+      if (M) A.meta[s] = TMeta{m.bf, m.len + M, m.cap, m.cut, (m.len == 0 || ft[0] > m.newest) ? ft[0] : m.newest};
       if (M && m.len == 0) {  // an empty log's oldest entry: the oldest appended one (kept entries are a prefix)
         u64 o = ft[0];
 #pragma unroll
@@ -335,14 +412,15 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
         // the interpolated search from the hint (one window of 1-2 lines; the
         // 16-ary probes read 16 lines a round), then the new oldest entry --
         // inside the window, a cache hit
-        drop = ts_interp(A.pool, m.base, 0, m.len, hv, m.newest, cut);  // oldest first: a prefix
-        oldest = drop < m.len ? A.pool[m.base + drop].ts : 0;
+        drop = ts_interp(A.pool, mb, 0, m.len, hv, m.newest, cut);  // oldest first: a prefix
+        oldest = drop < m.len ? A.pool[mb + drop].ts : 0;
       } else if (m.len > 0) {
         oldest = hv;  // the hint (round 3 loaded pool[base].ts here: one dependent random line per slow key)
       }
       l_oldest[tid] = oldest;  // for the interpolated searches
       sc = hole ? 0 : ne;  // a hole's entries (a spill's unspilled keys) are never walked
-      l_base[tid] = m.base;
+      l_base[tid] = mb;
+      front = (u32)tm_front(m);
       l_newest[tid] = m.newest;
       l_cut[tid] = cut;
       l_len[tid] = m.len;
@@ -350,6 +428,8 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
       l_drop[tid] = drop;
       l_bad[tid] = bad;
       l_M[tid] = 0;
+      l_Mi[tid] = 0;
+      l_mx[tid] = 0;
       l_minrank[tid] = 0xFFFFFFFFu;
       l_tn[tid] = 0;
       l_to[tid] = ~0ull;
@@ -366,6 +446,10 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
   }
   __syncthreads();
   const u64 F = l_soff[nt];
+  JY_TCLK(ck1);
+#ifdef JY_TLOG_PROBE
+  u64 pl = 0, ps = 0, pe = 0, pa = 0, pb = 0;
+#endif
   // 2. slow entries, one per lane per pass
   u32 carry = 0;
   constexpr int kCacheN = kCache > 0 ? kCache : 1;
@@ -375,6 +459,9 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
   for (int c = 0; c < kCache; c++) c_q[c] = c_i[c] = 0, c_t[c] = c_p[c] = c_l[c] = 0;
   int pass = 0;
   for (u64 c0 = 0; c0 < F; c0 += kTile, pass++) {
+#ifdef JY_TLOG_PROBE
+    const u64 pst = wall_clock64();
+#endif
     const u64 f = c0 + tid;
     u32 idx = 0, flag = 0, rank = 0, lo = 0, hi = 0;
     u64 t = 0, pp = 0, ll = 0, j = 0;
@@ -400,23 +487,34 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
         }
       }
     }
+#ifdef JY_TLOG_PROBE
+    __builtin_amdgcn_s_waitcnt(0);
+    JY_TCLKV(pa);
+    pl += pa - pst;
+#endif
     if (flag == 2) {
       // the first log entry not older than x: a binary search of the
       // timestamps (16-ary probes read ~2x the lines: measured slower), then
       // the values of the (usually 0 or 1) entries with x's timestamp
       const u64 base = l_base[idx];
+      const u64 w = rec_w2(ll, A.arena);  // issued before the search: in flight with it
       const u32 r = ts_interp(A.pool, base, lo, hi, l_oldest[idx], l_newest[idx], t);
       int c = 1;
       u32 e = r;
       for (; e < hi; e++) {
         const TRec y = A.pool[base + e];
         if (y.ts != t) break;
-        c = jy_value_cmp(y.pre, y.lr, pp, ll, A.arena);
+        c = JY_TLOG_W2 ? jy_value_cmp_w(y.pre, y.pad, y.lr, pp, w, ll, A.arena)
+                       : jy_value_cmp(y.pre, y.lr, pp, ll, A.arena);
         if (c >= 0) break;
       }
       rank = e;
       flag = c != 0;  // c == 0: a duplicate of entry e
     }
+#ifdef JY_TLOG_PROBE
+    JY_TCLKV(pb);
+    ps += pb - pa;
+#endif
     // kept ranks in entry order (a wave ballot per pass)
     const u64 mask = __ballot(flag != 0);
     const u32 g = carry + (u32)__popcll(mask & lanelt);
@@ -433,6 +531,10 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
         atomicMin(&l_minrank[idx], rank);
         atomicMax((unsigned long long*)&l_tn[idx], (unsigned long long)t);  // newest kept
         atomicMin((unsigned long long*)&l_to[idx], (unsigned long long)t);  // oldest kept (the hint)
+        if (rank < l_len[idx]) {
+          atomicAdd(&l_Mi[idx], 1u);
+          atomicMax(&l_mx[idx], rank);
+        }
       }
     }
 #pragma unroll
@@ -441,7 +543,16 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
         c_t[c] = t, c_p[c] = pp, c_l[c] = ll, c_q[c] = qx, c_i[c] = idx;
       }
     __syncthreads();  // l_gstart reuse
+#ifdef JY_TLOG_PROBE
+    __builtin_amdgcn_s_waitcnt(0);
+    {
+      u64 pc;
+      JY_TCLKV(pc);
+      pe += pc - pb;
+    }
+#endif
   }
+  JY_TCLK(ck2);
   // 3. per slow key: append (meta published here), rebuild (planned) or skip
   u32 mode = kFast;
   PInfo P{};
@@ -474,18 +585,32 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
         const u64 so = l_oldest[tid], dlo = l_to[tid];
         A.hint[P.s] = surv == 0 ? dlo : (M > 0 && dlo < so ? dlo : so);
       }
-      if ((M == 0 || l_minrank[tid] == len) && (u64)len + M <= l_cap[tid]) {
+      const u64 base = l_base[tid], fr = (u64)front + drop;  // front room once the dropped prefix is free
+      const u32 cap = l_cap[tid], Mi = l_Mi[tid];
+      const bool up_ok = (u64)len + M <= cap;
+      if ((M == 0 || l_minrank[tid] == len) && up_ok) {
         mode = kAppend;
-        A.meta[P.s] = TMeta{l_base[tid] + drop, P.newlen, l_cap[tid] - drop, P.cut, nn};
-      } else if ((u64)len + M <= l_cap[tid]) {
-        // interleaves, but the segment has room: the log's suffix from
-        // minrank moves up in place (no fresh space)
-        mode = kInsert;
-        A.meta[P.s] = TMeta{l_base[tid] + drop, P.newlen, l_cap[tid] - drop, P.cut, nn};  // moved in stage 5
+        A.meta[P.s] = TMeta{tm_bf(base + drop, fr), P.newlen, cap - drop, P.cut, nn};
       } else {
-        mode = kRebuild;
-        P.cap = pow2_cap(surv + M);
-        A.pinfo[k] = P;
+        // interleaves: if the segment has room the log is rewritten in place
+        // (stage 5) -- its suffix from the smallest inserted rank moves up
+        // into the tail room, or its prefix below the largest inserted rank
+        // moves down into the front room, whichever moves fewer entries
+        const bool dn_ok = Mi <= fr && (u64)len + (M - Mi) <= cap;
+        const u32 up = len - l_minrank[tid], dn = l_mx[tid] - drop;
+        if (dn_ok && (!up_ok || dn < up)) {
+          mode = kInsertDn;
+          const u64 nc = (u64)cap - drop + Mi;
+          A.meta[P.s] = TMeta{tm_bf(base + drop - Mi, fr - Mi), P.newlen, nc < 0xFFFFFFFFull ? (u32)nc : 0xFFFFFFFFu,
+                              P.cut, nn};
+        } else if (up_ok) {
+          mode = kInsert;
+          A.meta[P.s] = TMeta{tm_bf(base + drop, fr), P.newlen, cap - drop, P.cut, nn};
+        } else {
+          mode = kRebuild;
+          P.cap = pow2_cap(surv + M, hist_room(A.hist[P.s], surv + M, A.epoch));
+          A.pinfo[k] = P;
+        }
       }
     }
     l_mode[tid] = mode;
@@ -498,6 +623,7 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
     if (tid == 0) A.rsum[blockIdx.x] = r;
   }
   __syncthreads();
+  JY_TCLK(ck3);
   // 4. appends: kept entries of append keys go to the tail, oldest first
   pass = 0;
   for (u64 c0 = 0; c0 < F; c0 += kTile, pass++) {
@@ -520,8 +646,10 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
       t = A.dts[j], pp = A.dpre[j], ll = A.dlr[j];
     }
     const u64 tail = l_base[idx] + l_len[idx] + l_M[idx] - 1;
-    store_rec(pool + tail - (qx & ~kKept), t, pp, ll);
+    store_rec(pool + tail - (qx & ~kKept), t, pp, ll, rec_w2(ll, A.arena));
   }
+  JY_TCLK(ck4);
+  u32 s5items = 0;
   // 5. in-place inserts: each insert key's delta entries, then its state
   //    entries from minrank, flattened (a wave scan of their counts) and
   //    moved from the last item down -- one wave, so a pass's loads all
@@ -533,11 +661,15 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
   //      state entry i: (i - drop) + #kept deltas with rank <= i
   //    relative to the log's new base (base + drop).  Reads and writes both
   //    go through `pool`.
+  //    A kInsertDn key numbers its moved state entries from the largest
+  //    index down (so the passes, last item first, move them lowest first:
+  //    entries only move down, so every one is read before anything is
+  //    written over it), and its new base is base + drop - Mi.
   {
     u32 w = 0, ne = 0;
-    if (tid < nt && l_mode[tid] == kInsert) {
+    if (tid < nt && (l_mode[tid] == kInsert || l_mode[tid] == kInsertDn)) {
       ne = l_soff[tid + 1] - l_soff[tid];  // an insert key walked every entry (stage 2)
-      w = ne + (l_len[tid] - l_minrank[tid]);
+      w = ne + (l_mode[tid] == kInsert ? l_len[tid] - l_minrank[tid] : l_mx[tid] - l_drop[tid]);
     }
     const u32 winc = jyscan::wave_incl<u32>(w);
     const u32 wtot = __shfl(winc, 63);
@@ -548,6 +680,7 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
     }
     if (tid == 0) l_soff[nt] = wtot;
     __syncthreads();
+    s5items = wtot;
     for (long long c0 = wtot ? (long long)((wtot - 1) / kTile) * kTile : -1; c0 >= 0; c0 -= kTile) {
       const u32 item = (u32)c0 + tid;
       bool write = false;
@@ -556,17 +689,19 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
       if (item < wtot) {
         const u32 a = lds_last_le(l_soff, nt - 1, item);
         const u32 r = item - l_soff[a], nek = l_gstart[a], drop = l_drop[a], M = l_M[a];
-        const u64 jb = gb0 + l_gb[a], dst = l_base[a] + drop;
+        const bool dn = l_mode[a] == kInsertDn;
+        const u64 jb = gb0 + l_gb[a], dst = l_base[a] + drop - (dn ? l_Mi[a] : 0u);
         if (r < nek) {
           const u64 j = jb + r;
           const u32 qx = eqx[j], rank = erank[j];
           x.ts = A.dts[j];
           x.pre = A.dpre[j];
           x.lr = A.dlr[j];
+          x.pad = rec_w2(x.lr, A.arena);
           write = (qx & kKept) != 0;
           at = dst + (u64)(rank - drop) + (M - 1 - (qx & ~kKept));
         } else {
-          const u64 i = l_minrank[a] + (r - nek);
+          const u64 i = dn ? l_mx[a] - 1 - (r - nek) : l_minrank[a] + (r - nek);
           x = load_rec(pool + l_base[a] + i);
           // the first delta entry with rank <= i (ranks fall along the
           // newest-first segment): a short segment counted at once, a long
@@ -601,9 +736,29 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
           at = dst + (i - drop) + (lo < jb + nek ? M - q : 0u);
         }
       }
-      if (write) store_rec(pool + at, x.ts, x.pre, x.lr);
+      if (write) store_rec(pool + at, x.ts, x.pre, x.lr, x.pad);
     }
   }
+#ifdef JY_TLOG_PROBE
+  __builtin_amdgcn_s_waitcnt(0);
+#endif
+  JY_TCLK(ck5);
+  JY_TPROBE(0, 1);
+  JY_TPROBE(1, ck1 - ck0);
+  JY_TPROBE(2, ck2 - ck1);
+  JY_TPROBE(3, ck3 - ck2);
+  JY_TPROBE(4, ck4 - ck3);
+  JY_TPROBE(5, ck5 - ck4);
+  JY_TPROBE(6, F);
+  JY_TPROBE(7, (F + kTile - 1) / kTile);
+  JY_TPROBE(8, s5items);
+  JY_TPROBE(9, (s5items + kTile - 1) / kTile);
+#ifdef JY_TLOG_PROBE
+  JY_TPROBE(10, pl);
+  JY_TPROBE(11, ps);
+  JY_TPROBE(12, pe);
+#endif
+  (void)s5items;
 }
 
 // KEY TILES again, after the scan of rebuilt sizes (tiles without a rebuilt
@@ -653,9 +808,11 @@ __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __
   if (cap) {
     const u64 k = k0 + tid;
     const PInfo P = A.pinfo[k];
-    const u64 src = A.meta[P.s].base;
-    const u64 dst = ctr[0] + roff_k;
-    A.meta[P.s] = TMeta{dst, P.newlen, P.cap, P.cut, P.newest};
+    const u64 src = tm_base(A.meta[P.s]);
+    const u32 f = rebuild_front(P.cap, P.newlen);
+    const u64 dst = ctr[0] + roff_k + f;
+    A.meta[P.s] = TMeta{tm_bf(dst, f), P.newlen, P.cap - f, P.cut, P.newest};
+    A.hist[P.s] = (u64)P.newlen << 32 | A.epoch;
     const u64 blo = A.doff[k], bhi = A.doff[k + 1];
     l_src[tid] = src;
     l_dst[tid] = dst;
@@ -681,7 +838,7 @@ __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __
   // before the passes above it have stored.
   struct CItem {
     bool live, st;
-    u32 a, qx;
+    u32 a, qx, rank;
     u64 i, j;
     TRec x;
   };
@@ -709,7 +866,8 @@ __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __
         c.x.ts = A.dts[c.j];
         c.x.pre = A.dpre[c.j];
         c.x.lr = A.dlr[c.j];
-        c.x.pad = erank[c.j];
+        c.rank = erank[c.j];
+        c.x.pad = rec_w2(c.x.lr, A.arena);
       }
     }
     return c;
@@ -767,9 +925,9 @@ __global__ __launch_bounds__(kTile) void k_tlog_commit(TlogArgs A, const u64* __
         pos = (cur.i - l_drop[a]) + (lo < l_bhi[a] ? M - (qx & ~kKept) : 0u);
       } else {
         write = (qx & kKept) != 0;
-        pos = (u64)((u32)cur.x.pad - l_drop[a]) + (M - 1 - (qx & ~kKept));
+        pos = (u64)(cur.rank - l_drop[a]) + (M - 1 - (qx & ~kKept));
       }
-      if (write) store_rec(pool + l_dst[a] + pos, cur.x.ts, cur.x.pre, cur.x.lr);
+      if (write) store_rec(pool + l_dst[a] + pos, cur.x.ts, cur.x.pre, cur.x.lr, cur.x.pad);
     }
     cur = nxt;
   }
@@ -791,7 +949,8 @@ __global__ void k_tlog_bump(u64* __restrict__ ctr, const u64* __restrict__ roff,
 constexpr u32 kTileOut = 2048;
 
 // ---- compaction: every log rewritten back to back into a fresh pool ----
-__global__ __launch_bounds__(kThreads) void k_cmp_size(const TMeta* __restrict__ meta, u64 nk, u64* __restrict__ sz,
+__global__ __launch_bounds__(kThreads) void k_cmp_size(const TMeta* __restrict__ meta, const u64* __restrict__ hist,
+                                                       u32 epoch, u64 nk, u64* __restrict__ sz,
                                                        u64* __restrict__ lens) {
   const u64 s = gid();
   if (s > nk) return;
@@ -804,8 +963,12 @@ __global__ __launch_bounds__(kThreads) void k_cmp_size(const TMeta* __restrict__
   // headroom for appends: as long again, and never less than the segment had
   // (a merge between its tile and commit pass may have planned an in-place
   // insert against that capacity)
-  const u64 want = (u64)n + (n > 4 ? n : 4);
-  sz[s] = n ? (want > m.cap ? want : m.cap) : 0;
+  // (and front room below the log); a log with an update history gets room
+  // for kHorizon merges at its rate, as a rebuild does
+  const u64 hr = hist_room(hist[s], n, epoch);
+  u64 want = (u64)n + (n > 4 ? n : 4);
+  if ((u64)n + hr > want) want = (u64)n + hr;
+  sz[s] = n ? (want > m.cap ? want : m.cap) + cmp_front(n) : 0;
   lens[s] = n;
 }
 
@@ -833,8 +996,8 @@ __global__ __launch_bounds__(kThreads) void k_cmp_copy(const TMeta* __restrict__
   if (lds) {
     for (u64 j = threadIdx.x; j < cnt; j += kThreads) {
       const TMeta m = meta[k0 + j];
-      l_off[j] = roff[k0 + j];
-      l_base[j] = m.base;
+      l_off[j] = roff[k0 + j] + cmp_front(m.len);  // the log's first entry
+      l_base[j] = tm_base(m);
       l_len[j] = m.len;
     }
   }
@@ -849,7 +1012,7 @@ __global__ __launch_bounds__(kThreads) void k_cmp_copy(const TMeta* __restrict__
         if (l_off[m] <= t) lo = m;
         else hi = m - 1;
       }
-      base = l_base[lo], len = l_len[lo], r = t - l_off[lo];
+      base = l_base[lo], len = l_len[lo], r = t - l_off[lo];  // wraps below the log: skipped
     } else {
       u64 lo = k0, hi = k0 + cnt - 1;
       while (lo < hi) {
@@ -858,19 +1021,20 @@ __global__ __launch_bounds__(kThreads) void k_cmp_copy(const TMeta* __restrict__
         else hi = m - 1;
       }
       const TMeta m = meta[lo];
-      base = m.base, len = m.len, r = t - roff[lo];
+      base = tm_base(m), len = m.len, r = t - roff[lo] - cmp_front(m.len);
     }
     if (r >= len) continue;  // headroom
     const TRec x = load_rec(src + base + r);
-    store_rec(dst + t, x.ts, x.pre, x.lr);
+    store_rec(dst + t, x.ts, x.pre, x.lr, x.pad);
   }
 }
 
 __global__ __launch_bounds__(kThreads) void k_cmp_meta(TMeta* __restrict__ meta, u64 nk, const u64* __restrict__ roff) {
   const u64 s = gid();
   if (s >= nk) return;
-  meta[s].base = roff[s];
-  meta[s].cap = (u32)(roff[s + 1] - roff[s]);
+  const u32 f = cmp_front(meta[s].len);
+  meta[s].bf = tm_bf(roff[s] + f, f);
+  meta[s].cap = (u32)(roff[s + 1] - roff[s] - f);
 }
 
 // ---- reads ----
@@ -894,7 +1058,7 @@ __global__ __launch_bounds__(kThreads) void k_tlog_gather(const TMeta* __restric
   const TMeta m = meta[slots[i]];
   u64 o = ooff[i];
   for (u64 q = m.len; q-- > 0; o++) {
-    const TRec& x = pool[m.base + q];
+    const TRec& x = pool[tm_base(m) + q];
     ots[o] = x.ts;
     opre[o] = x.pre;
     olr[o] = x.lr;
@@ -943,13 +1107,13 @@ __global__ __launch_bounds__(kThreads) void k_tlog_wprep(WCmd W, u64 n, const TM
     ent = true;
     const Ent x{W.ts[i], W.pre[i], W.lr[i]};
     if (x.t >= m.cut) {  // present? the log is ascending (ts, value) from base
-      u64 lo = m.base, hi = m.base + m.len;
+      u64 lo = tm_base(m), hi = tm_base(m) + m.len;
       while (lo < hi) {
         const u64 mid = (lo + hi) >> 1;
         if (cmp_at(pool, mid, x, arena) < 0) lo = mid + 1;
         else hi = mid;
       }
-      changed = !(lo < m.base + m.len && cmp_at(pool, lo, x, arena) == 0);
+      changed = !(lo < tm_base(m) + m.len && cmp_at(pool, lo, x, arena) == 0);
     }
   } else if (op == JY_TLOG_TRIMAT) {
     raise = W.ts[i];
@@ -962,7 +1126,7 @@ __global__ __launch_bounds__(kThreads) void k_tlog_wprep(WCmd W, u64 n, const TM
         changed = raise > m.cut;
       }
     } else if (cnt - 1 < m.len) {
-      raise = pool[m.base + m.len - cnt].ts;
+      raise = pool[tm_base(m) + m.len - cnt].ts;
       changed = raise > m.cut;
     }
     if (!changed) raise = 0;
@@ -1036,7 +1200,7 @@ int32_t tlog_compact(jy_engine* eng, TlogState& t, u64 room) {
   u64* roff = sz + nk + 1;
   u64* lens = roff + nk + 1;
   u64* loff = lens + nk + 1;
-  LAUNCH(k_cmp_size, nk + 1, t.meta, nk, sz, lens);
+  LAUNCH(k_cmp_size, nk + 1, t.meta, t.hist, eng->tl_epoch, nk, sz, lens);
   JY_TRY(scan_excl_u64(eng, sz, roff, nk + 1));
   JY_TRY(scan_excl_u64(eng, lens, loff, nk + 1));
   JY_HIP(eng, hipMemcpyAsync(t.pin, roff + nk, 8, hipMemcpyDeviceToHost, eng->stream));
@@ -1104,6 +1268,9 @@ int32_t tlog_grow_store(jy_engine* eng, TlogState& t, u64 need) {
   void* m = t.meta;
   JY_TRY(jy_realloc(eng, &m, t.kcap * sizeof(TMeta), nk * sizeof(TMeta), true));  // empty logs
   t.meta = static_cast<TMeta*>(m);
+  void* hs = t.hist;
+  JY_TRY(jy_realloc(eng, &hs, t.kcap * 8, nk * 8, true));
+  t.hist = static_cast<u64*>(hs);
   void* h = t.hint;
   JY_TRY(jy_realloc(eng, &h, t.kcap * 8, nk * 8, true));
   t.hint = static_cast<u64*>(h);
@@ -1228,6 +1395,7 @@ int32_t tlog_launch(jy_engine* eng, TlogState& t, int r, u64 nd, const u32* slot
   LAUNCH(k_tlog_prep, nd, A);
   A.meta = t.meta;
   A.hint = t.hint;
+  A.hist = t.hist;
   A.pool = t.pool;
   hipLaunchKernelGGL(k_tlog_tile, dim3(tiles), dim3(kTile), 0, eng->stream, A, t.pool, erank, eqx);
   JY_HIP(eng, hipGetLastError());
@@ -1240,6 +1408,26 @@ int32_t tlog_launch(jy_engine* eng, TlogState& t, int r, u64 nd, const u32* slot
   hipLaunchKernelGGL(k_tlog_bump, dim3(1), dim3(1), 0, eng->stream, t.ctr, A.rsum, (u64)tiles, t.pcap,
                      t.pin_dev + 8 + 4 * r);
   JY_HIP(eng, hipGetLastError());
+#ifdef JY_TLOG_PROBE
+  if (const char* path = getenv("JY_TLOG_PROBE_OUT")) {
+    static unsigned long long buf[kProbeSlots][kProbeN];
+    JY_HIP(eng, hipStreamSynchronize(eng->stream));
+    JY_HIP(eng, hipMemcpyFromSymbol(buf, HIP_SYMBOL(g_tprobe), sizeof(buf)));
+    unsigned long long tot[kProbeN] = {};
+    for (int i = 0; i < kProbeSlots; i++)
+      for (int j = 0; j < kProbeN; j++) tot[j] += buf[i][j];
+    if (FILE* f = fopen(path, "a")) {
+      const double n = tot[0] ? (double)tot[0] : 1.0;
+      fprintf(f, "merge %llu tiles %llu | per tile (us): s1 %.2f s2 %.2f [load %.2f search %.2f end %.2f] s3 %.2f s4 %.2f "
+              "s5 %.2f | slow ent %.1f passes %.2f s5 items %.1f s5 passes %.2f\n", (unsigned long long)t.seq, tot[0],
+              tot[1] / n / 100, tot[2] / n / 100, tot[10] / n / 100, tot[11] / n / 100, tot[12] / n / 100,
+              tot[3] / n / 100, tot[4] / n / 100, tot[5] / n / 100, tot[6] / n, tot[7] / n, tot[8] / n, tot[9] / n);
+      fclose(f);
+    }
+    std::memset(buf, 0, sizeof(buf));
+    JY_HIP(eng, hipMemcpyToSymbol(HIP_SYMBOL(g_tprobe), buf, sizeof(buf)));
+  }
+#endif
   JY_HIP(eng, hipEventRecord(sp.done, eng->stream));
   sp.seq = ++t.seq;
   sp.busy = true;
