@@ -254,8 +254,9 @@ struct KeyDir {
   u64 blen = 0, bcap = 0;
   u64* kref = nullptr;   // [scap] offset << 24 | length
   u64* khash = nullptr;  // [scap] table hash
+  u64* kw = nullptr;     // [scap][2] the key's bytes 0..7 and 8..15, zero filled (the probe's compare words)
   u64 n = 0, scap = 0;   // keys, slot capacity
-  u64* table = nullptr;  // [tcap] 32-B records (k_keys.hip TRec): tag << 32 | slot (~0 empty), len, 2 key words
+  u64* table = nullptr;  // [tcap] 8-B entries: tag << 32 | slot (~0 empty)
   u64 tcap = 0;
   u32 lg = 0;
 };

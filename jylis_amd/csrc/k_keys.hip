@@ -8,15 +8,19 @@
 //   bytes[]      key bytes, appended in slot order
 //   kref[slot]   (byte offset << 24) | length
 //   khash[slot]  64-bit table hash (kept for rehashing)
+//   kw[slot]     the key's bytes 0..7 and 8..15, zero filled (16 B)
 //   table[tcap]  open addressing, linear probing, tcap a power of two kept
-//                >= 2x the keys: a 32-B record {tag32 << 32 | slot, length,
-//                key bytes 0..7, key bytes 8..15} (EMPTY: e = ~0).  The slot
-//                position is the top bits of the hash, the tag its low 32
-//                bits.  A key of up to 16 bytes is found with ONE dependent
-//                access -- its record -- instead of three (entry, the slot's
-//                kref, the directory's bytes: 350 us for 8.39M keys of the
-//                node TREG call, round 5); longer keys compare the rest of
-//                their bytes in the directory.
+//                >= 2x the keys: an 8-B entry tag32 << 32 | slot (EMPTY ~0).
+//                The position is the top bits of the hash, the tag its low
+//                32 bits.  8 B per entry keeps the table MALL-resident at
+//                node scale (2^24 entries: 128 MiB of the 256 MiB Infinity
+//                Cache; round 5's 32-B records {entry, length, two key words}
+//                made it 512 MiB, and the probe's one random line per key
+//                came from HBM: 329-440 us for 8.39M keys).  A tag match is
+//                confirmed against the slot's kref (length) and kw (first 16
+//                bytes), which a batch in slot order reads as a stream;
+//                longer keys compare the rest of their bytes in the
+//                directory.
 //
 // Interning n keys is deterministic and lock-free (no thread ever waits on
 // another):
@@ -40,6 +44,7 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "jy_dscan.hpp"
@@ -112,28 +117,16 @@ __device__ __attribute__((noinline)) bool key_tail_equal(const uint8_t* __restri
   return true;
 }
 
-struct alignas(32) TRec {
-  u64 e;       // tag32 << 32 | slot (kPending: a claim of this launch, slot = its input index); EMPTY ~0
-  u64 len;     // the key's length
-  u64 w0, w1;  // its bytes 0..7 and 8..15, zero filled (key_words)
-};
-static_assert(sizeof(TRec) == 32, "32-B key records");
-
+// table entries: tag32 << 32 | slot (kPending: a claim of this launch, slot = its input index); EMPTY ~0
 struct Dir {
   const uint8_t* bytes;
   u64* kref;
   u64* khash;
-  TRec* table;
+  ulonglong2* kw;  // [slot] {w0, w1}
+  u64* table;
   u64 mask;
   u32 shift;  // 64 - log2(tcap)
 };
-
-// one record, two 16-B loads issued together
-__device__ __forceinline__ TRec load_rec(const TRec* __restrict__ t, u64 p) {
-  const ulonglong2* q = reinterpret_cast<const ulonglong2*>(t + p);
-  const ulonglong2 a = q[0], b = q[1];
-  return TRec{a.x, a.y, b.x, b.y};
-}
 
 struct In {
   const uint8_t* kb;
@@ -163,12 +156,21 @@ __global__ __launch_bounds__(kThreads) void k_key_probe(In I, Dir D, u32* __rest
     const u64 t = table_hash(I.kb + a, len, kw);
     u64 p = t >> D.shift;
     u32 slot = kMiss;
-    for (;;) {
-      const TRec r = load_rec(D.table, p);
-      if (r.e == kEmpty) break;
-      if ((u32)(r.e >> 32) == tag_of(t) && !(r.e & kPending) && r.len == len && r.w0 == kw.w0 && r.w1 == kw.w1) {
-        const u32 s = (u32)(r.e & kIdxMask);
-        if (len <= 16 || key_tail_equal(D.bytes + (D.kref[s] >> JY_LR_LEN_BITS), I.kb + a, len)) {
+    // at most every entry once: the table always keeps EMPTY entries, so a
+    // walk that finds none met a corrupt table -- it ends, and is counted
+    for (u64 walk = 0;; walk++) {
+      if (walk > D.mask) {
+        c[2] = 1;  // reported with the oversized-key count: the call fails
+        break;
+      }
+      const u64 e = D.table[p];
+      if (e == kEmpty) break;
+      if ((u32)(e >> 32) == tag_of(t) && !(e & kPending)) {
+        const u32 s = (u32)(e & kIdxMask);
+        const u64 kr = D.kref[s];
+        const ulonglong2 w = D.kw[s];
+        if ((kr & JY_LR_LEN_MASK) == len && w.x == kw.w0 && w.y == kw.w1 &&
+            (len <= 16 || key_tail_equal(D.bytes + (kr >> JY_LR_LEN_BITS), I.kb + a, len))) {
           slot = s;
           break;
         }
@@ -180,7 +182,7 @@ __global__ __launch_bounds__(kThreads) void k_key_probe(In I, Dir D, u32* __rest
       th[i] = t;  // read only for misses (claim, commit): a found key writes no hash
       c[0] = 1;
       c[1] = len;
-      c[2] = len > JY_LR_LEN_MASK;
+      c[2] |= len > JY_LR_LEN_MASK;
     }
   }
   const int w = threadIdx.x >> 6;
@@ -255,10 +257,10 @@ __global__ __launch_bounds__(kThreads) void k_key_claim(In I, Dir D, const u32* 
   const KeyW kw = key_words(k, len);
   const u64 mine = ((u64)tag_of(t) << 32) | kPending | i;
   u64 p = t >> D.shift;
-  u64 e = D.table[p].e;
-  for (;;) {
+  u64 e = D.table[p];
+  for (u64 walk = 0; walk <= D.mask; walk++) {  // (an EMPTY entry or the group's claim is always met)
     if (e == kEmpty) {
-      const u64 prev = atomicCAS(reinterpret_cast<unsigned long long*>(&D.table[p].e), kEmpty, mine);
+      const u64 prev = atomicCAS(reinterpret_cast<unsigned long long*>(&D.table[p]), kEmpty, mine);
       if (prev == kEmpty) {
         owner[i] = (u32)i;
         pos[i] = p;
@@ -276,7 +278,7 @@ __global__ __launch_bounds__(kThreads) void k_key_claim(In I, Dir D, const u32* 
       }
     }
     p = (p + 1) & D.mask;
-    e = D.table[p].e;
+    e = D.table[p];
   }
 }
 
@@ -324,16 +326,11 @@ __global__ __launch_bounds__(kThreads) void k_key_commit(In I, Dir D, uint8_t* _
     for (u64 b = 0; b < len; b++) dbytes[at + b] = src[b];  // (word reads + byte stores: 72 -> 79 us)
     D.kref[slot] = (at << JY_LR_LEN_BITS) | len;
     D.khash[slot] = th[i];
+    const KeyW kw = key_words(src, len);
+    D.kw[slot] = ulonglong2{kw.w0, kw.w1};
   }
-  if (o == (u32)i) {  // (probes and claims of other keys run in other launches)
-    TRec& r = D.table[pos[i]];
-    const u64 len = I.ko[i + 1] - I.ko[i];
-    const KeyW kw = key_words(I.kb + I.ko[i], len);
-    r.len = len;
-    r.w0 = kw.w0;
-    r.w1 = kw.w1;
-    r.e = ((u64)tag_of(th[i]) << 32) | slot;
-  }
+  if (o == (u32)i)  // (probes and claims of other keys run in other launches)
+    D.table[pos[i]] = ((u64)tag_of(th[i]) << 32) | slot;
 }
 
 // rebuild the table from the per-slot hashes
@@ -343,16 +340,15 @@ __global__ __launch_bounds__(kThreads) void k_key_rehash(Dir D, u64 nk) {
   const u64 t = D.khash[s];
   const u64 e = ((u64)tag_of(t) << 32) | s;
   u64 p = t >> D.shift;
-  while (atomicCAS(reinterpret_cast<unsigned long long*>(&D.table[p].e), kEmpty, e) != kEmpty) p = (p + 1) & D.mask;
-  const u64 r = D.kref[s], len = r & JY_LR_LEN_MASK;
-  const KeyW kw = key_words(D.bytes + (r >> JY_LR_LEN_BITS), len);
-  D.table[p].len = len;
-  D.table[p].w0 = kw.w0;
-  D.table[p].w1 = kw.w1;
+  while (atomicCAS(reinterpret_cast<unsigned long long*>(&D.table[p]), kEmpty, e) != kEmpty) p = (p + 1) & D.mask;
 }
 
-// how long the host spins on the sums' completion word before it falls back
-// to a stream synchronise (a probe of 8.39M keys takes ~0.3 ms)
+// how the host waits for the sums' completion word: a tight spin (pause) for
+// as long as a large probe takes (8.39M keys: ~0.3-0.45 ms), then a yielding
+// poll -- earlier converges may still be queued ahead of the probe on the
+// engine stream, and the core is the other repos' too -- and past kSpinUs a
+// stream synchronise (which also reports a launch that never ends)
+constexpr double kTightUs = 600.0;
 constexpr double kSpinUs = 20000.0;
 
 u32 blocks_for(u64 n) { return (u32)std::max<u64>(1, (n + kThreads - 1) / kThreads); }
@@ -368,7 +364,8 @@ Dir dir_of(KeyDir& K) {
   D.bytes = K.bytes;
   D.kref = K.kref;
   D.khash = K.khash;
-  D.table = reinterpret_cast<TRec*>(K.table);
+  D.kw = reinterpret_cast<ulonglong2*>(K.kw);
+  D.table = K.table;
   D.mask = K.tcap - 1;
   D.shift = 64 - K.lg;
   return D;
@@ -384,10 +381,10 @@ int32_t grow_table(jy_engine* eng, KeyDir& K, u64 need_keys) {
   if (K.table && want <= K.tcap) return JY_OK;
   jy_dev_free(eng, K.table);
   K.table = nullptr;
-  JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&K.table), want * sizeof(TRec), "key table"));
+  JY_TRY(jy_dev_alloc(eng, reinterpret_cast<void**>(&K.table), want * 8, "key table"));
   K.tcap = want;
   K.lg = lg;
-  JY_HIP(eng, hipMemsetAsync(K.table, 0xFF, want * sizeof(TRec), eng->stream));
+  JY_HIP(eng, hipMemsetAsync(K.table, 0xFF, want * 8, eng->stream));
   if (K.n) LAUNCH(k_key_rehash, K.n, dir_of(K), K.n);
   return JY_OK;
 }
@@ -401,6 +398,9 @@ int32_t grow_slots(jy_engine* eng, KeyDir& K, u64 need) {
   void* b = K.khash;
   JY_TRY(jy_realloc(eng, &b, K.n * 8, nc * 8, false));
   K.khash = static_cast<u64*>(b);
+  void* c = K.kw;
+  JY_TRY(jy_realloc(eng, &c, K.n * 16, nc * 16, false));
+  K.kw = static_cast<u64*>(c);
   K.scap = nc;
   return JY_OK;
 }
@@ -425,7 +425,7 @@ int32_t jy_keydir_reserve(jy_engine* eng, int32_t type, u64 cap) {
 
 void jy_keydir_free(jy_engine* eng, KeyDir& K) {
   for (void* p : {static_cast<void*>(K.bytes), static_cast<void*>(K.kref), static_cast<void*>(K.khash),
-                  static_cast<void*>(K.table)})
+                  static_cast<void*>(K.kw), static_cast<void*>(K.table)})
     jy_dev_free(eng, p);
   K = KeyDir{};
 }
@@ -493,7 +493,11 @@ int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, co
       seen = true;
       break;
     }
-    if ((spin & 255) == 255 && jy_now_us() - t0 > kSpinUs) break;
+    if ((spin & 255) == 255) {
+      const double w = jy_now_us() - t0;
+      if (w > kSpinUs) break;
+      if (w > kTightUs) std::this_thread::yield();
+    }
     __builtin_ia32_pause();
   }
   if (!seen) JY_HIP(eng, hipStreamSynchronize(eng->stream));
@@ -504,8 +508,8 @@ int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, co
     for (int q = 0; q < 3; q++) hc[q] += hg[g * 3 + q];
   const u64 m = hc[0], mbytes = hc[1];
   JY_TRACE("keydir %llu keys: %llu misses (create %d)", (unsigned long long)n, (unsigned long long)m, (int)create);
+  if (hc[2]) return eng->fail(JY_ERANGE, "key longer than 16 MiB, or a probe walked the whole key table");
   if (!create || m == 0) return JY_OK;  // (a miss's kMiss is JY_NO_SLOT)
-  if (hc[2]) return eng->fail(JY_ERANGE, "key longer than 16 MiB");
   if (K.n + m >= kIdxMask) return eng->fail(JY_ERANGE, "slot space exhausted");
   JY_TRY(grow_table(eng, K, K.n + m));
   JY_TRY(grow_slots(eng, K, K.n + m));

@@ -60,6 +60,10 @@ constexpr int kThreads = 256;
 #define JY_TREG_UNROLL 4
 #endif
 constexpr int kUnroll = JY_TREG_UNROLL;
+// <true> form: load the old handles with the state timestamps (A/B switch)
+#ifndef JY_TREG_PRELOAD
+#define JY_TREG_PRELOAD 1
+#endif
 constexpr u64 kMallBytes = 256ull << 20;  // MI355X Infinity Cache (MALL)
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
@@ -217,10 +221,20 @@ __global__ __launch_bounds__(kThreads) void k_treg_lww(TregK K, const u32* __res
         s[u] = 0;
       }
   }
+  // <true> (a state streamed from HBM): the old handles come with the state
+  // timestamps, in the same round trip -- a loser rewrites its own, and at
+  // ~1/3 losers nearly every 64-B handle line holds one, so those lines were
+  // fetched anyway (PMC, profiles/r06_pmc_treg.json: 48 B read per key, not
+  // the 37 B of ts + loser handles); the decision no longer waits for a
+  // second, dependent load
+  TVal h0[kRewriteAll && !kSet && JY_TREG_PRELOAD ? kUnroll : 1];
   if (!kSet) {
 #pragma unroll
     for (int u = 0; u < kUnroll; u++)
-      if (valid[u]) t0[u] = K.ts[s[u]];
+      if (valid[u]) {
+        t0[u] = K.ts[s[u]];
+        if constexpr (kRewriteAll && JY_TREG_PRELOAD) h0[u] = K.val[s[u]];
+      }
   }
   if (kDense) {
 #pragma unroll
@@ -239,6 +253,12 @@ __global__ __launch_bounds__(kThreads) void k_treg_lww(TregK K, const u32* __res
     }
     if (kSet) {
       set_one(K, s[u], t[u], p[u], l[u]);
+      continue;
+    }
+    if constexpr (kRewriteAll && JY_TREG_PRELOAD) {
+      const bool w = t[u] > t0[u] || (t[u] == t0[u] && jy_value_cmp(p[u], l[u], h0[u].pre, h0[u].lr, K.arena) > 0);
+      K.ts[s[u]] = w ? t[u] : t0[u];
+      K.val[s[u]] = w ? TVal{p[u], l[u]} : h0[u];
       continue;
     }
     const bool w = t[u] >= t0[u] && lww_wins(t[u], t0[u], p[u], l[u], K.val, s[u], K.arena);

@@ -13,6 +13,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
+    import faulthandler
+    faulthandler.dump_traceback_later(float(os.environ.get("JY_DUMP_AFTER", "100")), exit=False)
     import numpy as np
     import torch
     from jylis_amd._lib import TREG
@@ -27,6 +29,9 @@ def main():
     digits = torch.stack([(idx // 10 ** (9 - j)) % 10 + 48 for j in range(10)], 1).to(torch.uint8)
     kb = torch.cat([torch.full((n, 1), ord("t"), dtype=torch.uint8, device=dev), digits], 1).reshape(-1)
     ko = torch.arange(n + 1, device=dev, dtype=torch.int64) * 11
+    # the engine runs on its own stream when torch's is the legacy default
+    # one: the keys must be in HBM before it reads them
+    torch.cuda.synchronize(dev)
     slots = eng.intern_device(TREG, kb, ko)
     del kb, ko, digits
     assert bool((slots == idx.to(torch.int32)).all())
