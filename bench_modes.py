@@ -13,6 +13,35 @@ import time
 import numpy as np
 
 HBM_PEAK_GBS = 8000.0
+_HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def pmc_traffic(name, workload=None):
+    """HBM bytes per converge (or launch) from a committed PMC summary,
+    profiles/r06_pmc_bench_<name>.json (scripts/gpu_r06_pmc.sh: separate
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this same bench line,
+    scripts/pmc_converge.py: FETCH x2, WRITE as is).  The counters cannot be
+    read live beside the timed region, so the line quotes the committed run
+    of its own workload -> (bytes or None, source)"""
+    path = os.path.join(_HERE, "profiles", f"r06_pmc_bench_{name}.json")
+    try:
+        import json
+        with open(path) as f:
+            d = json.load(f)
+        if workload is not None and d.get("workload", workload) != workload:
+            return None, None
+        return float(d["moved_MB"]) * 1e6, os.path.relpath(path, _HERE)
+    except Exception:
+        return None, None
+
+
+def with_traffic(roof, name, workload=None):
+    t, src = pmc_traffic(name, workload)
+    roof["traffic"] = t
+    if t is not None:
+        roof["traffic_source"] = src
+        roof["traffic_note"] = "HBM bytes per converge from the committed PMC passes of this bench line (FETCH x2, WRITE)"
+    return roof
 
 
 def _timed(steps, warmup, step, dist, dev, eng=None, before_timed=None, drain=None):
@@ -525,6 +554,8 @@ def bench_treg(args, eng, dev, dist, rank, world):
                            "bytes_moved_note": ("" if block else "4 slot + ") + "24 delta (ts, pre, lr) + 8 state ts "
                                                "read + 8 ts rewritten + 16 handle write x winner fraction (a state "
                                                "over the 256 MiB MALL: every handle written, losers' read)"}
+        if Kper == 8 << 20:  # the PMC run's workload (scripts/gpu_r06_pmc.sh MODES=treg)
+            with_traffic(out["roofline"], "treg" if block else "treg_keyed")
         if block:
             out["form"] = ("block: the step's batch holds one delta for every slot in slot order "
                            "(jy_treg_converge_block, no slot stream, no claim); the keyed form "
@@ -534,6 +565,10 @@ def bench_treg(args, eng, dev, dist, rank, world):
                             "value": world * (n + m) * args.steps / el2,
                             "frac": bytes_per_key * n / k2 / 1e9 / HBM_PEAK_GBS,
                             "bytes_moved_per_unit": moved + 4}
+            if Kper == 8 << 20:
+                t_k, src_k = pmc_traffic("treg_keyed")
+                out["keyed"]["traffic"] = t_k
+                out["keyed"]["traffic_source"] = src_k
     else:
         out["step_ms_avg_events"] = k * 1e3
         out["self_direct"] = tr.self_direct
@@ -646,6 +681,9 @@ def bench_treg_node(args, eng, dev, dist, rank, world):
            "ms_per_step": ms, "setup_s": setup_s, "node_shards": shards,
            "exchange_bytes_sent_per_step": st["bytes_sent"], "keys_received_per_step": st["keys_received"],
            "verified_sampled_keys": verified}
+    if Kper == 8 << 20 and world == 1 and shards == 1:  # the PMC run's workload (scripts/gpu_r06_pmc.sh MODES=node)
+        tr, src = pmc_traffic("node")
+        out["traffic_per_call"], out["traffic_source"] = tr, src
     node.close()
     return out
 
@@ -725,6 +763,18 @@ def bench_tlog(args, eng, dev, dist, rank, world):
     k = float(np.mean(kt))
     avg_b = float(np.mean(byts))
     units = float(np.mean(ins))
+    roof = {"bound": "hbm", "achieved": avg_b / k / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": avg_b / k / 1e9 / HBM_PEAK_GBS,
+            "kernel": "TLOG converge (k_tlog_*, all launches of one call)",
+            "converge_ms_avg": k * 1e3, "bytes_per_converge": avg_b,
+            "bytes_note": "SURVEY 8d: 16 B read per input entry (state + delta) + 16 B written per "
+                          "output entry + 24 B per key (a whole-state rewrite)",
+            "min_bytes_moved_per_converge": float(np.mean(moved)),
+            "frac_moved": float(np.mean(moved)) / k / 1e9 / HBM_PEAK_GBS,
+            "min_bytes_moved_note": "append layout lower bound: 24 B per delta entry read + 32 B per "
+                                    "net new entry written + 64 B meta per delta key"}
+    if K == 4 << 20:  # the PMC run's workload (scripts/gpu_r06_pmc.sh MODES=tlog)
+        with_traffic(roof, "tlog")
     return {"workload": f"TLOG converge: {K} logs, state ~Geom(8, cap 64) entries, delta ~Geom(2) per key "
                         f"per step, dups/ties/cutoffs (SURVEY 8d config 4); {n_state0} initial entries",
             "unit_of_work": "log entry (input)", "value": world * units * args.steps / t,
@@ -732,16 +782,7 @@ def bench_tlog(args, eng, dev, dist, rank, world):
             # merges of warmup + timed steps that spilled (re-merged after a
             # compaction, host never waited) and the compactions they caused
             "spills_compactions": [st1["spills"] - st0["spills"], st1["compactions"] - st0["compactions"]],
-            "roofline": {"bound": "hbm", "achieved": avg_b / k / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": avg_b / k / 1e9 / HBM_PEAK_GBS,
-                         "kernel": "TLOG converge (k_tlog_*, all launches of one call)",
-                         "converge_ms_avg": k * 1e3, "bytes_per_converge": avg_b,
-                         "bytes_note": "SURVEY 8d: 16 B read per input entry (state + delta) + 16 B written per "
-                                       "output entry + 24 B per key (a whole-state rewrite)",
-                         "min_bytes_moved_per_converge": float(np.mean(moved)),
-                         "frac_moved": float(np.mean(moved)) / k / 1e9 / HBM_PEAK_GBS,
-                         "min_bytes_moved_note": "append layout lower bound: 24 B per delta entry read + 32 B per "
-                                                 "net new entry written + 64 B meta per delta key"}}
+            "roofline": roof}
 
 
 def _verify_tlog(eng, st, applied, K, nsample=128, locate=None, ask=None):
@@ -945,6 +986,20 @@ def bench_ujson(args, eng, dev, dist, rank, world):
              16 * d["delta_el"] + 8 * d["delta_cloud"] + 16 * d["inplace_added_el"] + 8 * d["inplace_added_cloud"] +
              64 * R * d["inplace_docs"] + 24 * R * (d["delta_docs"] - d["inplace_docs"]))
     dots_examined = st_el + st_cl + d["delta_el"] + d["delta_cloud"]
+    roof = {"bound": "hbm", "achieved": bytes_conv / k / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": bytes_conv / k / 1e9 / HBM_PEAK_GBS,
+            "frac_moved": moved / k / 1e9 / HBM_PEAK_GBS, "bytes_moved_per_converge": moved,
+            "bytes_moved_note": "the regular path's rewrite of the documents it takes, plus for each "
+                                "document in place: its delta dots read, the appended ones written, "
+                                "R column records read + rewritten",
+            "kernel": "UJSON converge (k_uj_*, all launches of one call)",
+            "converge_ms_avg": k * 1e3, "bytes_per_converge": bytes_conv,
+            "bytes_note": "SURVEY 8d, from jy_ujson_stats_ext over the timed converges: 16 B per "
+                          "element read (every state element of a delta's document + delta) and "
+                          "written (merged), 8 B per cloud dot read and written, 24R B context per "
+                          "delta doc; untouched documents are not counted"}
+    if D == 1 << 20:  # the PMC run's workload (scripts/gpu_r06_pmc.sh MODES=ujson: warmup 6, 4 timed converges)
+        with_traffic(roof, "ujson")
     return {"workload": f"UJSON converge: {D} docs (~8 leaves, R=16), Zipf(1.1) delta docs per step "
                         f"({int(d['delta_docs'])} docs, {int(d['delta_el'])} dots, {int(d['delta_cloud'])} cloud dots; "
                         f"{int(st_el)} state elements examined, {int(d['inplace_state_el'])} of them in "
@@ -954,18 +1009,7 @@ def bench_ujson(args, eng, dev, dist, rank, world):
             "ms_per_step": t / args.steps * 1e3, "generate_s": gen_s,
             "delta_docs_per_s": world * d["delta_docs"] * args.steps / t, "verified_sampled_docs": verified,
             "per_converge": d,
-            "roofline": {"bound": "hbm", "achieved": bytes_conv / k / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": bytes_conv / k / 1e9 / HBM_PEAK_GBS,
-                         "frac_moved": moved / k / 1e9 / HBM_PEAK_GBS, "bytes_moved_per_converge": moved,
-                         "bytes_moved_note": "the regular path's rewrite of the documents it takes, plus for each "
-                                             "document in place: its delta dots read, the appended ones written, "
-                                             "R column records read + rewritten",
-                         "kernel": "UJSON converge (k_uj_*, all launches of one call)",
-                         "converge_ms_avg": k * 1e3, "bytes_per_converge": bytes_conv,
-                         "bytes_note": "SURVEY 8d, from jy_ujson_stats_ext over the timed converges: 16 B per "
-                                       "element read (every state element of a delta's document + delta) and "
-                                       "written (merged), 8 B per cloud dot read and written, 24R B context per "
-                                       "delta doc; untouched documents are not counted"}}
+            "roofline": roof}
 
 
 # ---- end-to-end ingest: the ABI path the Pony glue calls (host batches) -----------
