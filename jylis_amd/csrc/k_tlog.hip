@@ -358,6 +358,7 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
   // 1. keys
   u64 sc = 0;      // slow entries of this lane's key
   u32 front = 0;   // its front room (stage 3 is this lane's again)
+  bool raise = false;  // its cutoff rises over part of its log: a drop search
   if (tid < nt) {
     const u64 k = k0 + tid;
     const u32 s = A.slot[k];
@@ -406,18 +407,14 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
         A.hint[s] = o;
       }
     } else {
-      u32 drop = 0;
-      u64 oldest = 0;
-      if (cd > m.cut && m.len > 0) {
-        // the interpolated search from the hint (one window of 1-2 lines; the
-        // 16-ary probes read 16 lines a round), then the new oldest entry --
-        // inside the window, a cache hit
-        drop = ts_interp(A.pool, mb, 0, m.len, hv, m.newest, cut);  // oldest first: a prefix
-        oldest = drop < m.len ? A.pool[mb + drop].ts : 0;
-      } else if (m.len > 0) {
-        oldest = hv;  // the hint (round 3 loaded pool[base].ts here: one dependent random line per slow key)
-      }
-      l_oldest[tid] = oldest;  // for the interpolated searches
+      // a raised cutoff's dropped prefix is searched in stage 2, in the same
+      // search passes as the entries (round 6: searched here, it was a
+      // dependent chain of its own that the whole tile waited for)
+      raise = cd > m.cut && m.len > 0;
+      // the oldest timestamp (hint: no dependent load of the log's first
+      // record) -- the lower bound of every search; the drop search replaces
+      // it by the oldest surviving one, for the hint stage 3 publishes
+      l_oldest[tid] = m.len > 0 ? hv : 0;
       sc = hole ? 0 : ne;  // a hole's entries (a spill's unspilled keys) are never walked
       l_base[tid] = mb;
       front = (u32)tm_front(m);
@@ -425,7 +422,7 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
       l_cut[tid] = cut;
       l_len[tid] = m.len;
       l_cap[tid] = m.cap;
-      l_drop[tid] = drop;
+      l_drop[tid] = 0;
       l_bad[tid] = bad;
       l_M[tid] = 0;
       l_Mi[tid] = 0;
@@ -450,20 +447,82 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
 #ifdef JY_TLOG_PROBE
   u64 pl = 0, ps = 0, pe = 0, pa = 0, pb = 0;
 #endif
-  // 2. slow entries, one per lane per pass
+  // 2. slow entries.  (a) one per lane per pass: order check, cutoff, and
+  //    the rank of an entry newer than the log (its length); an entry that
+  //    needs a search joins the tile's SEARCH QUEUE (LDS), with the raised
+  //    cutoffs' drop searches.  (b) the queue in passes of 64 searches: the
+  //    rank in the log (an aligned-line interpolation search, then the value
+  //    order on equal timestamps, duplicates dropped).  A tile's searches run
+  //    as ONE chain of dependent loads (two when it has more than 64), not
+  //    one per entry pass.  (c) per pass again: kept flags from (a) / (b),
+  //    q = kept entries of the key before it (ballot with carry), the keys'
+  //    counts and bounds.  erank / eqx carry the ranks and states between
+  //    them (eqx: 0 dropped, 1 kept, until (c) writes the final word).
+  __shared__ u32 l_q[kTile];   // queued items: entry index f, or kDropItem | key
+  __shared__ u64 l_qx[kTile];  // their timestamps (the value searched for)
+  constexpr u32 kDropItem = 0x80000000u;
+  u32 nq = 0;  // wave-uniform
+  {
+    const u64 m = __ballot(raise);
+    if (raise) {
+      const u32 at = (u32)__popcll(m & lanelt);
+      l_q[at] = kDropItem | tid;
+      l_qx[at] = l_cut[tid];
+    }
+    nq = (u32)__popcll(m);
+  }
+  // the n queued searches, lane = item
+  auto run_searches = [&](u32 n) {
+    __syncthreads();  // the queue's writes
+    u32 item = 0, idx = 0, r = 0;
+    u64 x = 0, j = 0;
+    bool live = tid < n;
+    if (live) {
+      item = l_q[tid];
+      x = l_qx[tid];
+      idx = (item & kDropItem) ? (item & (kTile - 1)) : lds_last_le(l_soff, nt - 1, item);
+      const u64 base = l_base[idx];
+      const u32 len = l_len[idx];
+      u64 pp = 0, ll = 0;
+      if (!(item & kDropItem)) {
+        j = gb0 + l_gb[idx] + (item - l_soff[idx]);
+        pp = A.dpre[j];  // in flight with the search
+        ll = A.dlr[j];
+      }
+      r = ts_interp(A.pool, base, 0, len, l_oldest[idx], l_newest[idx], x);
+      if (item & kDropItem) {
+        l_drop[idx] = r;  // oldest first: the dropped prefix
+        l_oldest[idx] = r < len ? A.pool[base + r].ts : 0;
+      } else {
+        int c = 1;
+        u32 e = r;
+        for (; e < len; e++) {
+          const TRec y = A.pool[base + e];
+          if (y.ts != x) break;
+          c = jy_value_cmp(y.pre, y.lr, pp, ll, A.arena);
+          if (c >= 0) break;
+        }
+        erank[j] = e;
+        eqx[j] = c != 0 ? 1u : 0u;  // c == 0: a duplicate of entry e
+      }
+    }
+    __syncthreads();  // l_oldest / l_drop / erank / eqx
+  };
+  // the drop searches read l_oldest / l_newest of their own key only, and the
+  // entry searches of a raise key run in the same pass or later: their lower
+  // bound may already be the surviving oldest, a tighter one -- either is a
+  // valid bound (every timestamp searched is >= the cutoff)
   u32 carry = 0;
   constexpr int kCacheN = kCache > 0 ? kCache : 1;
   u64 c_t[kCacheN], c_p[kCacheN], c_l[kCacheN];
   u32 c_q[kCacheN], c_i[kCacheN];
 #pragma unroll
   for (int c = 0; c < kCache; c++) c_q[c] = c_i[c] = 0, c_t[c] = c_p[c] = c_l[c] = 0;
+  // (a)
   int pass = 0;
   for (u64 c0 = 0; c0 < F; c0 += kTile, pass++) {
-#ifdef JY_TLOG_PROBE
-    const u64 pst = wall_clock64();
-#endif
     const u64 f = c0 + tid;
-    u32 idx = 0, flag = 0, rank = 0, lo = 0, hi = 0;
+    u32 idx = 0, st = 0;
     u64 t = 0, pp = 0, ll = 0, j = 0;
     if (f < F) {
       idx = lds_last_le(l_soff, nt - 1, f);
@@ -475,58 +534,73 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
       // strictly newest first; the previous value is read only on a ts tie
       if (f > l_soff[idx] && (pt < t || (pt == t && jy_value_cmp(A.dpre[j - 1], A.dlr[j - 1], pp, ll, A.arena) <= 0)))
         atomicOr(&l_bad[idx], 2u);
-      const u32 len = l_len[idx], drop = l_drop[idx];
+      const u32 len = l_len[idx];
       if (t >= l_cut[idx]) {
-        if (len == drop || t > l_newest[idx]) {
-          flag = 1;
-          rank = len;
+        if (len == 0 || t > l_newest[idx]) {
+          st = 1;
+          erank[j] = len;
+          eqx[j] = 1u;
         } else {
-          lo = drop;  // search: first entry of the log not older than x
-          hi = len;
-          flag = 2;   // pending
+          st = 2;  // a search; every state entry below the cutoff is older than t, so [0, len) does
         }
+      } else {
+        erank[j] = 0u;  // (below the cutoff: the oldest entries, rank 0 keeps the ranks non-increasing)
+        eqx[j] = 0u;
       }
     }
-#ifdef JY_TLOG_PROBE
-    __builtin_amdgcn_s_waitcnt(0);
-    JY_TCLKV(pa);
-    pl += pa - pst;
-#endif
-    if (flag == 2) {
-      // the first log entry not older than x: a binary search of the
-      // timestamps (16-ary probes read ~2x the lines: measured slower), then
-      // the values of the (usually 0 or 1) entries with x's timestamp
-      const u64 base = l_base[idx];
-      const u64 w = rec_w2(ll, A.arena);  // issued before the search: in flight with it
-      const u32 r = ts_interp(A.pool, base, lo, hi, l_oldest[idx], l_newest[idx], t);
-      int c = 1;
-      u32 e = r;
-      for (; e < hi; e++) {
-        const TRec y = A.pool[base + e];
-        if (y.ts != t) break;
-        c = JY_TLOG_W2 ? jy_value_cmp_w(y.pre, y.pad, y.lr, pp, w, ll, A.arena)
-                       : jy_value_cmp(y.pre, y.lr, pp, ll, A.arena);
-        if (c >= 0) break;
-      }
-      rank = e;
-      flag = c != 0;  // c == 0: a duplicate of entry e
+    const u64 m = __ballot(st == 2);
+    if (nq + (u32)__popcll(m) > kTile) {  // no room: the queue's searches first
+      run_searches(nq);
+      nq = 0;
     }
+    if (st == 2) {
+      const u32 at = nq + (u32)__popcll(m & lanelt);
+      l_q[at] = (u32)f;
+      l_qx[at] = t;
+    }
+    nq += (u32)__popcll(m);
+#pragma unroll
+    for (int c = 0; c < kCache; c++)
+      if (c == pass) c_t[c] = t, c_p[c] = pp, c_l[c] = ll, c_i[c] = idx;
+  }
+  if (nq) run_searches(nq);
+  else __syncthreads();  // (a)'s global stores, for (c)
 #ifdef JY_TLOG_PROBE
-    JY_TCLKV(pb);
-    ps += pb - pa;
+  __builtin_amdgcn_s_waitcnt(0);
+  JY_TCLKV(pa);
+  pl = pa - ck1;
 #endif
+  // (c)
+  pass = 0;
+  for (u64 c0 = 0; c0 < F; c0 += kTile, pass++) {
+    const u64 f = c0 + tid;
+    u32 idx = 0, kept = 0, rank = 0;
+    u64 t = 0, j = 0;
+    if (f < F) {
+      if (pass < kCache) {
+        idx = c_i[0], t = c_t[0];
+#pragma unroll
+        for (int c = 1; c < kCache; c++)
+          if (c == pass) idx = c_i[c], t = c_t[c];
+      } else {
+        idx = lds_last_le(l_soff, nt - 1, f);
+      }
+      j = gb0 + l_gb[idx] + (f - l_soff[idx]);
+      if (pass >= kCache) t = A.dts[j];
+      kept = eqx[j];
+      rank = kept ? erank[j] : 0u;
+    }
     // kept ranks in entry order (a wave ballot per pass)
-    const u64 mask = __ballot(flag != 0);
+    const u64 mask = __ballot(kept != 0);
     const u32 g = carry + (u32)__popcll(mask & lanelt);
     carry += (u32)__popcll(mask);
     if (f < F && f == l_soff[idx]) l_gstart[idx] = g;
     __syncthreads();
     u32 qx = 0;
     if (f < F) {
-      qx = (g - l_gstart[idx]) | (flag ? kKept : 0u);
-      erank[j] = rank;
+      qx = (g - l_gstart[idx]) | (kept ? kKept : 0u);
       eqx[j] = qx;
-      if (flag) {
+      if (kept) {
         atomicAdd(&l_M[idx], 1u);
         atomicMin(&l_minrank[idx], rank);
         atomicMax((unsigned long long*)&l_tn[idx], (unsigned long long)t);  // newest kept
@@ -539,19 +613,15 @@ __global__ __launch_bounds__(kTile) JY_TLOG_TILE_ATTR void k_tlog_tile(TlogArgs 
     }
 #pragma unroll
     for (int c = 0; c < kCache; c++)
-      if (c == pass) {
-        c_t[c] = t, c_p[c] = pp, c_l[c] = ll, c_q[c] = qx, c_i[c] = idx;
-      }
+      if (c == pass) c_q[c] = qx;
     __syncthreads();  // l_gstart reuse
-#ifdef JY_TLOG_PROBE
-    __builtin_amdgcn_s_waitcnt(0);
-    {
-      u64 pc;
-      JY_TCLKV(pc);
-      pe += pc - pb;
-    }
-#endif
   }
+#ifdef JY_TLOG_PROBE
+  __builtin_amdgcn_s_waitcnt(0);
+  JY_TCLKV(pb);
+  ps = 0;
+  pe = pb - pa;
+#endif
   JY_TCLK(ck2);
   // 3. per slow key: append (meta published here), rebuild (planned) or skip
   u32 mode = kFast;
