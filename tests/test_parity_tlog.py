@@ -234,3 +234,50 @@ def test_spilled_merges_in_flight(oracle_mod):
         assert stats["merges"] >= len(dl) + 1
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_inserts_near_the_oldest_end(oracle_mod, engine, seed):
+    """Round 6's in-place inserts that move the SHORTER side of a log: long
+    logs receive, merge after merge, entries older than almost all of their
+    entries (just above the oldest: the prefix moves down into the front
+    room), entries near the newest (the suffix moves up), duplicates, ties,
+    fresh appends, and cutoff raises that free front room -- until the room
+    runs out and logs are rebuilt (update-history capacities) -- against the
+    oracle after every merge."""
+    from jylis_amd.repo import RepoTLOG
+    O = oracle_mod
+    rng = np.random.default_rng(seed)
+    want = O.Repo(O.TLOG)
+    got = RepoTLOG(engine)
+    nkeys = 48
+    logs = {f"k{i}": sorted({int(t) for t in rng.integers(1000, 100000, 40 + 7 * i)}) for i in range(nkeys)}
+    state = [(k, 0, _canon([(b"s%d" % t, t) for t in ts])) for k, ts in logs.items()]
+    b = _log_batch(state)
+    want.converge(b)
+    got.converge_deltas(b)
+    cut = {k: 0 for k in logs}
+    for merge in range(12):
+        delta = []
+        for k, ts in logs.items():
+            live = [t for t in ts if t >= cut[k]]
+            ents = []
+            if live:
+                lo = live[min(len(live) - 1, int(rng.integers(0, 3)))]  # just above the oldest live entry
+                ents.append((b"old%d" % merge, lo + 1 if lo + 1 not in ts else lo))  # an insert near the start (or a tie)
+                ents.append((b"s%d" % live[0], live[0]))  # a duplicate of the oldest
+                hi = live[-1]
+                ents.append((b"near-new%d" % merge, hi - 1))  # an insert near the newest end
+            for a in range(int(rng.integers(0, 4))):  # appends
+                ents.append((b"new%d.%d" % (merge, a), 200000 + 100 * merge + a))
+            c = 0
+            if live and rng.random() < 0.25:  # a cutoff raise into the log (frees front room)
+                c = live[min(len(live) - 1, int(rng.integers(1, 6)))]
+                cut[k] = max(cut[k], c)
+            delta.append((k, c, _canon(ents)))
+            ts.extend(t for _, t in ents)
+            ts.sort()
+        b = _log_batch(delta)
+        want.converge(b)
+        got.converge_deltas(b)
+        assert_state_equal(O.TLOG, want.state(), got.state())
