@@ -190,7 +190,8 @@ int32_t jy_counter_deltas_size(jy_engine* eng, int32_t type, uint64_t* n_out);
 int32_t jy_counter_flush(jy_engine* eng, int32_t type, uint64_t cap, uint32_t* slot_out,
                          uint64_t* vals_out, uint32_t* mask_out, uint64_t* n_out, int32_t mem);
 
-/* ---- TREG: TRegString.converge (repo_treg.pony:51-52), LWW by (ts, value) ---- */
+/* ---- TREG: TRegString.converge (repo_treg.pony:51-52), LWW by (ts, value) ----
+ * An entry whose slot is JY_NO_SLOT is skipped (a key not interned). */
 int32_t jy_treg_converge(jy_engine* eng, uint64_t n, const uint32_t* slot, const uint64_t* ts,
                          const uint64_t* pre, const uint64_t* lr, int32_t mem);
 /* The same join for a BLOCK batch: entry i is the delta of slot slot0 + i

@@ -570,11 +570,12 @@ static int32_t keys_host(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb,
 // node's one-shard path enqueues its long values there)
 }  // extern "C"
 int32_t jy_keys_intern_dev(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, const u64* ko, u32* slots,
-                           int32_t (*after)(void*), void* arg) {
+                           int32_t (*after)(void*), void* arg, u64* created_out) {
   JY_TRY(check_type(eng, type));
   JY_HIP(eng, hipSetDevice(eng->device));
   u64 created = 0;
   JY_TRY(jy_keydir_run(eng, type, n, kb, ko, slots, true, &created, after, arg));
+  if (created_out) *created_out = created;
   return keys_created(eng, type, created);
 }
 extern "C" {

@@ -757,7 +757,7 @@ void jy_keydir_free(jy_engine* eng, KeyDir& K);
 int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, const u64* ko, u32* slots, bool create,
                       u64* created, int32_t (*after_probe)(void*) = nullptr, void* arg = nullptr);
 int32_t jy_keys_intern_dev(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, const u64* ko, u32* slots,
-                           int32_t (*after)(void*), void* arg);
+                           int32_t (*after)(void*), void* arg, u64* created_out = nullptr);
 int32_t jy_ujson_grow(jy_engine* eng, u64 need_slots);
 int32_t jy_ujson_extend(jy_engine* eng, u64 from, u64 to);
 int32_t jy_ujson_sizes(jy_engine* eng, u64 n, const u32* slots, u64* ne, u64* nc);

@@ -1446,6 +1446,10 @@ struct OneVals {
   const uint8_t* vb = nullptr;
   u64 vbytes = 0;  // the values' bytes in all (bounds the long values' arena total)
 };
+struct LongJob;
+// what a caller merges right behind the probe (before the host has read the
+// miss count): the engine stream already waits for the values
+typedef int32_t (*SpecMerge)(void* arg, const LongJob& j);
 struct LongJob {
   jy_node* nd;
   NdShard* sh;
@@ -1454,6 +1458,10 @@ struct LongJob {
   u64 nvt;
   const u64* toff;
   u64* lr;
+  u32* slots = nullptr;
+  u64* pre = nullptr;
+  SpecMerge spec = nullptr;
+  void* spec_arg = nullptr;
 };
 // on the host while the probe runs: the total, the arena, the long values
 int32_t long_values(void* p) {
@@ -1472,10 +1480,15 @@ int32_t long_values(void* p) {
                      j.vals->vb, j.toff, dst, rebase, j.lr);
   if (hipGetLastError() != hipSuccess || hipEventRecord(sh.ev_rs_out, sh.rs) != hipSuccess)
     return eng->fail(JY_EHIP, "node: long values");
+  if (j.spec) {
+    if (hipStreamWaitEvent(eng->stream, sh.ev_rs_out, 0) != hipSuccess) return eng->fail(JY_EHIP, "node: value wait");
+    JY_TRY(j.spec(j.spec_arg, j));
+  }
   return JY_OK;
 }
 int32_t one_keys_values(jy_node* nd, NdShard& sh, int32_t type, u64 n, const uint8_t* kbase, const u64* ko,
-                        const OneVals* vals, u32** slots, u64** pre, u64** lr) {
+                        const OneVals* vals, u32** slots, u64** pre, u64** lr, SpecMerge spec = nullptr,
+                        void* spec_arg = nullptr, u64* created = nullptr) {
   jy_engine* eng = sh.eng;
   JY_TRY(bufT(nd, sh, R_SLOTS, std::max<u64>(n, 1), slots));
   const u64 ne = vals ? vals->ne : 0;
@@ -1487,7 +1500,9 @@ int32_t one_keys_values(jy_node* nd, NdShard& sh, int32_t type, u64 n, const uin
     JY_TRY(bufT(nd, sh, R_VOFF, nvt + 1, &toff));
     JY_TRY(bufT(nd, sh, R_LR, std::max<u64>(ne, 1), lr));
   }
-  LongJob job{nd, &sh, type, vals, nvt, toff, vals ? *lr : nullptr};
+  LongJob job{nd, &sh, type, vals, nvt, toff, vals ? *lr : nullptr, *slots, vals ? *pre : nullptr,
+              ne ? spec : nullptr, spec_arg};
+  if (created) *created = 0;
   if (ne) {
     // the arena holds the long values' total already (at most every value's
     // bytes + a granule's padding each): long_values then only advances its
@@ -1506,7 +1521,7 @@ int32_t one_keys_values(jy_node* nd, NdShard& sh, int32_t type, u64 n, const uin
     ND_HIP(nd, hipGetLastError());
   }
   if (n)
-    ND_ENG(nd, sh, jy_keys_intern_dev(eng, type, n, kbase, ko, *slots, ne ? long_values : nullptr, &job));
+    ND_ENG(nd, sh, jy_keys_intern_dev(eng, type, n, kbase, ko, *slots, ne ? long_values : nullptr, &job, created));
   else if (ne)
     ND_ENG(nd, sh, long_values(&job));
   if (ne) ND_HIP(nd, hipStreamWaitEvent(eng->stream, sh.ev_rs_out, 0));
@@ -1546,9 +1561,25 @@ int32_t run_treg_one(jy_node* nd, u64 n, const uint8_t* kb, const u64* ko, const
   OneVals vals{n, static_cast<const u64*>(dvo), on_host(mem) ? v0 : 0, static_cast<const uint8_t*>(dvb), v1 - v0};
   u32* slots;
   u64 *pre, *lr;
+  // The merge goes in right behind the probe, before the host reads the miss
+  // count back: the keys found take their LWW with no host round trip between
+  // the two (a key still missing has slot JY_NO_SLOT, which the merge skips).
+  // New keys then get a second, whole merge once they have slots -- LWW is
+  // idempotent, so the keys merged twice are exact.
+  struct Spec {
+    u64 n;
+    const u64* ts;
+    bool done;
+  } sp{n, static_cast<const u64*>(dts), false};
+  const SpecMerge spec = [](void* a, const LongJob& j) -> int32_t {
+    Spec& s = *static_cast<Spec*>(a);
+    s.done = true;
+    return jy_treg_merge(j.sh->eng, s.n, j.slots, s.ts, j.pre, j.lr);
+  };
+  u64 created = 0;
   JY_TRY(one_keys_values(nd, sh, JY_TREG, n, rebased(dkb, on_host(mem) ? k0 : 0), static_cast<const u64*>(dko),
-                         &vals, &slots, &pre, &lr));
-  ND_ENG(nd, sh, jy_treg_merge(sh.eng, n, slots, static_cast<const u64*>(dts), pre, lr));
+                         &vals, &slots, &pre, &lr, spec, &sp, &created));
+  if (!sp.done || created) ND_ENG(nd, sh, jy_treg_merge(sh.eng, n, slots, static_cast<const u64*>(dts), pre, lr));
   return JY_OK;
 }
 

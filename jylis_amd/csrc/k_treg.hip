@@ -206,6 +206,11 @@ __global__ __launch_bounds__(kThreads) void k_treg_lww(TregK K, const u32* __res
     s[u] = 0;
     if (valid[u]) {
       s[u] = kDense ? slot0 + (u32)i : __builtin_nontemporal_load(slot + i);
+      if (!kDense && !kOwned && s[u] == JY_NO_SLOT) {  // a key with no slot (yet): skipped
+        valid[u] = false;
+        s[u] = 0;
+        continue;
+      }
       t[u] = __builtin_nontemporal_load(dts + i);
       p[u] = __builtin_nontemporal_load(dpre + i);
       l[u] = __builtin_nontemporal_load(dlr + i);
