@@ -257,3 +257,49 @@ def test_node_rejects_bad_config():
         Node(2, "rccl", nlocal=1)  # a multi-process node needs the shared unique id
     with pytest.raises(EngineError):
         Node(0, "copy")
+
+
+@pytest.mark.parametrize("mem", ["host", "device"])
+def test_node_one_shard_arena_grows_in_call(oracle_mod, mem):
+    """at S = 1 the long values go into the arena on the read-back
+    stream beside the key probe -- the arena must be grown (jy_arena_ensure)
+    before that stream may run, never under it.  A 4 KiB arena, then TREG and
+    TLOG batches whose long values take megabytes: the arena grows inside
+    every call, and the states equal the oracle's."""
+    O = oracle_mod
+    rng = np.random.default_rng(99)
+    node = _node(1, "rccl", arena_capacity=1 << 12)
+    try:
+        eng = node.engines[0]
+        seen_r, seen_l = [], []
+        caps = []
+        for step in range(3):
+            b = _treg_batch(rng, 20000, 30000)
+            # every value long: 40-200 bytes
+            from jylis_amd.engine import encode_keys
+            vals = [bytes(rng.integers(0, 256, int(rng.integers(40, 200))).astype(np.uint8)) for _ in range(20000)]
+            b["val_bytes"], b["val_offs"] = encode_keys(vals)
+            seen_r.append(b)
+            args = [b["key_bytes"], b["key_offs"], b["ts"], b["val_bytes"], b["val_offs"]]
+            node.treg_converge(*(args if mem == "host" else [_dev(a) for a in args]))
+            t = _tlog_batch(rng, 5000, 8000, 1000 + 20 * step)
+            # long values, each key's segment kept strictly newest first
+            eo = np.asarray(t["ent_offs"], np.int64)
+            lv, ts = [], []
+            for k in range(len(eo) - 1):
+                ents = sorted({(int(t["ts"][j]), bytes(rng.integers(97, 123, int(rng.integers(30, 120))).astype(np.uint8)))
+                               for j in range(eo[k], eo[k + 1])}, reverse=True)
+                ts += [e[0] for e in ents]
+                lv += [e[1] for e in ents]
+            t["ts"] = np.array(ts, np.uint64)
+            t["val_bytes"], t["val_offs"] = encode_keys(lv)
+            seen_l.append(t)
+            targs = [t[k] for k in ("key_bytes", "key_offs", "cutoff", "ent_offs", "ts", "val_bytes", "val_offs")]
+            node.tlog_converge(*(targs if mem == "host" else [_dev(a) for a in targs]))
+            node.sync()
+            caps.append(eng.arena_usage(O.TREG)[1])
+        assert caps[-1] > (1 << 20) and caps[0] > (1 << 12)
+        assert_state_equal(O.TREG, _want(O, O.TREG, seen_r), _union(O, O.TREG, node))
+        assert_state_equal(O.TLOG, _want(O, O.TLOG, seen_l), _union(O, O.TLOG, node))
+    finally:
+        node.close()
