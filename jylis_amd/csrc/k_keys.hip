@@ -160,7 +160,7 @@ __global__ __launch_bounds__(kThreads) void k_key_probe(In I, Dir D, u32* __rest
     // walk that finds none met a corrupt table -- it ends, and is counted
     for (u64 walk = 0;; walk++) {
       if (walk > D.mask) {
-        c[2] = 1;  // reported with the oversized-key count: the call fails
+        c[2] |= 1ull << 32;  // counted above the oversized keys: the call fails
         break;
       }
       const u64 e = D.table[p];
@@ -508,8 +508,9 @@ int32_t jy_keydir_run(jy_engine* eng, int32_t type, u64 n, const uint8_t* kb, co
     for (int q = 0; q < 3; q++) hc[q] += hg[g * 3 + q];
   const u64 m = hc[0], mbytes = hc[1];
   JY_TRACE("keydir %llu keys: %llu misses (create %d)", (unsigned long long)n, (unsigned long long)m, (int)create);
-  if (hc[2]) return eng->fail(JY_ERANGE, "key longer than 16 MiB, or a probe walked the whole key table");
+  if (hc[2] >> 32) return eng->fail(JY_EINVAL, "key directory: a probe walked the whole table (corrupt table)");
   if (!create || m == 0) return JY_OK;  // (a miss's kMiss is JY_NO_SLOT)
+  if (hc[2]) return eng->fail(JY_ERANGE, "key longer than 16 MiB");
   if (K.n + m >= kIdxMask) return eng->fail(JY_ERANGE, "slot space exhausted");
   JY_TRY(grow_table(eng, K, K.n + m));
   JY_TRY(grow_slots(eng, K, K.n + m));
