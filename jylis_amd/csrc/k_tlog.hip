@@ -289,7 +289,10 @@ __device__ __forceinline__ u32 lds_last_le(const T* a, u32 n, u64 x) {
 
 // key tiles are one wave: no cross-wave barriers, many tiles in flight per CU
 constexpr int kTile = 64;
-constexpr int kFastEnt = 4;  // delta entries a key may have for the lane-per-key fast path
+#ifndef JY_TLOG_FASTENT
+#define JY_TLOG_FASTENT 4
+#endif
+constexpr int kFastEnt = JY_TLOG_FASTENT;  // delta entries a key may have for the lane-per-key fast path
 #ifndef JY_TLOG_KCACHE
 #define JY_TLOG_KCACHE 1
 #endif
