@@ -957,16 +957,38 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt) {
   const u64 xc = jyscan::block_excl<kThreads, u64>(csz, S.red, tot);
   const u64 pc = jyscan::lookback(A.st_co, t, A.epoch, tot, &S.pre);
   JY_CLK(c1);
-  if (k < A.nd) {
-    A.co[k] = pc + xc;
-    // per-item doc ids; a long segment names its doc once per whole tile
-    // in the tile map and writes ids only in its partial end tiles
+  if (k < A.nd) A.co[k] = pc + xc;
+  {
+    // per-item doc ids.  A short segment's ids are written by its wave
+    // together: pass p of the wave covers items [64p, 64p + 64) of the wave's
+    // short segments laid end to end, each lane finding its segment by a
+    // search over the lanes' run offsets (round 6: one lane per document
+    // looping over its items waited for the wave's longest segment, ~13 us
+    // of the tile).  A long segment names its doc once per whole tile in the
+    // tile map, and its lane writes ids only in its partial end tiles.
+    const bool live = k < A.nd;
+    const u32 lane = threadIdx.x & 63;
+    const u64 kw = (u64)t * kDocTile + (threadIdx.x & ~63u);  // the wave's first doc
     auto ids = [&](u32* sid, u64* tm, u64 off, u64 sz) {
       const u64 f0 = (off + kTile - 1) / kTile, f1 = (off + sz) / kTile;  // whole tiles [f0, f1)
-      if (sz <= kLongSeg || f0 >= f1) {
-        for (u64 j = 0; j < sz; j++) sid[off + j] = (u32)k;
-        return;
+      const bool shrt = sz <= kLongSeg || f0 >= f1;
+      const u32 cs = live && shrt ? (u32)sz : 0u;
+      u32 inc = cs;
+      for (u32 d = 1; d < 64; d <<= 1) {
+        const u32 y = __shfl_up(inc, d);
+        if (lane >= d) inc += y;
       }
+      const u32 lo = inc - cs, W = __shfl(inc, 63);
+      for (u32 j0 = 0; j0 < W; j0 += 64) {  // wave-uniform
+        const u32 j = j0 + lane;
+        u32 r = 0;  // the last lane whose run starts at or before j (its run holds j)
+        for (u32 s = 32; s; s >>= 1)
+          if (__shfl(lo, (int)(r + s)) <= j) r += s;
+        const u32 ro = __shfl(lo, (int)r);
+        const u64 roff = __shfl(off, (int)r);
+        if (j < W) sid[roff + (j - ro)] = (u32)(kw + r);
+      }
+      if (!live || shrt) return;
       for (u64 j = off; j < f0 * kTile; j++) sid[j] = (u32)k;
       for (u64 j = f1 * kTile; j < off + sz; j++) sid[j] = (u32)k;
       const u32 q = atomicAdd(&l_nlong, 1u);  // the workgroup fills its tile-map run
@@ -978,9 +1000,9 @@ __global__ __launch_bounds__(kThreads) void k_uj_docs(UjArgs A, u64 ndt) {
     };
     ids(A.sidA, A.tmA, pa + xa, asz);
     ids(A.sidC, A.tmC, pc + xc, csz);
-    const u64 b0 = A.deoff[k], d0 = A.dcoff[k];
-    ids(A.sidB, A.tmB, b0, A.deoff[k + 1] - b0);
-    ids(A.sidD, A.tmD, d0, A.dcoff[k + 1] - d0);
+    const u64 b0 = live ? A.deoff[k] : 0, d0 = live ? A.dcoff[k] : 0;
+    ids(A.sidB, A.tmB, b0, live ? A.deoff[k + 1] - b0 : 0);
+    ids(A.sidD, A.tmD, d0, live ? A.dcoff[k + 1] - d0 : 0);
   }
   if (t == ndt - 1 && threadIdx.x == 0) {
     A.co[A.nd] = pc + tot;
