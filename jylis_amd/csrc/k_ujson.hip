@@ -648,8 +648,25 @@ __device__ void uj_job_chunk(const UjArgs& A, const UJob& J, u64 q) {
     l_pre[2 * R] = acc;
   }
   __syncthreads();
+  // every item's load first, then the stores: a copy's source and destination
+  // never overlap (regrowth moves into fresh room), and with one load-store
+  // pair per iteration each of the kPerT rounds waited a whole memory round
+  // trip (the loop could not move a load above the previous store)
+  static_assert(kJobChunk % kThreads == 0, "a chunk is whole rounds of the workgroup");
+  constexpr u32 kPerT = (u32)(kJobChunk / kThreads);
   const u64 i0 = q * kJobChunk, i1 = i0 + kJobChunk < J.n ? i0 + kJobChunk : J.n;
-  for (u64 t = i0 + threadIdx.x; t < i1; t += kThreads) {
+  const URec* es = J.what == UJ_PROMOTE ? A.epool_out : A.lpe;
+  const u64* cs = J.what == UJ_PROMOTE ? A.cpool_out : A.lpc;
+  URec* ed = J.what == UJ_DEMOTE ? A.epool_out : A.lpe;
+  u64* cd = J.what == UJ_DEMOTE ? A.cpool_out : A.lpc;
+  URec v[kPerT];
+  u64 di[kPerT];
+  u32 sg[kPerT];
+#pragma unroll
+  for (u32 u = 0; u < kPerT; u++) {
+    const u64 t = i0 + (u64)u * kThreads + threadIdx.x;
+    sg[u] = ~0u;
+    if (t >= i1) continue;
     u32 lo = 0, hi = 2 * R - 1;  // the last segment g with l_pre[g] <= t
     while (lo < hi) {
       const u32 mid = (lo + hi + 1) >> 1;
@@ -657,16 +674,17 @@ __device__ void uj_job_chunk(const UjArgs& A, const UJob& J, u64 q) {
       else hi = mid - 1;
     }
     const u64 o = t - l_pre[lo];
-    const u64 si = l_src[lo] + o, di = l_dst[lo] + o;
-    if (lo < R) {
-      if (J.what == UJ_DEMOTE) A.epool_out[di] = A.lpe[si];
-      else if (J.what == UJ_REGROW) A.lpe[di] = A.lpe[si];
-      else A.lpe[di] = A.epool_out[si];
-    } else {
-      if (J.what == UJ_DEMOTE) A.cpool_out[di] = A.lpc[si];
-      else if (J.what == UJ_REGROW) A.lpc[di] = A.lpc[si];
-      else A.lpc[di] = A.cpool_out[si];
-    }
+    const u64 si = l_src[lo] + o;
+    di[u] = l_dst[lo] + o;
+    sg[u] = lo;
+    if (lo < R) v[u] = es[si];
+    else v[u].dot = cs[si];
+  }
+#pragma unroll
+  for (u32 u = 0; u < kPerT; u++) {
+    if (sg[u] == ~0u) continue;
+    if (sg[u] < R) ed[di[u]] = v[u];
+    else cd[di[u]] = v[u].dot;
   }
 }
 
