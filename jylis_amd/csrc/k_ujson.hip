@@ -73,8 +73,15 @@ namespace {
 #define JY_UJ_THREADS 256
 #endif
 constexpr int kThreads = JY_UJ_THREADS;
-constexpr int kPer = 4;                         // items per thread in item tiles
-constexpr u64 kTile1 = (u64)kThreads * kPer;    // U1 item tiles: 1024 items
+// U1 items per thread (round 6, in-box A/B, ms per config-5 step: 4 items
+// 0.495 / 0.495 / 0.494, 2 items 0.509 / 0.481 / 0.477, 1 item 0.469 /
+// 0.478 / 0.468 -- a thread's items ran one after another: each item's
+// stores kept the next item's loads behind them)
+#ifndef JY_UJ_PER
+#define JY_UJ_PER 1
+#endif
+constexpr int kPer = JY_UJ_PER;                 // items per thread in U1 item tiles
+constexpr u64 kTile1 = (u64)kThreads * kPer;    // U1 item tiles
 constexpr u64 kTile = kThreads;                 // U2 / U3 / U5 item tiles: one item per thread
 constexpr u64 kDocTile = kThreads;              // docs per doc tile
 constexpr u64 kLdsDocs = 1023;                  // docs a tile stages in LDS for its search
